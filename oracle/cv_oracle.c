@@ -1,0 +1,946 @@
+/*
+ * cv_oracle.c — CPU restatement of Cilium's L3/L4 verdict path (TEST INFRASTRUCTURE).
+ * See cv_oracle.h.  Reference = Taeung/cilium v1.1.90 under /root/reference.
+ * Restated, not copied: every block cites the reference lines it follows.
+ */
+#include "cv_oracle.h"
+
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ===================================================================== */
+/* Kernel map semantics                                                   */
+/* HASH: kernel/bpf/hashtab.c htab_map_update_elem: flags > BPF_EXIST ->  */
+/*   -EINVAL; NOEXIST on existing -> -EEXIST; EXIST on missing ->         */
+/*   -ENOENT; new element when count == max_entries -> -E2BIG.            */
+/* LPM_TRIE: kernel/bpf/lpm_trie.c: a key is (prefixlen, first prefixlen  */
+/*   bits of data); prefixlen > max -> -EINVAL; full -> -ENOSPC; lookup   */
+/*   returns the longest stored prefix whose prefixlen <= the lookup key's */
+/*   prefixlen and whose bits match; delete is exact.                     */
+/* ===================================================================== */
+
+typedef struct {
+    uint32_t ks, vs, cap, count;
+    uint8_t *keys, *vals, *used;
+} or_hash;
+
+static uint64_t hbytes(const uint8_t *k, uint32_t n)
+{
+    uint64_t h = 1469598103934665603ULL;
+    for (uint32_t i = 0; i < n; i++) { h ^= k[i]; h *= 1099511628211ULL; }
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33;
+    return h;
+}
+
+static or_hash *hnew(uint32_t ks, uint32_t vs, uint32_t cap)
+{
+    or_hash *h = calloc(1, sizeof(*h));
+    uint32_t c = 16;
+    while (c < cap) c <<= 1;
+    h->ks = ks; h->vs = vs; h->cap = c;
+    h->keys = calloc((size_t)c, ks);
+    h->vals = calloc((size_t)c, vs ? vs : 1);
+    h->used = calloc(c, 1);
+    return h;
+}
+
+static void hfree(or_hash *h)
+{
+    if (!h) return;
+    free(h->keys); free(h->vals); free(h->used); free(h);
+}
+
+static int64_t hfind(const or_hash *h, const uint8_t *k)
+{
+    uint32_t m = h->cap - 1, i = (uint32_t)hbytes(k, h->ks) & m;
+    while (h->used[i]) {
+        if (!memcmp(h->keys + (size_t)i * h->ks, k, h->ks)) return i;
+        i = (i + 1) & m;
+    }
+    return -1;
+}
+
+static void hgrow(or_hash *h)
+{
+    or_hash *n = hnew(h->ks, h->vs, h->cap * 2);
+    for (uint32_t i = 0; i < h->cap; i++) {
+        if (!h->used[i]) continue;
+        uint32_t m = n->cap - 1, j = (uint32_t)hbytes(h->keys + (size_t)i * h->ks, h->ks) & m;
+        while (n->used[j]) j = (j + 1) & m;
+        n->used[j] = 1;
+        memcpy(n->keys + (size_t)j * h->ks, h->keys + (size_t)i * h->ks, h->ks);
+        memcpy(n->vals + (size_t)j * h->vs, h->vals + (size_t)i * h->vs, h->vs);
+    }
+    n->count = h->count;
+    free(h->keys); free(h->vals); free(h->used);
+    *h = *n; free(n);
+}
+
+/* returns slot of key, inserting a zero value if missing */
+static int64_t hput(or_hash *h, const uint8_t *k)
+{
+    int64_t s = hfind(h, k);
+    if (s >= 0) return s;
+    if ((h->count + 1) * 2 > h->cap) hgrow(h);
+    uint32_t m = h->cap - 1, i = (uint32_t)hbytes(k, h->ks) & m;
+    while (h->used[i]) i = (i + 1) & m;
+    h->used[i] = 1; h->count++;
+    memcpy(h->keys + (size_t)i * h->ks, k, h->ks);
+    memset(h->vals + (size_t)i * h->vs, 0, h->vs);
+    return i;
+}
+
+static void hdel_slot(or_hash *h, uint32_t i)
+{   /* backward-shift deletion for linear probing */
+    uint32_t m = h->cap - 1, j = i;
+    h->used[i] = 0; h->count--;
+    for (;;) {
+        j = (j + 1) & m;
+        if (!h->used[j]) break;
+        uint32_t k = (uint32_t)hbytes(h->keys + (size_t)j * h->ks, h->ks) & m;
+        int move = (j > i) ? (k <= i || k > j) : (k <= i && k > j);
+        if (move) {
+            memcpy(h->keys + (size_t)i * h->ks, h->keys + (size_t)j * h->ks, h->ks);
+            memcpy(h->vals + (size_t)i * h->vs, h->vals + (size_t)j * h->vs, h->vs);
+            h->used[i] = 1; h->used[j] = 0;
+            i = j;
+        }
+    }
+}
+
+struct or_map {
+    int type;
+    uint32_t ks, vs, max;
+    or_hash *h;              /* HASH / LRU_HASH */
+    uint32_t dbits;          /* LPM: data bits */
+    or_hash **lpm;           /* LPM: per prefixlen, key = masked data, val = orig data + value */
+    uint32_t lpm_count;
+};
+
+or_map *or_map_create(int type, uint32_t key_size, uint32_t val_size, uint32_t max_entries)
+{
+    if (!key_size || !max_entries) return NULL;
+    or_map *m = calloc(1, sizeof(*m));
+    m->type = type; m->ks = key_size; m->vs = val_size; m->max = max_entries;
+    if (type == OR_MAP_LPM_TRIE) {
+        if (key_size <= 4) { free(m); return NULL; }
+        m->dbits = (key_size - 4) * 8;
+        m->lpm = calloc(m->dbits + 1, sizeof(or_hash *));
+    } else {
+        m->h = hnew(key_size, val_size, 64);
+    }
+    return m;
+}
+
+void or_map_free(or_map *m)
+{
+    if (!m) return;
+    hfree(m->h);
+    if (m->lpm) {
+        for (uint32_t i = 0; i <= m->dbits; i++) hfree(m->lpm[i]);
+        free(m->lpm);
+    }
+    free(m);
+}
+
+static void mask_bits(uint8_t *d, uint32_t nbytes, uint32_t plen)
+{
+    for (uint32_t b = 0; b < nbytes; b++) {
+        uint32_t lo = b * 8;
+        if (plen >= lo + 8) continue;
+        d[b] = plen <= lo ? 0 : (uint8_t)(d[b] & (0xFF00u >> (plen - lo)));
+    }
+}
+
+int or_map_update(or_map *m, const void *key, const void *val, uint64_t flags)
+{
+    if (flags > OR_BPF_EXIST) return -EINVAL;
+    if (m->type == OR_MAP_LPM_TRIE) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        uint32_t nb = m->ks - 4;
+        if (plen > m->dbits) return -EINVAL;
+        uint8_t mk[64]; memcpy(mk, (const uint8_t *)key + 4, nb); mask_bits(mk, nb, plen);
+        if (!m->lpm[plen]) m->lpm[plen] = hnew(nb, nb + m->vs, 16);
+        int64_t s = hfind(m->lpm[plen], mk);
+        if (s >= 0) {
+            if (flags == OR_BPF_NOEXIST) return -EEXIST;
+        } else {
+            if (flags == OR_BPF_EXIST) return -ENOENT;
+            if (m->lpm_count >= m->max) return -ENOSPC;
+            s = hput(m->lpm[plen], mk);
+            m->lpm_count++;
+        }
+        uint8_t *v = m->lpm[plen]->vals + (size_t)s * (nb + m->vs);
+        memcpy(v, (const uint8_t *)key + 4, nb);
+        memcpy(v + nb, val, m->vs);
+        return 0;
+    }
+    int64_t s = hfind(m->h, key);
+    if (s >= 0) {
+        if (flags == OR_BPF_NOEXIST) return -EEXIST;
+    } else {
+        if (flags == OR_BPF_EXIST) return -ENOENT;
+        if (m->h->count >= m->max) return -E2BIG;
+        s = hput(m->h, key);
+    }
+    memcpy(m->h->vals + (size_t)s * m->vs, val, m->vs);
+    return 0;
+}
+
+void *or_map_lookup_ptr(or_map *m, const void *key)
+{
+    if (m->type == OR_MAP_LPM_TRIE) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        uint32_t nb = m->ks - 4;
+        if (plen > m->dbits) plen = m->dbits;
+        for (int l = (int)plen; l >= 0; l--) {
+            if (!m->lpm[l] || !m->lpm[l]->count) continue;
+            uint8_t mk[64]; memcpy(mk, (const uint8_t *)key + 4, nb); mask_bits(mk, nb, (uint32_t)l);
+            int64_t s = hfind(m->lpm[l], mk);
+            if (s >= 0) return m->lpm[l]->vals + (size_t)s * (nb + m->vs) + nb;
+        }
+        return NULL;
+    }
+    int64_t s = hfind(m->h, key);
+    return s >= 0 ? m->h->vals + (size_t)s * m->vs : NULL;
+}
+
+int or_map_lookup(or_map *m, const void *key, void *val_out)
+{
+    void *p = or_map_lookup_ptr(m, key);
+    if (!p) return -ENOENT;
+    if (val_out) memcpy(val_out, p, m->vs);
+    return 0;
+}
+
+int or_map_delete(or_map *m, const void *key)
+{
+    if (m->type == OR_MAP_LPM_TRIE) {
+        uint32_t plen; memcpy(&plen, key, 4);
+        uint32_t nb = m->ks - 4;
+        if (plen > m->dbits || !m->lpm[plen]) return -ENOENT;
+        uint8_t mk[64]; memcpy(mk, (const uint8_t *)key + 4, nb); mask_bits(mk, nb, plen);
+        int64_t s = hfind(m->lpm[plen], mk);
+        if (s < 0) return -ENOENT;
+        hdel_slot(m->lpm[plen], (uint32_t)s);
+        m->lpm_count--;
+        return 0;
+    }
+    int64_t s = hfind(m->h, key);
+    if (s < 0) return -ENOENT;
+    hdel_slot(m->h, (uint32_t)s);
+    return 0;
+}
+
+uint32_t or_map_count(const or_map *m)
+{
+    return m->type == OR_MAP_LPM_TRIE ? m->lpm_count : m->h->count;
+}
+
+static uint32_t g_sort_ks;
+static int cmp_rows(const void *a, const void *b) { return memcmp(a, b, g_sort_ks); }
+
+uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max)
+{
+    uint32_t n = or_map_count(m), row = m->ks + m->vs, k = 0;
+    uint8_t *tmp = malloc((size_t)(n ? n : 1) * row);
+    if (m->type == OR_MAP_LPM_TRIE) {
+        uint32_t nb = m->ks - 4;
+        for (uint32_t l = 0; l <= m->dbits; l++) {
+            or_hash *h = m->lpm[l];
+            if (!h) continue;
+            for (uint32_t i = 0; i < h->cap; i++) {
+                if (!h->used[i]) continue;
+                uint8_t *r = tmp + (size_t)k++ * row;
+                memcpy(r, &l, 4);
+                memcpy(r + 4, h->vals + (size_t)i * (nb + m->vs), nb + m->vs);
+            }
+        }
+    } else {
+        for (uint32_t i = 0; i < m->h->cap; i++) {
+            if (!m->h->used[i]) continue;
+            uint8_t *r = tmp + (size_t)k++ * row;
+            memcpy(r, m->h->keys + (size_t)i * m->ks, m->ks);
+            memcpy(r + m->ks, m->h->vals + (size_t)i * m->vs, m->vs);
+        }
+    }
+    g_sort_ks = m->ks;
+    qsort(tmp, k, row, cmp_rows);
+    if (k > max) k = max;
+    for (uint32_t i = 0; i < k; i++) {
+        if (keys) memcpy((uint8_t *)keys + (size_t)i * m->ks, tmp + (size_t)i * row, m->ks);
+        if (vals) memcpy((uint8_t *)vals + (size_t)i * m->vs, tmp + (size_t)i * row + m->ks, m->vs);
+    }
+    free(tmp);
+    return k;
+}
+
+/* ===================================================================== */
+/* Byte order + helpers                                                   */
+/* ===================================================================== */
+
+static inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+/* GET_PREFIX (bpf/lib/ipv6.h:136-138), evaluated in int arithmetic as the macro does */
+uint32_t or_get_prefix(int prefix)
+{
+    uint32_t host = prefix <= 0 ? 0u : prefix < 32 ? (uint32_t)(((1u << prefix) - 1u) << (32 - prefix))
+                                                   : 0xFFFFFFFFu;
+    return bswap32(host);
+}
+
+/* ipv6_addr_clear_suffix (bpf/lib/ipv6.h:140-150) */
+void or_ipv6_addr_clear_suffix(uint8_t addr[16], int prefix)
+{
+    for (int w = 0; w < 4; w++) {
+        uint32_t p; memcpy(&p, addr + 4 * w, 4);
+        p &= or_get_prefix(prefix);
+        memcpy(addr + 4 * w, &p, 4);
+        prefix -= 32;
+    }
+}
+
+/* skb_load_bytes / direct access bound: bytes [off, off+n) must lie inside skb->len.
+ * `avail` = bytes present in the record (min(len, stride)).  Returns 0, 1 (beyond
+ * len: the reference's helper fails) or OR_E_TRUNC (inside len but not in the record). */
+static inline int ld(const uint8_t *f, uint32_t avail, uint32_t len, int off, uint32_t n, void *to)
+{
+    if (off < 0 || (uint64_t)off + n > len) return 1;
+    if ((uint64_t)off + n > avail) return OR_E_TRUNC;
+    memcpy(to, f + off, n);
+    return 0;
+}
+
+#define ETH_HLEN 14
+#define HOST_ID 1     /* bpf/node_config.h */
+#define WORLD_ID 2
+#define CLUSTER_ID 3
+#define HEALTH_ID 4
+#define HOST_IFINDEX 1
+
+/* ===================================================================== */
+/* Datapath container                                                     */
+/* ===================================================================== */
+
+or_dp *or_dp_create(uint32_t flags)
+{
+    or_dp *dp = calloc(1, sizeof(*dp));
+    dp->flags = flags;
+    return dp;
+}
+
+void or_dp_free(or_dp *dp) { free(dp); }
+
+int or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *policy, or_map *ct4)
+{
+    if (dp->n_ep >= OR_MAX_EP) return -E2BIG;
+    or_endpoint_prog *e = &dp->ep[dp->n_ep];
+    e->lxc_id = lxc_id; e->seclabel = seclabel; e->policy = policy; e->ct4 = ct4;
+    return (int)dp->n_ep++;
+}
+
+void or_dp_metrics(const or_dp *dp, uint64_t *out) { memcpy(out, dp->metrics, sizeof(dp->metrics)); }
+
+/* update_metrics (bpf/lib/metrics.h:43-58) summed over CPUs; dir 1 ingress, 2 egress */
+static void update_metrics(or_dp *dp, uint32_t bytes, uint8_t dir, uint8_t reason)
+{
+    __atomic_fetch_add(&dp->metrics[reason][dir & 3][0], 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&dp->metrics[reason][dir & 3][1], (uint64_t)bytes, __ATOMIC_RELAXED);
+}
+
+static or_endpoint_prog *find_ep(or_dp *dp, uint16_t lxc_id)
+{
+    for (uint32_t i = 0; i < dp->n_ep; i++)
+        if (dp->ep[i].lxc_id == lxc_id) return &dp->ep[i];
+    return NULL;
+}
+
+/* lookup_ip4_endpoint / lookup_ip6_endpoint (bpf/lib/eps.h:26-46) */
+static or_endpoint_info *lookup_ip4_endpoint(or_dp *dp, uint32_t daddr, uint8_t *nl)
+{
+    if (!dp->lxc) return NULL;
+    or_endpoint_key k; memset(&k, 0, sizeof(k));
+    memcpy(k.ip, &daddr, 4); k.family = 1;
+    (*nl)++;
+    return or_map_lookup_ptr(dp->lxc, &k);
+}
+
+static or_endpoint_info *lookup_ip6_endpoint(or_dp *dp, const uint8_t *daddr, uint8_t *nl)
+{
+    if (!dp->lxc) return NULL;
+    or_endpoint_key k; memset(&k, 0, sizeof(k));
+    memcpy(k.ip, daddr, 16); k.family = 2;
+    (*nl)++;
+    return or_map_lookup_ptr(dp->lxc, &k);
+}
+
+/* ipcache_lookup4 (bpf/lib/eps.h:309-319) with prefix = V4_CACHE_KEY_LEN (32):
+ * key.lpm prefixlen = IPCACHE_PREFIX_LEN(32) = 32 static bits + 32. */
+static or_remote_endpoint_info *ipcache_lookup4(or_dp *dp, uint32_t addr, int prefix, uint8_t *nl)
+{
+    if (!dp->ipcache) return NULL;
+    or_ipcache_key k; memset(&k, 0, sizeof(k));
+    k.prefixlen = 32 + (uint32_t)prefix; k.family = 1;
+    addr &= or_get_prefix(prefix);
+    memcpy(k.ip, &addr, 4);
+    (*nl)++;
+    return or_map_lookup_ptr(dp->ipcache, &k);
+}
+
+/* ipcache_lookup6 (bpf/lib/eps.h:295-305) */
+static or_remote_endpoint_info *ipcache_lookup6(or_dp *dp, const uint8_t *addr, int prefix, uint8_t *nl)
+{
+    if (!dp->ipcache) return NULL;
+    or_ipcache_key k; memset(&k, 0, sizeof(k));
+    k.prefixlen = 32 + (uint32_t)prefix; k.family = 2;
+    memcpy(k.ip, addr, 16);
+    or_ipv6_addr_clear_suffix(k.ip, prefix);
+    (*nl)++;
+    return or_map_lookup_ptr(dp->ipcache, &k);
+}
+
+/* ===================================================================== */
+/* Config 1: XDP prefilter (bpf/bpf_xdp.c:88-184)                         */
+/* ===================================================================== */
+
+static int xdp_one(or_dp *dp, const uint8_t *f, uint32_t len, uint8_t *nl)
+{
+    /* check_filters (:158-178): no room for ethhdr -> DROP */
+    if (len < ETH_HLEN) return OR_XDP_DROP;
+    uint16_t proto; memcpy(&proto, f + 12, 2);
+    if (proto == 0x0008) {                     /* bpf_htons(ETH_P_IP) */
+        /* check_v4 (:97-121) */
+        if (len < ETH_HLEN + 20) return OR_XDP_DROP;
+        uint32_t saddr, daddr; memcpy(&saddr, f + 26, 4); memcpy(&daddr, f + 30, 4);
+        if (dp->v4_fix) {                      /* CIDR4_FILTER */
+            or_lpm_v4_key k; k.prefixlen = 32; memcpy(k.addr, &saddr, 4);
+            if (dp->v4_dyn) {                  /* CIDR4_LPM_PREFILTER */
+                (*nl)++;
+                if (or_map_lookup_ptr(dp->v4_dyn, &k)) return OR_XDP_DROP;
+            }
+            (*nl)++;
+            if (or_map_lookup_ptr(dp->v4_fix, &k)) return OR_XDP_DROP;
+        }
+        /* check_v4_endpoint (:88-95) */
+        return lookup_ip4_endpoint(dp, daddr, nl) ? OR_XDP_PASS : OR_XDP_DROP;
+    } else if (proto == 0xDD86) {              /* bpf_htons(ETH_P_IPV6) */
+        /* check_v6 (:132-156) */
+        if (len < ETH_HLEN + 40) return OR_XDP_DROP;
+        if (dp->v6_fix) {
+            or_lpm_v6_key k; k.prefixlen = 128; memcpy(k.addr, f + 22, 16);
+            if (dp->v6_dyn) {
+                (*nl)++;
+                if (or_map_lookup_ptr(dp->v6_dyn, &k)) return OR_XDP_DROP;
+            }
+            (*nl)++;
+            if (or_map_lookup_ptr(dp->v6_fix, &k)) return OR_XDP_DROP;
+        }
+        return lookup_ip6_endpoint(dp, f + 38, nl) ? OR_XDP_PASS : OR_XDP_DROP;
+    }
+    return OR_XDP_PASS;
+}
+
+void or_xdp_prefilter(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                      uint32_t n, or_out *out)
+{
+    #pragma omp parallel for schedule(static)
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t nl = 0;
+        uint32_t l = len[i] < stride ? len[i] : stride;  /* prefilter reads only the first 54 B */
+        uint8_t v = xdp_one(dp, frames + (size_t)i * stride, l, &nl);
+        if (out->xdp) out->xdp[i] = v;
+        if (out->nl) out->nl[i] = nl;
+        if (out->nu) out->nu[i] = 0;
+    }
+}
+
+/* ===================================================================== */
+/* Policy (bpf/lib/policy.h:217-329)                                      */
+/* ===================================================================== */
+
+static inline void ctr_add(or_policy_entry *p, uint32_t len)
+{   /* __sync_fetch_and_add (policy.h:76-77, 88-89, 99-100) */
+    __atomic_fetch_add(&p->packets, 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&p->bytes, (uint64_t)len, __ATOMIC_RELAXED);
+}
+
+/* __policy_can_access (policy.h:217-285); cb[CB_POLICY] is always 0 on this path
+ * (policy_clear_mark at bpf_lxc.c:881, bpf_clear_cb at bpf_lxc.c:679). */
+static int policy_can_access(or_map *map, uint32_t flags, uint32_t skb_len, uint32_t identity,
+                             uint16_t dport, uint8_t proto, int dir, uint8_t *nl, uint8_t *nu)
+{
+    if (flags & OR_F_DROP_ALL) return OR_DROP_POLICY;
+    or_policy_key key = { identity, dport, proto, (uint8_t)(!dir) };
+    or_policy_entry *p;
+    if (flags & OR_F_HAVE_L4_POLICY) {
+        (*nl)++;
+        p = or_map_lookup_ptr(map, &key);
+        if (p) { ctr_add(p, skb_len); (*nu)++; return p->proxy_port; }
+    }
+    key.dport = 0; key.protocol = 0;
+    (*nl)++;
+    p = or_map_lookup_ptr(map, &key);
+    if (p) { ctr_add(p, skb_len); (*nu)++; return OR_TC_ACT_OK; }
+    if (flags & OR_F_HAVE_L4_POLICY) {
+        key.sec_label = 0; key.dport = dport; key.protocol = proto;
+        (*nl)++;
+        p = or_map_lookup_ptr(map, &key);
+        if (p) { ctr_add(p, skb_len); (*nu)++; return p->proxy_port; }
+    }
+    return OR_DROP_POLICY;
+}
+
+/* policy_can_access_ingress (policy.h:305-329) */
+static int policy_can_access_ingress(or_map *map, uint32_t flags, uint32_t skb_len, uint32_t src,
+                                     uint16_t dport, uint8_t proto, uint8_t *nl, uint8_t *nu)
+{
+    if (!(flags & OR_F_POLICY_INGRESS))
+        return (flags & OR_F_DROP_ALL) ? OR_DROP_POLICY : OR_TC_ACT_OK;
+    if (flags & OR_F_DROP_ALL) return OR_DROP_POLICY;
+    int ret = policy_can_access(map, flags, skb_len, src, dport, proto, OR_CT_INGRESS, nl, nu);
+    if (ret >= OR_TC_ACT_OK) return ret;
+    return OR_DROP_POLICY;                      /* !IGNORE_DROP */
+}
+
+/* ===================================================================== */
+/* Conntrack (bpf/lib/conntrack.h)                                        */
+/* ===================================================================== */
+
+#define CT_LIFETIME_TCP    21600
+#define CT_LIFETIME_NONTCP 60
+#define CT_SYN_TIMEOUT     60
+#define CT_CLOSE_TIMEOUT   10
+#define CT_REPORT_INTERVAL 5
+#define TUPLE_F_OUT     0
+#define TUPLE_F_IN      1
+#define TUPLE_F_RELATED 2
+#define TUPLE_F_SERVICE 4
+#define ACTION_UNSPEC 0
+#define ACTION_CREATE 1
+#define ACTION_CLOSE  2
+#define B_RX_CLOSING 0x1
+#define B_TX_CLOSING 0x2
+#define B_LB_LOOPBACK 0x8
+#define B_SEEN_NON_SYN 0x10
+#define TCPF_FIN 0x01   /* union tcp_flags.lower_bits: TCP flags byte (conntrack.h:74-86) */
+#define TCPF_SYN 0x02
+#define TCPF_RST 0x04
+
+/* __ct_update_timeout (conntrack.h:103-161) */
+static int ct_update_timeout_raw(or_ct_entry *e, uint32_t lifetime, int dir, uint8_t seen, uint32_t now)
+{
+    e->lifetime = now + lifetime;                        /* NEEDS_TIMEOUT (common.h:33) */
+    uint8_t *acc = dir == OR_CT_INGRESS ? &e->rx_flags_seen : &e->tx_flags_seen;
+    uint32_t *last = dir == OR_CT_INGRESS ? &e->last_rx_report : &e->last_tx_report;
+    seen |= *acc;
+    if (*last + CT_REPORT_INTERVAL < now || *acc != seen) {
+        *last = now; *acc = seen;
+        return 1;
+    }
+    return 0;
+}
+
+/* ct_update_timeout (conntrack.h:169-186) */
+static int ct_update_timeout(or_ct_entry *e, int tcp, int dir, uint8_t seen, uint32_t now)
+{
+    uint32_t lifetime = CT_LIFETIME_NONTCP;
+    if (tcp) {
+        if (!(seen & TCPF_SYN)) e->bits |= B_SEEN_NON_SYN;
+        lifetime = (e->bits & B_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+    }
+    return ct_update_timeout_raw(e, lifetime, dir, seen, now);
+}
+
+static inline int ct_alive(const or_ct_entry *e)   /* conntrack.h:194-197 */
+{
+    return !(e->bits & B_RX_CLOSING) || !(e->bits & B_TX_CLOSING);
+}
+
+/* __ct_lookup (conntrack.h:199-263) */
+static int ct_lookup_one(or_map *map, const or_ipv4_ct_tuple *t, int action, int dir, or_ct_state *st,
+                         int tcp, uint8_t seen, uint32_t skb_len, uint32_t now, uint32_t flags,
+                         uint8_t *nl, uint8_t *nu)
+{
+    (*nl)++;
+    or_ct_entry *e = or_map_lookup_ptr(map, t);
+    if (!e) return OR_CT_NEW;
+    (*nu)++;
+    if (ct_alive(e)) ct_update_timeout(e, tcp, dir, seen, now);
+    if (st) {
+        st->rev_nat_index = e->rev_nat_index;
+        st->loopback = (e->bits & B_LB_LOOPBACK) ? 1 : 0;
+        st->slave = e->slave;
+    }
+    if (flags & OR_F_CT_ACCOUNTING) {
+        if (dir == OR_CT_INGRESS) { e->rx_packets += 1; e->rx_bytes += skb_len; }
+        else                      { e->tx_packets += 1; e->tx_bytes += skb_len; }
+    }
+    switch (action) {
+    case ACTION_CREATE:
+        if ((e->bits & B_RX_CLOSING) + ((e->bits & B_TX_CLOSING) >> 1) >= 1) {
+            e->bits &= (uint16_t)~(B_RX_CLOSING | B_TX_CLOSING);
+            ct_update_timeout(e, tcp, dir, seen, now);
+        }
+        break;
+    case ACTION_CLOSE:
+        if (dir == OR_CT_INGRESS) e->bits |= B_RX_CLOSING; else e->bits |= B_TX_CLOSING;
+        if (ct_alive(e)) break;
+        ct_update_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
+        break;
+    }
+    return OR_CT_ESTABLISHED;
+}
+
+/* ipv4_ct_tuple_reverse (conntrack.h:414-431) */
+static void ct_tuple_reverse4(or_ipv4_ct_tuple *t)
+{
+    uint32_t a = t->saddr; t->saddr = t->daddr; t->daddr = a;
+    uint16_t p = t->sport; t->sport = t->dport; t->dport = p;
+    if (t->flags & TUPLE_F_IN) t->flags &= (uint8_t)~TUPLE_F_IN; else t->flags |= TUPLE_F_IN;
+}
+
+/* ct_lookup4 (conntrack.h:442-562) */
+int or_ct_lookup4(or_map *ct, or_ipv4_ct_tuple *t, const uint8_t *f, uint32_t avail, uint32_t len,
+                  int off, int dir, or_ct_state *st, uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu)
+{
+    int action = ACTION_UNSPEC, r;
+    int tcp = t->nexthdr == 6;
+    uint8_t seen = 0;
+    if (dir == OR_CT_INGRESS) t->flags = TUPLE_F_OUT;
+    else if (dir == OR_CT_EGRESS) t->flags = TUPLE_F_IN;
+    else if (dir == OR_CT_SERVICE) t->flags = TUPLE_F_SERVICE;
+    else return OR_DROP_CT_INVALID_HDR;
+
+    switch (t->nexthdr) {
+    case 1: {                                         /* IPPROTO_ICMP */
+        uint8_t type;
+        r = ld(f, avail, len, off, 1, &type);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        t->sport = 0; t->dport = 0;
+        switch (type) {
+        case 3: case 11: case 12:                     /* DEST_UNREACH, TIME_EXCEEDED, PARAMETERPROB */
+            t->flags |= TUPLE_F_RELATED; break;
+        case 0:                                       /* ECHOREPLY: dport = ICMP_ECHO (raw 8) */
+            t->dport = 8; break;
+        case 8:                                       /* ECHO: sport = type, fall through */
+            t->sport = type; /* fallthrough */
+        default:
+            action = ACTION_CREATE; break;
+        }
+        break;
+    }
+    case 6: {                                         /* IPPROTO_TCP */
+        uint8_t fl[2];
+        r = ld(f, avail, len, off + 12, 2, fl);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        seen = fl[1];
+        action = (seen & (TCPF_RST | TCPF_FIN)) ? ACTION_CLOSE : ACTION_CREATE;
+        r = ld(f, avail, len, off, 4, &t->dport);     /* loads dport then sport slots */
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        break;
+    }
+    case 17:                                          /* IPPROTO_UDP */
+        r = ld(f, avail, len, off, 4, &t->dport);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        action = ACTION_CREATE;
+        break;
+    default:
+        return OR_DROP_CT_UNKNOWN_PROTO;
+    }
+
+    int ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, len, now, flags, nl, nu);
+    if (ret != OR_CT_NEW)
+        return (t->flags & TUPLE_F_RELATED) ? OR_CT_RELATED : OR_CT_REPLY;
+    if (dir != OR_CT_SERVICE) {
+        ct_tuple_reverse4(t);
+        ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, len, now, flags, nl, nu);
+    }
+    return ret;
+}
+
+/* ct_create4 (conntrack.h:663-744) */
+int or_ct_create4(or_map *ct, or_ipv4_ct_tuple *t, uint32_t skb_len, int dir, const or_ct_state *st,
+                  uint32_t now)
+{
+    or_ct_entry e; memset(&e, 0, sizeof(e));
+    int tcp = t->nexthdr == 6;
+    e.rev_nat_index = st->rev_nat_index;
+    if (st->loopback) e.bits |= B_LB_LOOPBACK;
+    e.slave = st->slave;
+    ct_update_timeout(&e, tcp, dir, tcp ? TCPF_SYN : 0, now);
+    if (dir == OR_CT_INGRESS) { e.rx_packets = 1; e.rx_bytes = skb_len; }
+    else                      { e.tx_packets = 1; e.tx_bytes = skb_len; }
+    e.src_sec_id = st->src_sec_id;
+    if (or_map_update(ct, t, &e, 0) < 0) return OR_DROP_CT_CREATE_FAILED;
+    if (st->addr) {
+        uint8_t fl = t->flags; uint32_t sa = t->saddr, da = t->daddr;
+        if (dir == OR_CT_INGRESS) t->saddr = st->addr; else t->daddr = st->addr;
+        if (st->loopback) {
+            t->flags = TUPLE_F_IN;
+            if (dir == OR_CT_INGRESS) t->daddr = st->svc_addr; else t->saddr = st->svc_addr;
+        }
+        if (or_map_update(ct, t, &e, 0) < 0) return OR_DROP_CT_CREATE_FAILED;
+        t->saddr = sa; t->daddr = da; t->flags = fl;
+    }
+    or_ipv4_ct_tuple it; memset(&it, 0, sizeof(it));
+    it.daddr = t->daddr; it.saddr = t->saddr; it.nexthdr = 1;
+    it.flags = t->flags | TUPLE_F_RELATED;
+    e.bits |= B_SEEN_NON_SYN;
+    if (or_map_update(ct, &it, &e, 0) < 0) return OR_DROP_CT_CREATE_FAILED;
+    return 0;
+}
+
+/* ===================================================================== */
+/* Ingress: from_netdev -> handle_ipv4 -> ipv4_policy                     */
+/* ===================================================================== */
+
+static inline int IS_ERR(int x) { return x < 0 || x == OR_TC_ACT_SHOT; }   /* common.h:231 */
+
+typedef struct {
+    uint8_t ct; uint16_t proxy; uint8_t nl, nu;
+} pkt_state;
+
+/* ipv4_policy (bpf/bpf_lxc.c:865-979) for endpoint `ep`, LXC_NAT46 off.  ifindex is
+ * skb->cb[CB_IFINDEX] set by ipv4_local_delivery (l3.h:264). */
+static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, const uint8_t *f, uint32_t avail, uint32_t len,
+                       uint32_t ifindex, uint32_t src_label, int skip_proxy, uint32_t now, pkt_state *ps)
+{
+    if (len < ETH_HLEN + 20) return OR_DROP_INVALID;   /* revalidate_data */
+    or_ipv4_ct_tuple t; memset(&t, 0, sizeof(t));
+    or_ct_state st, st_new; memset(&st, 0, sizeof(st)); memset(&st_new, 0, sizeof(st_new));
+    t.nexthdr = f[23];
+    memcpy(&t.daddr, f + 30, 4); memcpy(&t.saddr, f + 26, 4);
+    int l4_off = ETH_HLEN + (f[14] & 0x0F) * 4;
+    int ret = or_ct_lookup4(ep->ct4, &t, f, avail, len, l4_off, OR_CT_INGRESS, &st, now, dp->flags,
+                            &ps->nl, &ps->nu);
+    if (ret < 0) return ret;
+    ps->ct = (uint8_t)ret;
+    /* REPLY with rev_nat_index && !loopback -> lb4_rev_nat (rewrite; rows with
+     * rev-NAT come from the egress LB path, config 5) */
+    int verdict = policy_can_access_ingress(ep->policy, dp->flags, len, src_label, t.dport, t.nexthdr,
+                                            &ps->nl, &ps->nu);
+    if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
+        if (ret == OR_CT_ESTABLISHED) {               /* ct_delete4 */
+            if (or_map_delete(ep->ct4, &t) == 0) ps->nu++;
+        }
+        return OR_DROP_POLICY;
+    }
+    if (skip_proxy) verdict = 0;
+    if (ret == OR_CT_NEW) {
+        st_new.orig_dport = t.dport;
+        st_new.src_sec_id = src_label;
+        int r = or_ct_create4(ep->ct4, &t, len, OR_CT_INGRESS, &st_new, now);
+        ps->nu += 2;
+        if (IS_ERR(r)) return r;
+    }
+    if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
+        /* ipv4_redirect_to_host_port (lib/lxc.h:97-142): rewrite + proxy-map insert
+         * (L7 side effect, out of scope); the verdict redirects to HOST_IFINDEX. */
+        ps->proxy = (uint16_t)verdict;
+        ifindex = HOST_IFINDEX;
+    }
+    if (ifindex) return OR_TC_ACT_REDIRECT;           /* redirect(ifindex, 0) */
+    return OR_TC_ACT_OK;
+}
+
+/* handle_ipv4 (bpf/bpf_netdev.c:357-453), ENCAP_IFINDEX paths (overlay) disabled,
+ * reverse_proxy with an empty cilium_proxy4 map (L7 out of scope).  When the packet
+ * reaches the endpoint, the tail-called policy program (handle_policy ->
+ * tail_ipv4_policy, bpf_lxc.c:981-1038) runs and its return value is final:
+ * *final = 1 and the return is TC_ACT_SHOT / TC_ACT_OK / TC_ACT_REDIRECT. */
+static int handle_ipv4(or_dp *dp, const uint8_t *f, uint32_t avail, uint32_t len, uint32_t src_identity,
+                       int skip_proxy, uint32_t now, uint32_t *out_identity, pkt_state *ps, int *final)
+{
+    *final = 0;
+    if (len < ETH_HLEN + 20) return OR_DROP_INVALID;
+    int l4_off = ETH_HLEN + (f[14] & 0x0F) * 4;
+    uint32_t secctx = WORLD_ID;                        /* derive_ipv4_sec_ctx (:278-290) */
+    uint8_t nexthdr = f[23];
+    uint32_t saddr, daddr; memcpy(&saddr, f + 26, 4); memcpy(&daddr, f + 30, 4);
+    if (src_identity < HEALTH_ID) {                    /* identity_is_reserved (policy.h:212-215) */
+        or_remote_endpoint_info *info = ipcache_lookup4(dp, saddr, 32, &ps->nl);
+        if (info && info->sec_label && info->sec_label != CLUSTER_ID && info->sec_label != HOST_ID)
+            src_identity = info->sec_label;
+    }
+    *out_identity = src_identity;
+    if (dp->flags & OR_F_FROM_HOST) {
+        secctx = src_identity;
+        if (nexthdr == 6 || nexthdr == 17) {           /* reverse_proxy (:293-354): port load */
+            uint8_t p[4];
+            int r = ld(f, avail, len, l4_off, 4, p);
+            if (r == OR_E_TRUNC) return r;
+            if (r) return OR_DROP_CT_INVALID_HDR;
+        }
+    }
+    or_endpoint_info *ep = lookup_ip4_endpoint(dp, daddr, &ps->nl);
+    if (ep) {
+        if (ep->flags & 1) return OR_TC_ACT_OK;        /* ENDPOINT_F_HOST */
+        /* ipv4_local_delivery (l3.h:247-276): ipv4_l3 -> ipv4_dec_ttl (ipv4.h:124-137) */
+        if (f[22] <= 1) return OR_DROP_INVALID;
+        or_endpoint_prog *prog = find_ep(dp, ep->lxc_id);
+        if (!prog) return OR_DROP_MISSED_TAIL_CALL;   /* tail_call(cilium_policy, lxc_id) missed */
+        int ret = ipv4_policy(dp, prog, f, avail, len, ep->ifindex, secctx, skip_proxy, now, ps);
+        if (ret == OR_E_TRUNC) return ret;
+        *final = 1;
+        if (IS_ERR(ret)) {                             /* tail_ipv4_policy: send_drop_notify */
+            update_metrics(dp, len, 1, (uint8_t)(-ret));
+            return OR_TC_ACT_SHOT;
+        }
+        return ret;
+    }
+    return OR_TC_ACT_OK;
+}
+
+/* handle_identity_from_host (bpf_netdev.c:128-153) */
+static uint32_t identity_from_mark(uint32_t mark, int *skip_proxy)
+{
+    uint32_t magic = mark & 0xF00;
+    if (magic == 0xA00) { *skip_proxy = 1; return ((mark & 0xFF) << 16) | (mark >> 16); }
+    if (magic == 0xB00) return ((mark & 0xFF) << 16) | (mark >> 16);
+    if (magic == 0xC00) return HOST_ID;
+    return WORLD_ID;
+}
+
+void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                       const uint32_t *mark, uint32_t n, uint32_t now, int with_prefilter, or_out *out)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *f = frames + (size_t)i * stride;
+        uint32_t L = len[i], avail = L < stride ? L : stride;
+        pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
+        uint8_t xv = OR_XDP_PASS;
+        int32_t ret = OR_TC_ACT_OK;
+        uint32_t ident = 0;
+        if (with_prefilter) xv = (uint8_t)xdp_one(dp, f, avail, &ps.nl);
+        if (xv == OR_XDP_PASS) {
+            /* from_netdev (bpf_netdev.c:470-524) */
+            uint32_t identity = 0; int skip_proxy = 0;
+            if (dp->flags & OR_F_FROM_HOST) identity = identity_from_mark(mark ? mark[i] : 0, &skip_proxy);
+            uint16_t proto = 0;
+            if (avail >= 14) memcpy(&proto, f + 12, 2);      /* skb->protocol */
+            ident = identity;
+            if (proto == 0x0008) {
+                int final = 0;
+                int r = handle_ipv4(dp, f, avail, L, identity, skip_proxy, now, &ident, &ps, &final);
+                if (r == OR_E_TRUNC || final) ret = r;
+                else if (IS_ERR(r)) {                        /* tail_handle_ipv4 (:457-466) */
+                    update_metrics(dp, L, 1, (uint8_t)(-r));
+                    ret = OR_TC_ACT_SHOT;
+                } else ret = r;
+            } else {
+                ret = OR_TC_ACT_OK;                          /* IPv6 path: config 5; others to stack */
+            }
+        }
+        if (out->xdp) out->xdp[i] = xv;
+        if (out->ret) out->ret[i] = ret;
+        if (out->identity) out->identity[i] = ident;
+        if (out->ct) out->ct[i] = ps.ct;
+        if (out->proxy) out->proxy[i] = ps.proxy;
+        if (out->nl) out->nl[i] = ps.nl;
+        if (out->nu) out->nu[i] = ps.nu;
+    }
+}
+
+/* ===================================================================== */
+/* Config 2: stateless ingress verdict for one endpoint                   */
+/* ===================================================================== */
+
+void or_policy_ingress(or_dp *dp, uint32_t ep_index, const uint8_t *frames, uint32_t stride,
+                       const uint32_t *len, const uint32_t *mark, uint32_t n, or_out *out)
+{
+    or_endpoint_prog *ep = &dp->ep[ep_index];
+    #pragma omp parallel for schedule(static)
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *f = frames + (size_t)i * stride;
+        uint32_t L = len[i], avail = L < stride ? L : stride;
+        pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
+        int skip_proxy = 0;
+        uint32_t identity = 0;
+        int32_t ret;
+        if (dp->flags & OR_F_FROM_HOST) identity = identity_from_mark(mark ? mark[i] : 0, &skip_proxy);
+        uint16_t proto = 0;
+        if (avail >= 14) memcpy(&proto, f + 12, 2);
+        if (proto != 0x0008) {
+            ret = OR_DROP_UNKNOWN_L3;
+        } else if (L < ETH_HLEN + 20) {
+            ret = OR_DROP_INVALID;
+        } else {
+            uint32_t saddr; memcpy(&saddr, f + 26, 4);
+            if (identity < HEALTH_ID) {                       /* bpf_netdev.c:375-398 */
+                or_remote_endpoint_info *info = ipcache_lookup4(dp, saddr, 32, &ps.nl);
+                if (info && info->sec_label && info->sec_label != CLUSTER_ID && info->sec_label != HOST_ID)
+                    identity = info->sec_label;
+            }
+            /* L4 key as ct_lookup4 (conntrack.h:471-530) leaves it after the reverse
+             * (forward-direction) lookup of a NEW flow. */
+            or_ipv4_ct_tuple t; memset(&t, 0, sizeof(t));
+            t.nexthdr = f[23];
+            int off = ETH_HLEN + (f[14] & 0x0F) * 4, r = 0;
+            ret = 0;
+            switch (t.nexthdr) {
+            case 1: {
+                uint8_t type;
+                r = ld(f, avail, L, off, 1, &type);
+                if (r == OR_E_TRUNC) { ret = r; break; }
+                if (r) { ret = OR_DROP_CT_INVALID_HDR; break; }
+                t.sport = 0; t.dport = 0;
+                if (type == 0) t.dport = 8; else if (type == 8) t.sport = type;
+                break;
+            }
+            case 6: {
+                uint8_t fl[2];
+                r = ld(f, avail, L, off + 12, 2, fl);
+                if (!r) r = ld(f, avail, L, off, 4, &t.dport);
+                if (r == OR_E_TRUNC) { ret = r; break; }
+                if (r) { ret = OR_DROP_CT_INVALID_HDR; break; }
+                break;
+            }
+            case 17:
+                r = ld(f, avail, L, off, 4, &t.dport);
+                if (r == OR_E_TRUNC) { ret = r; break; }
+                if (r) { ret = OR_DROP_CT_INVALID_HDR; break; }
+                break;
+            default:
+                ret = OR_DROP_CT_UNKNOWN_PROTO;
+            }
+            if (ret == 0) {
+                uint16_t p = t.sport; t.sport = t.dport; t.dport = p;   /* ipv4_ct_tuple_reverse */
+                int v = policy_can_access_ingress(ep->policy, dp->flags, L, identity, t.dport, t.nexthdr,
+                                                  &ps.nl, &ps.nu);
+                if (v < 0) ret = OR_DROP_POLICY;
+                else { ret = v; if (!skip_proxy && v > 0) ps.proxy = (uint16_t)v; }
+                if (skip_proxy && v > 0) ret = 0;
+            }
+        }
+        if (ret < 0 && ret != OR_E_TRUNC) update_metrics(dp, L, 1, (uint8_t)(-ret));
+        if (out->ret) out->ret[i] = ret;
+        if (out->identity) out->identity[i] = identity;
+        if (out->proxy) out->proxy[i] = ps.proxy;
+        if (out->ct) out->ct[i] = OR_CT_NONE;
+        if (out->nl) out->nl[i] = ps.nl;
+        if (out->nu) out->nu[i] = ps.nu;
+    }
+}
+
+/* ===================================================================== */
+/* Load balancer lookup (bpf/lib/lb.h:604-635), LB_L4 and LB_L3 on        */
+/* ===================================================================== */
+
+const or_lb4_service *or_lb4_lookup_service(or_map *svc_map, or_lb4_key *key, uint8_t *nl)
+{
+    if (key->dport) {
+        (*nl)++;
+        or_lb4_service *s = or_map_lookup_ptr(svc_map, key);
+        if (s && s->count != 0) return s;
+        key->dport = 0;
+    }
+    (*nl)++;
+    or_lb4_service *s = or_map_lookup_ptr(svc_map, key);
+    if (s && s->count != 0) return s;
+    return NULL;
+}

@@ -1,0 +1,191 @@
+/*
+ * cv_oracle.h — CPU restatement of Cilium's L3/L4 verdict path (TEST INFRASTRUCTURE).
+ *
+ * This is the parity oracle for the MI355X verdict engine.  It is NOT product
+ * code: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load it, and only as the checker.  The product library (cilium_amd/) never
+ * links or calls anything under oracle/.
+ *
+ * Every function restates a function of the reference (Taeung/cilium v1.1.90,
+ * /root/reference) and cites the file:line it follows.  Kernel map semantics
+ * (HASH / LRU_HASH / LPM_TRIE from Linux kernel/bpf/{hashtab,lpm_trie}.c, a
+ * third-party dependency absent from the reference) are restated from their
+ * published behaviour and pinned against the container kernel's own maps
+ * (oracle/kernel_golden.py -> tests/golden/).
+ */
+#ifndef CV_ORACLE_H
+#define CV_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- BPF map types / flags (include/linux/bpf.h in the reference) ---- */
+#define OR_MAP_HASH      1
+#define OR_MAP_LRU_HASH  9
+#define OR_MAP_LPM_TRIE 11
+#define OR_BPF_ANY       0
+#define OR_BPF_NOEXIST   1
+#define OR_BPF_EXIST     2
+
+/* ---- return codes (bpf/include/bpf/api.h:18-25, include/linux/bpf.h:623-628) */
+#define OR_TC_ACT_OK        0
+#define OR_TC_ACT_SHOT      2
+#define OR_TC_ACT_REDIRECT  7
+#define OR_XDP_DROP 1
+#define OR_XDP_PASS 2
+
+/* ---- datapath drop codes (bpf/lib/common.h:237-269) */
+#define OR_DROP_INVALID_SMAC      -130
+#define OR_DROP_INVALID_DMAC      -131
+#define OR_DROP_INVALID_SIP       -132
+#define OR_DROP_POLICY            -133
+#define OR_DROP_INVALID           -134
+#define OR_DROP_CT_INVALID_HDR    -135
+#define OR_DROP_CT_UNKNOWN_PROTO  -137
+#define OR_DROP_UNKNOWN_L3        -139
+#define OR_DROP_MISSED_TAIL_CALL  -140
+#define OR_DROP_UNKNOWN_L4        -142
+#define OR_DROP_NO_LXC            -152
+#define OR_DROP_CT_CREATE_FAILED  -155
+#define OR_DROP_INVALID_EXTHDR    -156
+#define OR_DROP_FRAG_NOSUPPORT    -157
+#define OR_DROP_NO_SERVICE        -158
+/* oracle-only: a header byte the reference would read lies beyond the record */
+#define OR_E_TRUNC                -1
+
+/* CT results (bpf/lib/common.h:331-336) */
+#define OR_CT_NEW 0
+#define OR_CT_ESTABLISHED 1
+#define OR_CT_REPLY 2
+#define OR_CT_RELATED 3
+#define OR_CT_NONE 0xff
+
+/* CT directions (bpf/lib/common.h:327-329) */
+#define OR_CT_EGRESS  0
+#define OR_CT_INGRESS 1
+#define OR_CT_SERVICE 2
+
+/* ---- key/value layouts (bpf/lib/common.h, bpf/lib/maps.h, bpf/lib/xdp.h) */
+#pragma pack(push, 1)
+typedef struct { uint32_t prefixlen; uint8_t addr[4]; } or_lpm_v4_key;    /* xdp.h:23-26 */
+typedef struct { uint32_t prefixlen; uint8_t addr[16]; } or_lpm_v6_key;   /* xdp.h:28-31 */
+typedef struct { uint8_t ip[16]; uint8_t family; uint8_t pad4; uint16_t pad5; } or_endpoint_key; /* common.h:147-160 */
+typedef struct { uint32_t prefixlen; uint8_t pad[3]; uint8_t family; uint8_t ip[16]; } or_ipcache_key; /* maps.h:135-148 */
+typedef struct { uint32_t daddr, saddr; uint16_t dport, sport; uint8_t nexthdr, flags; } or_ipv4_ct_tuple; /* common.h:359-367 */
+typedef struct { uint32_t address; uint16_t dport; uint16_t slave; } or_lb4_key;                /* common.h:427-431 */
+typedef struct { uint32_t target; uint16_t port; uint16_t count; uint16_t rev_nat_index; uint16_t weight; } or_lb4_service; /* common.h:433-439 */
+typedef struct { uint8_t address[16]; uint16_t dport; uint16_t slave; } or_lb6_key;             /* common.h:408-412 */
+typedef struct { uint8_t target[16]; uint16_t port; uint16_t count; uint16_t rev_nat_index; uint16_t weight; } or_lb6_service; /* common.h:414-420 */
+#pragma pack(pop)
+
+typedef struct {             /* common.h:165-173, 48 bytes */
+    uint32_t ifindex; uint16_t unused; uint16_t lxc_id; uint32_t flags;
+    uint32_t mac_lo, mac_hi, node_mac_lo, node_mac_hi; uint32_t pad[4];
+} or_endpoint_info;
+typedef struct { uint32_t sec_label; uint32_t tunnel_endpoint; } or_remote_endpoint_info; /* common.h:175-178 */
+typedef struct { uint32_t sec_label; uint16_t dport; uint8_t protocol; uint8_t egress_pad; } or_policy_key; /* common.h:180-186 */
+typedef struct { uint16_t proxy_port; uint16_t pad[3]; uint64_t packets; uint64_t bytes; } or_policy_entry;  /* common.h:188-193 */
+typedef struct {             /* common.h:380-406, 56 bytes; bits@36: rx_closing b0, tx_closing b1, nat46 b2, lb_loopback b3, seen_non_syn b4 */
+    uint64_t rx_packets, rx_bytes, tx_packets, tx_bytes;
+    uint32_t lifetime; uint16_t bits; uint16_t rev_nat_index; uint16_t slave;
+    uint8_t tx_flags_seen, rx_flags_seen; uint32_t src_sec_id; uint32_t last_tx_report, last_rx_report;
+} or_ct_entry;
+typedef struct {             /* common.h:452-461 (internal) */
+    uint16_t rev_nat_index; uint16_t loopback; uint16_t orig_dport; uint32_t addr, svc_addr, src_sec_id; uint16_t slave;
+} or_ct_state;
+
+/* ---- generic kernel-semantics map ---- */
+typedef struct or_map or_map;
+or_map  *or_map_create(int type, uint32_t key_size, uint32_t val_size, uint32_t max_entries);
+void     or_map_free(or_map *m);
+int      or_map_update(or_map *m, const void *key, const void *val, uint64_t flags);
+int      or_map_lookup(or_map *m, const void *key, void *val_out);
+int      or_map_delete(or_map *m, const void *key);
+uint32_t or_map_count(const or_map *m);
+/* all entries, sorted by key bytes; returns the count written (<= max) */
+uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max);
+void    *or_map_lookup_ptr(or_map *m, const void *key);
+
+/* ---- restated helpers pinned by test/bpf/unit-test.c ---- */
+uint32_t or_get_prefix(int prefix);                               /* ipv6.h:136-138 (GET_PREFIX) */
+void     or_ipv6_addr_clear_suffix(uint8_t addr[16], int prefix); /* ipv6.h:140-150 */
+
+/* ---- datapath configuration ---- */
+#define OR_F_FROM_HOST      0x1   /* bpf_netdev.c built with netdev_config.h FROM_HOST */
+#define OR_F_HAVE_L4_POLICY 0x2   /* lxc_config.h HAVE_L4_POLICY */
+#define OR_F_DROP_ALL       0x4   /* pkg/endpoint/bpf.go DROP_ALL */
+#define OR_F_CT_ACCOUNTING  0x8   /* CONNTRACK_ACCOUNTING (daemon/main.go:676 default on) */
+#define OR_F_POLICY_INGRESS 0x10  /* POLICY_INGRESS */
+#define OR_F_POLICY_EGRESS  0x20  /* POLICY_EGRESS */
+#define OR_F_DEFAULT (OR_F_FROM_HOST | OR_F_HAVE_L4_POLICY | OR_F_CT_ACCOUNTING | OR_F_POLICY_INGRESS | OR_F_POLICY_EGRESS)
+
+#define OR_MAX_EP 64
+typedef struct {
+    uint16_t lxc_id; uint32_t seclabel;
+    or_map *policy;          /* cilium_policy_<id> */
+    or_map *ct4;             /* CT_MAP4 of this endpoint (may be a shared global map) */
+} or_endpoint_prog;
+
+typedef struct or_dp {
+    /* prefilter (bpf_xdp.c); NULL disables the map (filter_config.h) */
+    or_map *v4_fix, *v4_dyn, *v6_fix, *v6_dyn;
+    or_map *lxc;             /* cilium_lxc  (maps.h:27-33) */
+    or_map *ipcache;         /* cilium_ipcache (maps.h:151-158) */
+    or_map *lb4_services, *lb6_services;
+    uint32_t flags;
+    uint32_t n_ep;
+    or_endpoint_prog ep[OR_MAX_EP];   /* tail-call targets of cilium_policy (maps.h:44-51) */
+    uint64_t metrics[256][4][2];      /* Σ over CPUs of cilium_metrics (metrics.h:43-58): [reason][dir]{count,bytes} */
+} or_dp;
+
+or_dp *or_dp_create(uint32_t flags);
+void   or_dp_free(or_dp *dp);          /* does not free maps */
+int    or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *policy, or_map *ct4);
+void   or_dp_metrics(const or_dp *dp, uint64_t *out /* [256][4][2] */);
+
+/* per-packet outputs (SoA; any pointer may be NULL) */
+typedef struct {
+    uint8_t  *xdp;        /* XDP verdict (1 drop / 2 pass) */
+    int32_t  *ret;        /* tc verdict: negative DROP_*, TC_ACT_OK, TC_ACT_REDIRECT */
+    uint32_t *identity;   /* resolved source identity */
+    uint8_t  *ct;         /* CT result or OR_CT_NONE */
+    uint16_t *proxy;      /* proxy port (raw be16) when redirected to proxy */
+    uint8_t  *nl;         /* map lookups performed (algorithmic bytes) */
+    uint8_t  *nu;         /* map entry writes performed */
+} or_out;
+
+/* Config 1: bpf_xdp.c xdp_start over a batch of frames (records of `stride` bytes). */
+void or_xdp_prefilter(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                      uint32_t n, or_out *out);
+
+/* Config 2: ingress verdict of a NEW flow for one endpoint: netdev identity resolution
+ * (bpf_netdev.c:357-398) + policy_can_access_ingress (policy.h:305-329) with the L4
+ * key as ct_lookup4 leaves it (conntrack.h:442-562) on a CT miss.  Parallel (OpenMP)
+ * with atomic policy counters. */
+void or_policy_ingress(or_dp *dp, uint32_t ep_index, const uint8_t *frames, uint32_t stride,
+                       const uint32_t *len, const uint32_t *mark, uint32_t n, or_out *out);
+
+/* Config 3: full ingress path: [XDP prefilter] -> from_netdev/handle_ipv4 -> tail call
+ * into the endpoint's ipv4_policy (CT lookup/create, policy).  Sequential, as one CPU. */
+void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                       const uint32_t *mark, uint32_t n, uint32_t now, int with_prefilter, or_out *out);
+
+/* ct_create4 on a given tuple (conntrack.h:663-744), for building preloaded tables. */
+int or_ct_create4(or_map *ct, or_ipv4_ct_tuple *tuple, uint32_t skb_len, int dir,
+                  const or_ct_state *st, uint32_t now);
+/* ct_lookup4 on a frame (conntrack.h:442-562); tuple in/out. */
+int or_ct_lookup4(or_map *ct, or_ipv4_ct_tuple *tuple, const uint8_t *frame, uint32_t avail,
+                  uint32_t len, int l4_off, int dir, or_ct_state *st, uint32_t now, uint32_t flags,
+                  uint8_t *nl, uint8_t *nu);
+
+/* lb4_lookup_service (lb.h:604-635) */
+const or_lb4_service *or_lb4_lookup_service(or_map *svc_map, or_lb4_key *key, uint8_t *nl);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,212 @@
+"""ctypes binding of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module, and only as the checker.  See cv_oracle.h for what it restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libcv_oracle.so")
+REF_PROBE = os.path.join(HERE, "_ref", "libref_probe.so")
+
+F_FROM_HOST, F_HAVE_L4_POLICY, F_DROP_ALL, F_CT_ACCOUNTING = 0x1, 0x2, 0x4, 0x8
+F_POLICY_INGRESS, F_POLICY_EGRESS = 0x10, 0x20
+F_DEFAULT = F_FROM_HOST | F_HAVE_L4_POLICY | F_CT_ACCOUNTING | F_POLICY_INGRESS | F_POLICY_EGRESS
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+        L.or_map_create.restype = vp
+        L.or_map_create.argtypes = [i32, u32, u32, u32]
+        L.or_map_free.argtypes = [vp]
+        L.or_map_update.argtypes = [vp, vp, vp, u64]
+        L.or_map_lookup.argtypes = [vp, vp, vp]
+        L.or_map_delete.argtypes = [vp, vp]
+        L.or_map_count.restype = u32
+        L.or_map_count.argtypes = [vp]
+        L.or_map_dump.restype = u32
+        L.or_map_dump.argtypes = [vp, vp, vp, u32]
+        L.or_get_prefix.restype = u32
+        L.or_get_prefix.argtypes = [i32]
+        L.or_ipv6_addr_clear_suffix.argtypes = [vp, i32]
+        L.or_dp_create.restype = vp
+        L.or_dp_create.argtypes = [u32]
+        L.or_dp_free.argtypes = [vp]
+        L.or_dp_add_endpoint.argtypes = [vp, C.c_uint16, u32, vp, vp]
+        L.or_dp_metrics.argtypes = [vp, vp]
+        L.or_xdp_prefilter.argtypes = [vp, vp, u32, vp, u32, vp]
+        L.or_policy_ingress.argtypes = [vp, u32, vp, u32, vp, vp, u32, vp]
+        L.or_netdev_ingress.argtypes = [vp, vp, u32, vp, vp, u32, u32, i32, vp]
+        L.or_ct_create4.argtypes = [vp, vp, u32, i32, vp, u32]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class OMap:
+    def __init__(self, type_, key_size, val_size, max_entries):
+        self.h = lib().or_map_create(type_, key_size, val_size, max_entries)
+        if not self.h:
+            raise ValueError("or_map_create failed")
+        self.ks, self.vs = key_size, val_size
+
+    @classmethod
+    def from_spec(cls, spec):
+        m = cls(spec.type, spec.key_size, spec.val_size, spec.max_entries)
+        m.load(spec.keys, spec.vals)
+        return m
+
+    def load(self, keys, vals):
+        L = lib()
+        keys = np.ascontiguousarray(keys, np.uint8)
+        vals = np.ascontiguousarray(vals, np.uint8)
+        for i in range(len(keys)):
+            r = L.or_map_update(self.h, keys[i].ctypes.data, vals[i].ctypes.data, 0)
+            if r != 0:
+                raise OSError(-r, f"or_map_update[{i}]")
+
+    def update(self, key, val, flags=0):
+        k = np.ascontiguousarray(np.frombuffer(bytes(key), np.uint8))
+        v = np.ascontiguousarray(np.frombuffer(bytes(val), np.uint8))
+        return lib().or_map_update(self.h, k.ctypes.data, v.ctypes.data, flags)
+
+    def lookup(self, key):
+        k = np.ascontiguousarray(np.frombuffer(bytes(key), np.uint8))
+        v = np.zeros(self.vs, np.uint8)
+        r = lib().or_map_lookup(self.h, k.ctypes.data, v.ctypes.data)
+        return (r, bytes(v) if r == 0 else None)
+
+    def delete(self, key):
+        k = np.ascontiguousarray(np.frombuffer(bytes(key), np.uint8))
+        return lib().or_map_delete(self.h, k.ctypes.data)
+
+    def __len__(self):
+        return lib().or_map_count(self.h)
+
+    def dump(self):
+        n = len(self)
+        keys = np.zeros((max(n, 1), self.ks), np.uint8)
+        vals = np.zeros((max(n, 1), self.vs), np.uint8)
+        k = lib().or_map_dump(self.h, _p(keys), _p(vals), n)
+        return keys[:k], vals[:k]
+
+    def __del__(self):
+        try:
+            lib().or_map_free(self.h)
+        except Exception:
+            pass
+
+
+class Out:
+    """Per-packet oracle outputs (SoA)."""
+
+    def __init__(self, n):
+        self.xdp = np.zeros(n, np.uint8)
+        self.ret = np.zeros(n, np.int32)
+        self.identity = np.zeros(n, np.uint32)
+        self.ct = np.zeros(n, np.uint8)
+        self.proxy = np.zeros(n, np.uint16)
+        self.nl = np.zeros(n, np.uint8)
+        self.nu = np.zeros(n, np.uint8)
+
+    def struct(self):
+        return (C.c_void_p * 7)(*[a.ctypes.data for a in
+                                  (self.xdp, self.ret, self.identity, self.ct, self.proxy, self.nl, self.nu)])
+
+
+class ODp:
+    """The oracle datapath: maps bound by role, endpoints, metrics."""
+
+    ROLES = ("v4_fix", "v4_dyn", "v6_fix", "v6_dyn", "lxc", "ipcache", "lb4_services", "lb6_services")
+
+    def __init__(self, flags=F_DEFAULT):
+        self.h = lib().or_dp_create(flags)
+        self.maps = {}
+        self.keep = []
+
+    def bind(self, role, omap):
+        idx = self.ROLES.index(role)
+        # or_dp layout: 8 map pointers first
+        ptrs = C.cast(self.h, C.POINTER(C.c_void_p))
+        ptrs[idx] = omap.h
+        self.maps[role] = omap
+
+    def add_endpoint(self, lxc_id, seclabel, policy, ct4=None):
+        self.keep += [policy, ct4]
+        return lib().or_dp_add_endpoint(self.h, lxc_id, seclabel, policy.h if policy else None,
+                                        ct4.h if ct4 else None)
+
+    def metrics(self):
+        m = np.zeros((256, 4, 2), np.uint64)
+        lib().or_dp_metrics(self.h, m.ctypes.data)
+        return m
+
+    def xdp_prefilter(self, frames, length):
+        n = len(length)
+        out = Out(n)
+        frames = np.ascontiguousarray(frames, np.uint8)
+        length = np.ascontiguousarray(length, np.uint32)
+        s = out.struct()
+        lib().or_xdp_prefilter(self.h, _p(frames), frames.shape[1], _p(length), n, C.byref(s))
+        return out
+
+    def policy_ingress(self, ep_index, frames, length, mark=None):
+        n = len(length)
+        out = Out(n)
+        frames = np.ascontiguousarray(frames, np.uint8)
+        length = np.ascontiguousarray(length, np.uint32)
+        mark = None if mark is None else np.ascontiguousarray(mark, np.uint32)
+        s = out.struct()
+        lib().or_policy_ingress(self.h, ep_index, _p(frames), frames.shape[1], _p(length), _p(mark), n,
+                                C.byref(s))
+        return out
+
+    def netdev_ingress(self, frames, length, mark=None, now=0, with_prefilter=True):
+        n = len(length)
+        out = Out(n)
+        frames = np.ascontiguousarray(frames, np.uint8)
+        length = np.ascontiguousarray(length, np.uint32)
+        mark = None if mark is None else np.ascontiguousarray(mark, np.uint32)
+        s = out.struct()
+        lib().or_netdev_ingress(self.h, _p(frames), frames.shape[1], _p(length), _p(mark), n, now,
+                                1 if with_prefilter else 0, C.byref(s))
+        return out
+
+    def __del__(self):
+        try:
+            lib().or_dp_free(self.h)
+        except Exception:
+            pass
+
+
+def ref_probe():
+    """The reference's own pure helpers (oracle/_ref), or None if not built."""
+    if not os.path.exists(REF_PROBE):
+        return None
+    L = C.CDLL(REF_PROBE)
+    L.ref_get_prefix.restype = C.c_uint32
+    L.ref_get_prefix.argtypes = [C.c_int]
+    L.ref_ipv6_addr_clear_suffix.argtypes = [C.c_void_p, C.c_int]
+    L.ref_layout.restype = C.c_long
+    L.ref_layout.argtypes = [C.c_int]
+    return L

@@ -1,0 +1,898 @@
+// cv_ctx.cpp — the C-ABI (include/cilium_hip.h): map store, program->map binding,
+// compilation of the device tables and the batch entry points.
+//
+// Maps: every map the agent creates lives in a HostMap with the kernel's semantics
+// (pkg/bpf/bpf.go:101-245 -> kernel/bpf).  Maps the datapath reads are compiled into
+// per-role device tables (cv_hash.hpp, cv_lpm.hpp) at the next batch boundary
+// (cv_sync).  Two kinds of state are written by the datapath itself and are
+// device-authoritative: policy counters (policy.h:76-100) and conntrack tables
+// (conntrack.h); host reads of them fetch from HBM.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/cilium_hip.h"
+#include "cv_dp.hpp"
+#include "cv_hostmap.hpp"
+
+using namespace cv;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    int alloc(size_t bytes)
+    {
+        release();
+        if (!bytes) return 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) { p = nullptr; return -ENOMEM; }
+        n = bytes;
+        return 0;
+    }
+    int upload(const void *src, size_t bytes)
+    {
+        int r = alloc(bytes);
+        if (r) return r;
+        return hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// A device hash table plus the host image it was built from.
+struct DevHash {
+    DevBuf buckets, vals;
+    std::vector<uint32_t> hb;   // host image of the buckets
+    HashTable view{};
+    uint64_t nb = 0;
+};
+
+template <class S>
+int build_hash(DevHash &d, const std::vector<std::vector<uint32_t>> &keys, const std::vector<std::vector<uint32_t>> &ivals,
+               uint32_t vstride, const std::vector<uint8_t> *vals, std::vector<int64_t> *slots)
+{
+    uint64_t nb = buckets_for(keys.size(), S::SPB);
+    for (int attempt = 0; attempt < 8; ++attempt, nb <<= 1) {
+        d.hb.assign(nb * S::BW, 0);
+        HashTable t{d.hb.data(), nullptr, nb - 1, vstride, (uint32_t)S::SPB};
+        bool ok = true;
+        if (slots) slots->assign(keys.size(), -1);
+        for (size_t i = 0; i < keys.size() && ok; ++i) {
+            int64_t s = host_upsert<S>(t, keys[i].data(), S::IVW ? ivals[i].data() : nullptr);
+            if (s < 0) ok = false;
+            else if (slots) (*slots)[i] = s;
+        }
+        if (!ok) continue;
+        d.nb = nb;
+        int r = d.buckets.upload(d.hb.data(), d.hb.size() * 4);
+        if (r) return r;
+        if (vstride) {
+            std::vector<uint8_t> hv(nb * S::SPB * vstride, 0);
+            if (vals && slots)
+                for (size_t i = 0; i < keys.size(); ++i)
+                    memcpy(&hv[(size_t)(*slots)[i] * vstride], vals->data() + i * vstride, vstride);
+            r = d.vals.upload(hv.data(), hv.size());
+            if (r) return r;
+        } else {
+            d.vals.release();
+        }
+        d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, vstride, (uint32_t)S::SPB};
+        return 0;
+    }
+    return -E2BIG;
+}
+
+struct DevLpm4 {
+    DevBuf l1, chunks;
+    Lpm4 view{nullptr, nullptr};
+};
+
+struct DevLpm6 {
+    DevHash h;
+    DevBuf lens;
+    Lpm6 view{};
+};
+
+enum MapKind { MK_PLAIN = 0, MK_CT4 = 1 };
+
+struct MapObj {
+    std::unique_ptr<HostMap> hm;
+    int kind = MK_PLAIN;
+    // policy compilation (when bound as an endpoint policy map)
+    bool is_policy = false;
+    DevHash pol;
+    uint64_t pol_version = 0;
+    std::set<std::string> written;      // keys whose value the agent wrote since the last sync
+    // conntrack (device-authoritative)
+    DevHash ct;
+    uint32_t ct_id = 0;
+};
+
+struct Endpoint {
+    uint16_t lxc_id;
+    uint32_t seclabel;
+    int policy, ct4;
+};
+
+}  // namespace
+
+struct cv_ctx {
+    int device = 0;
+    uint32_t flags = CV_F_DEFAULT;
+    std::mutex mu;
+    std::vector<std::unique_ptr<MapObj>> maps;
+    int role[CV_NUM_ROLES];
+    uint64_t role_version[CV_NUM_ROLES];
+    DevHash cidr4_fix, cidr6_fix, lxc4, lxc6;
+    DevLpm4 cidr4_dyn, ipc4;
+    DevLpm6 cidr6_dyn, ipc6;
+    std::vector<Endpoint> eps;
+    bool eps_dirty = true;
+    DevBuf eps_dev, ep_of_lxc;
+    DevBuf metrics_own;
+    unsigned long long *metrics = nullptr;
+    DevBuf gtable, gslot, gnext, gsecctx, gmeta;
+    uint64_t gcap = 0, gn = 0;
+    uint32_t epoch = 0;
+    DevBuf ctio;
+    uint32_t next_ct_id = 1;
+};
+
+namespace {
+
+MapObj *get(cv_ctx *c, int h)
+{
+    if (h < 0 || (size_t)h >= c->maps.size()) return nullptr;
+    return c->maps[h].get();
+}
+
+int set_device(cv_ctx *c)
+{
+    if (c->device < 0) return -ENODEV;      // host-only context
+    return hipSetDevice(c->device) == hipSuccess ? 0 : -ENODEV;
+}
+
+std::string kstr(const uint8_t *k, uint32_t n) { return std::string(reinterpret_cast<const char *>(k), n); }
+
+inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+// ---------------------------------------------------------------- role compilers
+int compile_lxc(cv_ctx *c, HostMap *m)
+{
+    std::vector<std::vector<uint32_t>> k4, v4, k6, v6;
+    if (m) {
+        if (m->ks != 20 || m->vs < 12) return -EINVAL;
+        m->for_each([&](const uint8_t *k, const uint8_t *v) {
+            if (k[17] || k[18] || k[19]) return;            // pads are zero in datapath keys
+            const uint32_t iv = rd16(v + 6) | ((rd32(v + 8) & 1u) << 16) | ((rd32(v) != 0) << 17);
+            if (k[16] == 1) {
+                for (int i = 4; i < 16; ++i) if (k[i]) return;
+                k4.push_back({rd32(k)});
+                v4.push_back({iv});
+            } else if (k[16] == 2) {
+                k6.push_back({rd32(k), rd32(k + 4), rd32(k + 8), rd32(k + 12)});
+                v6.push_back({iv});
+            }
+        });
+    }
+    int r = build_hash<LxcV4Spec>(c->lxc4, k4, v4, 0, nullptr, nullptr);
+    if (!r) r = build_hash<LxcV6Spec>(c->lxc6, k6, v6, 0, nullptr, nullptr);
+    if (!m) { c->lxc4.view = HashTable{}; c->lxc6.view = HashTable{}; }
+    return r;
+}
+
+int compile_cidr_fix(cv_ctx *c, HostMap *m, bool v6)
+{
+    std::vector<std::vector<uint32_t>> keys, none;
+    DevHash &d = v6 ? c->cidr6_fix : c->cidr4_fix;
+    if (!m) { d.view = HashTable{}; return 0; }
+    if (m->ks != (v6 ? 20u : 8u)) return -EINVAL;
+    m->for_each([&](const uint8_t *k, const uint8_t *) {
+        if (rd32(k) != (v6 ? 128u : 32u)) return;           // datapath keys carry prefixlen 32/128
+        if (v6) keys.push_back({rd32(k + 4), rd32(k + 8), rd32(k + 12), rd32(k + 16)});
+        else keys.push_back({rd32(k + 4)});
+    });
+    return v6 ? build_hash<Cidr6Spec>(d, keys, none, 0, nullptr, nullptr)
+              : build_hash<Cidr4Spec>(d, keys, none, 0, nullptr, nullptr);
+}
+
+struct Pfx {
+    uint32_t prio;       // full prefixlen in the map
+    int plen;            // prefix length within the address
+    uint32_t a[4];       // address words (raw network order)
+    uint32_t value;
+};
+
+int upload_lpm4(DevLpm4 &d, std::vector<Pfx> &px)
+{
+    std::stable_sort(px.begin(), px.end(), [](const Pfx &x, const Pfx &y) { return x.prio < y.prio; });
+    Lpm4Builder b;
+    for (const Pfx &p : px) b.insert(bswap32(p.a[0]), p.plen, p.value);
+    int r = d.l1.upload(b.l1.data(), b.l1.size() * 4);
+    if (!r) {
+        if (b.chunks.empty()) b.chunks.assign(256, 0);
+        r = d.chunks.upload(b.chunks.data(), b.chunks.size() * 4);
+    }
+    d.view = r ? Lpm4{nullptr, nullptr} : Lpm4{d.l1.as<uint32_t>(), d.chunks.as<uint32_t>()};
+    return r;
+}
+
+int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
+{
+    std::stable_sort(px.begin(), px.end(), [](const Pfx &x, const Pfx &y) { return x.prio < y.prio; });
+    // later (higher priority) entries win for identical (masked addr, plen)
+    std::map<std::vector<uint32_t>, uint32_t> uniq;
+    std::set<int> lens;
+    for (const Pfx &p : px) {
+        std::vector<uint32_t> k(5);
+        for (int w = 0; w < 4; ++w) {
+            int bits = p.plen - 32 * w;
+            uint32_t m = bits <= 0 ? 0u : bits >= 32 ? 0xFFFFFFFFu : bswap32(0xFFFFFFFFu << (32 - bits));
+            k[w] = p.a[w] & m;
+        }
+        k[4] = (uint32_t)p.plen;
+        uniq[k] = p.value;
+        lens.insert(p.plen);
+    }
+    std::vector<std::vector<uint32_t>> keys, vals;
+    for (auto &kv : uniq) { keys.push_back(kv.first); vals.push_back({kv.second}); }
+    int r = build_hash<Lpm6Spec>(d.h, keys, vals, 0, nullptr, nullptr);
+    if (r) return r;
+    std::vector<uint8_t> l(lens.rbegin(), lens.rend());
+    if (l.empty()) l.push_back(0);
+    r = d.lens.upload(l.data(), l.size());
+    d.view = Lpm6{d.h.view, d.lens.as<uint8_t>(), (uint32_t)lens.size()};
+    return r;
+}
+
+int compile_cidr_dyn(cv_ctx *c, HostMap *m, bool v6)
+{
+    if (!m) {
+        if (v6) c->cidr6_dyn.view = Lpm6{}; else c->cidr4_dyn.view = Lpm4{nullptr, nullptr};
+        return 0;
+    }
+    if (!m->is_lpm() || m->ks != (v6 ? 20u : 8u)) return -EINVAL;
+    std::vector<Pfx> px;
+    m->for_each([&](const uint8_t *k, const uint8_t *) {
+        Pfx p{};
+        p.prio = rd32(k);
+        p.plen = (int)p.prio;
+        for (int w = 0; w < (v6 ? 4 : 1); ++w) p.a[w] = rd32(k + 4 + 4 * w);
+        p.value = 1;
+        px.push_back(p);
+    });
+    return v6 ? upload_lpm6(c->cidr6_dyn, px) : upload_lpm4(c->cidr4_dyn, px);
+}
+
+// cilium_ipcache: a v4 lookup key is {prefixlen 64, pad 0, family 1, ip4, 0...}
+// (eps.h:309-319); it matches stored elements with prefixlen <= 64 whose first
+// min(prefixlen, 32) bits equal {0, 0, 0, 1}.  Same for v6 with family 2, 160.
+int compile_ipcache(cv_ctx *c, HostMap *m)
+{
+    if (!m) { c->ipc4.view = Lpm4{nullptr, nullptr}; c->ipc6.view = Lpm6{}; return 0; }
+    if (!m->is_lpm() || m->ks != 24 || m->vs < 4) return -EINVAL;
+    std::vector<Pfx> p4, p6;
+    int err = 0;
+    m->for_each([&](const uint8_t *k, const uint8_t *v) {
+        const uint32_t plen = rd32(k);
+        const uint32_t label = rd32(v);
+        for (int fam = 1; fam <= 2; ++fam) {
+            const uint8_t want[4] = {0, 0, 0, (uint8_t)fam};
+            const uint32_t sbits = plen < 32 ? plen : 32;
+            bool match = true;
+            for (uint32_t bit = 0; bit < sbits; ++bit) {
+                const uint8_t mb = 0x80 >> (bit & 7);
+                if ((k[4 + bit / 8] & mb) != (want[bit / 8] & mb)) { match = false; break; }
+            }
+            if (!match) continue;
+            if (fam == 1 && plen > 64) continue;
+            if (label & 0x80000000u) { err = -ERANGE; continue; }
+            Pfx p{};
+            p.prio = plen;
+            p.plen = plen > 32 ? (int)(plen - 32) : 0;
+            p.value = label;
+            for (int w = 0; w < 4; ++w) p.a[w] = rd32(k + 8 + 4 * w);
+            (fam == 1 ? p4 : p6).push_back(p);
+        }
+    });
+    if (err) return err;
+    int r = upload_lpm4(c->ipc4, p4);
+    if (!r) r = upload_lpm6(c->ipc6, p6);
+    return r;
+}
+
+// policy map -> PolicySpec table + 32-B side values; device counters of entries the
+// agent did not rewrite since the last sync are carried over.
+int compile_policy(cv_ctx *c, MapObj *mo)
+{
+    (void)c;
+    HostMap *m = mo->hm.get();
+    if (m->ks != 8 || m->vs != 24 || m->is_lpm()) return -EINVAL;
+    if (mo->pol.view.buckets) {
+        std::vector<uint8_t> dv(mo->pol.vals.n);
+        if (hipMemcpy(dv.data(), mo->pol.vals.p, dv.size(), hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+        HashTable old{mo->pol.hb.data(), nullptr, mo->pol.nb - 1, 32, PolicySpec::SPB};
+        m->for_each([&](const uint8_t *k, const uint8_t *v) {
+            if (mo->written.count(kstr(k, 8))) return;
+            uint32_t kw[2] = {rd32(k), rd32(k + 4)};
+            int64_t s = host_find<PolicySpec>(old, kw);
+            if (s >= 0) memcpy(const_cast<uint8_t *>(v) + 8, &dv[(size_t)s * 32 + 8], 16);
+        });
+    }
+    mo->written.clear();
+    std::vector<std::vector<uint32_t>> keys, none;
+    std::vector<uint8_t> vals;
+    m->for_each([&](const uint8_t *k, const uint8_t *v) {
+        keys.push_back({rd32(k), rd32(k + 4)});
+        size_t o = vals.size();
+        vals.resize(o + 32, 0);
+        memcpy(&vals[o], v, 24);
+    });
+    std::vector<int64_t> slots;
+    int r = build_hash<PolicySpec>(mo->pol, keys, none, 32, &vals, &slots);
+    if (!r) mo->pol_version = m->version;
+    return r;
+}
+
+// CT table sized for max_entries (+ its ICMP-related twins), filled from the host store
+int compile_ct(cv_ctx *c, MapObj *mo)
+{
+    HostMap *m = mo->hm.get();
+    if (m->ks != 14 || m->vs != 56) return -EINVAL;
+    std::vector<std::vector<uint32_t>> keys, none;
+    std::vector<uint8_t> vals;
+    m->for_each([&](const uint8_t *k, const uint8_t *v) {
+        uint8_t kk[16] = {0};
+        memcpy(kk, k, 14);
+        keys.push_back({rd32(kk), rd32(kk + 4), rd32(kk + 8), rd32(kk + 12)});
+        size_t o = vals.size();
+        vals.resize(o + 64, 0);
+        memcpy(&vals[o], v, 56);
+    });
+    // capacity: max_entries at 60% bucket load
+    const uint64_t want = std::max<uint64_t>(m->max_entries, keys.size());
+    std::vector<std::vector<uint32_t>> pad;
+    DevHash &d = mo->ct;
+    uint64_t nb = buckets_for(want, Ct4Spec::SPB);
+    d.hb.assign(nb * Ct4Spec::BW, 0);
+    HashTable t{d.hb.data(), nullptr, nb - 1, 64, Ct4Spec::SPB};
+    std::vector<uint8_t> hv(nb * Ct4Spec::SPB * 64, 0);
+    for (size_t i = 0; i < keys.size(); ++i) {
+        int64_t s = host_upsert<Ct4Spec>(t, keys[i].data(), nullptr);
+        if (s < 0) return -E2BIG;
+        memcpy(&hv[(size_t)s * 64], &vals[i * 64], 64);
+    }
+    d.nb = nb;
+    int r = d.buckets.upload(d.hb.data(), d.hb.size() * 4);
+    if (!r) r = d.vals.upload(hv.data(), hv.size());
+    if (r) return r;
+    d.hb.clear();
+    d.hb.shrink_to_fit();
+    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, Ct4Spec::SPB};
+    mo->kind = MK_CT4;
+    mo->ct_id = c->next_ct_id++;
+    return 0;
+}
+
+int sync_locked(cv_ctx *c)
+{
+    bool dirty = c->eps_dirty;
+    for (int r = 0; r < CV_NUM_ROLES; ++r) {
+        MapObj *m = get(c, c->role[r]);
+        uint64_t v = m ? m->hm->version : 0;
+        if (v != c->role_version[r]) dirty = true;
+    }
+    for (auto &e : c->eps) {
+        MapObj *p = get(c, e.policy);
+        if (p && p->hm->version != p->pol_version) dirty = true;
+    }
+    if (!dirty) return 0;
+    int r = set_device(c);
+    if (r) return r;
+    (void)hipDeviceSynchronize();          // no batch may still read a table we replace
+    for (int role = 0; role < CV_NUM_ROLES; ++role) {
+        MapObj *m = get(c, c->role[role]);
+        uint64_t v = m ? m->hm->version : 0;
+        if (v == c->role_version[role]) continue;
+        HostMap *hm = m ? m->hm.get() : nullptr;
+        switch (role) {
+        case CV_ROLE_CIDR4_FIX: r = compile_cidr_fix(c, hm, false); break;
+        case CV_ROLE_CIDR6_FIX: r = compile_cidr_fix(c, hm, true); break;
+        case CV_ROLE_CIDR4_DYN: r = compile_cidr_dyn(c, hm, false); break;
+        case CV_ROLE_CIDR6_DYN: r = compile_cidr_dyn(c, hm, true); break;
+        case CV_ROLE_LXC: r = compile_lxc(c, hm); break;
+        case CV_ROLE_IPCACHE: r = compile_ipcache(c, hm); break;
+        default: r = 0; break;             // LB roles: egress path (config 5)
+        }
+        if (r) return r;
+        c->role_version[role] = v;
+    }
+    bool eps_changed = c->eps_dirty;
+    for (auto &e : c->eps) {
+        MapObj *p = get(c, e.policy);
+        if (p && p->hm->version != p->pol_version) {
+            r = compile_policy(c, p);
+            if (r) return r;
+            eps_changed = true;
+        }
+    }
+    if (eps_changed) {
+        std::vector<EpDev> ev;
+        std::vector<uint16_t> of(65536, 0);
+        for (size_t i = 0; i < c->eps.size(); ++i) {
+            const Endpoint &e = c->eps[i];
+            EpDev d{};
+            MapObj *p = get(c, e.policy);
+            MapObj *t = get(c, e.ct4);
+            if (p) d.policy = p->pol.view;
+            if (t) { d.ct4 = t->ct.view; d.ct_id = t->ct_id; }
+            d.seclabel = e.seclabel;
+            ev.push_back(d);
+            of[e.lxc_id] = (uint16_t)(i + 1);
+        }
+        if (ev.empty()) ev.push_back(EpDev{});
+        r = c->eps_dev.upload(ev.data(), ev.size() * sizeof(EpDev));
+        if (!r) r = c->ep_of_lxc.upload(of.data(), of.size() * 2);
+        if (r) return r;
+        c->eps_dirty = false;
+    }
+    return 0;
+}
+
+DpParams params(cv_ctx *c)
+{
+    DpParams p{};
+    p.flags = c->flags;
+    p.n_eps = (uint32_t)c->eps.size();
+    p.cidr4_fix = c->role[CV_ROLE_CIDR4_FIX] >= 0 ? c->cidr4_fix.view : HashTable{};
+    p.cidr6_fix = c->role[CV_ROLE_CIDR6_FIX] >= 0 ? c->cidr6_fix.view : HashTable{};
+    p.lxc4 = c->role[CV_ROLE_LXC] >= 0 ? c->lxc4.view : HashTable{};
+    p.lxc6 = c->role[CV_ROLE_LXC] >= 0 ? c->lxc6.view : HashTable{};
+    p.cidr4_dyn = c->role[CV_ROLE_CIDR4_DYN] >= 0 ? c->cidr4_dyn.view : Lpm4{nullptr, nullptr};
+    p.cidr6_dyn = c->role[CV_ROLE_CIDR6_DYN] >= 0 ? c->cidr6_dyn.view : Lpm6{};
+    p.ipc4 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc4.view : Lpm4{nullptr, nullptr};
+    p.ipc6 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc6.view : Lpm6{};
+    p.eps = c->eps_dev.as<EpDev>();
+    p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
+    p.metrics = c->metrics;
+    return p;
+}
+
+int check_batch(const cv_batch *b)
+{
+    if (!b || (!b->frames && b->n) || (!b->len && b->n)) return -EINVAL;
+    if (b->stride < 64 || (b->stride & 15)) return -EINVAL;
+    if ((reinterpret_cast<uintptr_t>(b->frames) & 15)) return -EINVAL;
+    return 0;
+}
+
+BatchDev to_dev(const cv_batch *b) { return BatchDev{b->frames, b->stride, b->n, b->len, b->mark}; }
+
+OutDev to_dev(const cv_out *o)
+{
+    OutDev d{};
+    if (o) { d.xdp = o->xdp; d.ret = o->ret; d.identity = o->identity; d.ct = o->ct; d.proxy = o->proxy; d.nl = o->nl; d.nu = o->nu; }
+    return d;
+}
+
+int ct_io(cv_ctx *c, MapObj *mo, int op, const uint8_t *key, const uint8_t *val, uint8_t *val_out, uint64_t fl)
+{
+    if (!c->ctio.p && c->ctio.alloc(32 * 4)) return -ENOMEM;
+    uint32_t io[32] = {0};
+    uint8_t kk[16] = {0};
+    memcpy(kk, key, 14);
+    memcpy(io, kk, 16);
+    if (val) memcpy(io + 4, val, 56);
+    if (hipMemcpy(c->ctio.p, io, sizeof(io), hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    if (launch_ct_op(mo->ct.view, op, fl, c->ctio.as<uint32_t>(), nullptr)) return -EIO;
+    if (hipMemcpy(io, c->ctio.p, sizeof(io), hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+    int rc = (int)io[20];
+    if (!rc && val_out) memcpy(val_out, io + 4, 56);
+    return rc;
+}
+
+// all (key, value) rows of a device CT table
+int ct_dump(cv_ctx *c, MapObj *mo, std::vector<uint8_t> &keys, std::vector<uint8_t> &vals)
+{
+    const uint64_t slots = mo->ct.nb * Ct4Spec::SPB;
+    const uint32_t max = (uint32_t)std::min<uint64_t>(slots, 0xFFFFFFF0ull);
+    DevBuf dk, dv, dc;
+    if (dk.alloc((size_t)max * 16) || dv.alloc((size_t)max * 64) || dc.alloc(4)) return -ENOMEM;
+    (void)hipMemset(dc.p, 0, 4);
+    if (launch_ct_scan(mo->ct.view, mo->ct.nb, dk.as<uint32_t>(), dv.as<uint32_t>(), dc.as<uint32_t>(), max, nullptr))
+        return -EIO;
+    uint32_t n = 0;
+    (void)hipMemcpy(&n, dc.p, 4, hipMemcpyDeviceToHost);
+    n = std::min(n, max);
+    std::vector<uint8_t> k16((size_t)n * 16), v64((size_t)n * 64);
+    if (n) {
+        (void)hipMemcpy(k16.data(), dk.p, k16.size(), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(v64.data(), dv.p, v64.size(), hipMemcpyDeviceToHost);
+    }
+    keys.resize((size_t)n * 14);
+    vals.resize((size_t)n * 56);
+    for (uint32_t i = 0; i < n; ++i) {
+        memcpy(&keys[(size_t)i * 14], &k16[(size_t)i * 16], 14);
+        memcpy(&vals[(size_t)i * 56], &v64[(size_t)i * 64], 56);
+    }
+    return (int)n;
+}
+
+// live policy counters of one key from HBM (device-authoritative)
+void policy_counters(MapObj *mo, const uint8_t *key, uint8_t *val)
+{
+    if (!mo->is_policy || !mo->pol.view.buckets || mo->written.count(kstr(key, 8))) return;
+    if (mo->pol_version != mo->hm->version) {
+        // the table was not recompiled since the last write; slots of unchanged keys
+        // are still those of the image
+    }
+    HashTable img{mo->pol.hb.data(), nullptr, mo->pol.nb - 1, 32, PolicySpec::SPB};
+    uint32_t kw[2] = {rd32(key), rd32(key + 4)};
+    int64_t s = host_find<PolicySpec>(img, kw);
+    if (s < 0) return;
+    uint8_t v[32];
+    if (hipMemcpy(v, mo->pol.vals.as<uint8_t>() + (size_t)s * 32, 32, hipMemcpyDeviceToHost) == hipSuccess)
+        memcpy(val + 8, v + 8, 16);
+}
+
+}  // namespace
+
+// ======================================================================= C-ABI
+extern "C" {
+
+const char *cv_version(void) { return "cilium_hip 0.1.0 gfx950"; }
+
+int cv_open(int hip_device, cv_ctx **out)
+{
+    if (!out) return -EINVAL;
+    cv_ctx *c = new cv_ctx();
+    c->device = hip_device;
+    for (int r = 0; r < CV_NUM_ROLES; ++r) { c->role[r] = -1; c->role_version[r] = 0; }
+    if (hip_device == -1) {                 // host-only context: map store without a device
+        *out = c;
+        return 0;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || hip_device < 0 || hip_device >= n) { delete c; return -ENODEV; }
+    if (set_device(c)) { delete c; return -ENODEV; }
+    if (c->metrics_own.alloc(METRICS_WORDS * 8)) { delete c; return -ENOMEM; }
+    (void)hipMemset(c->metrics_own.p, 0, METRICS_WORDS * 8);
+    c->metrics = c->metrics_own.as<unsigned long long>();
+    *out = c;
+    return 0;
+}
+
+void cv_close(cv_ctx *c)
+{
+    if (!c) return;
+    if (c->device >= 0) {
+        (void)hipSetDevice(c->device);
+        (void)hipDeviceSynchronize();
+    }
+    delete c;
+}
+
+int cv_set_flags(cv_ctx *c, uint32_t flags)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->flags = flags;
+    return 0;
+}
+
+int cv_map_create(cv_ctx *c, int type, uint32_t ks, uint32_t vs, uint32_t max_entries, uint32_t flags, int *handle)
+{
+    if (!c || !handle) return -EINVAL;
+    if (type != CV_MAP_HASH && type != CV_MAP_LRU_HASH && type != CV_MAP_LPM_TRIE && type != CV_MAP_PERCPU_HASH)
+        return -EINVAL;
+    if (!ks || !vs || !max_entries || ks > 256) return -EINVAL;
+    if (type == CV_MAP_LPM_TRIE && (ks <= 4 || ks > 4 + 256 / 8 * 8 || !(flags & 1))) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    auto mo = std::make_unique<MapObj>();
+    mo->hm = std::make_unique<HostMap>(type, ks, vs, max_entries, flags);
+    c->maps.push_back(std::move(mo));
+    *handle = (int)c->maps.size() - 1;
+    return 0;
+}
+
+int cv_map_close(cv_ctx *c, int h)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    for (int r = 0; r < CV_NUM_ROLES; ++r) if (c->role[r] == h) return -EBUSY;
+    for (auto &e : c->eps) if (e.policy == h || e.ct4 == h) return -EBUSY;
+    if (c->device >= 0) (void)hipDeviceSynchronize();
+    c->maps[h].reset(new MapObj());
+    c->maps[h]->hm.reset(new HostMap(CV_MAP_HASH, 1, 1, 1, 0));
+    return 0;
+}
+
+int cv_map_update(cv_ctx *c, int h, const void *key, const void *val, uint64_t fl)
+{
+    if (!c || !key || !val) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    if (m->kind == MK_CT4) {
+        if (set_device(c)) return -ENODEV;
+        return ct_io(c, m, 1, (const uint8_t *)key, (const uint8_t *)val, nullptr, fl);
+    }
+    int r = m->hm->update((const uint8_t *)key, (const uint8_t *)val, fl);
+    if (!r && m->is_policy) m->written.insert(kstr((const uint8_t *)key, 8));
+    return r;
+}
+
+int cv_map_update_batch(cv_ctx *c, int h, const void *keys, const void *vals, uint32_t n, uint64_t fl, uint32_t *done)
+{
+    if (!c || (n && (!keys || !vals))) return -EINVAL;
+    MapObj *m;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        m = get(c, h);
+        if (!m) return -EBADF;
+    }
+    const uint8_t *k = (const uint8_t *)keys, *v = (const uint8_t *)vals;
+    for (uint32_t i = 0; i < n; ++i) {
+        int r = cv_map_update(c, h, k + (size_t)i * m->hm->ks, v + (size_t)i * m->hm->vs, fl);
+        if (r) { if (done) *done = i; return r; }
+    }
+    if (done) *done = n;
+    return 0;
+}
+
+int cv_map_lookup(cv_ctx *c, int h, const void *key, void *val)
+{
+    if (!c || !key || !val) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    if (m->kind == MK_CT4) {
+        if (set_device(c)) return -ENODEV;
+        return ct_io(c, m, 0, (const uint8_t *)key, nullptr, (uint8_t *)val, 0);
+    }
+    const uint8_t *v = m->hm->lookup((const uint8_t *)key);
+    if (!v) return -ENOENT;
+    memcpy(val, v, m->hm->vs);
+    if (m->is_policy) { (void)set_device(c); policy_counters(m, (const uint8_t *)key, (uint8_t *)val); }
+    return 0;
+}
+
+int cv_map_delete(cv_ctx *c, int h, const void *key)
+{
+    if (!c || !key) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    if (m->kind == MK_CT4) {
+        if (set_device(c)) return -ENODEV;
+        return ct_io(c, m, 2, (const uint8_t *)key, nullptr, nullptr, 0);
+    }
+    int r = m->hm->remove((const uint8_t *)key);
+    if (!r && m->is_policy) m->written.erase(kstr((const uint8_t *)key, 8));
+    return r;
+}
+
+int cv_map_get_next_key(cv_ctx *c, int h, const void *key, void *next)
+{
+    if (!c || !next) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    if (m->kind == MK_CT4) {
+        std::vector<uint8_t> ks, vs;
+        if (set_device(c)) return -ENODEV;
+        int n = ct_dump(c, m, ks, vs);
+        if (n < 0) return n;
+        int at = 0;
+        if (key) {
+            for (int i = 0; i < n; ++i)
+                if (!memcmp(&ks[(size_t)i * 14], key, 14)) { at = i + 1; break; }
+        }
+        if (at >= n) return -ENOENT;
+        memcpy(next, &ks[(size_t)at * 14], 14);
+        return 0;
+    }
+    return m->hm->next_key((const uint8_t *)key, (uint8_t *)next);
+}
+
+int cv_map_count(cv_ctx *c, int h, uint32_t *count)
+{
+    if (!c || !count) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    if (m->kind == MK_CT4) {
+        std::vector<uint8_t> ks, vs;
+        if (set_device(c)) return -ENODEV;
+        int n = ct_dump(c, m, ks, vs);
+        if (n < 0) return n;
+        *count = (uint32_t)n;
+        return 0;
+    }
+    *count = m->hm->count();
+    return 0;
+}
+
+int cv_map_dump(cv_ctx *c, int h, void *keys, void *vals, uint32_t max)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    const uint32_t ks = m->hm->ks, vs = m->hm->vs;
+    if (m->kind == MK_CT4) {
+        std::vector<uint8_t> kb, vb;
+        if (set_device(c)) return -ENODEV;
+        int n = ct_dump(c, m, kb, vb);
+        if (n < 0) return n;
+        uint32_t w = std::min<uint32_t>((uint32_t)n, max);
+        if (keys) memcpy(keys, kb.data(), (size_t)w * ks);
+        if (vals) memcpy(vals, vb.data(), (size_t)w * vs);
+        return (int)w;
+    }
+    uint32_t w = 0;
+    if (m->is_policy) (void)set_device(c);
+    m->hm->for_each([&](const uint8_t *k, const uint8_t *v) {
+        if (w >= max) return;
+        if (keys) memcpy((uint8_t *)keys + (size_t)w * ks, k, ks);
+        if (vals) {
+            uint8_t *dst = (uint8_t *)vals + (size_t)w * vs;
+            memcpy(dst, v, vs);
+            if (m->is_policy) policy_counters(m, k, dst);
+        }
+        w++;
+    });
+    return (int)w;
+}
+
+int cv_bind(cv_ctx *c, int role, int h)
+{
+    if (!c || role < 0 || role >= CV_NUM_ROLES) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (h >= 0) {
+        MapObj *m = get(c, h);
+        if (!m) return -EBADF;
+        const HostMap *hm = m->hm.get();
+        const bool lpm = hm->is_lpm();
+        switch (role) {
+        case CV_ROLE_CIDR4_FIX: if (lpm || hm->ks != 8) return -EINVAL; break;
+        case CV_ROLE_CIDR6_FIX: if (lpm || hm->ks != 20) return -EINVAL; break;
+        case CV_ROLE_CIDR4_DYN: if (!lpm || hm->ks != 8) return -EINVAL; break;
+        case CV_ROLE_CIDR6_DYN: if (!lpm || hm->ks != 20) return -EINVAL; break;
+        case CV_ROLE_LXC: if (lpm || hm->ks != 20 || hm->vs != 48) return -EINVAL; break;
+        case CV_ROLE_IPCACHE: if (!lpm || hm->ks != 24 || hm->vs != 8) return -EINVAL; break;
+        default: break;
+        }
+    }
+    c->role[role] = h;
+    c->role_version[role] = (uint64_t)-1;   // force recompilation
+    return 0;
+}
+
+int cv_endpoint_add(cv_ctx *c, uint16_t lxc_id, uint32_t seclabel, int policy_map, int ct4_map)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *p = policy_map >= 0 ? get(c, policy_map) : nullptr;
+    MapObj *t = ct4_map >= 0 ? get(c, ct4_map) : nullptr;
+    if ((policy_map >= 0 && !p) || (ct4_map >= 0 && !t)) return -EBADF;
+    if (p && (p->hm->ks != 8 || p->hm->vs != 24 || p->hm->is_lpm())) return -EINVAL;
+    if (t && (t->hm->ks != 14 || t->hm->vs != 56 || t->hm->is_lpm())) return -EINVAL;
+    for (auto &e : c->eps) if (e.lxc_id == lxc_id) return -EEXIST;
+    if (set_device(c)) return -ENODEV;
+    if (p && !p->is_policy) { p->is_policy = true; p->pol_version = 0; }
+    if (t && t->kind != MK_CT4) {
+        int r = compile_ct(c, t);
+        if (r) return r;
+    }
+    c->eps.push_back(Endpoint{lxc_id, seclabel, policy_map, ct4_map});
+    c->eps_dirty = true;
+    return (int)c->eps.size() - 1;
+}
+
+int cv_sync(cv_ctx *c)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return sync_locked(c);
+}
+
+int cv_xdp_prefilter(cv_ctx *c, const cv_batch *b, cv_out *o, void *stream)
+{
+    if (!c) return -EINVAL;
+    int r = check_batch(b);
+    if (r) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    return launch_xdp_prefilter(params(c), to_dev(b), to_dev(o), (hipStream_t)stream);
+}
+
+int cv_policy_ingress(cv_ctx *c, int ep, const cv_batch *b, cv_out *o, void *stream)
+{
+    if (!c) return -EINVAL;
+    int r = check_batch(b);
+    if (r) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (ep < 0 || (size_t)ep >= c->eps.size() || c->eps[ep].policy < 0) return -EINVAL;
+    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    return launch_policy_ingress(params(c), ep, to_dev(b), to_dev(o), (hipStream_t)stream);
+}
+
+int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefilter, cv_out *o, void *stream)
+{
+    if (!c) return -EINVAL;
+    int r = check_batch(b);
+    if (r) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
+    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    if (b->n > c->gn) {
+        uint64_t cap = 1024;
+        while (cap < 2ull * b->n) cap <<= 1;
+        (void)hipDeviceSynchronize();
+        if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)b->n * 4) || c->gnext.alloc((size_t)b->n * 4) ||
+            c->gsecctx.alloc((size_t)b->n * 4) || c->gmeta.alloc((size_t)b->n * 4))
+            return -ENOMEM;
+        (void)hipMemset(c->gtable.p, 0, cap * 16);
+        c->gcap = cap;
+        c->gn = b->n;
+        c->epoch = 0;
+    }
+    if (++c->epoch == 0) {                      // 2^32 batches: clear stale tags
+        (void)hipMemsetAsync(c->gtable.p, 0, c->gcap * 16, (hipStream_t)stream);
+        c->epoch = 1;
+    }
+    GroupScratch gs{c->gtable.as<unsigned long long>(), (uint32_t)(c->gcap - 1), c->epoch, c->gslot.as<uint32_t>(),
+                    c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(), c->gmeta.as<uint32_t>()};
+    return launch_netdev_ingress(params(c), to_dev(b), now, with_prefilter, to_dev(o), gs, (hipStream_t)stream);
+}
+
+int cv_metrics_read(cv_ctx *c, uint64_t *out)
+{
+    if (!c || !out) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_device(c)) return -ENODEV;
+    (void)hipDeviceSynchronize();
+    return hipMemcpy(out, c->metrics, METRICS_WORDS * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -EIO;
+}
+
+int cv_metrics_reset(cv_ctx *c)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_device(c)) return -ENODEV;
+    return hipMemset(c->metrics, 0, METRICS_WORDS * 8) == hipSuccess ? 0 : -EIO;
+}
+
+uint64_t *cv_metrics_device_ptr(cv_ctx *c) { return c ? reinterpret_cast<uint64_t *>(c->metrics) : nullptr; }
+
+int cv_metrics_attach(cv_ctx *c, uint64_t *buf)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->metrics = buf ? reinterpret_cast<unsigned long long *>(buf) : c->metrics_own.as<unsigned long long>();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,64 @@
+// cv_dp.hpp — the datapath parameter block handed to the gfx950 kernels, and the
+// launch entry points implemented in cv_kernels.hip.
+#pragma once
+#include "cv_hash.hpp"
+#include "cv_lpm.hpp"
+
+namespace cv {
+
+struct EpDev {                 // one tail-call target of cilium_policy (bpf_lxc.c:1003)
+    HashTable policy;          // PolicySpec + 32-B side values {proxy_port, pad, packets, bytes}
+    HashTable ct4;             // Ct4Spec + 64-B side values (struct ct_entry)
+    uint32_t seclabel;
+    uint32_t ct_id;            // identifies the CT map (group key component)
+};
+
+struct DpParams {              // by value as the kernel argument
+    uint32_t flags;
+    uint32_t n_eps;
+    HashTable cidr4_fix, cidr6_fix, lxc4, lxc6;
+    Lpm4 cidr4_dyn, ipc4;
+    Lpm6 cidr6_dyn, ipc6;
+    const EpDev *eps;
+    const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
+    unsigned long long *metrics;   // [256][4][2]
+};
+
+struct BatchDev {
+    const uint8_t *frames;
+    uint32_t stride, n;
+    const uint32_t *len;
+    const uint32_t *mark;
+};
+
+struct OutDev {
+    uint8_t *xdp;
+    int32_t *ret;
+    uint32_t *identity;
+    uint8_t *ct;
+    uint16_t *proxy;
+    uint8_t *nl, *nu;          // optional accounting of map lookups / entry writes
+};
+
+struct GroupScratch {          // address-pair grouping for conntrack (config 3)
+    unsigned long long *table; // 2 * cap u64: {epoch << 32 | hash, epoch << 32 | head}
+    uint32_t cap_mask;
+    uint32_t epoch;
+    uint32_t *gslot;           // per packet: group slot or ~0
+    uint32_t *next;            // per packet: previous inserter in the group or ~0
+    uint32_t *secctx;          // per packet: source label handed to the policy program
+    uint32_t *meta;            // per packet: ep index | skip_proxy << 16 | ifindex != 0 << 17
+};
+
+int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, hipStream_t s);
+int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);
+int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter,
+                          const OutDev &o, const GroupScratch &g, hipStream_t s);
+// single-element operations on a device-resident conntrack table (map API path):
+// op 0 lookup, 1 update (BPF_ANY/NOEXIST/EXIST in flags), 2 delete.
+// io = {key[4 words], value[16 words], rc}
+int launch_ct_op(const HashTable &t, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s);
+int launch_ct_scan(const HashTable &t, uint64_t nb, uint32_t *out_keys, uint32_t *out_vals, uint32_t *count,
+                   uint32_t max, hipStream_t s);
+
+}  // namespace cv

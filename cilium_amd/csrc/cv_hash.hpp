@@ -1,0 +1,254 @@
+// cv_hash.hpp — device-resident exact-match tables (the HASH / LRU_HASH maps of the
+// reference: cilium_lxc, v4_fix/v6_fix, cilium_policy_*, cilium_ct4_*, lb services).
+//
+// Layout, sized for HBM3E lines: a table is nb (power of two) buckets of BW 32-bit
+// words (64 or 128 B, one cache line).  Word 0-1 hold one tag byte per slot
+// (0 empty, 1 dead, 2 busy, 3..255 hash fingerprint); then SPB keys of KW words;
+// then SPB inline values of IVW words.  Larger values live in a side array indexed
+// by slot (bucket * SPB + slot) with a fixed byte stride.  Tag 2 marks a slot a
+// device thread is claiming (skipped by lookups, never matched).  Linear probing over
+// buckets; a lookup ends at the first bucket holding an empty slot, so one probe
+// is one line read in the common case.  The same code runs on the host (table
+// build) and on the device (lookups, conntrack inserts).
+#pragma once
+#include "cv_common.hpp"
+
+namespace cv {
+
+constexpr uint32_t TAG_EMPTY = 0, TAG_DEAD = 1, TAG_BUSY = 2;
+constexpr int MAX_PROBE = 64;
+constexpr uint64_t HASH_SEED = 0x243F6A8885A308D3ULL;
+
+struct HashTable {            // POD view, passed by value to kernels
+    uint32_t *buckets;        // nb * BW words
+    uint8_t  *vals;           // nb * SPB * vstride bytes, or null
+    uint64_t  mask;           // nb - 1
+    uint32_t  vstride;
+    uint32_t  spb;
+};
+
+template <int KW_, int IVW_, int SPB_, int BW_>
+struct HashSpec {
+    static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_;
+    static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KW;
+    static_assert(IVAL0 + SPB * IVW <= BW, "bucket overflow");
+    static_assert(SPB <= 8, "eight tag bytes");
+    static_assert(BW % 4 == 0, "bucket = whole 16-B vectors");
+};
+
+// table shapes per role
+using LxcV4Spec  = HashSpec<1, 1, 7, 16>;   // ip4 -> {lxc_id | HOST<<16 | ifindex!=0 <<17}
+using LxcV6Spec  = HashSpec<4, 1, 6, 32>;
+using Cidr4Spec  = HashSpec<1, 0, 8, 16>;   // /32 deny set (v4_fix)
+using Cidr6Spec  = HashSpec<4, 0, 7, 32>;   // /128 deny set (v6_fix)
+using PolicySpec = HashSpec<2, 0, 7, 16>;   // policy_key (8 B) -> side array policy_entry (stride 32)
+using Ct4Spec    = HashSpec<4, 0, 7, 32>;   // ipv4_ct_tuple (14 B + 2 zero) -> side array ct_entry (stride 64)
+using Lpm6Spec   = HashSpec<5, 1, 5, 32>;   // (masked v6 addr, plen) -> value
+
+CV_HD uint32_t tag_of(uint64_t h)
+{
+    uint32_t t = (uint32_t)(h >> 56);
+    return t < 3 ? t + 3 : t;
+}
+
+template <class S>
+CV_HD uint64_t key_hash(const uint32_t *key) { return hash_words<S::KW>(key, HASH_SEED); }
+
+// Match `key` in one bucket snapshot w[BW].  Returns the slot or -1; *stop is set
+// when the bucket has an empty slot (end of the probe chain).
+template <class S>
+CV_HD int match_bucket(const uint32_t *w, const uint32_t *key, uint32_t tag, bool *stop)
+{
+    uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    int hit = -1;
+    bool empty = false;
+#pragma unroll
+    for (int s = S::SPB - 1; s >= 0; --s) {
+        uint32_t t = (uint32_t)(tags >> (8 * s)) & 0xFFu;
+        empty |= (t == TAG_EMPTY);
+        bool eq = (t == tag);
+#pragma unroll
+        for (int j = 0; j < S::KW; ++j) eq &= (w[S::KEY0 + s * S::KW + j] == key[j]);
+        hit = eq ? s : hit;
+    }
+    *stop = empty;
+    return hit;
+}
+
+// ---------------------------------------------------------------- device lookup
+template <class S>
+__device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets, uint64_t b, uint32_t (&w)[S::BW])
+{
+    const uint4 *q = reinterpret_cast<const uint4 *>(buckets + b * S::BW);
+#pragma unroll
+    for (int i = 0; i < S::BW / 4; ++i) {
+        uint4 v = q[i];
+        w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+}
+
+// Returns the slot index (bucket * SPB + slot) or -1; copies the inline value.
+template <class S>
+__device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *key, uint32_t *ival)
+{
+    if (!t.buckets) return -1;
+    const uint64_t h = key_hash<S>(key);
+    const uint32_t tag = tag_of(h);
+    uint64_t b = h & t.mask;
+    for (int p = 0; p < MAX_PROBE; ++p) {
+        uint32_t w[S::BW];
+        load_bucket<S>(t.buckets, b, w);
+        bool stop;
+        int s = match_bucket<S>(w, key, tag, &stop);
+        if (s >= 0) {
+#pragma unroll
+            for (int q = 0; q < S::SPB; ++q)       // select without a runtime register index
+#pragma unroll
+                for (int j = 0; j < S::IVW; ++j)
+                    if (q == s) ival[j] = w[S::IVAL0 + q * S::IVW + j];
+            return (int64_t)(b * S::SPB + s);
+        }
+        if (stop) return -1;
+        b = (b + 1) & t.mask;
+    }
+    return -1;
+}
+
+// Conntrack insert (map_update_elem BPF_ANY on an LRU_HASH, conntrack.h:694,720,740).
+// The caller guarantees that no other thread of the launch touches `key` (packets
+// are grouped by address pair), so the only race is for free slots: claim one with
+// an agent-scope CAS of its tag byte (empty/dead -> busy), write the key, release,
+// then publish the fingerprint.  Lookups skip busy slots.  Returns the slot, or -1
+// when the probe limit is hit (-> DROP_CT_CREATE_FAILED); *created tells whether
+// the key was new.
+template <class S>
+__device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t *key, bool *created)
+{
+    const uint64_t h = key_hash<S>(key);
+    const uint32_t tag = tag_of(h);
+    uint64_t b = h & t.mask;
+    *created = false;
+    for (int p = 0; p < MAX_PROBE; ++p) {          // 1) existing entry?
+        uint32_t w[S::BW];
+        load_bucket<S>(t.buckets, b, w);
+        bool stop;
+        int s = match_bucket<S>(w, key, tag, &stop);
+        if (s >= 0) return (int64_t)(b * S::SPB + s);
+        if (stop) break;
+        b = (b + 1) & t.mask;
+    }
+    b = h & t.mask;                                 // 2) claim the first free slot
+    for (int p = 0; p < MAX_PROBE; ++p) {
+        uint32_t *bw = t.buckets + b * S::BW;
+#pragma unroll 1
+        for (int s = 0; s < S::SPB; ++s) {
+            uint32_t *tw = bw + (s >> 2);
+            const int sh = 8 * (s & 3);
+            uint32_t cur = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (((cur >> sh) & 0xFFu) < TAG_BUSY) {
+                const uint32_t nw = (cur & ~(0xFFu << sh)) | (TAG_BUSY << sh);
+                if (__hip_atomic_compare_exchange_strong(tw, &cur, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
+                    for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + s * S::KW + j] = key[j];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    uint32_t c2 = nw;
+                    for (;;) {
+                        const uint32_t n2 = (c2 & ~(0xFFu << sh)) | (tag << sh);
+                        if (__hip_atomic_compare_exchange_strong(tw, &c2, n2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT))
+                            break;
+                    }
+                    *created = true;
+                    return (int64_t)(b * S::SPB + s);
+                }
+            }
+        }
+        b = (b + 1) & t.mask;
+    }
+    return -1;
+}
+
+// Conntrack delete (map_delete_elem, conntrack.h:641-647): tag -> dead.
+template <class S>
+__device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
+{
+    const uint64_t b = (uint64_t)slot / S::SPB;
+    const int s = (int)((uint64_t)slot % S::SPB);
+    uint32_t *tw = t.buckets + b * S::BW + (s >> 2);
+    const int sh = 8 * (s & 3);
+    uint32_t c = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const uint32_t n = (c & ~(0xFFu << sh)) | (TAG_DEAD << sh);
+        if (__hip_atomic_compare_exchange_strong(tw, &c, n, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            break;
+    }
+}
+
+// ---------------------------------------------------------------- host build
+template <class S>
+inline uint32_t *host_bucket(HashTable &t, uint64_t b) { return t.buckets + b * S::BW; }
+
+// Insert or overwrite on a host copy.  Returns slot, or -1 when the chain is longer
+// than MAX_PROBE (caller grows the table).
+template <class S>
+inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *ival)
+{
+    const uint64_t h = key_hash<S>(key);
+    const uint32_t tag = tag_of(h);
+    uint64_t b = h & t.mask;
+    int64_t free_slot = -1;
+    for (int p = 0; p < MAX_PROBE; ++p) {
+        uint32_t *w = host_bucket<S>(t, b);
+        bool stop;
+        int s = match_bucket<S>(w, key, tag, &stop);
+        if (s >= 0) {
+            for (int j = 0; j < S::IVW; ++j) w[S::IVAL0 + s * S::IVW + j] = ival ? ival[j] : 0;
+            return (int64_t)(b * S::SPB + s);
+        }
+        if (free_slot < 0) {
+            uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            for (int q = 0; q < S::SPB; ++q)
+                if (((tags >> (8 * q)) & 0xFF) < TAG_BUSY) { free_slot = (int64_t)(b * S::SPB + q); break; }
+        }
+        if (stop) break;
+        b = (b + 1) & t.mask;
+    }
+    if (free_slot < 0) return -1;
+    uint64_t fb = (uint64_t)free_slot / S::SPB;
+    int q = (int)((uint64_t)free_slot % S::SPB);
+    uint32_t *w = host_bucket<S>(t, fb);
+    for (int j = 0; j < S::KW; ++j) w[S::KEY0 + q * S::KW + j] = key[j];
+    for (int j = 0; j < S::IVW; ++j) w[S::IVAL0 + q * S::IVW + j] = ival ? ival[j] : 0;
+    uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    tags = (tags & ~(0xFFULL << (8 * q))) | ((uint64_t)tag << (8 * q));
+    w[0] = (uint32_t)tags; w[1] = (uint32_t)(tags >> 32);
+    return free_slot;
+}
+
+template <class S>
+inline int64_t host_find(const HashTable &t, const uint32_t *key)
+{
+    const uint64_t h = key_hash<S>(key);
+    const uint32_t tag = tag_of(h);
+    uint64_t b = h & t.mask;
+    for (int p = 0; p < MAX_PROBE; ++p) {
+        const uint32_t *w = t.buckets + b * S::BW;
+        bool stop;
+        int s = match_bucket<S>(w, key, tag, &stop);
+        if (s >= 0) return (int64_t)(b * S::SPB + s);
+        if (stop) return -1;
+        b = (b + 1) & t.mask;
+    }
+    return -1;
+}
+
+inline uint64_t buckets_for(uint64_t n, int spb, double load = 0.6)
+{
+    uint64_t need = (uint64_t)((double)(n ? n : 1) / (spb * load)) + 1, nb = 16;
+    while (nb < need) nb <<= 1;
+    return nb;
+}
+
+}  // namespace cv

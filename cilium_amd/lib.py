@@ -1,0 +1,235 @@
+"""ctypes binding of the product library (include/cilium_hip.h).
+
+The library is the HIP path; there is no CPU fallback.  ``load()`` raises when
+``cilium_amd/_lib/libcilium_hip.so`` is missing (build it with
+``python -m cilium_amd.build``).  Batch entry points take torch CUDA (HIP) tensors
+already resident in HBM and launch on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libcilium_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "cilium_hip.h")
+
+MAP_HASH, MAP_LRU_HASH, MAP_LPM_TRIE, MAP_PERCPU_HASH = 1, 9, 11, 5
+BPF_F_NO_PREALLOC = 1
+ROLE_CIDR4_FIX, ROLE_CIDR4_DYN, ROLE_CIDR6_FIX, ROLE_CIDR6_DYN = 0, 1, 2, 3
+ROLE_LXC, ROLE_IPCACHE, ROLE_LB4_SERVICES, ROLE_LB6_SERVICES = 4, 5, 6, 7
+ROLES = {"v4_fix": 0, "v4_dyn": 1, "v6_fix": 2, "v6_dyn": 3, "lxc": 4, "ipcache": 5,
+         "lb4_services": 6, "lb6_services": 7}
+F_FROM_HOST, F_HAVE_L4_POLICY, F_DROP_ALL, F_CT_ACCOUNTING = 0x1, 0x2, 0x4, 0x8
+F_POLICY_INGRESS, F_POLICY_EGRESS, F_DEFAULT = 0x10, 0x20, 0x3B
+
+_lib = None
+
+
+class CvError(OSError):
+    pass
+
+
+class Batch(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("stride", C.c_uint32), ("len", C.c_void_p), ("mark", C.c_void_p),
+                ("n", C.c_uint32)]
+
+
+class Out(C.Structure):
+    _fields_ = [("xdp", C.c_void_p), ("ret", C.c_void_p), ("identity", C.c_void_p), ("ct", C.c_void_p),
+                ("proxy", C.c_void_p), ("nl", C.c_void_p), ("nu", C.c_void_p)]
+
+
+def header_functions():
+    """Names of the functions include/cilium_hip.h declares."""
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cv_[a-z0-9_]+)\s*\(", src)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CvError(2, f"{LIB_PATH} missing: the HIP library is the product path; "
+                         "build it with `python -m cilium_amd.build`")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, u32, u64 = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64
+    sig = {
+        "cv_open": (i32, [i32, C.POINTER(vp)]),
+        "cv_close": (None, [vp]),
+        "cv_set_flags": (i32, [vp, u32]),
+        "cv_version": (C.c_char_p, []),
+        "cv_map_create": (i32, [vp, i32, u32, u32, u32, u32, C.POINTER(i32)]),
+        "cv_map_update": (i32, [vp, i32, vp, vp, u64]),
+        "cv_map_lookup": (i32, [vp, i32, vp, vp]),
+        "cv_map_delete": (i32, [vp, i32, vp]),
+        "cv_map_get_next_key": (i32, [vp, i32, vp, vp]),
+        "cv_map_close": (i32, [vp, i32]),
+        "cv_map_update_batch": (i32, [vp, i32, vp, vp, u32, u64, C.POINTER(u32)]),
+        "cv_map_count": (i32, [vp, i32, C.POINTER(u32)]),
+        "cv_map_dump": (i32, [vp, i32, vp, vp, u32]),
+        "cv_bind": (i32, [vp, i32, i32]),
+        "cv_endpoint_add": (i32, [vp, C.c_uint16, u32, i32, i32]),
+        "cv_sync": (i32, [vp]),
+        "cv_xdp_prefilter": (i32, [vp, C.POINTER(Batch), C.POINTER(Out), vp]),
+        "cv_policy_ingress": (i32, [vp, i32, C.POINTER(Batch), C.POINTER(Out), vp]),
+        "cv_netdev_ingress": (i32, [vp, C.POINTER(Batch), u32, i32, C.POINTER(Out), vp]),
+        "cv_metrics_read": (i32, [vp, vp]),
+        "cv_metrics_reset": (i32, [vp]),
+        "cv_metrics_device_ptr": (vp, [vp]),
+        "cv_metrics_attach": (i32, [vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _lib = L
+    return L
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise CvError(-rc, f"{what}: {os.strerror(-rc)}")
+    return rc
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Map:
+    """A map handle; byte-level BPF semantics (pkg/bpf/bpf.go)."""
+
+    def __init__(self, ctx, handle, type_, ks, vs, max_entries):
+        self.ctx, self.h, self.type, self.ks, self.vs, self.max_entries = ctx, handle, type_, ks, vs, max_entries
+
+    def update(self, key, val, flags=0):
+        k, v = bytes(key), bytes(val)
+        assert len(k) == self.ks and len(v) == self.vs
+        return load().cv_map_update(self.ctx.h, self.h, k, v, flags)
+
+    def update_batch(self, keys, vals, flags=0):
+        keys = np.ascontiguousarray(keys, np.uint8)
+        vals = np.ascontiguousarray(vals, np.uint8)
+        done = C.c_uint32(0)
+        rc = load().cv_map_update_batch(self.ctx.h, self.h, keys.ctypes.data, vals.ctypes.data, len(keys), flags,
+                                        C.byref(done))
+        _check(rc, "cv_map_update_batch")
+        return done.value
+
+    def lookup(self, key):
+        v = C.create_string_buffer(self.vs)
+        rc = load().cv_map_lookup(self.ctx.h, self.h, bytes(key), v)
+        return (rc, v.raw if rc == 0 else None)
+
+    def delete(self, key):
+        return load().cv_map_delete(self.ctx.h, self.h, bytes(key))
+
+    def next_key(self, key=None):
+        out = C.create_string_buffer(self.ks)
+        rc = load().cv_map_get_next_key(self.ctx.h, self.h, None if key is None else bytes(key), out)
+        return (rc, out.raw if rc == 0 else None)
+
+    def __len__(self):
+        n = C.c_uint32(0)
+        _check(load().cv_map_count(self.ctx.h, self.h, C.byref(n)), "cv_map_count")
+        return n.value
+
+    def dump(self):
+        n = len(self)
+        keys = np.zeros((max(n, 1), self.ks), np.uint8)
+        vals = np.zeros((max(n, 1), self.vs), np.uint8)
+        k = _check(load().cv_map_dump(self.ctx.h, self.h, keys.ctypes.data, vals.ctypes.data, n), "cv_map_dump")
+        return keys[:k], vals[:k]
+
+
+class Ctx:
+    """One device context (one MI355X)."""
+
+    def __init__(self, device=0, flags=F_DEFAULT):
+        L = load()
+        h = C.c_void_p()
+        _check(L.cv_open(device, C.byref(h)), "cv_open")
+        self.h = h
+        self.device = device
+        if flags != F_DEFAULT:
+            _check(L.cv_set_flags(self.h, flags), "cv_set_flags")
+
+    def close(self):
+        if self.h:
+            load().cv_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def map_create(self, type_, ks, vs, max_entries, flags=None):
+        if flags is None:
+            flags = BPF_F_NO_PREALLOC if type_ == MAP_LPM_TRIE else 0
+        h = C.c_int(-1)
+        _check(load().cv_map_create(self.h, type_, ks, vs, max_entries, flags, C.byref(h)), "cv_map_create")
+        return Map(self, h.value, type_, ks, vs, max_entries)
+
+    def map_from_spec(self, spec):
+        m = self.map_create(spec.type, spec.key_size, spec.val_size, spec.max_entries)
+        m.update_batch(spec.keys, spec.vals)
+        return m
+
+    def bind(self, role, m):
+        role = ROLES[role] if isinstance(role, str) else role
+        _check(load().cv_bind(self.h, role, -1 if m is None else m.h), "cv_bind")
+
+    def endpoint_add(self, lxc_id, seclabel, policy, ct4=None):
+        return _check(load().cv_endpoint_add(self.h, lxc_id, seclabel, -1 if policy is None else policy.h,
+                                             -1 if ct4 is None else ct4.h), "cv_endpoint_add")
+
+    def sync(self):
+        _check(load().cv_sync(self.h), "cv_sync")
+
+    # ---- batches (torch tensors on this device) ----
+    @staticmethod
+    def _batch(frames, length, mark=None):
+        return Batch(frames.data_ptr(), frames.shape[1], length.data_ptr(),
+                     None if mark is None else mark.data_ptr(), length.shape[0])
+
+    @staticmethod
+    def _out(o):
+        o = o or {}
+        return Out(*[None if o.get(k) is None else o[k].data_ptr() for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu")])
+
+    def xdp_prefilter(self, frames, length, out):
+        b, o = self._batch(frames, length), self._out(out)
+        _check(load().cv_xdp_prefilter(self.h, C.byref(b), C.byref(o), _stream()), "cv_xdp_prefilter")
+
+    def policy_ingress(self, ep, frames, length, out, mark=None):
+        b, o = self._batch(frames, length, mark), self._out(out)
+        _check(load().cv_policy_ingress(self.h, ep, C.byref(b), C.byref(o), _stream()), "cv_policy_ingress")
+
+    def netdev_ingress(self, frames, length, out, now, mark=None, with_prefilter=True):
+        b, o = self._batch(frames, length, mark), self._out(out)
+        _check(load().cv_netdev_ingress(self.h, C.byref(b), now, 1 if with_prefilter else 0, C.byref(o), _stream()),
+               "cv_netdev_ingress")
+
+    def metrics(self):
+        m = np.zeros((256, 4, 2), np.uint64)
+        _check(load().cv_metrics_read(self.h, m.ctypes.data), "cv_metrics_read")
+        return m
+
+    def metrics_reset(self):
+        _check(load().cv_metrics_reset(self.h), "cv_metrics_reset")
+
+    def metrics_attach(self, tensor):
+        _check(load().cv_metrics_attach(self.h, None if tensor is None else C.c_void_p(tensor.data_ptr())),
+               "cv_metrics_attach")

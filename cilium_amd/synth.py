@@ -343,3 +343,126 @@ def config2(n_pkts: int = 1 << 20, seed: int = 0xC1A00002, n_cidrs: int = 102400
     return Workload("config2", {"ipcache": ipcache, "policy": policy, "lxc": lxc}, frames,
                     np.full(n_pkts, 64, np.uint32), np.zeros(n_pkts, np.uint32),
                     [{"lxc_id": 1, "seclabel": 0x1010, "ip": int(ep_ip[0]), "ifindex": 7}])
+
+
+# --------------------------------------------------------------------------
+# Config 3: full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + CT
+# --------------------------------------------------------------------------
+
+def ct4_keys(daddr, saddr, dport, sport, nexthdr, flags) -> np.ndarray:
+    """struct ipv4_ct_tuple (bpf/lib/common.h:359-367), packed 14 bytes."""
+    n = len(daddr)
+    k = np.zeros((n, 14), np.uint8)
+    k[:, 0:4] = be32_bytes(daddr)
+    k[:, 4:8] = be32_bytes(saddr)
+    k[:, 8:10] = be16_bytes(np.asarray(dport, np.uint16))
+    k[:, 10:12] = be16_bytes(np.asarray(sport, np.uint16))
+    k[:, 12] = np.asarray(nexthdr, np.uint8)
+    k[:, 13] = np.asarray(flags, np.uint8)
+    return k
+
+
+def ct_entries(n, now, ingress, tcp, src_sec_id, seen_non_syn=False, length=64) -> np.ndarray:
+    """struct ct_entry (bpf/lib/common.h:380-406), 56 bytes: an established entry
+    as an agent restore would write it (counters of one packet, lifetime now+60/21600)."""
+    v = np.zeros((n, 56), np.uint8)
+    ingress = np.asarray(ingress, bool)
+    tcp = np.asarray(tcp, bool)
+    one = np.ones(n, np.uint64)
+    ln = np.full(n, length, np.uint64)
+    rx = np.where(ingress, one, 0).astype("<u8")
+    tx = np.where(ingress, 0, one).astype("<u8")
+    v[:, 0:8] = rx.view(np.uint8).reshape(n, 8)
+    v[:, 8:16] = np.where(ingress, ln, 0).astype("<u8").view(np.uint8).reshape(n, 8)
+    v[:, 16:24] = tx.view(np.uint8).reshape(n, 8)
+    v[:, 24:32] = np.where(ingress, 0, ln).astype("<u8").view(np.uint8).reshape(n, 8)
+    life = np.where(tcp & ~np.asarray(seen_non_syn, bool), 60, np.where(tcp, 21600, 60)) + now
+    v[:, 32:36] = le32_bytes(life.astype(np.uint32))
+    bits = np.where(np.asarray(seen_non_syn, bool), 0x10, 0).astype(np.uint16)
+    v[:, 36:38] = le16_bytes(bits)
+    fl = np.where(tcp, TCP_SYN, 0).astype(np.uint8)
+    v[:, 42] = np.where(ingress, 0, fl)          # tx_flags_seen
+    v[:, 43] = np.where(ingress, fl, 0)          # rx_flags_seen
+    v[:, 44:48] = le32_bytes(np.asarray(src_sec_id, np.uint32))
+    v[:, 48:52] = le32_bytes(np.where(ingress, 0, now).astype(np.uint32))   # last_tx_report
+    v[:, 52:56] = le32_bytes(np.where(ingress, now, 0).astype(np.uint32))   # last_rx_report
+    return v
+
+
+def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A00003, now0: int = 1_000_000,
+            n_cidrs: int = 102400, n_ids: int = 10000, n_ep: int = 4096, ct_max: Optional[int] = None,
+            ttl_low: float = 0.0005) -> Workload:
+    s = Stream(seed)
+    c1 = config1(16, n_ep=n_ep)
+    c2 = config2(16, n_cidrs=n_cidrs, n_ids=n_ids)
+    maps = {k: c1.maps[k] for k in ("v4_fix", "v4_dyn", "lxc")}
+    maps["ipcache"] = c2.maps["ipcache"]
+    maps["policy"] = c2.maps["policy"]
+    lxc_ip = c1.extra["lxc_ip"][:n_ep]                   # endpoints (not the host IPs)
+    ep_ids = np.arange(1, n_ep + 1)
+    # flows: remote (inside an ipcache CIDR) <-> endpoint
+    ipk = c2.maps["ipcache"].keys[:-1]
+    cidr_addr = ipk[:, 8:12].copy().view(">u4").reshape(-1).astype(np.uint32)
+    cidr_plen = ipk[:, 0:4].copy().view("<u4").reshape(-1).astype(np.int64) - 32
+    pick = s.choice(n_flows, len(cidr_addr))
+    remote = _rand_addrs_in(s, cidr_addr[pick], cidr_plen[pick])
+    epi = s.choice(n_flows, n_ep)
+    local = lxc_ip[epi]
+    pol = c2.maps["policy"].keys
+    pol_port = pol[:, 4:6].copy().view(">u2").reshape(-1)
+    pol_proto = pol[:, 6]
+    l4 = pol_proto != 0
+    pp, pr = pol_port[l4], pol_proto[l4]
+    sel = s.choice(n_flows, len(pp))
+    fport = pp[sel].astype(np.int64)
+    fproto = pr[sel].astype(np.uint8)
+    eport = s.randint(n_flows, 1024, 65536)
+    ingress_init = s.frac(n_flows) < 0.75
+    # CT entries: ingress-initiated {daddr remote, saddr local, dport fport, sport eport, IN}
+    #             egress-initiated  {daddr local, saddr remote, dport fport(remote), sport eport(local), OUT}
+    d_addr = np.where(ingress_init, remote, local)
+    s_addr = np.where(ingress_init, local, remote)
+    keys = ct4_keys(d_addr, s_addr, fport, eport, fproto, np.where(ingress_init, 1, 0))
+    tcp = fproto == TCP
+    seclabel = (0x1000 + ep_ids[epi]).astype(np.uint32)
+    ident = c2.maps["ipcache"].vals[pick, 0:4].copy().view("<u4").reshape(-1)
+    vals = ct_entries(n_flows, now0, ingress_init, tcp, np.where(ingress_init, ident, seclabel),
+                      seen_non_syn=tcp)
+    # ICMP-related twins (conntrack.h:727-741): one per address pair, last writer wins
+    rk = ct4_keys(d_addr, s_addr, np.zeros(n_flows), np.zeros(n_flows), np.full(n_flows, ICMP),
+                  np.where(ingress_init, 3, 2))
+    rv = vals.copy()
+    rv[:, 36] |= 0x10
+    all_k = np.concatenate([keys, rk])
+    all_v = np.concatenate([vals, rv])
+    cap = ct_max or max(1 << 20, 1 << int(np.ceil(np.log2(len(all_k) * 1.25))))
+    maps["ct4"] = MapSpec("cilium_ct4_global", MAP_LRU_HASH, 14, 56, cap, all_k, all_v)
+    # packets: 60% existing forward (ingress-initiated), 20% reply (egress-initiated), 20% new
+    r = s.frac(n_pkts)
+    ing_idx = np.nonzero(ingress_init)[0]
+    egr_idx = np.nonzero(~ingress_init)[0]
+    fi = ing_idx[s.choice(n_pkts, len(ing_idx))]
+    fe = egr_idx[s.choice(n_pkts, max(len(egr_idx), 1))] if len(egr_idx) else fi
+    kind = np.where(r < 0.6, 0, np.where(r < 0.8, 1, 2))
+    f = np.where(kind == 0, fi, fe)
+    saddr = remote[f].copy()
+    daddr = local[f].copy()
+    sport = np.where(kind == 0, eport[f], fport[f])
+    dport = np.where(kind == 0, fport[f], eport[f])
+    proto = fproto[f].copy()
+    new = kind == 2
+    nn = int(new.sum())
+    npk = s.choice(nn, len(cidr_addr))
+    saddr[new] = _rand_addrs_in(s, cidr_addr[npk], cidr_plen[npk])
+    daddr[new] = lxc_ip[s.choice(nn, n_ep)]
+    sport[new] = s.randint(nn, 1024, 65536)
+    nsel = s.choice(nn, len(pp))
+    dport[new] = np.where(s.frac(nn) < 0.8, pp[nsel], s.randint(nn, 1, 65536))
+    proto[new] = pr[nsel]
+    rf = s.frac(n_pkts)
+    flags = np.where(rf < 0.90, TCP_ACK, np.where(rf < 0.95, TCP_SYN, np.where(rf < 0.98, TCP_FIN | TCP_ACK, TCP_RST)))
+    ttl = np.where(s.frac(n_pkts) < ttl_low, 1, 64)
+    frames = ipv4_frames(saddr, daddr, proto, sport, dport, flags, ttl)
+    eps = [{"lxc_id": int(i), "seclabel": int(0x1000 + i), "ip": int(lxc_ip[i - 1])} for i in ep_ids]
+    return Workload("config3", maps, frames, np.full(n_pkts, 64, np.uint32), np.zeros(n_pkts, np.uint32), eps,
+                    now=now0 + 1, extra={"kind": kind})

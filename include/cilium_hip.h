@@ -1,0 +1,155 @@
+/*
+ * cilium_hip.h — C-ABI of the MI355X batch packet-verdict engine.
+ *
+ * This is the drop-in boundary for Cilium's L3/L4 verdict path.  It replaces two
+ * boundaries of the reference (Taeung/cilium v1.1.90):
+ *
+ *  (1) the control boundary agent -> tables: the bpf(2) map syscalls wrapped by
+ *      pkg/bpf (CreateMap bpf.go:101-139, UpdateElement :146-167, LookupElement
+ *      :170-189, DeleteElement :191-216, GetNextKey :218-245, ObjClose :285-297)
+ *      that pkg/maps/{cidrmap,ipcache,policymap,ctmap,lbmap,lxcmap,metricsmap}
+ *      call.  Keys and values keep the BPF byte layouts of bpf/lib/common.h,
+ *      bpf/lib/maps.h and bpf/lib/xdp.h; return codes are the kernel's negative
+ *      errnos (-EEXIST, -ENOENT, -E2BIG, -ENOSPC, -EINVAL).
+ *
+ *  (2) the packet boundary kernel -> program: xdp_start (bpf/bpf_xdp.c:180-184),
+ *      from_netdev (bpf/bpf_netdev.c:470-524) and the per-endpoint handle_policy
+ *      tail-call target (bpf/bpf_lxc.c:1003-1038), here as batch entry points
+ *      over packed frame records in device memory.  Per-packet results use the
+ *      reference's own codes (XDP_*, TC_ACT_*, DROP_* of bpf/lib/common.h:237-269).
+ *
+ * Which map a program reads (the bpf_elf_map names compiled into the reference's
+ * programs, and the cilium_policy prog array) becomes an explicit binding:
+ * cv_bind() and cv_endpoint_add().  Writes become visible to the datapath at the
+ * next batch boundary (cv_sync(), called implicitly by every batch entry point),
+ * the way the kernel gives RCU visibility per element.
+ *
+ * Ownership: the caller owns every key/value/batch buffer; the library owns the
+ * device-resident tables.  Errors are negative errnos; nothing aborts.
+ * Pointers in cv_batch / cv_out are DEVICE pointers (HBM); `stream` is a
+ * hipStream_t (NULL = default stream).
+ */
+#ifndef CILIUM_HIP_H
+#define CILIUM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cv_ctx cv_ctx;
+
+/* ---- BPF map types and update flags (include/linux/bpf.h) ---- */
+#define CV_MAP_HASH         1
+#define CV_MAP_ARRAY        2
+#define CV_MAP_PERCPU_HASH  5
+#define CV_MAP_LRU_HASH     9
+#define CV_MAP_LPM_TRIE    11
+#define CV_ANY      0
+#define CV_NOEXIST  1
+#define CV_EXIST    2
+
+/* ---- roles: the maps the programs of the reference refer to by name ---- */
+#define CV_ROLE_CIDR4_FIX   0   /* v4_fix  HASH lpm_v4_key->lpm_val   (bpf_xdp.c:45-52)  */
+#define CV_ROLE_CIDR4_DYN   1   /* v4_dyn  LPM  lpm_v4_key->lpm_val   (bpf_xdp.c:55-62)  */
+#define CV_ROLE_CIDR6_FIX   2   /* v6_fix  HASH lpm_v6_key->lpm_val   (bpf_xdp.c:67-74)  */
+#define CV_ROLE_CIDR6_DYN   3   /* v6_dyn  LPM  lpm_v6_key->lpm_val   (bpf_xdp.c:77-84)  */
+#define CV_ROLE_LXC         4   /* cilium_lxc endpoint_key->endpoint_info (maps.h:27-33) */
+#define CV_ROLE_IPCACHE     5   /* cilium_ipcache ipcache_key->remote_endpoint_info (maps.h:151-158) */
+#define CV_ROLE_LB4_SERVICES 6  /* cilium_lb4_services (lb.h:75-81)  */
+#define CV_ROLE_LB6_SERVICES 7  /* cilium_lb6_services (lb.h:43-49)  */
+#define CV_NUM_ROLES        8
+
+/* ---- datapath options (compile-time #defines of the reference) ---- */
+#define CV_F_FROM_HOST       0x1   /* netdev_config.h FROM_HOST                     */
+#define CV_F_HAVE_L4_POLICY  0x2   /* HAVE_L4_POLICY                                */
+#define CV_F_DROP_ALL        0x4   /* DROP_ALL (pkg/endpoint/bpf.go)                */
+#define CV_F_CT_ACCOUNTING   0x8   /* CONNTRACK_ACCOUNTING (daemon/main.go:676)     */
+#define CV_F_POLICY_INGRESS  0x10  /* POLICY_INGRESS                                */
+#define CV_F_POLICY_EGRESS   0x20  /* POLICY_EGRESS                                 */
+#define CV_F_DEFAULT         0x3b
+
+/* ---- per-packet codes (bpf/include/linux/bpf.h:623-628, bpf/include/bpf/api.h:18-25) */
+#define CV_XDP_DROP 1
+#define CV_XDP_PASS 2
+#define CV_TC_ACT_OK 0
+#define CV_TC_ACT_SHOT 2
+#define CV_TC_ACT_REDIRECT 7
+#define CV_E_TRUNC (-1)      /* a header byte the path reads lies beyond the record */
+#define CV_CT_NONE 0xff
+
+/* ---- context ----
+ * cv_open(-1, ..) gives a host-only context: the map store and bindings work
+ * (agent-side control plane, CPU tests), batch entry points return -ENODEV. */
+int  cv_open(int hip_device, cv_ctx **out);
+void cv_close(cv_ctx *ctx);
+int  cv_set_flags(cv_ctx *ctx, uint32_t flags);
+const char *cv_version(void);
+
+/* ---- maps (pkg/bpf/bpf.go:101-297 semantics) ---- */
+int cv_map_create(cv_ctx *ctx, int type, uint32_t key_size, uint32_t val_size,
+                  uint32_t max_entries, uint32_t flags, int *handle);
+int cv_map_update(cv_ctx *ctx, int h, const void *key, const void *val, uint64_t flags);
+int cv_map_lookup(cv_ctx *ctx, int h, const void *key, void *val);
+int cv_map_delete(cv_ctx *ctx, int h, const void *key);
+int cv_map_get_next_key(cv_ctx *ctx, int h, const void *key, void *next_key);
+int cv_map_close(cv_ctx *ctx, int h);
+/* bulk form of cv_map_update in array order (later writes of a key win);
+ * *done = elements applied before the first error */
+int cv_map_update_batch(cv_ctx *ctx, int h, const void *keys, const void *vals, uint32_t n,
+                        uint64_t flags, uint32_t *done);
+int cv_map_count(cv_ctx *ctx, int h, uint32_t *count);
+/* every entry (keys/vals host buffers of max rows); order unspecified, like a
+ * GetNextKey walk.  Returns the number of rows written or -errno. */
+int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
+
+/* ---- binding: programs -> maps ---- */
+int cv_bind(cv_ctx *ctx, int role, int map_handle /* -1 unbinds */);
+/* tail-call target cilium_policy[lxc_id] (maps.h:44-51): endpoint policy map and
+ * CT_MAP4 (bpf_lxc.c:65-75).  Returns the endpoint index or -errno. */
+int cv_endpoint_add(cv_ctx *ctx, uint16_t lxc_id, uint32_t seclabel, int policy_map, int ct4_map);
+/* make every pending map write visible to the next batch */
+int cv_sync(cv_ctx *ctx);
+
+/* ---- batches ---- */
+typedef struct {
+    const uint8_t  *frames;   /* n records of `stride` bytes: the first bytes of each frame */
+    uint32_t        stride;   /* 64 (IPv4) or 128 (IPv6) */
+    const uint32_t *len;      /* skb->len / data_end - data per packet */
+    const uint32_t *mark;     /* skb->mark per packet, or NULL (0) */
+    uint32_t        n;
+} cv_batch;
+
+typedef struct {              /* any pointer may be NULL */
+    uint8_t  *xdp;            /* XDP_DROP / XDP_PASS */
+    int32_t  *ret;            /* tc result: DROP_* (<0), TC_ACT_OK, TC_ACT_REDIRECT, proxy port */
+    uint32_t *identity;       /* resolved source security identity */
+    uint8_t  *ct;             /* CT_NEW..CT_RELATED, or CV_CT_NONE */
+    uint16_t *proxy;          /* proxy port (network order) of an L7 redirect, else 0 */
+    uint8_t  *nl;             /* map lookups the path performed (algorithmic-bytes accounting) */
+    uint8_t  *nu;             /* map entry writes the path performed */
+} cv_out;
+
+/* config 1: bpf_xdp.c xdp_start over the batch */
+int cv_xdp_prefilter(cv_ctx *ctx, const cv_batch *b, cv_out *o, void *stream);
+/* config 2: ingress verdict of a NEW flow at endpoint `ep` (identity resolution of
+ * bpf_netdev.c:357-398 + policy_can_access_ingress, policy.h:305-329) */
+int cv_policy_ingress(cv_ctx *ctx, int ep, const cv_batch *b, cv_out *o, void *stream);
+/* config 3: [xdp_start ->] from_netdev -> handle_ipv4 -> endpoint ipv4_policy with
+ * conntrack, in packet order semantics; `now` = bpf_ktime_get_sec() of the batch */
+int cv_netdev_ingress(cv_ctx *ctx, const cv_batch *b, uint32_t now, int with_prefilter,
+                      cv_out *o, void *stream);
+
+/* ---- cilium_metrics (metrics.h:43-58): dense [256 reasons][4 dirs]{count, bytes} u64,
+ * device resident.  Read sums it to host; the device pointer lets a caller reduce it
+ * across GPUs (RCCL) without a copy; an external buffer may replace it. */
+int cv_metrics_read(cv_ctx *ctx, uint64_t *out /* 2048 u64 */);
+int cv_metrics_reset(cv_ctx *ctx);
+uint64_t *cv_metrics_device_ptr(cv_ctx *ctx);
+int cv_metrics_attach(cv_ctx *ctx, uint64_t *device_buf /* 2048 u64, or NULL = own */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

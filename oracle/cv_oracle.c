@@ -337,6 +337,7 @@ int or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *po
     if (dp->n_ep >= OR_MAX_EP) return -E2BIG;
     or_endpoint_prog *e = &dp->ep[dp->n_ep];
     e->lxc_id = lxc_id; e->seclabel = seclabel; e->policy = policy; e->ct4 = ct4;
+    dp->ep_of_lxc[lxc_id] = (uint16_t)(dp->n_ep + 1);
     return (int)dp->n_ep++;
 }
 
@@ -351,9 +352,8 @@ static void update_metrics(or_dp *dp, uint32_t bytes, uint8_t dir, uint8_t reaso
 
 static or_endpoint_prog *find_ep(or_dp *dp, uint16_t lxc_id)
 {
-    for (uint32_t i = 0; i < dp->n_ep; i++)
-        if (dp->ep[i].lxc_id == lxc_id) return &dp->ep[i];
-    return NULL;
+    uint16_t e = dp->ep_of_lxc[lxc_id];
+    return e ? &dp->ep[e - 1] : NULL;
 }
 
 /* lookup_ip4_endpoint / lookup_ip6_endpoint (bpf/lib/eps.h:26-46) */

@@ -123,7 +123,7 @@ void     or_ipv6_addr_clear_suffix(uint8_t addr[16], int prefix); /* ipv6.h:140-
 #define OR_F_POLICY_EGRESS  0x20  /* POLICY_EGRESS */
 #define OR_F_DEFAULT (OR_F_FROM_HOST | OR_F_HAVE_L4_POLICY | OR_F_CT_ACCOUNTING | OR_F_POLICY_INGRESS | OR_F_POLICY_EGRESS)
 
-#define OR_MAX_EP 64
+#define OR_MAX_EP 8192
 typedef struct {
     uint16_t lxc_id; uint32_t seclabel;
     or_map *policy;          /* cilium_policy_<id> */
@@ -139,6 +139,7 @@ typedef struct or_dp {
     uint32_t flags;
     uint32_t n_ep;
     or_endpoint_prog ep[OR_MAX_EP];   /* tail-call targets of cilium_policy (maps.h:44-51) */
+    uint16_t ep_of_lxc[65536];        /* lxc_id -> index + 1 */
     uint64_t metrics[256][4][2];      /* Σ over CPUs of cilium_metrics (metrics.h:43-58): [reason][dir]{count,bytes} */
 } or_dp;
 

@@ -1,0 +1,79 @@
+"""Builds the oracle (checker) and the product (HIP library) from one synthetic
+workload so parity tests compare them on identical bytes."""
+from __future__ import annotations
+
+import numpy as np
+
+from cilium_amd import synth
+
+ROLE_NAMES = ("v4_fix", "v4_dyn", "v6_fix", "v6_dyn", "lxc", "ipcache")
+
+
+def oracle_dp(w: synth.Workload, flags=None, with_ct=True):
+    from oracle import oracle as O
+    dp = O.ODp(O.F_DEFAULT if flags is None else flags)
+    maps = {}
+    for name, spec in w.maps.items():
+        maps[name] = O.OMap.from_spec(spec)
+        if name in ROLE_NAMES:
+            dp.bind(name, maps[name])
+    pol = maps.get("policy")
+    ct = maps.get("ct4") if with_ct else None
+    if w.endpoints:
+        for e in w.endpoints:
+            dp.add_endpoint(e["lxc_id"], e["seclabel"], pol, ct)
+    dp.keep += list(maps.values())
+    return dp, maps
+
+
+def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True):
+    from cilium_amd import lib
+    ctx = lib.Ctx(device, lib.F_DEFAULT if flags is None else flags)
+    maps = {}
+    for name, spec in w.maps.items():
+        maps[name] = ctx.map_from_spec(spec)
+        if name in ROLE_NAMES:
+            ctx.bind(name, maps[name])
+    pol = maps.get("policy")
+    ct = maps.get("ct4") if with_ct else None
+    for e in w.endpoints:
+        ctx.endpoint_add(e["lxc_id"], e["seclabel"], pol, ct)
+    ctx.sync()
+    return ctx, maps
+
+
+def to_dev(w: synth.Workload, device="cuda:0", lo=0, hi=None):
+    import torch
+    hi = w.n if hi is None else hi
+    frames = torch.from_numpy(np.ascontiguousarray(w.frames[lo:hi])).to(device)
+    length = torch.from_numpy(np.ascontiguousarray(w.length[lo:hi])).to(device)
+    mark = torch.from_numpy(np.ascontiguousarray(w.mark[lo:hi])).to(device)
+    return frames, length, mark
+
+
+def dev_out(n, device="cuda:0"):
+    import torch
+    return {
+        "xdp": torch.zeros(n, dtype=torch.uint8, device=device),
+        "ret": torch.zeros(n, dtype=torch.int32, device=device),
+        "identity": torch.zeros(n, dtype=torch.int32, device=device),
+        "ct": torch.zeros(n, dtype=torch.uint8, device=device),
+        "proxy": torch.zeros(n, dtype=torch.int16, device=device),
+        "nl": torch.zeros(n, dtype=torch.uint8, device=device),
+        "nu": torch.zeros(n, dtype=torch.uint8, device=device),
+    }
+
+
+def host_out(out):
+    import torch
+    torch.cuda.synchronize()
+    r = {k: v.cpu().numpy() for k, v in out.items()}
+    r["identity"] = r["identity"].view(np.uint32)
+    r["proxy"] = r["proxy"].view(np.uint16)
+    return r
+
+
+def sorted_rows(keys, vals):
+    rows = np.concatenate([keys, vals], axis=1)
+    order = np.lexsort(keys.T[::-1])
+    return rows[order]

@@ -1,0 +1,205 @@
+"""Parity of the HIP path (via the C-ABI) with the CPU oracle and the kernel golden
+vectors, bit-exact: verdicts, identities, CT results and CT tables, policy
+counters, cilium_metrics and the per-packet lookup/write accounting."""
+import os
+
+import numpy as np
+import pytest
+
+from cilium_amd import synth
+from tests import harness as H
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return "cuda:0"
+
+
+def run_xdp(ctx, w, dev):
+    f, l, _ = H.to_dev(w, dev)
+    out = H.dev_out(w.n, dev)
+    ctx.xdp_prefilter(f, l, out)
+    return H.host_out(out)
+
+
+def test_config1_vs_kernel_golden(dev, golden_dir):
+    g = np.load(os.path.join(golden_dir, "c1_xdp_kernel.npz"))
+    maps = {}
+    for key in g.files:
+        if key.startswith("map_") and key.endswith("_meta"):
+            name = key[4:-5]
+            t, ks, vs, mx = (int(x) for x in g[key])
+            maps[name] = synth.MapSpec(name, t, ks, vs, mx, g[f"map_{name}_keys"], g[f"map_{name}_vals"])
+    w = synth.Workload("golden1", maps, g["frames"], g["length"], np.zeros(len(g["length"]), np.uint32), [])
+    ctx, _ = H.product_ctx(w)
+    o = run_xdp(ctx, w, dev)
+    assert (o["xdp"] == g["verdict"]).all()
+
+
+def test_config1_vs_oracle(dev):
+    w = synth.config1(1 << 18)
+    dp, _ = H.oracle_dp(w)
+    ref = dp.xdp_prefilter(w.frames, w.length)
+    ctx, _ = H.product_ctx(w)
+    o = run_xdp(ctx, w, dev)
+    assert (o["xdp"] == ref.xdp).all()
+    assert (o["nl"] == ref.nl).all()
+    assert set(np.unique(o["xdp"])) == {1, 2}
+
+
+def run_policy(ctx, w, dev, ep=0):
+    f, l, m = H.to_dev(w, dev)
+    out = H.dev_out(w.n, dev)
+    ctx.policy_ingress(ep, f, l, out, mark=m)
+    return H.host_out(out)
+
+
+def check_policy_maps(pmap, omap):
+    pk, pv = pmap.dump()
+    ok, ov = omap.dump()
+    assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all()
+
+
+def test_config2_vs_kernel_golden(dev, golden_dir):
+    g = np.load(os.path.join(golden_dir, "c2_policy_kernel.npz"))
+    maps = {}
+    for name in ("ipcache", "policy", "lxc"):
+        t, ks, vs, mx = (int(x) for x in g[f"map_{name}_meta"])
+        maps[name] = synth.MapSpec(name, t, ks, vs, mx, g[f"map_{name}_keys"], g[f"map_{name}_vals"])
+    w = synth.Workload("golden2", maps, g["frames"], g["length"], g["mark"],
+                       [{"lxc_id": 1, "seclabel": 0x1010}])
+    ctx, pm = H.product_ctx(w)
+    o = run_policy(ctx, w, dev)
+    assert (o["ret"] == g["ret"]).all()
+    assert (o["identity"] == g["identity"]).all()
+    for i, k in enumerate(g["map_policy_keys"]):
+        rc, v = pm["policy"].lookup(k.tobytes())
+        assert rc == 0 and v == g["policy_vals_after"][i].tobytes(), i
+
+
+def test_config2_vs_oracle(dev):
+    w = synth.config2(1 << 18)
+    s = synth.Stream(7)
+    w.mark[:] = np.where(s.frac(w.n) < 0.03, 0xC00, np.where(s.frac(w.n) < 0.03, (300 << 16) | 0xA00, 0))
+    w.length[: 1000] = s.randint(1000, 20, 64).astype(np.uint32)
+    dp, om = H.oracle_dp(w)
+    ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+    ctx, pm = H.product_ctx(w)
+    o = run_policy(ctx, w, dev)
+    for k in ("ret", "identity", "proxy", "nl", "nu"):
+        assert (o[k] == getattr(ref, k)).all(), k
+    assert (ctx.metrics() == dp.metrics()).all()
+    check_policy_maps(pm["policy"], om["policy"])
+    # a second batch accumulates counters on the device
+    o2 = run_policy(ctx, w, dev)
+    ref2 = dp.policy_ingress(0, w.frames, w.length, w.mark)
+    assert (o2["ret"] == ref2.ret).all()
+    check_policy_maps(pm["policy"], om["policy"])
+    assert (ctx.metrics() == dp.metrics()).all()
+
+
+def test_policy_counters_across_agent_updates(dev):
+    w = synth.config2(1 << 14, n_cidrs=2048, n_ids=200)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    run_policy(ctx, w, dev)
+    dp.policy_ingress(0, w.frames, w.length, w.mark)
+    # agent rewrites some entries (counters reset, BPF_ANY) and adds/deletes others
+    keys = w.maps["policy"].keys
+    for k in keys[:50]:
+        v = bytes(24)
+        assert pm["policy"].update(k.tobytes(), v) == 0
+        assert om["policy"].update(k.tobytes(), v) == 0
+    for k in keys[50:80]:
+        assert pm["policy"].delete(k.tobytes()) == 0
+        assert om["policy"].delete(k.tobytes()) == 0
+    newk = synth.policy_keys(np.arange(9000, 9010), np.full(10, 80), np.full(10, 6))
+    for k in newk:
+        assert pm["policy"].update(k.tobytes(), bytes(24)) == 0
+        assert om["policy"].update(k.tobytes(), bytes(24)) == 0
+    check_policy_maps(pm["policy"], om["policy"])
+    o = run_policy(ctx, w, dev)
+    ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+    assert (o["ret"] == ref.ret).all()
+    check_policy_maps(pm["policy"], om["policy"])
+
+
+def run_ingress(ctx, w, dev, lo, hi, with_prefilter=True):
+    f, l, m = H.to_dev(w, dev, lo, hi)
+    out = H.dev_out(hi - lo, dev)
+    ctx.netdev_ingress(f, l, out, w.now, mark=m, with_prefilter=with_prefilter)
+    return H.host_out(out)
+
+
+def check_ingress(w, dev, batches, with_prefilter=True):
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    cuts = np.linspace(0, w.n, batches + 1).astype(int)
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        o = run_ingress(ctx, w, dev, lo, hi, with_prefilter)
+        ref = dp.netdev_ingress(w.frames[lo:hi], w.length[lo:hi], w.mark[lo:hi], now=w.now,
+                                with_prefilter=with_prefilter)
+        for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu"):
+            bad = np.nonzero(o[k] != getattr(ref, k))[0]
+            assert len(bad) == 0, (k, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+    assert (ctx.metrics() == dp.metrics()).all()
+    check_policy_maps(pm["policy"], om["policy"])
+    ck, cv = pm["ct4"].dump()
+    ok, ov = om["ct4"].dump()
+    assert len(ck) == len(ok)
+    assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
+    return dp
+
+
+def test_config3_vs_oracle(dev):
+    w = synth.config3(1 << 17, 1 << 15, n_ep=512, n_cidrs=8192, n_ids=1000)
+    check_ingress(w, dev, batches=4)
+
+
+def test_config3_hot_groups(dev):
+    # few flows -> groups far larger than the in-register limit, FIN/RST/SYN mixes
+    w = synth.config3(1 << 15, 64, n_ep=16, n_cidrs=512, n_ids=50, seed=11)
+    check_ingress(w, dev, batches=3)
+
+
+def test_config3_icmp_and_options(dev):
+    w = synth.config3(1 << 14, 1 << 10, n_ep=32, n_cidrs=512, n_ids=50, seed=12)
+    s = synth.Stream(99)
+    n = w.n
+    sel = s.frac(n) < 0.15                                  # ICMP echo / echo-reply / unreachable
+    w.frames[sel, 23] = 1
+    w.frames[sel, 34] = np.array([8, 0, 3, 11, 12, 5], np.uint8)[s.choice(int(sel.sum()), 6)]
+    opt = s.frac(n) < 0.03                                  # IP options: ihl 6..8, L4 moves
+    w.frames[opt, 14] = 0x40 | (6 + s.choice(int(opt.sum()), 3)).astype(np.uint8)
+    short = s.frac(n) < 0.02
+    w.length[short] = s.randint(int(short.sum()), 14, 60).astype(np.uint32)
+    other = s.frac(n) < 0.01
+    w.frames[other, 23] = 47
+    check_ingress(w, dev, batches=2)
+    check_ingress(w, dev, batches=1, with_prefilter=False)
+
+
+def test_ct_map_api_on_device(dev):
+    w = synth.config3(1 << 10, 256, n_ep=8, n_cidrs=256, n_ids=20, seed=5)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    ct_p, ct_o = pm["ct4"], om["ct4"]
+    keys = w.maps["ct4"].keys
+    for k in keys[:20]:
+        assert ct_p.lookup(k.tobytes()) == ct_o.lookup(k.tobytes())
+        assert ct_p.delete(k.tobytes()) == 0 == ct_o.delete(k.tobytes())
+        assert ct_p.lookup(k.tobytes())[0] == ct_o.lookup(k.tobytes())[0] < 0
+    v = bytes(range(56))
+    assert ct_p.update(keys[0].tobytes(), v, 2) == ct_o.update(keys[0].tobytes(), v, 2)    # EXIST on missing
+    assert ct_p.update(keys[0].tobytes(), v, 1) == 0 == ct_o.update(keys[0].tobytes(), v, 1)
+    assert ct_p.update(keys[0].tobytes(), v, 1) == ct_o.update(keys[0].tobytes(), v, 1)    # EEXIST
+    assert ct_p.lookup(keys[0].tobytes()) == (0, v)
+    assert len(ct_p) == len(ct_o)
+    ck, cv = ct_p.dump()
+    ok, ov = ct_o.dump()
+    assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()

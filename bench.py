@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X batch verdict engine (BASELINE.json metric).
+
+A step = one pass of the verdict path over one batch of synthetic packets already
+resident in HBM.  Default workload = BASELINE.json configs[1] (config 2): ipcache
+LPM (102,401 CIDRs -> identities) + policymap (10k identities x 8 L4 ports + L3 +
+wildcards, 81,055 entries) ingress verdicts on 2^24 64-B IPv4 headers per step, one
+MI355X per rank.  --workload config1 / config3 measure the other paths.
+
+Multi-GPU (torchrun): tables are replicated, every rank verdicts its own batch
+(weak scaling, no data-path collective); cilium_metrics is summed across ranks
+with one RCCL all_reduce after the timed region.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = "Mpps verdicts at 1/2/4/8 GPUs (64B hdrs); achieved HBM GB/s vs peak"
+
+WORKLOADS = {
+    "config2": "ipcache LPM (100k CIDRs->identities) + policymap (10k identities x L4 ports) ingress verdicts",
+    "config1": "bpf_xdp.c CIDR deny-list prefilter, 1k IPv4 prefixes + cilium_lxc",
+    "config3": "full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + ct_lookup4/ct_create4, 16M-flow CT",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def lib_sha():
+    from cilium_amd import lib
+    with open(lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def make_workload(name, n, rank):
+    from cilium_amd import synth
+    if name == "config2":
+        return synth.config2(n)
+    if name == "config1":
+        return synth.config1(n)
+    if name == "config3":
+        return synth.config3(n, n_flows=1 << 24)
+    raise SystemExit(f"unknown workload {name}")
+
+
+def algorithmic_bytes(name, nl, nu):
+    """B(p) = R + V + 64*L(p) + 64*U(p), summed over the batch."""
+    R = 64
+    V = {"config1": 4, "config2": 8, "config3": 9}[name]
+    n = len(nl)
+    return n * (R + V) + 64 * (int(nl.astype(np.int64).sum()) + int(nu.astype(np.int64).sum()))
+
+
+def cpu_baseline(name, w, min_seconds=10.0):
+    """The oracle (plain-C restatement, OpenMP over the host cores it is given) on a
+    bounded sample of the same workload; config 2 (stateless) only."""
+    from tests import harness as H
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    sample = min(w.n, 1 << 21)
+    dp, _ = H.oracle_dp(w)
+    frames, length, mark = w.frames[:sample], w.length[:sample], w.mark[:sample]
+    if name == "config1":
+        run = lambda: dp.xdp_prefilter(frames, length)
+    elif name == "config2":
+        run = lambda: dp.policy_ingress(0, frames, length, mark)
+    else:
+        sample = min(sample, 1 << 18)
+        frames, length, mark = frames[:sample], length[:sample], mark[:sample]
+        run = lambda: dp.netdev_ingress(frames, length, mark, now=w.now)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        done += sample
+        el = time.perf_counter() - t0
+        if el >= min_seconds or name == "config3":
+            break
+    return {"value": round(done / el / 1e6, 3), "unit": "Mpps", "cores": threads if name != "config3" else 1,
+            "kind": "port",
+            "sample": f"oracle/cv_oracle.c over {done} packets of the same synthetic {name} batch "
+                      f"({el:.1f} s, {'OpenMP ' + str(threads) + ' threads' if name != 'config3' else '1 thread, sequential'})"}
+
+
+def pmc_traffic(name, sha):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary of this exact
+    library build (profiles/pmc_<workload>.json), else None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None
+    if d.get("lib_sha") != sha:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--packets", type=int, default=1 << 24)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = f"cuda:{local}"
+    torch.cuda.set_device(local)
+
+    from cilium_amd import build as cvbuild
+    cvbuild.build()
+    from tests import harness as H
+
+    name = args.workload
+    t0 = time.time()
+    w = make_workload(name, args.packets, rank)
+    log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
+    ctx, maps = H.product_ctx(w, device=local)
+    metrics_t = torch.zeros(2048, dtype=torch.int64, device=device)
+    ctx.metrics_attach(metrics_t)
+    frames, length, mark = H.to_dev(w, device)
+    n = w.n
+    out = {"ret": torch.empty(n, dtype=torch.int32, device=device),
+           "identity": torch.empty(n, dtype=torch.int32, device=device)}
+    if name == "config1":
+        out = {"xdp": torch.empty(n, dtype=torch.uint8, device=device)}
+    if name == "config3":
+        out["ct"] = torch.empty(n, dtype=torch.uint8, device=device)
+
+    def step(o):
+        if name == "config1":
+            ctx.xdp_prefilter(frames, length, o)
+        elif name == "config2":
+            ctx.policy_ingress(0, frames, length, o, mark=mark)
+        else:
+            ctx.netdev_ingress(frames, length, o, w.now, mark=mark)
+
+    # accounting pass (untimed): L(p), U(p) of the same batch for the algorithmic bytes
+    acct = dict(out)
+    acct["nl"] = torch.zeros(n, dtype=torch.uint8, device=device)
+    acct["nu"] = torch.zeros(n, dtype=torch.uint8, device=device)
+    step(acct)
+    torch.cuda.synchronize()
+    alg_bytes = algorithmic_bytes(name, acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy())
+    del acct
+
+    for _ in range(args.warmup):
+        step(out)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step(out)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.all_reduce(metrics_t)           # cilium_metrics: the one RCCL reduction
+    torch.cuda.synchronize()
+
+    total_pkts = n * args.steps * world
+    value = total_pkts / elapsed / 1e6
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    sha = lib_sha()
+    traffic = pmc_traffic(name, sha)
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            log("[rank 0] cpu baseline ...")
+            cpu = cpu_baseline(name, w)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (SplitMix64, SURVEY.md §8(d) seeds), tables + headers resident in HBM",
+            "config": {
+                "workload": f"{name}: {WORKLOADS[name]}",
+                "packets_per_step_per_gpu": n,
+                "header_bytes": int(w.frames.shape[1]),
+                "parallelism": f"replicated tables, {world} GPU(s), batch per GPU",
+                "tables": {k: len(v) for k, v in w.maps.items()},
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kern_ms, 4),
+                "algorithmic_bytes_per_launch": alg_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -59,7 +59,7 @@ struct DevBuf {
 
 // A device hash table plus the host image it was built from.
 struct DevHash {
-    DevBuf buckets, vals;
+    DevBuf buckets, vals, aux;
     std::vector<uint32_t> hb;   // host image of the buckets
     HashTable view{};
     uint64_t nb = 0;
@@ -102,7 +102,8 @@ int build_hash(DevHash &d, const std::vector<std::vector<uint32_t>> &keys, const
 
 struct DevLpm4 {
     DevBuf l1, chunks;
-    Lpm4 view{nullptr, nullptr};
+    DevHash full;              // the /32 prefixes (hash front of the trie)
+    Lpm4 view{nullptr, nullptr, HashTable{}};
 };
 
 struct DevLpm6 {
@@ -154,6 +155,7 @@ struct cv_ctx {
     uint32_t epoch = 0;
     DevBuf ctio;
     uint32_t next_ct_id = 1;
+    uint32_t chunk = MAX_CHUNK;    // packets per launch (CV_MAX_CHUNK env may lower it, tests)
 };
 
 namespace {
@@ -226,13 +228,19 @@ int upload_lpm4(DevLpm4 &d, std::vector<Pfx> &px)
 {
     std::stable_sort(px.begin(), px.end(), [](const Pfx &x, const Pfx &y) { return x.prio < y.prio; });
     Lpm4Builder b;
-    for (const Pfx &p : px) b.insert(bswap32(p.a[0]), p.plen, p.value);
+    std::vector<std::vector<uint32_t>> k32, v32;
+    for (const Pfx &p : px) {
+        if (p.plen == 32) { k32.push_back({p.a[0]}); v32.push_back({p.value}); }   // /32: hash front
+        else b.insert(bswap32(p.a[0]), p.plen, p.value);
+    }
     int r = d.l1.upload(b.l1.data(), b.l1.size() * 4);
     if (!r) {
         if (b.chunks.empty()) b.chunks.assign(256, 0);
         r = d.chunks.upload(b.chunks.data(), b.chunks.size() * 4);
     }
-    d.view = r ? Lpm4{nullptr, nullptr} : Lpm4{d.l1.as<uint32_t>(), d.chunks.as<uint32_t>()};
+    if (!r && !k32.empty()) r = build_hash<Host32Spec>(d.full, k32, v32, 0, nullptr, nullptr);
+    d.view = r ? Lpm4{nullptr, nullptr, HashTable{}}
+               : Lpm4{d.l1.as<uint32_t>(), d.chunks.as<uint32_t>(), k32.empty() ? HashTable{} : d.full.view};
     return r;
 }
 
@@ -267,7 +275,7 @@ int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
 int compile_cidr_dyn(cv_ctx *c, HostMap *m, bool v6)
 {
     if (!m) {
-        if (v6) c->cidr6_dyn.view = Lpm6{}; else c->cidr4_dyn.view = Lpm4{nullptr, nullptr};
+        if (v6) c->cidr6_dyn.view = Lpm6{}; else c->cidr4_dyn.view = Lpm4{nullptr, nullptr, HashTable{}};
         return 0;
     }
     if (!m->is_lpm() || m->ks != (v6 ? 20u : 8u)) return -EINVAL;
@@ -288,7 +296,7 @@ int compile_cidr_dyn(cv_ctx *c, HostMap *m, bool v6)
 // min(prefixlen, 32) bits equal {0, 0, 0, 1}.  Same for v6 with family 2, 160.
 int compile_ipcache(cv_ctx *c, HostMap *m)
 {
-    if (!m) { c->ipc4.view = Lpm4{nullptr, nullptr}; c->ipc6.view = Lpm6{}; return 0; }
+    if (!m) { c->ipc4.view = Lpm4{nullptr, nullptr, HashTable{}}; c->ipc6.view = Lpm6{}; return 0; }
     if (!m->is_lpm() || m->ks != 24 || m->vs < 4) return -EINVAL;
     std::vector<Pfx> p4, p6;
     int err = 0;
@@ -349,8 +357,15 @@ int compile_policy(cv_ctx *c, MapObj *mo)
     });
     std::vector<int64_t> slots;
     int r = build_hash<PolicySpec>(mo->pol, keys, none, 32, &vals, &slots);
-    if (!r) mo->pol_version = m->version;
-    return r;
+    if (r) return r;
+    // counter deltas: one 64-bit word per slot, apart from the value lines so the
+    // datapath's atomics do not share lines with proxy_port reads
+    const size_t nslots = mo->pol.nb * PolicySpec::SPB;
+    if ((r = mo->pol.aux.alloc(nslots * 8))) return r;
+    if (hipMemset(mo->pol.aux.p, 0, nslots * 8) != hipSuccess) return -EIO;
+    mo->pol.view.aux = mo->pol.aux.as<unsigned long long>();
+    mo->pol_version = m->version;
+    return 0;
 }
 
 // CT table sized for max_entries (+ its ICMP-related twins), filled from the host store
@@ -467,13 +482,15 @@ DpParams params(cv_ctx *c)
     p.cidr6_fix = c->role[CV_ROLE_CIDR6_FIX] >= 0 ? c->cidr6_fix.view : HashTable{};
     p.lxc4 = c->role[CV_ROLE_LXC] >= 0 ? c->lxc4.view : HashTable{};
     p.lxc6 = c->role[CV_ROLE_LXC] >= 0 ? c->lxc6.view : HashTable{};
-    p.cidr4_dyn = c->role[CV_ROLE_CIDR4_DYN] >= 0 ? c->cidr4_dyn.view : Lpm4{nullptr, nullptr};
+    p.cidr4_dyn = c->role[CV_ROLE_CIDR4_DYN] >= 0 ? c->cidr4_dyn.view : Lpm4{nullptr, nullptr, HashTable{}};
     p.cidr6_dyn = c->role[CV_ROLE_CIDR6_DYN] >= 0 ? c->cidr6_dyn.view : Lpm6{};
-    p.ipc4 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc4.view : Lpm4{nullptr, nullptr};
+    p.ipc4 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc4.view : Lpm4{nullptr, nullptr, HashTable{}};
     p.ipc6 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc6.view : Lpm6{};
     p.eps = c->eps_dev.as<EpDev>();
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
+    const char *ab = getenv("CV_ABLATE");
+    p.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
     return p;
 }
 
@@ -487,10 +504,29 @@ int check_batch(const cv_batch *b)
 
 BatchDev to_dev(const cv_batch *b) { return BatchDev{b->frames, b->stride, b->n, b->len, b->mark}; }
 
+// packets [off, off + n) of a batch / its outputs
+BatchDev chunk(const cv_batch *b, uint32_t off, uint32_t n)
+{
+    return BatchDev{b->frames + (size_t)off * b->stride, b->stride, n, b->len + off, b->mark ? b->mark + off : nullptr};
+}
+
 OutDev to_dev(const cv_out *o)
 {
     OutDev d{};
     if (o) { d.xdp = o->xdp; d.ret = o->ret; d.identity = o->identity; d.ct = o->ct; d.proxy = o->proxy; d.nl = o->nl; d.nu = o->nu; }
+    return d;
+}
+
+OutDev chunk(const cv_out *o, uint32_t off)
+{
+    OutDev d = to_dev(o);
+    if (d.xdp) d.xdp += off;
+    if (d.ret) d.ret += off;
+    if (d.identity) d.identity += off;
+    if (d.ct) d.ct += off;
+    if (d.proxy) d.proxy += off;
+    if (d.nl) d.nl += off;
+    if (d.nu) d.nu += off;
     return d;
 }
 
@@ -577,6 +613,10 @@ int cv_open(int hip_device, cv_ctx **out)
     if (c->metrics_own.alloc(METRICS_WORDS * 8)) { delete c; return -ENOMEM; }
     (void)hipMemset(c->metrics_own.p, 0, METRICS_WORDS * 8);
     c->metrics = c->metrics_own.as<unsigned long long>();
+    if (const char *e = getenv("CV_MAX_CHUNK")) {
+        const unsigned long v = strtoul(e, nullptr, 0);
+        if (v >= 1 && v <= MAX_CHUNK) c->chunk = (uint32_t)v;
+    }
     *out = c;
     return 0;
 }
@@ -836,7 +876,14 @@ int cv_policy_ingress(cv_ctx *c, int ep, const cv_batch *b, cv_out *o, void *str
     std::lock_guard<std::mutex> g(c->mu);
     if (ep < 0 || (size_t)ep >= c->eps.size() || c->eps[ep].policy < 0) return -EINVAL;
     if ((r = set_device(c)) || (r = sync_locked(c))) return r;
-    return launch_policy_ingress(params(c), ep, to_dev(b), to_dev(o), (hipStream_t)stream);
+    const DpParams p = params(c);
+    const HashTable pol = get(c, c->eps[ep].policy)->pol.view;
+    for (uint32_t off = 0; off < b->n; off += c->chunk) {
+        const uint32_t n = std::min(c->chunk, b->n - off);
+        if ((r = launch_policy_ingress(p, ep, chunk(b, off, n), chunk(o, off), (hipStream_t)stream))) return r;
+        if ((r = launch_policy_fold(pol, (hipStream_t)stream))) return r;
+    }
+    return 0;
 }
 
 int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefilter, cv_out *o, void *stream)
@@ -847,25 +894,42 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     std::lock_guard<std::mutex> g(c->mu);
     for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
     if ((r = set_device(c)) || (r = sync_locked(c))) return r;
-    if (b->n > c->gn) {
+    const uint32_t cmax = std::min(b->n, c->chunk);
+    if (cmax > c->gn) {
         uint64_t cap = 1024;
-        while (cap < 2ull * b->n) cap <<= 1;
+        while (cap < 2ull * cmax) cap <<= 1;
         (void)hipDeviceSynchronize();
-        if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)b->n * 4) || c->gnext.alloc((size_t)b->n * 4) ||
-            c->gsecctx.alloc((size_t)b->n * 4) || c->gmeta.alloc((size_t)b->n * 4))
+        if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
+            c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4))
             return -ENOMEM;
         (void)hipMemset(c->gtable.p, 0, cap * 16);
         c->gcap = cap;
-        c->gn = b->n;
+        c->gn = cmax;
         c->epoch = 0;
     }
-    if (++c->epoch == 0) {                      // 2^32 batches: clear stale tags
-        (void)hipMemsetAsync(c->gtable.p, 0, c->gcap * 16, (hipStream_t)stream);
-        c->epoch = 1;
+    std::set<const void *> seen;
+    std::vector<HashTable> pols;
+    for (auto &e : c->eps) {
+        const HashTable &t = get(c, e.policy)->pol.view;
+        if (seen.insert(t.vals).second) pols.push_back(t);
     }
-    GroupScratch gs{c->gtable.as<unsigned long long>(), (uint32_t)(c->gcap - 1), c->epoch, c->gslot.as<uint32_t>(),
-                    c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(), c->gmeta.as<uint32_t>()};
-    return launch_netdev_ingress(params(c), to_dev(b), now, with_prefilter, to_dev(o), gs, (hipStream_t)stream);
+    const DpParams p = params(c);
+    for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
+        const uint32_t n = std::min(c->chunk, b->n - off);
+        if (++c->epoch == 0) {                  // 2^32 launches: clear stale group tags
+            (void)hipMemsetAsync(c->gtable.p, 0, c->gcap * 16, (hipStream_t)stream);
+            c->epoch = 1;
+        }
+        GroupScratch gs{c->gtable.as<unsigned long long>(), (uint32_t)(c->gcap - 1), c->epoch,
+                        c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(),
+                        c->gmeta.as<uint32_t>()};
+        if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off), gs,
+                                       (hipStream_t)stream)))
+            return r;
+        for (const HashTable &t : pols)
+            if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
+    }
+    return 0;
 }
 
 int cv_metrics_read(cv_ctx *c, uint64_t *out)

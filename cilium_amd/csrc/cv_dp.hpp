@@ -6,6 +6,12 @@
 
 namespace cv {
 
+// policy side values: 32-B slots {proxy_port u16, pad, packets u64 @8, bytes u64 @16}
+// (struct policy_entry); the datapath adds {count:24 | bytes:40} deltas with one atomic
+// per hit into HashTable::aux[slot] and k_policy_fold folds them into packets/bytes
+// after every launch chunk of at most MAX_CHUNK packets (no field can overflow).
+constexpr uint32_t MAX_CHUNK = 1u << 23;
+
 struct EpDev {                 // one tail-call target of cilium_policy (bpf_lxc.c:1003)
     HashTable policy;          // PolicySpec + 32-B side values {proxy_port, pad, packets, bytes}
     HashTable ct4;             // Ct4Spec + 64-B side values (struct ct_entry)
@@ -22,7 +28,12 @@ struct DpParams {              // by value as the kernel argument
     const EpDev *eps;
     const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
     unsigned long long *metrics;   // [256][4][2]
+    uint32_t ablate;           // timing-only ablations (CV_ABLATE env); 0 in every real run
 };
+
+// ablation bits: each removes one part of the work to price it (results are wrong)
+constexpr uint32_t AB_NO_POLICY_ATOMICS = 1, AB_NO_IPCACHE = 2, AB_NO_POLICY = 4, AB_NO_METRICS = 8,
+                   AB_NO_RECORD = 16;
 
 struct BatchDev {
     const uint8_t *frames;
@@ -50,6 +61,7 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *meta;            // per packet: ep index | skip_proxy << 16 | ifindex != 0 << 17
 };
 
+int launch_policy_fold(const HashTable &pol, hipStream_t s);
 int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter,

@@ -25,6 +25,7 @@ struct HashTable {            // POD view, passed by value to kernels
     uint64_t  mask;           // nb - 1
     uint32_t  vstride;
     uint32_t  spb;
+    unsigned long long *aux;  // per-slot 64-bit side words (policy counter deltas), or null
 };
 
 template <int KW_, int IVW_, int SPB_, int BW_>

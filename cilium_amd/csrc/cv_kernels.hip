@@ -157,9 +157,23 @@ __device__ __forceinline__ uint32_t identity_from_mark(uint32_t mark, bool &skip
     return WORLD_ID;
 }
 
-// __policy_can_access (policy.h:217-285); cb[CB_POLICY] is 0 on these paths
+// A policy counter update held back by the lane: the atomic is issued after the
+// lane's last dependent lookup, so in-order vmcnt never makes a lookup wait for it.
+struct Hit {
+    unsigned long long *p;
+    unsigned long long inc;
+};
+
+__device__ __forceinline__ void hit_flush(const Hit &h)
+{
+    if (h.p) atomicAdd(h.p, h.inc);
+}
+
+// __policy_can_access (policy.h:217-285); cb[CB_POLICY] is 0 on these paths.  With
+// `defer` the counter update is returned instead of issued.
 __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
-                                             uint32_t dport_raw, uint32_t proto, int dir, Acct &a)
+                                             uint32_t dport_raw, uint32_t proto, int dir, Acct &a,
+                                             Hit *defer = nullptr)
 {
     if (flags & F_DROP_ALL) return DROP_POLICY;
     const uint32_t eg = dir ? 0u : 1u;
@@ -186,18 +200,30 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
     if (s < 0) return DROP_POLICY;
     a.nu++;
     uint8_t *v = pol.vals + (size_t)s * pol.vstride;
-    atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);          // __sync_fetch_and_add
-    atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
+    if (!(flags & (AB_NO_POLICY_ATOMICS << 16))) {
+        // __sync_fetch_and_add(packets, 1) and (bytes, len) as ONE 64-bit atomic on the
+        // slot's delta word {count:24 | bytes:40} (launches are chunked to <= 2^23
+        // packets and folded after each chunk, so neither field can overflow)
+        if (len < (1u << 17)) {
+            unsigned long long *d = pol.aux + s;
+            const unsigned long long inc = (1ull << 40) | len;
+            if (defer) *defer = Hit{d, inc};
+            else atomicAdd(d, inc);
+        } else {
+            atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
+        }
+    }
     return l4 ? (int)*reinterpret_cast<const uint16_t *>(v) : TC_ACT_OK;
 }
 
 // policy_can_access_ingress (policy.h:305-329)
 __device__ __forceinline__ int policy_ingress(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t src,
-                                              uint32_t dport_raw, uint32_t proto, Acct &a)
+                                              uint32_t dport_raw, uint32_t proto, Acct &a, Hit *defer = nullptr)
 {
     if (!(flags & F_POLICY_INGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
     if (flags & F_DROP_ALL) return DROP_POLICY;
-    int r = policy_access(pol, flags, len, src, dport_raw, proto, CT_INGRESS, a);
+    int r = policy_access(pol, flags, len, src, dport_raw, proto, CT_INGRESS, a, defer);
     return r >= TC_ACT_OK ? r : DROP_POLICY;
 }
 
@@ -289,12 +315,22 @@ __device__ __forceinline__ int l4_key_new_flow(const Rec &r, uint32_t &dport_raw
     }
 }
 
+// PPT packets per lane: lane t of workgroup w takes packets w*PPT*BLOCK + k*BLOCK + t
+// (coalesced per k); its policy counter atomics wait in registers until its last
+// lookup is done.
+constexpr int PPT = 4;
+
 __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
 {
     __shared__ LdsMetrics lm;
     lm_init(lm);
     const HashTable pol = p.eps[ep].policy;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+    Hit hits[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        hits[k] = Hit{nullptr, 0};
+        const uint32_t i = blockIdx.x * (PPT * BLOCK) + k * BLOCK + threadIdx.x;
+        if (i >= b.n) continue;
         Rec r;
         rec_load(r, b, i, 3);
         Acct a{0, 0};
@@ -309,26 +345,31 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
         } else if (r.len < 34) {
             ret = DROP_INVALID;
         } else {
-            if (identity < HEALTH_ID) {                          // bpf_netdev.c:375-398
+            if (identity < HEALTH_ID && !(p.ablate & AB_NO_IPCACHE)) {   // bpf_netdev.c:375-398
                 const uint32_t lab = ipcache4(p, rec_raw32c<26>(r), a);
                 if (lab && lab != CLUSTER_ID && lab != HOST_ID) identity = lab;
             }
             uint32_t dport, proto;
             ret = l4_key_new_flow(r, dport, proto);
             if (ret == 0) {
-                const int v = policy_ingress(pol, p.flags, r.len, identity, dport, proto, a);
+                const int v = (p.ablate & AB_NO_POLICY)
+                                  ? (int)(identity & 1)
+                                  : policy_ingress(pol, p.flags | (p.ablate << 16), r.len, identity, dport, proto, a,
+                                                   &hits[k]);
                 if (v < 0) ret = DROP_POLICY;
                 else if (skip_proxy && v > 0) ret = 0;
                 else { ret = v; proxy = v > 0 ? (uint16_t)v : 0; }
             }
         }
-        if (ret < 0 && ret != E_TRUNC) lm_add(lm, ret, r.len);
+        if (ret < 0 && ret != E_TRUNC && !(p.ablate & AB_NO_METRICS)) lm_add(lm, ret, r.len);
         if (o.ret) o.ret[i] = ret;
         if (o.identity) o.identity[i] = identity;
         if (o.proxy) o.proxy[i] = proxy;
         if (o.ct) o.ct[i] = CT_NONE;
         store_out(o, i, a);
     }
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) hit_flush(hits[k]);
     lm_flush(lm, p.metrics, METRIC_INGRESS);
 }
 
@@ -798,10 +839,34 @@ int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, 
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// fold the per-chunk delta words into policy_entry.packets / .bytes
+__global__ void __launch_bounds__(BLOCK) k_policy_fold(HashTable t, uint64_t nslots)
+{
+    for (uint64_t x = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; x < nslots; x += (uint64_t)gridDim.x * BLOCK) {
+        const unsigned long long d = t.aux[x];
+        if (!d) continue;
+        unsigned long long *v = reinterpret_cast<unsigned long long *>(t.vals + x * t.vstride);
+        v[1] += d >> 40;
+        v[2] += d & ((1ull << 40) - 1);
+        t.aux[x] = 0;
+    }
+}
+
+int launch_policy_fold(const HashTable &pol, hipStream_t s)
+{
+    if (!pol.buckets || !pol.vals || !pol.aux) return 0;
+    const uint64_t slots = (pol.mask + 1) * pol.spb;
+    uint64_t g = (slots + BLOCK - 1) / BLOCK;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_policy_fold, dim3((uint32_t)g), dim3(BLOCK), 0, s, pol, slots);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s)
 {
     if (!b.n) return 0;
-    hipLaunchKernelGGL(k_policy_ingress, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, ep, b, o);
+    const uint32_t grid = (b.n + PPT * BLOCK - 1) / (PPT * BLOCK);
+    hipLaunchKernelGGL(k_policy_ingress, dim3(grid), dim3(BLOCK), 0, s, p, ep, b, o);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -23,10 +23,19 @@ namespace cv {
 struct Lpm4 {                  // POD device view
     const uint32_t *l1;        // 65536 slots
     const uint32_t *chunks;    // nchunks * 256 slots
+    HashTable full;            // optional /32 front (Host32Spec): a /32 is always the longest
+                               // match, so a hit ends the lookup in one L2-resident line
 };
+
+using Host32Spec = HashSpec<1, 1, 7, 16>;   // raw ip4 -> value
 
 __device__ __forceinline__ uint32_t lpm4_lookup(const Lpm4 &t, uint32_t addr /* host order */)
 {
+    if (t.full.buckets) {
+        const uint32_t k = bswap32(addr);
+        uint32_t v;
+        if (dev_find<Host32Spec>(t.full, &k, &v) >= 0) return v;
+    }
     uint32_t e = t.l1[addr >> 16];
     if (e & 0x80000000u) {
         e = t.chunks[((e & 0x7FFFFFFFu) << 8) | ((addr >> 8) & 0xFFu)];

@@ -203,3 +203,22 @@ def test_ct_map_api_on_device(dev):
     ck, cv = ct_p.dump()
     ok, ov = ct_o.dump()
     assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
+
+
+def test_chunked_launches_config2(dev, monkeypatch):
+    # batches larger than one launch chunk: per-chunk delta fold keeps counters exact
+    monkeypatch.setenv("CV_MAX_CHUNK", "10007")
+    w = synth.config2(1 << 16, n_cidrs=4096, n_ids=300)
+    dp, om = H.oracle_dp(w)
+    ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+    ctx, pm = H.product_ctx(w)
+    o = run_policy(ctx, w, dev)
+    for k in ("ret", "identity", "proxy", "nl", "nu"):
+        assert (o[k] == getattr(ref, k)).all(), k
+    check_policy_maps(pm["policy"], om["policy"])
+
+
+def test_chunked_launches_config3(dev, monkeypatch):
+    monkeypatch.setenv("CV_MAX_CHUNK", "7001")
+    w = synth.config3(1 << 15, 1 << 9, n_ep=64, n_cidrs=1024, n_ids=100, seed=21)
+    check_ingress(w, dev, batches=2)

@@ -7,10 +7,10 @@
 namespace cv {
 
 // policy side values: 32-B slots {proxy_port u16, pad, packets u64 @8, bytes u64 @16}
-// (struct policy_entry); the datapath adds {count:24 | bytes:40} deltas with one atomic
+// (struct policy_entry); the datapath adds {count:25 | bytes:39} deltas with one atomic
 // per hit into HashTable::aux[slot] and k_policy_fold folds them into packets/bytes
 // after every launch chunk of at most MAX_CHUNK packets (no field can overflow).
-constexpr uint32_t MAX_CHUNK = 1u << 23;
+constexpr uint32_t MAX_CHUNK = 1u << 24;
 
 struct EpDev {                 // one tail-call target of cilium_policy (bpf_lxc.c:1003)
     HashTable policy;          // PolicySpec + 32-B side values {proxy_port, pad, packets, bytes}

@@ -202,11 +202,11 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
     uint8_t *v = pol.vals + (size_t)s * pol.vstride;
     if (!(flags & (AB_NO_POLICY_ATOMICS << 16))) {
         // __sync_fetch_and_add(packets, 1) and (bytes, len) as ONE 64-bit atomic on the
-        // slot's delta word {count:24 | bytes:40} (launches are chunked to <= 2^23
+        // slot's delta word {count:25 | bytes:39} (launches are chunked to <= 2^24
         // packets and folded after each chunk, so neither field can overflow)
-        if (len < (1u << 17)) {
+        if (len < (1u << 15)) {
             unsigned long long *d = pol.aux + s;
-            const unsigned long long inc = (1ull << 40) | len;
+            const unsigned long long inc = (1ull << 39) | len;
             if (defer) *defer = Hit{d, inc};
             else atomicAdd(d, inc);
         } else {
@@ -846,8 +846,8 @@ __global__ void __launch_bounds__(BLOCK) k_policy_fold(HashTable t, uint64_t nsl
         const unsigned long long d = t.aux[x];
         if (!d) continue;
         unsigned long long *v = reinterpret_cast<unsigned long long *>(t.vals + x * t.vstride);
-        v[1] += d >> 40;
-        v[2] += d & ((1ull << 40) - 1);
+        v[1] += d >> 39;
+        v[2] += d & ((1ull << 39) - 1);
         t.aux[x] = 0;
     }
 }

@@ -87,6 +87,9 @@ def test_config2_vs_oracle(dev):
     s = synth.Stream(7)
     w.mark[:] = np.where(s.frac(w.n) < 0.03, 0xC00, np.where(s.frac(w.n) < 0.03, (300 << 16) | 0xA00, 0))
     w.length[: 1000] = s.randint(1000, 20, 64).astype(np.uint32)
+    # GSO-sized lengths either side of the packed-delta limit (2^15) take the two-atomic path
+    w.length[1000: 3000] = s.randint(2000, (1 << 15) - 4, (1 << 17) + 4).astype(np.uint32)
+    w.length[3000: 3004] = [(1 << 15) - 1, 1 << 15, 65535, 0xFFFFFFFF]
     dp, om = H.oracle_dp(w)
     ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
     ctx, pm = H.product_ctx(w)

@@ -76,7 +76,7 @@ int build_hash(DevHash &d, const std::vector<std::vector<uint32_t>> &keys, const
         bool ok = true;
         if (slots) slots->assign(keys.size(), -1);
         for (size_t i = 0; i < keys.size() && ok; ++i) {
-            int64_t s = host_upsert<S>(t, keys[i].data(), S::IVW ? ivals[i].data() : nullptr);
+            int64_t s = host_upsert<S>(t, keys[i].data(), (S::IVW || S::IVH) ? ivals[i].data() : nullptr);
             if (s < 0) ok = false;
             else if (slots) (*slots)[i] = s;
         }
@@ -328,7 +328,8 @@ int compile_ipcache(cv_ctx *c, HostMap *m)
     return r;
 }
 
-// policy map -> PolicySpec table + 32-B side values; device counters of entries the
+// policy map -> PolicySpec table (proxy_port inline, so a lookup is one line) + 32-B
+// side values {proxy_port, pad, packets, bytes}; device counters of entries the
 // agent did not rewrite since the last sync are carried over.
 int compile_policy(cv_ctx *c, MapObj *mo)
 {
@@ -347,16 +348,17 @@ int compile_policy(cv_ctx *c, MapObj *mo)
         });
     }
     mo->written.clear();
-    std::vector<std::vector<uint32_t>> keys, none;
+    std::vector<std::vector<uint32_t>> keys, proxy;
     std::vector<uint8_t> vals;
     m->for_each([&](const uint8_t *k, const uint8_t *v) {
         keys.push_back({rd32(k), rd32(k + 4)});
+        proxy.push_back({(uint32_t)v[0] | (uint32_t)v[1] << 8});   // raw be16 bytes, as stored
         size_t o = vals.size();
         vals.resize(o + 32, 0);
         memcpy(&vals[o], v, 24);
     });
     std::vector<int64_t> slots;
-    int r = build_hash<PolicySpec>(mo->pol, keys, none, 32, &vals, &slots);
+    int r = build_hash<PolicySpec>(mo->pol, keys, proxy, 32, &vals, &slots);
     if (r) return r;
     // counter deltas: one 64-bit word per slot, apart from the value lines so the
     // datapath's atomics do not share lines with proxy_port reads

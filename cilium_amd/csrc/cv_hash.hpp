@@ -4,7 +4,8 @@
 // Layout, sized for HBM3E lines: a table is nb (power of two) buckets of BW 32-bit
 // words (64 or 128 B, one cache line).  Word 0-1 hold one tag byte per slot
 // (0 empty, 1 dead, 2 busy, 3..255 hash fingerprint); then SPB keys of KW words;
-// then SPB inline values of IVW words.  Larger values live in a side array indexed
+// then SPB inline values of IVW words, or of one 16-bit halfword each (IVH = 1, the
+// policy table's proxy_port).  Larger values live in a side array indexed
 // by slot (bucket * SPB + slot) with a fixed byte stride.  Tag 2 marks a slot a
 // device thread is claiming (skipped by lookups, never matched).  Linear probing over
 // buckets; a lookup ends at the first bucket holding an empty slot, so one probe
@@ -28,11 +29,12 @@ struct HashTable {            // POD view, passed by value to kernels
     unsigned long long *aux;  // per-slot 64-bit side words (policy counter deltas), or null
 };
 
-template <int KW_, int IVW_, int SPB_, int BW_>
+template <int KW_, int IVW_, int SPB_, int BW_, int IVH_ = 0>
 struct HashSpec {
-    static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_;
-    static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KW;
+    static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_, IVH = IVH_;
+    static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KW, HVAL0 = 2 * IVAL0;   // HVAL0 in halfwords
     static_assert(IVAL0 + SPB * IVW <= BW, "bucket overflow");
+    static_assert(IVH == 0 || (IVW == 0 && IVH == 1 && HVAL0 + SPB <= 2 * BW), "halfword values");
     static_assert(SPB <= 8, "eight tag bytes");
     static_assert(BW % 4 == 0, "bucket = whole 16-B vectors");
 };
@@ -42,7 +44,7 @@ using LxcV4Spec  = HashSpec<1, 1, 7, 16>;   // ip4 -> {lxc_id | HOST<<16 | ifind
 using LxcV6Spec  = HashSpec<4, 1, 6, 32>;
 using Cidr4Spec  = HashSpec<1, 0, 8, 16>;   // /32 deny set (v4_fix)
 using Cidr6Spec  = HashSpec<4, 0, 7, 32>;   // /128 deny set (v6_fix)
-using PolicySpec = HashSpec<2, 0, 7, 16>;   // policy_key (8 B) -> side array policy_entry (stride 32)
+using PolicySpec = HashSpec<2, 0, 5, 16, 1>; // policy_key (8 B) -> inline proxy_port; side array policy_entry (stride 32)
 using Ct4Spec    = HashSpec<4, 0, 7, 32>;   // ipv4_ct_tuple (14 B + 2 zero) -> side array ct_entry (stride 64)
 using Lpm6Spec   = HashSpec<5, 1, 5, 32>;   // (masked v6 addr, plen) -> value
 
@@ -51,6 +53,9 @@ CV_HD uint32_t tag_of(uint64_t h)
     uint32_t t = (uint32_t)(h >> 56);
     return t < 3 ? t + 3 : t;
 }
+
+template <class S>
+CV_HD uint32_t half_at(const uint32_t *w, int h) { return (w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu; }
 
 template <class S>
 CV_HD uint64_t key_hash(const uint32_t *key) { return hash_words<S::KW>(key, HASH_SEED); }
@@ -103,10 +108,12 @@ __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *
         int s = match_bucket<S>(w, key, tag, &stop);
         if (s >= 0) {
 #pragma unroll
-            for (int q = 0; q < S::SPB; ++q)       // select without a runtime register index
+            for (int q = 0; q < S::SPB; ++q) {     // select without a runtime register index
 #pragma unroll
                 for (int j = 0; j < S::IVW; ++j)
                     if (q == s) ival[j] = w[S::IVAL0 + q * S::IVW + j];
+                if (S::IVH && q == s) ival[0] = half_at<S>(w, S::HVAL0 + q);
+            }
             return (int64_t)(b * S::SPB + s);
         }
         if (stop) return -1;
@@ -191,6 +198,16 @@ __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
 template <class S>
 inline uint32_t *host_bucket(HashTable &t, uint64_t b) { return t.buckets + b * S::BW; }
 
+template <class S>
+inline void host_set_ival(uint32_t *w, int s, const uint32_t *ival)
+{
+    for (int j = 0; j < S::IVW; ++j) w[S::IVAL0 + s * S::IVW + j] = ival ? ival[j] : 0;
+    if (S::IVH) {
+        const int h = S::HVAL0 + s, sh = 16 * (h & 1);
+        w[h >> 1] = (w[h >> 1] & ~(0xFFFFu << sh)) | ((ival ? ival[0] & 0xFFFFu : 0u) << sh);
+    }
+}
+
 // Insert or overwrite on a host copy.  Returns slot, or -1 when the chain is longer
 // than MAX_PROBE (caller grows the table).
 template <class S>
@@ -205,7 +222,7 @@ inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *iv
         bool stop;
         int s = match_bucket<S>(w, key, tag, &stop);
         if (s >= 0) {
-            for (int j = 0; j < S::IVW; ++j) w[S::IVAL0 + s * S::IVW + j] = ival ? ival[j] : 0;
+            host_set_ival<S>(w, s, ival);
             return (int64_t)(b * S::SPB + s);
         }
         if (free_slot < 0) {
@@ -221,7 +238,7 @@ inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *iv
     int q = (int)((uint64_t)free_slot % S::SPB);
     uint32_t *w = host_bucket<S>(t, fb);
     for (int j = 0; j < S::KW; ++j) w[S::KEY0 + q * S::KW + j] = key[j];
-    for (int j = 0; j < S::IVW; ++j) w[S::IVAL0 + q * S::IVW + j] = ival ? ival[j] : 0;
+    host_set_ival<S>(w, q, ival);
     uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
     tags = (tags & ~(0xFFULL << (8 * q))) | ((uint64_t)tag << (8 * q));
     w[0] = (uint32_t)tags; w[1] = (uint32_t)(tags >> 32);

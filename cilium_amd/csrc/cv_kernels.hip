@@ -179,22 +179,23 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
     const uint32_t eg = dir ? 0u : 1u;
     uint32_t k[2];
     int64_t s = -1;
+    uint32_t px[1] = {0};
     bool l4 = false;
     if (flags & F_HAVE_L4_POLICY) {
         k[0] = identity; k[1] = (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24);
         a.nl++;
-        s = dev_find<PolicySpec>(pol, k, nullptr);
+        s = dev_find<PolicySpec>(pol, k, px);
         l4 = s >= 0;
     }
     if (s < 0) {
         k[0] = identity; k[1] = eg << 24;
         a.nl++;
-        s = dev_find<PolicySpec>(pol, k, nullptr);
+        s = dev_find<PolicySpec>(pol, k, px);
     }
     if (s < 0 && (flags & F_HAVE_L4_POLICY)) {
         k[0] = 0; k[1] = (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24);
         a.nl++;
-        s = dev_find<PolicySpec>(pol, k, nullptr);
+        s = dev_find<PolicySpec>(pol, k, px);
         l4 = s >= 0;
     }
     if (s < 0) return DROP_POLICY;
@@ -214,7 +215,7 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
             atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
         }
     }
-    return l4 ? (int)*reinterpret_cast<const uint16_t *>(v) : TC_ACT_OK;
+    return l4 ? (int)px[0] : TC_ACT_OK;
 }
 
 // policy_can_access_ingress (policy.h:305-329)

@@ -466,3 +466,356 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     eps = [{"lxc_id": int(i), "seclabel": int(0x1000 + i), "ip": int(lxc_ip[i - 1])} for i in ep_ids]
     return Workload("config3", maps, frames, np.full(n_pkts, 64, np.uint32), np.zeros(n_pkts, np.uint32), eps,
                     now=now0 + 1, extra={"kind": kind})
+
+
+# --------------------------------------------------------------------------
+# Config 5: from-container egress, dual stack, lb4/lb6 services (50k) + policy
+# --------------------------------------------------------------------------
+
+NODE_MAC = np.array([0xDE, 0xAD, 0xBE, 0xEF, 0xC0, 0xDE], np.uint8)     # bpf/node_config.h:51
+IPV4_LOOPBACK = 0x0AF5FF1F            # 10.245.255.31 (node_config.h:45 raw 0x1ffff50a)
+CLUSTER_V4 = (0x0A000000, 0xFF000000)  # IPV4_CLUSTER_RANGE / _MASK: 10.0.0.0/8
+V6_POD_PREFIX = bytes([0xFD, 0, 0, 0, 0, 0, 0, 0])          # ROUTER_IP's /64 (ipv6_match_prefix_64)
+ROUTER_IP6 = V6_POD_PREFIX + bytes([0, 0, 0, 0, 0, 0, 0, 1])
+ICMPV6 = 58
+
+
+def v6_addrs(prefix8: bytes, hi: np.ndarray, lo: np.ndarray) -> np.ndarray:
+    """(n, 16) addresses: 8-byte prefix + be32 hi + be32 lo."""
+    n = len(lo)
+    a = np.zeros((n, 16), np.uint8)
+    a[:, 0:8] = np.frombuffer(prefix8, np.uint8)
+    a[:, 8:12] = be32_bytes(np.asarray(hi, np.uint32))
+    a[:, 12:16] = be32_bytes(np.asarray(lo, np.uint32))
+    return a
+
+
+def endpoint_keys_v6(ip6: np.ndarray) -> np.ndarray:
+    k = np.zeros((len(ip6), 20), np.uint8)
+    k[:, 0:16] = ip6
+    k[:, 16] = 2
+    return k
+
+
+def ipcache_keys_v6(addr6: np.ndarray, plen: np.ndarray) -> np.ndarray:
+    k = np.zeros((len(addr6), 24), np.uint8)
+    k[:, 0:4] = le32_bytes(np.asarray(plen, np.uint32) + 32)
+    k[:, 7] = 2
+    k[:, 8:24] = addr6
+    return k
+
+
+def lb4_keys(addr, dport, slave) -> np.ndarray:
+    """struct lb4_key (common.h:427-431): be32 address, be16 dport, u16 slave."""
+    n = len(addr)
+    k = np.zeros((n, 8), np.uint8)
+    k[:, 0:4] = be32_bytes(np.asarray(addr, np.uint32))
+    k[:, 4:6] = be16_bytes(np.asarray(dport, np.uint16))
+    k[:, 6:8] = le16_bytes(np.asarray(slave, np.uint16))
+    return k
+
+
+def lb4_services(target, port, count, rev_nat, weight) -> np.ndarray:
+    """struct lb4_service (common.h:433-439) as pkg/maps/lbmap writes it: port, rev_nat
+    and weight in network order (Service4Value.ToNetwork), count host order."""
+    n = len(target)
+    v = np.zeros((n, 12), np.uint8)
+    v[:, 0:4] = be32_bytes(np.asarray(target, np.uint32))
+    v[:, 4:6] = be16_bytes(np.asarray(port, np.uint16))
+    v[:, 6:8] = le16_bytes(np.asarray(count, np.uint16))
+    v[:, 8:10] = be16_bytes(np.asarray(rev_nat, np.uint16))
+    v[:, 10:12] = be16_bytes(np.asarray(weight, np.uint16))
+    return v
+
+
+def lb6_keys(addr6, dport, slave) -> np.ndarray:
+    n = len(addr6)
+    k = np.zeros((n, 20), np.uint8)
+    k[:, 0:16] = addr6
+    k[:, 16:18] = be16_bytes(np.asarray(dport, np.uint16))
+    k[:, 18:20] = le16_bytes(np.asarray(slave, np.uint16))
+    return k
+
+
+def lb6_services(target6, port, count, rev_nat, weight) -> np.ndarray:
+    n = len(target6)
+    v = np.zeros((n, 24), np.uint8)
+    v[:, 0:16] = target6
+    v[:, 16:18] = be16_bytes(np.asarray(port, np.uint16))
+    v[:, 18:20] = le16_bytes(np.asarray(count, np.uint16))
+    v[:, 20:22] = be16_bytes(np.asarray(rev_nat, np.uint16))
+    v[:, 22:24] = be16_bytes(np.asarray(weight, np.uint16))
+    return v
+
+
+def revnat4(index, addr, port):
+    """cilium_lb4_reverse_nat: be16 index -> {be32 address, be16 port} (lbmap RevNat4*.ToNetwork)."""
+    k = be16_bytes(np.asarray(index, np.uint16)).copy()
+    v = np.zeros((len(addr), 6), np.uint8)
+    v[:, 0:4] = be32_bytes(np.asarray(addr, np.uint32))
+    v[:, 4:6] = be16_bytes(np.asarray(port, np.uint16))
+    return k, v
+
+
+def revnat6(index, addr6, port):
+    k = be16_bytes(np.asarray(index, np.uint16)).copy()
+    v = np.zeros((len(addr6), 18), np.uint8)
+    v[:, 0:16] = addr6
+    v[:, 16:18] = be16_bytes(np.asarray(port, np.uint16))
+    return k, v
+
+
+def ipv6_frames(saddr6, daddr6, proto, sport, dport, tcp_flags, hoplimit, smac, dmac,
+                icmp_type=None, hbh=None, stride: int = 128) -> np.ndarray:
+    """Ethernet + IPv6 (+ optional 8-B hop-by-hop header) + L4 records."""
+    n = len(saddr6)
+    f = np.zeros((n, stride), np.uint8)
+    f[:, 0:6] = dmac
+    f[:, 6:12] = smac
+    f[:, 12:14] = be16_bytes(np.full(n, ETH_P_IPV6, np.uint16))
+    f[:, 14] = 0x60
+    f[:, 18:20] = be16_bytes(np.full(n, 40, np.uint16))
+    proto = np.asarray(proto, np.uint8)
+    hbh = np.zeros(n, bool) if hbh is None else np.asarray(hbh, bool)
+    f[:, 20] = np.where(hbh, 0, proto)
+    f[:, 21] = np.asarray(hoplimit, np.uint8)
+    f[:, 22:38] = saddr6
+    f[:, 38:54] = daddr6
+    f[hbh, 54] = proto[hbh]                          # hop-by-hop: nexthdr, hdrlen 0 (8 bytes)
+    l4 = np.where(hbh, 62, 54)
+    rows = np.arange(n)
+    sp = be16_bytes(np.asarray(sport, np.uint16))
+    dp = be16_bytes(np.asarray(dport, np.uint16))
+    ports = (proto == TCP) | (proto == UDP)
+    for j in range(2):
+        f[rows[ports], l4[ports] + j] = sp[ports, j]
+        f[rows[ports], l4[ports] + 2 + j] = dp[ports, j]
+    tcp = proto == TCP
+    f[rows[tcp], l4[tcp] + 12] = 0x50
+    f[rows[tcp], l4[tcp] + 13] = np.asarray(tcp_flags, np.uint8)[tcp]
+    if icmp_type is not None:
+        ic = proto == ICMPV6
+        f[rows[ic], l4[ic]] = np.asarray(icmp_type, np.uint8)[ic]
+    return f
+
+
+def flow_hash32(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """A per-flow stand-in for the kernel's skb hash (get_hash_recalc): the same
+    5-tuple always hashes the same (the kernel's key is boot-random, so the hash is
+    an input of the verdict, not an output to match)."""
+    with np.errstate(over="ignore"):
+        z = (a.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ (b.astype(np.uint64) << np.uint64(17)) \
+            ^ c.astype(np.uint64)
+        z = (z ^ (z >> np.uint64(31))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = z ^ (z >> np.uint64(29))
+    return (z >> np.uint64(16)).astype(np.uint32)
+
+
+def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n_ep: int = 4096,
+            n_remote: int = 16384, v6_frac: float = 0.5, vip_frac: float = 0.70, reply_frac: float = 0.20,
+            n_flows: Optional[int] = None, ct_max: Optional[int] = None, stride: Optional[int] = None,
+            family: Optional[int] = None, odd_frac: float = 1.0) -> Workload:
+    """Egress from local pods through lb4/lb6 services, dual stack.
+
+    Tables: 4096 local endpoints (v4 10.0.x.y + v6 fd00::a:x, each its own MAC),
+    16k remote pods (ipcache only), 50k services (half v4, half v6; half L4, half
+    L3) with 1-16 backends drawn from local + remote pods, rev-NAT entries, one
+    policy map with ingress and egress L4/L3 rules, empty v4/v6 conntrack.
+    Packets: `vip_frac` to service VIPs, the rest pod-to-pod / to the world,
+    `reply_frac` of the pod-to-pod / service flows sent back by their responder;
+    TCP/UDP/ICMP(v6) mix, with rare invalid MACs / source IPs / TTL 1 / ARP /
+    unknown protocols / hop-by-hop headers.  `family` 4 or 6 restricts the batch.
+    """
+    s = Stream(seed)
+    stride = stride or (64 if family == 4 else 128)
+    n_flows = n_flows or max(n_pkts // 4, 1)
+    ep_idx = np.arange(n_ep)
+    ep_ip4 = np.uint32(0x0A000000) | (ep_idx + 256).astype(np.uint32)                 # 10.0.1.0 ...
+    ep_ip6 = v6_addrs(V6_POD_PREFIX, np.full(n_ep, 0x000A0000), (ep_idx + 0x100).astype(np.uint32) * 0x10001)
+    ep_mac = np.zeros((n_ep, 6), np.uint8)
+    ep_mac[:, 0] = 0x02
+    ep_mac[:, 4:6] = be16_bytes((ep_idx + 1).astype(np.uint16))
+    seclabel = (0x2000 + ep_idx).astype(np.uint32)
+    remote4 = (np.uint32(0x0A100000) | np.arange(n_remote, dtype=np.uint32))          # 10.16.0.0/16-ish
+    remote6 = v6_addrs(V6_POD_PREFIX, np.full(n_remote, 0x00100000), np.arange(n_remote, dtype=np.uint32) + 1)
+    remote_id = (0x3000 + s.choice(n_remote, 4000)).astype(np.uint32)
+
+    # cilium_lxc: local endpoints v4 + v6, plus 2 host addresses
+    host4 = np.array([0x0A0000FE, 0x0A0000FD], np.uint32)
+    lk = np.concatenate([endpoint_keys_v4(ep_ip4), endpoint_keys_v6(ep_ip6), endpoint_keys_v4(host4)])
+    lv = np.concatenate([endpoint_infos(100 + ep_idx, ep_idx + 1, np.zeros(n_ep)),
+                         endpoint_infos(100 + ep_idx, ep_idx + 1, np.zeros(n_ep)),
+                         endpoint_infos([0, 0], [0, 0], [1, 1])])
+    lv[:2 * n_ep, 16:22] = np.concatenate([ep_mac, ep_mac])
+    maps = {"lxc": MapSpec("cilium_lxc", MAP_HASH, 20, 48, 65536, lk, lv)}
+
+    # ipcache: every pod /32 (/128), a few CIDRs, world
+    cid4 = s.u32(512) & prefix_mask(np.full(512, 16))
+    ik = np.concatenate([ipcache_keys_v4(ep_ip4, np.full(n_ep, 32)), ipcache_keys_v4(remote4, np.full(n_remote, 32)),
+                         ipcache_keys_v4(cid4, np.full(512, 16)), ipcache_keys_v4(np.zeros(1, np.uint32), np.zeros(1)),
+                         ipcache_keys_v6(ep_ip6, np.full(n_ep, 128)), ipcache_keys_v6(remote6, np.full(n_remote, 128))])
+    ids4 = np.concatenate([seclabel, remote_id, (0x4000 + s.choice(512, 64)).astype(np.uint32),
+                           np.full(1, WORLD_ID, np.uint32), seclabel, remote_id])
+    maps["ipcache"] = MapSpec("cilium_ipcache", MAP_LPM_TRIE, 24, 8, 512000, ik, remote_endpoint_infos(ids4))
+
+    # services: half v4, half v6; half L4 (port), half L3 (port 0); 1..16 backends
+    n4 = n_svc // 2
+    n6 = n_svc - n4
+    rev = np.arange(1, n_svc + 1, dtype=np.uint32)
+    fam_pods4 = np.concatenate([ep_ip4, remote4])
+    fam_pods6 = np.concatenate([ep_ip6, remote6])
+    svc_l4 = s.frac(n_svc) < 0.5
+    svc_port = np.where(svc_l4, np.array([80, 443, 8080, 53, 9090], np.int64)[s.choice(n_svc, 5)], 0)
+    nbe = s.randint(n_svc, 1, 17)
+    be_port = np.where(s.frac(n_svc) < 0.5, svc_port, s.randint(n_svc, 1024, 32768))
+    vip4 = (np.uint32(0xAC140000) | np.arange(n4, dtype=np.uint32))                   # 172.20.0.0/16
+    vip6 = v6_addrs(bytes([0xFD, 0, 0, 0, 0, 0, 0xFF, 0xFF]), np.zeros(n6), np.arange(n6, dtype=np.uint32))
+    tot_be = int(nbe.sum())
+    be_pick = s.choice(tot_be, n_ep + n_remote)
+    svc_of_be = np.repeat(np.arange(n_svc), nbe)
+    slave_of_be = np.arange(tot_be) - np.repeat(np.cumsum(nbe) - nbe, nbe) + 1
+    be4 = svc_of_be < n4
+    k4 = np.concatenate([lb4_keys(vip4, svc_port[:n4], np.zeros(n4)),
+                         lb4_keys(vip4[svc_of_be[be4]], svc_port[svc_of_be[be4]], slave_of_be[be4])])
+    v4 = np.concatenate([lb4_services(np.zeros(n4), np.zeros(n4), nbe[:n4], np.zeros(n4), np.zeros(n4)),
+                         lb4_services(fam_pods4[be_pick[be4]], be_port[svc_of_be[be4]], np.zeros(int(be4.sum())),
+                                      rev[svc_of_be[be4]], np.zeros(int(be4.sum())))])
+    i6 = svc_of_be[~be4] - n4
+    k6 = np.concatenate([lb6_keys(vip6, svc_port[n4:], np.zeros(n6)),
+                         lb6_keys(vip6[i6], svc_port[svc_of_be[~be4]], slave_of_be[~be4])])
+    v6 = np.concatenate([lb6_services(np.zeros((n6, 16), np.uint8), np.zeros(n6), nbe[n4:], np.zeros(n6), np.zeros(n6)),
+                         lb6_services(fam_pods6[be_pick[~be4]], be_port[svc_of_be[~be4]], np.zeros(int((~be4).sum())),
+                                      rev[svc_of_be[~be4]], np.zeros(int((~be4).sum())))])
+    cap_lb = 1 << int(np.ceil(np.log2(max(len(k4), len(k6)) * 1.25)))
+    maps["lb4_services"] = MapSpec("cilium_lb4_services", MAP_HASH, 8, 12, cap_lb, k4, v4)
+    maps["lb6_services"] = MapSpec("cilium_lb6_services", MAP_HASH, 20, 24, cap_lb, k6, v6)
+    rk4, rv4 = revnat4(rev[:n4], vip4, svc_port[:n4])
+    rk6, rv6 = revnat6(rev[n4:], vip6, svc_port[n4:])
+    maps["lb4_revnat"] = MapSpec("cilium_lb4_reverse_nat", MAP_HASH, 2, 6, 65536, rk4, rv4)
+    maps["lb6_revnat"] = MapSpec("cilium_lb6_reverse_nat", MAP_HASH, 2, 18, 65536, rk6, rv6)
+
+    # policy (one map for every endpoint): pod identities x {80,443,8080,53,9090,
+    # backend ports} egress + ingress, L3 allow for 20% of identities, wildcards
+    all_ids = np.unique(np.concatenate([seclabel, remote_id]))
+    ports = np.array([80, 443, 8080, 53, 9090], np.int64)
+    pk = []
+    for eg in (0, 1):
+        rid = np.repeat(all_ids, len(ports) * 2)
+        rp = np.tile(np.repeat(ports, 2), len(all_ids))
+        rpr = np.tile([TCP, UDP], len(all_ids) * len(ports))
+        keep = s.frac(len(rid)) < 0.7
+        pk.append(policy_keys(rid[keep], rp[keep], rpr[keep], eg))
+        l3 = np.concatenate([all_ids[s.frac(len(all_ids)) < 0.4], [WORLD_ID] if eg else []]).astype(np.uint32)
+        pk.append(policy_keys(l3, np.zeros(len(l3)), np.zeros(len(l3)), eg))
+        wp = s.randint(32, 1024, 32768)
+        pk.append(policy_keys(np.zeros(32), wp, np.full(32, TCP), eg))
+    pk = np.unique(np.concatenate(pk), axis=0)
+    proxy = np.where(s.frac(len(pk)) < 0.02, s.randint(len(pk), 10000, 20000), 0)
+    maps["policy"] = MapSpec("cilium_policy", MAP_HASH, 8, 24, 1 << int(np.ceil(np.log2(len(pk) * 1.25))),
+                             pk, policy_entries(proxy))
+    cap = ct_max or max(1 << 16, 1 << int(np.ceil(np.log2(n_flows * 8))))
+    maps["ct4"] = MapSpec("cilium_ct4_global", MAP_LRU_HASH, 14, 56, cap, np.zeros((0, 14), np.uint8),
+                          np.zeros((0, 56), np.uint8))
+    maps["ct6"] = MapSpec("cilium_ct6_global", MAP_LRU_HASH, 40, 56, cap, np.zeros((0, 40), np.uint8),
+                          np.zeros((0, 56), np.uint8))
+
+    # ---- flows: (family, client ep, destination kind, dst, ports, proto)
+    F = n_flows
+    fam6 = (s.frac(F) < v6_frac) if family is None else np.full(F, family == 6)
+    cli = s.choice(F, n_ep)
+    r = s.frac(F)
+    kind = np.where(r < vip_frac, 0, np.where(r < vip_frac + 0.15, 1, np.where(r < vip_frac + 0.25, 2, 3)))
+    # 0 service, 1 local pod, 2 remote pod, 3 world
+    svc = np.where(fam6, n4 + s.choice(F, n6), s.choice(F, n4))
+    rp = s.frac(F)
+    proto = np.where(rp < 0.80, TCP, np.where(rp < 0.95, UDP, ICMP)).astype(np.uint8)
+    proto = np.where(fam6 & (proto == ICMP), ICMPV6, proto).astype(np.uint8)
+    sport = s.randint(F, 1024, 65536)
+    dport = np.where(kind == 0, np.where(svc_port[svc] > 0, svc_port[svc], ports[s.choice(F, 5)]),
+                     ports[s.choice(F, 5)])
+    dst_ep = s.choice(F, n_ep)
+    dst_rm = s.choice(F, n_remote)
+    world4 = (np.uint32(0x08000000) | s.u32(F) >> np.uint32(8))
+    d4 = np.where(kind == 0, vip4[np.minimum(svc, n4 - 1)],
+                  np.where(kind == 1, ep_ip4[dst_ep], np.where(kind == 2, remote4[dst_rm], world4)))
+    d6 = np.where((kind == 0)[:, None], vip6[np.clip(svc - n4, 0, n6 - 1)],
+                  np.where((kind == 1)[:, None], ep_ip6[dst_ep],
+                           np.where((kind == 2)[:, None], remote6[dst_rm],
+                                    v6_addrs(bytes([0x20, 0x01, 0x0D, 0xB8, 0, 0, 0, 0]), s.u32(F), s.u32(F)))))
+    fh = flow_hash32(cli.astype(np.uint64) * 65536 + sport, np.where(fam6, svc, d4.astype(np.int64)), dport)
+    # the responder of a flow: the destination pod, or the service backend the
+    # flow's hash selects (lb_select_slave: hash % count + 1)
+    slave = (fh % nbe[svc].astype(np.uint32)).astype(np.int64) + 1
+    be_base = np.cumsum(nbe) - nbe
+    be_row = be_base[svc] + slave - 1
+    resp4 = np.where(kind == 0, fam_pods4[be_pick[be_row]], d4)
+    resp6 = np.where((kind == 0)[:, None], fam_pods6[be_pick[be_row]], d6)
+    resp_port = np.where((kind == 0) & (be_port[svc] > 0), be_port[svc], dport)
+    # responder endpoint index if local (replies are only generated from local pods)
+    loc4 = {int(a): i for i, a in enumerate(ep_ip4)}
+    resp_ep = np.array([loc4.get(int(a), -1) for a in resp4], np.int64)
+    if kind.size:
+        is_loc6 = (resp6[:, 8:12].view(">u4").reshape(-1) == 0x000A0000) & (resp6[:, :8] == np.frombuffer(V6_POD_PREFIX, np.uint8)).all(1)
+        lo6 = resp6[:, 12:16].view(">u4").reshape(-1).astype(np.int64) // 0x10001 - 0x100
+        resp_ep6 = np.where(is_loc6 & (lo6 >= 0) & (lo6 < n_ep), lo6, -1)
+        resp_ep = np.where(fam6, resp_ep6, resp_ep)
+
+    # ---- packets
+    fi = s.choice(n_pkts, F)
+    rep = (s.frac(n_pkts) < reply_frac) & (resp_ep[fi] >= 0) & (kind[fi] <= 1)
+    f6 = fam6[fi]
+    src_ep = np.where(rep, resp_ep[fi], cli[fi]).astype(np.uint16)
+    rf = s.frac(n_pkts)
+    tflags = np.where(rf < 0.90, TCP_ACK, np.where(rf < 0.95, TCP_SYN, np.where(rf < 0.98, TCP_FIN | TCP_ACK, TCP_RST)))
+    pr = proto[fi]
+    p_sport = np.where(rep, resp_port[fi], sport[fi])
+    p_dport = np.where(rep, sport[fi], dport[fi])
+    icmp_t = np.where(rep, np.where(f6, 129, 0), np.where(f6, 128, 8))
+    ttl = np.full(n_pkts, 64)
+    smac = ep_mac[src_ep]
+    dmac = np.broadcast_to(NODE_MAC, (n_pkts, 6)).copy()
+    # rare odd cases
+    odd = s.frac(n_pkts)
+    o = odd_frac
+    smac[odd < 0.001 * o] = 0x33
+    dmac[(odd >= 0.001 * o) & (odd < 0.002 * o)] = 0x44
+    ttl[(odd >= 0.002 * o) & (odd < 0.0025 * o)] = 1
+    pr = np.where((odd >= 0.0025 * o) & (odd < 0.0035 * o), 47, pr).astype(np.uint8)     # GRE: unknown L4
+    bad_sip = (odd >= 0.0035 * o) & (odd < 0.0045 * o)
+    hbh = f6 & (odd >= 0.0045 * o) & (odd < 0.0145 * o)
+    arp = (odd >= 0.0145 * o) & (odd < 0.0155 * o)
+    ns6 = f6 & (odd >= 0.0155 * o) & (odd < 0.0160 * o)
+    frames = np.zeros((n_pkts, stride), np.uint8)
+    i4 = np.nonzero(~f6)[0]
+    if len(i4):
+        sa = np.where(rep[i4], resp4[fi[i4]], ep_ip4[src_ep[i4]]).astype(np.uint32)
+        da = np.where(rep[i4], ep_ip4[cli[fi[i4]]], d4[fi[i4]]).astype(np.uint32)
+        sa = np.where(bad_sip[i4], sa ^ np.uint32(0x00000F00), sa).astype(np.uint32)
+        fr = ipv4_frames(sa, da, pr[i4], p_sport[i4], p_dport[i4], tflags[i4], ttl[i4],
+                         np.where(arp[i4], ETH_P_ARP, ETH_P_IP), stride=stride, icmp_type=icmp_t[i4])
+        fr[:, 0:6] = dmac[i4]
+        fr[:, 6:12] = smac[i4]
+        frames[i4] = fr
+    i6 = np.nonzero(f6)[0]
+    if len(i6):
+        if stride < 128:
+            raise ValueError("IPv6 records need stride 128")
+        sa6 = np.where(rep[i6][:, None], resp6[fi[i6]], ep_ip6[src_ep[i6]])
+        da6 = np.where(rep[i6][:, None], ep_ip6[cli[fi[i6]]], d6[fi[i6]])
+        sa6 = sa6.copy()
+        sa6[bad_sip[i6], 15] ^= 0x5A
+        pr6 = pr[i6].copy()
+        it6 = icmp_t[i6].copy()
+        pr6[ns6[i6]] = ICMPV6
+        it6[ns6[i6]] = 135
+        frames[i6] = ipv6_frames(sa6, da6, pr6, p_sport[i6], p_dport[i6], tflags[i6], ttl[i6], smac[i6], dmac[i6],
+                                 icmp_type=it6, hbh=hbh[i6], stride=stride)
+    fhash = np.where(rep, flow_hash32(fh[fi].astype(np.uint64), np.full(n_pkts, 7), p_dport), fh[fi]).astype(np.uint32)
+    length = np.where(f6, 90, 64).astype(np.uint32)
+    eps = [{"lxc_id": int(i + 1), "seclabel": int(seclabel[i]), "ip": int(ep_ip4[i]), "ip6": bytes(ep_ip6[i]),
+            "mac": bytes(ep_mac[i]), "node_mac": bytes(NODE_MAC), "ifindex": int(100 + i)} for i in range(n_ep)]
+    return Workload("config5", maps, frames, length, np.zeros(n_pkts, np.uint32), eps, now=2_000_000,
+                    extra={"src_ep": src_ep, "flow_hash": fhash,
+                           "node": {"cluster_mask": CLUSTER_V4[1], "cluster_range": CLUSTER_V4[0],
+                                    "loopback": IPV4_LOOPBACK, "router_ip6": ROUTER_IP6},
+                           "kind": kind[fi], "reply": rep, "v6": f6})

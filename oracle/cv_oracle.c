@@ -332,6 +332,25 @@ or_dp *or_dp_create(uint32_t flags)
 
 void or_dp_free(or_dp *dp) { free(dp); }
 
+int or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_t *ipv6, const uint8_t *mac,
+                          const uint8_t *node_mac, or_map *ct6)
+{
+    if (ep >= dp->n_ep) return -EINVAL;
+    or_endpoint_prog *e = &dp->ep[ep];
+    e->ipv4 = ipv4;
+    if (ipv6) memcpy(e->ipv6, ipv6, 16);
+    if (mac) memcpy(e->mac, mac, 6);
+    if (node_mac) memcpy(e->node_mac, node_mac, 6);
+    e->ct6 = ct6;
+    return 0;
+}
+
+void or_dp_node_config(or_dp *dp, uint32_t mask, uint32_t range, uint32_t loopback, const uint8_t *router_ip6)
+{
+    dp->v4_cluster_mask = mask; dp->v4_cluster_range = range; dp->v4_loopback = loopback;
+    if (router_ip6) memcpy(dp->router_ip6, router_ip6, 16);
+}
+
 int or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *policy, or_map *ct4)
 {
     if (dp->n_ep >= OR_MAX_EP) return -E2BIG;
@@ -452,6 +471,7 @@ void or_xdp_prefilter(or_dp *dp, const uint8_t *frames, uint32_t stride, const u
         if (out->xdp) out->xdp[i] = v;
         if (out->nl) out->nl[i] = nl;
         if (out->nu) out->nu[i] = 0;
+        if (out->reason) out->reason[i] = 0;
     }
 }
 
@@ -558,7 +578,7 @@ static inline int ct_alive(const or_ct_entry *e)   /* conntrack.h:194-197 */
 }
 
 /* __ct_lookup (conntrack.h:199-263) */
-static int ct_lookup_one(or_map *map, const or_ipv4_ct_tuple *t, int action, int dir, or_ct_state *st,
+static int ct_lookup_one(or_map *map, const void *t, int action, int dir, or_ct_state *st,
                          int tcp, uint8_t seen, uint32_t skb_len, uint32_t now, uint32_t flags,
                          uint8_t *nl, uint8_t *nu)
 {
@@ -696,6 +716,34 @@ int or_ct_create4(or_map *ct, or_ipv4_ct_tuple *t, uint32_t skb_len, int dir, co
 }
 
 /* ===================================================================== */
+/* The skb: a writable copy of the frame record.  Loads and stores follow  */
+/* skb_load_bytes / skb_store_bytes bounds (skb->len); bytes inside len    */
+/* but beyond the record give OR_E_TRUNC.                                 */
+/* ===================================================================== */
+
+#define OR_SKB_MAX 256
+typedef struct { uint8_t b[OR_SKB_MAX]; uint32_t avail, len; } or_skb;
+
+static void skb_init(or_skb *s, const uint8_t *f, uint32_t stride, uint32_t len)
+{
+    uint32_t rec = stride < OR_SKB_MAX ? stride : OR_SKB_MAX;
+    s->len = len;
+    s->avail = len < rec ? len : rec;
+    memcpy(s->b, f, s->avail);
+}
+
+static inline int sld(const or_skb *s, int off, uint32_t n, void *to) { return ld(s->b, s->avail, s->len, off, n, to); }
+
+/* skb_store_bytes: 0, 1 (beyond len: the helper fails) or OR_E_TRUNC */
+static inline int sst(or_skb *s, int off, uint32_t n, const void *from)
+{
+    if (off < 0 || (uint64_t)off + n > s->len) return 1;
+    if ((uint64_t)off + n > s->avail) return OR_E_TRUNC;
+    memcpy(s->b + off, from, n);
+    return 0;
+}
+
+/* ===================================================================== */
 /* Ingress: from_netdev -> handle_ipv4 -> ipv4_policy                     */
 /* ===================================================================== */
 
@@ -705,30 +753,78 @@ typedef struct {
     uint8_t ct; uint16_t proxy; uint8_t nl, nu;
 } pkt_state;
 
-/* ipv4_policy (bpf/bpf_lxc.c:865-979) for endpoint `ep`, LXC_NAT46 off.  ifindex is
- * skb->cb[CB_IFINDEX] set by ipv4_local_delivery (l3.h:264). */
-static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, const uint8_t *f, uint32_t avail, uint32_t len,
-                       uint32_t ifindex, uint32_t src_label, int skip_proxy, uint32_t now, pkt_state *ps)
+#define TCP_DPORT_OFF 2
+#define TCP_SPORT_OFF 0
+
+/* lb4_rev_nat / __lb4_rev_nat (lb.h:426-517): rewrites of the reverse translation;
+ * checksums are not modelled (no verdict depends on them). */
+static int lb4_rev_nat(or_dp *dp, or_skb *skb, int l4_off, const or_ct_state *st, or_ipv4_ct_tuple *t,
+                       int tuple_saddr, uint8_t *nl)
 {
-    if (len < ETH_HLEN + 20) return OR_DROP_INVALID;   /* revalidate_data */
+    if (!dp->lb4_revnat) return 0;
+    (*nl)++;
+    or_lb4_reverse_nat *nat = or_map_lookup_ptr(dp->lb4_revnat, &st->rev_nat_index);
+    if (!nat) return 0;
+    int r;
+    if (nat->port) {                                  /* reverse_map_l4_port (lb.h:222-252) */
+        switch (t->nexthdr) {
+        case 6: case 17: {
+            uint16_t old;
+            if ((r = sld(skb, l4_off + TCP_SPORT_OFF, 2, &old))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
+            if (nat->port != old) {
+                if ((r = sst(skb, l4_off + TCP_SPORT_OFF, 2, &nat->port))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+            }
+            break;
+        }
+        case 1: case 58: break;
+        default: return OR_DROP_UNKNOWN_L4;
+        }
+    }
+    uint32_t old_sip, new_sip = nat->address;
+    if (tuple_saddr) { old_sip = t->saddr; t->saddr = new_sip; }
+    else if ((r = sld(skb, ETH_HLEN + 12, 4, &old_sip))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
+    if (st->loopback) {
+        uint32_t old_dip;
+        if ((r = sld(skb, ETH_HLEN + 16, 4, &old_dip))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
+        if ((r = sst(skb, ETH_HLEN + 16, 4, &old_sip))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+        t->saddr = old_sip;
+    }
+    if ((r = sst(skb, ETH_HLEN + 12, 4, &new_sip))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    return 0;
+}
+
+/* ipv4_policy (bpf/bpf_lxc.c:865-979) for endpoint `ep`, LXC_NAT46 off; its caller
+ * tail_ipv4_policy (:981-993).  ifindex is skb->cb[CB_IFINDEX] set by
+ * ipv4_local_delivery (l3.h:103-132).  Returns the program's final verdict
+ * (TC_ACT_*; drops accounted as METRIC_INGRESS) or OR_E_TRUNC. */
+static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t ifindex, uint32_t src_label,
+                       int skip_proxy, uint32_t now, pkt_state *ps, int32_t *reason)
+{
+    int ret;
+    uint32_t len = skb->len;
+    if (len < ETH_HLEN + 20) { ret = OR_DROP_INVALID; goto drop; }     /* revalidate_data */
     or_ipv4_ct_tuple t; memset(&t, 0, sizeof(t));
     or_ct_state st, st_new; memset(&st, 0, sizeof(st)); memset(&st_new, 0, sizeof(st_new));
+    const uint8_t *f = skb->b;
     t.nexthdr = f[23];
     memcpy(&t.daddr, f + 30, 4); memcpy(&t.saddr, f + 26, 4);
     int l4_off = ETH_HLEN + (f[14] & 0x0F) * 4;
-    int ret = or_ct_lookup4(ep->ct4, &t, f, avail, len, l4_off, OR_CT_INGRESS, &st, now, dp->flags,
-                            &ps->nl, &ps->nu);
-    if (ret < 0) return ret;
+    ret = or_ct_lookup4(ep->ct4, &t, skb->b, skb->avail, len, l4_off, OR_CT_INGRESS, &st, now, dp->flags,
+                        &ps->nl, &ps->nu);
+    if (ret < 0) goto drop;
     ps->ct = (uint8_t)ret;
-    /* REPLY with rev_nat_index && !loopback -> lb4_rev_nat (rewrite; rows with
-     * rev-NAT come from the egress LB path, config 5) */
+    if (ret == OR_CT_REPLY && st.rev_nat_index && !st.loopback) {     /* :904-913 */
+        int r2 = lb4_rev_nat(dp, skb, l4_off, &st, &t, 1, &ps->nl);
+        if (IS_ERR(r2)) { ret = r2; goto drop; }
+    }
     int verdict = policy_can_access_ingress(ep->policy, dp->flags, len, src_label, t.dport, t.nexthdr,
                                             &ps->nl, &ps->nu);
     if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
         if (ret == OR_CT_ESTABLISHED) {               /* ct_delete4 */
             if (or_map_delete(ep->ct4, &t) == 0) ps->nu++;
         }
-        return OR_DROP_POLICY;
+        ret = OR_DROP_POLICY;
+        goto drop;
     }
     if (skip_proxy) verdict = 0;
     if (ret == OR_CT_NEW) {
@@ -736,16 +832,46 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, const uint8_t *f, uint32
         st_new.src_sec_id = src_label;
         int r = or_ct_create4(ep->ct4, &t, len, OR_CT_INGRESS, &st_new, now);
         ps->nu += 2;
-        if (IS_ERR(r)) return r;
+        if (IS_ERR(r)) { ret = r; goto drop; }
     }
     if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
         /* ipv4_redirect_to_host_port (lib/lxc.h:97-142): rewrite + proxy-map insert
          * (L7 side effect, out of scope); the verdict redirects to HOST_IFINDEX. */
         ps->proxy = (uint16_t)verdict;
         ifindex = HOST_IFINDEX;
+    } else {
+        update_metrics(dp, len, 1, 0);                /* send_trace_notify(TRACE_TO_LXC) */
     }
     if (ifindex) return OR_TC_ACT_REDIRECT;           /* redirect(ifindex, 0) */
     return OR_TC_ACT_OK;
+drop:
+    if (ret == OR_E_TRUNC) return ret;
+    update_metrics(dp, len, 1, (uint8_t)(-ret));      /* tail_ipv4_policy: send_drop_notify */
+    if (reason) *reason = ret;
+    return OR_TC_ACT_SHOT;
+}
+
+static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t ifindex, uint32_t src_label,
+                       int skip_proxy, uint32_t now, pkt_state *ps, int32_t *reason);
+
+/* handle_policy (bpf_lxc.c:1003-1038): the cilium_policy[lxc_id] tail-call target;
+ * DROP_ALL drops before any conntrack work; an IPv4 packet needs LXC_IPV4. */
+static int handle_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t ifindex, uint32_t src_label,
+                         int skip_proxy, uint32_t now, pkt_state *ps, int32_t *reason)
+{
+    uint16_t proto = 0;
+    if (skb->avail >= 14) memcpy(&proto, skb->b + 12, 2);
+    int ret;
+    if (dp->flags & OR_F_DROP_ALL) ret = OR_DROP_POLICY;
+    else if (proto == 0xDD86) {
+        if (ep->ct6) return ipv6_policy(dp, ep, skb, ifindex, src_label, skip_proxy, now, ps, reason);
+        ret = OR_DROP_MISSED_TAIL_CALL;
+    } else if (proto == 0x0008 && ep->ipv4) {
+        return ipv4_policy(dp, ep, skb, ifindex, src_label, skip_proxy, now, ps, reason);
+    } else ret = OR_DROP_UNKNOWN_L3;
+    update_metrics(dp, skb->len, 1, (uint8_t)(-ret));
+    if (reason) *reason = ret;
+    return OR_TC_ACT_SHOT;
 }
 
 /* handle_ipv4 (bpf/bpf_netdev.c:357-453), ENCAP_IFINDEX paths (overlay) disabled,
@@ -753,10 +879,12 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, const uint8_t *f, uint32
  * reaches the endpoint, the tail-called policy program (handle_policy ->
  * tail_ipv4_policy, bpf_lxc.c:981-1038) runs and its return value is final:
  * *final = 1 and the return is TC_ACT_SHOT / TC_ACT_OK / TC_ACT_REDIRECT. */
-static int handle_ipv4(or_dp *dp, const uint8_t *f, uint32_t avail, uint32_t len, uint32_t src_identity,
-                       int skip_proxy, uint32_t now, uint32_t *out_identity, pkt_state *ps, int *final)
+static int handle_ipv4(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_proxy, uint32_t now,
+                       uint32_t *out_identity, pkt_state *ps, int *final, int32_t *reason)
 {
     *final = 0;
+    uint32_t len = skb->len;
+    const uint8_t *f = skb->b;
     if (len < ETH_HLEN + 20) return OR_DROP_INVALID;
     int l4_off = ETH_HLEN + (f[14] & 0x0F) * 4;
     uint32_t secctx = WORLD_ID;                        /* derive_ipv4_sec_ctx (:278-290) */
@@ -772,7 +900,7 @@ static int handle_ipv4(or_dp *dp, const uint8_t *f, uint32_t avail, uint32_t len
         secctx = src_identity;
         if (nexthdr == 6 || nexthdr == 17) {           /* reverse_proxy (:293-354): port load */
             uint8_t p[4];
-            int r = ld(f, avail, len, l4_off, 4, p);
+            int r = sld(skb, l4_off, 4, p);
             if (r == OR_E_TRUNC) return r;
             if (r) return OR_DROP_CT_INVALID_HDR;
         }
@@ -784,14 +912,8 @@ static int handle_ipv4(or_dp *dp, const uint8_t *f, uint32_t avail, uint32_t len
         if (f[22] <= 1) return OR_DROP_INVALID;
         or_endpoint_prog *prog = find_ep(dp, ep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;   /* tail_call(cilium_policy, lxc_id) missed */
-        int ret = ipv4_policy(dp, prog, f, avail, len, ep->ifindex, secctx, skip_proxy, now, ps);
-        if (ret == OR_E_TRUNC) return ret;
         *final = 1;
-        if (IS_ERR(ret)) {                             /* tail_ipv4_policy: send_drop_notify */
-            update_metrics(dp, len, 1, (uint8_t)(-ret));
-            return OR_TC_ACT_SHOT;
-        }
-        return ret;
+        return handle_policy(dp, prog, skb, ep->ifindex, secctx, skip_proxy, now, ps, reason);
     }
     return OR_TC_ACT_OK;
 }
@@ -809,31 +931,33 @@ static uint32_t identity_from_mark(uint32_t mark, int *skip_proxy)
 void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
                        const uint32_t *mark, uint32_t n, uint32_t now, int with_prefilter, or_out *out)
 {
+    or_skb skb;
     for (uint32_t i = 0; i < n; i++) {
-        const uint8_t *f = frames + (size_t)i * stride;
-        uint32_t L = len[i], avail = L < stride ? L : stride;
+        skb_init(&skb, frames + (size_t)i * stride, stride, len[i]);
+        uint32_t L = len[i];
         pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
         uint8_t xv = OR_XDP_PASS;
-        int32_t ret = OR_TC_ACT_OK;
+        int32_t ret = OR_TC_ACT_OK, reason = 0;
         uint32_t ident = 0;
-        if (with_prefilter) xv = (uint8_t)xdp_one(dp, f, avail, &ps.nl);
+        if (with_prefilter) xv = (uint8_t)xdp_one(dp, skb.b, skb.avail, &ps.nl);
         if (xv == OR_XDP_PASS) {
             /* from_netdev (bpf_netdev.c:470-524) */
             uint32_t identity = 0; int skip_proxy = 0;
             if (dp->flags & OR_F_FROM_HOST) identity = identity_from_mark(mark ? mark[i] : 0, &skip_proxy);
             uint16_t proto = 0;
-            if (avail >= 14) memcpy(&proto, f + 12, 2);      /* skb->protocol */
+            if (skb.avail >= 14) memcpy(&proto, skb.b + 12, 2);      /* skb->protocol */
             ident = identity;
             if (proto == 0x0008) {
                 int final = 0;
-                int r = handle_ipv4(dp, f, avail, L, identity, skip_proxy, now, &ident, &ps, &final);
+                int r = handle_ipv4(dp, &skb, identity, skip_proxy, now, &ident, &ps, &final, &reason);
                 if (r == OR_E_TRUNC || final) ret = r;
                 else if (IS_ERR(r)) {                        /* tail_handle_ipv4 (:457-466) */
                     update_metrics(dp, L, 1, (uint8_t)(-r));
+                    reason = r;
                     ret = OR_TC_ACT_SHOT;
                 } else ret = r;
             } else {
-                ret = OR_TC_ACT_OK;                          /* IPv6 path: config 5; others to stack */
+                ret = OR_TC_ACT_OK;                          /* IPv6 and others: to the stack here */
             }
         }
         if (out->xdp) out->xdp[i] = xv;
@@ -843,6 +967,7 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
         if (out->proxy) out->proxy[i] = ps.proxy;
         if (out->nl) out->nl[i] = ps.nl;
         if (out->nu) out->nu[i] = ps.nu;
+        if (out->reason) out->reason[i] = reason;
     }
 }
 
@@ -924,6 +1049,7 @@ void or_policy_ingress(or_dp *dp, uint32_t ep_index, const uint8_t *frames, uint
         if (out->ct) out->ct[i] = OR_CT_NONE;
         if (out->nl) out->nl[i] = ps.nl;
         if (out->nu) out->nu[i] = ps.nu;
+        if (out->reason) out->reason[i] = (ret < 0 && ret != OR_E_TRUNC) ? ret : 0;
     }
 }
 
@@ -943,4 +1069,658 @@ const or_lb4_service *or_lb4_lookup_service(or_map *svc_map, or_lb4_key *key, ui
     or_lb4_service *s = or_map_lookup_ptr(svc_map, key);
     if (s && s->count != 0) return s;
     return NULL;
+}
+
+/* lb4_lookup_slave (lb.h:637-651) */
+static or_lb4_service *lb4_lookup_slave(or_map *m, or_lb4_key *key, uint16_t slave, uint8_t *nl)
+{
+    key->slave = slave;
+    (*nl)++;
+    return or_map_lookup_ptr(m, key);
+}
+
+/* lb4_select_slave / lb6_select_slave (lb.h:158-190, the WRR branch is #if 0):
+ * slave 0 is the master, so (hash % count) + 1; hash = get_hash_recalc(), an input */
+static inline uint16_t lb_select_slave(uint32_t hash, uint16_t count) { return (uint16_t)(hash % count + 1); }
+
+/* lb6_lookup_service (lb.h:334-368) with LB_L4 and LB_L3 (pkg/endpoint/bpf.go:193-194) */
+static or_lb6_service *lb6_lookup_service(or_map *m, or_lb6_key *key, uint8_t *nl)
+{
+    or_lb6_service *svc;
+    if (!m) return NULL;
+    if (key->dport) {
+        (*nl)++;
+        svc = or_map_lookup_ptr(m, key);
+        if (svc && svc->count != 0) return svc;
+        key->dport = 0;
+    }
+    (*nl)++;
+    svc = or_map_lookup_ptr(m, key);
+    if (svc && svc->count != 0) return svc;
+    return NULL;
+}
+
+/* lb6_lookup_slave (lb.h:370-384) */
+static or_lb6_service *lb6_lookup_slave(or_map *m, or_lb6_key *key, uint16_t slave, uint8_t *nl)
+{
+    key->slave = slave;
+    (*nl)++;
+    return or_map_lookup_ptr(m, key);
+}
+
+/* ct_update4_slave / ct_update6_slave (conntrack.h:573-585, 649-661) */
+static void ct_update_slave(or_map *map, const void *t, const or_ct_state *st, uint8_t *nl, uint8_t *nu)
+{
+    (*nl)++;
+    or_ct_entry *e = or_map_lookup_ptr(map, t);
+    if (!e) return;
+    e->slave = st->slave;
+    (*nu)++;
+}
+
+/* extract_l4_port (lb.h:192-216): TCP/UDP dport; ICMP/ICMPv6 none; else DROP_UNKNOWN_L4 */
+static int extract_l4_port(const or_skb *skb, uint8_t nexthdr, int l4_off, uint16_t *port)
+{
+    switch (nexthdr) {
+    case 6: case 17: {
+        int r = sld(skb, l4_off + TCP_DPORT_OFF, 2, port);   /* l4_load_port (l4.h:62-65) */
+        if (r) return r == OR_E_TRUNC ? r : OR_E_FAULT;
+        return 0;
+    }
+    case 58: case 1: return 0;
+    default: return OR_DROP_UNKNOWN_L4;
+    }
+}
+
+/* l4_modify_port (l4.h:50-60) of the destination port; checksum not modelled */
+static int l4_store_dport(or_skb *skb, int l4_off, uint16_t port)
+{
+    int r = sst(skb, l4_off + TCP_DPORT_OFF, 2, &port);
+    return r == OR_E_TRUNC ? r : r ? OR_DROP_WRITE_ERROR : 0;
+}
+
+/* lb4_local (lb.h:700-775) + lb4_xlate (:653-697) */
+static int lb4_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb4_key *key, or_ipv4_ct_tuple *t,
+                     or_lb4_service *svc, or_ct_state *st, uint32_t saddr, uint32_t hash, uint32_t now, pkt_state *ps)
+{
+    uint8_t flags = t->flags;
+    uint32_t new_saddr = 0, new_daddr;
+    int ret = or_ct_lookup4(ct, t, skb->b, skb->avail, skb->len, l4_off, OR_CT_SERVICE, st, now, dp->flags,
+                            &ps->nl, &ps->nu);
+    if (ret == OR_E_TRUNC) return ret;
+    switch (ret) {
+    case OR_CT_NEW:
+        st->slave = lb_select_slave(hash, svc->count);
+        ret = or_ct_create4(ct, t, skb->len, OR_CT_SERVICE, st, now);
+        ps->nu += 2;
+        if (IS_ERR(ret)) { t->flags = flags; return OR_DROP_NO_SERVICE; }
+        break;
+    case OR_CT_ESTABLISHED: case OR_CT_RELATED: case OR_CT_REPLY:
+        break;
+    default:
+        t->flags = flags;
+        return OR_DROP_NO_SERVICE;
+    }
+    if (!(svc = lb4_lookup_slave(dp->lb4_services, key, st->slave, &ps->nl))) {
+        if (!(svc = (or_lb4_service *)or_lb4_lookup_service(dp->lb4_services, key, &ps->nl))) {
+            t->flags = flags;
+            return OR_DROP_NO_SERVICE;
+        }
+        st->slave = lb_select_slave(hash, svc->count);
+        ct_update_slave(ct, t, st, &ps->nl, &ps->nu);
+    }
+    t->flags = flags;
+    st->rev_nat_index = svc->rev_nat_index;
+    st->addr = new_daddr = svc->target;
+    if (saddr == svc->target) {                       /* !DISABLE_LOOPBACK_LB (:753-767) */
+        new_saddr = dp->v4_loopback;
+        st->loopback = 1;
+        st->addr = new_saddr;
+        st->svc_addr = saddr;
+    }
+    if (!st->loopback) t->daddr = svc->target;
+    /* lb4_xlate */
+    int r = sst(skb, ETH_HLEN + 16, 4, &new_daddr);
+    if (r) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    if (new_saddr) {
+        r = sst(skb, ETH_HLEN + 12, 4, &new_saddr);
+        if (r) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    }
+    if (svc->port && key->dport != svc->port && (t->nexthdr == 6 || t->nexthdr == 17)) {
+        r = l4_store_dport(skb, l4_off, svc->port);
+        if (r) return r;
+    }
+    return OR_TC_ACT_OK;
+}
+
+/* policy_can_egress (policy.h:181-200) with POLICY_EGRESS && LXC_ID */
+static int policy_can_egress(or_map *map, uint32_t flags, uint32_t len, uint32_t identity, uint16_t dport,
+                             uint8_t proto, uint8_t *nl, uint8_t *nu)
+{
+    if (!(flags & OR_F_POLICY_EGRESS)) return (flags & OR_F_DROP_ALL) ? OR_DROP_POLICY : OR_TC_ACT_OK;
+    if (flags & OR_F_DROP_ALL) return OR_DROP_POLICY;
+    int ret = policy_can_access(map, flags, len, identity, dport, proto, OR_CT_EGRESS, nl, nu);
+    if (ret >= 0) return ret;
+    return OR_DROP_POLICY;
+}
+
+/* ipv4_l3 (l3.h:54-69): TTL <= 1 -> DROP_INVALID (ipv4_dec_ttl, ipv4.h:30-43) */
+static int ipv4_l3(or_skb *skb)
+{
+    uint8_t ttl = skb->b[22];
+    if (ttl <= 1) return OR_DROP_INVALID;
+    ttl--;
+    skb->b[22] = ttl;
+    return OR_TC_ACT_OK;
+}
+
+/* handle_ipv4_from_lxc (bpf_lxc.c:402-649) of endpoint `ep`, direct routing (no
+ * ENCAP_IFINDEX), LXC_NAT46 off.  A local destination gets the tail call into its
+ * policy program: *final = 1 and the return is that program's verdict. */
+static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t hash, uint32_t now,
+                                uint32_t *dst_id, pkt_state *ps, int *final, int32_t *reason)
+{
+    or_ipv4_ct_tuple t; memset(&t, 0, sizeof(t));
+    or_ct_state st_new, st; memset(&st_new, 0, sizeof(st_new)); memset(&st, 0, sizeof(st));
+    or_lb4_key key; memset(&key, 0, sizeof(key));
+    uint32_t len = skb->len;
+    uint8_t *f = skb->b;
+    int ret, verdict;
+    *final = 0;
+    if (len < ETH_HLEN + 20) return OR_DROP_INVALID;               /* revalidate_data */
+    t.nexthdr = f[23];
+    if (memcmp(f + 6, ep->mac, 6)) return OR_DROP_INVALID_SMAC;    /* is_valid_lxc_src_mac (lxc.h:31-37) */
+    if (memcmp(f + 0, ep->node_mac, 6)) return OR_DROP_INVALID_DMAC;  /* is_valid_gw_dst_mac (:69-75) */
+    uint32_t saddr; memcpy(&saddr, f + 26, 4);
+    if (saddr != ep->ipv4) return OR_DROP_INVALID_SIP;             /* is_valid_lxc_src_ipv4 (:54-61) */
+    memcpy(&t.daddr, f + 30, 4);
+    t.saddr = saddr;
+    int l4_off = ETH_HLEN + (f[14] & 0x0F) * 4;
+    /* lb4_extract_key (lb.h:519-541): key.address = daddr (CT_EGRESS) */
+    key.address = t.daddr;
+    ret = extract_l4_port(skb, t.nexthdr, l4_off, &key.dport);
+    if (ret == OR_E_TRUNC) return ret;
+    if (IS_ERR(ret)) {
+        if (ret != OR_DROP_UNKNOWN_L4) return ret;
+    } else {
+        st_new.orig_dport = key.dport;
+        or_lb4_service *svc = (or_lb4_service *)(dp->lb4_services ? or_lb4_lookup_service(dp->lb4_services, &key, &ps->nl) : NULL);
+        if (svc) {
+            ret = lb4_local(dp, ep->ct4, skb, l4_off, &key, &t, svc, &st_new, saddr, hash, now, ps);
+            if (ret == OR_E_TRUNC || IS_ERR(ret)) return ret;
+        }
+    }
+    uint32_t orig_dip = t.daddr;                                    /* skip_service_lookup: */
+    ret = or_ct_lookup4(ep->ct4, &t, skb->b, skb->avail, len, l4_off, OR_CT_EGRESS, &st, now, dp->flags,
+                        &ps->nl, &ps->nu);
+    if (ret < 0) return ret;
+    ps->ct = (uint8_t)ret;
+    /* destination category (:482-494) */
+    uint32_t dst = WORLD_ID;
+    or_remote_endpoint_info *info = ipcache_lookup4(dp, orig_dip, 32, &ps->nl);
+    if (info && info->sec_label) dst = info->sec_label;
+    else if ((orig_dip & dp->v4_cluster_mask) == dp->v4_cluster_range) dst = CLUSTER_ID;
+    *dst_id = dst;
+    verdict = policy_can_egress(ep->policy, dp->flags, len, dst, t.dport, t.nexthdr, &ps->nl, &ps->nu);
+    if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
+        if (ret == OR_CT_ESTABLISHED) {                             /* ct_delete4 */
+            if (or_map_delete(ep->ct4, &t) == 0) ps->nu++;
+        }
+        return verdict;
+    }
+    switch (ret) {
+    case OR_CT_NEW: {
+        st_new.src_sec_id = ep->seclabel;
+        int nat = st_new.addr != 0;
+        int r = or_ct_create4(ep->ct4, &t, len, OR_CT_EGRESS, &st_new, now);
+        ps->nu += nat ? 3 : 2;
+        if (IS_ERR(r)) return r;
+        break;
+    }
+    case OR_CT_ESTABLISHED:
+        break;
+    case OR_CT_RELATED: case OR_CT_REPLY:
+        if (st.rev_nat_index) {
+            int r = lb4_rev_nat(dp, skb, l4_off, &st, &t, 0, &ps->nl);
+            if (r == OR_E_TRUNC || IS_ERR(r)) return r;
+        }
+        break;
+    default:
+        return OR_DROP_POLICY;
+    }
+    if (verdict > 0) {                                              /* redirect_to_proxy */
+        /* ipv4_redirect_to_host_port: dport := proxy port, daddr := IPV4_GATEWAY,
+         * proxy-map insert (L7 side effect, out of scope) */
+        ps->proxy = (uint16_t)verdict;
+        int r = ipv4_l3(skb);
+        if (r != OR_TC_ACT_OK) return r;
+        return OR_TC_ACT_REDIRECT;                                  /* redirect(HOST_IFINDEX) */
+    }
+    uint32_t daddr; memcpy(&daddr, skb->b + 30, 4);                 /* after the L4/L3 rewrites */
+    or_endpoint_info *dep = lookup_ip4_endpoint(dp, daddr, &ps->nl);
+    if (dep) {
+        int r = ipv4_l3(skb);
+        if (r != OR_TC_ACT_OK) return r;
+        update_metrics(dp, len, 2, 0);            /* to_host: TRACE_TO_HOST / ipv4_local_delivery */
+        if (dep->flags & 1) return OR_TC_ACT_REDIRECT;              /* ENDPOINT_F_HOST: redirect(HOST_IFINDEX) */
+        or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
+        if (!prog) return OR_DROP_MISSED_TAIL_CALL;
+        *final = 1;                                                 /* handle_policy -> tail_ipv4_policy */
+        return handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
+    }
+    int r = ipv4_l3(skb);                                           /* pass_to_stack */
+    if (r != OR_TC_ACT_OK) return r;
+    update_metrics(dp, len, 2, 0);                                  /* TRACE_TO_STACK */
+    return OR_TC_ACT_OK;
+}
+
+/* ===================================================================== */
+/* IPv6                                                                   */
+/* ===================================================================== */
+
+/* ipv6_hdrlen (ipv6.h:61-98); the AUTH length is chosen by the type of the header
+ * that FOLLOWS (nh is updated first), as the reference does */
+static int ipv6_hdrlen(const or_skb *skb, int l3_off, uint8_t *nexthdr)
+{
+    int len = 40;
+    uint8_t nh = *nexthdr;
+    for (int i = 0; i < 4; i++) {
+        switch (nh) {
+        case 59: return OR_DROP_INVALID_EXTHDR;
+        case 44: return OR_DROP_FRAG_NOSUPPORT;
+        case 0: case 43: case 51: case 60: {
+            uint8_t opt[2];
+            int r = sld(skb, l3_off + len, 2, opt);
+            if (r == OR_E_TRUNC) return r;
+            if (r) return OR_DROP_INVALID;
+            nh = opt[0];
+            if (nh == 51) len += (opt[1] + 2) << 2;
+            else len += (opt[1] + 1) << 3;
+            break;
+        }
+        default:
+            *nexthdr = nh;
+            return len;
+        }
+    }
+    return OR_DROP_INVALID_EXTHDR;
+}
+
+/* ipv6_ct_tuple_reverse (conntrack.h:264-284) */
+static void ct_tuple_reverse6(or_ipv6_ct_tuple *t)
+{
+    uint8_t a[16]; memcpy(a, t->saddr, 16); memcpy(t->saddr, t->daddr, 16); memcpy(t->daddr, a, 16);
+    uint16_t p = t->sport; t->sport = t->dport; t->dport = p;
+    if (t->flags & TUPLE_F_IN) t->flags &= (uint8_t)~TUPLE_F_IN; else t->flags |= TUPLE_F_IN;
+}
+
+/* ct_lookup6 (conntrack.h:286-412) */
+static int ct_lookup6(or_map *ct, or_ipv6_ct_tuple *t, const or_skb *skb, int off, int dir, or_ct_state *st,
+                      uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu)
+{
+    int action = ACTION_UNSPEC, r;
+    int tcp = t->nexthdr == 6;
+    uint8_t seen = 0;
+    if (dir == OR_CT_INGRESS) t->flags = TUPLE_F_OUT;
+    else if (dir == OR_CT_EGRESS) t->flags = TUPLE_F_IN;
+    else if (dir == OR_CT_SERVICE) t->flags = TUPLE_F_SERVICE;
+    else return OR_DROP_CT_INVALID_HDR;
+    switch (t->nexthdr) {
+    case 58: {                                        /* IPPROTO_ICMPV6 */
+        uint8_t type;
+        r = sld(skb, off, 1, &type);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        t->sport = 0; t->dport = 0;
+        switch (type) {
+        case 1: case 2: case 3: case 4:               /* DEST_UNREACH, PKT_TOOBIG, TIME_EXCEED, PARAMPROB */
+            t->flags |= TUPLE_F_RELATED; break;
+        case 129:                                     /* ECHO_REPLY: dport = ICMPV6_ECHO_REQUEST (raw 128) */
+            t->dport = 128; break;
+        case 128:                                     /* ECHO_REQUEST */
+            t->sport = type; /* fallthrough */
+        default:
+            action = ACTION_CREATE; break;
+        }
+        break;
+    }
+    case 6: {
+        uint8_t fl[2];
+        r = sld(skb, off + 12, 2, fl);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        seen = fl[1];
+        action = (seen & (TCPF_RST | TCPF_FIN)) ? ACTION_CLOSE : ACTION_CREATE;
+        r = sld(skb, off, 4, &t->dport);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        break;
+    }
+    case 17:
+        r = sld(skb, off, 4, &t->dport);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_DROP_CT_INVALID_HDR;
+        action = ACTION_CREATE;
+        break;
+    default:
+        return OR_DROP_CT_UNKNOWN_PROTO;
+    }
+    int ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, skb->len, now, flags, nl, nu);
+    if (ret != OR_CT_NEW) return (t->flags & TUPLE_F_RELATED) ? OR_CT_RELATED : OR_CT_REPLY;
+    if (dir != OR_CT_SERVICE) {
+        ct_tuple_reverse6(t);
+        ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, skb->len, now, flags, nl, nu);
+    }
+    return ret;
+}
+
+/* ct_create6 (conntrack.h:589-639) */
+static int ct_create6(or_map *ct, const or_ipv6_ct_tuple *t, uint32_t skb_len, int dir, const or_ct_state *st,
+                      uint32_t now)
+{
+    or_ct_entry e; memset(&e, 0, sizeof(e));
+    int tcp = t->nexthdr == 6;
+    e.rev_nat_index = st->rev_nat_index;
+    if (st->loopback) e.bits |= B_LB_LOOPBACK;
+    e.slave = st->slave;
+    ct_update_timeout(&e, tcp, dir, tcp ? TCPF_SYN : 0, now);
+    if (dir == OR_CT_INGRESS) { e.rx_packets = 1; e.rx_bytes = skb_len; }
+    else                      { e.tx_packets = 1; e.tx_bytes = skb_len; }
+    e.src_sec_id = st->src_sec_id;
+    if (or_map_update(ct, t, &e, 0) < 0) return OR_DROP_CT_CREATE_FAILED;
+    or_ipv6_ct_tuple it; memset(&it, 0, sizeof(it));
+    it.nexthdr = 58;
+    it.flags = t->flags | TUPLE_F_RELATED;
+    e.bits |= B_SEEN_NON_SYN;
+    memcpy(it.daddr, t->daddr, 16); memcpy(it.saddr, t->saddr, 16);
+    if (or_map_update(ct, &it, &e, 0) < 0) return OR_DROP_CT_CREATE_FAILED;
+    return 0;
+}
+
+/* lb6_rev_nat / __lb6_rev_nat (lb.h:254-315), flags = 0 on every caller here:
+ * rewrites the source address (and port) of the packet */
+static int lb6_rev_nat(or_dp *dp, or_skb *skb, int l4_off, uint16_t index, const or_ipv6_ct_tuple *t, uint8_t *nl)
+{
+    if (!dp->lb6_revnat) return 0;
+    (*nl)++;
+    or_lb6_reverse_nat *nat = or_map_lookup_ptr(dp->lb6_revnat, &index);
+    if (!nat) return 0;
+    int r;
+    if (nat->port) {
+        switch (t->nexthdr) {
+        case 6: case 17: {
+            uint16_t old;
+            if ((r = sld(skb, l4_off + TCP_SPORT_OFF, 2, &old))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
+            if (nat->port != old) {
+                if ((r = sst(skb, l4_off + TCP_SPORT_OFF, 2, &nat->port))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+            }
+            break;
+        }
+        case 1: case 58: break;
+        default: return OR_DROP_UNKNOWN_L4;
+        }
+    }
+    uint8_t old[16];
+    if ((r = sld(skb, ETH_HLEN + 8, 16, old))) return r == OR_E_TRUNC ? r : OR_DROP_INVALID;   /* ipv6_load_saddr */
+    if ((r = sst(skb, ETH_HLEN + 8, 16, nat->address))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    return 0;
+}
+
+/* lb6_local (lb.h:426-483) + lb6_xlate (:386-424) */
+static int lb6_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb6_key *key, or_ipv6_ct_tuple *t,
+                     or_lb6_service *svc, or_ct_state *st, uint32_t hash, uint32_t now, pkt_state *ps)
+{
+    uint8_t flags = t->flags;
+    int ret = ct_lookup6(ct, t, skb, l4_off, OR_CT_SERVICE, st, now, dp->flags, &ps->nl, &ps->nu);
+    if (ret == OR_E_TRUNC) return ret;
+    switch (ret) {
+    case OR_CT_NEW:
+        st->slave = lb_select_slave(hash, svc->count);
+        ret = ct_create6(ct, t, skb->len, OR_CT_SERVICE, st, now);
+        ps->nu += 2;
+        if (IS_ERR(ret)) { t->flags = flags; return OR_DROP_NO_SERVICE; }
+        break;
+    case OR_CT_ESTABLISHED: case OR_CT_RELATED: case OR_CT_REPLY:
+        break;
+    default:
+        t->flags = flags;
+        return OR_DROP_NO_SERVICE;
+    }
+    if (!(svc = lb6_lookup_slave(dp->lb6_services, key, st->slave, &ps->nl))) {
+        if (!(svc = lb6_lookup_service(dp->lb6_services, key, &ps->nl))) {
+            t->flags = flags;
+            return OR_DROP_NO_SERVICE;
+        }
+        st->slave = lb_select_slave(hash, svc->count);
+        ct_update_slave(ct, t, st, &ps->nl, &ps->nu);
+    }
+    t->flags = flags;
+    memcpy(t->daddr, svc->target, 16);
+    st->rev_nat_index = svc->rev_nat_index;
+    int r = sst(skb, ETH_HLEN + 24, 16, svc->target);              /* ipv6_store_daddr */
+    if (r) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    if (svc->port && key->dport != svc->port && (t->nexthdr == 6 || t->nexthdr == 17)) {
+        r = l4_store_dport(skb, l4_off, svc->port);
+        if (r) return r;
+    }
+    return OR_TC_ACT_OK;
+}
+
+/* ipv6_l3 (l3.h:30-51): hop limit <= 1 -> icmp6_send_time_exceeded tail call */
+static int ipv6_l3(or_skb *skb)
+{
+    uint8_t hl = skb->b[21];
+    if (hl <= 1) return OR_E_PUNT;
+    skb->b[21] = (uint8_t)(hl - 1);
+    return OR_TC_ACT_OK;
+}
+
+/* ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862) */
+static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t ifindex, uint32_t src_label,
+                       int skip_proxy, uint32_t now, pkt_state *ps, int32_t *reason)
+{
+    int ret, verdict;
+    uint32_t len = skb->len;
+    if (len < ETH_HLEN + 40) { ret = OR_DROP_INVALID; goto drop; }
+    or_ipv6_ct_tuple t; memset(&t, 0, sizeof(t));
+    or_ct_state st, st_new; memset(&st, 0, sizeof(st)); memset(&st_new, 0, sizeof(st_new));
+    t.nexthdr = skb->b[20];
+    memcpy(t.daddr, skb->b + 38, 16); memcpy(t.saddr, skb->b + 22, 16);
+    ret = ipv6_hdrlen(skb, ETH_HLEN, &t.nexthdr);
+    if (ret < 0) goto drop;
+    int l4_off = ETH_HLEN + ret;
+    /* derive reverse NAT index and zero it (:750-766): low 16 bits of daddr word 3 */
+    uint32_t w3; memcpy(&w3, skb->b + 38 + 12, 4);
+    st_new.rev_nat_index = (uint16_t)(w3 & 0xFFFF);
+    if (st_new.rev_nat_index) {
+        w3 &= ~0xFFFFu;
+        int r = sst(skb, ETH_HLEN + 24 + 12, 4, &w3);
+        if (r) { ret = r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR; goto drop; }
+    }
+    ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_INGRESS, &st, now, dp->flags, &ps->nl, &ps->nu);
+    if (ret < 0) goto drop;
+    ps->ct = (uint8_t)ret;
+    if (st.rev_nat_index) {
+        int r2 = lb6_rev_nat(dp, skb, l4_off, st.rev_nat_index, &t, &ps->nl);
+        if (r2 == OR_E_TRUNC || IS_ERR(r2)) { ret = r2; goto drop; }
+    }
+    verdict = policy_can_access_ingress(ep->policy, dp->flags, len, src_label, t.dport, t.nexthdr, &ps->nl, &ps->nu);
+    if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
+        if (ret == OR_CT_ESTABLISHED) {
+            if (or_map_delete(ep->ct6, &t) == 0) ps->nu++;
+        }
+        ret = OR_DROP_POLICY;
+        goto drop;
+    }
+    if (skip_proxy) verdict = 0;
+    if (ret == OR_CT_NEW) {
+        st_new.orig_dport = t.dport;
+        st_new.src_sec_id = src_label;
+        int r = ct_create6(ep->ct6, &t, len, OR_CT_INGRESS, &st_new, now);
+        ps->nu += 2;
+        if (IS_ERR(r)) { ret = r; goto drop; }
+    }
+    if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
+        ps->proxy = (uint16_t)verdict;                /* ipv6_redirect_to_host_port */
+        ifindex = HOST_IFINDEX;
+    } else {
+        update_metrics(dp, len, 1, 0);                /* TRACE_TO_LXC */
+    }
+    return ifindex ? OR_TC_ACT_REDIRECT : OR_TC_ACT_OK;
+drop:
+    if (ret == OR_E_TRUNC) return ret;
+    update_metrics(dp, len, 1, (uint8_t)(-ret));
+    if (reason) *reason = ret;
+    return OR_TC_ACT_SHOT;
+}
+
+/* handle_ipv6 (bpf_lxc.c:354-380) + ipv6_l3_from_lxc (:82-352), direct routing */
+static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t hash, uint32_t now,
+                                uint32_t *dst_id, pkt_state *ps, int *final, int32_t *reason)
+{
+    or_ipv6_ct_tuple t; memset(&t, 0, sizeof(t));
+    or_ct_state st_new, st; memset(&st_new, 0, sizeof(st_new)); memset(&st, 0, sizeof(st));
+    or_lb6_key key; memset(&key, 0, sizeof(key));
+    uint32_t len = skb->len;
+    uint8_t *f = skb->b;
+    int ret, verdict;
+    *final = 0;
+    if (!ep->ct6) return OR_DROP_MISSED_TAIL_CALL;                  /* endpoint without an IPv6 program */
+    if (len < ETH_HLEN + 40) return OR_DROP_INVALID;
+    if (f[20] == 58) {                                              /* icmp6_handle (icmp6.h:390-412) */
+        if (len < ETH_HLEN + 40 + 8) return OR_DROP_INVALID;
+        uint8_t type = f[54];
+        if (type == 135) return OR_E_PUNT;                          /* icmp6_handle_ns tail call */
+        if (type == 128 && !memcmp(f + 38, dp->router_ip6, 16)) return OR_E_PUNT;   /* echo reply */
+    }
+    t.nexthdr = f[20];
+    if (memcmp(f + 6, ep->mac, 6)) return OR_DROP_INVALID_SMAC;
+    if (memcmp(f + 0, ep->node_mac, 6)) return OR_DROP_INVALID_DMAC;
+    if (memcmp(f + 22, ep->ipv6, 16)) return OR_DROP_INVALID_SIP;  /* is_valid_lxc_src_ip (:41-49) */
+    memcpy(t.daddr, f + 38, 16); memcpy(t.saddr, f + 22, 16);
+    ret = ipv6_hdrlen(skb, ETH_HLEN, &t.nexthdr);
+    if (ret < 0) return ret;
+    int l4_off = ETH_HLEN + ret;
+    memcpy(key.address, t.daddr, 16);                               /* lb6_extract_key (lb.h:317-332) */
+    ret = extract_l4_port(skb, t.nexthdr, l4_off, &key.dport);
+    if (ret == OR_E_TRUNC) return ret;
+    if (IS_ERR(ret)) {
+        if (ret != OR_DROP_UNKNOWN_L4) return ret;
+    } else {
+        st_new.orig_dport = key.dport;
+        or_lb6_service *svc = lb6_lookup_service(dp->lb6_services, &key, &ps->nl);
+        if (svc) {
+            ret = lb6_local(dp, ep->ct6, skb, l4_off, &key, &t, svc, &st_new, hash, now, ps);
+            if (ret == OR_E_TRUNC || IS_ERR(ret)) return ret;
+        }
+    }
+    uint8_t orig_dip[16]; memcpy(orig_dip, t.daddr, 16);
+    ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_EGRESS, &st, now, dp->flags, &ps->nl, &ps->nu);
+    if (ret < 0) return ret;
+    ps->ct = (uint8_t)ret;
+    uint32_t dst = WORLD_ID;
+    or_remote_endpoint_info *info = ipcache_lookup6(dp, orig_dip, 128, &ps->nl);
+    if (info && info->sec_label) dst = info->sec_label;
+    else if (!memcmp(skb->b + 38, dp->router_ip6, 8)) dst = CLUSTER_ID;   /* ipv6_match_prefix_64 */
+    *dst_id = dst;
+    verdict = policy_can_egress(ep->policy, dp->flags, len, dst, t.dport, t.nexthdr, &ps->nl, &ps->nu);
+    if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
+        if (ret == OR_CT_ESTABLISHED) {
+            if (or_map_delete(ep->ct6, &t) == 0) ps->nu++;
+        }
+        return verdict;
+    }
+    switch (ret) {
+    case OR_CT_NEW: {
+        st_new.src_sec_id = ep->seclabel;
+        int r = ct_create6(ep->ct6, &t, len, OR_CT_EGRESS, &st_new, now);
+        ps->nu += 2;
+        if (IS_ERR(r)) return r;
+        break;
+    }
+    case OR_CT_ESTABLISHED:
+        break;
+    case OR_CT_RELATED: case OR_CT_REPLY:
+        if (st.rev_nat_index) {
+            int r = lb6_rev_nat(dp, skb, l4_off, st.rev_nat_index, &t, &ps->nl);
+            if (r == OR_E_TRUNC || IS_ERR(r)) return r;
+        }
+        break;
+    default:
+        return OR_DROP_POLICY;
+    }
+    if (verdict > 0) {
+        ps->proxy = (uint16_t)verdict;                              /* ipv6_redirect_to_host_port */
+        int r = ipv6_l3(skb);
+        if (r != OR_TC_ACT_OK) return r;
+        return OR_TC_ACT_REDIRECT;
+    }
+    or_endpoint_info *dep = lookup_ip6_endpoint(dp, skb->b + 38, &ps->nl);
+    if (dep) {
+        int r = ipv6_l3(skb);
+        if (r != OR_TC_ACT_OK) return r;
+        update_metrics(dp, len, 2, 0);
+        if (dep->flags & 1) return OR_TC_ACT_REDIRECT;
+        or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
+        if (!prog) return OR_DROP_MISSED_TAIL_CALL;
+        *final = 1;
+        return handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
+    }
+    int r = ipv6_l3(skb);                                           /* pass_to_stack */
+    if (r != OR_TC_ACT_OK) return r;
+    update_metrics(dp, len, 2, 0);
+    return OR_TC_ACT_OK;
+}
+
+/* handle_ingress (bpf_lxc.c:672-716, "from-container") + tail_handle_ipv{4,6}
+ * (:382-392, 651-661): the verdict of one packet from endpoint ep */
+static int from_container(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t hash, uint32_t now,
+                          uint32_t *dst_id, pkt_state *ps, int32_t *reason)
+{
+    uint16_t proto = 0;
+    if (skb->avail >= 14) memcpy(&proto, skb->b + 12, 2);           /* skb->protocol */
+    int ret, final = 0;
+    if (dp->flags & OR_F_DROP_ALL) {
+        if (proto == 0x0608) return OR_E_PUNT;                      /* ARP responder */
+        ret = OR_DROP_POLICY;
+    } else if (proto == 0xDD86) {
+        ret = handle_ipv6_from_lxc(dp, ep, skb, hash, now, dst_id, ps, &final, reason);
+    } else if (proto == 0x0008) {
+        if (!ep->ipv4) ret = OR_DROP_MISSED_TAIL_CALL;              /* no CILIUM_CALL_IPV4_FROM_LXC */
+        else ret = handle_ipv4_from_lxc(dp, ep, skb, hash, now, dst_id, ps, &final, reason);
+    } else if (proto == 0x0608) {
+        return OR_E_PUNT;
+    } else {
+        ret = OR_DROP_UNKNOWN_L3;
+    }
+    if (final || ret == OR_E_TRUNC || ret == OR_E_PUNT) return ret;
+    if (IS_ERR(ret)) {                                              /* send_drop_notify(METRIC_EGRESS) */
+        update_metrics(dp, skb->len, 2, (uint8_t)(-ret));
+        *reason = ret;
+        return OR_TC_ACT_SHOT;
+    }
+    return ret;
+}
+
+void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                   const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
+                   uint32_t now, or_out *out)
+{
+    or_skb skb;
+    for (uint32_t i = 0; i < n; i++) {
+        skb_init(&skb, frames + (size_t)i * stride, stride, len[i]);
+        pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
+        uint32_t e = src_ep ? src_ep[i] : ep0, dst = 0;
+        int32_t reason = 0, ret;
+        if (e >= dp->n_ep) ret = OR_DROP_MISSED_TAIL_CALL;
+        else ret = from_container(dp, &dp->ep[e], &skb, flow_hash ? flow_hash[i] : 0, now, &dst, &ps, &reason);
+        if (out->ret) out->ret[i] = ret;
+        if (out->identity) out->identity[i] = dst;
+        if (out->ct) out->ct[i] = ps.ct;
+        if (out->proxy) out->proxy[i] = ps.proxy;
+        if (out->nl) out->nl[i] = ps.nl;
+        if (out->nu) out->nu[i] = ps.nu;
+        if (out->reason) out->reason[i] = reason;
+        if (out->xdp) out->xdp[i] = 0;
+    }
 }

@@ -54,8 +54,15 @@ extern "C" {
 #define OR_DROP_INVALID_EXTHDR    -156
 #define OR_DROP_FRAG_NOSUPPORT    -157
 #define OR_DROP_NO_SERVICE        -158
+#define OR_DROP_WRITE_ERROR       -141
+#define OR_DROP_PROXYMAP_CREATE_FAILED -159
 /* oracle-only: a header byte the reference would read lies beyond the record */
 #define OR_E_TRUNC                -1
+/* oracle-only: the packet left this path through a tail call into a responder
+ * program outside it (ARP / ICMPv6 NS / echo-to-router / hop-limit-exceeded) */
+#define OR_E_PUNT                 -2
+/* skb_load_bytes() failure as the BPF helper reports it (-EFAULT) */
+#define OR_E_FAULT                -14
 
 /* CT results (bpf/lib/common.h:331-336) */
 #define OR_CT_NEW 0
@@ -97,6 +104,13 @@ typedef struct {             /* common.h:380-406, 56 bytes; bits@36: rx_closing 
 typedef struct {             /* common.h:452-461 (internal) */
     uint16_t rev_nat_index; uint16_t loopback; uint16_t orig_dport; uint32_t addr, svc_addr, src_sec_id; uint16_t slave;
 } or_ct_state;
+typedef struct {             /* common.h:338-346, 40 bytes, unpacked: 2 zero pad bytes */
+    uint8_t daddr[16], saddr[16]; uint16_t dport, sport; uint8_t nexthdr, flags; uint16_t pad;
+} or_ipv6_ct_tuple;
+#pragma pack(push, 1)
+typedef struct { uint32_t address; uint16_t port; } or_lb4_reverse_nat;       /* common.h:441-444 */
+typedef struct { uint8_t address[16]; uint16_t port; } or_lb6_reverse_nat;    /* common.h:422-425 */
+#pragma pack(pop)
 
 /* ---- generic kernel-semantics map ---- */
 typedef struct or_map or_map;
@@ -128,6 +142,12 @@ typedef struct {
     uint16_t lxc_id; uint32_t seclabel;
     or_map *policy;          /* cilium_policy_<id> */
     or_map *ct4;             /* CT_MAP4 of this endpoint (may be a shared global map) */
+    or_map *ct6;             /* CT_MAP6 (bpf_lxc.c:53-63) */
+    /* lxc_config.h constants of the endpoint's program (pkg/endpoint/bpf.go:152-200) */
+    uint32_t ipv4;           /* LXC_IPV4 (raw, network order); 0 = no IPv4 program */
+    uint8_t  ipv6[16];       /* LXC_IP */
+    uint8_t  mac[6];         /* LXC_MAC */
+    uint8_t  node_mac[6];    /* NODE_MAC */
 } or_endpoint_prog;
 
 typedef struct or_dp {
@@ -136,7 +156,11 @@ typedef struct or_dp {
     or_map *lxc;             /* cilium_lxc  (maps.h:27-33) */
     or_map *ipcache;         /* cilium_ipcache (maps.h:151-158) */
     or_map *lb4_services, *lb6_services;
+    or_map *lb4_revnat, *lb6_revnat;   /* cilium_lb{4,6}_reverse_nat (lb.h:37-65) */
     uint32_t flags;
+    /* node_config.h constants (raw network-order words) */
+    uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
+    uint8_t  router_ip6[16];
     uint32_t n_ep;
     or_endpoint_prog ep[OR_MAX_EP];   /* tail-call targets of cilium_policy (maps.h:44-51) */
     uint16_t ep_of_lxc[65536];        /* lxc_id -> index + 1 */
@@ -146,6 +170,12 @@ typedef struct or_dp {
 or_dp *or_dp_create(uint32_t flags);
 void   or_dp_free(or_dp *dp);          /* does not free maps */
 int    or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *policy, or_map *ct4);
+/* the endpoint program's lxc_config.h constants and its CT_MAP6 */
+int    or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_t *ipv6, const uint8_t *mac,
+                             const uint8_t *node_mac, or_map *ct6);
+/* node_config.h: IPV4_CLUSTER_MASK / IPV4_CLUSTER_RANGE / IPV4_LOOPBACK / ROUTER_IP */
+void   or_dp_node_config(or_dp *dp, uint32_t v4_cluster_mask, uint32_t v4_cluster_range, uint32_t v4_loopback,
+                         const uint8_t *router_ip6);
 void   or_dp_metrics(const or_dp *dp, uint64_t *out /* [256][4][2] */);
 
 /* per-packet outputs (SoA; any pointer may be NULL) */
@@ -157,6 +187,7 @@ typedef struct {
     uint16_t *proxy;      /* proxy port (raw be16) when redirected to proxy */
     uint8_t  *nl;         /* map lookups performed (algorithmic bytes) */
     uint8_t  *nu;         /* map entry writes performed */
+    int32_t  *reason;     /* DROP_* behind a TC_ACT_SHOT, else 0 */
 } or_out;
 
 /* Config 1: bpf_xdp.c xdp_start over a batch of frames (records of `stride` bytes). */
@@ -174,6 +205,15 @@ void or_policy_ingress(or_dp *dp, uint32_t ep_index, const uint8_t *frames, uint
  * into the endpoint's ipv4_policy (CT lookup/create, policy).  Sequential, as one CPU. */
 void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
                        const uint32_t *mark, uint32_t n, uint32_t now, int with_prefilter, or_out *out);
+
+/* Config 5: from-container (bpf_lxc.c:672-716 handle_ingress) of the packets' source
+ * endpoints: handle_ipv4_from_lxc / ipv6_l3_from_lxc with lb4/lb6 service lookup,
+ * lb{4,6}_local, egress conntrack and policy, and local delivery into the destination
+ * endpoint's ipv{4,6}_policy.  Sequential, as one CPU.  src_ep[i] = endpoint index
+ * of packet i (NULL: all from ep0); flow_hash[i] = get_hash_recalc() of packet i. */
+void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                   const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
+                   uint32_t now, or_out *out);
 
 /* ct_create4 on a given tuple (conntrack.h:663-744), for building preloaded tables. */
 int or_ct_create4(or_map *ct, or_ipv4_ct_tuple *tuple, uint32_t skb_len, int dir,

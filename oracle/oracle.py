@@ -55,6 +55,9 @@ def lib():
         L.or_policy_ingress.argtypes = [vp, u32, vp, u32, vp, vp, u32, vp]
         L.or_netdev_ingress.argtypes = [vp, vp, u32, vp, vp, u32, u32, i32, vp]
         L.or_ct_create4.argtypes = [vp, vp, u32, i32, vp, u32]
+        L.or_dp_endpoint_config.argtypes = [vp, u32, u32, vp, vp, vp, vp]
+        L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp]
+        L.or_lxc_egress.argtypes = [vp, vp, u32, vp, vp, u32, vp, u32, u32, vp]
         _lib = L
     return _lib
 
@@ -128,16 +131,19 @@ class Out:
         self.proxy = np.zeros(n, np.uint16)
         self.nl = np.zeros(n, np.uint8)
         self.nu = np.zeros(n, np.uint8)
+        self.reason = np.zeros(n, np.int32)
+
+    FIELDS = ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason")
 
     def struct(self):
-        return (C.c_void_p * 7)(*[a.ctypes.data for a in
-                                  (self.xdp, self.ret, self.identity, self.ct, self.proxy, self.nl, self.nu)])
+        return (C.c_void_p * 8)(*[getattr(self, k).ctypes.data for k in self.FIELDS])
 
 
 class ODp:
     """The oracle datapath: maps bound by role, endpoints, metrics."""
 
-    ROLES = ("v4_fix", "v4_dyn", "v6_fix", "v6_dyn", "lxc", "ipcache", "lb4_services", "lb6_services")
+    ROLES = ("v4_fix", "v4_dyn", "v6_fix", "v6_dyn", "lxc", "ipcache", "lb4_services", "lb6_services",
+             "lb4_revnat", "lb6_revnat")
 
     def __init__(self, flags=F_DEFAULT):
         self.h = lib().or_dp_create(flags)
@@ -146,20 +152,49 @@ class ODp:
 
     def bind(self, role, omap):
         idx = self.ROLES.index(role)
-        # or_dp layout: 8 map pointers first
+        # or_dp layout: the role map pointers first, in ROLES order
         ptrs = C.cast(self.h, C.POINTER(C.c_void_p))
         ptrs[idx] = omap.h
         self.maps[role] = omap
 
     def add_endpoint(self, lxc_id, seclabel, policy, ct4=None):
         self.keep += [policy, ct4]
-        return lib().or_dp_add_endpoint(self.h, lxc_id, seclabel, policy.h if policy else None,
-                                        ct4.h if ct4 else None)
+        return lib().or_dp_add_endpoint(self.h, lxc_id, seclabel, policy.h if policy is not None else None,
+                                        ct4.h if ct4 is not None else None)
+
+    def endpoint_config(self, ep, ipv4=0, ipv6=None, mac=None, node_mac=None, ct6=None):
+        """lxc_config.h constants of endpoint `ep` (ipv4 as a host-order int) and its CT_MAP6."""
+        import struct
+        raw4 = struct.unpack("<I", struct.pack(">I", ipv4))[0]
+        bufs = [None if b is None else C.create_string_buffer(bytes(b), len(bytes(b))) for b in (ipv6, mac, node_mac)]
+        if ct6 is not None:
+            self.keep.append(ct6)
+        r = lib().or_dp_endpoint_config(self.h, ep, raw4, *bufs, ct6.h if ct6 is not None else None)
+        if r:
+            raise OSError(-r, "or_dp_endpoint_config")
+
+    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=b"\0" * 16):
+        """node_config.h constants; the v4 words as host-order ints (written in network order)."""
+        import struct
+        raw = [struct.unpack("<I", struct.pack(">I", v))[0] for v in (cluster_mask, cluster_range, loopback)]
+        lib().or_dp_node_config(self.h, *raw, C.create_string_buffer(bytes(router_ip6), 16))
 
     def metrics(self):
         m = np.zeros((256, 4, 2), np.uint64)
         lib().or_dp_metrics(self.h, m.ctypes.data)
         return m
+
+    def lxc_egress(self, frames, length, src_ep=None, flow_hash=None, now=0, ep0=0):
+        n = len(length)
+        out = Out(n)
+        frames = np.ascontiguousarray(frames, np.uint8)
+        length = np.ascontiguousarray(length, np.uint32)
+        src_ep = None if src_ep is None else np.ascontiguousarray(src_ep, np.uint16)
+        flow_hash = None if flow_hash is None else np.ascontiguousarray(flow_hash, np.uint32)
+        s = out.struct()
+        lib().or_lxc_egress(self.h, _p(frames), frames.shape[1], _p(length), _p(src_ep), ep0, _p(flow_hash), n,
+                            now, C.byref(s))
+        return out
 
     def xdp_prefilter(self, frames, length):
         n = len(length)

@@ -6,7 +6,15 @@ import numpy as np
 
 from cilium_amd import synth
 
-ROLE_NAMES = ("v4_fix", "v4_dyn", "v6_fix", "v6_dyn", "lxc", "ipcache")
+ROLE_NAMES = ("v4_fix", "v4_dyn", "v6_fix", "v6_dyn", "lxc", "ipcache", "lb4_services", "lb6_services",
+              "lb4_revnat", "lb6_revnat")
+DEFAULT_MAC = bytes([0xAA, 0xBB, 0xCC, 0xDD, 0xEE, 0xFF])          # bpf/lxc_config.h:23 LXC_MAC
+NODE_MAC = bytes([0xDE, 0xAD, 0xBE, 0xEF, 0xC0, 0xDE])             # bpf/node_config.h:51
+
+
+def _ep_cfg(e):
+    return dict(ipv4=e.get("ip", 0), ipv6=e.get("ip6", bytes(16)), mac=e.get("mac", DEFAULT_MAC),
+                node_mac=e.get("node_mac", NODE_MAC))
 
 
 def oracle_dp(w: synth.Workload, flags=None, with_ct=True):
@@ -19,9 +27,13 @@ def oracle_dp(w: synth.Workload, flags=None, with_ct=True):
             dp.bind(name, maps[name])
     pol = maps.get("policy")
     ct = maps.get("ct4") if with_ct else None
+    ct6 = maps.get("ct6") if with_ct else None
     if w.endpoints:
         for e in w.endpoints:
-            dp.add_endpoint(e["lxc_id"], e["seclabel"], pol, ct)
+            i = dp.add_endpoint(e["lxc_id"], e["seclabel"], pol, ct)
+            dp.endpoint_config(i, ct6=ct6, **_ep_cfg(e))
+    if w.extra and "node" in w.extra:
+        dp.node_config(**w.extra["node"])
     dp.keep += list(maps.values())
     return dp, maps
 

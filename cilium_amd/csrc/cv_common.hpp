@@ -10,11 +10,17 @@ namespace cv {
 
 // bpf/lib/common.h:237-269
 enum : int32_t {
+    DROP_INVALID_SMAC = -130, DROP_INVALID_DMAC = -131, DROP_INVALID_SIP = -132,
     DROP_POLICY = -133, DROP_INVALID = -134, DROP_CT_INVALID_HDR = -135,
     DROP_CT_UNKNOWN_PROTO = -137, DROP_UNKNOWN_L3 = -139, DROP_MISSED_TAIL_CALL = -140,
-    DROP_UNKNOWN_L4 = -142, DROP_CT_CREATE_FAILED = -155, DROP_NO_SERVICE = -158,
+    DROP_WRITE_ERROR = -141, DROP_UNKNOWN_L4 = -142, DROP_CT_CREATE_FAILED = -155,
+    DROP_INVALID_EXTHDR = -156, DROP_FRAG_NOSUPPORT = -157, DROP_NO_SERVICE = -158,
 };
-enum : int32_t { TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7, E_TRUNC = -1 };
+// E_TRUNC: a byte the path reads lies beyond the record (the caller must hand over
+// more of the frame); E_PUNT: the packet left the path through a tail call into a
+// responder program (ARP, ICMPv6 NS / echo-to-router / hop limit); E_FAULT: the
+// -EFAULT of a failed skb_load_bytes(), which the reference treats as a drop code.
+enum : int32_t { TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7, E_TRUNC = -1, E_PUNT = -2, E_FAULT = -14 };
 enum : uint8_t { XDP_DROP = 1, XDP_PASS = 2 };
 enum : uint8_t { CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3, CT_NONE = 0xff };
 enum : int { CT_EGRESS = 0, CT_INGRESS = 1, CT_SERVICE = 2 };

@@ -112,7 +112,7 @@ struct DevLpm6 {
     Lpm6 view{};
 };
 
-enum MapKind { MK_PLAIN = 0, MK_CT4 = 1 };
+enum MapKind { MK_PLAIN = 0, MK_CT4 = 1, MK_CT6 = 2 };
 
 struct MapObj {
     std::unique_ptr<HostMap> hm;
@@ -131,6 +131,10 @@ struct Endpoint {
     uint16_t lxc_id;
     uint32_t seclabel;
     int policy, ct4;
+    int ct6 = -1;
+    uint32_t ipv4 = 0;         // LXC_IPV4 (raw); set by cv_endpoint_config
+    uint32_t ipv6[4] = {0, 0, 0, 0};
+    uint32_t mac[2] = {0, 0}, node_mac[2] = {0, 0};
 };
 
 }  // namespace
@@ -145,13 +149,17 @@ struct cv_ctx {
     DevHash cidr4_fix, cidr6_fix, lxc4, lxc6;
     DevLpm4 cidr4_dyn, ipc4;
     DevLpm6 cidr6_dyn, ipc6;
+    DevHash lb4, lb6;
+    DevBuf revnat4, revnat6;
+    cv_node_cfg node{};
     std::vector<Endpoint> eps;
     bool eps_dirty = true;
     DevBuf eps_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
-    DevBuf gtable, gslot, gnext, gsecctx, gmeta;
+    DevBuf gtable, gslot, gnext, gsecctx, gmeta, gparent, geg;
     uint64_t gcap = 0, gn = 0;
+    bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
     DevBuf ctio;
     uint32_t next_ct_id = 1;
@@ -370,31 +378,34 @@ int compile_policy(cv_ctx *c, MapObj *mo)
     return 0;
 }
 
-// CT table sized for max_entries (+ its ICMP-related twins), filled from the host store
-int compile_ct(cv_ctx *c, MapObj *mo)
+// CT table sized for max_entries (+ its ICMP-related twins), filled from the host store;
+// v6 tables hold struct ipv6_ct_tuple keys (40 B) in Ct6Spec buckets
+template <class S>
+int compile_ct_t(cv_ctx *c, MapObj *mo, uint32_t ks, int kind)
 {
     HostMap *m = mo->hm.get();
-    if (m->ks != 14 || m->vs != 56) return -EINVAL;
-    std::vector<std::vector<uint32_t>> keys, none;
+    if (m->ks != ks || m->vs != 56) return -EINVAL;
+    std::vector<std::vector<uint32_t>> keys;
     std::vector<uint8_t> vals;
     m->for_each([&](const uint8_t *k, const uint8_t *v) {
-        uint8_t kk[16] = {0};
-        memcpy(kk, k, 14);
-        keys.push_back({rd32(kk), rd32(kk + 4), rd32(kk + 8), rd32(kk + 12)});
+        uint8_t kk[S::KW * 4] = {0};
+        memcpy(kk, k, ks);
+        std::vector<uint32_t> w(S::KW);
+        memcpy(w.data(), kk, S::KW * 4);
+        keys.push_back(w);
         size_t o = vals.size();
         vals.resize(o + 64, 0);
         memcpy(&vals[o], v, 56);
     });
     // capacity: max_entries at 60% bucket load
     const uint64_t want = std::max<uint64_t>(m->max_entries, keys.size());
-    std::vector<std::vector<uint32_t>> pad;
     DevHash &d = mo->ct;
-    uint64_t nb = buckets_for(want, Ct4Spec::SPB);
-    d.hb.assign(nb * Ct4Spec::BW, 0);
-    HashTable t{d.hb.data(), nullptr, nb - 1, 64, Ct4Spec::SPB};
-    std::vector<uint8_t> hv(nb * Ct4Spec::SPB * 64, 0);
+    uint64_t nb = buckets_for(want, S::SPB);
+    d.hb.assign(nb * S::BW, 0);
+    HashTable t{d.hb.data(), nullptr, nb - 1, 64, (uint32_t)S::SPB};
+    std::vector<uint8_t> hv(nb * S::SPB * 64, 0);
     for (size_t i = 0; i < keys.size(); ++i) {
-        int64_t s = host_upsert<Ct4Spec>(t, keys[i].data(), nullptr);
+        int64_t s = host_upsert<S>(t, keys[i].data(), nullptr);
         if (s < 0) return -E2BIG;
         memcpy(&hv[(size_t)s * 64], &vals[i * 64], 64);
     }
@@ -404,10 +415,50 @@ int compile_ct(cv_ctx *c, MapObj *mo)
     if (r) return r;
     d.hb.clear();
     d.hb.shrink_to_fit();
-    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, Ct4Spec::SPB};
-    mo->kind = MK_CT4;
+    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, (uint32_t)S::SPB};
+    mo->kind = kind;
     mo->ct_id = c->next_ct_id++;
     return 0;
+}
+
+int compile_ct(cv_ctx *c, MapObj *mo) { return compile_ct_t<Ct4Spec>(c, mo, 14, MK_CT4); }
+int compile_ct6(cv_ctx *c, MapObj *mo) { return compile_ct_t<Ct6Spec>(c, mo, 40, MK_CT6); }
+
+// cilium_lb{4,6}_services: lb{4,6}_key -> lb{4,6}_service, values inline
+int compile_lb(cv_ctx *c, HostMap *m, bool v6)
+{
+    DevHash &d = v6 ? c->lb6 : c->lb4;
+    if (!m) { d.view = HashTable{}; return 0; }
+    const uint32_t ks = v6 ? 20 : 8, vs = v6 ? 24 : 12;
+    if (m->is_lpm() || m->ks != ks || m->vs != vs) return -EINVAL;
+    std::vector<std::vector<uint32_t>> keys, vals;
+    m->for_each([&](const uint8_t *k, const uint8_t *v) {
+        std::vector<uint32_t> kw(ks / 4), vw(vs / 4);
+        memcpy(kw.data(), k, ks);
+        memcpy(vw.data(), v, vs);
+        keys.push_back(kw);
+        vals.push_back(vw);
+    });
+    return v6 ? build_hash<Lb6Spec>(d, keys, vals, 0, nullptr, nullptr)
+              : build_hash<Lb4Spec>(d, keys, vals, 0, nullptr, nullptr);
+}
+
+// cilium_lb{4,6}_reverse_nat: u16 key -> dense table [65536] {address, port | valid << 16}
+int compile_revnat(cv_ctx *c, HostMap *m, bool v6)
+{
+    DevBuf &d = v6 ? c->revnat6 : c->revnat4;
+    if (!m) { d.release(); return 0; }
+    const uint32_t vs = v6 ? 18 : 6, w = v6 ? 8 : 2;
+    if (m->is_lpm() || m->ks != 2 || m->vs != vs) return -EINVAL;
+    std::vector<uint32_t> tab((size_t)65536 * w, 0);
+    m->for_each([&](const uint8_t *k, const uint8_t *v) {
+        const uint32_t idx = rd16(k);
+        uint32_t *e = &tab[(size_t)idx * w];
+        const uint32_t na = v6 ? 4 : 1;
+        memcpy(e, v, na * 4);
+        e[na] = rd16(v + na * 4) | (1u << 16);
+    });
+    return d.upload(tab.data(), tab.size() * 4);
 }
 
 int sync_locked(cv_ctx *c)
@@ -438,7 +489,11 @@ int sync_locked(cv_ctx *c)
         case CV_ROLE_CIDR6_DYN: r = compile_cidr_dyn(c, hm, true); break;
         case CV_ROLE_LXC: r = compile_lxc(c, hm); break;
         case CV_ROLE_IPCACHE: r = compile_ipcache(c, hm); break;
-        default: r = 0; break;             // LB roles: egress path (config 5)
+        case CV_ROLE_LB4_SERVICES: r = compile_lb(c, hm, false); break;
+        case CV_ROLE_LB6_SERVICES: r = compile_lb(c, hm, true); break;
+        case CV_ROLE_LB4_REVNAT: r = compile_revnat(c, hm, false); break;
+        case CV_ROLE_LB6_REVNAT: r = compile_revnat(c, hm, true); break;
+        default: r = 0; break;
         }
         if (r) return r;
         c->role_version[role] = v;
@@ -460,9 +515,14 @@ int sync_locked(cv_ctx *c)
             EpDev d{};
             MapObj *p = get(c, e.policy);
             MapObj *t = get(c, e.ct4);
+            MapObj *t6 = get(c, e.ct6);
             if (p) d.policy = p->pol.view;
             if (t) { d.ct4 = t->ct.view; d.ct_id = t->ct_id; }
+            if (t6) d.ct6 = t6->ct.view;
             d.seclabel = e.seclabel;
+            d.ipv4 = e.ipv4;
+            for (int j = 0; j < 4; ++j) d.ipv6[j] = e.ipv6[j];
+            for (int j = 0; j < 2; ++j) { d.mac[j] = e.mac[j]; d.node_mac[j] = e.node_mac[j]; }
             ev.push_back(d);
             of[e.lxc_id] = (uint16_t)(i + 1);
         }
@@ -491,6 +551,14 @@ DpParams params(cv_ctx *c)
     p.eps = c->eps_dev.as<EpDev>();
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
+    p.lb4 = c->role[CV_ROLE_LB4_SERVICES] >= 0 ? c->lb4.view : HashTable{};
+    p.lb6 = c->role[CV_ROLE_LB6_SERVICES] >= 0 ? c->lb6.view : HashTable{};
+    p.revnat4 = c->role[CV_ROLE_LB4_REVNAT] >= 0 ? c->revnat4.as<uint32_t>() : nullptr;
+    p.revnat6 = c->role[CV_ROLE_LB6_REVNAT] >= 0 ? c->revnat6.as<uint32_t>() : nullptr;
+    p.v4_cluster_mask = c->node.ipv4_cluster_mask;
+    p.v4_cluster_range = c->node.ipv4_cluster_range;
+    p.v4_loopback = c->node.ipv4_loopback;
+    memcpy(p.router6, c->node.router_ip6, 16);
     const char *ab = getenv("CV_ABLATE");
     p.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
     return p;
@@ -515,7 +583,10 @@ BatchDev chunk(const cv_batch *b, uint32_t off, uint32_t n)
 OutDev to_dev(const cv_out *o)
 {
     OutDev d{};
-    if (o) { d.xdp = o->xdp; d.ret = o->ret; d.identity = o->identity; d.ct = o->ct; d.proxy = o->proxy; d.nl = o->nl; d.nu = o->nu; }
+    if (o) {
+        d.xdp = o->xdp; d.ret = o->ret; d.identity = o->identity; d.ct = o->ct; d.proxy = o->proxy;
+        d.nl = o->nl; d.nu = o->nu; d.reason = o->reason;
+    }
     return d;
 }
 
@@ -529,47 +600,94 @@ OutDev chunk(const cv_out *o, uint32_t off)
     if (d.proxy) d.proxy += off;
     if (d.nl) d.nl += off;
     if (d.nu) d.nu += off;
+    if (d.reason) d.reason += off;
     return d;
+}
+
+// per-launch group scratch: a node table of >= 2 (ingress) / 8 (egress: up to five
+// address-pair nodes per packet) slots per packet, so probing always terminates
+int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
+{
+    const uint64_t per = egress ? 8 : 2;
+    if (cmax <= c->gn && (!egress || c->g_egress) && c->gcap >= per * cmax) return 0;
+    cmax = std::max<uint32_t>(cmax, (uint32_t)c->gn);
+    uint64_t cap = 1024;
+    while (cap < per * cmax || cap < c->gcap) cap <<= 1;
+    (void)hipDeviceSynchronize();
+    if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
+        c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4))
+        return -ENOMEM;
+    (void)hipMemset(c->gtable.p, 0, cap * 16);
+    if (egress || c->g_egress) {
+        if (c->gparent.alloc(cap * 8) || c->geg.alloc((size_t)cmax * EG_WORDS * 4)) return -ENOMEM;
+        (void)hipMemset(c->gparent.p, 0, cap * 8);
+        c->g_egress = true;
+    }
+    c->gcap = cap;
+    c->gn = cmax;
+    c->epoch = 0;
+    return 0;
+}
+
+// the scratch view for the next launch, which uses `epochs` fresh epochs
+GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
+{
+    if (c->epoch + epochs < c->epoch || c->epoch == 0) {   // start, or 2^32 launches: clear stale tags
+        (void)hipMemsetAsync(c->gtable.p, 0, c->gcap * 16, stream);
+        if (c->gparent.p) (void)hipMemsetAsync(c->gparent.p, 0, c->gcap * 8, stream);
+        c->epoch = 0;
+    }
+    GroupScratch gs{c->gtable.as<unsigned long long>(), (uint32_t)(c->gcap - 1), c->epoch + 1,
+                    c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(),
+                    c->gmeta.as<uint32_t>(), c->gparent.as<unsigned long long>(), c->geg.as<uint32_t>()};
+    c->epoch += epochs;
+    return gs;
 }
 
 int ct_io(cv_ctx *c, MapObj *mo, int op, const uint8_t *key, const uint8_t *val, uint8_t *val_out, uint64_t fl)
 {
+    const bool v6 = mo->kind == MK_CT6;
+    const uint32_t ks = v6 ? 40 : 14, kw = v6 ? 10 : 4;
     if (!c->ctio.p && c->ctio.alloc(32 * 4)) return -ENOMEM;
     uint32_t io[32] = {0};
-    uint8_t kk[16] = {0};
-    memcpy(kk, key, 14);
-    memcpy(io, kk, 16);
-    if (val) memcpy(io + 4, val, 56);
+    uint8_t kk[40] = {0};
+    memcpy(kk, key, ks);
+    memcpy(io, kk, kw * 4);
+    if (val) memcpy(io + kw, val, 56);
     if (hipMemcpy(c->ctio.p, io, sizeof(io), hipMemcpyHostToDevice) != hipSuccess) return -EIO;
-    if (launch_ct_op(mo->ct.view, op, fl, c->ctio.as<uint32_t>(), nullptr)) return -EIO;
+    if (launch_ct_op(mo->ct.view, v6, op, fl, c->ctio.as<uint32_t>(), nullptr)) return -EIO;
     if (hipMemcpy(io, c->ctio.p, sizeof(io), hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
-    int rc = (int)io[20];
-    if (!rc && val_out) memcpy(val_out, io + 4, 56);
+    int rc = (int)io[kw + 16];
+    if (!rc && val_out) memcpy(val_out, io + kw, 56);
     return rc;
 }
 
 // all (key, value) rows of a device CT table
 int ct_dump(cv_ctx *c, MapObj *mo, std::vector<uint8_t> &keys, std::vector<uint8_t> &vals)
 {
-    const uint64_t slots = mo->ct.nb * Ct4Spec::SPB;
+    (void)c;
+    const bool v6 = mo->kind == MK_CT6;
+    const uint32_t ks = v6 ? 40 : 14, kw = v6 ? 10 : 4;
+    const uint64_t slots = mo->ct.nb * (v6 ? Ct6Spec::SPB : Ct4Spec::SPB);
     const uint32_t max = (uint32_t)std::min<uint64_t>(slots, 0xFFFFFFF0ull);
     DevBuf dk, dv, dc;
-    if (dk.alloc((size_t)max * 16) || dv.alloc((size_t)max * 64) || dc.alloc(4)) return -ENOMEM;
+    if (dk.alloc((size_t)max * kw * 4) || dv.alloc((size_t)max * 64) || dc.alloc(4)) return -ENOMEM;
     (void)hipMemset(dc.p, 0, 4);
-    if (launch_ct_scan(mo->ct.view, mo->ct.nb, dk.as<uint32_t>(), dv.as<uint32_t>(), dc.as<uint32_t>(), max, nullptr))
+    if (launch_ct_scan(mo->ct.view, v6, mo->ct.nb, dk.as<uint32_t>(), dv.as<uint32_t>(), dc.as<uint32_t>(), max,
+                       nullptr))
         return -EIO;
     uint32_t n = 0;
     (void)hipMemcpy(&n, dc.p, 4, hipMemcpyDeviceToHost);
     n = std::min(n, max);
-    std::vector<uint8_t> k16((size_t)n * 16), v64((size_t)n * 64);
+    std::vector<uint8_t> kraw((size_t)n * kw * 4), v64((size_t)n * 64);
     if (n) {
-        (void)hipMemcpy(k16.data(), dk.p, k16.size(), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(kraw.data(), dk.p, kraw.size(), hipMemcpyDeviceToHost);
         (void)hipMemcpy(v64.data(), dv.p, v64.size(), hipMemcpyDeviceToHost);
     }
-    keys.resize((size_t)n * 14);
+    keys.resize((size_t)n * ks);
     vals.resize((size_t)n * 56);
     for (uint32_t i = 0; i < n; ++i) {
-        memcpy(&keys[(size_t)i * 14], &k16[(size_t)i * 16], 14);
+        memcpy(&keys[(size_t)i * ks], &kraw[(size_t)i * kw * 4], ks);
         memcpy(&vals[(size_t)i * 56], &v64[(size_t)i * 64], 56);
     }
     return (int)n;
@@ -663,7 +781,7 @@ int cv_map_close(cv_ctx *c, int h)
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
     for (int r = 0; r < CV_NUM_ROLES; ++r) if (c->role[r] == h) return -EBUSY;
-    for (auto &e : c->eps) if (e.policy == h || e.ct4 == h) return -EBUSY;
+    for (auto &e : c->eps) if (e.policy == h || e.ct4 == h || e.ct6 == h) return -EBUSY;
     if (c->device >= 0) (void)hipDeviceSynchronize();
     c->maps[h].reset(new MapObj());
     c->maps[h]->hm.reset(new HostMap(CV_MAP_HASH, 1, 1, 1, 0));
@@ -676,7 +794,7 @@ int cv_map_update(cv_ctx *c, int h, const void *key, const void *val, uint64_t f
     std::lock_guard<std::mutex> g(c->mu);
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
-    if (m->kind == MK_CT4) {
+    if (m->kind != MK_PLAIN) {
         if (set_device(c)) return -ENODEV;
         return ct_io(c, m, 1, (const uint8_t *)key, (const uint8_t *)val, nullptr, fl);
     }
@@ -709,7 +827,7 @@ int cv_map_lookup(cv_ctx *c, int h, const void *key, void *val)
     std::lock_guard<std::mutex> g(c->mu);
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
-    if (m->kind == MK_CT4) {
+    if (m->kind != MK_PLAIN) {
         if (set_device(c)) return -ENODEV;
         return ct_io(c, m, 0, (const uint8_t *)key, nullptr, (uint8_t *)val, 0);
     }
@@ -726,7 +844,7 @@ int cv_map_delete(cv_ctx *c, int h, const void *key)
     std::lock_guard<std::mutex> g(c->mu);
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
-    if (m->kind == MK_CT4) {
+    if (m->kind != MK_PLAIN) {
         if (set_device(c)) return -ENODEV;
         return ct_io(c, m, 2, (const uint8_t *)key, nullptr, nullptr, 0);
     }
@@ -741,18 +859,19 @@ int cv_map_get_next_key(cv_ctx *c, int h, const void *key, void *next)
     std::lock_guard<std::mutex> g(c->mu);
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
-    if (m->kind == MK_CT4) {
+    if (m->kind != MK_PLAIN) {
         std::vector<uint8_t> ks, vs;
         if (set_device(c)) return -ENODEV;
         int n = ct_dump(c, m, ks, vs);
         if (n < 0) return n;
+        const uint32_t ksz = m->hm->ks;
         int at = 0;
         if (key) {
             for (int i = 0; i < n; ++i)
-                if (!memcmp(&ks[(size_t)i * 14], key, 14)) { at = i + 1; break; }
+                if (!memcmp(&ks[(size_t)i * ksz], key, ksz)) { at = i + 1; break; }
         }
         if (at >= n) return -ENOENT;
-        memcpy(next, &ks[(size_t)at * 14], 14);
+        memcpy(next, &ks[(size_t)at * ksz], ksz);
         return 0;
     }
     return m->hm->next_key((const uint8_t *)key, (uint8_t *)next);
@@ -764,7 +883,7 @@ int cv_map_count(cv_ctx *c, int h, uint32_t *count)
     std::lock_guard<std::mutex> g(c->mu);
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
-    if (m->kind == MK_CT4) {
+    if (m->kind != MK_PLAIN) {
         std::vector<uint8_t> ks, vs;
         if (set_device(c)) return -ENODEV;
         int n = ct_dump(c, m, ks, vs);
@@ -783,7 +902,7 @@ int cv_map_dump(cv_ctx *c, int h, void *keys, void *vals, uint32_t max)
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
     const uint32_t ks = m->hm->ks, vs = m->hm->vs;
-    if (m->kind == MK_CT4) {
+    if (m->kind != MK_PLAIN) {
         std::vector<uint8_t> kb, vb;
         if (set_device(c)) return -ENODEV;
         int n = ct_dump(c, m, kb, vb);
@@ -824,6 +943,10 @@ int cv_bind(cv_ctx *c, int role, int h)
         case CV_ROLE_CIDR6_DYN: if (!lpm || hm->ks != 20) return -EINVAL; break;
         case CV_ROLE_LXC: if (lpm || hm->ks != 20 || hm->vs != 48) return -EINVAL; break;
         case CV_ROLE_IPCACHE: if (!lpm || hm->ks != 24 || hm->vs != 8) return -EINVAL; break;
+        case CV_ROLE_LB4_SERVICES: if (lpm || hm->ks != 8 || hm->vs != 12) return -EINVAL; break;
+        case CV_ROLE_LB6_SERVICES: if (lpm || hm->ks != 20 || hm->vs != 24) return -EINVAL; break;
+        case CV_ROLE_LB4_REVNAT: if (lpm || hm->ks != 2 || hm->vs != 6) return -EINVAL; break;
+        case CV_ROLE_LB6_REVNAT: if (lpm || hm->ks != 2 || hm->vs != 18) return -EINVAL; break;
         default: break;
         }
     }
@@ -851,6 +974,38 @@ int cv_endpoint_add(cv_ctx *c, uint16_t lxc_id, uint32_t seclabel, int policy_ma
     c->eps.push_back(Endpoint{lxc_id, seclabel, policy_map, ct4_map});
     c->eps_dirty = true;
     return (int)c->eps.size() - 1;
+}
+
+int cv_endpoint_config(cv_ctx *c, int ep, const cv_endpoint_cfg *cfg)
+{
+    if (!c || !cfg) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (ep < 0 || (size_t)ep >= c->eps.size()) return -EINVAL;
+    MapObj *t6 = cfg->ct6_map >= 0 ? get(c, cfg->ct6_map) : nullptr;
+    if (cfg->ct6_map >= 0 && !t6) return -EBADF;
+    if (t6 && (t6->hm->ks != 40 || t6->hm->vs != 56 || t6->hm->is_lpm())) return -EINVAL;
+    if (t6 && t6->kind != MK_CT6) {
+        if (t6->kind != MK_PLAIN) return -EINVAL;
+        if (set_device(c)) return -ENODEV;
+        int r = compile_ct6(c, t6);
+        if (r) return r;
+    }
+    Endpoint &e = c->eps[ep];
+    e.ct6 = cfg->ct6_map;
+    e.ipv4 = cfg->ipv4;
+    memcpy(e.ipv6, cfg->ipv6, 16);
+    e.mac[0] = rd32(cfg->mac); e.mac[1] = rd16(cfg->mac + 4);
+    e.node_mac[0] = rd32(cfg->node_mac); e.node_mac[1] = rd16(cfg->node_mac + 4);
+    c->eps_dirty = true;
+    return 0;
+}
+
+int cv_node_config(cv_ctx *c, const cv_node_cfg *cfg)
+{
+    if (!c || !cfg) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->node = *cfg;
+    return 0;
 }
 
 int cv_sync(cv_ctx *c)
@@ -897,18 +1052,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
     if ((r = set_device(c)) || (r = sync_locked(c))) return r;
     const uint32_t cmax = std::min(b->n, c->chunk);
-    if (cmax > c->gn) {
-        uint64_t cap = 1024;
-        while (cap < 2ull * cmax) cap <<= 1;
-        (void)hipDeviceSynchronize();
-        if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
-            c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4))
-            return -ENOMEM;
-        (void)hipMemset(c->gtable.p, 0, cap * 16);
-        c->gcap = cap;
-        c->gn = cmax;
-        c->epoch = 0;
-    }
+    if ((r = ensure_groups(c, cmax, false))) return r;
     std::set<const void *> seen;
     std::vector<HashTable> pols;
     for (auto &e : c->eps) {
@@ -918,15 +1062,40 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     const DpParams p = params(c);
     for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
         const uint32_t n = std::min(c->chunk, b->n - off);
-        if (++c->epoch == 0) {                  // 2^32 launches: clear stale group tags
-            (void)hipMemsetAsync(c->gtable.p, 0, c->gcap * 16, (hipStream_t)stream);
-            c->epoch = 1;
-        }
-        GroupScratch gs{c->gtable.as<unsigned long long>(), (uint32_t)(c->gcap - 1), c->epoch,
-                        c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(),
-                        c->gmeta.as<uint32_t>()};
+        GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
         if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off), gs,
                                        (hipStream_t)stream)))
+            return r;
+        for (const HashTable &t : pols)
+            if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
+    }
+    return 0;
+}
+
+int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash,
+                  uint32_t now, cv_out *o, void *stream)
+{
+    if (!c) return -EINVAL;
+    int r = check_batch(b);
+    if (r) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
+    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    const uint32_t cmax = std::min(b->n, c->chunk);
+    if ((r = ensure_groups(c, cmax, true))) return r;
+    std::set<const void *> seen;
+    std::vector<HashTable> pols;
+    for (auto &e : c->eps) {
+        const HashTable &t = get(c, e.policy)->pol.view;
+        if (seen.insert(t.vals).second) pols.push_back(t);
+    }
+    const DpParams p = params(c);
+    for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
+        const uint32_t n = std::min(c->chunk, b->n - off);
+        GroupScratch gs = next_groups(c, 2, (hipStream_t)stream);
+        if ((r = launch_lxc_egress(p, chunk(b, off, n), src_ep ? src_ep + off : nullptr, ep0,
+                                   flow_hash ? flow_hash + off : nullptr, now, chunk(o, off), gs,
+                                   (hipStream_t)stream)))
             return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;

@@ -1,0 +1,1023 @@
+// cv_dev.hpp — device-side building blocks shared by the gfx950 kernels: frame
+// records in registers, the per-packet "skb" view after rewrites, map probes,
+// policy, conntrack (v4 and v6), reverse NAT, cilium_metrics aggregation and the
+// address-pair grouping that gives a batch sequential (one-CPU) semantics.
+//
+// Every function restates a function of the reference (Taeung/cilium v1.1.90) and
+// cites it; the CPU restatement in oracle/cv_oracle.c follows the same lines.
+#pragma once
+#include <errno.h>
+#include <hip/hip_runtime.h>
+
+#include "cv_dp.hpp"
+
+namespace cv {
+
+constexpr int BLOCK = 256;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// ------------------------------------------------------------------ records
+// The first 4*NW bytes of a frame record live in NW VGPRs (loaded with 16-B
+// non-temporal loads, so streamed records do not evict tables from L2 / MALL);
+// bytes at runtime offsets outside the common layout come from HBM.
+template <int NW>
+struct RecT {
+    uint32_t w[NW];
+    const uint8_t *base;
+    uint32_t len, stride;
+};
+using Rec = RecT<16>;    // IPv4: Ethernet + IPv4 + L4 in 64 B
+using Rec6 = RecT<32>;   // IPv6: Ethernet + IPv6 + L4 in 128 B
+
+template <int NW>
+__device__ __forceinline__ void rec_load(RecT<NW> &r, const BatchDev &b, uint32_t i, int nvec)
+{
+    r.base = b.frames + (size_t)i * b.stride;
+    r.len = b.len[i];
+    r.stride = b.stride;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(r.base);
+#pragma unroll
+    for (int k = 0; k < NW / 4; ++k) {
+        if (k < nvec) {
+            u32x4 v = __builtin_nontemporal_load(q + k);
+            r.w[4 * k] = v.x; r.w[4 * k + 1] = v.y; r.w[4 * k + 2] = v.z; r.w[4 * k + 3] = v.w;
+        } else {
+            r.w[4 * k] = r.w[4 * k + 1] = r.w[4 * k + 2] = r.w[4 * k + 3] = 0;
+        }
+    }
+}
+
+template <int O, int NW>
+__device__ __forceinline__ uint32_t rec_u8c(const RecT<NW> &r)
+{
+    static_assert(O >= 0 && O < 4 * NW, "register window");
+    return (r.w[O >> 2] >> (8 * (O & 3))) & 0xFFu;
+}
+
+template <int O, int NW>
+__device__ __forceinline__ uint32_t rec_raw16c(const RecT<NW> &r)   // raw LE load of 2 network-order bytes
+{
+    static_assert(O >= 0 && O + 2 <= 4 * NW, "register window");
+    if constexpr ((O & 3) == 3) return rec_u8c<O>(r) | (rec_u8c<O + 1>(r) << 8);
+    else return (r.w[O >> 2] >> (8 * (O & 3))) & 0xFFFFu;
+}
+
+template <int O, int NW>
+__device__ __forceinline__ uint32_t rec_raw32c(const RecT<NW> &r)
+{
+    static_assert(O >= 0 && O + 4 <= 4 * NW, "register window");
+    if constexpr ((O & 3) == 0) return r.w[O >> 2];
+    else return (r.w[O >> 2] >> (8 * (O & 3))) | (r.w[(O >> 2) + 1] << (32 - 8 * (O & 3)));
+}
+
+// byte K of the L4 header at runtime offset `off`: registers when off == FAST
+template <int FAST, int K, int NW>
+__device__ __forceinline__ uint32_t l4_u8(const RecT<NW> &r, int off)
+{
+    if (off == FAST) return rec_u8c<FAST + K>(r);
+    return r.base[off + K];
+}
+
+template <int FAST, int K, int NW>
+__device__ __forceinline__ uint32_t l4_raw16(const RecT<NW> &r, int off)
+{
+    if (off == FAST) return rec_raw16c<FAST + K>(r);
+    return r.base[off + K] | ((uint32_t)r.base[off + K + 1] << 8);
+}
+
+// skb_load_bytes / skb_store_bytes bound: 0 ok, 1 beyond skb->len (the helper
+// fails), E_TRUNC inside len but beyond the record
+template <int NW>
+__device__ __forceinline__ int rec_chk(const RecT<NW> &r, int off, int n)
+{
+    if (off < 0 || (uint32_t)(off + n) > r.len) return 1;
+    if ((uint32_t)(off + n) > r.stride) return E_TRUNC;
+    return 0;
+}
+
+// The L4 bytes the programs read, with the outcome of each load the reference
+// does: [off,1) ICMP type, [off+12,2) TCP flags, [off,4) ports, [off,2) sport,
+// [off+2,2) dport.  Rewrites (lb xlate, rev-NAT) update p0 / p2 in place, as the
+// reference's skb_store_bytes would.
+struct L4Hdr {
+    int8_t c1, c14, c4, c2a, c2b;
+    uint32_t type, tflags;
+    uint32_t p0, p2;          // raw be16 of bytes 0-1 and 2-3
+};
+
+template <int FAST, int NW>
+__device__ __forceinline__ L4Hdr l4_read(const RecT<NW> &r, int off)
+{
+    L4Hdr h;
+    h.c1 = (int8_t)rec_chk(r, off, 1);
+    h.c14 = (int8_t)rec_chk(r, off + 12, 2);
+    h.c4 = (int8_t)rec_chk(r, off, 4);
+    h.c2a = (int8_t)rec_chk(r, off, 2);
+    h.c2b = (int8_t)rec_chk(r, off + 2, 2);
+    h.type = h.c1 == 0 ? l4_u8<FAST, 0>(r, off) : 0u;
+    h.tflags = h.c14 == 0 ? l4_u8<FAST, 13>(r, off) : 0u;
+    h.p0 = h.c2a == 0 ? l4_raw16<FAST, 0>(r, off) : 0u;
+    h.p2 = h.c2b == 0 ? l4_raw16<FAST, 2>(r, off) : 0u;
+    return h;
+}
+
+__device__ __forceinline__ int chk_err(int c, int code) { return c == E_TRUNC ? E_TRUNC : code; }
+__device__ __forceinline__ bool is_err(int x) { return x < 0 || x == TC_ACT_SHOT; }   // common.h:231
+
+// ------------------------------------------------------------------ metrics
+// cilium_metrics (metrics.h:43-58): drops go through a per-workgroup LDS table
+// [256 reasons][2 dirs]{count, bytes}; forwards (reason 0, one per delivered packet)
+// accumulate in the lane's registers and are wave-reduced once per kernel.
+struct LdsMetrics {
+    unsigned long long c[256 * 2 * 2];
+};
+
+struct Fwd {
+    uint32_t c[2];
+    unsigned long long b[2];
+};
+
+struct Met {
+    LdsMetrics *lm;
+    Fwd f;
+    __device__ void drop(int32_t code, uint32_t len, int dir)          // send_drop_notify
+    {
+        const uint32_t r = (uint8_t)(-code);
+        const int k = (r * 2 + (dir - 1)) * 2;
+        atomicAdd(&lm->c[k], 1ull);
+        atomicAdd(&lm->c[k + 1], (unsigned long long)len);
+    }
+    __device__ void fwd(uint32_t len, int dir)                         // update_metrics(.., REASON_FORWARDED)
+    {
+        f.c[dir - 1] += 1;
+        f.b[dir - 1] += len;
+    }
+};
+
+__device__ __forceinline__ void met_init(Met &m, LdsMetrics &lm)
+{
+    for (int i = threadIdx.x; i < 256 * 4; i += blockDim.x) lm.c[i] = 0;
+    m.lm = &lm;
+    m.f.c[0] = m.f.c[1] = 0;
+    m.f.b[0] = m.f.b[1] = 0;
+    __syncthreads();
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ void met_flush(Met &m, unsigned long long *g)
+{
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        const unsigned long long c = wave_sum(m.f.c[d]), b = wave_sum(m.f.b[d]);
+        if ((threadIdx.x & 63) == 0 && c) {
+            atomicAdd(&m.lm->c[(0 * 2 + d) * 2], c);
+            atomicAdd(&m.lm->c[(0 * 2 + d) * 2 + 1], b);
+        }
+    }
+    __syncthreads();
+    if (!g) return;
+    for (int i = threadIdx.x; i < 256 * 2; i += blockDim.x) {
+        const int r = i >> 1, d = i & 1;
+        const unsigned long long c = m.lm->c[i * 2];
+        if (c) {
+            atomicAdd(&g[(r * 4 + d + 1) * 2], c);
+            atomicAdd(&g[(r * 4 + d + 1) * 2 + 1], m.lm->c[i * 2 + 1]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ lookups
+struct Acct { uint32_t nl, nu; };
+
+// lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
+__device__ __forceinline__ bool lxc4_find(const DpParams &p, uint32_t daddr_raw, uint32_t &ival, Acct &a)
+{
+    if (!p.lxc4.buckets) return false;
+    a.nl++;
+    return dev_find<LxcV4Spec>(p.lxc4, &daddr_raw, &ival) >= 0;
+}
+
+// lookup_ip6_endpoint (eps.h:26-35)
+__device__ __forceinline__ bool lxc6_find(const DpParams &p, const uint32_t *daddr, uint32_t &ival, Acct &a)
+{
+    if (!p.lxc6.buckets) return false;
+    a.nl++;
+    return dev_find<LxcV6Spec>(p.lxc6, daddr, &ival) >= 0;
+}
+
+// ipcache_lookup4 (eps.h:309-319) -> remote_endpoint_info.sec_label (0 = none)
+__device__ __forceinline__ uint32_t ipcache4(const DpParams &p, uint32_t addr_raw, Acct &a)
+{
+    if (!p.ipc4.l1) return 0;
+    a.nl++;
+    return lpm4_lookup(p.ipc4, bswap32(addr_raw));
+}
+
+// ipcache_lookup6 (eps.h:295-305) at /128
+__device__ __forceinline__ uint32_t ipcache6(const DpParams &p, const uint32_t *addr, Acct &a)
+{
+    if (!p.ipc6.h.buckets) return 0;
+    a.nl++;
+    return lpm6_lookup(p.ipc6, addr);
+}
+
+// handle_identity_from_host (bpf_netdev.c:128-153)
+__device__ __forceinline__ uint32_t identity_from_mark(uint32_t mark, bool &skip_proxy)
+{
+    const uint32_t magic = mark & 0xF00u;
+    skip_proxy = false;
+    if (magic == 0xA00u) { skip_proxy = true; return ((mark & 0xFFu) << 16) | (mark >> 16); }
+    if (magic == 0xB00u) return ((mark & 0xFFu) << 16) | (mark >> 16);
+    if (magic == 0xC00u) return HOST_ID;
+    return WORLD_ID;
+}
+
+// A policy counter update held back by the lane: the atomic is issued after the
+// lane's last dependent lookup, so in-order vmcnt never makes a lookup wait for it.
+struct Hit {
+    unsigned long long *p;
+    unsigned long long inc;
+};
+
+__device__ __forceinline__ void hit_flush(const Hit &h)
+{
+    if (h.p) atomicAdd(h.p, h.inc);
+}
+
+// __policy_can_access (policy.h:217-285); cb[CB_POLICY] is 0 on these paths.  With
+// `defer` the counter update is returned instead of issued.
+__device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
+                                             uint32_t dport_raw, uint32_t proto, int dir, Acct &a,
+                                             Hit *defer = nullptr)
+{
+    if (flags & F_DROP_ALL) return DROP_POLICY;
+    const uint32_t eg = dir ? 0u : 1u;                           // policy_key.egress = !dir
+    uint32_t k[2];
+    int64_t s = -1;
+    uint32_t px[1] = {0};
+    bool l4 = false;
+    if (flags & F_HAVE_L4_POLICY) {
+        k[0] = identity; k[1] = (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24);
+        a.nl++;
+        s = dev_find<PolicySpec>(pol, k, px);
+        l4 = s >= 0;
+    }
+    if (s < 0) {
+        k[0] = identity; k[1] = eg << 24;
+        a.nl++;
+        s = dev_find<PolicySpec>(pol, k, px);
+    }
+    if (s < 0 && (flags & F_HAVE_L4_POLICY)) {
+        k[0] = 0; k[1] = (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24);
+        a.nl++;
+        s = dev_find<PolicySpec>(pol, k, px);
+        l4 = s >= 0;
+    }
+    if (s < 0) return DROP_POLICY;
+    a.nu++;
+    uint8_t *v = pol.vals + (size_t)s * pol.vstride;
+    if (!(flags & (AB_NO_POLICY_ATOMICS << 16))) {
+        // __sync_fetch_and_add(packets, 1) and (bytes, len) as ONE 64-bit atomic on the
+        // slot's delta word {count:25 | bytes:39} (launches are chunked to <= 2^24
+        // packets and folded after each chunk, so neither field can overflow)
+        if (len < (1u << 15)) {
+            unsigned long long *d = pol.aux + s;
+            const unsigned long long inc = (1ull << 39) | len;
+            if (defer) *defer = Hit{d, inc};
+            else atomicAdd(d, inc);
+        } else {
+            atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
+        }
+    }
+    return l4 ? (int)px[0] : TC_ACT_OK;
+}
+
+// policy_can_access_ingress (policy.h:305-329)
+__device__ __forceinline__ int policy_ingress(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t src,
+                                              uint32_t dport_raw, uint32_t proto, Acct &a, Hit *defer = nullptr)
+{
+    if (!(flags & F_POLICY_INGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
+    if (flags & F_DROP_ALL) return DROP_POLICY;
+    int r = policy_access(pol, flags, len, src, dport_raw, proto, CT_INGRESS, a, defer);
+    return r >= TC_ACT_OK ? r : DROP_POLICY;
+}
+
+// policy_can_egress (policy.h:181-200), POLICY_EGRESS && LXC_ID
+__device__ __forceinline__ int policy_egress(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
+                                             uint32_t dport_raw, uint32_t proto, Acct &a)
+{
+    if (!(flags & F_POLICY_EGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
+    if (flags & F_DROP_ALL) return DROP_POLICY;
+    int r = policy_access(pol, flags, len, identity, dport_raw, proto, CT_EGRESS, a);
+    return r >= 0 ? r : DROP_POLICY;
+}
+
+__device__ __forceinline__ void store_out(const OutDev &o, uint32_t i, const Acct &a)
+{
+    if (o.nl) o.nl[i] = (uint8_t)a.nl;
+    if (o.nu) o.nu[i] = (uint8_t)a.nu;
+}
+
+// ------------------------------------------------------------------ config 1
+// check_filters / check_v4 / check_v6 (bpf_xdp.c:88-178)
+template <int NW>
+__device__ __forceinline__ uint8_t xdp_verdict(const DpParams &p, const RecT<NW> &r, Acct &a)
+{
+    if (r.len < 14) return XDP_DROP;
+    const uint32_t proto = rec_raw16c<12>(r);
+    if (proto == 0x0008u) {
+        if (r.len < 34) return XDP_DROP;
+        uint32_t saddr = rec_raw32c<26>(r), daddr = rec_raw32c<30>(r);
+        if (p.cidr4_fix.buckets) {                          // CIDR4_FILTER
+            if (p.cidr4_dyn.l1) {                           // CIDR4_LPM_PREFILTER
+                a.nl++;
+                if (lpm4_lookup(p.cidr4_dyn, bswap32(saddr))) return XDP_DROP;
+            }
+            a.nl++;
+            if (dev_find<Cidr4Spec>(p.cidr4_fix, &saddr, nullptr) >= 0) return XDP_DROP;
+        }
+        uint32_t iv;
+        return lxc4_find(p, daddr, iv, a) ? XDP_PASS : XDP_DROP;
+    }
+    if (proto == 0xDD86u) {
+        if (r.len < 54) return XDP_DROP;
+        uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
+        uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
+        if (p.cidr6_fix.buckets) {
+            if (p.cidr6_dyn.h.buckets) {
+                a.nl++;
+                if (lpm6_lookup(p.cidr6_dyn, sa)) return XDP_DROP;
+            }
+            a.nl++;
+            if (dev_find<Cidr6Spec>(p.cidr6_fix, sa, nullptr) >= 0) return XDP_DROP;
+        }
+        if (!p.lxc6.buckets) return XDP_DROP;
+        a.nl++;
+        uint32_t iv;
+        return dev_find<LxcV6Spec>(p.lxc6, da, &iv) >= 0 ? XDP_PASS : XDP_DROP;
+    }
+    return XDP_PASS;
+}
+
+// ------------------------------------------------------------------ conntrack
+// struct ct_entry (common.h:380-406) held in 16 words: counters w0-7, lifetime w8,
+// bits | rev_nat_index << 16 in w9, slave | tx_flags_seen << 16 | rx_flags_seen << 24
+// in w10, src_sec_id w11, last_tx_report w12, last_rx_report w13
+struct CtE {
+    uint32_t w[16];
+    __device__ uint16_t bits() const { return (uint16_t)(w[9] & 0xFFFFu); }
+    __device__ void set_bits(uint16_t b) { w[9] = (w[9] & 0xFFFF0000u) | b; }
+    __device__ void add64(int k, uint64_t v)
+    {
+        uint64_t x = ((uint64_t)w[k + 1] << 32 | w[k]) + v;
+        w[k] = (uint32_t)x; w[k + 1] = (uint32_t)(x >> 32);
+    }
+};
+
+// struct ct_state (common.h:452-461)
+struct CtState {
+    uint32_t rev_nat, loopback, slave;
+    uint32_t addr, svc_addr, src_sec_id;
+};
+
+__device__ __forceinline__ void ct_load(const HashTable &t, int64_t slot, CtE &e)
+{
+    const uint4 *q = reinterpret_cast<const uint4 *>(t.vals + (size_t)slot * t.vstride);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint4 v = q[k];
+        e.w[4 * k] = v.x; e.w[4 * k + 1] = v.y; e.w[4 * k + 2] = v.z; e.w[4 * k + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void ct_store(const HashTable &t, int64_t slot, const CtE &e)
+{
+    uint4 *q = reinterpret_cast<uint4 *>(t.vals + (size_t)slot * t.vstride);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = make_uint4(e.w[4 * k], e.w[4 * k + 1], e.w[4 * k + 2], e.w[4 * k + 3]);
+}
+
+// __ct_update_timeout (conntrack.h:103-161)
+__device__ __forceinline__ void ct_timeout_raw(CtE &e, uint32_t lifetime, int dir, uint32_t seen, uint32_t now)
+{
+    e.w[8] = now + lifetime;
+    const int fsh = dir == CT_INGRESS ? 24 : 16;                // rx_flags_seen @43, tx_flags_seen @42
+    const int li = dir == CT_INGRESS ? 13 : 12;                 // last_rx_report @52, last_tx_report @48
+    const uint32_t acc = (e.w[10] >> fsh) & 0xFFu;
+    seen = (seen | acc) & 0xFFu;
+    if (e.w[li] + CT_REPORT_INTERVAL < now || acc != seen) {
+        e.w[li] = now;
+        e.w[10] = (e.w[10] & ~(0xFFu << fsh)) | (seen << fsh);
+    }
+}
+
+// ct_update_timeout (conntrack.h:169-186)
+__device__ __forceinline__ void ct_timeout(CtE &e, bool tcp, int dir, uint32_t seen, uint32_t now)
+{
+    uint32_t lifetime = CT_LIFETIME_NONTCP;
+    if (tcp) {
+        if (!(seen & TCPF_SYN)) e.set_bits(e.bits() | CTB_SEEN_NON_SYN);
+        lifetime = (e.bits() & CTB_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+    }
+    ct_timeout_raw(e, lifetime, dir, seen, now);
+}
+
+__device__ __forceinline__ bool ct_alive(const CtE &e)
+{
+    return !(e.bits() & CTB_RX_CLOSING) || !(e.bits() & CTB_TX_CLOSING);
+}
+
+struct Tuple4 {                 // struct ipv4_ct_tuple packed into 4 words (+2 zero bytes)
+    uint32_t daddr, saddr;
+    uint32_t dport, sport;      // raw be16 values
+    uint32_t nexthdr, flags;
+    __device__ void key(uint32_t *k) const
+    {
+        k[0] = daddr; k[1] = saddr; k[2] = (dport & 0xFFFFu) | (sport << 16); k[3] = nexthdr | (flags << 8);
+    }
+    __device__ void reverse()   // ipv4_ct_tuple_reverse (conntrack.h:414-431)
+    {
+        uint32_t x = saddr; saddr = daddr; daddr = x;
+        x = sport; sport = dport; dport = x;
+        flags ^= TUPLE_F_IN;
+    }
+    static constexpr int KW = 4;
+    using Spec = Ct4Spec;
+};
+
+struct Tuple6 {                 // struct ipv6_ct_tuple (common.h:338-346), 10 words
+    uint32_t daddr[4], saddr[4];
+    uint32_t dport, sport;
+    uint32_t nexthdr, flags;
+    __device__ void key(uint32_t *k) const
+    {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { k[j] = daddr[j]; k[4 + j] = saddr[j]; }
+        k[8] = (dport & 0xFFFFu) | (sport << 16);
+        k[9] = nexthdr | (flags << 8);
+    }
+    __device__ void reverse()   // ipv6_ct_tuple_reverse (conntrack.h:264-284)
+    {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { uint32_t x = saddr[j]; saddr[j] = daddr[j]; daddr[j] = x; }
+        uint32_t x = sport; sport = dport; dport = x;
+        flags ^= TUPLE_F_IN;
+    }
+    static constexpr int KW = 10;
+    using Spec = Ct6Spec;
+};
+
+enum { ACTION_UNSPEC = 0, ACTION_CREATE = 1, ACTION_CLOSE = 2 };
+
+// __ct_lookup (conntrack.h:199-263) -> CT_NEW / CT_ESTABLISHED; *slot = hit slot;
+// a hit fills ct_state's rev_nat_index / loopback / slave
+template <class T>
+__device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, int action, int dir, bool tcp,
+                                             uint32_t seen, uint32_t len, uint32_t now, uint32_t flags, int64_t &slot,
+                                             CtState *st, Acct &a)
+{
+    uint32_t k[T::KW];
+    t.key(k);
+    a.nl++;
+    slot = dev_find<typename T::Spec>(ct, k, nullptr);
+    if (slot < 0) return CT_NEW;
+    a.nu++;
+    CtE e;
+    ct_load(ct, slot, e);
+    if (ct_alive(e)) ct_timeout(e, tcp, dir, seen, now);
+    if (st) {
+        st->rev_nat = e.w[9] >> 16;
+        st->loopback = (e.bits() & CTB_LB_LOOPBACK) ? 1u : 0u;
+        st->slave = e.w[10] & 0xFFFFu;
+    }
+    if (flags & F_CT_ACCOUNTING) {
+        if (dir == CT_INGRESS) { e.add64(0, 1); e.add64(2, len); }
+        else                   { e.add64(4, 1); e.add64(6, len); }
+    }
+    if (action == ACTION_CREATE) {
+        if ((e.bits() & CTB_RX_CLOSING) || (e.bits() & CTB_TX_CLOSING)) {
+            e.set_bits(e.bits() & ~(CTB_RX_CLOSING | CTB_TX_CLOSING));
+            ct_timeout(e, tcp, dir, seen, now);
+        }
+    } else if (action == ACTION_CLOSE) {
+        e.set_bits(e.bits() | (dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING));
+        if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
+    }
+    ct_store(ct, slot, e);
+    return CT_ESTABLISHED;
+}
+
+__device__ __forceinline__ uint8_t dir_flags(int dir)
+{
+    return dir == CT_INGRESS ? TUPLE_F_OUT : dir == CT_EGRESS ? TUPLE_F_IN : TUPLE_F_SERVICE;
+}
+
+// The L4 part of ct_lookup4 / ct_lookup6 (conntrack.h:471-530 / 319-374): fills the
+// tuple's ports / flags and returns the action, or a DROP code / E_TRUNC (< 0).
+template <bool V6, class T>
+__device__ __forceinline__ int ct_l4(T &t, const L4Hdr &h, int dir, uint32_t &seen)
+{
+    t.flags = dir_flags(dir);
+    seen = 0;
+    const uint32_t icmp = V6 ? 58u : 1u;
+    if (t.nexthdr == icmp) {
+        if (h.c1) return chk_err(h.c1, DROP_CT_INVALID_HDR);
+        t.sport = 0; t.dport = 0;
+        const uint32_t type = h.type;
+        if (V6 ? (type >= 1 && type <= 4) : (type == 3 || type == 11 || type == 12)) {
+            t.flags |= TUPLE_F_RELATED;
+            return ACTION_UNSPEC;
+        }
+        if (type == (V6 ? 129u : 0u)) { t.dport = V6 ? 128u : 8u; return ACTION_UNSPEC; }   // echo reply
+        if (type == (V6 ? 128u : 8u)) t.sport = type;                                      // echo request
+        return ACTION_CREATE;
+    }
+    if (t.nexthdr == 6) {
+        if (h.c14) return chk_err(h.c14, DROP_CT_INVALID_HDR);
+        seen = h.tflags;
+        const int action = (seen & (TCPF_RST | TCPF_FIN)) ? ACTION_CLOSE : ACTION_CREATE;
+        if (h.c4) return chk_err(h.c4, DROP_CT_INVALID_HDR);
+        t.dport = h.p0; t.sport = h.p2;
+        return action;
+    }
+    if (t.nexthdr == 17) {
+        if (h.c4) return chk_err(h.c4, DROP_CT_INVALID_HDR);
+        t.dport = h.p0; t.sport = h.p2;
+        return ACTION_CREATE;
+    }
+    return DROP_CT_UNKNOWN_PROTO;
+}
+
+// ct_lookup4 / ct_lookup6 (conntrack.h:442-562 / 286-412); tuple in/out
+template <bool V6, class T>
+__device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr &h, int dir, uint32_t len,
+                                         uint32_t now, uint32_t flags, int64_t &slot, CtState *st, Acct &a)
+{
+    uint32_t seen;
+    const int action = ct_l4<V6>(t, h, dir, seen);
+    if (action < 0) return action;
+    const bool tcp = t.nexthdr == 6;
+    int ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a);
+    if (ret != CT_NEW) return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+    if (dir != CT_SERVICE) {
+        t.reverse();
+        ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a);
+    }
+    return ret;
+}
+
+template <class T>
+__device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const CtE &e)
+{
+    uint32_t k[T::KW];
+    t.key(k);
+    bool created;
+    const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created);
+    if (s < 0) return false;
+    ct_store(ct, s, e);
+    return true;
+}
+
+// ct_create4 / ct_create6 (conntrack.h:663-744 / 589-639): the entry, the NATed
+// tuple when ct_state->addr is set (v4 only), and the ICMP-RELATED twin
+template <bool V6, class T>
+__device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32_t len, int dir, const CtState &st,
+                                         uint32_t now, Acct &a)
+{
+    CtE e;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) e.w[k] = 0;
+    const bool tcp = t.nexthdr == 6;
+    e.w[9] = (st.rev_nat & 0xFFFFu) << 16 | (st.loopback ? CTB_LB_LOOPBACK : 0u);
+    e.w[10] = st.slave & 0xFFFFu;
+    ct_timeout(e, tcp, dir, tcp ? TCPF_SYN : 0u, now);
+    if (dir == CT_INGRESS) { e.w[0] = 1; e.w[2] = len; }
+    else                   { e.w[4] = 1; e.w[6] = len; }
+    e.w[11] = st.src_sec_id;
+    const bool nat = !V6 && st.addr;
+    a.nu += nat ? 3 : 2;
+    if (!ct_put(ct, t, e)) return DROP_CT_CREATE_FAILED;
+    if constexpr (!V6) {
+        if (nat) {
+            Tuple4 n = t;
+            if (dir == CT_INGRESS) n.saddr = st.addr; else n.daddr = st.addr;
+            if (st.loopback) {
+                n.flags = TUPLE_F_IN;
+                if (dir == CT_INGRESS) n.daddr = st.svc_addr; else n.saddr = st.svc_addr;
+            }
+            if (!ct_put(ct, n, e)) return DROP_CT_CREATE_FAILED;
+        }
+    }
+    T it = t;
+    it.nexthdr = V6 ? 58u : 1u;
+    it.sport = 0; it.dport = 0;
+    it.flags = t.flags | TUPLE_F_RELATED;
+    e.set_bits(e.bits() | CTB_SEEN_NON_SYN);
+    if (!ct_put(ct, it, e)) return DROP_CT_CREATE_FAILED;
+    return 0;
+}
+
+// ------------------------------------------------------------------ reverse NAT
+// cilium_lb4_reverse_nat / cilium_lb6_reverse_nat lookups (lb.h:501-517, 305-315):
+// dense tables indexed by the raw u16 key
+__device__ __forceinline__ bool revnat4(const DpParams &p, uint32_t index, uint32_t &addr, uint32_t &port, Acct &a)
+{
+    if (!p.revnat4) return false;
+    a.nl++;
+    const uint2 v = reinterpret_cast<const uint2 *>(p.revnat4)[index & 0xFFFFu];
+    if (!(v.y >> 16)) return false;
+    addr = v.x;
+    port = v.y & 0xFFFFu;
+    return true;
+}
+
+__device__ __forceinline__ bool revnat6(const DpParams &p, uint32_t index, uint32_t *addr, uint32_t &port, Acct &a)
+{
+    if (!p.revnat6) return false;
+    a.nl++;
+    const uint4 *q = reinterpret_cast<const uint4 *>(p.revnat6) + 2 * (size_t)(index & 0xFFFFu);
+    const uint4 v0 = q[0], v1 = q[1];
+    if (!(v1.x >> 16)) return false;
+    addr[0] = v0.x; addr[1] = v0.y; addr[2] = v0.z; addr[3] = v0.w;
+    port = v1.x & 0xFFFFu;
+    return true;
+}
+
+// reverse_map_l4_port (lb.h:222-252) inside __lb{4,6}_rev_nat: 0 or a code
+__device__ __forceinline__ int rev_map_port(L4Hdr &h, uint32_t nexthdr, uint32_t port)
+{
+    if (!port) return 0;
+    if (nexthdr == 6 || nexthdr == 17) {
+        if (h.c2a) return chk_err(h.c2a, E_FAULT);
+        if (port != h.p0) h.p0 = port;               // l4_modify_port(TCP_SPORT_OFF)
+        return 0;
+    }
+    if (nexthdr == 1 || nexthdr == 58) return 0;
+    return DROP_UNKNOWN_L4;
+}
+
+// ------------------------------------------------------------------ the skb after rewrites
+struct Skb4 {
+    uint32_t saddr, daddr, len, nexthdr, ttl;
+    int l4off;
+    L4Hdr h;
+};
+
+struct Skb6 {
+    uint32_t saddr[4], daddr[4];
+    uint32_t len, nexthdr, hoplimit;
+    int l4off;                  // ETH_HLEN + ipv6_hdrlen, or the (negative) ipv6_hdrlen error
+    L4Hdr h;
+};
+
+// ipv6_hdrlen (ipv6.h:61-98): returns the IPv6 header length or a DROP code and
+// the final next header.  The AUTH length is chosen by the type of the header that
+// FOLLOWS (nh is updated first), as the reference does.
+template <int NW>
+__device__ __forceinline__ int ipv6_hdrlen(const RecT<NW> &r, uint32_t &nexthdr)
+{
+    int len = 40;
+    uint32_t nh = rec_u8c<20>(r);
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        if (nh == 59) return DROP_INVALID_EXTHDR;
+        if (nh == 44) return DROP_FRAG_NOSUPPORT;
+        if (nh == 0 || nh == 43 || nh == 51 || nh == 60) {
+            const int off = 14 + len;
+            const int c = rec_chk(r, off, 2);
+            if (c) return chk_err(c, DROP_INVALID);
+            const uint32_t b0 = off == 54 ? rec_u8c<54>(r) : r.base[off];
+            const uint32_t b1 = off == 54 ? rec_u8c<55>(r) : r.base[off + 1];
+            nh = b0;
+            len += nh == 51 ? (int)((b1 + 2) << 2) : (int)((b1 + 1) << 3);
+            continue;
+        }
+        nexthdr = nh;
+        return len;
+    }
+    return DROP_INVALID_EXTHDR;
+}
+
+__device__ __forceinline__ Skb6 skb6_from(const Rec6 &r)
+{
+    Skb6 s;
+    s.saddr[0] = rec_raw32c<22>(r); s.saddr[1] = rec_raw32c<26>(r); s.saddr[2] = rec_raw32c<30>(r); s.saddr[3] = rec_raw32c<34>(r);
+    s.daddr[0] = rec_raw32c<38>(r); s.daddr[1] = rec_raw32c<42>(r); s.daddr[2] = rec_raw32c<46>(r); s.daddr[3] = rec_raw32c<50>(r);
+    s.len = r.len;
+    s.hoplimit = rec_u8c<21>(r);
+    uint32_t nh = rec_u8c<20>(r);
+    const int hl = ipv6_hdrlen(r, nh);
+    s.nexthdr = nh;
+    s.l4off = hl < 0 ? hl : 14 + hl;
+    if (hl >= 0) s.h = l4_read<54>(r, s.l4off);
+    return s;
+}
+
+__device__ __forceinline__ Skb4 skb4_from(const Rec &r)
+{
+    Skb4 s;
+    s.saddr = rec_raw32c<26>(r);
+    s.daddr = rec_raw32c<30>(r);
+    s.len = r.len;
+    s.nexthdr = rec_u8c<23>(r);
+    s.ttl = rec_u8c<22>(r);
+    s.l4off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
+    s.h = l4_read<34>(r, s.l4off);
+    return s;
+}
+
+// ------------------------------------------------------------------ endpoint ingress programs
+// ipv4_policy (bpf_lxc.c:865-979) + tail_ipv4_policy (:981-993), LXC_NAT46 off.
+// Returns the final verdict (TC_ACT_*, drops accounted as METRIC_INGRESS) or E_TRUNC.
+__device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
+                                           bool skip_proxy, bool ifindex_nz, uint32_t now, uint8_t &ct_out,
+                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
+{
+    int ret;
+    int verdict;
+    Tuple4 t;
+    CtState st{0, 0, 0, 0, 0, 0};
+    int64_t slot;
+    if (s.len < 34) { ret = DROP_INVALID; goto drop; }          // revalidate_data
+    t.nexthdr = s.nexthdr;
+    t.daddr = s.daddr;
+    t.saddr = s.saddr;
+    t.dport = t.sport = 0;
+    ret = ct_lookup<false>(ep.ct4, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a);
+    if (ret < 0) goto drop;
+    ct_out = (uint8_t)ret;
+    if (ret == CT_REPLY && st.rev_nat && !st.loopback) {         // lb4_rev_nat(REV_NAT_F_TUPLE_SADDR)
+        uint32_t na, np;
+        if (revnat4(p, st.rev_nat, na, np, a)) {
+            const int r2 = rev_map_port(s.h, t.nexthdr, np);
+            if (r2) { ret = r2; goto drop; }
+            t.saddr = na;
+        }
+    }
+    verdict = policy_ingress(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) { dev_kill<Ct4Spec>(ep.ct4, slot); a.nu++; }   // ct_delete4
+        ret = DROP_POLICY;
+        goto drop;
+    }
+    if (skip_proxy) verdict = 0;
+    if (ret == CT_NEW) {
+        CtState sn{0, 0, 0, 0, 0, src_label};
+        const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a);
+        if (is_err(c)) { ret = c; goto drop; }
+    }
+    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        proxy = (uint16_t)verdict;                                 // ipv4_redirect_to_host_port
+        return TC_ACT_REDIRECT;                                    // redirect(HOST_IFINDEX)
+    }
+    m.fwd(s.len, METRIC_INGRESS);                                  // send_trace_notify(TRACE_TO_LXC)
+    return ifindex_nz ? TC_ACT_REDIRECT : TC_ACT_OK;
+drop:
+    if (ret == E_TRUNC) return ret;
+    m.drop(ret, s.len, METRIC_INGRESS);
+    reason = ret;
+    return TC_ACT_SHOT;
+}
+
+__device__ __forceinline__ bool eq4(const uint32_t *a, const uint32_t *b)
+{
+    return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
+}
+
+// ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862)
+__device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
+                                           bool skip_proxy, bool ifindex_nz, uint32_t now, uint8_t &ct_out,
+                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
+{
+    int ret;
+    int verdict;
+    Tuple6 t;
+    CtState st{0, 0, 0, 0, 0, 0};
+    CtState sn{0, 0, 0, 0, 0, src_label};
+    int64_t slot;
+    if (s.len < 54) { ret = DROP_INVALID; goto drop; }
+    if (s.l4off < 0) { ret = s.l4off; goto drop; }              // ipv6_hdrlen error
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
+    t.nexthdr = s.nexthdr;
+    t.dport = t.sport = 0;
+    sn.rev_nat = s.daddr[3] & 0xFFFFu;                           // derive reverse NAT index (:750-766)
+    ret = ct_lookup<true>(ep.ct6, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a);
+    if (ret < 0) goto drop;
+    ct_out = (uint8_t)ret;
+    if (st.rev_nat) {                                            // lb6_rev_nat(.., 0)
+        uint32_t na[4], np;
+        if (revnat6(p, st.rev_nat, na, np, a)) {
+            const int r2 = rev_map_port(s.h, t.nexthdr, np);
+            if (r2) { ret = r2; goto drop; }
+        }
+    }
+    verdict = policy_ingress(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) { dev_kill<Ct6Spec>(ep.ct6, slot); a.nu++; }
+        ret = DROP_POLICY;
+        goto drop;
+    }
+    if (skip_proxy) verdict = 0;
+    if (ret == CT_NEW) {
+        const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a);
+        if (is_err(c)) { ret = c; goto drop; }
+    }
+    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        proxy = (uint16_t)verdict;
+        return TC_ACT_REDIRECT;
+    }
+    m.fwd(s.len, METRIC_INGRESS);
+    return ifindex_nz ? TC_ACT_REDIRECT : TC_ACT_OK;
+drop:
+    if (ret == E_TRUNC) return ret;
+    m.drop(ret, s.len, METRIC_INGRESS);
+    reason = ret;
+    return TC_ACT_SHOT;
+}
+
+// handle_policy (bpf_lxc.c:1003-1038) for an IPv4 / IPv6 packet: DROP_ALL drops
+// before any conntrack work; IPv4 needs the endpoint's LXC_IPV4 program.
+__device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
+                                              bool skip_proxy, bool ifindex_nz, uint32_t now, uint8_t &ct_out,
+                                              uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
+{
+    int ret;
+    if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
+    else if (ep.ipv4) return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex_nz, now, ct_out, proxy, reason, a, m);
+    else ret = DROP_UNKNOWN_L3;
+    m.drop(ret, s.len, METRIC_INGRESS);
+    reason = ret;
+    return TC_ACT_SHOT;
+}
+
+__device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
+                                              bool ifindex_nz, uint32_t now, uint8_t &ct_out, uint16_t &proxy,
+                                              int32_t &reason, Acct &a, Met &m)
+{
+    int ret;
+    if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
+    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, false, ifindex_nz, now, ct_out, proxy, reason, a, m);
+    else ret = DROP_MISSED_TAIL_CALL;
+    m.drop(ret, s.len, METRIC_INGRESS);
+    reason = ret;
+    return TC_ACT_SHOT;
+}
+
+// ------------------------------------------------------------------ grouping
+// Packets whose conntrack work can touch a common entry are put in one group and
+// run by one lane in packet order; groups are independent, so the batch result
+// equals a sequential run on one CPU.  A group is a node of an epoch-tagged open-
+// addressing table (hash tag | head of a linked list of packets); the egress path
+// also merges nodes with a lock-free union-find (parent pointers per slot).
+
+// find-or-insert the node of 64-bit key hash `gh`; returns its slot
+__device__ __forceinline__ uint32_t group_node(const GroupScratch &g, uint64_t gh)
+{
+    const uint32_t h32 = (uint32_t)gh | 1u;
+    const unsigned long long tagged = (unsigned long long)g.epoch << 32 | h32;
+    uint32_t s = (uint32_t)(gh >> 32) & g.cap_mask;
+    for (;;) {
+        unsigned long long cur = __hip_atomic_load(&g.table[2 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == tagged) return s;
+        if ((uint32_t)(cur >> 32) != g.epoch) {
+            if (__hip_atomic_compare_exchange_strong(&g.table[2 * s], &cur, tagged, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                return s;
+            if (cur == tagged) return s;
+            if ((uint32_t)(cur >> 32) != g.epoch) continue;
+        }
+        s = (s + 1) & g.cap_mask;
+    }
+}
+
+// push packet i on the list of node s
+__device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, uint32_t i)
+{
+    const unsigned long long prev = __hip_atomic_exchange(&g.table[2 * s + 1], (unsigned long long)g.epoch << 32 | i,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g.gslot[i] = s;
+    g.next[i] = (uint32_t)(prev >> 32) == g.epoch ? (uint32_t)prev : NONE;
+}
+
+__device__ __forceinline__ uint32_t uf_parent(const GroupScratch &g, uint32_t s)
+{
+    const unsigned long long v = __hip_atomic_load(&g.parent[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (uint32_t)(v >> 32) == g.epoch ? (uint32_t)v : s;
+}
+
+__device__ __forceinline__ uint32_t uf_find(const GroupScratch &g, uint32_t s)
+{
+    for (;;) {
+        const uint32_t p = uf_parent(g, s);
+        if (p == s) return s;
+        const uint32_t gp = uf_parent(g, p);
+        if (gp != p) {                                            // path halving (best effort)
+            unsigned long long exp = (unsigned long long)g.epoch << 32 | p;
+            __hip_atomic_compare_exchange_strong(&g.parent[s], &exp, (unsigned long long)g.epoch << 32 | gp,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s = gp;
+    }
+}
+
+// merge the groups of nodes a and b: the larger root is linked under the smaller
+__device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint32_t b)
+{
+    for (;;) {
+        a = uf_find(g, a);
+        b = uf_find(g, b);
+        if (a == b) return;
+        if (a < b) { const uint32_t x = a; a = b; b = x; }
+        unsigned long long cur = __hip_atomic_load(&g.parent[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(cur >> 32) == g.epoch && (uint32_t)cur != a) continue;   // no longer a root
+        if (__hip_atomic_compare_exchange_strong(&g.parent[a], &cur, (unsigned long long)g.epoch << 32 | b,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
+    }
+}
+
+constexpr int GMAX = 16;
+
+// Run fn(i) for every member of the group whose list starts at `head`, in
+// ascending packet order (<= GMAX sorted in registers, else repeated minimum).
+template <class F>
+__device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t head, F &&fn)
+{
+    if (g.next[head] == NONE) { fn(head); return; }
+    uint32_t m[GMAX];
+    int cnt = 0;
+    bool overflow = false;
+    for (uint32_t x = head; x != NONE; x = g.next[x]) {
+        if (cnt == GMAX) { overflow = true; break; }
+        int pos = 0;
+#pragma unroll
+        for (int j = 0; j < GMAX; ++j) pos += (j < cnt && m[j] < x) ? 1 : 0;
+#pragma unroll
+        for (int j = GMAX - 1; j >= 0; --j) {
+            const uint32_t left = j > 0 ? m[j - 1] : 0u;
+            m[j] = (j < pos) ? m[j] : (j == pos ? x : left);
+        }
+        ++cnt;
+    }
+    if (!overflow) {
+#pragma unroll 1
+        for (int j = 0; j < GMAX; ++j) {
+            if (j >= cnt) break;
+            uint32_t v = m[0];
+#pragma unroll
+            for (int q = 1; q < GMAX; ++q) v = (q == j) ? m[q] : v;
+            fn(v);
+        }
+        return;
+    }
+    uint32_t last = 0;
+    bool first = true;
+    for (;;) {                                                     // repeated minimum scan
+        uint32_t best = NONE;
+        for (uint32_t x = head; x != NONE; x = g.next[x])
+            if ((first || x > last) && x < best) best = x;
+        if (best == NONE) break;
+        fn(best);
+        last = best;
+        first = false;
+    }
+}
+
+// node key of an unordered address pair (v4 words or v6 4-word addresses), mixed
+// with a salt that separates families / stages
+__device__ __forceinline__ uint64_t pair_hash4(uint32_t a, uint32_t b, uint64_t salt)
+{
+    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    return mix64(((uint64_t)lo << 32 | hi) ^ salt);
+}
+
+__device__ __forceinline__ bool lt6(const uint32_t *a, const uint32_t *b)
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (a[j] != b[j]) return a[j] < b[j];
+    return false;
+}
+
+__device__ __forceinline__ uint64_t pair_hash6(const uint32_t *a, const uint32_t *b, uint64_t salt)
+{
+    const uint32_t *lo = lt6(a, b) ? a : b, *hi = lt6(a, b) ? b : a;
+    uint64_t h = salt ^ 0x6A09E667F3BCC908ULL;
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+        h = mix64(h ^ ((uint64_t)lo[j] | (uint64_t)lo[j + 1] << 32)) + 0x9E3779B97F4A7C15ULL;
+        h = mix64(h ^ ((uint64_t)hi[j] | (uint64_t)hi[j + 1] << 32)) + 0x9E3779B97F4A7C15ULL;
+    }
+    return mix64(h);
+}
+
+}  // namespace cv

@@ -12,11 +12,16 @@ namespace cv {
 // after every launch chunk of at most MAX_CHUNK packets (no field can overflow).
 constexpr uint32_t MAX_CHUNK = 1u << 24;
 
-struct EpDev {                 // one tail-call target of cilium_policy (bpf_lxc.c:1003)
+struct EpDev {                 // one endpoint program (bpf_lxc.c), its maps and lxc_config.h constants
     HashTable policy;          // PolicySpec + 32-B side values {proxy_port, pad, packets, bytes}
     HashTable ct4;             // Ct4Spec + 64-B side values (struct ct_entry)
+    HashTable ct6;             // Ct6Spec + 64-B side values
     uint32_t seclabel;
     uint32_t ct_id;            // identifies the CT map (group key component)
+    uint32_t ipv4;             // LXC_IPV4 (raw network-order word); 0 = no IPv4 programs
+    uint32_t ipv6[4];          // LXC_IP
+    uint32_t mac[2];           // LXC_MAC bytes 0-3 | 4-5
+    uint32_t node_mac[2];      // NODE_MAC
 };
 
 struct DpParams {              // by value as the kernel argument
@@ -29,6 +34,13 @@ struct DpParams {              // by value as the kernel argument
     const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
     unsigned long long *metrics;   // [256][4][2]
     uint32_t ablate;           // timing-only ablations (CV_ABLATE env); 0 in every real run
+    // load balancer (lb.h): services and dense reverse-NAT tables indexed by the raw u16 key
+    HashTable lb4, lb6;        // Lb4Spec / Lb6Spec
+    const uint32_t *revnat4;   // [65536][2]  {address, port | valid << 16}
+    const uint32_t *revnat6;   // [65536][8]  {address[4], port | valid << 16, 0, 0, 0}
+    // node_config.h constants (raw network-order words)
+    uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
+    uint32_t router6[4];
 };
 
 // ablation bits: each removes one part of the work to price it (results are wrong)
@@ -49,6 +61,7 @@ struct OutDev {
     uint8_t *ct;
     uint16_t *proxy;
     uint8_t *nl, *nu;          // optional accounting of map lookups / entry writes
+    int32_t *reason;           // DROP_* behind a TC_ACT_SHOT, else 0
 };
 
 struct GroupScratch {          // address-pair grouping for conntrack (config 3)
@@ -59,18 +72,24 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *next;            // per packet: previous inserter in the group or ~0
     uint32_t *secctx;          // per packet: source label handed to the policy program
     uint32_t *meta;            // per packet: ep index | skip_proxy << 16 | ifindex != 0 << 17
+    unsigned long long *parent;// per table slot: epoch << 32 | union-find parent (egress path)
+    uint32_t *eg;              // per packet: EG_WORDS words of egress scratch (egress path)
 };
+constexpr int EG_WORDS = 16;
 
 int launch_policy_fold(const HashTable &pol, hipStream_t s);
 int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter,
                           const OutDev &o, const GroupScratch &g, hipStream_t s);
+// config 5: from-container of the packets' source endpoints (src_ep[i], or ep0)
+int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
+                      const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s);
 // single-element operations on a device-resident conntrack table (map API path):
-// op 0 lookup, 1 update (BPF_ANY/NOEXIST/EXIST in flags), 2 delete.
-// io = {key[4 words], value[16 words], rc}
-int launch_ct_op(const HashTable &t, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s);
-int launch_ct_scan(const HashTable &t, uint64_t nb, uint32_t *out_keys, uint32_t *out_vals, uint32_t *count,
+// op 0 lookup, 1 update (BPF_ANY/NOEXIST/EXIST in flags), 2 delete; v6 selects the
+// ipv6_ct_tuple table.  io = {key[KW words], value[16 words], rc}
+int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s);
+int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint32_t *out_keys, uint32_t *out_vals, uint32_t *count,
                    uint32_t max, hipStream_t s);
 
 }  // namespace cv

@@ -1,0 +1,750 @@
+// cv_egress.hip — gfx950 kernels of the from-container (egress) path, config 5.
+//
+// Restates bpf_lxc.c handle_ingress (:672-716) -> tail_handle_ipv4 /
+// tail_handle_ipv6 -> handle_ipv4_from_lxc (:402-649) / ipv6_l3_from_lxc
+// (:82-352) with lb4/lb6 service lookup and lb{4,6}_local (lib/lb.h), egress
+// conntrack and policy, and local delivery into the destination endpoint's
+// handle_policy (:1003-1038) -> ipv{4,6}_policy, direct routing (no ENCAP_IFINDEX),
+// over a batch of frame records in HBM.  One lane = one packet.
+//
+// Batch semantics are those of one CPU running the packets in order.  Conntrack
+// work is split in two disjoint key sets that commute:
+//   * service entries (tuple flags with TUPLE_F_SERVICE), touched only by
+//     lb{4,6}_local: k_lb_stage runs them grouped by (source, VIP) pair;
+//   * all other entries: k_egress_ct runs them grouped by connected components of
+//     the address pairs a packet can touch — its egress tuple, the NATed tuple a
+//     service create writes, the pair its local delivery sees after rewrites and the
+//     pairs a reverse-NAT of an entry it reads or creates can lead to — built by
+//     k_egress_pairs (lock-free union-find) and linked by k_group_link.
+// Within a group packets run in packet order; groups share no entry.
+#include "cv_dev.hpp"
+
+namespace cv {
+
+int grid_for(uint32_t n);
+
+// egress scratch words (GroupScratch::eg, EG_WORDS per packet)
+enum : uint32_t {
+    EG_STAGE = 0x3u, EG_V6 = 0x4u, EG_LOOPBACK = 0x8u, EG_SVC = 0x10u, EG_DPORT_RW = 0x20u,
+};
+enum : uint32_t { STAGE_DONE = 0, STAGE_LB = 1, STAGE_CT = 2 };
+constexpr uint64_t SALT_SVC4 = 0x5356433400000000ULL, SALT_SVC6 = 0x5356433600000000ULL,
+                   SALT_CT4 = 0x4354340000000000ULL, SALT_CT6 = 0x4354360000000000ULL;
+
+struct EgOut {                  // per-packet results on the way to the outputs
+    int32_t ret, reason;
+    uint32_t dst;
+    uint8_t ct;
+    uint16_t proxy;
+};
+
+__device__ __forceinline__ void eg_final(const OutDev &o, uint32_t i, const EgOut &r, const Acct &a)
+{
+    if (o.ret) o.ret[i] = r.ret;
+    if (o.reason) o.reason[i] = r.reason;
+    if (o.identity) o.identity[i] = r.dst;
+    if (o.ct) o.ct[i] = r.ct;
+    if (o.proxy) o.proxy[i] = r.proxy;
+    if (o.xdp) o.xdp[i] = 0;
+    store_out(o, i, a);
+}
+
+// tail_handle_ipv{4,6} / handle_ingress: IS_ERR -> send_drop_notify(METRIC_EGRESS)
+__device__ __forceinline__ void eg_drop(EgOut &r, int32_t code, uint32_t len, Met &m)
+{
+    if (code == E_TRUNC || code == E_PUNT) { r.ret = code; return; }
+    m.drop(code, len, METRIC_EGRESS);
+    r.reason = code;
+    r.ret = TC_ACT_SHOT;
+}
+
+__device__ __forceinline__ bool mac_eq(uint32_t w0, uint32_t h1, const uint32_t *mac)
+{
+    return w0 == mac[0] && h1 == (mac[1] & 0xFFFFu);
+}
+
+// ================================================================== front
+// handle_ingress dispatch + the from-container prologue up to lb{4,6}_lookup_service.
+// Returns STAGE_LB (service found), STAGE_CT, or STAGE_DONE with r filled.
+template <int NW>
+__device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep, const RecT<NW> &r, uint32_t *eg,
+                                              EgOut &res, Acct &a, Met &m)
+{
+    const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
+    int ret;
+    if (p.flags & F_DROP_ALL) {
+        if (eth == 0x0608u) { res.ret = E_PUNT; return STAGE_DONE; }   // ARP responder tail call
+        eg_drop(res, DROP_POLICY, r.len, m);
+        return STAGE_DONE;
+    }
+    if (eth == 0x0008u) {
+        if (!ep.ipv4) { eg_drop(res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
+        // handle_ipv4_from_lxc (bpf_lxc.c:402-446)
+        if (r.len < 34) { eg_drop(res, DROP_INVALID, r.len, m); return STAGE_DONE; }
+        if (!mac_eq(rec_raw32c<6>(r), rec_raw16c<10>(r), ep.mac)) ret = DROP_INVALID_SMAC;
+        else if (!mac_eq(rec_raw32c<0>(r), rec_raw16c<4>(r), ep.node_mac)) ret = DROP_INVALID_DMAC;
+        else if (rec_raw32c<26>(r) != ep.ipv4) ret = DROP_INVALID_SIP;
+        else ret = 0;
+        if (ret) { eg_drop(res, ret, r.len, m); return STAGE_DONE; }
+        const uint32_t nexthdr = rec_u8c<23>(r);
+        const int off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
+        const L4Hdr h = l4_read<34>(r, off);
+        uint32_t dport = 0;
+        if (nexthdr == 6 || nexthdr == 17) {                      // lb4_extract_key / extract_l4_port
+            if (h.c2b) { eg_drop(res, chk_err(h.c2b, E_FAULT), r.len, m); return STAGE_DONE; }
+            dport = h.p2;
+        } else if (nexthdr != 1) {
+            return STAGE_CT;                                      // DROP_UNKNOWN_L4: skip_service_lookup
+        }
+        if (!p.lb4.buckets) return STAGE_CT;
+        // lb4_lookup_service (lb.h:590-623), LB_L4 + LB_L3
+        const uint32_t daddr = rec_raw32c<30>(r);
+        uint32_t k[2], v[3];
+        if (dport) {
+            k[0] = daddr; k[1] = dport;
+            a.nl++;
+            if (dev_find<Lb4Spec>(p.lb4, k, v) >= 0 && (v[1] >> 16)) {
+                eg[1] |= dport << 16; eg[2] = v[1] >> 16;
+                return STAGE_LB;
+            }
+            dport = 0;
+        }
+        k[0] = daddr; k[1] = 0;
+        a.nl++;
+        if (dev_find<Lb4Spec>(p.lb4, k, v) >= 0 && (v[1] >> 16)) {
+            eg[2] = v[1] >> 16;
+            return STAGE_LB;
+        }
+        return STAGE_CT;
+    }
+    if (eth == 0xDD86u) {
+        if constexpr (NW < 32) {
+            res.ret = E_TRUNC;                                    // IPv6 needs 128-B records
+            return STAGE_DONE;
+        } else {
+            if (!ep.ct6.buckets) { eg_drop(res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
+            // handle_ipv6 (bpf_lxc.c:354-380) + ipv6_l3_from_lxc (:82-125)
+            if (r.len < 54) { eg_drop(res, DROP_INVALID, r.len, m); return STAGE_DONE; }
+            eg[0] |= EG_V6;
+            if (rec_u8c<20>(r) == 58) {                          // icmp6_handle (icmp6.h:390-412)
+                if (r.len < 62) { eg_drop(res, DROP_INVALID, r.len, m); return STAGE_DONE; }
+                const uint32_t type = rec_u8c<54>(r);
+                const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
+                if (type == 135 || (type == 128 && eq4(da, p.router6))) { res.ret = E_PUNT; return STAGE_DONE; }
+            }
+            const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
+            if (!mac_eq(rec_raw32c<6>(r), rec_raw16c<10>(r), ep.mac)) ret = DROP_INVALID_SMAC;
+            else if (!mac_eq(rec_raw32c<0>(r), rec_raw16c<4>(r), ep.node_mac)) ret = DROP_INVALID_DMAC;
+            else if (!eq4(sa, ep.ipv6)) ret = DROP_INVALID_SIP;
+            else ret = 0;
+            if (ret) { eg_drop(res, ret, r.len, m); return STAGE_DONE; }
+            uint32_t nexthdr;
+            const int hl = ipv6_hdrlen(r, nexthdr);
+            if (hl < 0) { eg_drop(res, hl, r.len, m); return STAGE_DONE; }
+            const int off = 14 + hl;
+            const L4Hdr h = l4_read<54>(r, off);
+            uint32_t dport = 0;
+            if (nexthdr == 6 || nexthdr == 17) {
+                if (h.c2b) { eg_drop(res, chk_err(h.c2b, E_FAULT), r.len, m); return STAGE_DONE; }
+                dport = h.p2;
+            } else if (nexthdr != 58 && nexthdr != 1) {
+                return STAGE_CT;
+            }
+            if (!p.lb6.buckets) return STAGE_CT;
+            uint32_t k[5] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r), 0};
+            uint32_t v[6];
+            if (dport) {                                          // lb6_lookup_service (lb.h:334-368)
+                k[4] = dport;
+                a.nl++;
+                if (dev_find<Lb6Spec>(p.lb6, k, v) >= 0 && (v[4] >> 16)) {
+                    eg[1] |= dport << 16; eg[2] = v[4] >> 16;
+                    return STAGE_LB;
+                }
+            }
+            k[4] = 0;
+            a.nl++;
+            if (dev_find<Lb6Spec>(p.lb6, k, v) >= 0 && (v[4] >> 16)) {
+                eg[2] = v[4] >> 16;
+                return STAGE_LB;
+            }
+            return STAGE_CT;
+        }
+    }
+    if (eth == 0x0608u) { res.ret = E_PUNT; return STAGE_DONE; }
+    eg_drop(res, DROP_UNKNOWN_L3, r.len, m);
+    return STAGE_DONE;
+}
+
+template <int NW>
+__global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
+                                                        OutDev o, GroupScratch g)
+{
+    __shared__ LdsMetrics lm;
+    Met m;
+    met_init(m, lm);
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        RecT<NW> r;
+        rec_load(r, b, i, NW / 4);
+        Acct a{0, 0};
+        EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
+        uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        const uint32_t e = src_ep ? src_ep[i] : ep0;
+        eg[1] = e & 0xFFFFu;
+        eg[2] = 0;
+        eg[0] = 0;
+        uint32_t stage;
+        if (e >= p.n_eps) {
+            eg_drop(res, DROP_MISSED_TAIL_CALL, r.len, m);        // no program for the source
+            stage = STAGE_DONE;
+        } else {
+            stage = front_one(p, p.eps[e], r, eg, res, a, m);
+        }
+        eg[0] |= stage;
+        g.gslot[i] = NONE;
+        if (stage == STAGE_DONE) {
+            eg_final(o, i, res, a);
+        } else {
+            store_out(o, i, a);
+            if (stage == STAGE_LB) {                              // join the (source, VIP) service group
+                const EpDev &ep = p.eps[e];
+                uint64_t gh;
+                if (eg[0] & EG_V6) {
+                    if constexpr (NW >= 32) {
+                        const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
+                        const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
+                        gh = pair_hash6(sa, da, SALT_SVC6 ^ ep.ct_id);
+                    } else {
+                        gh = 0;
+                    }
+                } else {
+                    gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ep.ct_id);
+                }
+                group_push(g, group_node(g, gh), i);
+            }
+        }
+    }
+    met_flush(m, p.metrics);
+}
+
+// ================================================================== service stage
+// lb4_local (lb.h:700-775) + lb4_xlate (:653-697) of one packet; the packet leaves
+// with its translation in the scratch words, or final.
+__device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, const uint32_t *hash, uint32_t now,
+                                        const OutDev &o, const GroupScratch &g, uint32_t i, Met &m)
+{
+    Rec r;
+    rec_load(r, b, i, 4);
+    uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
+    const uint32_t hsh = hash ? hash[i] : 0u;
+    uint32_t key_dport = eg[1] >> 16;
+    const uint32_t count = eg[2] & 0xFFFFu;
+    const uint32_t saddr = rec_raw32c<26>(r), vip = rec_raw32c<30>(r);
+    const int off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
+    L4Hdr h = l4_read<34>(r, off);
+    Tuple4 t;
+    t.daddr = vip; t.saddr = saddr; t.nexthdr = rec_u8c<23>(r); t.dport = t.sport = 0;
+    CtState st{0, 0, 0, 0, 0, 0};
+    int64_t slot;
+    int ret = ct_lookup<false>(ep.ct4, t, h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
+    uint32_t k[2], v[3];
+    bool have = false;
+    if (ret == E_TRUNC) goto fin;
+    if (ret == CT_NEW) {
+        st.slave = hsh % count + 1;                               // lb4_select_slave
+        const int c = ct_create<false>(ep.ct4, t, r.len, CT_SERVICE, st, now, a);
+        if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
+    } else if (ret < 0) {
+        ret = DROP_NO_SERVICE;
+        goto fin;
+    }
+    k[0] = vip; k[1] = key_dport | st.slave << 16;                // lb4_lookup_slave
+    a.nl++;
+    have = dev_find<Lb4Spec>(p.lb4, k, v) >= 0;
+    if (!have) {                                                  // backend gone: lb4_lookup_service with the slave key
+        if (key_dport) {
+            a.nl++;
+            have = dev_find<Lb4Spec>(p.lb4, k, v) >= 0 && (v[1] >> 16);
+            if (!have) { key_dport = 0; k[1] = st.slave << 16; }
+        }
+        if (!have) {
+            a.nl++;
+            have = dev_find<Lb4Spec>(p.lb4, k, v) >= 0 && (v[1] >> 16);
+        }
+        if (!have) { ret = DROP_NO_SERVICE; goto fin; }
+        st.slave = hsh % (v[1] >> 16) + 1;
+        uint32_t tk[4];                                           // ct_update4_slave
+        t.key(tk);
+        a.nl++;
+        const int64_t s2 = dev_find<Ct4Spec>(ep.ct4, tk, nullptr);
+        if (s2 >= 0) {
+            CtE e;
+            ct_load(ep.ct4, s2, e);
+            e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
+            ct_store(ep.ct4, s2, e);
+            a.nu++;
+        }
+    }
+    {
+        const uint32_t target = v[0], sport_svc = v[1] & 0xFFFFu;
+        st.rev_nat = v[2] & 0xFFFFu;
+        st.addr = target;
+        uint32_t skb_saddr = saddr;
+        if (saddr == target) {                                    // !DISABLE_LOOPBACK_LB
+            skb_saddr = p.v4_loopback;
+            st.loopback = 1;
+            st.addr = p.v4_loopback;
+            st.svc_addr = saddr;
+        }
+        const uint32_t tdaddr = st.loopback ? vip : target;
+        uint32_t flags = STAGE_CT | EG_SVC | (st.loopback ? EG_LOOPBACK : 0u);
+        uint32_t ndport = 0;
+        if (sport_svc && key_dport != sport_svc && (t.nexthdr == 6 || t.nexthdr == 17)) {
+            if (h.c2b) { ret = chk_err(h.c2b, DROP_WRITE_ERROR); goto fin; }
+            ndport = sport_svc;
+            flags |= EG_DPORT_RW;
+        }
+        eg[0] = flags;
+        eg[2] = ndport << 16;
+        eg[3] = (st.rev_nat & 0xFFFFu) | st.slave << 16;
+        eg[4] = st.addr;
+        eg[5] = st.svc_addr;
+        eg[6] = tdaddr;
+        eg[7] = target;                                           // skb daddr after lb4_xlate
+        eg[8] = skb_saddr;
+        store_out(o, i, a);
+        return;
+    }
+fin:
+    eg[0] = STAGE_DONE;
+    eg_drop(res, ret, r.len, m);
+    eg_final(o, i, res, a);
+}
+
+// lb6_local (lb.h:426-483) + lb6_xlate (:386-424)
+__device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, const uint32_t *hash, uint32_t now,
+                                        const OutDev &o, const GroupScratch &g, uint32_t i, Met &m)
+{
+    Rec6 r;
+    rec_load(r, b, i, 8);
+    uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
+    const uint32_t hsh = hash ? hash[i] : 0u;
+    uint32_t key_dport = eg[1] >> 16;
+    const uint32_t count = eg[2] & 0xFFFFu;
+    Skb6 s = skb6_from(r);
+    Tuple6 t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
+    t.nexthdr = s.nexthdr; t.dport = t.sport = 0;
+    CtState st{0, 0, 0, 0, 0, 0};
+    int64_t slot;
+    int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
+    uint32_t k[5] = {s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3], 0}, v[6];
+    bool have = false;
+    if (ret == E_TRUNC) goto fin;
+    if (ret == CT_NEW) {
+        st.slave = hsh % count + 1;
+        const int c = ct_create<true>(ep.ct6, t, r.len, CT_SERVICE, st, now, a);
+        if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
+    } else if (ret < 0) {
+        ret = DROP_NO_SERVICE;
+        goto fin;
+    }
+    k[4] = key_dport | st.slave << 16;
+    a.nl++;
+    have = dev_find<Lb6Spec>(p.lb6, k, v) >= 0;
+    if (!have) {
+        if (key_dport) {
+            a.nl++;
+            have = dev_find<Lb6Spec>(p.lb6, k, v) >= 0 && (v[4] >> 16);
+            if (!have) { key_dport = 0; k[4] = st.slave << 16; }
+        }
+        if (!have) {
+            a.nl++;
+            have = dev_find<Lb6Spec>(p.lb6, k, v) >= 0 && (v[4] >> 16);
+        }
+        if (!have) { ret = DROP_NO_SERVICE; goto fin; }
+        st.slave = hsh % (v[4] >> 16) + 1;
+        uint32_t tk[10];                                          // ct_update6_slave
+        t.key(tk);
+        a.nl++;
+        const int64_t s2 = dev_find<Ct6Spec>(ep.ct6, tk, nullptr);
+        if (s2 >= 0) {
+            CtE e;
+            ct_load(ep.ct6, s2, e);
+            e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
+            ct_store(ep.ct6, s2, e);
+            a.nu++;
+        }
+    }
+    {
+        const uint32_t sport_svc = v[4] & 0xFFFFu;
+        st.rev_nat = v[5] & 0xFFFFu;
+        uint32_t flags = STAGE_CT | EG_V6 | EG_SVC;
+        uint32_t ndport = 0;
+        if (sport_svc && key_dport != sport_svc && (t.nexthdr == 6 || t.nexthdr == 17)) {
+            if (s.h.c2b) { ret = chk_err(s.h.c2b, DROP_WRITE_ERROR); goto fin; }
+            ndport = sport_svc;
+            flags |= EG_DPORT_RW;
+        }
+        eg[0] = flags;
+        eg[2] = ndport << 16;
+        eg[3] = (st.rev_nat & 0xFFFFu) | st.slave << 16;
+        eg[4] = 0; eg[5] = 0;
+        eg[12] = v[0]; eg[13] = v[1]; eg[14] = v[2]; eg[15] = v[3];   // tuple daddr = skb daddr = target
+        store_out(o, i, a);
+        return;
+    }
+fin:
+    eg[0] = STAGE_DONE;
+    eg_drop(res, ret, r.len, m);
+    eg_final(o, i, res, a);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
+                                                    OutDev o, GroupScratch g)
+{
+    __shared__ LdsMetrics lm;
+    Met m;
+    met_init(m, lm);
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint32_t s = g.gslot[i];
+        if (s == NONE || g.next[i] != NONE) continue;             // not a service packet / not the group's tail
+        const uint32_t head = (uint32_t)g.table[2 * s + 1];
+        group_in_order(g, head, [&](uint32_t x) {
+            if (g.eg[(size_t)x * EG_WORDS] & EG_V6) lb6_one(p, b, hash, now, o, g, x, m);
+            else lb4_one(p, b, hash, now, o, g, x, m);
+        });
+    }
+    met_flush(m, p.metrics);
+}
+
+// ================================================================== egress state of a packet
+struct Eg4 {
+    Skb4 s;
+    Tuple4 t;                   // tuple before ct_lookup4(CT_EGRESS)
+    CtState stn;                // ct_state_new from the service stage
+};
+
+__device__ __forceinline__ void eg4_state(const Rec &r, const uint32_t *eg, Eg4 &x)
+{
+    x.s = skb4_from(r);
+    x.t.nexthdr = x.s.nexthdr;
+    x.t.saddr = x.s.saddr;
+    x.t.daddr = x.s.daddr;
+    x.t.dport = x.t.sport = 0;
+    x.stn = CtState{0, 0, 0, 0, 0, 0};
+    if (eg[0] & EG_SVC) {
+        x.t.daddr = eg[6];
+        x.s.daddr = eg[7];
+        x.s.saddr = eg[8];
+        if (eg[0] & EG_DPORT_RW) x.s.h.p2 = eg[2] >> 16;
+        x.stn.rev_nat = eg[3] & 0xFFFFu;
+        x.stn.slave = eg[3] >> 16;
+        x.stn.loopback = (eg[0] & EG_LOOPBACK) ? 1u : 0u;
+        x.stn.addr = eg[4];
+        x.stn.svc_addr = eg[5];
+    }
+}
+
+struct Eg6 {
+    Skb6 s;
+    Tuple6 t;
+    CtState stn;
+};
+
+__device__ __forceinline__ void eg6_state(const Rec6 &r, const uint32_t *eg, Eg6 &x)
+{
+    x.s = skb6_from(r);
+    if (eg[0] & EG_SVC) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x.s.daddr[j] = eg[12 + j];
+        if (eg[0] & EG_DPORT_RW) x.s.h.p2 = eg[2] >> 16;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x.t.daddr[j] = x.s.daddr[j]; x.t.saddr[j] = x.s.saddr[j]; }
+    x.t.nexthdr = x.s.nexthdr;
+    x.t.dport = x.t.sport = 0;
+    x.stn = CtState{eg[3] & 0xFFFFu, 0, eg[3] >> 16, 0, 0, 0};
+    if (!(eg[0] & EG_SVC)) x.stn = CtState{0, 0, 0, 0, 0, 0};
+}
+
+// ================================================================== pairs -> components
+// Every conntrack entry a packet can read or write outside the service set
+// contains one of the address pairs unioned here (SURVEY.md §7 hard part 1).
+__global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; continue; }
+        const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+        Acct na{0, 0};                                            // speculative probes are not accounted
+        if (!(eg[0] & EG_V6)) {
+            Rec r;
+            rec_load(r, b, i, 4);
+            Eg4 x;
+            eg4_state(r, eg, x);
+            const uint32_t S = x.t.saddr;
+            const uint32_t P = group_node(g, pair_hash4(S, x.t.daddr, SALT_CT4));
+            g.gslot[i] = P;
+            // local delivery sees the packet after the service / loopback rewrites
+            uf_union(g, P, group_node(g, pair_hash4(x.s.saddr, x.s.daddr, SALT_CT4)));
+            if (x.stn.addr) {                                     // the NATed tuple ct_create4 writes
+                const uint32_t other = x.stn.loopback ? x.stn.svc_addr : x.t.daddr;
+                uf_union(g, P, group_node(g, pair_hash4(x.stn.addr, other, SALT_CT4)));
+                uint32_t na4, np;                                 // its reply's rev-NAT target
+                if (x.stn.loopback && revnat4(p, x.stn.rev_nat, na4, np, na))
+                    uf_union(g, P, group_node(g, pair_hash4(na4, S, SALT_CT4)));
+            }
+            // the entry lookup 1 would hit today: a REPLY with rev-NAT rewrites the packet
+            Tuple4 t1 = x.t;
+            uint32_t seen;
+            if (ct_l4<false>(t1, x.s.h, CT_EGRESS, seen) >= 0 && ep.ct4.buckets) {
+                uint32_t k[4];
+                t1.key(k);
+                const int64_t sl = dev_find<Ct4Spec>(ep.ct4, k, nullptr);
+                if (sl >= 0) {
+                    CtE e;
+                    ct_load(ep.ct4, sl, e);
+                    uint32_t na4, np;
+                    if ((e.w[9] >> 16) && revnat4(p, e.w[9] >> 16, na4, np, na)) {
+                        const bool lb = e.bits() & CTB_LB_LOOPBACK;
+                        uf_union(g, P, group_node(g, pair_hash4(na4, lb ? x.s.saddr : x.s.daddr, SALT_CT4)));
+                    }
+                }
+            }
+        } else {
+            Rec6 r;
+            rec_load(r, b, i, 8);
+            Eg6 x;
+            eg6_state(r, eg, x);
+            const uint32_t P = group_node(g, pair_hash6(x.t.saddr, x.t.daddr, SALT_CT6));
+            g.gslot[i] = P;
+            uint32_t xs[4] = {x.s.saddr[0], x.s.saddr[1], x.s.saddr[2], x.s.saddr[3]};
+            Tuple6 t1 = x.t;
+            uint32_t seen;
+            if (x.s.l4off >= 0 && ct_l4<true>(t1, x.s.h, CT_EGRESS, seen) >= 0) {
+                uint32_t k[10];
+                t1.key(k);
+                const int64_t sl = dev_find<Ct6Spec>(ep.ct6, k, nullptr);
+                if (sl >= 0) {
+                    CtE e;
+                    ct_load(ep.ct6, sl, e);
+                    uint32_t na6[4], np;
+                    if ((e.w[9] >> 16) && revnat6(p, e.w[9] >> 16, na6, np, na)) {
+                        uf_union(g, P, group_node(g, pair_hash6(na6, x.s.daddr, SALT_CT6)));
+                        xs[0] = na6[0]; xs[1] = na6[1]; xs[2] = na6[2]; xs[3] = na6[3];
+                    }
+                }
+            }
+            // an entry the destination's ipv6_policy creates carries rev_nat_index =
+            // low 16 bits of the destination address; a reply through it is rev-NATed
+            uint32_t na6[4], np;
+            if ((x.s.daddr[3] & 0xFFFFu) && revnat6(p, x.s.daddr[3] & 0xFFFFu, na6, np, na)) {
+                uf_union(g, P, group_node(g, pair_hash6(na6, x.t.saddr, SALT_CT6)));
+                uf_union(g, P, group_node(g, pair_hash6(na6, xs, SALT_CT6)));
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_group_link(BatchDev b, GroupScratch g)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint32_t s = g.gslot[i];
+        if (s == NONE) { g.next[i] = NONE; continue; }
+        group_push(g, uf_find(g, s), i);
+    }
+}
+
+// ================================================================== egress conntrack + delivery
+// handle_ipv4_from_lxc (bpf_lxc.c:464-649) from skip_service_lookup on
+__device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                            const GroupScratch &g, uint32_t i, Met &m)
+{
+    Rec r;
+    rec_load(r, b, i, 4);
+    const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
+    Eg4 x;
+    eg4_state(r, eg, x);
+    Skb4 &s = x.s;
+    Tuple4 &t = x.t;
+    CtState st{0, 0, 0, 0, 0, 0};
+    int64_t slot;
+    const uint32_t orig_dip = t.daddr;
+    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a);
+    int verdict;
+    uint32_t iv;
+    if (ret < 0) goto drop;
+    res.ct = (uint8_t)ret;
+    {                                                             // destination category (:482-494)
+        const uint32_t lab = ipcache4(p, orig_dip, a);
+        res.dst = lab ? lab : ((orig_dip & p.v4_cluster_mask) == p.v4_cluster_range ? CLUSTER_ID : WORLD_ID);
+    }
+    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) { dev_kill<Ct4Spec>(ep.ct4, slot); a.nu++; }   // ct_delete4
+        ret = verdict;
+        goto drop;
+    }
+    if (ret == CT_NEW) {
+        x.stn.src_sec_id = ep.seclabel;
+        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a);
+        if (is_err(c)) { ret = c; goto drop; }
+    } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
+        uint32_t na, np;
+        if (revnat4(p, st.rev_nat, na, np, a)) {
+            const int r2 = rev_map_port(s.h, t.nexthdr, np);
+            if (r2) { ret = r2; goto drop; }
+            const uint32_t old_sip = s.saddr;
+            if (st.loopback) s.daddr = old_sip;
+            s.saddr = na;
+        }
+    }
+    if (verdict > 0) {                                            // ipv4_redirect_to_host_port + ipv4_l3
+        res.proxy = (uint16_t)verdict;
+        if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }
+        res.ret = TC_ACT_REDIRECT;
+        eg_final(o, i, res, a);
+        return;
+    }
+    if (lxc4_find(p, s.daddr, iv, a)) {
+        if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
+        m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
+        if (iv & (1u << 16)) { res.ret = TC_ACT_REDIRECT; eg_final(o, i, res, a); return; }
+        const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
+        if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
+        uint8_t ct2 = CT_NONE;
+        res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, (iv >> 17) & 1u, now, ct2, res.proxy,
+                                 res.reason, a, m);
+        eg_final(o, i, res, a);
+        return;
+    }
+    if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }            // pass_to_stack: ipv4_l3
+    m.fwd(s.len, METRIC_EGRESS);                                  // TRACE_TO_STACK
+    res.ret = TC_ACT_OK;
+    eg_final(o, i, res, a);
+    return;
+drop:
+    eg_drop(res, ret, s.len, m);
+    eg_final(o, i, res, a);
+}
+
+// ipv6_l3_from_lxc (bpf_lxc.c:133-352) from skip_service_lookup on
+__device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                            const GroupScratch &g, uint32_t i, Met &m)
+{
+    Rec6 r;
+    rec_load(r, b, i, 8);
+    const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
+    Eg6 x;
+    eg6_state(r, eg, x);
+    Skb6 &s = x.s;
+    Tuple6 &t = x.t;
+    CtState st{0, 0, 0, 0, 0, 0};
+    int64_t slot;
+    const uint32_t orig_dip[4] = {t.daddr[0], t.daddr[1], t.daddr[2], t.daddr[3]};
+    int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a);
+    int verdict;
+    uint32_t iv;
+    if (ret < 0) goto drop;
+    res.ct = (uint8_t)ret;
+    {
+        const uint32_t lab = ipcache6(p, orig_dip, a);
+        res.dst = lab ? lab
+                      : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
+    }
+    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+        if (ret == CT_ESTABLISHED) { dev_kill<Ct6Spec>(ep.ct6, slot); a.nu++; }
+        ret = verdict;
+        goto drop;
+    }
+    if (ret == CT_NEW) {
+        x.stn.src_sec_id = ep.seclabel;
+        const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a);
+        if (is_err(c)) { ret = c; goto drop; }
+    } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
+        uint32_t na[4], np;
+        if (revnat6(p, st.rev_nat, na, np, a)) {
+            const int r2 = rev_map_port(s.h, t.nexthdr, np);
+            if (r2) { ret = r2; goto drop; }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s.saddr[j] = na[j];
+        }
+    }
+    if (verdict > 0) {                                            // ipv6_redirect_to_host_port + ipv6_l3
+        res.proxy = (uint16_t)verdict;
+        if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
+        res.ret = TC_ACT_REDIRECT;
+        eg_final(o, i, res, a);
+        return;
+    }
+    if (lxc6_find(p, s.daddr, iv, a)) {
+        if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
+        m.fwd(s.len, METRIC_EGRESS);
+        if (iv & (1u << 16)) { res.ret = TC_ACT_REDIRECT; eg_final(o, i, res, a); return; }
+        const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
+        if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
+        uint8_t ct2 = CT_NONE;
+        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, (iv >> 17) & 1u, now, ct2, res.proxy, res.reason,
+                                 a, m);
+        eg_final(o, i, res, a);
+        return;
+    }
+    if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
+    m.fwd(s.len, METRIC_EGRESS);
+    res.ret = TC_ACT_OK;
+    eg_final(o, i, res, a);
+    return;
+drop:
+    eg_drop(res, ret, s.len, m);
+    eg_final(o, i, res, a);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
+{
+    __shared__ LdsMetrics lm;
+    Met m;
+    met_init(m, lm);
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint32_t s = g.gslot[i];
+        if (s == NONE || g.next[i] != NONE) continue;
+        const uint32_t head = (uint32_t)g.table[2 * s + 1];
+        group_in_order(g, head, [&](uint32_t x) {
+            if (g.eg[(size_t)x * EG_WORDS] & EG_V6) egress6_one(p, b, now, o, g, x, m);
+            else egress4_one(p, b, now, o, g, x, m);
+        });
+    }
+    met_flush(m, p.metrics);
+}
+
+// ================================================================== launcher
+// g.epoch and g.epoch + 1 are used (service groups, conntrack groups).
+int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
+                      const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s)
+{
+    if (!b.n) return 0;
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
+    if (b.stride >= 128) hipLaunchKernelGGL(k_egress_front<32>, grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+    else hipLaunchKernelGGL(k_egress_front<16>, grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+    hipLaunchKernelGGL(k_lb_stage, grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    g.epoch += 1;
+    hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
+    hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
+    hipLaunchKernelGGL(k_egress_ct, grid, blk, 0, s, p, b, now, o, g);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace cv

@@ -46,6 +46,9 @@ using Cidr4Spec  = HashSpec<1, 0, 8, 16>;   // /32 deny set (v4_fix)
 using Cidr6Spec  = HashSpec<4, 0, 7, 32>;   // /128 deny set (v6_fix)
 using PolicySpec = HashSpec<2, 0, 5, 16, 1>; // policy_key (8 B) -> inline proxy_port; side array policy_entry (stride 32)
 using Ct4Spec    = HashSpec<4, 0, 7, 32>;   // ipv4_ct_tuple (14 B + 2 zero) -> side array ct_entry (stride 64)
+using Ct6Spec    = HashSpec<10, 0, 3, 32>;  // ipv6_ct_tuple (40 B) -> side array ct_entry (stride 64)
+using Lb4Spec    = HashSpec<2, 3, 6, 32>;   // lb4_key (8 B) -> lb4_service (12 B) inline
+using Lb6Spec    = HashSpec<5, 6, 4, 64>;   // lb6_key (20 B) -> lb6_service (24 B) inline
 using Lpm6Spec   = HashSpec<5, 1, 5, 32>;   // (masked v6 addr, plen) -> value
 
 CV_HD uint32_t tag_of(uint64_t h)

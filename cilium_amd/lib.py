@@ -21,8 +21,9 @@ MAP_HASH, MAP_LRU_HASH, MAP_LPM_TRIE, MAP_PERCPU_HASH = 1, 9, 11, 5
 BPF_F_NO_PREALLOC = 1
 ROLE_CIDR4_FIX, ROLE_CIDR4_DYN, ROLE_CIDR6_FIX, ROLE_CIDR6_DYN = 0, 1, 2, 3
 ROLE_LXC, ROLE_IPCACHE, ROLE_LB4_SERVICES, ROLE_LB6_SERVICES = 4, 5, 6, 7
+ROLE_LB4_REVNAT, ROLE_LB6_REVNAT = 8, 9
 ROLES = {"v4_fix": 0, "v4_dyn": 1, "v6_fix": 2, "v6_dyn": 3, "lxc": 4, "ipcache": 5,
-         "lb4_services": 6, "lb6_services": 7}
+         "lb4_services": 6, "lb6_services": 7, "lb4_revnat": 8, "lb6_revnat": 9}
 F_FROM_HOST, F_HAVE_L4_POLICY, F_DROP_ALL, F_CT_ACCOUNTING = 0x1, 0x2, 0x4, 0x8
 F_POLICY_INGRESS, F_POLICY_EGRESS, F_DEFAULT = 0x10, 0x20, 0x3B
 
@@ -38,9 +39,27 @@ class Batch(C.Structure):
                 ("n", C.c_uint32)]
 
 
+OUT_FIELDS = ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason")
+
+
 class Out(C.Structure):
-    _fields_ = [("xdp", C.c_void_p), ("ret", C.c_void_p), ("identity", C.c_void_p), ("ct", C.c_void_p),
-                ("proxy", C.c_void_p), ("nl", C.c_void_p), ("nu", C.c_void_p)]
+    _fields_ = [(k, C.c_void_p) for k in OUT_FIELDS]
+
+
+class EndpointCfg(C.Structure):
+    _fields_ = [("ipv4", C.c_uint32), ("ipv6", C.c_uint8 * 16), ("mac", C.c_uint8 * 6),
+                ("node_mac", C.c_uint8 * 6), ("ct6_map", C.c_int)]
+
+
+class NodeCfg(C.Structure):
+    _fields_ = [("ipv4_cluster_mask", C.c_uint32), ("ipv4_cluster_range", C.c_uint32),
+                ("ipv4_loopback", C.c_uint32), ("router_ip6", C.c_uint8 * 16)]
+
+
+def _raw_be32(v):
+    """a host-order IPv4 int as the raw network-order word the C-ABI takes"""
+    import struct
+    return struct.unpack("<I", struct.pack(">I", v))[0]
 
 
 def header_functions():
@@ -79,6 +98,9 @@ def load():
         "cv_xdp_prefilter": (i32, [vp, C.POINTER(Batch), C.POINTER(Out), vp]),
         "cv_policy_ingress": (i32, [vp, i32, C.POINTER(Batch), C.POINTER(Out), vp]),
         "cv_netdev_ingress": (i32, [vp, C.POINTER(Batch), u32, i32, C.POINTER(Out), vp]),
+        "cv_lxc_egress": (i32, [vp, C.POINTER(Batch), vp, u32, vp, u32, C.POINTER(Out), vp]),
+        "cv_endpoint_config": (i32, [vp, i32, C.POINTER(EndpointCfg)]),
+        "cv_node_config": (i32, [vp, C.POINTER(NodeCfg)]),
         "cv_metrics_read": (i32, [vp, vp]),
         "cv_metrics_reset": (i32, [vp]),
         "cv_metrics_device_ptr": (vp, [vp]),
@@ -195,6 +217,18 @@ class Ctx:
         return _check(load().cv_endpoint_add(self.h, lxc_id, seclabel, -1 if policy is None else policy.h,
                                              -1 if ct4 is None else ct4.h), "cv_endpoint_add")
 
+    def endpoint_config(self, ep, ipv4=0, ipv6=bytes(16), mac=bytes(6), node_mac=bytes(6), ct6=None):
+        """lxc_config.h constants of endpoint `ep` (ipv4 as a host-order int) and its CT_MAP6."""
+        cfg = EndpointCfg(_raw_be32(ipv4), (C.c_uint8 * 16)(*bytes(ipv6)), (C.c_uint8 * 6)(*bytes(mac)),
+                          (C.c_uint8 * 6)(*bytes(node_mac)), -1 if ct6 is None else ct6.h)
+        _check(load().cv_endpoint_config(self.h, ep, C.byref(cfg)), "cv_endpoint_config")
+
+    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=bytes(16)):
+        """node_config.h constants; the v4 words as host-order ints."""
+        cfg = NodeCfg(_raw_be32(cluster_mask), _raw_be32(cluster_range), _raw_be32(loopback),
+                      (C.c_uint8 * 16)(*bytes(router_ip6)))
+        _check(load().cv_node_config(self.h, C.byref(cfg)), "cv_node_config")
+
     def sync(self):
         _check(load().cv_sync(self.h), "cv_sync")
 
@@ -207,7 +241,7 @@ class Ctx:
     @staticmethod
     def _out(o):
         o = o or {}
-        return Out(*[None if o.get(k) is None else o[k].data_ptr() for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu")])
+        return Out(*[None if o.get(k) is None else o[k].data_ptr() for k in OUT_FIELDS])
 
     def xdp_prefilter(self, frames, length, out):
         b, o = self._batch(frames, length), self._out(out)
@@ -221,6 +255,11 @@ class Ctx:
         b, o = self._batch(frames, length, mark), self._out(out)
         _check(load().cv_netdev_ingress(self.h, C.byref(b), now, 1 if with_prefilter else 0, C.byref(o), _stream()),
                "cv_netdev_ingress")
+
+    def lxc_egress(self, frames, length, out, now, src_ep=None, flow_hash=None, ep0=0):
+        b, o = self._batch(frames, length), self._out(out)
+        _check(load().cv_lxc_egress(self.h, C.byref(b), _ptr(src_ep), ep0, _ptr(flow_hash), now, C.byref(o),
+                                    _stream()), "cv_lxc_egress")
 
     def metrics(self):
         m = np.zeros((256, 4, 2), np.uint64)

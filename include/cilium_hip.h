@@ -57,9 +57,11 @@ typedef struct cv_ctx cv_ctx;
 #define CV_ROLE_CIDR6_DYN   3   /* v6_dyn  LPM  lpm_v6_key->lpm_val   (bpf_xdp.c:77-84)  */
 #define CV_ROLE_LXC         4   /* cilium_lxc endpoint_key->endpoint_info (maps.h:27-33) */
 #define CV_ROLE_IPCACHE     5   /* cilium_ipcache ipcache_key->remote_endpoint_info (maps.h:151-158) */
-#define CV_ROLE_LB4_SERVICES 6  /* cilium_lb4_services (lb.h:75-81)  */
-#define CV_ROLE_LB6_SERVICES 7  /* cilium_lb6_services (lb.h:43-49)  */
-#define CV_NUM_ROLES        8
+#define CV_ROLE_LB4_SERVICES 6  /* cilium_lb4_services lb4_key->lb4_service (lb.h:75-81) */
+#define CV_ROLE_LB6_SERVICES 7  /* cilium_lb6_services lb6_key->lb6_service (lb.h:43-49) */
+#define CV_ROLE_LB4_REVNAT  8   /* cilium_lb4_reverse_nat u16->lb4_reverse_nat (lb.h:67-73) */
+#define CV_ROLE_LB6_REVNAT  9   /* cilium_lb6_reverse_nat u16->lb6_reverse_nat (lb.h:37-41) */
+#define CV_NUM_ROLES        10
 
 /* ---- datapath options (compile-time #defines of the reference) ---- */
 #define CV_F_FROM_HOST       0x1   /* netdev_config.h FROM_HOST                     */
@@ -77,6 +79,8 @@ typedef struct cv_ctx cv_ctx;
 #define CV_TC_ACT_SHOT 2
 #define CV_TC_ACT_REDIRECT 7
 #define CV_E_TRUNC (-1)      /* a header byte the path reads lies beyond the record */
+#define CV_E_PUNT  (-2)      /* left the path through a tail call into a responder program
+                                (ARP, ICMPv6 NS / echo to the router, hop limit exceeded) */
 #define CV_CT_NONE 0xff
 
 /* ---- context ----
@@ -107,8 +111,30 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
 /* ---- binding: programs -> maps ---- */
 int cv_bind(cv_ctx *ctx, int role, int map_handle /* -1 unbinds */);
 /* tail-call target cilium_policy[lxc_id] (maps.h:44-51): endpoint policy map and
- * CT_MAP4 (bpf_lxc.c:65-75).  Returns the endpoint index or -errno. */
+ * CT_MAP4 (bpf_lxc.c:65-75).  Returns the endpoint index or -errno.  Its program
+ * constants (LXC_IPV4, ...) and CT_MAP6 come from cv_endpoint_config. */
 int cv_endpoint_add(cv_ctx *ctx, uint16_t lxc_id, uint32_t seclabel, int policy_map, int ct4_map);
+/* the endpoint program's lxc_config.h constants (pkg/endpoint/bpf.go:152-200) and
+ * its CT_MAP6 (bpf_lxc.c:53-63); addresses in network order.  ipv4 == 0: the
+ * endpoint has no IPv4 programs (no LXC_IPV4). */
+typedef struct {
+    uint32_t ipv4;            /* LXC_IPV4, raw network-order word */
+    uint8_t  ipv6[16];        /* LXC_IP */
+    uint8_t  mac[6];          /* LXC_MAC */
+    uint8_t  node_mac[6];     /* NODE_MAC */
+    int      ct6_map;         /* ipv6_ct_tuple -> ct_entry map, or -1 */
+} cv_endpoint_cfg;
+int cv_endpoint_config(cv_ctx *ctx, int ep, const cv_endpoint_cfg *cfg);
+
+/* node_config.h constants (raw network-order words; pkg/node/node_address.go) */
+typedef struct {
+    uint32_t ipv4_cluster_mask;   /* IPV4_CLUSTER_MASK  */
+    uint32_t ipv4_cluster_range;  /* IPV4_CLUSTER_RANGE */
+    uint32_t ipv4_loopback;       /* IPV4_LOOPBACK      */
+    uint8_t  router_ip6[16];      /* ROUTER_IP          */
+} cv_node_cfg;
+int cv_node_config(cv_ctx *ctx, const cv_node_cfg *cfg);
+
 /* make every pending map write visible to the next batch */
 int cv_sync(cv_ctx *ctx);
 
@@ -129,6 +155,7 @@ typedef struct {              /* any pointer may be NULL */
     uint16_t *proxy;          /* proxy port (network order) of an L7 redirect, else 0 */
     uint8_t  *nl;             /* map lookups the path performed (algorithmic-bytes accounting) */
     uint8_t  *nu;             /* map entry writes the path performed */
+    int32_t  *reason;         /* DROP_* code behind a TC_ACT_SHOT (the cilium_metrics reason), else 0 */
 } cv_out;
 
 /* config 1: bpf_xdp.c xdp_start over the batch */
@@ -140,6 +167,18 @@ int cv_policy_ingress(cv_ctx *ctx, int ep, const cv_batch *b, cv_out *o, void *s
  * conntrack, in packet order semantics; `now` = bpf_ktime_get_sec() of the batch */
 int cv_netdev_ingress(cv_ctx *ctx, const cv_batch *b, uint32_t now, int with_prefilter,
                       cv_out *o, void *stream);
+
+/* config 5: from-container (bpf_lxc.c:672-716 handle_ingress -> tail_handle_ipv4/6)
+ * of each packet's source endpoint: handle_ipv4_from_lxc / ipv6_l3_from_lxc with
+ * lb4/lb6 service lookup and lb{4,6}_local, egress conntrack and policy, and local
+ * delivery into the destination endpoint's policy program; direct routing.
+ * src_ep[i] = endpoint index (cv_endpoint_add order) of packet i, or NULL: all from
+ * ep0.  flow_hash[i] = the packet's get_hash_recalc() (the LB slave choice; the
+ * kernel's is keyed by a boot-random secret, so it is an input).  `identity` out =
+ * the destination identity (dstID), `ct` = the egress CT result.  IPv6 needs
+ * records of >= 128 bytes.  Device pointers. */
+int cv_lxc_egress(cv_ctx *ctx, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0,
+                  const uint32_t *flow_hash, uint32_t now, cv_out *o, void *stream);
 
 /* ---- cilium_metrics (metrics.h:43-58): dense [256 reasons][4 dirs]{count, bytes} u64,
  * device resident.  Read sums it to host; the device pointer lets a caller reduce it

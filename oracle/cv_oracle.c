@@ -1306,7 +1306,10 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;
         *final = 1;                                                 /* handle_policy -> tail_ipv4_policy */
-        return handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
+        uint8_t ct_egress = ps->ct;                                 /* out.ct reports the egress CT result */
+        r = handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
+        ps->ct = ct_egress;
+        return r;
     }
     int r = ipv4_l3(skb);                                           /* pass_to_stack */
     if (r != OR_TC_ACT_OK) return r;
@@ -1664,7 +1667,10 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;
         *final = 1;
-        return handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
+        uint8_t ct_egress = ps->ct;
+        r = handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
+        ps->ct = ct_egress;
+        return r;
     }
     int r = ipv6_l3(skb);                                           /* pass_to_stack */
     if (r != OR_TC_ACT_OK) return r;

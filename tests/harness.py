@@ -48,8 +48,12 @@ def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True):
             ctx.bind(name, maps[name])
     pol = maps.get("policy")
     ct = maps.get("ct4") if with_ct else None
+    ct6 = maps.get("ct6") if with_ct else None
     for e in w.endpoints:
-        ctx.endpoint_add(e["lxc_id"], e["seclabel"], pol, ct)
+        i = ctx.endpoint_add(e["lxc_id"], e["seclabel"], pol, ct)
+        ctx.endpoint_config(i, ct6=ct6, **_ep_cfg(e))
+    if w.extra and "node" in w.extra:
+        ctx.node_config(**w.extra["node"])
     ctx.sync()
     return ctx, maps
 
@@ -63,6 +67,15 @@ def to_dev(w: synth.Workload, device="cuda:0", lo=0, hi=None):
     return frames, length, mark
 
 
+def egress_inputs(w: synth.Workload, device="cuda:0", lo=0, hi=None):
+    """src_ep (int16 view of the u16 endpoint indexes) and flow_hash (int32 view) on the device."""
+    import torch
+    hi = w.n if hi is None else hi
+    src = torch.from_numpy(np.ascontiguousarray(w.extra["src_ep"][lo:hi]).view(np.int16)).to(device)
+    fh = torch.from_numpy(np.ascontiguousarray(w.extra["flow_hash"][lo:hi]).view(np.int32)).to(device)
+    return src, fh
+
+
 def dev_out(n, device="cuda:0"):
     import torch
     return {
@@ -73,6 +86,7 @@ def dev_out(n, device="cuda:0"):
         "proxy": torch.zeros(n, dtype=torch.int16, device=device),
         "nl": torch.zeros(n, dtype=torch.uint8, device=device),
         "nu": torch.zeros(n, dtype=torch.uint8, device=device),
+        "reason": torch.zeros(n, dtype=torch.int32, device=device),
     }
 
 

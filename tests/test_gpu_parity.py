@@ -147,7 +147,7 @@ def check_ingress(w, dev, batches, with_prefilter=True):
         o = run_ingress(ctx, w, dev, lo, hi, with_prefilter)
         ref = dp.netdev_ingress(w.frames[lo:hi], w.length[lo:hi], w.mark[lo:hi], now=w.now,
                                 with_prefilter=with_prefilter)
-        for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu"):
+        for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
             bad = np.nonzero(o[k] != getattr(ref, k))[0]
             assert len(bad) == 0, (k, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
     assert (ctx.metrics() == dp.metrics()).all()

@@ -34,6 +34,8 @@ WORKLOADS = {
     "config2": "ipcache LPM (100k CIDRs->identities) + policymap (10k identities x L4 ports) ingress verdicts",
     "config1": "bpf_xdp.c CIDR deny-list prefilter, 1k IPv4 prefixes + cilium_lxc",
     "config3": "full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + ct_lookup4/ct_create4, 16M-flow CT",
+    "config5": "dual-stack from-container egress: lb4/lb6 (50k services) + CT4/CT6 + egress policy + local delivery "
+               "(v4 64-B and v6 128-B records, 1:1)",
 }
 
 
@@ -55,13 +57,28 @@ def make_workload(name, n, rank):
         return synth.config1(n)
     if name == "config3":
         return synth.config3(n, n_flows=1 << 24)
+    if name == "config5":
+        return synth.config5(n)
     raise SystemExit(f"unknown workload {name}")
 
 
-def algorithmic_bytes(name, nl, nu):
+def split_families(w):
+    """config 5: the v4 packets as 64-B records and the v6 packets as 128-B records
+    (two launches per step; v4 and v6 state are disjoint, so order between them is free)."""
+    import numpy as np
+    v6 = w.extra["v6"]
+    parts = []
+    for sel, stride in ((~v6, 64), (v6, 128)):
+        idx = np.nonzero(sel)[0]
+        parts.append({"frames": np.ascontiguousarray(w.frames[idx, :stride]), "length": w.length[idx],
+                      "src_ep": w.extra["src_ep"][idx], "flow_hash": w.extra["flow_hash"][idx]})
+    return parts
+
+
+def algorithmic_bytes(name, nl, nu, record=64):
     """B(p) = R + V + 64*L(p) + 64*U(p), summed over the batch."""
-    R = 64
-    V = {"config1": 4, "config2": 8, "config3": 9}[name]
+    R = record
+    V = {"config1": 4, "config2": 8, "config3": 9, "config5": 9}[name]
     n = len(nl)
     return n * (R + V) + 64 * (int(nl.astype(np.int64).sum()) + int(nu.astype(np.int64).sum()))
 
@@ -79,6 +96,11 @@ def cpu_baseline(name, w, min_seconds=10.0):
         run = lambda: dp.xdp_prefilter(frames, length)
     elif name == "config2":
         run = lambda: dp.policy_ingress(0, frames, length, mark)
+    elif name == "config5":
+        sample = min(sample, 1 << 18)
+        src, fh = w.extra["src_ep"][:sample], w.extra["flow_hash"][:sample]
+        frames, length = frames[:sample], length[:sample]
+        run = lambda: dp.lxc_egress(frames, length, src, fh, now=w.now)
     else:
         sample = min(sample, 1 << 18)
         frames, length, mark = frames[:sample], length[:sample], mark[:sample]
@@ -88,12 +110,13 @@ def cpu_baseline(name, w, min_seconds=10.0):
         run()
         done += sample
         el = time.perf_counter() - t0
-        if el >= min_seconds or name == "config3":
+        if el >= min_seconds or name in ("config3", "config5"):
             break
-    return {"value": round(done / el / 1e6, 3), "unit": "Mpps", "cores": threads if name != "config3" else 1,
+    seq = name in ("config3", "config5")
+    return {"value": round(done / el / 1e6, 3), "unit": "Mpps", "cores": 1 if seq else threads,
             "kind": "port",
             "sample": f"oracle/cv_oracle.c over {done} packets of the same synthetic {name} batch "
-                      f"({el:.1f} s, {'OpenMP ' + str(threads) + ' threads' if name != 'config3' else '1 thread, sequential'})"}
+                      f"({el:.1f} s, {'1 thread, sequential (stateful path)' if seq else 'OpenMP ' + str(threads) + ' threads'})"}
 
 
 def pmc_traffic(name, sha):
@@ -143,22 +166,40 @@ def main():
     w = make_workload(name, args.packets, rank)
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
     ctx, maps = H.product_ctx(w, device=local)
+    log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")
     metrics_t = torch.zeros(2048, dtype=torch.int64, device=device)
     ctx.metrics_attach(metrics_t)
-    frames, length, mark = H.to_dev(w, device)
     n = w.n
     out = {"ret": torch.empty(n, dtype=torch.int32, device=device),
            "identity": torch.empty(n, dtype=torch.int32, device=device)}
     if name == "config1":
         out = {"xdp": torch.empty(n, dtype=torch.uint8, device=device)}
-    if name == "config3":
+    if name in ("config3", "config5"):
         out["ct"] = torch.empty(n, dtype=torch.uint8, device=device)
+    if name == "config5":
+        parts = []
+        for part in split_families(w):
+            t = {}
+            for k, v in part.items():
+                if v.dtype == np.uint16 or (k == "flow_hash" and v.dtype == np.uint32):
+                    v = v.view(np.int16 if v.dtype == np.uint16 else np.int32)
+                t[k] = torch.from_numpy(np.ascontiguousarray(v)).to(device)
+            t["rows"] = len(part["length"])
+            parts.append(t)
+        offs = [0, parts[0]["rows"]]
+    else:
+        frames, length, mark = H.to_dev(w, device)
 
     def step(o):
         if name == "config1":
             ctx.xdp_prefilter(frames, length, o)
         elif name == "config2":
             ctx.policy_ingress(0, frames, length, o, mark=mark)
+        elif name == "config5":
+            for part, off in zip(parts, offs):
+                sub = {k: v[off:off + part["rows"]] for k, v in o.items()}
+                ctx.lxc_egress(part["frames"], part["length"], sub, w.now, src_ep=part["src_ep"],
+                               flow_hash=part["flow_hash"])
         else:
             ctx.netdev_ingress(frames, length, o, w.now, mark=mark)
 
@@ -168,12 +209,19 @@ def main():
     acct["nu"] = torch.zeros(n, dtype=torch.uint8, device=device)
     step(acct)
     torch.cuda.synchronize()
-    alg_bytes = algorithmic_bytes(name, acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy())
+    nl, nu = acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy()
+    log(f"[rank {rank}] accounting pass done ({time.time() - t0:.1f}s)")
+    if name == "config5":
+        k4 = offs[1]
+        alg_bytes = algorithmic_bytes(name, nl[:k4], nu[:k4], 64) + algorithmic_bytes(name, nl[k4:], nu[k4:], 128)
+    else:
+        alg_bytes = algorithmic_bytes(name, nl, nu)
     del acct
 
     for _ in range(args.warmup):
         step(out)
     torch.cuda.synchronize()
+    log(f"[rank {rank}] warmup done ({time.time() - t0:.1f}s)")
 
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -225,7 +273,7 @@ def main():
             "config": {
                 "workload": f"{name}: {WORKLOADS[name]}",
                 "packets_per_step_per_gpu": n,
-                "header_bytes": int(w.frames.shape[1]),
+                "header_bytes": "64 (v4) / 128 (v6)" if name == "config5" else int(w.frames.shape[1]),
                 "parallelism": f"replicated tables, {world} GPU(s), batch per GPU",
                 "tables": {k: len(v) for k, v in w.maps.items()},
             },

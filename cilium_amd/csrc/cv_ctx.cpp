@@ -157,10 +157,11 @@ struct cv_ctx {
     DevBuf eps_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
-    DevBuf gtable, gslot, gnext, gsecctx, gmeta, gparent, geg;
+    DevBuf gtable, gslot, gnext, gsecctx, gmeta, gparent, geg, gorder, gcursor, gqueue;
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
+    uint32_t serial = 0;       // launches so far (GroupScratch::serial)
     DevBuf ctio;
     uint32_t next_ct_id = 1;
     uint32_t chunk = MAX_CHUNK;    // packets per launch (CV_MAX_CHUNK env may lower it, tests)
@@ -615,7 +616,9 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     while (cap < per * cmax || cap < c->gcap) cap <<= 1;
     (void)hipDeviceSynchronize();
     if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
-        c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4))
+        c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4) ||
+        c->gorder.alloc((size_t)cmax * 4) || c->gcursor.alloc(CURSOR_WORDS * 4) ||
+        c->gqueue.alloc(((size_t)cmax / QSPLIT + 512) * QSPLIT * 4))
         return -ENOMEM;
     (void)hipMemset(c->gtable.p, 0, cap * 16);
     if (egress || c->g_egress) {
@@ -639,7 +642,10 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
     }
     GroupScratch gs{c->gtable.as<unsigned long long>(), (uint32_t)(c->gcap - 1), c->epoch + 1,
                     c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(),
-                    c->gmeta.as<uint32_t>(), c->gparent.as<unsigned long long>(), c->geg.as<uint32_t>()};
+                    c->gmeta.as<uint32_t>(), c->gparent.as<unsigned long long>(), c->geg.as<uint32_t>(),
+                    ++c->serial, c->gorder.as<uint32_t>(), c->gcursor.as<uint32_t>(), c->gqueue.as<uint32_t>(),
+                    (uint32_t)(c->gn / QSPLIT + 512)};
+    (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
 }
@@ -1092,7 +1098,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     const DpParams p = params(c);
     for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
         const uint32_t n = std::min(c->chunk, b->n - off);
-        GroupScratch gs = next_groups(c, 2, (hipStream_t)stream);
+        GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
         if ((r = launch_lxc_egress(p, chunk(b, off, n), src_ep ? src_ep + off : nullptr, ep0,
                                    flow_hash ? flow_hash + off : nullptr, now, chunk(o, off), gs,
                                    (hipStream_t)stream)))

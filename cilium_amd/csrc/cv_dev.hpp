@@ -586,34 +586,47 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
     return true;
 }
 
-// ct_create4 / ct_create6 (conntrack.h:663-744 / 589-639): the entry, the NATed
-// tuple when ct_state->addr is set (v4 only), and the ICMP-RELATED twin
-template <bool V6, class T>
-__device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32_t len, int dir, const CtState &st,
-                                         uint32_t now, Acct &a)
+// the entry ct_create4 / ct_create6 write for `t` (conntrack.h:668-690 / 593-612)
+__device__ __forceinline__ void ct_entry_new(CtE &e, bool tcp, uint32_t len, int dir, const CtState &st, uint32_t now)
 {
-    CtE e;
 #pragma unroll
     for (int k = 0; k < 16; ++k) e.w[k] = 0;
-    const bool tcp = t.nexthdr == 6;
     e.w[9] = (st.rev_nat & 0xFFFFu) << 16 | (st.loopback ? CTB_LB_LOOPBACK : 0u);
     e.w[10] = st.slave & 0xFFFFu;
     ct_timeout(e, tcp, dir, tcp ? TCPF_SYN : 0u, now);
     if (dir == CT_INGRESS) { e.w[0] = 1; e.w[2] = len; }
     else                   { e.w[4] = 1; e.w[6] = len; }
     e.w[11] = st.src_sec_id;
+}
+
+// the NATed tuple ct_create4 writes when ct_state->addr is set (conntrack.h:697-725)
+__device__ __forceinline__ Tuple4 ct_nat_tuple(const Tuple4 &t, int dir, const CtState &st)
+{
+    Tuple4 n = t;
+    if (dir == CT_INGRESS) n.saddr = st.addr; else n.daddr = st.addr;
+    if (st.loopback) {
+        n.flags = TUPLE_F_IN;
+        if (dir == CT_INGRESS) n.daddr = st.svc_addr; else n.saddr = st.svc_addr;
+    }
+    return n;
+}
+
+// ct_create4 / ct_create6 (conntrack.h:663-744 / 589-639): the entry, the NATed
+// tuple when ct_state->addr is set (v4 only; with defer_nat the caller writes it
+// later, see k_nat_apply), and the ICMP-RELATED twin
+template <bool V6, class T>
+__device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32_t len, int dir, const CtState &st,
+                                         uint32_t now, Acct &a, bool defer_nat = false)
+{
+    CtE e;
+    const bool tcp = t.nexthdr == 6;
+    ct_entry_new(e, tcp, len, dir, st, now);
     const bool nat = !V6 && st.addr;
     a.nu += nat ? 3 : 2;
     if (!ct_put(ct, t, e)) return DROP_CT_CREATE_FAILED;
     if constexpr (!V6) {
-        if (nat) {
-            Tuple4 n = t;
-            if (dir == CT_INGRESS) n.saddr = st.addr; else n.daddr = st.addr;
-            if (st.loopback) {
-                n.flags = TUPLE_F_IN;
-                if (dir == CT_INGRESS) n.daddr = st.svc_addr; else n.saddr = st.svc_addr;
-            }
-            if (!ct_put(ct, n, e)) return DROP_CT_CREATE_FAILED;
+        if (nat && !defer_nat) {
+            if (!ct_put(ct, ct_nat_tuple(t, dir, st), e)) return DROP_CT_CREATE_FAILED;
         }
     }
     T it = t;
@@ -899,13 +912,66 @@ __device__ __forceinline__ uint32_t group_node(const GroupScratch &g, uint64_t g
     }
 }
 
-// push packet i on the list of node s
-__device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, uint32_t i)
+// the node of `gh` if some thread inserted it in this epoch, else NONE
+__device__ __forceinline__ uint32_t group_find(const GroupScratch &g, uint64_t gh)
+{
+    const uint32_t h32 = (uint32_t)gh | 1u;
+    const unsigned long long tagged = (unsigned long long)g.epoch << 32 | h32;
+    uint32_t s = (uint32_t)(gh >> 32) & g.cap_mask;
+    for (uint32_t probes = 0; probes <= g.cap_mask; ++probes) {
+        const unsigned long long cur = __hip_atomic_load(&g.table[2 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == tagged) return s;
+        if ((uint32_t)(cur >> 32) != g.epoch) return NONE;
+        s = (s + 1) & g.cap_mask;
+    }
+    return NONE;
+}
+
+// wave-aggregated append: one atomic per wave; returns the lane's index or NONE
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred)
+{
+    const unsigned long long m = __ballot(pred);
+    if (!m) return NONE;
+    const int leader = __ffsll((long long)m) - 1;
+    const int lane = (int)__lane_id();
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return pred ? base + (uint32_t)__popcll(m & ((1ull << lane) - 1)) : NONE;
+}
+
+// push packet i on the list of node s; the group's first member (the list tail)
+// enters the dense queue q, so the stage that runs the groups has one lane per group
+__device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, uint32_t i, int q)
 {
     const unsigned long long prev = __hip_atomic_exchange(&g.table[2 * s + 1], (unsigned long long)g.epoch << 32 | i,
                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     g.gslot[i] = s;
-    g.next[i] = (uint32_t)(prev >> 32) == g.epoch ? (uint32_t)prev : NONE;
+    const bool first = (uint32_t)(prev >> 32) != g.epoch;
+    g.next[i] = first ? NONE : (uint32_t)prev;
+    const uint32_t k = blockIdx.x % QSPLIT;
+    const uint32_t at = wave_append(&g.cursor[qctr(q, k)], first);
+    if (first) g.queue[(size_t)k * g.qregion + at] = s;
+}
+
+// for every queued group (its slot s and current list head): fn(s, head)
+template <class F>
+__device__ __forceinline__ void for_each_group(const GroupScratch &g, int q, F &&fn)
+{
+    uint32_t n[QSPLIT], total = 0;
+#pragma unroll
+    for (int k = 0; k < QSPLIT; ++k) {
+        n[k] = __hip_atomic_load(&g.cursor[qctr(q, k)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        total += n[k];
+    }
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
+        uint32_t r = j, k = 0;                                    // flat index -> (region, slot)
+#pragma unroll
+        for (int t = 0; t < QSPLIT - 1; ++t)
+            if (k == (uint32_t)t && r >= n[t]) { r -= n[t]; k = t + 1; }
+        const uint32_t s = g.queue[(size_t)k * g.qregion + r];
+        fn(s, (uint32_t)g.table[2 * s + 1]);
+    }
 }
 
 __device__ __forceinline__ uint32_t uf_parent(const GroupScratch &g, uint32_t s)
@@ -948,16 +1014,16 @@ __device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint
 constexpr int GMAX = 16;
 
 // Run fn(i) for every member of the group whose list starts at `head`, in
-// ascending packet order (<= GMAX sorted in registers, else repeated minimum).
+// ascending packet order: <= GMAX members are sorted in registers; larger groups
+// are copied to a slice of g.order (cursor `cur`) and shell-sorted there.
 template <class F>
-__device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t head, F &&fn)
+__device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t head, int cur, F &&fn)
 {
     if (g.next[head] == NONE) { fn(head); return; }
     uint32_t m[GMAX];
     int cnt = 0;
-    bool overflow = false;
-    for (uint32_t x = head; x != NONE; x = g.next[x]) {
-        if (cnt == GMAX) { overflow = true; break; }
+    uint32_t x = head;
+    for (; x != NONE && cnt < GMAX; x = g.next[x]) {
         int pos = 0;
 #pragma unroll
         for (int j = 0; j < GMAX; ++j) pos += (j < cnt && m[j] < x) ? 1 : 0;
@@ -968,7 +1034,7 @@ __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t h
         }
         ++cnt;
     }
-    if (!overflow) {
+    if (x == NONE) {
 #pragma unroll 1
         for (int j = 0; j < GMAX; ++j) {
             if (j >= cnt) break;
@@ -979,17 +1045,20 @@ __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t h
         }
         return;
     }
-    uint32_t last = 0;
-    bool first = true;
-    for (;;) {                                                     // repeated minimum scan
-        uint32_t best = NONE;
-        for (uint32_t x = head; x != NONE; x = g.next[x])
-            if ((first || x > last) && x < best) best = x;
-        if (best == NONE) break;
-        fn(best);
-        last = best;
-        first = false;
+    uint32_t total = GMAX;
+    for (uint32_t y = x; y != NONE; y = g.next[y]) ++total;
+    uint32_t *o = g.order + atomicAdd(&g.cursor[cur], total);
+    uint32_t k = 0;
+    for (uint32_t y = head; y != NONE; y = g.next[y]) o[k++] = y;
+    for (uint32_t gap = total / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {   // shell sort
+        for (uint32_t i = gap; i < total; ++i) {
+            const uint32_t v = o[i];
+            uint32_t j = i;
+            for (; j >= gap && o[j - gap] > v; j -= gap) o[j] = o[j - gap];
+            o[j] = v;
+        }
     }
+    for (uint32_t i = 0; i < total; ++i) fn(o[i]);
 }
 
 // node key of an unordered address pair (v4 words or v6 4-word addresses), mixed

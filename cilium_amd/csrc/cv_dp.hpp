@@ -74,7 +74,20 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *meta;            // per packet: ep index | skip_proxy << 16 | ifindex != 0 << 17
     unsigned long long *parent;// per table slot: epoch << 32 | union-find parent (egress path)
     uint32_t *eg;              // per packet: EG_WORDS words of egress scratch (egress path)
+    uint32_t serial;           // launch serial (never reset; tags deferred CT writes)
+    uint32_t *order;           // per packet: members of large groups, sorted in place
+    uint32_t *cursor;          // [CURSOR_WORDS] zeroed per launch: [0..2] cursors into `order`,
+                               // [qctr(q, k)] length of sub-queue k of queue q (one 128-B line each)
+    uint32_t *queue;           // dense lists of group slots (one lane per group), QSPLIT regions
+    uint32_t qregion;          // words per region
 };
+// GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
+// contention on one counter); blocks b with b % QSPLIT == k hold at most
+// n / QSPLIT + BLOCK + QSPLIT packets (grids are multiples of QSPLIT or one block per 256
+// packets), so a region of n / QSPLIT + 512 words never overflows.
+enum : int { Q_NETDEV = 0, Q_LB = 1, Q_CT = 2, Q_NAT = 3 };
+constexpr int QSPLIT = 16, CURSOR_WORDS = 32 + 4 * QSPLIT * 32;
+__host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT + k) * 32; }
 constexpr int EG_WORDS = 16;
 
 int launch_policy_fold(const HashTable &pol, hipStream_t s);

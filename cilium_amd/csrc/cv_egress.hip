@@ -26,10 +26,13 @@ int grid_for(uint32_t n);
 // egress scratch words (GroupScratch::eg, EG_WORDS per packet)
 enum : uint32_t {
     EG_STAGE = 0x3u, EG_V6 = 0x4u, EG_LOOPBACK = 0x8u, EG_SVC = 0x10u, EG_DPORT_RW = 0x20u,
+    EG_NAT_DEFER = 0x40u,       // the NATed tuple's pair is read by no packet of the launch
+    EG_NAT_DONE = 0x80u,        // ... and ct_create4 reached it: k_nat_apply writes it
 };
 enum : uint32_t { STAGE_DONE = 0, STAGE_LB = 1, STAGE_CT = 2 };
 constexpr uint64_t SALT_SVC4 = 0x5356433400000000ULL, SALT_SVC6 = 0x5356433600000000ULL,
-                   SALT_CT4 = 0x4354340000000000ULL, SALT_CT6 = 0x4354360000000000ULL;
+                   SALT_CT4 = 0x4354340000000000ULL, SALT_CT6 = 0x4354360000000000ULL,
+                   SALT_NAT = 0x4E41540000000000ULL;
 
 struct EgOut {                  // per-packet results on the way to the outputs
     int32_t ret, reason;
@@ -219,7 +222,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
                 } else {
                     gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ep.ct_id);
                 }
-                group_push(g, group_node(g, gh), i);
+                group_push(g, group_node(g, gh), i, Q_LB);
             }
         }
     }
@@ -412,15 +415,12 @@ __global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, cons
     __shared__ LdsMetrics lm;
     Met m;
     met_init(m, lm);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
-        const uint32_t s = g.gslot[i];
-        if (s == NONE || g.next[i] != NONE) continue;             // not a service packet / not the group's tail
-        const uint32_t head = (uint32_t)g.table[2 * s + 1];
-        group_in_order(g, head, [&](uint32_t x) {
+    for_each_group(g, Q_LB, [&](uint32_t, uint32_t head) {
+        group_in_order(g, head, 1, [&](uint32_t x) {
             if (g.eg[(size_t)x * EG_WORDS] & EG_V6) lb6_one(p, b, hash, now, o, g, x, m);
             else lb4_one(p, b, hash, now, o, g, x, m);
         });
-    }
+    });
     met_flush(m, p.metrics);
 }
 
@@ -475,8 +475,12 @@ __device__ __forceinline__ void eg6_state(const Rec6 &r, const uint32_t *eg, Eg6
 }
 
 // ================================================================== pairs -> components
-// Every conntrack entry a packet can read or write outside the service set
-// contains one of the address pairs unioned here (SURVEY.md §7 hard part 1).
+// Every conntrack entry a packet can read outside the service set contains one of
+// the address pairs unioned here (SURVEY.md §7 hard part 1).  The one entry it can
+// write outside them, the NATed tuple of a service create (daddr = backend, saddr
+// = backend), is a blind write: k_egress_nat merges it into the component only
+// when some packet reads its pair, else its write is deferred to k_nat_apply, which
+// resolves writers of one key last-writer-wins, as the sequential run does.
 __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
@@ -494,13 +498,9 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             g.gslot[i] = P;
             // local delivery sees the packet after the service / loopback rewrites
             uf_union(g, P, group_node(g, pair_hash4(x.s.saddr, x.s.daddr, SALT_CT4)));
-            if (x.stn.addr) {                                     // the NATed tuple ct_create4 writes
-                const uint32_t other = x.stn.loopback ? x.stn.svc_addr : x.t.daddr;
-                uf_union(g, P, group_node(g, pair_hash4(x.stn.addr, other, SALT_CT4)));
-                uint32_t na4, np;                                 // its reply's rev-NAT target
-                if (x.stn.loopback && revnat4(p, x.stn.rev_nat, na4, np, na))
-                    uf_union(g, P, group_node(g, pair_hash4(na4, S, SALT_CT4)));
-            }
+            uint32_t na4, np;                                     // a loopback NAT entry's reply rev-NAT target
+            if (x.stn.addr && x.stn.loopback && revnat4(p, x.stn.rev_nat, na4, np, na))
+                uf_union(g, P, group_node(g, pair_hash4(na4, S, SALT_CT4)));
             // the entry lookup 1 would hit today: a REPLY with rev-NAT rewrites the packet
             Tuple4 t1 = x.t;
             uint32_t seen;
@@ -553,12 +553,24 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
     }
 }
 
+__global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, GroupScratch g)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        if ((eg[0] & (EG_STAGE | EG_V6 | EG_SVC)) != (STAGE_CT | EG_SVC) || !eg[4]) continue;
+        const uint32_t other = (eg[0] & EG_LOOPBACK) ? eg[5] : eg[6];
+        const uint32_t nn = group_find(g, pair_hash4(eg[4], other, SALT_CT4));
+        if (nn != NONE) uf_union(g, g.gslot[i], nn);
+        else eg[0] |= EG_NAT_DEFER;
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) k_group_link(BatchDev b, GroupScratch g)
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         const uint32_t s = g.gslot[i];
         if (s == NONE) { g.next[i] = NONE; continue; }
-        group_push(g, uf_find(g, s), i);
+        group_push(g, uf_find(g, s), i, Q_CT);
     }
 }
 
@@ -597,7 +609,9 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
-        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a);
+        const bool defer = eg[0] & EG_NAT_DEFER;
+        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, defer);
+        if (defer && c != DROP_CT_CREATE_FAILED) g.eg[(size_t)i * EG_WORDS] = eg[0] | EG_NAT_DONE;
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
         uint32_t na, np;
@@ -718,20 +732,62 @@ __global__ void __launch_bounds__(BLOCK) k_egress_ct(DpParams p, BatchDev b, uin
     __shared__ LdsMetrics lm;
     Met m;
     met_init(m, lm);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
-        const uint32_t s = g.gslot[i];
-        if (s == NONE || g.next[i] != NONE) continue;
-        const uint32_t head = (uint32_t)g.table[2 * s + 1];
-        group_in_order(g, head, [&](uint32_t x) {
+    for_each_group(g, Q_CT, [&](uint32_t, uint32_t head) {
+        group_in_order(g, head, 2, [&](uint32_t x) {
             if (g.eg[(size_t)x * EG_WORDS] & EG_V6) egress6_one(p, b, now, o, g, x, m);
             else egress4_one(p, b, now, o, g, x, m);
         });
-    }
+    });
     met_flush(m, p.metrics);
 }
 
+// ================================================================== deferred NAT tuples
+// Writers of one NAT pair join one group; its lane writes each member's entry if
+// no later packet of the launch wrote that key before (the padding words 14/15 of
+// the 64-B value slot hold {epoch, writer}), so every key ends with the value of
+// its highest-index writer.
+__global__ void __launch_bounds__(BLOCK) k_nat_group(BatchDev b, GroupScratch g)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        if (!(eg[0] & EG_NAT_DONE)) { g.gslot[i] = NONE; continue; }
+        group_push(g, group_node(g, pair_hash4(eg[4], eg[6], SALT_NAT)), i, Q_NAT);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uint32_t now, GroupScratch g)
+{
+    for_each_group(g, Q_NAT, [&](uint32_t, uint32_t head) {
+        for (uint32_t x = head; x != NONE; x = g.next[x]) {
+            Rec r;
+            rec_load(r, b, x, 4);
+            const uint32_t *eg = g.eg + (size_t)x * EG_WORDS;
+            const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+            Eg4 y;
+            eg4_state(r, eg, y);
+            uint32_t seen;
+            ct_l4<false>(y.t, y.s.h, CT_EGRESS, seen);            // the tuple ct_create4 saw: reversed,
+            y.t.reverse();                                        // after a NEW lookup
+            y.stn.src_sec_id = ep.seclabel;
+            CtE e;
+            ct_entry_new(e, y.t.nexthdr == 6, y.s.len, CT_EGRESS, y.stn, now);
+            const Tuple4 n = ct_nat_tuple(y.t, CT_EGRESS, y.stn);
+            uint32_t k[4];
+            n.key(k);
+            bool created;
+            const int64_t sl = dev_upsert<Ct4Spec>(ep.ct4, k, &created);
+            if (sl < 0) continue;                                 // table full: the reference fails the create
+            uint32_t *v = reinterpret_cast<uint32_t *>(ep.ct4.vals + (size_t)sl * ep.ct4.vstride);
+            if (!created && v[15] == g.serial && v[14] > x) continue;
+            e.w[14] = x;
+            e.w[15] = g.serial;
+            ct_store(ep.ct4, sl, e);
+        }
+    });
+}
+
 // ================================================================== launcher
-// g.epoch and g.epoch + 1 are used (service groups, conntrack groups).
+// g.epoch .. g.epoch + 2 are used (service groups, conntrack groups, NAT writers).
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s)
 {
@@ -742,8 +798,12 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     hipLaunchKernelGGL(k_lb_stage, grid, blk, 0, s, p, b, flow_hash, now, o, g);
     g.epoch += 1;
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
+    hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_egress_ct, grid, blk, 0, s, p, b, now, o, g);
+    g.epoch += 1;
+    hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
+    hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                                 const EpDev &ep = p.eps[e - 1];
                                 const uint32_t sa = rec_raw32c<26>(r), da = rec_raw32c<30>(r);
                                 const uint32_t s = group_node(g, pair_hash4(sa, da, (uint64_t)ep.ct_id << 17));
-                                group_push(g, s, i);
+                                group_push(g, s, i, Q_NETDEV);
                             }
                         }
                     }
@@ -234,12 +234,9 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutD
     __shared__ LdsMetrics lm;
     Met m;
     met_init(m, lm);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
-        const uint32_t s = g.gslot[i];
-        if (s == NONE || g.next[i] != NONE) continue;              // not staged / not the group's first inserter
-        const uint32_t head = (uint32_t)g.table[2 * s + 1];
-        group_in_order(g, head, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
-    }
+    for_each_group(g, Q_NETDEV, [&](uint32_t, uint32_t head) {
+        group_in_order(g, head, 0, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
+    });
     met_flush(m, p.metrics);
 }
 

@@ -752,8 +752,8 @@ def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n
     resp6 = np.where((kind == 0)[:, None], fam_pods6[be_pick[be_row]], d6)
     resp_port = np.where((kind == 0) & (be_port[svc] > 0), be_port[svc], dport)
     # responder endpoint index if local (replies are only generated from local pods)
-    loc4 = {int(a): i for i, a in enumerate(ep_ip4)}
-    resp_ep = np.array([loc4.get(int(a), -1) for a in resp4], np.int64)
+    off4 = resp4.astype(np.int64) - int(ep_ip4[0])                 # ep_ip4 is contiguous
+    resp_ep = np.where((off4 >= 0) & (off4 < n_ep), off4, -1)
     if kind.size:
         is_loc6 = (resp6[:, 8:12].view(">u4").reshape(-1) == 0x000A0000) & (resp6[:, :8] == np.frombuffer(V6_POD_PREFIX, np.uint8)).all(1)
         lo6 = resp6[:, 12:16].view(">u4").reshape(-1).astype(np.int64) // 0x10001 - 0x100

@@ -402,6 +402,18 @@ int compile_ct_t(cv_ctx *c, MapObj *mo, uint32_t ks, int kind)
     const uint64_t want = std::max<uint64_t>(m->max_entries, keys.size());
     DevHash &d = mo->ct;
     uint64_t nb = buckets_for(want, S::SPB);
+    if (keys.empty()) {                    // a fresh map: zeroed device buffers, no host image
+        int r = d.buckets.alloc(nb * S::BW * 4);
+        if (!r) r = d.vals.alloc(nb * S::SPB * 64);
+        if (r) return r;
+        if (hipMemset(d.buckets.p, 0, d.buckets.n) != hipSuccess || hipMemset(d.vals.p, 0, d.vals.n) != hipSuccess)
+            return -EIO;
+        d.nb = nb;
+        d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, (uint32_t)S::SPB};
+        mo->kind = kind;
+        mo->ct_id = c->next_ct_id++;
+        return 0;
+    }
     d.hb.assign(nb * S::BW, 0);
     HashTable t{d.hb.data(), nullptr, nb - 1, 64, (uint32_t)S::SPB};
     std::vector<uint8_t> hv(nb * S::SPB * 64, 0);

@@ -188,6 +188,16 @@ int or_map_update(or_map *m, const void *key, const void *val, uint64_t flags)
     return 0;
 }
 
+int or_map_update_batch(or_map *m, const void *keys, const void *vals, uint32_t n, uint64_t flags)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        int r = or_map_update(m, (const uint8_t *)keys + (size_t)i * m->ks, (const uint8_t *)vals + (size_t)i * m->vs,
+                              flags);
+        if (r) return r;
+    }
+    return 0;
+}
+
 void *or_map_lookup_ptr(or_map *m, const void *key)
 {
     if (m->type == OR_MAP_LPM_TRIE) {

@@ -117,6 +117,7 @@ typedef struct or_map or_map;
 or_map  *or_map_create(int type, uint32_t key_size, uint32_t val_size, uint32_t max_entries);
 void     or_map_free(or_map *m);
 int      or_map_update(or_map *m, const void *key, const void *val, uint64_t flags);
+int      or_map_update_batch(or_map *m, const void *keys, const void *vals, uint32_t n, uint64_t flags);
 int      or_map_lookup(or_map *m, const void *key, void *val_out);
 int      or_map_delete(or_map *m, const void *key);
 uint32_t or_map_count(const or_map *m);

@@ -37,6 +37,7 @@ def lib():
         L.or_map_create.argtypes = [i32, u32, u32, u32]
         L.or_map_free.argtypes = [vp]
         L.or_map_update.argtypes = [vp, vp, vp, u64]
+        L.or_map_update_batch.argtypes = [vp, vp, vp, u32, u64]
         L.or_map_lookup.argtypes = [vp, vp, vp]
         L.or_map_delete.argtypes = [vp, vp]
         L.or_map_count.restype = u32
@@ -80,13 +81,12 @@ class OMap:
         return m
 
     def load(self, keys, vals):
-        L = lib()
         keys = np.ascontiguousarray(keys, np.uint8)
         vals = np.ascontiguousarray(vals, np.uint8)
-        for i in range(len(keys)):
-            r = L.or_map_update(self.h, keys[i].ctypes.data, vals[i].ctypes.data, 0)
+        if len(keys):
+            r = lib().or_map_update_batch(self.h, keys.ctypes.data, vals.ctypes.data, len(keys), 0)
             if r != 0:
-                raise OSError(-r, f"or_map_update[{i}]")
+                raise OSError(-r, "or_map_update_batch")
 
     def update(self, key, val, flags=0):
         k = np.ascontiguousarray(np.frombuffer(bytes(key), np.uint8))

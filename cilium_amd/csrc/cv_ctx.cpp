@@ -572,6 +572,8 @@ DpParams params(cv_ctx *c)
     p.v4_cluster_range = c->node.ipv4_cluster_range;
     p.v4_loopback = c->node.ipv4_loopback;
     memcpy(p.router6, c->node.router_ip6, 16);
+    const char *rm = getenv("CV_RECMODE");
+    p.recmode = rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u;
     const char *ab = getenv("CV_ABLATE");
     p.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
     return p;

@@ -48,6 +48,59 @@ __device__ __forceinline__ void rec_load(RecT<NW> &r, const BatchDev &b, uint32_
     }
 }
 
+// plain (temporal) per-lane record load, for comparison with the non-temporal one
+template <int NW>
+__device__ __forceinline__ void rec_load_plain(RecT<NW> &r, const BatchDev &b, uint32_t i, int nvec)
+{
+    r.base = b.frames + (size_t)i * b.stride;
+    r.len = b.len[i];
+    r.stride = b.stride;
+    const uint4 *q = reinterpret_cast<const uint4 *>(r.base);
+#pragma unroll
+    for (int k = 0; k < NW / 4; ++k) {
+        if (k < nvec) {
+            const uint4 v = q[k];
+            r.w[4 * k] = v.x; r.w[4 * k + 1] = v.y; r.w[4 * k + 2] = v.z; r.w[4 * k + 3] = v.w;
+        } else {
+            r.w[4 * k] = r.w[4 * k + 1] = r.w[4 * k + 2] = r.w[4 * k + 3] = 0;
+        }
+    }
+}
+
+// Wave-cooperative load of the 64 consecutive 64-B records of a wave (i0 = the
+// wave's first packet): four fully coalesced 1-KiB loads per wave into LDS (`st`,
+// 4 KiB per wave), then every lane takes its own record's first nvec 16-B words.
+// Uniform per wave; the caller falls back to per-lane loads for partial waves.
+__device__ __forceinline__ void rec_load_wave64(Rec &r, const BatchDev &b, uint32_t i0, int nvec, uint4 *st)
+{
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(b.frames + (size_t)i0 * 64);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const u32x4 v = __builtin_nontemporal_load(src + c * 64 + lane);
+        const int chunk = c * 64 + lane;                          // record chunk/4, part chunk%4
+        st[(chunk & 3) * 64 + (chunk >> 2)] = make_uint4(v.x, v.y, v.z, v.w);   // part-major: conflict-free reads
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t i = i0 + lane;
+    r.base = b.frames + (size_t)i * 64;
+    r.len = b.len[i];
+    r.stride = 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < nvec) {
+            const uint4 v = st[k * 64 + lane];
+            r.w[4 * k] = v.x; r.w[4 * k + 1] = v.y; r.w[4 * k + 2] = v.z; r.w[4 * k + 3] = v.w;
+        } else {
+            r.w[4 * k] = r.w[4 * k + 1] = r.w[4 * k + 2] = r.w[4 * k + 3] = 0;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int O, int NW>
 __device__ __forceinline__ uint32_t rec_u8c(const RecT<NW> &r)
 {

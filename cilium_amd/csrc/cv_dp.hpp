@@ -34,6 +34,7 @@ struct DpParams {              // by value as the kernel argument
     const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
     unsigned long long *metrics;   // [256][4][2]
     uint32_t ablate;           // timing-only ablations (CV_ABLATE env); 0 in every real run
+    uint32_t recmode;          // record loads: 0 per-lane non-temporal, 1 per-lane plain, 2 wave-cooperative
     // load balancer (lb.h): services and dense reverse-NAT tables indexed by the raw u16 key
     HashTable lb4, lb6;        // Lb4Spec / Lb6Spec
     const uint32_t *revnat4;   // [65536][2]  {address, port | valid << 16}

@@ -63,6 +63,7 @@ constexpr int PPT = 4;
 __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
 {
     __shared__ LdsMetrics lm;
+    __shared__ uint4 stage[BLOCK / 64][256];
     Met m;
     met_init(m, lm);
     const HashTable pol = p.eps[ep].policy;
@@ -71,9 +72,12 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
     for (int k = 0; k < PPT; ++k) {
         hits[k] = Hit{nullptr, 0};
         const uint32_t i = blockIdx.x * (PPT * BLOCK) + k * BLOCK + threadIdx.x;
-        if (i >= b.n) continue;
+        const uint32_t i0 = i - (threadIdx.x & 63);
         Rec r;
-        rec_load(r, b, i, 3);
+        if (p.recmode == 2 && b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 3, stage[threadIdx.x >> 6]);
+        else if (i >= b.n) continue;
+        else if (p.recmode == 1) rec_load_plain(r, b, i, 3);
+        else rec_load(r, b, i, 3);
         Acct a{0, 0};
         bool skip_proxy = false;
         uint32_t identity = 0;

@@ -632,7 +632,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4) ||
         c->gorder.alloc((size_t)cmax * 4) || c->gcursor.alloc(CURSOR_WORDS * 4) ||
-        c->gqueue.alloc(((size_t)cmax / QSPLIT + 512) * QSPLIT * 4))
+        c->gqueue.alloc(((size_t)cmax / QSPLIT + 512) * QSPLIT * QBANKS * 4))
         return -ENOMEM;
     (void)hipMemset(c->gtable.p, 0, cap * 16);
     if (egress || c->g_egress) {

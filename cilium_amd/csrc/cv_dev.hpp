@@ -980,17 +980,27 @@ __device__ __forceinline__ uint32_t group_find(const GroupScratch &g, uint64_t g
     return NONE;
 }
 
-// wave-aggregated append: one atomic per wave; returns the lane's index or NONE
+// wave-aggregated append: one atomic per (wave, counter); lanes may target different
+// counters; returns the lane's index or NONE
 __device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred)
 {
-    const unsigned long long m = __ballot(pred);
-    if (!m) return NONE;
-    const int leader = __ffsll((long long)m) - 1;
     const int lane = (int)__lane_id();
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    return pred ? base + (uint32_t)__popcll(m & ((1ull << lane) - 1)) : NONE;
+    uint32_t res = NONE;
+    unsigned long long todo = __ballot(pred);
+    while (todo) {                                                // one round per distinct counter
+        const int leader = __ffsll((long long)todo) - 1;
+        const uintptr_t mine_p = reinterpret_cast<uintptr_t>(ctr);
+        const uint32_t lo = __shfl((uint32_t)mine_p, leader, 64), hi = __shfl((uint32_t)(mine_p >> 32), leader, 64);
+        uint32_t *lc = reinterpret_cast<uint32_t *>((uintptr_t)lo | ((uintptr_t)hi << 32));
+        const bool mine = pred && ctr == lc;
+        const unsigned long long m = __ballot(mine);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(lc, (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (mine) res = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        todo &= ~m;
+    }
+    return res;
 }
 
 // push packet i on the list of node s; the group's first member (the list tail)
@@ -1004,7 +1014,7 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
     g.next[i] = first ? NONE : (uint32_t)prev;
     const uint32_t k = blockIdx.x % QSPLIT;
     const uint32_t at = wave_append(&g.cursor[qctr(q, k)], first);
-    if (first) g.queue[(size_t)k * g.qregion + at] = s;
+    if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;
 }
 
 // for every queued group (its slot s and current list head): fn(s, head)
@@ -1022,7 +1032,7 @@ __device__ __forceinline__ void for_each_group(const GroupScratch &g, int q, F &
 #pragma unroll
         for (int t = 0; t < QSPLIT - 1; ++t)
             if (k == (uint32_t)t && r >= n[t]) { r -= n[t]; k = t + 1; }
-        const uint32_t s = g.queue[(size_t)k * g.qregion + r];
+        const uint32_t s = g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + r];
         fn(s, (uint32_t)g.table[2 * s + 1]);
     }
 }
@@ -1064,22 +1074,22 @@ __device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint
     }
 }
 
-constexpr int GMAX = 16;
+constexpr int GMAX = 8;
 
 // Run fn(i) for every member of the group whose list starts at `head`, in
 // ascending packet order: <= GMAX members are sorted in registers; larger groups
-// are copied to a slice of g.order (cursor `cur`) and shell-sorted there.
+// are copied to a slice of g.order (cursor `cur`) and shell-sorted there.  One call
+// site of fn, so its (large) body is inlined once.
 template <class F>
 __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t head, int cur, F &&fn)
 {
-    if (g.next[head] == NONE) { fn(head); return; }
     uint32_t m[GMAX];
-    int cnt = 0;
+    uint32_t cnt = 0;
     uint32_t x = head;
     for (; x != NONE && cnt < GMAX; x = g.next[x]) {
         int pos = 0;
 #pragma unroll
-        for (int j = 0; j < GMAX; ++j) pos += (j < cnt && m[j] < x) ? 1 : 0;
+        for (int j = 0; j < GMAX; ++j) pos += (j < (int)cnt && m[j] < x) ? 1 : 0;
 #pragma unroll
         for (int j = GMAX - 1; j >= 0; --j) {
             const uint32_t left = j > 0 ? m[j - 1] : 0u;
@@ -1087,31 +1097,33 @@ __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t h
         }
         ++cnt;
     }
-    if (x == NONE) {
+    uint32_t *o = nullptr;
+    if (x != NONE) {                                              // large group
+        for (uint32_t y = x; y != NONE; y = g.next[y]) ++cnt;
+        o = g.order + atomicAdd(&g.cursor[cur], cnt);
+        uint32_t k = 0;
+        for (uint32_t y = head; y != NONE; y = g.next[y]) o[k++] = y;
+        for (uint32_t gap = cnt / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {   // shell sort
+            for (uint32_t i = gap; i < cnt; ++i) {
+                const uint32_t v = o[i];
+                uint32_t j = i;
+                for (; j >= gap && o[j - gap] > v; j -= gap) o[j] = o[j - gap];
+                o[j] = v;
+            }
+        }
+    }
 #pragma unroll 1
-        for (int j = 0; j < GMAX; ++j) {
-            if (j >= cnt) break;
-            uint32_t v = m[0];
+    for (uint32_t j = 0; j < cnt; ++j) {
+        uint32_t v;
+        if (o) {
+            v = o[j];
+        } else {
+            v = m[0];
 #pragma unroll
-            for (int q = 1; q < GMAX; ++q) v = (q == j) ? m[q] : v;
-            fn(v);
+            for (int q = 1; q < GMAX; ++q) v = (q == (int)j) ? m[q] : v;
         }
-        return;
+        fn(v);
     }
-    uint32_t total = GMAX;
-    for (uint32_t y = x; y != NONE; y = g.next[y]) ++total;
-    uint32_t *o = g.order + atomicAdd(&g.cursor[cur], total);
-    uint32_t k = 0;
-    for (uint32_t y = head; y != NONE; y = g.next[y]) o[k++] = y;
-    for (uint32_t gap = total / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {   // shell sort
-        for (uint32_t i = gap; i < total; ++i) {
-            const uint32_t v = o[i];
-            uint32_t j = i;
-            for (; j >= gap && o[j - gap] > v; j -= gap) o[j] = o[j - gap];
-            o[j] = v;
-        }
-    }
-    for (uint32_t i = 0; i < total; ++i) fn(o[i]);
 }
 
 // node key of an unordered address pair (v4 words or v6 4-word addresses), mixed

@@ -86,8 +86,11 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
 // contention on one counter); blocks b with b % QSPLIT == k hold at most
 // n / QSPLIT + BLOCK + QSPLIT packets (grids are multiples of QSPLIT or one block per 256
 // packets), so a region of n / QSPLIT + 512 words never overflows.
-enum : int { Q_NETDEV = 0, Q_LB = 1, Q_CT = 2, Q_NAT = 3 };
-constexpr int QSPLIT = 16, CURSOR_WORDS = 32 + 4 * QSPLIT * 32;
+// Queues filled at the same time (the v4 and v6 lists of one stage) live in different
+// banks of `queue`: QSPLIT regions of qregion words each per bank.
+enum : int { Q_NETDEV = 0, Q_LB4 = 1, Q_LB6 = 2, Q_CT4 = 3, Q_CT6 = 4, Q_NAT = 5, NQUEUES = 6 };
+constexpr int QSPLIT = 16, QBANKS = 2, CURSOR_WORDS = 32 + NQUEUES * QSPLIT * 32;
+__host__ __device__ constexpr int qbank(int q) { return (q == Q_LB6 || q == Q_CT6) ? 1 : 0; }
 __host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT + k) * 32; }
 constexpr int EG_WORDS = 16;
 

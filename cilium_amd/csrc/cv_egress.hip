@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
                 } else {
                     gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ep.ct_id);
                 }
-                group_push(g, group_node(g, gh), i, Q_LB);
+                group_push(g, group_node(g, gh), i, (eg[0] & EG_V6) ? Q_LB6 : Q_LB4);
             }
         }
     }
@@ -409,15 +409,16 @@ fin:
     eg_final(o, i, res, a);
 }
 
+template <bool V6>
 __global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
                                                     OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     Met m;
     met_init(m, lm);
-    for_each_group(g, Q_LB, [&](uint32_t, uint32_t head) {
+    for_each_group(g, V6 ? Q_LB6 : Q_LB4, [&](uint32_t, uint32_t head) {
         group_in_order(g, head, 1, [&](uint32_t x) {
-            if (g.eg[(size_t)x * EG_WORDS] & EG_V6) lb6_one(p, b, hash, now, o, g, x, m);
+            if constexpr (V6) lb6_one(p, b, hash, now, o, g, x, m);
             else lb4_one(p, b, hash, now, o, g, x, m);
         });
     });
@@ -570,7 +571,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_link(BatchDev b, GroupScratch g
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         const uint32_t s = g.gslot[i];
         if (s == NONE) { g.next[i] = NONE; continue; }
-        group_push(g, uf_find(g, s), i, Q_CT);
+        group_push(g, uf_find(g, s), i, (g.eg[(size_t)i * EG_WORDS] & EG_V6) ? Q_CT6 : Q_CT4);
     }
 }
 
@@ -727,14 +728,15 @@ drop:
     eg_final(o, i, res, a);
 }
 
+template <bool V6>
 __global__ void __launch_bounds__(BLOCK) k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     Met m;
     met_init(m, lm);
-    for_each_group(g, Q_CT, [&](uint32_t, uint32_t head) {
+    for_each_group(g, V6 ? Q_CT6 : Q_CT4, [&](uint32_t, uint32_t head) {
         group_in_order(g, head, 2, [&](uint32_t x) {
-            if (g.eg[(size_t)x * EG_WORDS] & EG_V6) egress6_one(p, b, now, o, g, x, m);
+            if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
             else egress4_one(p, b, now, o, g, x, m);
         });
     });
@@ -795,12 +797,14 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     if (b.stride >= 128) hipLaunchKernelGGL(k_egress_front<32>, grid, blk, 0, s, p, b, src_ep, ep0, o, g);
     else hipLaunchKernelGGL(k_egress_front<16>, grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-    hipLaunchKernelGGL(k_lb_stage, grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    hipLaunchKernelGGL(k_lb_stage<false>, grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    if (b.stride >= 128) hipLaunchKernelGGL(k_lb_stage<true>, grid, blk, 0, s, p, b, flow_hash, now, o, g);
     g.epoch += 1;
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
-    hipLaunchKernelGGL(k_egress_ct, grid, blk, 0, s, p, b, now, o, g);
+    hipLaunchKernelGGL(k_egress_ct<false>, grid, blk, 0, s, p, b, now, o, g);
+    if (b.stride >= 128) hipLaunchKernelGGL(k_egress_ct<true>, grid, blk, 0, s, p, b, now, o, g);
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);

@@ -96,11 +96,60 @@ __device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets
     }
 }
 
+// bytes of the 8 tag bytes equal to `tag` (bit 7 of each matching byte), and empty slots
+template <class S>
+__device__ __forceinline__ void tag_masks(uint64_t tags, uint32_t tag, uint64_t &match, bool &empty)
+{
+    constexpr uint64_t ones = 0x0101010101010101ULL, highs = 0x8080808080808080ULL;
+    constexpr uint64_t valid = S::SPB >= 8 ? ~0ULL : ((1ULL << (8 * S::SPB)) - 1);
+    const uint64_t x = tags ^ (ones * tag);
+    match = (x - ones) & ~x & highs & valid;                       // zero bytes of x (exact for tag >= 3)
+    const uint64_t e = (tags - ones) & ~tags & highs & valid;       // zero bytes of tags: empty slots
+    empty = e != 0;
+}
+
+// Tag-first probe for wide buckets (>= 128 B): read the 8 tag bytes, then only the
+// keys (and inline values) of slots whose fingerprint matches, so a probe keeps a
+// few registers live instead of the whole bucket.  Same result as the full-bucket
+// match: a key is stored once; the chain ends at a bucket with an empty slot.
+template <class S>
+__device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_t *key, uint32_t *ival)
+{
+    const uint64_t h = key_hash<S>(key);
+    const uint32_t tag = tag_of(h);
+    uint64_t b = h & t.mask;
+    for (int p = 0; p < MAX_PROBE; ++p) {
+        const uint32_t *bw = t.buckets + b * S::BW;
+        const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
+        uint64_t match;
+        bool empty;
+        tag_masks<S>((uint64_t)tg.x | ((uint64_t)tg.y << 32), tag, match, empty);
+        while (match) {
+            const int sl = (__builtin_ctzll(match) >> 3);
+            match &= match - 1;
+            const uint32_t *kw = bw + S::KEY0 + sl * S::KW;
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+            if (eq) {
+#pragma unroll
+                for (int j = 0; j < S::IVW; ++j) ival[j] = bw[S::IVAL0 + sl * S::IVW + j];
+                if (S::IVH) ival[0] = half_at<S>(bw, S::HVAL0 + sl);
+                return (int64_t)(b * S::SPB + sl);
+            }
+        }
+        if (empty) return -1;
+        b = (b + 1) & t.mask;
+    }
+    return -1;
+}
+
 // Returns the slot index (bucket * SPB + slot) or -1; copies the inline value.
 template <class S>
 __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     if (!t.buckets) return -1;
+    if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);
     const uint64_t h = key_hash<S>(key);
     const uint32_t tag = tag_of(h);
     uint64_t b = h & t.mask;
@@ -139,14 +188,10 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     const uint32_t tag = tag_of(h);
     uint64_t b = h & t.mask;
     *created = false;
-    for (int p = 0; p < MAX_PROBE; ++p) {          // 1) existing entry?
-        uint32_t w[S::BW];
-        load_bucket<S>(t.buckets, b, w);
-        bool stop;
-        int s = match_bucket<S>(w, key, tag, &stop);
-        if (s >= 0) return (int64_t)(b * S::SPB + s);
-        if (stop) break;
-        b = (b + 1) & t.mask;
+    {                                               // 1) existing entry?
+        uint32_t none[S::IVW + 1];
+        const int64_t s = dev_find_tf<S>(t, key, none);
+        if (s >= 0) return s;
     }
     b = h & t.mask;                                 // 2) claim the first free slot
     for (int p = 0; p < MAX_PROBE; ++p) {

@@ -51,6 +51,11 @@ def check_egress(w, dev, batches, rounds=2):
                                 w.extra["flow_hash"][lo:hi], now=now)
             for k in FIELDS:
                 bad = np.nonzero(o[k] != getattr(ref, k))[0]
+                if len(bad):
+                    v6 = w.extra["v6"][lo:hi][bad]
+                    print("MISMATCH", k, "n", len(bad), "v6 frac", v6.mean(), "gpu ret/reason",
+                          o["ret"][bad[:12]], o["reason"][bad[:12]], "ref", ref.ret[bad[:12]], ref.reason[bad[:12]],
+                          "ct", o["ct"][bad[:12]], ref.ct[bad[:12]], "nl", o["nl"][bad[:12]], ref.nl[bad[:12]])
                 assert len(bad) == 0, (k, rnd, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
     assert (ctx.metrics() == dp.metrics()).all()
     for name in ("ct4", "ct6", "policy"):
@@ -98,3 +103,13 @@ def test_config5_drop_all(dev):
 def H_flags(drop_all=False):
     from cilium_amd import lib
     return lib.F_DEFAULT | (lib.F_DROP_ALL if drop_all else 0)
+
+
+def test_config5_v6_only(dev):
+    w = synth.config5(1 << 13, n_svc=500, n_ep=64, n_remote=128, family=6, seed=55)
+    check_egress(w, dev, batches=1, rounds=1)
+
+
+def test_config5_v4_records_128(dev):
+    w = synth.config5(1 << 13, n_svc=500, n_ep=64, n_remote=128, family=4, stride=128, seed=56)
+    check_egress(w, dev, batches=1, rounds=1)

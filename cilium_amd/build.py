@@ -22,17 +22,31 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = ["/opt/rocm/bin/hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-x", "hip"] + [os.path.join(SRC, s) for s in SOURCES] + ["-o", OUT + ".tmp"]
+def build(force=False, verbose=False, out=OUT, defines=()):
+    """Compile every source to an object in parallel, then link the shared library."""
+    if not force and out == OUT and not needs_build():
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    base = ["/opt/rocm/bin/hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            "-Wno-unused-function"] + [f"-D{d}" for d in defines]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = out + "." + os.path.splitext(src)[0] + ".o"
+        cmd = base + ["-c", "-x", "hip", os.path.join(SRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any(p.wait() for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = ["/opt/rocm/bin/hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    for o in objs:
+        os.remove(o)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -191,9 +191,54 @@ struct Fwd {
     unsigned long long b[2];
 };
 
+// Policy entry counters (the packets/bytes __policy_can_access adds to the hit entry)
+// summed per workgroup: a direct-mapped LDS table keyed by the entry's delta-word
+// address; a slot taken by another entry sends the update to global memory as
+// before.  Flushed once per workgroup: hot entries (one L3 rule hit by most packets)
+// see one global atomic per workgroup instead of one per packet.  Sums commute, so
+// the folded counters equal the per-packet updates.
+constexpr int PC_N = 256;
+struct LdsPolicy {
+    unsigned long long key[PC_N];
+    unsigned long long val[PC_N];
+};
+
+__device__ __forceinline__ void pol_add(LdsPolicy *pc, unsigned long long *d, unsigned long long inc)
+{
+    if (pc) {
+        const unsigned long long k = reinterpret_cast<uintptr_t>(d);
+        const uint32_t i = (uint32_t)(mix64(k) >> 40) & (PC_N - 1);
+        unsigned long long cur = pc->key[i];
+        if (cur == 0) {
+            unsigned long long exp = 0;
+            __hip_atomic_compare_exchange_strong(&pc->key[i], &exp, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            cur = exp == 0 ? k : exp;
+        }
+        if (cur == k) {
+            __hip_atomic_fetch_add(&pc->val[i], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+    }
+    atomicAdd(d, inc);
+}
+
+__device__ __forceinline__ void pol_cache_init(LdsPolicy &pc)
+{
+    for (int i = threadIdx.x; i < PC_N; i += blockDim.x) pc.key[i] = 0, pc.val[i] = 0;
+}
+
+// after a __syncthreads that follows the workgroup's last pol_add
+__device__ __forceinline__ void pol_cache_flush(const LdsPolicy &pc)
+{
+    for (int i = threadIdx.x; i < PC_N; i += blockDim.x)
+        if (pc.key[i] && pc.val[i]) atomicAdd(reinterpret_cast<unsigned long long *>(pc.key[i]), pc.val[i]);
+}
+
 struct Met {
     LdsMetrics *lm;
     Fwd f;
+    LdsPolicy *pc;             // optional policy counter cache (conntrack stages)
     __device__ void drop(int32_t code, uint32_t len, int dir)          // send_drop_notify
     {
         const uint32_t r = (uint8_t)(-code);
@@ -212,6 +257,7 @@ __device__ __forceinline__ void met_init(Met &m, LdsMetrics &lm)
 {
     for (int i = threadIdx.x; i < 256 * 4; i += blockDim.x) lm.c[i] = 0;
     m.lm = &lm;
+    m.pc = nullptr;
     m.f.c[0] = m.f.c[1] = 0;
     m.f.b[0] = m.f.b[1] = 0;
     __syncthreads();
@@ -247,7 +293,10 @@ __device__ __forceinline__ void met_flush(Met &m, unsigned long long *g)
 }
 
 // ------------------------------------------------------------------ lookups
-struct Acct { uint32_t nl, nu; };
+struct Acct {
+    uint32_t nl, nu;
+    LdsPolicy *pc = nullptr;   // policy counter cache of the workgroup, if any
+};
 
 // lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
 __device__ __forceinline__ bool lxc4_find(const DpParams &p, uint32_t daddr_raw, uint32_t &ival, Acct &a)
@@ -306,32 +355,60 @@ __device__ __forceinline__ void hit_flush(const Hit &h)
 
 // __policy_can_access (policy.h:217-285); cb[CB_POLICY] is 0 on these paths.  With
 // `defer` the counter update is returned instead of issued.
+// With ILP the three keys' buckets are read together (one round trip instead of up
+// to three dependent ones; more lines read when an early step hits).
+template <bool ILP = false>
 __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
                                              uint32_t dport_raw, uint32_t proto, int dir, Acct &a,
                                              Hit *defer = nullptr)
 {
     if (flags & F_DROP_ALL) return DROP_POLICY;
     const uint32_t eg = dir ? 0u : 1u;                           // policy_key.egress = !dir
-    uint32_t k[2];
     int64_t s = -1;
     uint32_t px[1] = {0};
     bool l4 = false;
-    if (flags & F_HAVE_L4_POLICY) {
-        k[0] = identity; k[1] = (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24);
-        a.nl++;
-        s = dev_find<PolicySpec>(pol, k, px);
-        l4 = s >= 0;
-    }
-    if (s < 0) {
-        k[0] = identity; k[1] = eg << 24;
-        a.nl++;
-        s = dev_find<PolicySpec>(pol, k, px);
-    }
-    if (s < 0 && (flags & F_HAVE_L4_POLICY)) {
-        k[0] = 0; k[1] = (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24);
-        a.nl++;
-        s = dev_find<PolicySpec>(pol, k, px);
-        l4 = s >= 0;
+    const uint32_t kl4[2] = {identity, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
+    const uint32_t kl3[2] = {identity, eg << 24};
+    const uint32_t kwc[2] = {0, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
+#ifdef CV_NO_ILP
+    if constexpr (false) {
+#else
+    if constexpr (ILP) {
+#endif
+        const bool have_l4 = flags & F_HAVE_L4_POLICY;
+        Probe<PolicySpec> p1, p3;
+        if (have_l4) p1 = probe_begin<PolicySpec>(pol, kl4);
+        const Probe<PolicySpec> p2 = probe_begin<PolicySpec>(pol, kl3);
+        if (have_l4) p3 = probe_begin<PolicySpec>(pol, kwc);
+        if (have_l4) {
+            a.nl++;
+            s = probe_end<PolicySpec>(p1, pol, kl4, px);
+            l4 = s >= 0;
+        }
+        if (s < 0) {
+            a.nl++;
+            s = probe_end<PolicySpec>(p2, pol, kl3, px);
+        }
+        if (s < 0 && have_l4) {
+            a.nl++;
+            s = probe_end<PolicySpec>(p3, pol, kwc, px);
+            l4 = s >= 0;
+        }
+    } else {
+        if (flags & F_HAVE_L4_POLICY) {
+            a.nl++;
+            s = dev_find<PolicySpec>(pol, kl4, px);
+            l4 = s >= 0;
+        }
+        if (s < 0) {
+            a.nl++;
+            s = dev_find<PolicySpec>(pol, kl3, px);
+        }
+        if (s < 0 && (flags & F_HAVE_L4_POLICY)) {
+            a.nl++;
+            s = dev_find<PolicySpec>(pol, kwc, px);
+            l4 = s >= 0;
+        }
     }
     if (s < 0) return DROP_POLICY;
     a.nu++;
@@ -344,7 +421,7 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
             unsigned long long *d = pol.aux + s;
             const unsigned long long inc = (1ull << 39) | len;
             if (defer) *defer = Hit{d, inc};
-            else atomicAdd(d, inc);
+            else pol_add(a.pc, d, inc);
         } else {
             atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);
             atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
@@ -354,12 +431,13 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
 }
 
 // policy_can_access_ingress (policy.h:305-329)
+template <bool ILP = false>
 __device__ __forceinline__ int policy_ingress(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t src,
                                               uint32_t dport_raw, uint32_t proto, Acct &a, Hit *defer = nullptr)
 {
     if (!(flags & F_POLICY_INGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
     if (flags & F_DROP_ALL) return DROP_POLICY;
-    int r = policy_access(pol, flags, len, src, dport_raw, proto, CT_INGRESS, a, defer);
+    int r = policy_access<ILP>(pol, flags, len, src, dport_raw, proto, CT_INGRESS, a, defer);
     return r >= TC_ACT_OK ? r : DROP_POLICY;
 }
 
@@ -369,7 +447,7 @@ __device__ __forceinline__ int policy_egress(const HashTable &pol, uint32_t flag
 {
     if (!(flags & F_POLICY_EGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
     if (flags & F_DROP_ALL) return DROP_POLICY;
-    int r = policy_access(pol, flags, len, identity, dport_raw, proto, CT_EGRESS, a);
+    int r = policy_access<true>(pol, flags, len, identity, dport_raw, proto, CT_EGRESS, a);
     return r >= 0 ? r : DROP_POLICY;
 }
 
@@ -532,6 +610,10 @@ enum { ACTION_UNSPEC = 0, ACTION_CREATE = 1, ACTION_CLOSE = 2 };
 
 // __ct_lookup (conntrack.h:199-263) -> CT_NEW / CT_ESTABLISHED; *slot = hit slot;
 // a hit fills ct_state's rev_nat_index / loopback / slave
+// the entry update of a __ct_lookup hit (conntrack.h:213-258)
+__device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
+                                       uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a);
+
 template <class T>
 __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, int action, int dir, bool tcp,
                                              uint32_t seen, uint32_t len, uint32_t now, uint32_t flags, int64_t &slot,
@@ -542,6 +624,13 @@ __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, in
     a.nl++;
     slot = dev_find<typename T::Spec>(ct, k, nullptr);
     if (slot < 0) return CT_NEW;
+    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a);
+    return CT_ESTABLISHED;
+}
+
+__device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
+                                       uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a)
+{
     a.nu++;
     CtE e;
     ct_load(ct, slot, e);
@@ -564,8 +653,7 @@ __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, in
         e.set_bits(e.bits() | (dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING));
         if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
     }
-    ct_store(ct, slot, e);
-    return CT_ESTABLISHED;
+    if (!(flags & (AB_EG_NO_CTSTORE << 16))) ct_store(ct, slot, e);
 }
 
 __device__ __forceinline__ uint8_t dir_flags(int dir)
@@ -610,14 +698,19 @@ __device__ __forceinline__ int ct_l4(T &t, const L4Hdr &h, int dir, uint32_t &se
 }
 
 // ct_lookup4 / ct_lookup6 (conntrack.h:442-562 / 286-412); tuple in/out
+// Both lookup keys are known before the first probe, so the reverse-direction
+// probe is issued together with the first one (its result is used only when the
+// first misses, as the reference's second __ct_lookup).
 template <bool V6, class T>
 __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr &h, int dir, uint32_t len,
                                          uint32_t now, uint32_t flags, int64_t &slot, CtState *st, Acct &a)
 {
+    using S = typename T::Spec;
     uint32_t seen;
     const int action = ct_l4<V6>(t, h, dir, seen);
     if (action < 0) return action;
     const bool tcp = t.nexthdr == 6;
+#ifdef CV_NO_ILP
     int ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a);
     if (ret != CT_NEW) return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
     if (dir != CT_SERVICE) {
@@ -625,6 +718,28 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
         ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a);
     }
     return ret;
+#endif
+    T t2 = t;
+    t2.reverse();
+    uint32_t k1[T::KW], k2[T::KW];
+    t.key(k1);
+    t2.key(k2);
+    const Probe<S> p1 = probe_begin<S>(ct, k1);
+    Probe<S> p2;
+    if (dir != CT_SERVICE) p2 = probe_begin<S>(ct, k2);
+    a.nl++;
+    slot = probe_end<S>(p1, ct, k1, nullptr);
+    if (slot >= 0) {
+        ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a);
+        return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+    }
+    if (dir == CT_SERVICE) return CT_NEW;
+    t = t2;
+    a.nl++;
+    slot = probe_end<S>(p2, ct, k2, nullptr);
+    if (slot < 0) return CT_NEW;
+    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a);
+    return CT_ESTABLISHED;
 }
 
 template <class T>
@@ -828,7 +943,7 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
             t.saddr = na;
         }
     }
-    verdict = policy_ingress(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
+    verdict = policy_ingress<true>(ep.policy, p.flags | (p.ablate << 16), s.len, src_label, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) { dev_kill<Ct4Spec>(ep.ct4, slot); a.nu++; }   // ct_delete4
         ret = DROP_POLICY;
@@ -886,7 +1001,7 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
             if (r2) { ret = r2; goto drop; }
         }
     }
-    verdict = policy_ingress(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
+    verdict = policy_ingress<true>(ep.policy, p.flags | (p.ablate << 16), s.len, src_label, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) { dev_kill<Ct6Spec>(ep.ct6, slot); a.nu++; }
         ret = DROP_POLICY;
@@ -1017,22 +1132,48 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
     if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;
 }
 
-// for every queued group (its slot s and current list head): fn(s, head)
-template <class F>
-__device__ __forceinline__ void for_each_group(const GroupScratch &g, int q, F &&fn)
+// ------------------------------------------------------------------ size-sorted runs
+// One lane runs a group's packets one after another, so a wave lasts as long as the
+// largest of its 64 groups.  Before a heavy stage the queue's groups are flattened
+// into runs {size, members in packet order} in `order` (k_group_flatten) and listed
+// in `work` by size class, largest first (k_group_schedule): the groups of one wave
+// then have about the same size and its lanes stay busy.
+__host__ __device__ constexpr int size_class(uint32_t n)
 {
-    uint32_t n[QSPLIT], total = 0;
+    return n <= 8 ? (n ? (int)n - 1 : 0) : n <= 12 ? 8 : n <= 16 ? 9 : n <= 24 ? 10 : n <= 32 ? 11
+         : n <= 64 ? 12 : n <= 128 ? 13 : n <= 1024 ? 14 : 15;
+}
+
+// sub-queue lengths of queue q; returns the number of queued groups
+__device__ __forceinline__ uint32_t queue_sizes(const GroupScratch &g, int q, uint32_t *n)
+{
+    uint32_t total = 0;
 #pragma unroll
     for (int k = 0; k < QSPLIT; ++k) {
         n[k] = __hip_atomic_load(&g.cursor[qctr(q, k)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         total += n[k];
     }
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
-        uint32_t r = j, k = 0;                                    // flat index -> (region, slot)
+    return total;
+}
+
+// the queue word of flat group index j
+__device__ __forceinline__ uint32_t *queue_entry(const GroupScratch &g, int q, const uint32_t *n, uint32_t j)
+{
+    uint32_t k = 0;
 #pragma unroll
-        for (int t = 0; t < QSPLIT - 1; ++t)
-            if (k == (uint32_t)t && r >= n[t]) { r -= n[t]; k = t + 1; }
-        const uint32_t s = g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + r];
+    for (int t = 0; t < QSPLIT - 1; ++t)
+        if (k == (uint32_t)t && j >= n[t]) { j -= n[t]; k = t + 1; }
+    return g.queue + ((size_t)qbank(q) * QSPLIT + k) * g.qregion + j;
+}
+
+// for every queued group (its slot s and current list head): fn(s, head)
+template <class F>
+__device__ __forceinline__ void for_each_group(const GroupScratch &g, int q, F &&fn)
+{
+    uint32_t n[QSPLIT];
+    const uint32_t total = queue_sizes(g, q, n);
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
+        const uint32_t s = *queue_entry(g, q, n, j);
         fn(s, (uint32_t)g.table[2 * s + 1]);
     }
 }
@@ -1123,6 +1264,27 @@ __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t h
             for (int q = 1; q < GMAX; ++q) v = (q == (int)j) ? m[q] : v;
         }
         fn(v);
+    }
+}
+
+// fn(i) for every member of every scheduled run of queue q, runs in `work` order and
+// members in packet order; the next member's index is loaded while fn runs
+// (SORTED false: the runs in queue order, when k_group_schedule did not run)
+template <bool SORTED = true, class F>
+__device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool first_only, F &&fn)
+{
+    uint32_t n[QSPLIT];
+    const uint32_t total = queue_sizes(g, q, n);
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
+        const uint32_t off = SORTED ? g.work[j] : *queue_entry(g, q, n, j);
+        const uint32_t cnt = first_only ? 1u : g.order[off];
+        uint32_t v = g.order[off + 1];
+#pragma unroll 1
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t vn = k + 1 < cnt ? g.order[off + 2 + k] : NONE;
+            fn(v);
+            v = vn;
+        }
     }
 }
 

@@ -46,7 +46,10 @@ struct DpParams {              // by value as the kernel argument
 
 // ablation bits: each removes one part of the work to price it (results are wrong)
 constexpr uint32_t AB_NO_POLICY_ATOMICS = 1, AB_NO_IPCACHE = 2, AB_NO_POLICY = 4, AB_NO_METRICS = 8,
-                   AB_NO_RECORD = 16;
+                   AB_NO_RECORD = 16,
+                   // egress (config 5) timing ablations
+                   AB_EG_NO_DELIVERY = 0x100, AB_EG_NO_POLICY = 0x200, AB_EG_NO_LOOKUPS = 0x400,
+                   AB_EG_NO_CTSTORE = 0x800, AB_EG_ONE_PER_GROUP = 0x1000;
 
 struct BatchDev {
     const uint8_t *frames;
@@ -76,11 +79,13 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     unsigned long long *parent;// per table slot: epoch << 32 | union-find parent (egress path)
     uint32_t *eg;              // per packet: EG_WORDS words of egress scratch (egress path)
     uint32_t serial;           // launch serial (never reset; tags deferred CT writes)
-    uint32_t *order;           // per packet: members of large groups, sorted in place
+    uint32_t *order;           // 2 words per packet: members of large groups sorted in place
+                               // (group_in_order), or the runs {size, members} of k_group_flatten
     uint32_t *cursor;          // [CURSOR_WORDS] zeroed per launch: [0..2] cursors into `order`,
                                // [qctr(q, k)] length of sub-queue k of queue q (one 128-B line each)
     uint32_t *queue;           // dense lists of group slots (one lane per group), QSPLIT regions
     uint32_t qregion;          // words per region
+    uint32_t *work;            // per group: `order` offset of its run, in size-class order
 };
 // GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
 // contention on one counter); blocks b with b % QSPLIT == k hold at most
@@ -89,11 +94,31 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
 // Queues filled at the same time (the v4 and v6 lists of one stage) live in different
 // banks of `queue`: QSPLIT regions of qregion words each per bank.
 enum : int { Q_NETDEV = 0, Q_LB4 = 1, Q_LB6 = 2, Q_CT4 = 3, Q_CT6 = 4, Q_NAT = 5, NQUEUES = 6 };
-constexpr int QSPLIT = 16, QBANKS = 2, CURSOR_WORDS = 32 + NQUEUES * QSPLIT * 32;
+// Size-sorted runs (k_group_flatten / k_group_schedule): per queue NCLASS group-size
+// classes, each a {count, fill} pair on its own line after the sub-queue counters; cursor[3] is
+// the allocation cursor of the runs in `order` ({size, members...}).
+constexpr int QSPLIT = 16, QBANKS = 2, NCLASS = 16;
+constexpr int CLS0 = 32 + NQUEUES * QSPLIT * 32, CURSOR_WORDS = CLS0 + NQUEUES * NCLASS * 32;
 __host__ __device__ constexpr int qbank(int q) { return (q == Q_LB6 || q == Q_CT6) ? 1 : 0; }
 __host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT + k) * 32; }
+__host__ __device__ constexpr int qcls(int q, int c) { return CLS0 + (q * NCLASS + c) * 32; }
+constexpr int RUN_CURSOR = 3;
 constexpr int EG_WORDS = 16;
 
+// flatten + schedule the groups of queue q (before the stage that runs them)
+// sched: 0 runs in queue order (no k_group_schedule), 1 largest size class first,
+// 2 smallest first
+void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStream_t s);
+// how a conntrack stage walks its groups: 0 linked lists (group_in_order), 1 runs
+// largest class first, 2 runs in queue order, 3 runs smallest class first
+// (build-time switches for A/B timing; CV_RUNS_MODE: config 3, CV_EG_RUNS: config 5)
+#ifndef CV_RUNS_MODE
+#define CV_RUNS_MODE 1
+#endif
+#ifndef CV_EG_RUNS
+#define CV_EG_RUNS 2
+#endif
+constexpr int runs_sched(int mode) { return mode == 1 ? 1 : mode == 3 ? 2 : 0; }
 int launch_policy_fold(const HashTable &pol, hipStream_t s);
 int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);

@@ -584,7 +584,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     rec_load(r, b, i, 4);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Eg4 x;
     eg4_state(r, eg, x);
@@ -593,16 +593,26 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
     const uint32_t orig_dip = t.daddr;
-    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a);
+    // issued ahead of the conntrack probes (independent reads of read-only tables):
+    // the ipcache lookup of orig_dip and the endpoint lookup of the packet's daddr
+    const bool lookups = !(p.ablate & AB_EG_NO_LOOKUPS);
+    Lpm4Pending ipq;
+    if (lookups && p.ipc4.l1) ipq = lpm4_begin(p.ipc4, bswap32(orig_dip));
+    const uint32_t lxc_key = s.daddr;
+    Probe<LxcV4Spec> lxq;
+    if (lookups && p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
+    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags | (p.ablate << 16), slot, &st, a);
     int verdict;
     uint32_t iv;
+    bool lxc_hit = false;
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
-    {                                                             // destination category (:482-494)
-        const uint32_t lab = ipcache4(p, orig_dip, a);
+    if (lookups) {                                                // destination category (:482-494)
+        uint32_t lab = 0;
+        if (p.ipc4.l1) { a.nl++; lab = lpm4_end(ipq, p.ipc4); }
         res.dst = lab ? lab : ((orig_dip & p.v4_cluster_mask) == p.v4_cluster_range ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+    verdict = (p.ablate & AB_EG_NO_POLICY) ? 0 : policy_egress(ep.policy, p.flags | (p.ablate << 16), s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) { dev_kill<Ct4Spec>(ep.ct4, slot); a.nu++; }   // ct_delete4
         ret = verdict;
@@ -631,13 +641,19 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         eg_final(o, i, res, a);
         return;
     }
-    if (lxc4_find(p, s.daddr, iv, a)) {
+    if (lookups && p.lxc4.buckets) {
+        a.nl++;                                                   // lookup_ip4_endpoint(ip4)
+        lxc_hit = s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv) >= 0
+                                     : dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv) >= 0;
+    }
+    if (lxc_hit) {
         if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
         m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
         if (iv & (1u << 16)) { res.ret = TC_ACT_REDIRECT; eg_final(o, i, res, a); return; }
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
+        if (p.ablate & AB_EG_NO_DELIVERY) { res.ret = TC_ACT_OK; eg_final(o, i, res, a); return; }
         res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, (iv >> 17) & 1u, now, ct2, res.proxy,
                                  res.reason, a, m);
         eg_final(o, i, res, a);
@@ -661,7 +677,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     rec_load(r, b, i, 8);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Eg6 x;
     eg6_state(r, eg, x);
@@ -670,9 +686,12 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
     const uint32_t orig_dip[4] = {t.daddr[0], t.daddr[1], t.daddr[2], t.daddr[3]};
+    Probe<LxcV6Spec> lxq;                                         // endpoint lookup of daddr, issued early
+    if (p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
     int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a);
     int verdict;
     uint32_t iv;
+    bool lxc_hit = false;
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     {
@@ -680,7 +699,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         res.dst = lab ? lab
                       : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+    verdict = policy_egress(ep.policy, p.flags | (p.ablate << 16), s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) { dev_kill<Ct6Spec>(ep.ct6, slot); a.nu++; }
         ret = verdict;
@@ -706,7 +725,11 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         eg_final(o, i, res, a);
         return;
     }
-    if (lxc6_find(p, s.daddr, iv, a)) {
+    if (p.lxc6.buckets) {                                         // lookup_ip6_endpoint (the daddr is unchanged)
+        a.nl++;
+        lxc_hit = probe_end<LxcV6Spec>(lxq, p.lxc6, s.daddr, &iv) >= 0;
+    }
+    if (lxc_hit) {
         if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
         m.fwd(s.len, METRIC_EGRESS);
         if (iv & (1u << 16)) { res.ret = TC_ACT_REDIRECT; eg_final(o, i, res, a); return; }
@@ -728,19 +751,42 @@ drop:
     eg_final(o, i, res, a);
 }
 
+#ifdef CV_EG_WPE
+#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WPE, 8)))
+#else
+#define CV_EG_OCC
+#endif
+
 template <bool V6>
-__global__ void __launch_bounds__(BLOCK) k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
+__global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
     Met m;
+    pol_cache_init(pc);
     met_init(m, lm);
+    m.pc = &pc;
+    // AB_EG_ONE_PER_GROUP (timing only): the first member of each group alone
+#if CV_EG_RUNS == 0
     for_each_group(g, V6 ? Q_CT6 : Q_CT4, [&](uint32_t, uint32_t head) {
+        if (p.ablate & AB_EG_ONE_PER_GROUP) {
+            if constexpr (V6) egress6_one(p, b, now, o, g, head, m);
+            else egress4_one(p, b, now, o, g, head, m);
+            return;
+        }
         group_in_order(g, head, 2, [&](uint32_t x) {
             if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
             else egress4_one(p, b, now, o, g, x, m);
         });
     });
-    met_flush(m, p.metrics);
+#else
+    for_each_run<CV_EG_RUNS != 2>(g, V6 ? Q_CT6 : Q_CT4, p.ablate & AB_EG_ONE_PER_GROUP, [&](uint32_t x) {
+        if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
+        else egress4_one(p, b, now, o, g, x, m);
+    });
+#endif
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
 }
 
 // ================================================================== deferred NAT tuples
@@ -803,8 +849,12 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
+    if (CV_EG_RUNS) launch_group_runs(g, Q_CT4, grid.x, runs_sched(CV_EG_RUNS), s);
     hipLaunchKernelGGL(k_egress_ct<false>, grid, blk, 0, s, p, b, now, o, g);
-    if (b.stride >= 128) hipLaunchKernelGGL(k_egress_ct<true>, grid, blk, 0, s, p, b, now, o, g);
+    if (b.stride >= 128) {
+        if (CV_EG_RUNS) launch_group_runs(g, Q_CT6, grid.x, runs_sched(CV_EG_RUNS), s);
+        hipLaunchKernelGGL(k_egress_ct<true>, grid, blk, 0, s, p, b, now, o, g);
+    }
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);

@@ -149,7 +149,9 @@ template <class S>
 __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     if (!t.buckets) return -1;
+#ifndef CV_NO_TAGFIRST
     if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);
+#endif
     const uint64_t h = key_hash<S>(key);
     const uint32_t tag = tag_of(h);
     uint64_t b = h & t.mask;
@@ -170,6 +172,123 @@ __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *
         }
         if (stop) return -1;
         b = (b + 1) & t.mask;
+    }
+    return -1;
+}
+
+// ---------------------------------------------------------------- split-phase probe
+// probe_begin issues the home bucket's first load (tags for wide buckets, the whole
+// 64-B line for narrow ones) and returns at once; probe_end waits for it and
+// finishes the lookup (following the probe chain when the home bucket is full).
+// Beginning several independent lookups before ending any keeps their first memory
+// round trips in flight together: a dependent-latency chain becomes one round trip.
+template <class S>
+struct Probe {
+    const uint32_t *bw;
+    uint64_t b;
+    uint32_t tag;
+    uint32_t w[S::BW >= 32 ? 2 : S::BW];
+};
+
+template <class S>
+__device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32_t *key)
+{
+    Probe<S> pr;
+    const uint64_t h = key_hash<S>(key);
+    pr.tag = tag_of(h);
+    pr.b = h & t.mask;
+    pr.bw = t.buckets ? t.buckets + pr.b * S::BW : nullptr;
+    if (!pr.bw) return pr;
+    if constexpr (S::BW >= 32) {
+        const uint2 tg = *reinterpret_cast<const uint2 *>(pr.bw);
+        pr.w[0] = tg.x; pr.w[1] = tg.y;
+    } else {
+        const uint4 *q = reinterpret_cast<const uint4 *>(pr.bw);
+#pragma unroll
+        for (int i = 0; i < S::BW / 4; ++i) {
+            const uint4 v = q[i];
+            pr.w[4 * i] = v.x; pr.w[4 * i + 1] = v.y; pr.w[4 * i + 2] = v.z; pr.w[4 * i + 3] = v.w;
+        }
+    }
+    return pr;
+}
+
+template <class S>
+__device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable &t, const uint32_t *key, uint32_t *ival)
+{
+    if (!pr.bw) return -1;
+    uint64_t b = pr.b;
+    bool stop;
+    if constexpr (S::BW >= 32) {
+        uint64_t match;
+        tag_masks<S>((uint64_t)pr.w[0] | ((uint64_t)pr.w[1] << 32), pr.tag, match, stop);
+        while (match) {
+            const int sl = (__builtin_ctzll(match) >> 3);
+            match &= match - 1;
+            const uint32_t *kw = pr.bw + S::KEY0 + sl * S::KW;
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+            if (eq) {
+#pragma unroll
+                for (int j = 0; j < S::IVW; ++j) ival[j] = pr.bw[S::IVAL0 + sl * S::IVW + j];
+                return (int64_t)(b * S::SPB + sl);
+            }
+        }
+    } else {
+        const int s = match_bucket<S>(pr.w, key, pr.tag, &stop);
+        if (s >= 0) {
+#pragma unroll
+            for (int q = 0; q < S::SPB; ++q) {
+#pragma unroll
+                for (int j = 0; j < S::IVW; ++j)
+                    if (q == s) ival[j] = pr.w[S::IVAL0 + q * S::IVW + j];
+                if (S::IVH && q == s) ival[0] = half_at<S>(pr.w, S::HVAL0 + q);
+            }
+            return (int64_t)(b * S::SPB + s);
+        }
+    }
+    if (stop) return -1;
+    // rare: the home bucket is full, continue the chain from the next bucket
+    for (int p = 1; p < MAX_PROBE; ++p) {
+        b = (b + 1) & t.mask;
+        Probe<S> nx;
+        nx.tag = pr.tag;
+        nx.b = b;
+        nx.bw = t.buckets + b * S::BW;
+        if constexpr (S::BW >= 32) {
+            const uint2 tg = *reinterpret_cast<const uint2 *>(nx.bw);
+            uint64_t match;
+            tag_masks<S>((uint64_t)tg.x | ((uint64_t)tg.y << 32), pr.tag, match, stop);
+            while (match) {
+                const int sl = (__builtin_ctzll(match) >> 3);
+                match &= match - 1;
+                const uint32_t *kw = nx.bw + S::KEY0 + sl * S::KW;
+                bool eq = true;
+#pragma unroll
+                for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+                if (eq) {
+#pragma unroll
+                    for (int j = 0; j < S::IVW; ++j) ival[j] = nx.bw[S::IVAL0 + sl * S::IVW + j];
+                    return (int64_t)(b * S::SPB + sl);
+                }
+            }
+        } else {
+            uint32_t w[S::BW];
+            load_bucket<S>(t.buckets, b, w);
+            const int s = match_bucket<S>(w, key, pr.tag, &stop);
+            if (s >= 0) {
+#pragma unroll
+                for (int q = 0; q < S::SPB; ++q) {
+#pragma unroll
+                    for (int j = 0; j < S::IVW; ++j)
+                        if (q == s) ival[j] = w[S::IVAL0 + q * S::IVW + j];
+                    if (S::IVH && q == s) ival[0] = half_at<S>(w, S::HVAL0 + q);
+                }
+                return (int64_t)(b * S::SPB + s);
+            }
+        }
+        if (stop) return -1;
     }
     return -1;
 }

@@ -218,7 +218,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     rec_load(r, b, i, 3);
     const uint32_t meta = g.meta[i];
     const EpDev &ep = p.eps[meta & 0xFFFFu];
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
     int32_t reason = 0;
@@ -232,16 +232,156 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     store_out(o, i, a);
 }
 
+#ifdef CV_EG_WPE
+#define CV_CT_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WPE, 8)))
+#else
+#define CV_CT_OCC
+#endif
+
 // stage 2: conntrack + policy, each address-pair group by one lane in packet order
-__global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+__global__ void __launch_bounds__(BLOCK) CV_CT_OCC k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
 {
     __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
     Met m;
+    pol_cache_init(pc);
     met_init(m, lm);
+    m.pc = &pc;
+#if CV_RUNS_MODE == 0
     for_each_group(g, Q_NETDEV, [&](uint32_t, uint32_t head) {
         group_in_order(g, head, 0, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
     });
-    met_flush(m, p.metrics);
+#else
+    for_each_run<CV_RUNS_MODE != 2>(g, Q_NETDEV, false, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
+#endif
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
+}
+
+// ------------------------------------------------------------------ size-sorted runs
+// k_group_flatten: every queued group of q becomes a run {size, members ascending}
+// in `order` (one block-aggregated allocation per 256 groups); the queue word is
+// replaced by the run's offset; per-class counts.  Block-uniform loop (the scans use
+// every lane).
+__global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q)
+{
+    __shared__ uint32_t hist[NCLASS], wsum[BLOCK / 64], bbase;
+    if (threadIdx.x < NCLASS) hist[threadIdx.x] = 0;
+    uint32_t n[QSPLIT];
+    const uint32_t total = queue_sizes(g, q, n);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t base = blockIdx.x * BLOCK; base < total; base += gridDim.x * BLOCK) {
+        const uint32_t j = base + threadIdx.x;
+        const bool act = j < total;
+        uint32_t *ent = nullptr, cnt = 0, x = NONE, head = NONE;
+        uint32_t m[GMAX];
+        if (act) {
+            ent = queue_entry(g, q, n, j);
+            head = (uint32_t)g.table[2 * *ent + 1];
+            for (x = head; x != NONE && cnt < GMAX; x = g.next[x]) {   // insertion into registers
+                int pos = 0;
+#pragma unroll
+                for (int t = 0; t < GMAX; ++t) pos += (t < (int)cnt && m[t] < x) ? 1 : 0;
+#pragma unroll
+                for (int t = GMAX - 1; t >= 0; --t) {
+                    const uint32_t left = t > 0 ? m[t - 1] : 0u;
+                    m[t] = (t < pos) ? m[t] : (t == pos ? x : left);
+                }
+                ++cnt;
+            }
+            for (uint32_t y = x; y != NONE; y = g.next[y]) ++cnt;
+        }
+        const uint32_t need = act ? cnt + 1 : 0;
+        uint32_t incl = need;                                     // wave inclusive scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += t;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int w = 0; w < BLOCK / 64; ++w) { const uint32_t t = wsum[w]; wsum[w] = acc; acc += t; }
+            bbase = acc ? atomicAdd(&g.cursor[RUN_CURSOR], acc) : 0;
+        }
+        __syncthreads();
+        if (act) {
+            const uint32_t off = bbase + wsum[wv] + incl - need;
+            uint32_t *o = g.order + off;
+            o[0] = cnt;
+            if (cnt <= GMAX) {
+#pragma unroll
+                for (int t = 0; t < GMAX; ++t)
+                    if (t < (int)cnt) o[1 + t] = m[t];
+            } else {                                              // large group: copy, shell sort
+                uint32_t k = 1;
+                for (uint32_t y = head; y != NONE; y = g.next[y]) o[k++] = y;
+                ++o;
+                for (uint32_t gap = cnt / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {
+                    for (uint32_t i = gap; i < cnt; ++i) {
+                        const uint32_t v = o[i];
+                        uint32_t t = i;
+                        for (; t >= gap && o[t - gap] > v; t -= gap) o[t] = o[t - gap];
+                        o[t] = v;
+                    }
+                }
+            }
+            *ent = off;
+            atomicAdd(&hist[size_class(cnt)], 1u);
+        }
+        __syncthreads();                                          // wsum / bbase reuse
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLASS && hist[threadIdx.x]) atomicAdd(&g.cursor[qcls(q, threadIdx.x)], hist[threadIdx.x]);
+}
+
+// k_group_schedule: `work` lists the runs class by class, largest class first
+constexpr int SCHED_PER_THREAD = 4;
+__global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q, bool largest_first)
+{
+    __shared__ uint32_t cbase[NCLASS], lcnt[NCLASS], lbase[NCLASS];
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < NCLASS; ++k) {
+            const int c = largest_first ? NCLASS - 1 - k : k;
+            cbase[c] = acc;
+            acc += g.cursor[qcls(q, c)];
+        }
+    }
+    uint32_t n[QSPLIT];
+    const uint32_t total = queue_sizes(g, q, n);
+    constexpr uint32_t SPAN = BLOCK * SCHED_PER_THREAD;
+    for (uint32_t base = blockIdx.x * SPAN; base < total; base += gridDim.x * SPAN) {
+        if (threadIdx.x < NCLASS) lcnt[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t off[SCHED_PER_THREAD], cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD];
+#pragma unroll
+        for (int u = 0; u < SCHED_PER_THREAD; ++u) {
+            const uint32_t j = base + u * BLOCK + threadIdx.x;
+            if (j < total) {
+                off[u] = *queue_entry(g, q, n, j);
+                cls[u] = size_class(g.order[off[u]]);
+                rank[u] = atomicAdd(&lcnt[cls[u]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < NCLASS && lcnt[threadIdx.x])
+            lbase[threadIdx.x] = atomicAdd(&g.cursor[qcls(q, threadIdx.x) + 1], lcnt[threadIdx.x]);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < SCHED_PER_THREAD; ++u) {
+            const uint32_t j = base + u * BLOCK + threadIdx.x;
+            if (j < total) g.work[cbase[cls[u]] + lbase[cls[u]] + rank[u]] = off[u];
+        }
+        __syncthreads();
+    }
+}
+
+void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_group_flatten, dim3(grid), dim3(BLOCK), 0, s, g, q);
+    if (sched) hipLaunchKernelGGL(k_group_schedule, dim3(grid), dim3(BLOCK), 0, s, g, q, sched == 1);
 }
 
 // ------------------------------------------------------------------ CT map API
@@ -366,6 +506,7 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
     if (!b.n) return 0;
     hipLaunchKernelGGL(k_netdev_front, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, with_prefilter);
     if (hipGetLastError() != hipSuccess) return -5;
+    if (CV_RUNS_MODE) launch_group_runs(g, Q_NETDEV, grid_for(b.n), runs_sched(CV_RUNS_MODE), s);
     hipLaunchKernelGGL(k_ct_stage, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, now);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -44,6 +44,39 @@ __device__ __forceinline__ uint32_t lpm4_lookup(const Lpm4 &t, uint32_t addr /* 
     return e;
 }
 
+// The same answer with the /32-front probe and the trie's first level read issued
+// together (one round trip when the front hits or the level-1 slot is final).
+struct Lpm4Pending {
+    Probe<Host32Spec> front;
+    uint32_t l1;
+    uint32_t addr;
+};
+
+__device__ __forceinline__ Lpm4Pending lpm4_begin(const Lpm4 &t, uint32_t addr /* host order */)
+{
+    Lpm4Pending q;
+    q.addr = addr;
+    const uint32_t k = bswap32(addr);
+    q.front = probe_begin<Host32Spec>(t.full, &k);
+    q.l1 = t.l1[addr >> 16];
+    return q;
+}
+
+__device__ __forceinline__ uint32_t lpm4_end(const Lpm4Pending &q, const Lpm4 &t)
+{
+    if (t.full.buckets) {
+        const uint32_t k = bswap32(q.addr);
+        uint32_t v;
+        if (probe_end<Host32Spec>(q.front, t.full, &k, &v) >= 0) return v;
+    }
+    uint32_t e = q.l1;
+    if (e & 0x80000000u) {
+        e = t.chunks[((e & 0x7FFFFFFFu) << 8) | ((q.addr >> 8) & 0xFFu)];
+        if (e & 0x80000000u) e = t.chunks[((e & 0x7FFFFFFFu) << 8) | (q.addr & 0xFFu)];
+    }
+    return e;
+}
+
 // Host builder.  Prefixes must be fed in non-decreasing priority (prefix length).
 struct Lpm4Builder {
     std::vector<uint32_t> l1 = std::vector<uint32_t>(65536, 0);

@@ -14,7 +14,7 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libcilium_hip.so")
+LIB_PATH = os.environ.get("CV_LIB") or os.path.join(HERE, "_lib", "libcilium_hip.so")   # CV_LIB: A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "cilium_hip.h")
 
 MAP_HASH, MAP_LRU_HASH, MAP_LPM_TRIE, MAP_PERCPU_HASH = 1, 9, 11, 5

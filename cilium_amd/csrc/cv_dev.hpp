@@ -322,6 +322,15 @@ __device__ __forceinline__ uint32_t ipcache4(const DpParams &p, uint32_t addr_ra
     return lpm4_lookup(p.ipc4, bswap32(addr_raw));
 }
 
+// ipcache4 through a quad probe of the /32 front (every lane calls; `want` as in
+// quad_find)
+__device__ __forceinline__ uint32_t ipcache4_q(const DpParams &p, uint32_t addr_raw, bool want, Acct &a, uint4 *st)
+{
+    if (!p.ipc4.l1) return 0;
+    if (want) a.nl++;
+    return lpm4_lookup_q(p.ipc4, bswap32(addr_raw), want, st);
+}
+
 // ipcache_lookup6 (eps.h:295-305) at /128
 __device__ __forceinline__ uint32_t ipcache6(const DpParams &p, const uint32_t *addr, Acct &a)
 {
@@ -340,6 +349,10 @@ __device__ __forceinline__ uint32_t identity_from_mark(uint32_t mark, bool &skip
     if (magic == 0xC00u) return HOST_ID;
     return WORLD_ID;
 }
+
+struct Hit;
+__device__ __forceinline__ int policy_hit(const HashTable &pol, uint32_t flags, uint32_t len, int64_t s, bool l4,
+                                          uint32_t proxy_port, Acct &a, Hit *defer);
 
 // A policy counter update held back by the lane: the atomic is issued after the
 // lane's last dependent lookup, so in-order vmcnt never makes a lookup wait for it.
@@ -410,6 +423,14 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
             l4 = s >= 0;
         }
     }
+    return policy_hit(pol, flags, len, s, l4, px[0], a, defer);
+}
+
+// the end of __policy_can_access once the lookups are done: slot s (or -1) of the
+// matching entry, l4 if it was an L4 key, its inline proxy port
+__device__ __forceinline__ int policy_hit(const HashTable &pol, uint32_t flags, uint32_t len, int64_t s, bool l4,
+                                          uint32_t proxy_port, Acct &a, Hit *defer)
+{
     if (s < 0) return DROP_POLICY;
     a.nu++;
     uint8_t *v = pol.vals + (size_t)s * pol.vstride;
@@ -427,7 +448,60 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
             atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
         }
     }
-    return l4 ? (int)px[0] : TC_ACT_OK;
+    return l4 ? (int)proxy_port : TC_ACT_OK;
+}
+
+// policy_access with quad probes (quad_find): every lane of the wave calls it;
+// `want` false = this lane does not look up (result unused)
+__device__ __forceinline__ int policy_access_q(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
+                                               uint32_t dport_raw, uint32_t proto, int dir, Acct &a, Hit *defer,
+                                               bool want, uint4 *st)
+{
+    want = want && !(flags & F_DROP_ALL);
+    const uint32_t eg = dir ? 0u : 1u;
+    const bool have_l4 = flags & F_HAVE_L4_POLICY;
+    int64_t s = -1;
+    uint32_t px = 0, v1 = 0, v2 = 0, v3 = 0;
+    bool l4 = false;
+    const uint32_t kl4[2] = {identity, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
+    const uint32_t kl3[2] = {identity, eg << 24};
+    const uint32_t kwc[2] = {0, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
+#ifdef CV_POL_PAIR
+    if (have_l4) {                                                // L4 and L3 keys read together
+        int64_t s1, s2;
+        quad_find2<PolicySpec>(pol, kl4, want, kl3, want, st, s1, &v1, s2, &v2);
+        if (want) { a.nl++; s = s1; px = v1; l4 = s1 >= 0; }
+        if (want && s < 0) { a.nl++; s = s2; px = v2; }
+    } else {
+        const int64_t s2 = quad_find<PolicySpec>(pol, kl3, want, st, &v2);
+        if (want) { a.nl++; s = s2; px = v2; }
+    }
+#else
+    if (have_l4) {
+        const int64_t s1 = quad_find<PolicySpec>(pol, kl4, want, st, &v1);
+        if (want) { a.nl++; s = s1; px = v1; l4 = s1 >= 0; }
+    }
+    const int64_t s2 = quad_find<PolicySpec>(pol, kl3, want && s < 0, st, &v2);
+    if (want && s < 0) { a.nl++; s = s2; px = v2; }
+#endif
+    if (have_l4) {
+        const int64_t s3 = quad_find<PolicySpec>(pol, kwc, want && s < 0, st, &v3);
+        if (want && s < 0) { a.nl++; s = s3; px = v3; l4 = s3 >= 0; }
+    }
+    if (!want) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
+    return policy_hit(pol, flags, len, s, l4, px, a, defer);
+}
+
+// policy_ingress through policy_access_q (convergent; `want` as there)
+__device__ __forceinline__ int policy_ingress_q(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t src,
+                                                uint32_t dport_raw, uint32_t proto, Acct &a, Hit *defer, bool want,
+                                                uint4 *st)
+{
+    const bool look = (flags & F_POLICY_INGRESS) && !(flags & F_DROP_ALL);
+    const int r = policy_access_q(pol, flags, len, src, dport_raw, proto, CT_INGRESS, a, defer, want && look, st);
+    if (!(flags & F_POLICY_INGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
+    if (flags & F_DROP_ALL) return DROP_POLICY;
+    return r >= TC_ACT_OK ? r : DROP_POLICY;
 }
 
 // policy_can_access_ingress (policy.h:305-329)

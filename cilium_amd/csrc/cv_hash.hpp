@@ -91,6 +91,12 @@ __device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets
     const uint4 *q = reinterpret_cast<const uint4 *>(buckets + b * S::BW);
 #pragma unroll
     for (int i = 0; i < S::BW / 4; ++i) {
+#ifdef CV_TIMING_BUCKET_VECS
+        if (S::BW == 16 && i >= CV_TIMING_BUCKET_VECS) {          // timing probe only: wrong answers
+            w[4 * i] = w[4 * i + 1] = w[4 * i + 2] = w[4 * i + 3] = 0;
+            continue;
+        }
+#endif
         uint4 v = q[i];
         w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
@@ -144,18 +150,32 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
     return -1;
 }
 
+// the full-bucket probe chain from bucket b (probe number p0 of MAX_PROBE)
+template <class S>
+__device__ __forceinline__ int64_t dev_find_from(const HashTable &t, const uint32_t *key, uint32_t tag, uint64_t b,
+                                                 int p0, uint32_t *ival);
+
 // Returns the slot index (bucket * SPB + slot) or -1; copies the inline value.
 template <class S>
 __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     if (!t.buckets) return -1;
 #ifndef CV_NO_TAGFIRST
+#ifdef CV_TF_ALL
+    if constexpr (true) return dev_find_tf<S>(t, key, ival);
+#else
     if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);
 #endif
+#endif
     const uint64_t h = key_hash<S>(key);
-    const uint32_t tag = tag_of(h);
-    uint64_t b = h & t.mask;
-    for (int p = 0; p < MAX_PROBE; ++p) {
+    return dev_find_from<S>(t, key, tag_of(h), h & t.mask, 0, ival);
+}
+
+template <class S>
+__device__ __forceinline__ int64_t dev_find_from(const HashTable &t, const uint32_t *key, uint32_t tag, uint64_t b,
+                                                 int p0, uint32_t *ival)
+{
+    for (int p = p0; p < MAX_PROBE; ++p) {
         uint32_t w[S::BW];
         load_bucket<S>(t.buckets, b, w);
         bool stop;
@@ -177,6 +197,156 @@ __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *
 }
 
 // ---------------------------------------------------------------- split-phase probe
+// ---------------------------------------------------------------- quad probes
+// A lane reading a whole 64-B bucket alone issues four 16-B loads to one line: four
+// line accesses in the texture path for 64 bytes.  Here the 4 lanes of a quad read
+// each other's home buckets together: in round k every lane of the quad loads one
+// 16-B part of quad-lane k's bucket, straight into LDS (global_load_lds_dwordx4), so
+// one wave-instruction touches 16 lines instead of 64; each lane then reads its own
+// bucket back from LDS.  Round k's lane r loads part (r + k) & 3, which places the 4
+// parts a lane reads back for one part index in 4 different LDS banks.
+//
+// Every lane of the wave must call it at the same point (quad-lane broadcasts);
+// `mine` = the lane's bucket or null (no lookup).  `st`: the wave's 4 KiB LDS stage.
+template <int K>
+__device__ __forceinline__ void quad_round(int plo, int phi, int r, uint4 *st)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp(plo, K * 0x55, 0xF, 0xF, false);   // quad_perm [K,K,K,K]
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp(phi, K * 0x55, 0xF, 0xF, false);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>((uintptr_t)((uint64_t)hi << 32 | lo));
+    if (src) __builtin_amdgcn_global_load_lds(src + 4 * ((r + K) & 3), st + K * 64, 16, 0, 0);
+}
+
+__device__ __forceinline__ void quad_load64(const uint32_t *mine, uint4 *st, uint32_t (&w)[16])
+{
+    const int lane = (int)(threadIdx.x & 63), r = lane & 3, qb = lane & ~3;
+    const uint64_t pm = (uint64_t)(uintptr_t)mine;
+    const int plo = (int)(uint32_t)pm, phi = (int)(uint32_t)(pm >> 32);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // earlier LDS reads of st are done
+    __builtin_amdgcn_wave_barrier();
+    quad_round<0>(plo, phi, r, st);
+    quad_round<1>(plo, phi, r, st);
+    quad_round<2>(plo, phi, r, st);
+    quad_round<3>(plo, phi, r, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (mine) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 v = st[r * 64 + qb + ((j - r) & 3)];
+            w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// two buckets per lane in one pass (8 rounds, one wait): stage `st` holds 8 KiB
+__device__ __forceinline__ void quad_load64x2(const uint32_t *m0, const uint32_t *m1, uint4 *st, uint32_t (&w0)[16],
+                                              uint32_t (&w1)[16])
+{
+    const int lane = (int)(threadIdx.x & 63), r = lane & 3, qb = lane & ~3;
+    const uint64_t p0 = (uint64_t)(uintptr_t)m0, p1 = (uint64_t)(uintptr_t)m1;
+    const int lo0 = (int)(uint32_t)p0, hi0 = (int)(uint32_t)(p0 >> 32);
+    const int lo1 = (int)(uint32_t)p1, hi1 = (int)(uint32_t)(p1 >> 32);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    quad_round<0>(lo0, hi0, r, st);
+    quad_round<1>(lo0, hi0, r, st);
+    quad_round<2>(lo0, hi0, r, st);
+    quad_round<3>(lo0, hi0, r, st);
+    quad_round<0>(lo1, hi1, r, st + 256);
+    quad_round<1>(lo1, hi1, r, st + 256);
+    quad_round<2>(lo1, hi1, r, st + 256);
+    quad_round<3>(lo1, hi1, r, st + 256);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (m0) {
+            const uint4 v = st[r * 64 + qb + ((j - r) & 3)];
+            w0[4 * j] = v.x; w0[4 * j + 1] = v.y; w0[4 * j + 2] = v.z; w0[4 * j + 3] = v.w;
+        }
+        if (m1) {
+            const uint4 v = st[256 + r * 64 + qb + ((j - r) & 3)];
+            w1[4 * j] = v.x; w1[4 * j + 1] = v.y; w1[4 * j + 2] = v.z; w1[4 * j + 3] = v.w;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the bucket snapshot w of bucket b: slot index or -1 (chain continued lane by lane)
+template <class S>
+__device__ __forceinline__ int64_t quad_match(const HashTable &t, const uint32_t *key, uint32_t tag, uint64_t b,
+                                              const uint32_t (&w)[16], uint32_t *ival)
+{
+    bool stop;
+    const int s = match_bucket<S>(w, key, tag, &stop);
+    if (s >= 0) {
+#pragma unroll
+        for (int q = 0; q < S::SPB; ++q) {
+#pragma unroll
+            for (int j = 0; j < S::IVW; ++j)
+                if (q == s) ival[j] = w[S::IVAL0 + q * S::IVW + j];
+            if (S::IVH && q == s) ival[0] = half_at<S>(w, S::HVAL0 + q);
+        }
+        return (int64_t)(b * S::SPB + s);
+    }
+    if (stop) return -1;
+    return dev_find_from<S>(t, key, tag, (b + 1) & t.mask, 1, ival);
+}
+
+// two quad_find in one pass
+template <class S>
+__device__ __forceinline__ void quad_find2(const HashTable &t, const uint32_t *k0, bool want0, const uint32_t *k1,
+                                           bool want1, uint4 *st, int64_t &s0, uint32_t *iv0, int64_t &s1,
+                                           uint32_t *iv1)
+{
+    const uint64_t h0 = key_hash<S>(k0), h1 = key_hash<S>(k1);
+    const uint64_t b0 = h0 & t.mask, b1 = h1 & t.mask;
+    const uint32_t *bw0 = (want0 && t.buckets) ? t.buckets + b0 * S::BW : nullptr;
+    const uint32_t *bw1 = (want1 && t.buckets) ? t.buckets + b1 * S::BW : nullptr;
+    uint32_t w0[16], w1[16];
+    quad_load64x2(bw0, bw1, st, w0, w1);
+    s0 = bw0 ? quad_match<S>(t, k0, tag_of(h0), b0, w0, iv0) : -1;
+    s1 = bw1 ? quad_match<S>(t, k1, tag_of(h1), b1, w1, iv1) : -1;
+}
+
+// dev_find for 64-B buckets through quad_load64 (same result); `want` false: no
+// lookup (the lane still takes part)
+template <class S>
+__device__ __forceinline__ int64_t quad_find(const HashTable &t, const uint32_t *key, bool want, uint4 *st,
+                                             uint32_t *ival)
+{
+    static_assert(S::BW == 16, "64-B buckets");
+    const uint64_t h = key_hash<S>(key);
+    const uint32_t tag = tag_of(h);
+    const uint64_t b = h & t.mask;
+    const uint32_t *bw = (want && t.buckets) ? t.buckets + b * S::BW : nullptr;
+    uint32_t w[16];
+    quad_load64(bw, st, w);
+    if (!bw) return -1;
+    bool stop;
+    const int s = match_bucket<S>(w, key, tag, &stop);
+    if (s >= 0) {
+#pragma unroll
+        for (int q = 0; q < S::SPB; ++q) {
+#pragma unroll
+            for (int j = 0; j < S::IVW; ++j)
+                if (q == s) ival[j] = w[S::IVAL0 + q * S::IVW + j];
+            if (S::IVH && q == s) ival[0] = half_at<S>(w, S::HVAL0 + q);
+        }
+        return (int64_t)(b * S::SPB + s);
+    }
+    if (stop) return -1;
+    return dev_find_from<S>(t, key, tag, (b + 1) & t.mask, 1, ival);   // rare: the chain goes on
+}
+
 // probe_begin issues the home bucket's first load (tags for wide buckets, the whole
 // 64-B line for narrow ones) and returns at once; probe_end waits for it and
 // finishes the lookup (following the probe chain when the home bucket is full).

@@ -58,8 +58,79 @@ __device__ __forceinline__ int l4_key_new_flow(const Rec &r, uint32_t &dport_raw
 // PPT packets per lane: lane t of workgroup w takes packets w*PPT*BLOCK + k*BLOCK + t
 // (coalesced per k); its policy counter atomics wait in registers until its last
 // lookup is done.
-constexpr int PPT = 4;
+#ifndef CV_PPT
+#define CV_PPT 4
+#endif
+constexpr int PPT = CV_PPT;
 
+#ifndef CV_NO_QUAD
+// Quad-probe form: the table probes are quad_find (cv_hash.hpp), so every lane of
+// the wave reaches each probe; lanes without a lookup (past the batch end, non-IPv4,
+// short or invalid headers) take part with want = false.  (Holding the results in
+// registers until after the last probe, so the probes' vmcnt waits skip the output
+// stores, measured 3 % slower.)
+__global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
+{
+    __shared__ LdsMetrics lm;
+#ifdef CV_POL_PAIR
+    __shared__ uint4 stage[BLOCK / 64][512];
+#else
+    __shared__ uint4 stage[BLOCK / 64][256];
+#endif
+    Met m;
+    met_init(m, lm);
+    const HashTable pol = p.eps[ep].policy;
+    uint4 *st = stage[threadIdx.x >> 6];
+    Hit hits[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        hits[k] = Hit{nullptr, 0};
+        const uint32_t i = blockIdx.x * (PPT * BLOCK) + k * BLOCK + threadIdx.x;
+        const uint32_t i0 = i - (threadIdx.x & 63);
+        if (i0 >= b.n) continue;                                  // the whole wave is past the end
+        const bool live = i < b.n;
+        Rec r;
+        if (p.recmode == 2 && b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 3, st);
+        else if (!live) { r.len = 0; for (int j = 0; j < 16; ++j) r.w[j] = 0; }
+        else if (p.recmode == 1) rec_load_plain(r, b, i, 3);
+        else rec_load(r, b, i, 3);
+        Acct a{0, 0};
+        bool skip_proxy = false;
+        uint32_t identity = 0;
+        if (live && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
+        const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
+        const bool v4 = live && eth == 0x0008u && r.len >= 34;
+        const bool want_ipc = v4 && identity < HEALTH_ID && !(p.ablate & AB_NO_IPCACHE);   // bpf_netdev.c:375-398
+        const uint32_t lab = ipcache4_q(p, rec_raw32c<26>(r), want_ipc, a, st);
+        if (want_ipc && lab && lab != CLUSTER_ID && lab != HOST_ID) identity = lab;
+        int32_t ret = eth != 0x0008u ? DROP_UNKNOWN_L3 : r.len < 34 ? DROP_INVALID : 0;
+        uint32_t dport = 0, proto = 0;
+        if (v4) ret = l4_key_new_flow(r, dport, proto);
+        const bool want_pol = v4 && ret == 0 && !(p.ablate & AB_NO_POLICY);
+        const int v = policy_ingress_q(pol, p.flags | (p.ablate << 16), r.len, identity, dport, proto, a, &hits[k],
+                                       want_pol, st);
+        uint16_t proxy = 0;
+        if (v4 && ret == 0) {
+            const int vv = (p.ablate & AB_NO_POLICY) ? (int)(identity & 1) : v;
+            if (vv < 0) ret = DROP_POLICY;
+            else if (skip_proxy && vv > 0) ret = 0;
+            else { ret = vv; proxy = vv > 0 ? (uint16_t)vv : 0; }
+        }
+        if (!live) continue;
+        const bool dropped = ret < 0 && ret != E_TRUNC;
+        if (dropped && !(p.ablate & AB_NO_METRICS)) m.drop(ret, r.len, METRIC_INGRESS);
+        if (o.ret) o.ret[i] = ret;
+        if (o.reason) o.reason[i] = dropped ? ret : 0;
+        if (o.identity) o.identity[i] = identity;
+        if (o.proxy) o.proxy[i] = proxy;
+        if (o.ct) o.ct[i] = CT_NONE;
+        store_out(o, i, a);
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) hit_flush(hits[k]);
+    met_flush(m, p.metrics);
+}
+#else
 __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
 {
     __shared__ LdsMetrics lm;
@@ -119,6 +190,7 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
     for (int k = 0; k < PPT; ++k) hit_flush(hits[k]);
     met_flush(m, p.metrics);
 }
+#endif
 
 // ================================================================== config 3
 // stage 1: XDP prefilter + from_netdev/handle_ipv4 up to the tail call into the

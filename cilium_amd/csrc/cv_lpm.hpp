@@ -44,6 +44,29 @@ __device__ __forceinline__ uint32_t lpm4_lookup(const Lpm4 &t, uint32_t addr /* 
     return e;
 }
 
+// lpm4_lookup with the /32 front read by a quad probe: every lane of the wave calls
+// it; returns 0 when `want` is false
+__device__ __forceinline__ uint32_t lpm4_lookup_q(const Lpm4 &t, uint32_t addr /* host order */, bool want, uint4 *st)
+{
+    const uint32_t k = bswap32(addr);
+    uint32_t v = 0;
+#ifdef CV_L1_PREFETCH
+    const uint32_t l1 = want ? t.l1[addr >> 16] : 0u;             // in flight with the front probe
+#endif
+    if (quad_find<Host32Spec>(t.full, &k, want, st, &v) >= 0) return v;
+    if (!want) return 0;
+#ifdef CV_L1_PREFETCH
+    uint32_t e = l1;
+#else
+    uint32_t e = t.l1[addr >> 16];
+#endif
+    if (e & 0x80000000u) {
+        e = t.chunks[((e & 0x7FFFFFFFu) << 8) | ((addr >> 8) & 0xFFu)];
+        if (e & 0x80000000u) e = t.chunks[((e & 0x7FFFFFFFu) << 8) | (addr & 0xFFu)];
+    }
+    return e;
+}
+
 // The same answer with the /32-front probe and the trie's first level read issued
 // together (one round trip when the front hits or the level-1 slot is final).
 struct Lpm4Pending {

@@ -106,6 +106,21 @@ def test_config2_vs_oracle(dev):
     assert (ctx.metrics() == dp.metrics()).all()
 
 
+@pytest.mark.parametrize("n", [1, 37, 5037, 4097])
+def test_config2_ragged(dev, n):
+    """Batch ends inside a wave / a workgroup (lanes past the end still take part in
+    the quad probes)."""
+    w = synth.config2(n)
+    dp, om = H.oracle_dp(w)
+    ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+    ctx, pm = H.product_ctx(w)
+    o = run_policy(ctx, w, dev)
+    for k in ("ret", "identity", "proxy", "nl", "nu"):
+        assert (o[k] == getattr(ref, k)).all(), k
+    assert (ctx.metrics() == dp.metrics()).all()
+    check_policy_maps(pm["policy"], om["policy"])
+
+
 def test_policy_counters_across_agent_updates(dev):
     w = synth.config2(1 << 14, n_cidrs=2048, n_ids=200)
     dp, om = H.oracle_dp(w)

@@ -22,7 +22,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage",
-            "config5": "k_egress_ct"}
+            "config5": "k_egress_ct<false>"}
 
 
 def per_kernel(path):

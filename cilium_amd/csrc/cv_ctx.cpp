@@ -874,6 +874,40 @@ int cv_map_delete(cv_ctx *c, int h, const void *key)
     return r;
 }
 
+// ctmap.GC with GCFilterByTime / ctmap.Flush (pkg/maps/ctmap/ctmap.go:325-432,
+// doFiltering :400-408): delete every entry of CT map h whose lifetime is below
+// `time`.  A bound (device-resident) CT map is swept on the GPU in one pass; an
+// unbound one in its host store.
+int cv_ct_gc(cv_ctx *c, int h, uint32_t time, uint32_t *deleted)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    uint32_t n = 0;
+    if (m->kind != MK_PLAIN) {
+        if (set_device(c)) return -ENODEV;
+        DevBuf d;
+        if (d.alloc(4)) return -ENOMEM;
+        if (hipMemset(d.p, 0, 4) != hipSuccess) return -EIO;
+        if (launch_ct_gc(m->ct.view, m->kind == MK_CT6, m->ct.nb, time, d.as<uint32_t>(), nullptr)) return -EIO;
+        if (hipMemcpy(&n, d.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+    } else {
+        HostMap *hm = m->hm.get();
+        if ((hm->ks != 14 && hm->ks != 40) || hm->vs != 56) return -EINVAL;
+        std::vector<std::vector<uint8_t>> dead;
+        hm->for_each([&](const uint8_t *k, const uint8_t *v) {
+            uint32_t life;
+            memcpy(&life, v + 32, 4);
+            if (life < time) dead.emplace_back(k, k + hm->ks);
+        });
+        for (auto &k : dead)
+            if (!hm->remove(k.data())) ++n;
+    }
+    if (deleted) *deleted = n;
+    return 0;
+}
+
 int cv_map_get_next_key(cv_ctx *c, int h, const void *key, void *next)
 {
     if (!c || !next) return -EINVAL;

@@ -131,6 +131,8 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
 // op 0 lookup, 1 update (BPF_ANY/NOEXIST/EXIST in flags), 2 delete; v6 selects the
 // ipv6_ct_tuple table.  io = {key[KW words], value[16 words], rc}
 int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s);
+// ctmap.GC (GCFilterByTime): mark entries with lifetime < time dead; adds the count
+int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s);
 int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint32_t *out_keys, uint32_t *out_vals, uint32_t *count,
                    uint32_t max, hipStream_t s);
 

@@ -71,14 +71,14 @@ constexpr int PPT = CV_PPT;
 // stores, measured 3 % slower.)
 __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
 {
-    __shared__ LdsMetrics lm;
+    __shared__ unsigned long long drops[256 * 2];                 // ingress drops {count, bytes} by reason
 #ifdef CV_POL_PAIR
     __shared__ uint4 stage[BLOCK / 64][512];
 #else
     __shared__ uint4 stage[BLOCK / 64][256];
 #endif
-    Met m;
-    met_init(m, lm);
+    for (int j = threadIdx.x; j < 256 * 2; j += BLOCK) drops[j] = 0;
+    __syncthreads();
     const HashTable pol = p.eps[ep].policy;
     uint4 *st = stage[threadIdx.x >> 6];
     Hit hits[PPT];
@@ -118,7 +118,11 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
         }
         if (!live) continue;
         const bool dropped = ret < 0 && ret != E_TRUNC;
-        if (dropped && !(p.ablate & AB_NO_METRICS)) m.drop(ret, r.len, METRIC_INGRESS);
+        if (dropped && !(p.ablate & AB_NO_METRICS)) {             // send_drop_notify -> cilium_metrics
+            const uint32_t rr = (uint8_t)(-ret);
+            atomicAdd(&drops[2 * rr], 1ull);
+            atomicAdd(&drops[2 * rr + 1], (unsigned long long)r.len);
+        }
         if (o.ret) o.ret[i] = ret;
         if (o.reason) o.reason[i] = dropped ? ret : 0;
         if (o.identity) o.identity[i] = identity;
@@ -128,7 +132,13 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
     }
 #pragma unroll
     for (int k = 0; k < PPT; ++k) hit_flush(hits[k]);
-    met_flush(m, p.metrics);
+    __syncthreads();
+    if (p.metrics)                                                // (no forwards are counted on this path)
+        for (int j = threadIdx.x; j < 256; j += BLOCK)
+            if (drops[2 * j]) {
+                atomicAdd(&p.metrics[(j * 4 + METRIC_INGRESS) * 2], drops[2 * j]);
+                atomicAdd(&p.metrics[(j * 4 + METRIC_INGRESS) * 2 + 1], drops[2 * j + 1]);
+            }
 }
 #else
 __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
@@ -524,6 +534,48 @@ __global__ void k_ct_scan(HashTable t, int v6, uint64_t nslots, uint32_t *keys, 
 {
     if (v6) ct_scan<Ct6Spec>(t, nslots, keys, vals, count, max);
     else ct_scan<Ct4Spec>(t, nslots, keys, vals, count, max);
+}
+
+// ctmap.GC with GCFilterByTime (pkg/maps/ctmap/ctmap.go:325-432): one pass over the
+// table, a lane per bucket: read the 8 tag bytes, then the lifetime word of every
+// live slot, and mark the expired ones dead (the bucket's tag word rewritten once;
+// the pass runs stream-ordered between batches, so it is the only writer).
+template <class S>
+__device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted)
+{
+    uint32_t mine = 0;
+    for (uint64_t b = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t *bw = t.buckets + b * S::BW;
+        const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
+        uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32), out = tags;
+#pragma unroll
+        for (int sl = 0; sl < S::SPB; ++sl) {
+            const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
+            if (tag < 3) continue;
+            const uint32_t life = *reinterpret_cast<const uint32_t *>(t.vals + (b * S::SPB + sl) * t.vstride + 32);
+            if (life < time) {
+                out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
+                ++mine;
+            }
+        }
+        if (out != tags) *reinterpret_cast<uint2 *>(bw) = make_uint2((uint32_t)out, (uint32_t)(out >> 32));
+    }
+    const unsigned long long tot = wave_sum(mine);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(deleted, (uint32_t)tot);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_ct_gc(HashTable t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted)
+{
+    if (v6) ct_gc<Ct6Spec>(t, nb, time, deleted);
+    else ct_gc<Ct4Spec>(t, nb, time, deleted);
+}
+
+int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s)
+{
+    uint64_t g = (nb + BLOCK - 1) / BLOCK;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_ct_gc, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, time, deleted);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 // ------------------------------------------------------------------ host launchers

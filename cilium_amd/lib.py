@@ -92,6 +92,7 @@ def load():
         "cv_map_update_batch": (i32, [vp, i32, vp, vp, u32, u64, C.POINTER(u32)]),
         "cv_map_count": (i32, [vp, i32, C.POINTER(u32)]),
         "cv_map_dump": (i32, [vp, i32, vp, vp, u32]),
+        "cv_ct_gc": (i32, [vp, i32, u32, C.POINTER(u32)]),
         "cv_bind": (i32, [vp, i32, i32]),
         "cv_endpoint_add": (i32, [vp, C.c_uint16, u32, i32, i32]),
         "cv_sync": (i32, [vp]),
@@ -164,6 +165,14 @@ class Map:
     def __len__(self):
         n = C.c_uint32(0)
         _check(load().cv_map_count(self.ctx.h, self.h, C.byref(n)), "cv_map_count")
+        return n.value
+
+    def ct_gc(self, time):
+        """ctmap.GC(GCFilterByTime) (pkg/maps/ctmap/ctmap.go:325-432): delete the
+        entries whose lifetime < time; time = 0xFFFFFFFF is ctmap.Flush.  Returns the
+        number deleted."""
+        n = C.c_uint32(0)
+        _check(load().cv_ct_gc(self.ctx.h, self.h, time, C.byref(n)), "cv_ct_gc")
         return n.value
 
     def dump(self):

@@ -107,6 +107,12 @@ int cv_map_count(cv_ctx *ctx, int h, uint32_t *count);
 /* every entry (keys/vals host buffers of max rows); order unspecified, like a
  * GetNextKey walk.  Returns the number of rows written or -errno. */
 int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
+/* conntrack garbage collection: delete every entry of CT map h (ipv4_ct_tuple or
+ * ipv6_ct_tuple keys, ct_entry values) whose lifetime < time; *deleted = count.
+ * Replaces ctmap.GC(m, name, GCFilterByTime) / doGC4 / doGC6 and, with
+ * time = 0xFFFFFFFF, ctmap.Flush (pkg/maps/ctmap/ctmap.go:325-455).  Runs on the GPU
+ * for a bound CT map, ordered after the batches already submitted. */
+int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
 
 /* ---- binding: programs -> maps ---- */
 int cv_bind(cv_ctx *ctx, int role, int map_handle /* -1 unbinds */);

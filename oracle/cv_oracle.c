@@ -1740,3 +1740,24 @@ void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint
         if (out->xdp) out->xdp[i] = 0;
     }
 }
+
+/* ctmap.GC with GCFilterByTime / Flush (pkg/maps/ctmap/ctmap.go:325-432): every
+ * entry whose ct_entry.lifetime (u32 @32, host order) is below `time` is deleted
+ * (doFiltering, :400-408).  Flush is time = MaxTime.  Returns the number deleted. */
+uint32_t or_ct_gc(or_map *m, uint32_t time)
+{
+    if (!m || m->vs < 36) return 0;
+    const uint32_t n = or_map_count(m);
+    if (!n) return 0;
+    uint8_t *keys = malloc((size_t)n * m->ks), *vals = malloc((size_t)n * m->vs);
+    const uint32_t got = or_map_dump(m, keys, vals, n);
+    uint32_t deleted = 0;
+    for (uint32_t i = 0; i < got; ++i) {
+        uint32_t lifetime;
+        memcpy(&lifetime, vals + (size_t)i * m->vs + 32, 4);
+        if (lifetime < time && or_map_delete(m, keys + (size_t)i * m->ks) == 0) ++deleted;
+    }
+    free(keys);
+    free(vals);
+    return deleted;
+}

@@ -123,6 +123,8 @@ int      or_map_delete(or_map *m, const void *key);
 uint32_t or_map_count(const or_map *m);
 /* all entries, sorted by key bytes; returns the count written (<= max) */
 uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max);
+/* ctmap.GC(GCFilterByTime) on a CT map: delete entries with lifetime < time */
+uint32_t or_ct_gc(or_map *m, uint32_t time);
 void    *or_map_lookup_ptr(or_map *m, const void *key);
 
 /* ---- restated helpers pinned by test/bpf/unit-test.c ---- */

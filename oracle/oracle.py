@@ -44,6 +44,8 @@ def lib():
         L.or_map_count.argtypes = [vp]
         L.or_map_dump.restype = u32
         L.or_map_dump.argtypes = [vp, vp, vp, u32]
+        L.or_ct_gc.restype = u32
+        L.or_ct_gc.argtypes = [vp, u32]
         L.or_get_prefix.restype = u32
         L.or_get_prefix.argtypes = [i32]
         L.or_ipv6_addr_clear_suffix.argtypes = [vp, i32]
@@ -102,6 +104,10 @@ class OMap:
     def delete(self, key):
         k = np.ascontiguousarray(np.frombuffer(bytes(key), np.uint8))
         return lib().or_map_delete(self.h, k.ctypes.data)
+
+    def ct_gc(self, time):
+        """ctmap.GC (GCFilterByTime): delete CT entries with lifetime < time."""
+        return lib().or_ct_gc(self.h, time)
 
     def __len__(self):
         return lib().or_map_count(self.h)

@@ -223,6 +223,33 @@ def test_ct_map_api_on_device(dev):
     assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
 
 
+@pytest.mark.parametrize("flush", [False, True])
+def test_ct_gc_on_device(dev, flush):
+    """ctmap.GC(GCFilterByTime) / Flush on the device-resident CT map between two
+    batches, against the oracle: the deleted count, the surviving entries, and the
+    next batch's verdicts over the table with its tombstones."""
+    w = synth.config3(1 << 14, 1 << 12, n_ep=16, n_cidrs=512, n_ids=50, seed=21)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    half = w.n // 2
+    run_ingress(ctx, w, dev, 0, half)
+    dp.netdev_ingress(w.frames[:half], w.length[:half], w.mark[:half], now=w.now)
+    _, ov = om["ct4"].dump()
+    life = np.ascontiguousarray(ov[:, 32:36]).view("<u4").ravel()
+    t = 0xFFFFFFFF if flush else int(np.median(life)) + 1
+    want = int((life < t).sum())
+    assert want > 0
+    assert pm["ct4"].ct_gc(t) == om["ct4"].ct_gc(t) == want
+    assert len(pm["ct4"]) == len(om["ct4"]) == len(life) - want
+    o = run_ingress(ctx, w, dev, half, w.n)
+    ref = dp.netdev_ingress(w.frames[half:], w.length[half:], w.mark[half:], now=w.now)
+    for k in ("ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
+        assert (o[k] == getattr(ref, k)).all(), k
+    ck, cv = pm["ct4"].dump()
+    ok, ov = om["ct4"].dump()
+    assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
+
+
 def test_chunked_launches_config2(dev, monkeypatch):
     # batches larger than one launch chunk: per-chunk delta fold keeps counters exact
     monkeypatch.setenv("CV_MAX_CHUNK", "10007")

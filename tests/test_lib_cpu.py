@@ -84,3 +84,35 @@ def test_bind_checks_layouts():
         ctx.bind("lxc", bad)
     ok = ctx.map_create(lib.MAP_LPM_TRIE, 24, 8, 10)
     ctx.bind("ipcache", ok)
+
+
+def test_ct_gc_host_store_vs_oracle():
+    """ctmap.GC(GCFilterByTime) on an unbound CT map (host store) against the oracle's
+    restatement of doFiltering (pkg/maps/ctmap/ctmap.go:400-408), then Flush."""
+    from cilium_amd import synth
+    from oracle.oracle import OMap
+    w = synth.config3(256, 4096, n_ep=8, n_cidrs=256, n_ids=20, seed=5)
+    spec = w.maps["ct4"]
+    life = np.ascontiguousarray(spec.vals[:, 32:36]).view("<u4").ravel()
+    vals = spec.vals.copy()                       # spread the lifetimes: every third entry older
+    vals[::3, 32:36] = (life[::3] - 5000).astype("<u4").view(np.uint8).reshape(-1, 4)
+    life = np.ascontiguousarray(vals[:, 32:36]).view("<u4").ravel()
+    t = int(np.median(life))
+    ctx = lib.Ctx(-1)
+    m = ctx.map_create(spec.type, spec.key_size, spec.val_size, spec.max_entries)
+    m.update_batch(spec.keys, vals)
+    om = OMap(spec.type, spec.key_size, spec.val_size, spec.max_entries)
+    om.load(spec.keys, vals)
+    _, ov = om.dump()                             # (the spec repeats shared RELATED twins)
+    live = np.ascontiguousarray(ov[:, 32:36]).view("<u4").ravel()
+    want = int((live < t).sum())
+    assert 0 < want < len(live) == len(m)
+    assert m.ct_gc(t) == om.ct_gc(t) == want
+    assert len(m) == len(om) == len(live) - want
+    k1, v1 = m.dump()
+    k2, v2 = om.dump()
+    rows = lambda k, v: sorted(bytes(a) + bytes(b) for a, b in zip(k, v))
+    assert rows(k1, v1) == rows(k2, v2)
+    assert m.ct_gc(t) == 0                        # idempotent
+    assert m.ct_gc(0xFFFFFFFF) == om.ct_gc(0xFFFFFFFF) == len(live) - want   # ctmap.Flush
+    assert len(m) == 0

@@ -572,6 +572,34 @@ __device__ __forceinline__ uint8_t xdp_verdict(const DpParams &p, const RecT<NW>
     return XDP_PASS;
 }
 
+// xdp_verdict with the IPv4 table probes as quad probes (cv_hash.hpp quad_find):
+// every lane of the wave calls it (`live` false past the batch end); other frames
+// take xdp_verdict's per-lane path, which then does no IPv4 probe.
+template <int NW>
+__device__ __forceinline__ uint8_t xdp_verdict_q(const DpParams &p, const RecT<NW> &r, Acct &a, bool live,
+                                                 uint4 *st)
+{
+    const bool v4 = live && r.len >= 34 && rec_raw16c<12>(r) == 0x0008u;
+    uint32_t saddr = rec_raw32c<26>(r), daddr = rec_raw32c<30>(r);
+    bool drop = false;
+    if (p.cidr4_fix.buckets) {                              // CIDR4_FILTER
+        if (p.cidr4_dyn.l1) {                               // CIDR4_LPM_PREFILTER
+            if (v4) a.nl++;
+            drop = lpm4_lookup_q(p.cidr4_dyn, bswap32(saddr), v4, st) != 0;
+        }
+        const bool want = v4 && !drop;
+        if (want) a.nl++;
+        drop = quad_find<Cidr4Spec>(p.cidr4_fix, &saddr, want, st, nullptr) >= 0 || drop;
+    }
+    uint32_t iv = 0;
+    const bool want_lxc = v4 && !drop && p.lxc4.buckets;
+    if (want_lxc) a.nl++;
+    const bool hit = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv) >= 0;
+    if (v4) return (!drop && hit) ? XDP_PASS : XDP_DROP;
+    if (!live) return XDP_PASS;
+    return xdp_verdict(p, r, a);
+}
+
 // ------------------------------------------------------------------ conntrack
 // struct ct_entry (common.h:380-406) held in 16 words: counters w0-7, lifetime w8,
 // bits | rev_nat_index << 16 in w9, slave | tx_flags_seen << 16 | rx_flags_seen << 24

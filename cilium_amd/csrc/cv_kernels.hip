@@ -15,13 +15,31 @@
 namespace cv {
 
 // ================================================================== config 1
+// A wave's record load and probes: wave-cooperative 1-KiB record loads through LDS
+// when the wave's 64 records are all in the batch (64-B stride), quad probes
+// (cv_hash.hpp) for the tables; the loops are wave-uniform so every lane reaches
+// every probe (lanes past the end with live = false).
+__device__ __forceinline__ void rec_load_wave(Rec &r, const DpParams &p, const BatchDev &b, uint32_t i0, uint32_t i,
+                                              bool live, uint4 *st)
+{
+    if (p.recmode == 2 && b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 4, st);
+    else if (!live) { r.len = 0; for (int j = 0; j < 16; ++j) r.w[j] = 0; }
+    else rec_load(r, b, i, 4);
+}
+
 __global__ void __launch_bounds__(BLOCK) k_xdp_prefilter(DpParams p, BatchDev b, OutDev o)
 {
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+    __shared__ uint4 stage[BLOCK / 64][256];
+    uint4 *st = stage[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < b.n; i0 += gridDim.x * BLOCK) {
+        const uint32_t i = i0 + lane;
+        const bool live = i < b.n;
         Rec r;
-        rec_load(r, b, i, 4);
+        rec_load_wave(r, p, b, i0, i, live, st);
         Acct a{0, 0};
-        const uint8_t v = xdp_verdict(p, r, a);
+        const uint8_t v = xdp_verdict_q(p, r, a, live, st);
+        if (!live) continue;
         if (o.xdp) o.xdp[i] = v;
         if (o.reason) o.reason[i] = 0;
         store_out(o, i, a);
@@ -209,73 +227,81 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                                                         int with_prefilter)
 {
     __shared__ LdsMetrics lm;
+    __shared__ uint4 stage[BLOCK / 64][256];
+    uint4 *st = stage[threadIdx.x >> 6];
     Met m;
     met_init(m, lm);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < b.n; i0 += gridDim.x * BLOCK) {
+        const uint32_t i = i0 + lane;
+        const bool live = i < b.n;
         Rec r;
-        rec_load(r, b, i, 4);
+        rec_load_wave(r, p, b, i0, i, live, st);
         Acct a{0, 0};
         uint8_t xv = XDP_PASS;
         int32_t ret = TC_ACT_OK, reason = 0;
         uint32_t ident = 0;
         bool staged = false;
-        if (with_prefilter) xv = xdp_verdict(p, r, a);
-        if (xv == XDP_PASS) {
-            bool skip_proxy = false;
-            uint32_t identity = 0;
-            if (p.flags & F_FROM_HOST) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
+        if (with_prefilter) xv = xdp_verdict_q(p, r, a, live, st);
+        const bool pass = live && xv == XDP_PASS;
+        bool skip_proxy = false;
+        uint32_t identity = 0;
+        if (pass && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
+        ident = identity;
+        const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
+        const bool v4 = pass && eth == 0x0008u && r.len >= 34;   // handle_ipv4 (bpf_netdev.c:357-453)
+        const uint32_t nexthdr = rec_u8c<23>(r);
+        const int l4 = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
+        uint32_t secctx = WORLD_ID;
+        const bool want_ipc = v4 && identity < HEALTH_ID;
+        const uint32_t lab = ipcache4_q(p, rec_raw32c<26>(r), want_ipc, a, st);
+        if (want_ipc && lab && lab != CLUSTER_ID && lab != HOST_ID) identity = lab;
+        int h = TC_ACT_OK;
+        if (v4) {
             ident = identity;
-            const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
-            if (eth == 0x0008u) {
-                int h;                                            // handle_ipv4 (bpf_netdev.c:357-453)
-                if (r.len < 34) {
-                    h = DROP_INVALID;
-                } else {
-                    const int l4 = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
-                    const uint32_t nexthdr = rec_u8c<23>(r);
-                    uint32_t secctx = WORLD_ID;
-                    if (identity < HEALTH_ID) {
-                        const uint32_t lab = ipcache4(p, rec_raw32c<26>(r), a);
-                        if (lab && lab != CLUSTER_ID && lab != HOST_ID) identity = lab;
-                    }
-                    ident = identity;
-                    h = TC_ACT_OK;
-                    if (p.flags & F_FROM_HOST) {
-                        secctx = identity;
-                        if (nexthdr == 6 || nexthdr == 17) {      // reverse_proxy port load
-                            const int c = rec_chk(r, l4, 4);
-                            if (c) h = chk_err(c, DROP_CT_INVALID_HDR);
-                        }
-                    }
-                    uint32_t iv;
-                    if (h == TC_ACT_OK && lxc4_find(p, rec_raw32c<30>(r), iv, a)) {
-                        if (iv & (1u << 16)) {
-                            h = TC_ACT_OK;                        // ENDPOINT_F_HOST
-                        } else if (rec_u8c<22>(r) <= 1) {
-                            h = DROP_INVALID;                     // ipv4_dec_ttl
-                        } else {
-                            const uint32_t e = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
-                            if (!e) {
-                                h = DROP_MISSED_TAIL_CALL;
-                            } else {
-                                staged = true;                    // -> handle_policy -> tail_ipv4_policy
-                                g.secctx[i] = secctx;
-                                g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
-                                const EpDev &ep = p.eps[e - 1];
-                                const uint32_t sa = rec_raw32c<26>(r), da = rec_raw32c<30>(r);
-                                const uint32_t s = group_node(g, pair_hash4(sa, da, (uint64_t)ep.ct_id << 17));
-                                group_push(g, s, i, Q_NETDEV);
-                            }
-                        }
-                    }
-                }
-                if (!staged) {
-                    if (h == E_TRUNC) ret = h;
-                    else if (is_err(h)) { m.drop(h, r.len, METRIC_INGRESS); reason = h; ret = TC_ACT_SHOT; }
-                    else ret = h;
+            if (p.flags & F_FROM_HOST) {
+                secctx = identity;
+                if (nexthdr == 6 || nexthdr == 17) {              // reverse_proxy port load
+                    const int c = rec_chk(r, l4, 4);
+                    if (c) h = chk_err(c, DROP_CT_INVALID_HDR);
                 }
             }
         }
+        const bool want_lxc = v4 && h == TC_ACT_OK && p.lxc4.buckets;
+        if (want_lxc) a.nl++;                                     // lookup_ip4_endpoint
+        uint32_t iv = 0;
+        uint32_t daddr = rec_raw32c<30>(r);
+        const bool lxc_hit = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv) >= 0;
+        if (pass && eth == 0x0008u) {
+            if (r.len < 34) {
+                h = DROP_INVALID;
+            } else if (want_lxc && lxc_hit) {
+                if (iv & (1u << 16)) {
+                    h = TC_ACT_OK;                                // ENDPOINT_F_HOST
+                } else if (rec_u8c<22>(r) <= 1) {
+                    h = DROP_INVALID;                             // ipv4_dec_ttl
+                } else {
+                    const uint32_t e = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
+                    if (!e) {
+                        h = DROP_MISSED_TAIL_CALL;
+                    } else {
+                        staged = true;                            // -> handle_policy -> tail_ipv4_policy
+                        g.secctx[i] = secctx;
+                        g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
+                    }
+                }
+            }
+            if (!staged) {
+                if (h == E_TRUNC) ret = h;
+                else if (is_err(h)) { m.drop(h, r.len, METRIC_INGRESS); reason = h; ret = TC_ACT_SHOT; }
+                else ret = h;
+            }
+        }
+        if (staged) {                                             // group by (CT map, address pair)
+            const EpDev &ep = p.eps[g.meta[i] & 0xFFFFu];
+            group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
+        }
+        if (!live) continue;
         if (!staged) {
             g.gslot[i] = NONE;
             if (o.ret) o.ret[i] = ret;

@@ -53,7 +53,7 @@ __device__ __forceinline__ uint32_t lpm4_lookup_q(const Lpm4 &t, uint32_t addr /
 #ifdef CV_L1_PREFETCH
     const uint32_t l1 = want ? t.l1[addr >> 16] : 0u;             // in flight with the front probe
 #endif
-    if (quad_find<Host32Spec>(t.full, &k, want, st, &v) >= 0) return v;
+    if (t.full.buckets && quad_find<Host32Spec>(t.full, &k, want, st, &v) >= 0) return v;   // (uniform test)
     if (!want) return 0;
 #ifdef CV_L1_PREFETCH
     uint32_t e = l1;

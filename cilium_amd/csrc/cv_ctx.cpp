@@ -665,6 +665,41 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
     return gs;
 }
 
+// diagnostics (CV_GROUP_STATS): per queue, groups per size class and the largest group
+void group_stats(cv_ctx *c, const char *what, hipStream_t stream)
+{
+    std::vector<uint32_t> cur(CURSOR_WORDS);
+    (void)hipStreamSynchronize(stream);
+    (void)hipMemcpy(cur.data(), c->gcursor.p, CURSOR_WORDS * 4, hipMemcpyDeviceToHost);
+    static const char *qn[NQUEUES] = {"netdev", "lb4", "lb6", "ct4", "ct6", "nat"};
+    for (int q = 0; q < NQUEUES; ++q) {
+        uint64_t groups = 0;
+        for (int k = 0; k < QSPLIT; ++k) groups += cur[qctr(q, k)];
+        if (!groups) continue;
+        fprintf(stderr, "[cv groups] %s %s: %llu groups, largest %u; by class:", what, qn[q],
+                (unsigned long long)groups, cur[GMAX_WORD0 + q]);
+        for (int k = 0; k < NCLASS; ++k) fprintf(stderr, " %u", cur[qcls(q, k)]);
+        fprintf(stderr, "\n");
+        if (q != Q_CT4 && q != Q_CT6 && q != Q_NETDEV) continue;
+        // members of the largest run (queue words hold run offsets after k_group_flatten)
+        std::vector<uint32_t> order((size_t)c->gn * 2);
+        (void)hipMemcpy(order.data(), c->gorder.p, order.size() * 4, hipMemcpyDeviceToHost);
+        const uint32_t qr = (uint32_t)(c->gn / QSPLIT + 512);
+        std::vector<uint32_t> qw((size_t)qr * QSPLIT);
+        (void)hipMemcpy(qw.data(), c->gqueue.as<uint32_t>() + (size_t)qbank(q) * QSPLIT * qr, qw.size() * 4,
+                        hipMemcpyDeviceToHost);
+        uint32_t best = 0, boff = 0;
+        for (int k = 0; k < QSPLIT; ++k)
+            for (uint32_t j = 0; j < cur[qctr(q, k)]; ++j) {
+                const uint32_t off = qw[(size_t)k * qr + j];
+                if (off < order.size() && order[off] > best) { best = order[off]; boff = off; }
+            }
+        fprintf(stderr, "[cv groups] %s %s largest run (%u):", what, qn[q], best);
+        for (uint32_t j = 0; j < best && j < 24; ++j) fprintf(stderr, " %u", order[boff + 1 + j]);
+        fprintf(stderr, "\n");
+    }
+}
+
 int ct_io(cv_ctx *c, MapObj *mo, int op, const uint8_t *key, const uint8_t *val, uint8_t *val_out, uint64_t fl)
 {
     const bool v6 = mo->kind == MK_CT6;
@@ -1123,6 +1158,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
             return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
+        if (getenv("CV_GROUP_STATS")) group_stats(c, "netdev", (hipStream_t)stream);
     }
     return 0;
 }
@@ -1154,6 +1190,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
             return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
+        if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream);
     }
     return 0;
 }

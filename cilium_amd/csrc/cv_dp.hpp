@@ -49,7 +49,7 @@ constexpr uint32_t AB_NO_POLICY_ATOMICS = 1, AB_NO_IPCACHE = 2, AB_NO_POLICY = 4
                    AB_NO_RECORD = 16,
                    // egress (config 5) timing ablations
                    AB_EG_NO_DELIVERY = 0x100, AB_EG_NO_POLICY = 0x200, AB_EG_NO_LOOKUPS = 0x400,
-                   AB_EG_NO_CTSTORE = 0x800, AB_EG_ONE_PER_GROUP = 0x1000;
+                   AB_EG_NO_CTSTORE = 0x800, AB_EG_ONE_PER_GROUP = 0x1000, AB_EG_NAT_DEFER_ALL = 0x2000;
 
 struct BatchDev {
     const uint8_t *frames;
@@ -103,6 +103,7 @@ __host__ __device__ constexpr int qbank(int q) { return (q == Q_LB6 || q == Q_CT
 __host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT + k) * 32; }
 __host__ __device__ constexpr int qcls(int q, int c) { return CLS0 + (q * NCLASS + c) * 32; }
 constexpr int RUN_CURSOR = 3;
+constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (k_group_flatten)
 constexpr int EG_WORDS = 16;
 
 // flatten + schedule the groups of queue q (before the stage that runs them)

@@ -32,7 +32,23 @@ enum : uint32_t {
 enum : uint32_t { STAGE_DONE = 0, STAGE_LB = 1, STAGE_CT = 2 };
 constexpr uint64_t SALT_SVC4 = 0x5356433400000000ULL, SALT_SVC6 = 0x5356433600000000ULL,
                    SALT_CT4 = 0x4354340000000000ULL, SALT_CT6 = 0x4354360000000000ULL,
-                   SALT_NAT = 0x4E41540000000000ULL;
+                   SALT_NAT = 0x4E41540000000000ULL, SALT_SELF = 0x53454C4600000000ULL;
+
+// The NATed tuple a non-loopback service create writes is a self-pair key (backend,
+// backend, the flow's ports).  A packet can read it only through a lookup key of the
+// same pair, protocol and (unordered) ports, so readers of self-pair keys register a
+// node keyed by (address, port pair, protocol) and a NAT writer joins a group only
+// through that node (k_egress_nat).  proto = 0x100: "any ports" (a rewritten key).
+__device__ __forceinline__ uint32_t port_sig(const Tuple4 &t)
+{
+    const uint32_t a = t.sport & 0xFFFFu, c = t.dport & 0xFFFFu;
+    return a < c ? (a | c << 16) : (c | a << 16);
+}
+
+__device__ __forceinline__ uint64_t self_hash(uint32_t x, uint32_t sig, uint32_t proto)
+{
+    return mix64(((uint64_t)x << 32 | sig) ^ ((uint64_t)proto << 52) ^ SALT_SELF);
+}
 
 struct EgOut {                  // per-packet results on the way to the outputs
     int32_t ret, reason;
@@ -485,7 +501,7 @@ __device__ __forceinline__ void eg6_state(const Rec6 &r, const uint32_t *eg, Eg6
 __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
-        const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; continue; }
         const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
         Acct na{0, 0};                                            // speculative probes are not accounted
@@ -505,7 +521,21 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             // the entry lookup 1 would hit today: a REPLY with rev-NAT rewrites the packet
             Tuple4 t1 = x.t;
             uint32_t seen;
-            if (ct_l4<false>(t1, x.s.h, CT_EGRESS, seen) >= 0 && ep.ct4.buckets) {
+            const bool l4ok = ct_l4<false>(t1, x.s.h, CT_EGRESS, seen) >= 0;
+            eg[9] = port_sig(t1);                                 // the key signature of this packet's
+            eg[10] = t1.nexthdr;                                  // create (and NAT) tuples
+            if (l4ok && S == x.t.daddr)                           // self-pair egress lookup keys
+                uf_union(g, P, group_node(g, self_hash(S, eg[9], t1.nexthdr)));
+            if (x.s.saddr == x.s.daddr) {                         // self-pair keys of the delivery lookups
+                Tuple4 ti;
+                ti.nexthdr = x.s.nexthdr;
+                ti.daddr = x.s.daddr;
+                ti.saddr = x.s.saddr;
+                ti.dport = ti.sport = 0;
+                if (ct_l4<false>(ti, x.s.h, CT_INGRESS, seen) >= 0)
+                    uf_union(g, P, group_node(g, self_hash(ti.saddr, port_sig(ti), ti.nexthdr)));
+            }
+            if (l4ok && ep.ct4.buckets) {
                 uint32_t k[4];
                 t1.key(k);
                 const int64_t sl = dev_find<Ct4Spec>(ep.ct4, k, nullptr);
@@ -515,7 +545,10 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
                     uint32_t na4, np;
                     if ((e.w[9] >> 16) && revnat4(p, e.w[9] >> 16, na4, np, na)) {
                         const bool lb = e.bits() & CTB_LB_LOOPBACK;
-                        uf_union(g, P, group_node(g, pair_hash4(na4, lb ? x.s.saddr : x.s.daddr, SALT_CT4)));
+                        const uint32_t other = lb ? x.s.saddr : x.s.daddr;
+                        uf_union(g, P, group_node(g, pair_hash4(na4, other, SALT_CT4)));
+                        if (na4 == other)                         // a rewritten self pair: any ports
+                            uf_union(g, P, group_node(g, self_hash(na4, 0, 0x100)));
                     }
                 }
             }
@@ -559,8 +592,14 @@ __global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, Gr
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         if ((eg[0] & (EG_STAGE | EG_V6 | EG_SVC)) != (STAGE_CT | EG_SVC) || !eg[4]) continue;
-        const uint32_t other = (eg[0] & EG_LOOPBACK) ? eg[5] : eg[6];
-        const uint32_t nn = group_find(g, pair_hash4(eg[4], other, SALT_CT4));
+        if (p.ablate & AB_EG_NAT_DEFER_ALL) { eg[0] |= EG_NAT_DEFER; continue; }   // timing only
+        uint32_t nn;
+        if (eg[0] & EG_LOOPBACK) {                                // (client, IPV4_LOOPBACK): by pair
+            nn = group_find(g, pair_hash4(eg[4], eg[5], SALT_CT4));
+        } else {                                                  // (backend, backend, ports, proto)
+            nn = group_find(g, self_hash(eg[4], eg[9], eg[10]));
+            if (nn == NONE) nn = group_find(g, self_hash(eg[4], 0, 0x100));
+        }
         if (nn != NONE) uf_union(g, g.gslot[i], nn);
         else eg[0] |= EG_NAT_DEFER;
     }

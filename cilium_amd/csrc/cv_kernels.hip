@@ -438,6 +438,10 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q)
             *ent = off;
             atomicAdd(&hist[size_class(cnt)], 1u);
         }
+        uint32_t big = cnt;                                       // the largest group (diagnostics)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) big = max(big, (uint32_t)__shfl_xor(big, d, 64));
+        if (lane == 0 && big > 8) atomicMax(&g.cursor[GMAX_WORD0 + q], big);
         __syncthreads();                                          // wsum / bbase reuse
     }
     __syncthreads();

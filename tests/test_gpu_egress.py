@@ -113,3 +113,49 @@ def test_config5_v6_only(dev):
 def test_config5_v4_records_128(dev):
     w = synth.config5(1 << 13, n_svc=500, n_ep=64, n_remote=128, family=4, stride=128, seed=56)
     check_egress(w, dev, batches=1, rounds=1)
+
+
+def nat_reader_workload():
+    """A config-5 batch plus packets that read the NATed tuples service creates write:
+    a non-loopback service create writes the self-pair key (backend, backend, flow
+    ports); a backend sending to its own address with those ports (both port orders)
+    looks it up later in the same batch.  The batch parallelism must order that reader
+    after the writer (k_egress_nat: port-qualified self-pair nodes)."""
+    w = synth.config5(1 << 13, n_svc=200, n_ep=64, n_remote=128, family=4, seed=61, vip_frac=0.9)
+    dp, om = H.oracle_dp(w)
+    dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    keys, _ = om["ct4"].dump()
+    da = np.ascontiguousarray(keys[:, 0:4]).view("<u4").ravel()
+    sa = np.ascontiguousarray(keys[:, 4:8]).view("<u4").ravel()
+    fsa = np.ascontiguousarray(w.frames[:, 26:30]).view("<u4").ravel()
+    v4ok = (w.frames[:, 12] == 8) & (w.frames[:, 13] == 0)
+    readers = []
+    for r in np.nonzero((da == sa) & np.isin(keys[:, 12], (6, 17)))[0]:
+        q = np.nonzero(v4ok & (fsa == da[r]))[0]
+        if not len(q):
+            continue
+        for ports in (keys[r, 8:12], np.concatenate([keys[r, 10:12], keys[r, 8:10]])):
+            f = w.frames[q[0]].copy()
+            f[30:34] = keys[r, 0:4]                               # daddr = the backend itself
+            f[23] = keys[r, 12]
+            f[34:38] = ports
+            readers.append((f, q[0]))
+        if len(readers) >= 64:
+            break
+    assert readers, "no NAT tuples in the batch"
+    idx = np.array([q for _, q in readers])
+    w.frames = np.concatenate([w.frames, np.stack([f for f, _ in readers])])
+    w.length = np.concatenate([w.length, w.length[idx]])
+    for k in ("src_ep", "flow_hash", "v6", "kind", "reply"):
+        if k in w.extra:
+            w.extra[k] = np.concatenate([w.extra[k], w.extra[k][idx]])
+    w.mark = np.concatenate([w.mark, w.mark[idx]])
+    return w, len(readers)
+
+
+def test_config5_nat_tuple_readers(dev):
+    w, nr = nat_reader_workload()
+    dp, _ = H.oracle_dp(w)
+    ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    assert (ref.ct[-nr:] != 0).any(), "no crafted packet reads a NAT tuple"
+    check_egress(w, dev, batches=1, rounds=1)

@@ -24,7 +24,7 @@ def main():
            "identity": torch.empty(n, dtype=torch.int32, device="cuda:0"),
            "ct": torch.empty(n, dtype=torch.uint8, device="cuda:0")}
     variants = {"full": 0, "no_delivery": 0x100, "no_policy": 0x200, "no_lookups": 0x300 | 0x400,
-                "no_ctstore": 0x800, "one_per_group": 0x1000, "skeleton": 0x1f00, "no_pol_atomics": 0x1}
+                "no_ctstore": 0x800, "one_per_group": 0x1000, "skeleton": 0x1f00, "no_pol_atomics": 0x1, "nat_defer_all": 0x2000}
     times = {k: [] for k in variants}
     for _ in range(2):
         ctx.lxc_egress(f, l, out, w.now, src_ep=src, flow_hash=fh)

@@ -157,7 +157,7 @@ struct cv_ctx {
     DevBuf eps_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
-    DevBuf gtable, gslot, gnext, gsecctx, gmeta, gparent, geg, gorder, gcursor, gqueue, gwork;
+    DevBuf gtable, gslot, gnext, gsecctx, gmeta, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -165,6 +165,10 @@ struct cv_ctx {
     DevBuf ctio;
     uint32_t next_ct_id = 1;
     uint32_t chunk = MAX_CHUNK;    // packets per launch (CV_MAX_CHUNK env may lower it, tests)
+    // drop notification ring (cv_notify_attach), device pointers
+    cv_drop_notify *notify = nullptr;
+    uint32_t notify_cap = 0;
+    uint32_t *notify_count = nullptr;
 };
 
 namespace {
@@ -190,6 +194,7 @@ inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v;
 int compile_lxc(cv_ctx *c, HostMap *m)
 {
     std::vector<std::vector<uint32_t>> k4, v4, k6, v6;
+    std::vector<uint8_t> if4, if6;                         // endpoint_info.ifindex per entry (side values)
     if (m) {
         if (m->ks != 20 || m->vs < 12) return -EINVAL;
         m->for_each([&](const uint8_t *k, const uint8_t *v) {
@@ -199,14 +204,17 @@ int compile_lxc(cv_ctx *c, HostMap *m)
                 for (int i = 4; i < 16; ++i) if (k[i]) return;
                 k4.push_back({rd32(k)});
                 v4.push_back({iv});
+                if4.insert(if4.end(), v, v + 4);
             } else if (k[16] == 2) {
                 k6.push_back({rd32(k), rd32(k + 4), rd32(k + 8), rd32(k + 12)});
                 v6.push_back({iv});
+                if6.insert(if6.end(), v, v + 4);
             }
         });
     }
-    int r = build_hash<LxcV4Spec>(c->lxc4, k4, v4, 0, nullptr, nullptr);
-    if (!r) r = build_hash<LxcV6Spec>(c->lxc6, k6, v6, 0, nullptr, nullptr);
+    std::vector<int64_t> s4, s6;
+    int r = build_hash<LxcV4Spec>(c->lxc4, k4, v4, 4, &if4, &s4);
+    if (!r) r = build_hash<LxcV6Spec>(c->lxc6, k6, v6, 4, &if6, &s6);
     if (!m) { c->lxc4.view = HashTable{}; c->lxc6.view = HashTable{}; }
     return r;
 }
@@ -533,6 +541,7 @@ int sync_locked(cv_ctx *c)
             if (t) { d.ct4 = t->ct.view; d.ct_id = t->ct_id; }
             if (t6) d.ct6 = t6->ct.view;
             d.seclabel = e.seclabel;
+            d.lxc_id = e.lxc_id;
             d.ipv4 = e.ipv4;
             for (int j = 0; j < 4; ++j) d.ipv6[j] = e.ipv6[j];
             for (int j = 0; j < 2; ++j) { d.mac[j] = e.mac[j]; d.node_mac[j] = e.node_mac[j]; }
@@ -576,6 +585,9 @@ DpParams params(cv_ctx *c)
     p.recmode = rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u;
     const char *ab = getenv("CV_ABLATE");
     p.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
+    p.notify = reinterpret_cast<uint32_t *>(c->notify);
+    p.notify_cap = c->notify_cap;
+    p.notify_count = c->notify_count;
     return p;
 }
 
@@ -587,12 +599,13 @@ int check_batch(const cv_batch *b)
     return 0;
 }
 
-BatchDev to_dev(const cv_batch *b) { return BatchDev{b->frames, b->stride, b->n, b->len, b->mark}; }
+BatchDev to_dev(const cv_batch *b) { return BatchDev{b->frames, b->stride, b->n, b->len, b->mark, 0, nullptr}; }
 
 // packets [off, off + n) of a batch / its outputs
 BatchDev chunk(const cv_batch *b, uint32_t off, uint32_t n)
 {
-    return BatchDev{b->frames + (size_t)off * b->stride, b->stride, n, b->len + off, b->mark ? b->mark + off : nullptr};
+    return BatchDev{b->frames + (size_t)off * b->stride, b->stride, n, b->len + off, b->mark ? b->mark + off : nullptr,
+                    off, nullptr};
 }
 
 OutDev to_dev(const cv_out *o)
@@ -631,7 +644,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     (void)hipDeviceSynchronize();
     if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsecctx.alloc((size_t)cmax * 4) || c->gmeta.alloc((size_t)cmax * 4) ||
-        c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) ||
+        c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) || c->gifx.alloc((size_t)cmax * 4) ||
         c->gcursor.alloc(CURSOR_WORDS * 4) ||
         c->gqueue.alloc(((size_t)cmax / QSPLIT + 512) * QSPLIT * QBANKS * 4))
         return -ENOMEM;
@@ -659,7 +672,7 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsecctx.as<uint32_t>(),
                     c->gmeta.as<uint32_t>(), c->gparent.as<unsigned long long>(), c->geg.as<uint32_t>(),
                     ++c->serial, c->gorder.as<uint32_t>(), c->gcursor.as<uint32_t>(), c->gqueue.as<uint32_t>(),
-                    (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>()};
+                    (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>()};
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1184,7 +1197,9 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
         const uint32_t n = std::min(c->chunk, b->n - off);
         GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
-        if ((r = launch_lxc_egress(p, chunk(b, off, n), src_ep ? src_ep + off : nullptr, ep0,
+        BatchDev bc = chunk(b, off, n);
+        bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
+        if ((r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0,
                                    flow_hash ? flow_hash + off : nullptr, now, chunk(o, off), gs,
                                    (hipStream_t)stream)))
             return r;
@@ -1213,6 +1228,18 @@ int cv_metrics_reset(cv_ctx *c)
 }
 
 uint64_t *cv_metrics_device_ptr(cv_ctx *c) { return c ? reinterpret_cast<uint64_t *>(c->metrics) : nullptr; }
+
+// the cilium_events drop stream (DROP_NOTIFY) into caller-owned device buffers
+int cv_notify_attach(cv_ctx *c, cv_drop_notify *records, uint32_t capacity, uint32_t *count)
+{
+    if (!c || (records && !count)) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->device >= 0) (void)hipDeviceSynchronize();
+    c->notify = records;
+    c->notify_cap = records ? capacity : 0;
+    c->notify_count = records ? count : nullptr;
+    return 0;
+}
 
 int cv_metrics_attach(cv_ctx *c, uint64_t *buf)
 {

@@ -239,6 +239,9 @@ struct Met {
     LdsMetrics *lm;
     Fwd f;
     LdsPolicy *pc;             // optional policy counter cache (conntrack stages)
+    // the packet being processed, for drop notifications: batch index, skb hash, and
+    // the sending endpoint program (egress: LXC_ID, SECLABEL)
+    uint32_t pkt, hash, src_id, src_label;
     __device__ void drop(int32_t code, uint32_t len, int dir)          // send_drop_notify
     {
         const uint32_t r = (uint8_t)(-code);
@@ -258,6 +261,7 @@ __device__ __forceinline__ void met_init(Met &m, LdsMetrics &lm)
     for (int i = threadIdx.x; i < 256 * 4; i += blockDim.x) lm.c[i] = 0;
     m.lm = &lm;
     m.pc = nullptr;
+    m.pkt = m.hash = m.src_id = m.src_label = 0;
     m.f.c[0] = m.f.c[1] = 0;
     m.f.b[0] = m.f.b[1] = 0;
     __syncthreads();
@@ -292,6 +296,47 @@ __device__ __forceinline__ void met_flush(Met &m, unsigned long long *g)
     }
 }
 
+// wave-aggregated append: one atomic per (wave, counter); lanes may target different
+// counters; returns the lane's index or NONE
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred)
+{
+    const int lane = (int)__lane_id();
+    uint32_t res = NONE;
+    unsigned long long todo = __ballot(pred);
+    while (todo) {                                                // one round per distinct counter
+        const int leader = __ffsll((long long)todo) - 1;
+        const uintptr_t mine_p = reinterpret_cast<uintptr_t>(ctr);
+        const uint32_t lo = __shfl((uint32_t)mine_p, leader, 64), hi = __shfl((uint32_t)(mine_p >> 32), leader, 64);
+        uint32_t *lc = reinterpret_cast<uint32_t *>((uintptr_t)lo | ((uintptr_t)hi << 32));
+        const bool mine = pred && ctr == lc;
+        const unsigned long long m = __ballot(mine);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(lc, (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (mine) res = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        todo &= ~m;
+    }
+    return res;
+}
+
+// send_drop_notify -> __send_drop_notify (bpf/lib/drop.h:50-108): one cv_drop_notify
+// record (10 words) per drop when a ring is attached; wave-aggregated slot claims
+__device__ __forceinline__ void notify_drop(const DpParams &p, const Met &m, int32_t code, uint32_t len,
+                                            uint32_t source, uint32_t src, uint32_t dst, uint32_t dst_id,
+                                            uint32_t ifindex)
+{
+    if (!p.notify) return;
+    const uint32_t at = wave_append(p.notify_count, true);
+    if (at >= p.notify_cap) return;                               // lost sample (ring full)
+    const uint32_t srcdst = (src << 16) | (dst & 0xFFFFu);       // skb->cb[1]
+    uint32_t *w = p.notify + (size_t)at * 10;
+    const uint32_t sub = (uint32_t)(uint8_t)(code < 0 ? -code : code);
+    *reinterpret_cast<uint4 *>(w) = make_uint4(1u | sub << 8 | (source & 0xFFFFu) << 16, m.hash, len,
+                                               len < 128 ? len : 128u);
+    *reinterpret_cast<uint4 *>(w + 4) = make_uint4(srcdst >> 16, srcdst & 0xFFFFu, dst_id, ifindex);
+    *reinterpret_cast<uint2 *>(w + 8) = make_uint2(m.pkt, 0u);
+}
+
 // ------------------------------------------------------------------ lookups
 struct Acct {
     uint32_t nl, nu;
@@ -312,6 +357,14 @@ __device__ __forceinline__ bool lxc6_find(const DpParams &p, const uint32_t *dad
     if (!p.lxc6.buckets) return false;
     a.nl++;
     return dev_find<LxcV6Spec>(p.lxc6, daddr, &ival) >= 0;
+}
+
+// endpoint_info.ifindex of the matched cilium_lxc entry (the 4-B side value of its
+// slot); without the side array, the inline nonzero bit
+__device__ __forceinline__ uint32_t lxc_ifindex(const HashTable &t, int64_t slot, uint32_t ival)
+{
+    if (t.vals && slot >= 0) return *reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * 4);
+    return (ival >> 17) & 1u;
 }
 
 // ipcache_lookup4 (eps.h:309-319) -> remote_endpoint_info.sec_label (0 = none)
@@ -1021,7 +1074,7 @@ __device__ __forceinline__ Skb4 skb4_from(const Rec &r)
 // ipv4_policy (bpf_lxc.c:865-979) + tail_ipv4_policy (:981-993), LXC_NAT46 off.
 // Returns the final verdict (TC_ACT_*, drops accounted as METRIC_INGRESS) or E_TRUNC.
 __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
-                                           bool skip_proxy, bool ifindex_nz, uint32_t now, uint8_t &ct_out,
+                                           bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                            uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
 {
     int ret;
@@ -1062,10 +1115,11 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
         return TC_ACT_REDIRECT;                                    // redirect(HOST_IFINDEX)
     }
     m.fwd(s.len, METRIC_INGRESS);                                  // send_trace_notify(TRACE_TO_LXC)
-    return ifindex_nz ? TC_ACT_REDIRECT : TC_ACT_OK;
+    return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
 drop:
     if (ret == E_TRUNC) return ret;
-    m.drop(ret, s.len, METRIC_INGRESS);
+    m.drop(ret, s.len, METRIC_INGRESS);                            // tail_ipv{4,6}_policy: send_drop_notify
+    notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
     reason = ret;
     return TC_ACT_SHOT;
 }
@@ -1077,7 +1131,7 @@ __device__ __forceinline__ bool eq4(const uint32_t *a, const uint32_t *b)
 
 // ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862)
 __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
-                                           bool skip_proxy, bool ifindex_nz, uint32_t now, uint8_t &ct_out,
+                                           bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                            uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
 {
     int ret;
@@ -1119,10 +1173,11 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
         return TC_ACT_REDIRECT;
     }
     m.fwd(s.len, METRIC_INGRESS);
-    return ifindex_nz ? TC_ACT_REDIRECT : TC_ACT_OK;
+    return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
 drop:
     if (ret == E_TRUNC) return ret;
-    m.drop(ret, s.len, METRIC_INGRESS);
+    m.drop(ret, s.len, METRIC_INGRESS);                            // tail_ipv{4,6}_policy: send_drop_notify
+    notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
     reason = ret;
     return TC_ACT_SHOT;
 }
@@ -1130,27 +1185,29 @@ drop:
 // handle_policy (bpf_lxc.c:1003-1038) for an IPv4 / IPv6 packet: DROP_ALL drops
 // before any conntrack work; IPv4 needs the endpoint's LXC_IPV4 program.
 __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
-                                              bool skip_proxy, bool ifindex_nz, uint32_t now, uint8_t &ct_out,
+                                              bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                               uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
 {
     int ret;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ipv4) return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex_nz, now, ct_out, proxy, reason, a, m);
+    else if (ep.ipv4) return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m);
     else ret = DROP_UNKNOWN_L3;
-    m.drop(ret, s.len, METRIC_INGRESS);
+    m.drop(ret, s.len, METRIC_INGRESS);                            // bpf_lxc.c:1032-1035
+    notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
     reason = ret;
     return TC_ACT_SHOT;
 }
 
 __device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
-                                              bool ifindex_nz, uint32_t now, uint8_t &ct_out, uint16_t &proxy,
+                                              uint32_t ifindex, uint32_t now, uint8_t &ct_out, uint16_t &proxy,
                                               int32_t &reason, Acct &a, Met &m)
 {
     int ret;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, false, ifindex_nz, now, ct_out, proxy, reason, a, m);
+    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, false, ifindex, now, ct_out, proxy, reason, a, m);
     else ret = DROP_MISSED_TAIL_CALL;
     m.drop(ret, s.len, METRIC_INGRESS);
+    notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
     reason = ret;
     return TC_ACT_SHOT;
 }
@@ -1195,29 +1252,6 @@ __device__ __forceinline__ uint32_t group_find(const GroupScratch &g, uint64_t g
         s = (s + 1) & g.cap_mask;
     }
     return NONE;
-}
-
-// wave-aggregated append: one atomic per (wave, counter); lanes may target different
-// counters; returns the lane's index or NONE
-__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred)
-{
-    const int lane = (int)__lane_id();
-    uint32_t res = NONE;
-    unsigned long long todo = __ballot(pred);
-    while (todo) {                                                // one round per distinct counter
-        const int leader = __ffsll((long long)todo) - 1;
-        const uintptr_t mine_p = reinterpret_cast<uintptr_t>(ctr);
-        const uint32_t lo = __shfl((uint32_t)mine_p, leader, 64), hi = __shfl((uint32_t)(mine_p >> 32), leader, 64);
-        uint32_t *lc = reinterpret_cast<uint32_t *>((uintptr_t)lo | ((uintptr_t)hi << 32));
-        const bool mine = pred && ctr == lc;
-        const unsigned long long m = __ballot(mine);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(lc, (uint32_t)__popcll(m));
-        base = __shfl(base, leader, 64);
-        if (mine) res = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-        todo &= ~m;
-    }
-    return res;
 }
 
 // push packet i on the list of node s; the group's first member (the list tail)

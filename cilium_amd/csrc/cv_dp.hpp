@@ -17,6 +17,7 @@ struct EpDev {                 // one endpoint program (bpf_lxc.c), its maps and
     HashTable ct4;             // Ct4Spec + 64-B side values (struct ct_entry)
     HashTable ct6;             // Ct6Spec + 64-B side values
     uint32_t seclabel;
+    uint32_t lxc_id;           // LXC_ID (EVENT_SOURCE of the program)
     uint32_t ct_id;            // identifies the CT map (group key component)
     uint32_t ipv4;             // LXC_IPV4 (raw network-order word); 0 = no IPv4 programs
     uint32_t ipv6[4];          // LXC_IP
@@ -42,6 +43,10 @@ struct DpParams {              // by value as the kernel argument
     // node_config.h constants (raw network-order words)
     uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
     uint32_t router6[4];
+    // drop notifications (cv_notify_attach): cv_drop_notify records of 10 words
+    uint32_t *notify;
+    uint32_t notify_cap;
+    uint32_t *notify_count;
 };
 
 // ablation bits: each removes one part of the work to price it (results are wrong)
@@ -56,6 +61,8 @@ struct BatchDev {
     uint32_t stride, n;
     const uint32_t *len;
     const uint32_t *mark;
+    uint32_t base;             // index of packet 0 in the caller's batch (launch chunks)
+    const uint32_t *hash;      // per-packet skb hash (cv_lxc_egress flow_hash) or null
 };
 
 struct OutDev {
@@ -86,6 +93,7 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *queue;           // dense lists of group slots (one lane per group), QSPLIT regions
     uint32_t qregion;          // words per region
     uint32_t *work;            // per group: `order` offset of its run, in size-class order
+    uint32_t *ifx;             // per packet: the destination endpoint's ifindex (netdev path)
 };
 // GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
 // contention on one counter); blocks b with b % QSPLIT == k hold at most

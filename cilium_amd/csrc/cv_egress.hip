@@ -69,10 +69,11 @@ __device__ __forceinline__ void eg_final(const OutDev &o, uint32_t i, const EgOu
 }
 
 // tail_handle_ipv{4,6} / handle_ingress: IS_ERR -> send_drop_notify(METRIC_EGRESS)
-__device__ __forceinline__ void eg_drop(EgOut &r, int32_t code, uint32_t len, Met &m)
+__device__ __forceinline__ void eg_drop(const DpParams &p, EgOut &r, int32_t code, uint32_t len, Met &m)
 {
     if (code == E_TRUNC || code == E_PUNT) { r.ret = code; return; }
     m.drop(code, len, METRIC_EGRESS);
+    notify_drop(p, m, code, len, m.src_id, m.src_label, 0, 0, 0);   // send_drop_notify(SECLABEL, 0, 0, 0)
     r.reason = code;
     r.ret = TC_ACT_SHOT;
 }
@@ -93,24 +94,24 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
     int ret;
     if (p.flags & F_DROP_ALL) {
         if (eth == 0x0608u) { res.ret = E_PUNT; return STAGE_DONE; }   // ARP responder tail call
-        eg_drop(res, DROP_POLICY, r.len, m);
+        eg_drop(p, res, DROP_POLICY, r.len, m);
         return STAGE_DONE;
     }
     if (eth == 0x0008u) {
-        if (!ep.ipv4) { eg_drop(res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
+        if (!ep.ipv4) { eg_drop(p, res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
         // handle_ipv4_from_lxc (bpf_lxc.c:402-446)
-        if (r.len < 34) { eg_drop(res, DROP_INVALID, r.len, m); return STAGE_DONE; }
+        if (r.len < 34) { eg_drop(p, res, DROP_INVALID, r.len, m); return STAGE_DONE; }
         if (!mac_eq(rec_raw32c<6>(r), rec_raw16c<10>(r), ep.mac)) ret = DROP_INVALID_SMAC;
         else if (!mac_eq(rec_raw32c<0>(r), rec_raw16c<4>(r), ep.node_mac)) ret = DROP_INVALID_DMAC;
         else if (rec_raw32c<26>(r) != ep.ipv4) ret = DROP_INVALID_SIP;
         else ret = 0;
-        if (ret) { eg_drop(res, ret, r.len, m); return STAGE_DONE; }
+        if (ret) { eg_drop(p, res, ret, r.len, m); return STAGE_DONE; }
         const uint32_t nexthdr = rec_u8c<23>(r);
         const int off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
         const L4Hdr h = l4_read<34>(r, off);
         uint32_t dport = 0;
         if (nexthdr == 6 || nexthdr == 17) {                      // lb4_extract_key / extract_l4_port
-            if (h.c2b) { eg_drop(res, chk_err(h.c2b, E_FAULT), r.len, m); return STAGE_DONE; }
+            if (h.c2b) { eg_drop(p, res, chk_err(h.c2b, E_FAULT), r.len, m); return STAGE_DONE; }
             dport = h.p2;
         } else if (nexthdr != 1) {
             return STAGE_CT;                                      // DROP_UNKNOWN_L4: skip_service_lookup
@@ -141,12 +142,12 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
             res.ret = E_TRUNC;                                    // IPv6 needs 128-B records
             return STAGE_DONE;
         } else {
-            if (!ep.ct6.buckets) { eg_drop(res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
+            if (!ep.ct6.buckets) { eg_drop(p, res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
             // handle_ipv6 (bpf_lxc.c:354-380) + ipv6_l3_from_lxc (:82-125)
-            if (r.len < 54) { eg_drop(res, DROP_INVALID, r.len, m); return STAGE_DONE; }
+            if (r.len < 54) { eg_drop(p, res, DROP_INVALID, r.len, m); return STAGE_DONE; }
             eg[0] |= EG_V6;
             if (rec_u8c<20>(r) == 58) {                          // icmp6_handle (icmp6.h:390-412)
-                if (r.len < 62) { eg_drop(res, DROP_INVALID, r.len, m); return STAGE_DONE; }
+                if (r.len < 62) { eg_drop(p, res, DROP_INVALID, r.len, m); return STAGE_DONE; }
                 const uint32_t type = rec_u8c<54>(r);
                 const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
                 if (type == 135 || (type == 128 && eq4(da, p.router6))) { res.ret = E_PUNT; return STAGE_DONE; }
@@ -156,15 +157,15 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
             else if (!mac_eq(rec_raw32c<0>(r), rec_raw16c<4>(r), ep.node_mac)) ret = DROP_INVALID_DMAC;
             else if (!eq4(sa, ep.ipv6)) ret = DROP_INVALID_SIP;
             else ret = 0;
-            if (ret) { eg_drop(res, ret, r.len, m); return STAGE_DONE; }
+            if (ret) { eg_drop(p, res, ret, r.len, m); return STAGE_DONE; }
             uint32_t nexthdr;
             const int hl = ipv6_hdrlen(r, nexthdr);
-            if (hl < 0) { eg_drop(res, hl, r.len, m); return STAGE_DONE; }
+            if (hl < 0) { eg_drop(p, res, hl, r.len, m); return STAGE_DONE; }
             const int off = 14 + hl;
             const L4Hdr h = l4_read<54>(r, off);
             uint32_t dport = 0;
             if (nexthdr == 6 || nexthdr == 17) {
-                if (h.c2b) { eg_drop(res, chk_err(h.c2b, E_FAULT), r.len, m); return STAGE_DONE; }
+                if (h.c2b) { eg_drop(p, res, chk_err(h.c2b, E_FAULT), r.len, m); return STAGE_DONE; }
                 dport = h.p2;
             } else if (nexthdr != 58 && nexthdr != 1) {
                 return STAGE_CT;
@@ -190,7 +191,7 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
         }
     }
     if (eth == 0x0608u) { res.ret = E_PUNT; return STAGE_DONE; }
-    eg_drop(res, DROP_UNKNOWN_L3, r.len, m);
+    eg_drop(p, res, DROP_UNKNOWN_L3, r.len, m);
     return STAGE_DONE;
 }
 
@@ -208,12 +209,16 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         const uint32_t e = src_ep ? src_ep[i] : ep0;
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+        m.src_id = e < p.n_eps ? p.eps[e].lxc_id : 0u;
+        m.src_label = e < p.n_eps ? p.eps[e].seclabel : 0u;
         eg[1] = e & 0xFFFFu;
         eg[2] = 0;
         eg[0] = 0;
         uint32_t stage;
         if (e >= p.n_eps) {
-            eg_drop(res, DROP_MISSED_TAIL_CALL, r.len, m);        // no program for the source
+            res.ret = DROP_MISSED_TAIL_CALL;                      // no program for the source: nothing ran
             stage = STAGE_DONE;
         } else {
             stage = front_one(p, p.eps[e], r, eg, res, a, m);
@@ -255,6 +260,10 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     rec_load(r, b, i, 4);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    m.src_id = ep.lxc_id;
+    m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
@@ -338,7 +347,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     }
 fin:
     eg[0] = STAGE_DONE;
-    eg_drop(res, ret, r.len, m);
+    eg_drop(p, res, ret, r.len, m);
     eg_final(o, i, res, a);
 }
 
@@ -350,6 +359,10 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     rec_load(r, b, i, 8);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    m.src_id = ep.lxc_id;
+    m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
@@ -421,7 +434,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     }
 fin:
     eg[0] = STAGE_DONE;
-    eg_drop(res, ret, r.len, m);
+    eg_drop(p, res, ret, r.len, m);
     eg_final(o, i, res, a);
 }
 
@@ -623,6 +636,10 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     rec_load(r, b, i, 4);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    m.src_id = ep.lxc_id;
+    m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Eg4 x;
@@ -644,6 +661,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
+    int64_t lxc_slot = -1;
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     if (lookups) {                                                // destination category (:482-494)
@@ -682,8 +700,9 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     if (lookups && p.lxc4.buckets) {
         a.nl++;                                                   // lookup_ip4_endpoint(ip4)
-        lxc_hit = s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv) >= 0
-                                     : dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv) >= 0;
+        lxc_slot = s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv)
+                                      : dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv);
+        lxc_hit = lxc_slot >= 0;
     }
     if (lxc_hit) {
         if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
@@ -693,8 +712,8 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
         if (p.ablate & AB_EG_NO_DELIVERY) { res.ret = TC_ACT_OK; eg_final(o, i, res, a); return; }
-        res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, (iv >> 17) & 1u, now, ct2, res.proxy,
-                                 res.reason, a, m);
+        res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, lxc_ifindex(p.lxc4, lxc_slot, iv), now,
+                                 ct2, res.proxy, res.reason, a, m);
         eg_final(o, i, res, a);
         return;
     }
@@ -704,7 +723,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     eg_final(o, i, res, a);
     return;
 drop:
-    eg_drop(res, ret, s.len, m);
+    eg_drop(p, res, ret, s.len, m);
     eg_final(o, i, res, a);
 }
 
@@ -716,6 +735,10 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     rec_load(r, b, i, 8);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    m.src_id = ep.lxc_id;
+    m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Eg6 x;
@@ -731,6 +754,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
+    int64_t lxc_slot = -1;
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     {
@@ -766,7 +790,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     if (p.lxc6.buckets) {                                         // lookup_ip6_endpoint (the daddr is unchanged)
         a.nl++;
-        lxc_hit = probe_end<LxcV6Spec>(lxq, p.lxc6, s.daddr, &iv) >= 0;
+        lxc_slot = probe_end<LxcV6Spec>(lxq, p.lxc6, s.daddr, &iv);
+        lxc_hit = lxc_slot >= 0;
     }
     if (lxc_hit) {
         if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
@@ -775,8 +800,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, (iv >> 17) & 1u, now, ct2, res.proxy, res.reason,
-                                 a, m);
+        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, lxc_ifindex(p.lxc6, lxc_slot, iv), now, ct2,
+                                 res.proxy, res.reason, a, m);
         eg_final(o, i, res, a);
         return;
     }
@@ -786,7 +811,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     eg_final(o, i, res, a);
     return;
 drop:
-    eg_drop(res, ret, s.len, m);
+    eg_drop(p, res, ret, s.len, m);
     eg_final(o, i, res, a);
 }
 

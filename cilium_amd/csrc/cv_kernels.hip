@@ -271,7 +271,8 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         if (want_lxc) a.nl++;                                     // lookup_ip4_endpoint
         uint32_t iv = 0;
         uint32_t daddr = rec_raw32c<30>(r);
-        const bool lxc_hit = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv) >= 0;
+        const int64_t lxc_slot = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv);
+        const bool lxc_hit = lxc_slot >= 0;
         if (pass && eth == 0x0008u) {
             if (r.len < 34) {
                 h = DROP_INVALID;
@@ -288,12 +289,20 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                         staged = true;                            // -> handle_policy -> tail_ipv4_policy
                         g.secctx[i] = secctx;
                         g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
+                        g.ifx[i] = lxc_ifindex(p.lxc4, lxc_slot, iv);   // cb[CB_IFINDEX] = ep->ifindex
                     }
                 }
             }
             if (!staged) {
                 if (h == E_TRUNC) ret = h;
-                else if (is_err(h)) { m.drop(h, r.len, METRIC_INGRESS); reason = h; ret = TC_ACT_SHOT; }
+                else if (is_err(h)) {                             // tail_handle_ipv4: send_drop_notify_error
+                    m.drop(h, r.len, METRIC_INGRESS);
+                    m.pkt = b.base + i;
+                    m.hash = b.hash ? b.hash[i] : 0u;
+                    notify_drop(p, m, h, r.len, 0, 0, 0, 0, 0);
+                    reason = h;
+                    ret = TC_ACT_SHOT;
+                }
                 else ret = h;
             }
         }
@@ -331,8 +340,9 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     uint16_t proxy = 0;
     int32_t reason = 0;
     Skb4 s = skb4_from(r);
-    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u, (meta >> 17) & 1u, now, ct, proxy,
-                                   reason, a, m);
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u, g.ifx[i], now, ct, proxy, reason, a, m);
     if (o.ret) o.ret[i] = ret;
     if (o.reason) o.reason[i] = reason;
     if (o.ct) o.ct[i] = ct;

@@ -106,6 +106,7 @@ def load():
         "cv_metrics_reset": (i32, [vp]),
         "cv_metrics_device_ptr": (vp, [vp]),
         "cv_metrics_attach": (i32, [vp, vp]),
+        "cv_notify_attach": (i32, [vp, vp, u32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -127,6 +128,13 @@ def _ptr(t):
 def _stream():
     import torch
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+# struct cv_drop_notify (include/cilium_hip.h): bpf/lib/drop.h's struct drop_notify + packet index
+DROP_NOTIFY = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"), ("hash", "<u4"),
+                        ("len_orig", "<u4"), ("len_cap", "<u4"), ("src_label", "<u4"), ("dst_label", "<u4"),
+                        ("dst_id", "<u4"), ("ifindex", "<u4"), ("packet", "<u4"), ("reserved", "<u4")])
+assert DROP_NOTIFY.itemsize == 40
 
 
 class Map:
@@ -281,3 +289,31 @@ class Ctx:
     def metrics_attach(self, tensor):
         _check(load().cv_metrics_attach(self.h, None if tensor is None else C.c_void_p(tensor.data_ptr())),
                "cv_metrics_attach")
+
+    def notify_attach(self, capacity):
+        """Attach a device ring for drop notifications (cv_notify_attach); capacity 0
+        detaches.  Returns self; read with notify_drain()."""
+        import torch
+        if not capacity:
+            _check(load().cv_notify_attach(self.h, None, 0, None), "cv_notify_attach")
+            self._notify = None
+            return self
+        dev = f"cuda:{self.device}"
+        rec = torch.zeros(capacity * DROP_NOTIFY.itemsize, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._notify = (rec, cnt, capacity)
+        _check(load().cv_notify_attach(self.h, C.c_void_p(rec.data_ptr()), capacity, C.c_void_p(cnt.data_ptr())),
+               "cv_notify_attach")
+        return self
+
+    def notify_drain(self):
+        """(records, count): the records written since the last drain (structured
+        array, DROP_NOTIFY) and the number of drops (> len(records) if the ring
+        overflowed); resets the ring."""
+        import torch
+        rec, cnt, cap = self._notify
+        torch.cuda.synchronize(rec.device)
+        n = int(cnt.item())
+        out = rec[: min(n, cap) * DROP_NOTIFY.itemsize].cpu().numpy().view(DROP_NOTIFY).copy()
+        cnt.zero_()
+        return out, n

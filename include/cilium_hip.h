@@ -194,6 +194,28 @@ int cv_metrics_reset(cv_ctx *ctx);
 uint64_t *cv_metrics_device_ptr(cv_ctx *ctx);
 int cv_metrics_attach(cv_ctx *ctx, uint64_t *device_buf /* 2048 u64, or NULL = own */);
 
+/* ---- drop notifications: send_drop_notify / __send_drop_notify (bpf/lib/drop.h:40-108)
+ * A drop on the conntrack paths (cv_netdev_ingress, cv_lxc_egress) appends one record:
+ * the 32-byte struct drop_notify the reference emits on cilium_events, followed by the
+ * packet's index in the batch (the perf sample's payload is the first len_cap bytes of
+ * that packet, which the caller holds).  `hash` is the batch's flow_hash where the
+ * entry point takes one (the skb hash, get_hash_recalc), else 0.  Records are appended
+ * in no particular order; *count counts every drop, also those past `capacity` (lost
+ * samples, as with a full perf ring).  The caller zeroes *count when it drains. */
+typedef struct cv_drop_notify {
+    uint8_t  type;        /* CILIUM_NOTIFY_DROP = 1 */
+    uint8_t  subtype;     /* -DROP_* */
+    uint16_t source;      /* EVENT_SOURCE: LXC_ID of the endpoint program, 0 for bpf_netdev */
+    uint32_t hash;
+    uint32_t len_orig, len_cap;   /* skb->len, min(TRACE_PAYLOAD_LEN = 128, len) */
+    uint32_t src_label, dst_label;   /* 16-bit fields of cb[1] = src << 16 | dst */
+    uint32_t dst_id, ifindex;
+    uint32_t packet;      /* index in the batch */
+    uint32_t reserved;
+} cv_drop_notify;
+/* device buffers; records NULL detaches (drops are then only counted in cilium_metrics) */
+int cv_notify_attach(cv_ctx *ctx, cv_drop_notify *records, uint32_t capacity, uint32_t *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -372,6 +372,41 @@ int or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *po
 
 void or_dp_metrics(const or_dp *dp, uint64_t *out) { memcpy(out, dp->metrics, sizeof(dp->metrics)); }
 
+void or_dp_notify_attach(or_dp *dp, or_drop_notify *buf, uint32_t cap)
+{
+    dp->notify = buf;
+    dp->notify_cap = buf ? cap : 0;
+    dp->notify_n = 0;
+}
+
+uint32_t or_dp_notify_count(const or_dp *dp) { return dp->notify_n; }
+
+/* send_drop_notify (bpf/lib/drop.h:94-108) -> __send_drop_notify (:50-79): the
+ * cilium_events record of a drop; cb[1] = src << 16 | (dst & 0xFFFF) is split back into
+ * 16-bit labels; subtype = -reason; source = EVENT_SOURCE of the program (LXC_ID in
+ * bpf_lxc, 0 in bpf_netdev); the update_metrics half is the caller's. */
+static void notify_drop(or_dp *dp, int reason, uint32_t len, uint16_t source, uint32_t src, uint32_t dst,
+                        uint32_t dst_id, uint32_t ifindex)
+{
+    if (!dp->notify) return;
+    const uint32_t at = dp->notify_n++;
+    if (at >= dp->notify_cap) return;
+    or_drop_notify *m = &dp->notify[at];
+    const uint32_t srcdst = (src << 16) | (dst & 0xFFFFu);
+    m->type = 1;                                   /* CILIUM_NOTIFY_DROP */
+    m->subtype = (uint8_t)(reason < 0 ? -reason : reason);
+    m->source = source;
+    m->hash = dp->cur_hash;
+    m->len_orig = len;
+    m->len_cap = len < 128 ? len : 128;            /* TRACE_PAYLOAD_LEN */
+    m->src_label = srcdst >> 16;
+    m->dst_label = srcdst & 0xFFFFu;
+    m->dst_id = dst_id;
+    m->ifindex = ifindex;
+    m->packet = dp->cur_pkt;
+    m->reserved = 0;
+}
+
 /* update_metrics (bpf/lib/metrics.h:43-58) summed over CPUs; dir 1 ingress, 2 egress */
 static void update_metrics(or_dp *dp, uint32_t bytes, uint8_t dir, uint8_t reason)
 {
@@ -857,6 +892,7 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
 drop:
     if (ret == OR_E_TRUNC) return ret;
     update_metrics(dp, len, 1, (uint8_t)(-ret));      /* tail_ipv4_policy: send_drop_notify */
+    notify_drop(dp, ret, len, ep->lxc_id, src_label, ep->seclabel, ep->lxc_id, ifindex);
     if (reason) *reason = ret;
     return OR_TC_ACT_SHOT;
 }
@@ -879,7 +915,8 @@ static int handle_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t 
     } else if (proto == 0x0008 && ep->ipv4) {
         return ipv4_policy(dp, ep, skb, ifindex, src_label, skip_proxy, now, ps, reason);
     } else ret = OR_DROP_UNKNOWN_L3;
-    update_metrics(dp, skb->len, 1, (uint8_t)(-ret));
+    update_metrics(dp, skb->len, 1, (uint8_t)(-ret));   /* bpf_lxc.c:1032-1035 */
+    notify_drop(dp, ret, skb->len, ep->lxc_id, src_label, ep->seclabel, ep->lxc_id, ifindex);
     if (reason) *reason = ret;
     return OR_TC_ACT_SHOT;
 }
@@ -945,6 +982,8 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
     for (uint32_t i = 0; i < n; i++) {
         skb_init(&skb, frames + (size_t)i * stride, stride, len[i]);
         uint32_t L = len[i];
+        dp->cur_pkt = i;
+        dp->cur_hash = 0;                              /* no skb hash input on this entry point */
         pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
         uint8_t xv = OR_XDP_PASS;
         int32_t ret = OR_TC_ACT_OK, reason = 0;
@@ -963,6 +1002,7 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
                 if (r == OR_E_TRUNC || final) ret = r;
                 else if (IS_ERR(r)) {                        /* tail_handle_ipv4 (:457-466) */
                     update_metrics(dp, L, 1, (uint8_t)(-r));
+                    notify_drop(dp, r, L, 0, 0, 0, 0, 0);        /* send_drop_notify_error */
                     reason = r;
                     ret = OR_TC_ACT_SHOT;
                 } else ret = r;
@@ -1582,7 +1622,8 @@ static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
     return ifindex ? OR_TC_ACT_REDIRECT : OR_TC_ACT_OK;
 drop:
     if (ret == OR_E_TRUNC) return ret;
-    update_metrics(dp, len, 1, (uint8_t)(-ret));
+    update_metrics(dp, len, 1, (uint8_t)(-ret));      /* tail_ipv6_policy: send_drop_notify */
+    notify_drop(dp, ret, len, ep->lxc_id, src_label, ep->seclabel, ep->lxc_id, ifindex);
     if (reason) *reason = ret;
     return OR_TC_ACT_SHOT;
 }
@@ -1712,6 +1753,7 @@ static int from_container(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t
     if (final || ret == OR_E_TRUNC || ret == OR_E_PUNT) return ret;
     if (IS_ERR(ret)) {                                              /* send_drop_notify(METRIC_EGRESS) */
         update_metrics(dp, skb->len, 2, (uint8_t)(-ret));
+        notify_drop(dp, ret, skb->len, ep->lxc_id, ep->seclabel, 0, 0, 0);
         *reason = ret;
         return OR_TC_ACT_SHOT;
     }
@@ -1726,6 +1768,8 @@ void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint
     for (uint32_t i = 0; i < n; i++) {
         skb_init(&skb, frames + (size_t)i * stride, stride, len[i]);
         pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
+        dp->cur_pkt = i;
+        dp->cur_hash = flow_hash ? flow_hash[i] : 0;   /* get_hash_recalc(skb) */
         uint32_t e = src_ep ? src_ep[i] : ep0, dst = 0;
         int32_t reason = 0, ret;
         if (e >= dp->n_ep) ret = OR_DROP_MISSED_TAIL_CALL;

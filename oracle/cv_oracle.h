@@ -153,6 +153,13 @@ typedef struct {
     uint8_t  node_mac[6];    /* NODE_MAC */
 } or_endpoint_prog;
 
+/* struct drop_notify (bpf/lib/drop.h:40-48) + the packet's batch index */
+typedef struct {
+    uint8_t  type, subtype;
+    uint16_t source;
+    uint32_t hash, len_orig, len_cap, src_label, dst_label, dst_id, ifindex, packet, reserved;
+} or_drop_notify;
+
 typedef struct or_dp {
     /* prefilter (bpf_xdp.c); NULL disables the map (filter_config.h) */
     or_map *v4_fix, *v4_dyn, *v6_fix, *v6_dyn;
@@ -168,6 +175,10 @@ typedef struct or_dp {
     or_endpoint_prog ep[OR_MAX_EP];   /* tail-call targets of cilium_policy (maps.h:44-51) */
     uint16_t ep_of_lxc[65536];        /* lxc_id -> index + 1 */
     uint64_t metrics[256][4][2];      /* Σ over CPUs of cilium_metrics (metrics.h:43-58): [reason][dir]{count,bytes} */
+    /* cilium_events drop notifications (DROP_NOTIFY), when attached */
+    or_drop_notify *notify;
+    uint32_t notify_cap, notify_n;
+    uint32_t cur_pkt, cur_hash;       /* the packet being processed and its skb hash */
 } or_dp;
 
 or_dp *or_dp_create(uint32_t flags);
@@ -180,6 +191,9 @@ int    or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_
 void   or_dp_node_config(or_dp *dp, uint32_t v4_cluster_mask, uint32_t v4_cluster_range, uint32_t v4_loopback,
                          const uint8_t *router_ip6);
 void   or_dp_metrics(const or_dp *dp, uint64_t *out /* [256][4][2] */);
+/* attach a record buffer (NULL detaches); returns and resets nothing: see or_dp_notify_count */
+void   or_dp_notify_attach(or_dp *dp, or_drop_notify *buf, uint32_t cap);
+uint32_t or_dp_notify_count(const or_dp *dp);
 
 /* per-packet outputs (SoA; any pointer may be NULL) */
 typedef struct {

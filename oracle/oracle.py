@@ -61,6 +61,9 @@ def lib():
         L.or_dp_endpoint_config.argtypes = [vp, u32, u32, vp, vp, vp, vp]
         L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp]
         L.or_lxc_egress.argtypes = [vp, vp, u32, vp, vp, u32, vp, u32, u32, vp]
+        L.or_dp_notify_attach.argtypes = [vp, vp, u32]
+        L.or_dp_notify_count.restype = u32
+        L.or_dp_notify_count.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -184,6 +187,19 @@ class ODp:
         import struct
         raw = [struct.unpack("<I", struct.pack(">I", v))[0] for v in (cluster_mask, cluster_range, loopback)]
         lib().or_dp_node_config(self.h, *raw, C.create_string_buffer(bytes(router_ip6), 16))
+
+    def notify_attach(self, capacity):
+        """Record drop notifications (send_drop_notify) into a host ring."""
+        from cilium_amd.lib import DROP_NOTIFY
+        self._nbuf = np.zeros(max(capacity, 1), DROP_NOTIFY)
+        self._ncap = capacity
+        lib().or_dp_notify_attach(self.h, self._nbuf.ctypes.data if capacity else None, capacity)
+
+    def notify_drain(self):
+        n = lib().or_dp_notify_count(self.h)
+        out = self._nbuf[: min(n, self._ncap)].copy()
+        lib().or_dp_notify_attach(self.h, self._nbuf.ctypes.data, self._ncap)
+        return out, n
 
     def metrics(self):
         m = np.zeros((256, 4, 2), np.uint64)

@@ -40,8 +40,11 @@ def same_table(pm, om, name):
 
 
 def check_egress(w, dev, batches, rounds=2):
+    from tests.test_gpu_parity import same_notifications
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)
+    ctx.notify_attach(w.n)
+    dp.notify_attach(w.n)
     cuts = np.linspace(0, w.n, batches + 1).astype(int)
     for rnd in range(rounds):
         now = w.now + rnd * 3
@@ -57,6 +60,7 @@ def check_egress(w, dev, batches, rounds=2):
                           o["ret"][bad[:12]], o["reason"][bad[:12]], "ref", ref.ret[bad[:12]], ref.reason[bad[:12]],
                           "ct", o["ct"][bad[:12]], ref.ct[bad[:12]], "nl", o["nl"][bad[:12]], ref.nl[bad[:12]])
                 assert len(bad) == 0, (k, rnd, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+            assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
     assert (ctx.metrics() == dp.metrics()).all()
     for name in ("ct4", "ct6", "policy"):
         same_table(pm, om, name)

@@ -154,10 +154,27 @@ def run_ingress(ctx, w, dev, lo, hi, with_prefilter=True):
     return H.host_out(out)
 
 
+def same_notifications(ctx, dp):
+    """The drop notification streams (send_drop_notify records) of one call, as sets
+    ordered by packet index (the device appends in no particular order)."""
+    got, n_got = ctx.notify_drain()
+    ref, n_ref = dp.notify_drain()
+    assert n_got == n_ref, (n_got, n_ref)
+    got = np.sort(got, order=["packet"])
+    ref = np.sort(ref, order=["packet"])
+    for f in ref.dtype.names:
+        bad = np.nonzero(got[f] != ref[f])[0]
+        assert len(bad) == 0, (f, bad[:5], got[bad[:5]], ref[bad[:5]])
+    return n_got
+
+
 def check_ingress(w, dev, batches, with_prefilter=True):
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)
+    ctx.notify_attach(w.n)
+    dp.notify_attach(w.n)
     cuts = np.linspace(0, w.n, batches + 1).astype(int)
+    drops = 0
     for lo, hi in zip(cuts[:-1], cuts[1:]):
         o = run_ingress(ctx, w, dev, lo, hi, with_prefilter)
         ref = dp.netdev_ingress(w.frames[lo:hi], w.length[lo:hi], w.mark[lo:hi], now=w.now,
@@ -165,6 +182,9 @@ def check_ingress(w, dev, batches, with_prefilter=True):
         for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
             bad = np.nonzero(o[k] != getattr(ref, k))[0]
             assert len(bad) == 0, (k, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+        assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
+        drops += int((o["reason"] != 0).sum())
+    assert drops > 0
     assert (ctx.metrics() == dp.metrics()).all()
     check_policy_maps(pm["policy"], om["policy"])
     ck, cv = pm["ct4"].dump()

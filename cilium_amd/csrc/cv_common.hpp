@@ -13,7 +13,8 @@ enum : int32_t {
     DROP_INVALID_SMAC = -130, DROP_INVALID_DMAC = -131, DROP_INVALID_SIP = -132,
     DROP_POLICY = -133, DROP_INVALID = -134, DROP_CT_INVALID_HDR = -135,
     DROP_CT_UNKNOWN_PROTO = -137, DROP_UNKNOWN_L3 = -139, DROP_MISSED_TAIL_CALL = -140,
-    DROP_WRITE_ERROR = -141, DROP_UNKNOWN_L4 = -142, DROP_CT_CREATE_FAILED = -155,
+    DROP_WRITE_ERROR = -141, DROP_UNKNOWN_L4 = -142, DROP_CSUM_L3 = -153, DROP_CSUM_L4 = -154,
+    DROP_CT_CREATE_FAILED = -155,
     DROP_INVALID_EXTHDR = -156, DROP_FRAG_NOSUPPORT = -157, DROP_NO_SERVICE = -158,
 };
 // E_TRUNC: a byte the path reads lies beyond the record (the caller must hand over

@@ -194,7 +194,13 @@ inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v;
 int compile_lxc(cv_ctx *c, HostMap *m)
 {
     std::vector<std::vector<uint32_t>> k4, v4, k6, v6;
-    std::vector<uint8_t> if4, if6;                         // endpoint_info.ifindex per entry (side values)
+    // 16-B side values per entry: endpoint_info.ifindex, .mac, .node_mac (common.h:165-173)
+    std::vector<uint8_t> if4, if6;
+    auto side = [](std::vector<uint8_t> &o, const uint8_t *v) {
+        o.insert(o.end(), v, v + 4);
+        o.insert(o.end(), v + 16, v + 22);
+        o.insert(o.end(), v + 24, v + 30);
+    };
     if (m) {
         if (m->ks != 20 || m->vs < 12) return -EINVAL;
         m->for_each([&](const uint8_t *k, const uint8_t *v) {
@@ -204,17 +210,17 @@ int compile_lxc(cv_ctx *c, HostMap *m)
                 for (int i = 4; i < 16; ++i) if (k[i]) return;
                 k4.push_back({rd32(k)});
                 v4.push_back({iv});
-                if4.insert(if4.end(), v, v + 4);
+                side(if4, v);
             } else if (k[16] == 2) {
                 k6.push_back({rd32(k), rd32(k + 4), rd32(k + 8), rd32(k + 12)});
                 v6.push_back({iv});
-                if6.insert(if6.end(), v, v + 4);
+                side(if6, v);
             }
         });
     }
     std::vector<int64_t> s4, s6;
-    int r = build_hash<LxcV4Spec>(c->lxc4, k4, v4, 4, &if4, &s4);
-    if (!r) r = build_hash<LxcV6Spec>(c->lxc6, k6, v6, 4, &if6, &s6);
+    int r = build_hash<LxcV4Spec>(c->lxc4, k4, v4, 16, &if4, &s4);
+    if (!r) r = build_hash<LxcV6Spec>(c->lxc6, k6, v6, 16, &if6, &s6);
     if (!m) { c->lxc4.view = HashTable{}; c->lxc6.view = HashTable{}; }
     return r;
 }
@@ -581,6 +587,8 @@ DpParams params(cv_ctx *c)
     p.v4_cluster_range = c->node.ipv4_cluster_range;
     p.v4_loopback = c->node.ipv4_loopback;
     memcpy(p.router6, c->node.router_ip6, 16);
+    p.host_mac[0] = p.host_mac[1] = 0;
+    memcpy(p.host_mac, c->node.host_mac, 6);
     const char *rm = getenv("CV_RECMODE");
     p.recmode = rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u;
     const char *ab = getenv("CV_ABLATE");
@@ -613,14 +621,15 @@ OutDev to_dev(const cv_out *o)
     OutDev d{};
     if (o) {
         d.xdp = o->xdp; d.ret = o->ret; d.identity = o->identity; d.ct = o->ct; d.proxy = o->proxy;
-        d.nl = o->nl; d.nu = o->nu; d.reason = o->reason;
+        d.nl = o->nl; d.nu = o->nu; d.reason = o->reason; d.frames = o->frames_out;
     }
     return d;
 }
 
-OutDev chunk(const cv_out *o, uint32_t off)
+OutDev chunk(const cv_out *o, uint32_t off, uint32_t stride = 0)
 {
     OutDev d = to_dev(o);
+    if (d.frames) d.frames += (size_t)off * stride;
     if (d.xdp) d.xdp += off;
     if (d.ret) d.ret += off;
     if (d.identity) d.identity += off;
@@ -1166,7 +1175,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
         const uint32_t n = std::min(c->chunk, b->n - off);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
-        if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off), gs,
+        if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off, b->stride), gs,
                                        (hipStream_t)stream)))
             return r;
         for (const HashTable &t : pols)
@@ -1200,7 +1209,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
         if ((r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0,
-                                   flow_hash ? flow_hash + off : nullptr, now, chunk(o, off), gs,
+                                   flow_hash ? flow_hash + off : nullptr, now, chunk(o, off, b->stride), gs,
                                    (hipStream_t)stream)))
             return r;
         for (const HashTable &t : pols)

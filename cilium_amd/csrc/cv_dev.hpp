@@ -363,8 +363,16 @@ __device__ __forceinline__ bool lxc6_find(const DpParams &p, const uint32_t *dad
 // slot); without the side array, the inline nonzero bit
 __device__ __forceinline__ uint32_t lxc_ifindex(const HashTable &t, int64_t slot, uint32_t ival)
 {
-    if (t.vals && slot >= 0) return *reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * 4);
+    if (t.vals && slot >= 0) return *reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * t.vstride);
     return (ival >> 17) & 1u;
+}
+
+// endpoint_info.mac / .node_mac of a matched cilium_lxc entry (words: bytes 0-3, 4-5)
+__device__ __forceinline__ void lxc_macs(const HashTable &t, int64_t slot, uint32_t *mac, uint32_t *node_mac)
+{
+    const uint32_t *v = reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * t.vstride);
+    mac[0] = v[1]; mac[1] = v[2] & 0xFFFFu;
+    node_mac[0] = (v[2] >> 16) | (v[3] << 16); node_mac[1] = v[3] >> 16;
 }
 
 // ipcache_lookup4 (eps.h:309-319) -> remote_endpoint_info.sec_label (0 = none)
@@ -1004,8 +1012,23 @@ __device__ __forceinline__ int rev_map_port(L4Hdr &h, uint32_t nexthdr, uint32_t
 struct Skb4 {
     uint32_t saddr, daddr, len, nexthdr, ttl;
     int l4off;
+    uint32_t avail;             // bytes of the frame in the record (loads past it: E_TRUNC)
     L4Hdr h;
 };
+
+// The L4 checksum update every IPv4 rewrite ends with (csum_l4_offset_and_flags,
+// csum.h:44-64: TCP check @16, UDP @6, none for ICMP): 0, or the code of the
+// helper's failed access to the field (DROP_CSUM_L4 past the packet, E_TRUNC past
+// the record).
+__device__ __forceinline__ int l4_csum_err(const Skb4 &s, uint32_t nexthdr)
+{
+    const int coff = nexthdr == 6 ? 16 : nexthdr == 17 ? 6 : 0;
+    if (!coff) return 0;
+    const uint32_t end = (uint32_t)(s.l4off + coff + 2);
+    if (s.l4off + coff < 0 || end > s.len) return DROP_CSUM_L4;
+    if (end > s.avail) return E_TRUNC;
+    return 0;
+}
 
 struct Skb6 {
     uint32_t saddr[4], daddr[4];
@@ -1066,8 +1089,152 @@ __device__ __forceinline__ Skb4 skb4_from(const Rec &r)
     s.nexthdr = rec_u8c<23>(r);
     s.ttl = rec_u8c<22>(r);
     s.l4off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
+    s.avail = r.stride;
     s.h = l4_read<34>(r, s.l4off);
     return s;
+}
+
+// ------------------------------------------------------------------ output frames (IPv4)
+// The frame rewrites of the reference (lb4_xlate lb.h:653-697, __lb4_rev_nat
+// lb.h:485-548, ipv4_l3 l3.h:54-69) replayed on the record's fields with the
+// kernel's checksum arithmetic (bpf_l3/l4_csum_replace, bpf_csum_diff for
+// CHECKSUM_NONE skbs; restated in oracle/cv_oracle.c and pinned there by
+// tests/golden/csum_kernel.npz).  Values are memory-order (LE loads of the bytes).
+__device__ __forceinline__ uint32_t cs_add(uint32_t a, uint32_t b) { const uint32_t r = a + b; return r + (r < b); }
+__device__ __forceinline__ uint32_t cs_fold(uint32_t x)
+{
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return ~x & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t cs16_add(uint32_t a, uint32_t b)
+{
+    const uint32_t r = (a + b) & 0xFFFFu;
+    return (r + (r < b)) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t csum_diff4(uint32_t from, uint32_t to, uint32_t seed)
+{
+    uint64_t t = (uint64_t)seed + ((uint64_t)(~from) | ((uint64_t)to << 32));
+    if (t < (uint64_t)seed) t++;
+    const uint64_t r = (t >> 32) + (t & 0xFFFFFFFFu);
+    uint32_t x = (uint32_t)r + (uint32_t)(r >> 32);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return (x & 0xFFFFu) + (x >> 16);
+}
+__device__ __forceinline__ uint32_t l3_by_diff(uint32_t c, uint32_t diff) { return cs_fold(cs_add(diff, ~c)); }
+__device__ __forceinline__ uint32_t l3_replace2(uint32_t c, uint32_t from, uint32_t to)
+{
+    return ~cs16_add(cs16_add(~c & 0xFFFFu, ~from & 0xFFFFu), to) & 0xFFFFu;
+}
+// bpf_l4_csum_replace: size 0 (diff in `to`) or 2; mm = BPF_F_MARK_MANGLED_0 (UDP)
+__device__ __forceinline__ uint32_t l4_replace(uint32_t c, uint32_t from, uint32_t to, int size, bool mm)
+{
+    if (mm && !c) return 0u;
+    uint32_t n = size == 0 ? cs_fold(cs_add(to, ~c)) : cs_fold(cs_add(cs_add(~c, ~(from & 0xFFFFu)), to & 0xFFFFu));
+    if (mm && !n) n = 0xFFFFu;
+    return n;
+}
+
+// a __lb4_rev_nat a program applied: {na, np} of the reverse NAT entry
+struct RevNatOut {
+    bool valid, loopback;
+    uint32_t na, np;
+};
+
+struct Frame4 {
+    uint32_t saddr, daddr, sp, dp, ttl, ipcs, l4cs;
+    uint32_t smac[2], dmac[2];
+    uint32_t nexthdr;
+    int l4off, coff;           // coff 0: no L4 checksum (ICMP, others)
+    bool mm, smac_set, dmac_set;
+};
+
+// the record as the program sees it before any rewrite; `csum_at` = the frame bytes
+// in global memory (the L4 checksum sits at a runtime offset)
+template <int NW>
+__device__ __forceinline__ void frame4_init(Frame4 &f, const RecT<NW> &r, const uint8_t *frame)
+{
+    f.saddr = rec_raw32c<26>(r);
+    f.daddr = rec_raw32c<30>(r);
+    f.ttl = rec_u8c<22>(r);
+    f.ipcs = rec_raw16c<24>(r);
+    f.nexthdr = rec_u8c<23>(r);
+    f.l4off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
+    f.coff = f.nexthdr == 6 ? 16 : f.nexthdr == 17 ? 6 : 0;
+    f.mm = f.nexthdr == 17;
+    const uint32_t lim = r.len < r.stride ? r.len : r.stride;
+    const bool ports = (uint32_t)f.l4off + 4 <= lim;
+    f.sp = ports ? (uint32_t)frame[f.l4off] | (uint32_t)frame[f.l4off + 1] << 8 : 0u;
+    f.dp = ports ? (uint32_t)frame[f.l4off + 2] | (uint32_t)frame[f.l4off + 3] << 8 : 0u;
+    const int co = f.l4off + f.coff;
+    f.l4cs = (f.coff && (uint32_t)co + 2 <= lim) ? ((uint32_t)frame[co] | (uint32_t)frame[co + 1] << 8) : 0u;
+    f.smac_set = f.dmac_set = false;
+}
+
+// lb4_xlate: daddr (and the loopback saddr), their diff into both checksums, the port
+__device__ __forceinline__ void frame4_xlate(Frame4 &f, uint32_t vip, uint32_t new_daddr, uint32_t new_saddr,
+                                             bool port_rw, uint32_t key_dport, uint32_t new_port)
+{
+    uint32_t sum = csum_diff4(vip, new_daddr, 0);
+    f.daddr = new_daddr;
+    if (new_saddr) { sum = csum_diff4(f.saddr, new_saddr, sum); f.saddr = new_saddr; }
+    f.ipcs = l3_by_diff(f.ipcs, sum);
+    if (f.coff) f.l4cs = l4_replace(f.l4cs, 0, sum, 0, f.mm);
+    if (port_rw) {                                                // l4_modify_port(TCP_DPORT_OFF)
+        if (f.coff) f.l4cs = l4_replace(f.l4cs, key_dport, new_port, 2, f.mm);
+        f.dp = new_port;
+    }
+}
+
+// __lb4_rev_nat with the reverse NAT entry {na, np}; old_sip = the tuple's saddr
+// (REV_NAT_F_TUPLE_SADDR) or the packet's
+__device__ __forceinline__ void frame4_revnat(Frame4 &f, uint32_t na, uint32_t np, bool loopback, uint32_t old_sip)
+{
+    if (np && (f.nexthdr == 6 || f.nexthdr == 17) && np != f.sp) {   // reverse_map_l4_port
+        if (f.coff) f.l4cs = l4_replace(f.l4cs, f.sp, np, 2, f.mm);
+        f.sp = np;
+    }
+    uint32_t sum = 0;
+    if (loopback) { sum = csum_diff4(f.daddr, old_sip, 0); f.daddr = old_sip; }
+    sum = csum_diff4(old_sip, na, sum);
+    f.saddr = na;
+    f.ipcs = l3_by_diff(f.ipcs, sum);
+    if (f.coff) f.l4cs = l4_replace(f.l4cs, 0, sum, 0, f.mm);
+}
+
+// ipv4_l3: ipv4_dec_ttl, then the MACs (smac optional)
+__device__ __forceinline__ void frame4_l3(Frame4 &f, const uint32_t *smac, const uint32_t *dmac)
+{
+    const uint32_t nt = (f.ttl - 1) & 0xFFu;
+    f.ipcs = l3_replace2(f.ipcs, f.ttl, nt);
+    f.ttl = nt;
+    if (smac) { f.smac[0] = smac[0]; f.smac[1] = smac[1]; f.smac_set = true; }
+    f.dmac[0] = dmac[0]; f.dmac[1] = dmac[1]; f.dmac_set = true;
+}
+
+// out = the input record with the rewritten fields
+__device__ __forceinline__ void frame4_emit(const Frame4 &f, const uint8_t *in, uint8_t *out, uint32_t stride,
+                                            uint32_t len)
+{
+    const uint32_t lim = len < stride ? len : stride;
+    for (uint32_t k = 0; k < stride; k += 16)
+        *reinterpret_cast<uint4 *>(out + k) = *reinterpret_cast<const uint4 *>(in + k);
+    auto put16 = [&](int off, uint32_t v) { out[off] = (uint8_t)v; out[off + 1] = (uint8_t)(v >> 8); };
+    auto put32 = [&](int off, uint32_t v) { put16(off, v & 0xFFFFu); put16(off + 2, v >> 16); };
+    if (f.dmac_set) { put32(0, f.dmac[0]); put16(4, f.dmac[1]); }
+    if (f.smac_set) { put32(6, f.smac[0]); put16(10, f.smac[1]); }
+    out[22] = (uint8_t)f.ttl;
+    put16(24, f.ipcs);
+    put32(26, f.saddr);
+    put32(30, f.daddr);
+    if ((uint32_t)f.l4off + 4 <= lim) { put16(f.l4off, f.sp); put16(f.l4off + 2, f.dp); }
+    if (f.coff && (uint32_t)(f.l4off + f.coff) + 2 <= lim) put16(f.l4off + f.coff, f.l4cs);
+}
+
+__device__ __forceinline__ void frame_copy(const uint8_t *in, uint8_t *out, uint32_t stride)
+{
+    for (uint32_t k = 0; k < stride; k += 16)
+        *reinterpret_cast<uint4 *>(out + k) = *reinterpret_cast<const uint4 *>(in + k);
 }
 
 // ------------------------------------------------------------------ endpoint ingress programs
@@ -1075,7 +1242,8 @@ __device__ __forceinline__ Skb4 skb4_from(const Rec &r)
 // Returns the final verdict (TC_ACT_*, drops accounted as METRIC_INGRESS) or E_TRUNC.
 __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
+                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m,
+                                           RevNatOut *rn = nullptr)
 {
     int ret;
     int verdict;
@@ -1095,7 +1263,10 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
         if (revnat4(p, st.rev_nat, na, np, a)) {
             const int r2 = rev_map_port(s.h, t.nexthdr, np);
             if (r2) { ret = r2; goto drop; }
+            const int r3 = l4_csum_err(s, t.nexthdr);             // __lb4_rev_nat checksum updates
+            if (r3) { ret = r3; goto drop; }
             t.saddr = na;
+            if (rn) *rn = RevNatOut{true, false, na, np};
         }
     }
     verdict = policy_ingress<true>(ep.policy, p.flags | (p.ablate << 16), s.len, src_label, t.dport, t.nexthdr, a);
@@ -1186,11 +1357,12 @@ drop:
 // before any conntrack work; IPv4 needs the endpoint's LXC_IPV4 program.
 __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                               bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                              uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
+                                              uint16_t &proxy, int32_t &reason, Acct &a, Met &m,
+                                              RevNatOut *rn = nullptr)
 {
     int ret;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ipv4) return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m);
+    else if (ep.ipv4) return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn);
     else ret = DROP_UNKNOWN_L3;
     m.drop(ret, s.len, METRIC_INGRESS);                            // bpf_lxc.c:1032-1035
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);

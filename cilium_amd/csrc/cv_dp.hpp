@@ -43,6 +43,7 @@ struct DpParams {              // by value as the kernel argument
     // node_config.h constants (raw network-order words)
     uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
     uint32_t router6[4];
+    uint32_t host_mac[2];      // HOST_IFINDEX_MAC bytes 0-3 | 4-5
     // drop notifications (cv_notify_attach): cv_drop_notify records of 10 words
     uint32_t *notify;
     uint32_t notify_cap;
@@ -73,6 +74,7 @@ struct OutDev {
     uint16_t *proxy;
     uint8_t *nl, *nu;          // optional accounting of map lookups / entry writes
     int32_t *reason;           // DROP_* behind a TC_ACT_SHOT, else 0
+    uint8_t *frames;           // optional output records (the batch's stride), see cv_out.frames_out
 };
 
 struct GroupScratch {          // address-pair grouping for conntrack (config 3)

@@ -209,6 +209,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         const uint32_t e = src_ep ? src_ep[i] : ep0;
+        if (o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
         m.pkt = b.base + i;
         m.hash = b.hash ? b.hash[i] : 0u;
         m.src_id = e < p.n_eps ? p.eps[e].lxc_id : 0u;
@@ -328,6 +329,11 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         }
         const uint32_t tdaddr = st.loopback ? vip : target;
         uint32_t flags = STAGE_CT | EG_SVC | (st.loopback ? EG_LOOPBACK : 0u);
+        const int coff = t.nexthdr == 6 ? 16 : t.nexthdr == 17 ? 6 : 0;   // lb4_xlate: the L4 checksum
+        if (coff) {                                               // update by diff (pseudo header)
+            const int c = rec_chk(r, off + coff, 2);
+            if (c) { ret = chk_err(c, DROP_CSUM_L4); goto fin; }
+        }
         uint32_t ndport = 0;
         if (sport_svc && key_dport != sport_svc && (t.nexthdr == 6 || t.nexthdr == 17)) {
             if (h.c2b) { ret = chk_err(h.c2b, DROP_WRITE_ERROR); goto fin; }
@@ -335,7 +341,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
             flags |= EG_DPORT_RW;
         }
         eg[0] = flags;
-        eg[2] = ndport << 16;
+        eg[2] = ndport << 16 | (key_dport & 0xFFFFu);                // (the final lb4_key.dport)
         eg[3] = (st.rev_nat & 0xFFFFu) | st.slave << 16;
         eg[4] = st.addr;
         eg[5] = st.svc_addr;
@@ -425,7 +431,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
             flags |= EG_DPORT_RW;
         }
         eg[0] = flags;
-        eg[2] = ndport << 16;
+        eg[2] = ndport << 16 | (key_dport & 0xFFFFu);                // (the final lb4_key.dport)
         eg[3] = (st.rev_nat & 0xFFFFu) | st.slave << 16;
         eg[4] = 0; eg[5] = 0;
         eg[12] = v[0]; eg[13] = v[1]; eg[14] = v[2]; eg[15] = v[3];   // tuple daddr = skb daddr = target
@@ -628,6 +634,37 @@ __global__ void __launch_bounds__(BLOCK) k_group_link(BatchDev b, GroupScratch g
 }
 
 // ================================================================== egress conntrack + delivery
+// The forwarded IPv4 frame of handle_ipv4_from_lxc: lb4_xlate (the LB stage's decision,
+// from the scratch words), the egress reverse NAT, then ipv4_l3 of the exit taken
+// (kind 0 pass_to_stack: dmac NODE_MAC; 1 to_host: NODE_MAC -> HOST_IFINDEX_MAC;
+// 2 ipv4_local_delivery: the endpoint's node_mac -> mac) and the destination
+// program's reverse NAT.
+__device__ __noinline__ void eg4_frame(const DpParams &p, const BatchDev &b, const OutDev &o, const uint32_t *eg,
+                                       uint32_t i, const EpDev &ep, const RevNatOut &rn1, int kind, int64_t lxc_slot,
+                                       const RevNatOut &rn2)
+{
+    Rec r;
+    rec_load(r, b, i, 3);
+    const uint8_t *in = b.frames + (size_t)i * b.stride;
+    Frame4 f;
+    frame4_init(f, r, in);
+    if (eg[0] & EG_SVC)
+        frame4_xlate(f, f.daddr, eg[7], (eg[0] & EG_LOOPBACK) ? eg[8] : 0u, eg[0] & EG_DPORT_RW, eg[2] & 0xFFFFu,
+                     eg[2] >> 16);
+    if (rn1.valid) frame4_revnat(f, rn1.na, rn1.np, rn1.loopback, f.saddr);
+    if (kind == 0) {
+        frame4_l3(f, nullptr, ep.node_mac);
+    } else if (kind == 1) {
+        frame4_l3(f, ep.node_mac, p.host_mac);
+    } else {
+        uint32_t mac[2], nmac[2];
+        lxc_macs(p.lxc4, lxc_slot, mac, nmac);
+        frame4_l3(f, nmac, mac);
+        if (rn2.valid) frame4_revnat(f, rn2.na, rn2.np, false, f.saddr);
+    }
+    frame4_emit(f, in, o.frames + (size_t)i * b.stride, b.stride, r.len);
+}
+
 // handle_ipv4_from_lxc (bpf_lxc.c:464-649) from skip_service_lookup on
 __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
                                             const GroupScratch &g, uint32_t i, Met &m)
@@ -662,6 +699,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     uint32_t iv;
     bool lxc_hit = false;
     int64_t lxc_slot = -1;
+    RevNatOut rn1{false, false, 0, 0}, rn2{false, false, 0, 0};                 // reverse NATs applied (output frames)
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     if (lookups) {                                                // destination category (:482-494)
@@ -686,6 +724,9 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (revnat4(p, st.rev_nat, na, np, a)) {
             const int r2 = rev_map_port(s.h, t.nexthdr, np);
             if (r2) { ret = r2; goto drop; }
+            const int r3 = l4_csum_err(s, t.nexthdr);             // __lb4_rev_nat checksum updates
+            if (r3) { ret = r3; goto drop; }
+            rn1 = RevNatOut{true, st.loopback != 0, na, np};
             const uint32_t old_sip = s.saddr;
             if (st.loopback) s.daddr = old_sip;
             s.saddr = na;
@@ -707,19 +748,27 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     if (lxc_hit) {
         if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
         m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
-        if (iv & (1u << 16)) { res.ret = TC_ACT_REDIRECT; eg_final(o, i, res, a); return; }
+        if (iv & (1u << 16)) {                                    // to_host
+            res.ret = TC_ACT_REDIRECT;
+            if (o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+            eg_final(o, i, res, a);
+            return;
+        }
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
         if (p.ablate & AB_EG_NO_DELIVERY) { res.ret = TC_ACT_OK; eg_final(o, i, res, a); return; }
         res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, lxc_ifindex(p.lxc4, lxc_slot, iv), now,
-                                 ct2, res.proxy, res.reason, a, m);
+                                 ct2, res.proxy, res.reason, a, m, &rn2);
+        if (o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
+            eg4_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv4_local_delivery
         eg_final(o, i, res, a);
         return;
     }
     if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }            // pass_to_stack: ipv4_l3
     m.fwd(s.len, METRIC_EGRESS);                                  // TRACE_TO_STACK
     res.ret = TC_ACT_OK;
+    if (o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
     return;
 drop:

@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                         staged = true;                            // -> handle_policy -> tail_ipv4_policy
                         g.secctx[i] = secctx;
                         g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
-                        g.ifx[i] = lxc_ifindex(p.lxc4, lxc_slot, iv);   // cb[CB_IFINDEX] = ep->ifindex
+                        g.ifx[i] = (uint32_t)lxc_slot;            // -> cb[CB_IFINDEX], MACs (stage 2)
                     }
                 }
             }
@@ -311,6 +311,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
         }
         if (!live) continue;
+        if (o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
         if (!staged) {
             g.gslot[i] = NONE;
             if (o.ret) o.ret[i] = ret;
@@ -342,7 +343,22 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     Skb4 s = skb4_from(r);
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
-    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u, g.ifx[i], now, ct, proxy, reason, a, m);
+    const int64_t lslot = (int32_t)g.ifx[i];                     // the destination's cilium_lxc slot
+    RevNatOut rn{false, false, 0, 0};
+    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u, lxc_ifindex(p.lxc4, lslot, 0u), now, ct,
+                                   proxy, reason, a, m, &rn);
+    if (o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
+        // the forwarded frame: ipv4_local_delivery's ipv4_l3 (bpf_netdev handle_ipv4), then
+        // the policy program's reverse NAT
+        const uint8_t *in = b.frames + (size_t)i * b.stride;
+        Frame4 f;
+        frame4_init(f, r, in);
+        uint32_t mac[2], nmac[2];
+        lxc_macs(p.lxc4, lslot, mac, nmac);
+        frame4_l3(f, nmac, mac);
+        if (rn.valid) frame4_revnat(f, rn.na, rn.np, false, f.saddr);
+        frame4_emit(f, in, o.frames + (size_t)i * b.stride, b.stride, r.len);
+    }
     if (o.ret) o.ret[i] = ret;
     if (o.reason) o.reason[i] = reason;
     if (o.ct) o.ct[i] = ct;

@@ -817,5 +817,6 @@ def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n
     return Workload("config5", maps, frames, length, np.zeros(n_pkts, np.uint32), eps, now=2_000_000,
                     extra={"src_ep": src_ep, "flow_hash": fhash,
                            "node": {"cluster_mask": CLUSTER_V4[1], "cluster_range": CLUSTER_V4[0],
-                                    "loopback": IPV4_LOOPBACK, "router_ip6": ROUTER_IP6},
+                                    "loopback": IPV4_LOOPBACK, "router_ip6": ROUTER_IP6,
+                                    "host_mac": bytes([0x02, 0x00, 0x00, 0x00, 0xFE, 0x01])},
                            "kind": kind[fi], "reply": rep, "v6": f6})

@@ -138,6 +138,7 @@ typedef struct {
     uint32_t ipv4_cluster_range;  /* IPV4_CLUSTER_RANGE */
     uint32_t ipv4_loopback;       /* IPV4_LOOPBACK      */
     uint8_t  router_ip6[16];      /* ROUTER_IP          */
+    uint8_t  host_mac[6];         /* HOST_IFINDEX_MAC   */
 } cv_node_cfg;
 int cv_node_config(cv_ctx *ctx, const cv_node_cfg *cfg);
 
@@ -162,6 +163,10 @@ typedef struct {              /* any pointer may be NULL */
     uint8_t  *nl;             /* map lookups the path performed (algorithmic-bytes accounting) */
     uint8_t  *nu;             /* map entry writes the path performed */
     int32_t  *reason;         /* DROP_* code behind a TC_ACT_SHOT (the cilium_metrics reason), else 0 */
+    uint8_t  *frames_out;     /* optional (cv_netdev_ingress, cv_lxc_egress): n records of the batch's
+                                 stride: the frame after the datapath's rewrites (lb4_xlate, rev-NAT,
+                                 ipv4_l3 TTL/MACs, with the kernel's checksum updates) for a
+                                 forwarded IPv4 packet, else the input record */
 } cv_out;
 
 /* config 1: bpf_xdp.c xdp_start over the batch */

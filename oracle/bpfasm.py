@@ -151,3 +151,18 @@ def prog_test_run(fd, data: bytes, repeat=1, ctx: bytes | None = None):
         raise OSError(-r, "BPF_PROG_TEST_RUN")
     _, retval, _, _, _, _, _, duration = struct.unpack_from("IIIIQQII", buf.raw)
     return retval, duration
+
+
+def prog_test_run_out(fd, data: bytes, ctx: bytes | None = None):
+    """BPF_PROG_TEST_RUN returning (retval, data_out): the packet after the program
+    (skb programs get a CHECKSUM_NONE skb)."""
+    db = C.create_string_buffer(data, len(data))
+    ob = C.create_string_buffer(len(data) + 256)
+    cb = C.create_string_buffer(ctx, len(ctx)) if ctx else None
+    attr = struct.pack("IIIIQQIIIIQQ", fd, 0, len(data), len(data) + 256, C.addressof(db), C.addressof(ob), 1, 0,
+                       len(ctx) if ctx else 0, 0, C.addressof(cb) if cb else 0, 0)
+    r, buf = _bpf(BPF_PROG_TEST_RUN, attr)
+    if r < 0:
+        raise OSError(-r, "BPF_PROG_TEST_RUN")
+    _, retval, _, size_out = struct.unpack_from("IIII", buf.raw)
+    return retval, ob.raw[:size_out]

@@ -355,10 +355,12 @@ int or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_t *
     return 0;
 }
 
-void or_dp_node_config(or_dp *dp, uint32_t mask, uint32_t range, uint32_t loopback, const uint8_t *router_ip6)
+void or_dp_node_config(or_dp *dp, uint32_t mask, uint32_t range, uint32_t loopback, const uint8_t *router_ip6,
+                       const uint8_t *host_mac)
 {
     dp->v4_cluster_mask = mask; dp->v4_cluster_range = range; dp->v4_loopback = loopback;
     if (router_ip6) memcpy(dp->router_ip6, router_ip6, 16);
+    if (host_mac) memcpy(dp->host_mac, host_mac, 6);
 }
 
 int or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *policy, or_map *ct4)
@@ -779,6 +781,18 @@ static void skb_init(or_skb *s, const uint8_t *f, uint32_t stride, uint32_t len)
 
 static inline int sld(const or_skb *s, int off, uint32_t n, void *to) { return ld(s->b, s->avail, s->len, off, n, to); }
 
+/* out->frames_out of packet i: the rewritten frame of a forwarded (TC_ACT_OK / REDIRECT,
+ * not to the L7 proxy) IPv4 packet, else the input frame (IPv6 rewrites: a later row) */
+static void emit_frame(const or_out *out, uint32_t i, const uint8_t *in, uint32_t stride, const or_skb *s,
+                       int32_t ret, uint16_t proxy)
+{
+    if (!out->frames_out) return;
+    uint8_t *o = out->frames_out + (size_t)i * stride;
+    memcpy(o, in, stride);
+    const int v4 = stride >= 14 && in[12] == 0x08 && in[13] == 0x00;
+    if (v4 && (ret == OR_TC_ACT_OK || ret == OR_TC_ACT_REDIRECT) && !proxy) memcpy(o, s->b, s->avail);
+}
+
 /* skb_store_bytes: 0, 1 (beyond len: the helper fails) or OR_E_TRUNC */
 static inline int sst(or_skb *s, int off, uint32_t n, const void *from)
 {
@@ -788,6 +802,122 @@ static inline int sst(or_skb *s, int off, uint32_t n, const void *from)
     return 0;
 }
 
+/* ---- checksum helpers of the packet rewrites -------------------------------
+ * Third-party arithmetic: the Linux kernel's bpf_l3_csum_replace /
+ * bpf_l4_csum_replace / bpf_csum_diff (net/core/filter.c) over csum_replace2/4,
+ * csum_replace_by_diff, inet_proto_csum_replace{4,_by_diff} and csum_partial
+ * (include/net/checksum.h, net/core/utils.c, arch/x86/lib/csum-partial_64.c) of the
+ * container's kernel 6.18, for CHECKSUM_NONE skbs (BPF_PROG_TEST_RUN; fully
+ * software-checksummed packets).  Pinned by tests/golden/csum_kernel.npz, produced
+ * by running the helpers in the kernel (oracle/kernel_golden.py gen_csum).  Values
+ * are in memory byte order (little-endian loads of network-order bytes). */
+static inline uint32_t cs_add(uint32_t a, uint32_t b) { uint32_t r = a + b; return r + (r < b); }
+static inline uint32_t cs_sub(uint32_t a, uint32_t b) { return cs_add(a, ~b); }
+static inline uint16_t cs_fold(uint32_t x)
+{
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return (uint16_t)~x;
+}
+static inline uint16_t cs16_add(uint16_t a, uint16_t b) { uint16_t r = (uint16_t)(a + b); return (uint16_t)(r + (r < b)); }
+
+/* bpf_csum_diff(&from, 4, &to, 4, seed): the 16-bit folded sum of ~from, to, seed */
+static uint32_t csum_diff4(uint32_t from, uint32_t to, uint32_t seed)
+{
+    uint64_t t = (uint64_t)seed + ((uint64_t)(~from) | ((uint64_t)to << 32));
+    if (t < (uint64_t)seed) t++;                           /* addq + adcq $0 */
+    uint64_t r = (t >> 32) + (t & 0xFFFFFFFFu);            /* add32_with_carry */
+    uint32_t x = (uint32_t)r + (uint32_t)(r >> 32);
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return x;
+}
+
+static inline uint16_t sum16_get(const or_skb *s, int off) { return (uint16_t)(s->b[off] | s->b[off + 1] << 8); }
+static inline void sum16_put(or_skb *s, int off, uint16_t v) { s->b[off] = (uint8_t)v; s->b[off + 1] = (uint8_t)(v >> 8); }
+
+/* the access check of both helpers: 0, OR_E_TRUNC (beyond the record), 1 (beyond the packet) */
+static inline int csum_at(const or_skb *s, int off)
+{
+    if (off < 0 || (uint64_t)off + 2 > s->len) return 1;
+    if ((uint64_t)off + 2 > s->avail) return OR_E_TRUNC;
+    return 0;
+}
+
+/* bpf_l3_csum_replace: size 0 = by diff (to), 2 / 4 = replace from -> to */
+static int l3_csum_replace(or_skb *s, int off, uint32_t from, uint32_t to, int size)
+{
+    int r = csum_at(s, off);
+    if (r) return r;
+    uint16_t c = sum16_get(s, off);
+    if (size == 0) c = cs_fold(cs_add(to, ~(uint32_t)c));
+    else if (size == 2) c = (uint16_t)~cs16_add(cs16_add((uint16_t)~c, (uint16_t)~(uint16_t)from), (uint16_t)to);
+    else c = cs_fold(cs_add(cs_sub(~(uint32_t)c, from), to));
+    sum16_put(s, off, c);
+    return 0;
+}
+
+#define OR_F_PSEUDO_HDR 0x10u
+#define OR_F_MARK_MANGLED_0 0x20u
+/* bpf_l4_csum_replace (size in flags & 0xF; CHECKSUM_NONE: BPF_F_PSEUDO_HDR has no effect) */
+static int l4_csum_replace(or_skb *s, int off, uint32_t from, uint32_t to, uint32_t flags)
+{
+    int r = csum_at(s, off);
+    if (r) return r;
+    uint16_t c = sum16_get(s, off);
+    const int mm = (flags & OR_F_MARK_MANGLED_0) != 0;
+    if (mm && !c) return 0;
+    if ((flags & 0xF) == 0) c = cs_fold(cs_add(to, ~(uint32_t)c));
+    else {
+        if ((flags & 0xF) == 2) { from &= 0xFFFFu; to &= 0xFFFFu; }
+        c = cs_fold(cs_add(cs_sub(~(uint32_t)c, from), to));
+    }
+    if (mm && !c) c = 0xFFFFu;                             /* CSUM_MANGLED_0 */
+    sum16_put(s, off, c);
+    return 0;
+}
+
+/* csum_l4_offset_and_flags (csum.h:44-64) */
+static inline void l4_csum_off(uint8_t nexthdr, int *off, uint32_t *flags)
+{
+    *off = 0; *flags = 0;
+    if (nexthdr == 6) *off = 16;
+    else if (nexthdr == 17) { *off = 6; *flags = OR_F_MARK_MANGLED_0; }
+    else if (nexthdr == 58) *off = 2;
+}
+
+static inline int csum_err(int r, int code) { return r == OR_E_TRUNC ? r : code; }
+
+/* l4_modify_port (l4.h:50-60): L4 checksum (2-byte replace), then the port */
+static int l4_modify_port(or_skb *s, int l4_off, int port_off, uint8_t nexthdr, uint16_t port, uint16_t old_port)
+{
+    int coff; uint32_t cfl;
+    l4_csum_off(nexthdr, &coff, &cfl);
+    if (coff) {
+        int r = l4_csum_replace(s, l4_off + coff, old_port, port, cfl | 2);
+        if (r) return csum_err(r, OR_DROP_CSUM_L4);
+    }
+    int r = sst(s, l4_off + port_off, 2, &port);
+    return r ? csum_err(r, OR_DROP_WRITE_ERROR) : 0;
+}
+
+/* ipv4_l3 (l3.h:54-69): ipv4_dec_ttl (ipv4.h:30-43: TTL <= 1 -> DROP_INVALID, else the
+ * 2-byte L3 checksum replace of the TTL and the new TTL), then the source MAC (when
+ * given) and the destination MAC */
+static int ipv4_l3(or_skb *skb, const uint8_t *smac, const uint8_t *dmac)
+{
+    uint8_t ttl = skb->b[22];
+    if (ttl <= 1) return OR_DROP_INVALID;
+    uint8_t nt = (uint8_t)(ttl - 1);
+    int r = l3_csum_replace(skb, ETH_HLEN + 10, ttl, nt, 2);
+    if (r) return csum_err(r, OR_DROP_CSUM_L3);
+    skb->b[22] = nt;
+    if (smac && sst(skb, 6, 6, smac)) return OR_DROP_WRITE_ERROR;
+    if (sst(skb, 0, 6, dmac)) return OR_DROP_WRITE_ERROR;
+    return OR_TC_ACT_OK;
+}
+
+_Static_assert(sizeof(or_endpoint_info) == 48, "struct endpoint_info");
 /* ===================================================================== */
 /* Ingress: from_netdev -> handle_ipv4 -> ipv4_policy                     */
 /* ===================================================================== */
@@ -816,25 +946,31 @@ static int lb4_rev_nat(or_dp *dp, or_skb *skb, int l4_off, const or_ct_state *st
         case 6: case 17: {
             uint16_t old;
             if ((r = sld(skb, l4_off + TCP_SPORT_OFF, 2, &old))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
-            if (nat->port != old) {
-                if ((r = sst(skb, l4_off + TCP_SPORT_OFF, 2, &nat->port))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
-            }
+            if (nat->port != old && (r = l4_modify_port(skb, l4_off, TCP_SPORT_OFF, t->nexthdr, nat->port, old)))
+                return r;
             break;
         }
         case 1: case 58: break;
         default: return OR_DROP_UNKNOWN_L4;
         }
     }
-    uint32_t old_sip, new_sip = nat->address;
+    uint32_t old_sip, new_sip = nat->address, sum = 0;
     if (tuple_saddr) { old_sip = t->saddr; t->saddr = new_sip; }
     else if ((r = sld(skb, ETH_HLEN + 12, 4, &old_sip))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
     if (st->loopback) {
         uint32_t old_dip;
         if ((r = sld(skb, ETH_HLEN + 16, 4, &old_dip))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
         if ((r = sst(skb, ETH_HLEN + 16, 4, &old_sip))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+        sum = csum_diff4(old_dip, old_sip, 0);
         t->saddr = old_sip;
     }
     if ((r = sst(skb, ETH_HLEN + 12, 4, &new_sip))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    sum = csum_diff4(old_sip, new_sip, sum);          /* __lb4_rev_nat (lb.h:540-547) */
+    if ((r = l3_csum_replace(skb, ETH_HLEN + 10, 0, sum, 0))) return csum_err(r, OR_DROP_CSUM_L3);
+    int coff; uint32_t cfl;
+    l4_csum_off(t->nexthdr, &coff, &cfl);
+    if (coff && (r = l4_csum_replace(skb, l4_off + coff, 0, sum, cfl | OR_F_PSEUDO_HDR)))
+        return csum_err(r, OR_DROP_CSUM_L4);
     return 0;
 }
 
@@ -955,8 +1091,9 @@ static int handle_ipv4(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_p
     or_endpoint_info *ep = lookup_ip4_endpoint(dp, daddr, &ps->nl);
     if (ep) {
         if (ep->flags & 1) return OR_TC_ACT_OK;        /* ENDPOINT_F_HOST */
-        /* ipv4_local_delivery (l3.h:247-276): ipv4_l3 -> ipv4_dec_ttl (ipv4.h:124-137) */
-        if (f[22] <= 1) return OR_DROP_INVALID;
+        /* ipv4_local_delivery (l3.h:103-132): ipv4_l3 -> ipv4_dec_ttl, MACs */
+        int rl3 = ipv4_l3(skb, ep->node_mac, ep->mac);
+        if (rl3 != OR_TC_ACT_OK) return rl3;
         or_endpoint_prog *prog = find_ep(dp, ep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;   /* tail_call(cilium_policy, lxc_id) missed */
         *final = 1;
@@ -1011,6 +1148,7 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
             }
         }
         if (out->xdp) out->xdp[i] = xv;
+        emit_frame(out, i, frames + (size_t)i * stride, stride, &skb, ret, ps.proxy);
         if (out->ret) out->ret[i] = ret;
         if (out->identity) out->identity[i] = ident;
         if (out->ct) out->ct[i] = ps.ct;
@@ -1229,15 +1367,23 @@ static int lb4_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb4_key 
         st->svc_addr = saddr;
     }
     if (!st->loopback) t->daddr = svc->target;
-    /* lb4_xlate */
+    /* lb4_xlate (lb.h:653-697): addresses, their checksum diff into the L3 and (pseudo
+     * header) L4 checksums, then the service port */
     int r = sst(skb, ETH_HLEN + 16, 4, &new_daddr);
     if (r) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    uint32_t sum = csum_diff4(key->address, new_daddr, 0);
     if (new_saddr) {
         r = sst(skb, ETH_HLEN + 12, 4, &new_saddr);
         if (r) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+        sum = csum_diff4(saddr, new_saddr, sum);
     }
+    if ((r = l3_csum_replace(skb, ETH_HLEN + 10, 0, sum, 0))) return csum_err(r, OR_DROP_CSUM_L3);
+    int coff; uint32_t cfl;
+    l4_csum_off(t->nexthdr, &coff, &cfl);
+    if (coff && (r = l4_csum_replace(skb, l4_off + coff, 0, sum, cfl | OR_F_PSEUDO_HDR)))
+        return csum_err(r, OR_DROP_CSUM_L4);
     if (svc->port && key->dport != svc->port && (t->nexthdr == 6 || t->nexthdr == 17)) {
-        r = l4_store_dport(skb, l4_off, svc->port);
+        r = l4_modify_port(skb, l4_off, TCP_DPORT_OFF, t->nexthdr, svc->port, key->dport);
         if (r) return r;
     }
     return OR_TC_ACT_OK;
@@ -1252,16 +1398,6 @@ static int policy_can_egress(or_map *map, uint32_t flags, uint32_t len, uint32_t
     int ret = policy_can_access(map, flags, len, identity, dport, proto, OR_CT_EGRESS, nl, nu);
     if (ret >= 0) return ret;
     return OR_DROP_POLICY;
-}
-
-/* ipv4_l3 (l3.h:54-69): TTL <= 1 -> DROP_INVALID (ipv4_dec_ttl, ipv4.h:30-43) */
-static int ipv4_l3(or_skb *skb)
-{
-    uint8_t ttl = skb->b[22];
-    if (ttl <= 1) return OR_DROP_INVALID;
-    ttl--;
-    skb->b[22] = ttl;
-    return OR_TC_ACT_OK;
 }
 
 /* handle_ipv4_from_lxc (bpf_lxc.c:402-649) of endpoint `ep`, direct routing (no
@@ -1342,14 +1478,17 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         /* ipv4_redirect_to_host_port: dport := proxy port, daddr := IPV4_GATEWAY,
          * proxy-map insert (L7 side effect, out of scope) */
         ps->proxy = (uint16_t)verdict;
-        int r = ipv4_l3(skb);
+        int r = ipv4_l3(skb, ep->node_mac, dp->host_mac);
         if (r != OR_TC_ACT_OK) return r;
         return OR_TC_ACT_REDIRECT;                                  /* redirect(HOST_IFINDEX) */
     }
     uint32_t daddr; memcpy(&daddr, skb->b + 30, 4);                 /* after the L4/L3 rewrites */
     or_endpoint_info *dep = lookup_ip4_endpoint(dp, daddr, &ps->nl);
     if (dep) {
-        int r = ipv4_l3(skb);
+        /* to_host: ipv4_l3(NODE_MAC, HOST_IFINDEX_MAC); local: ipv4_local_delivery (l3.h:
+         * 103-132) ipv4_l3(endpoint_info.node_mac, endpoint_info.mac) */
+        int r = (dep->flags & 1) ? ipv4_l3(skb, ep->node_mac, dp->host_mac)
+                                 : ipv4_l3(skb, dep->node_mac, dep->mac);
         if (r != OR_TC_ACT_OK) return r;
         update_metrics(dp, len, 2, 0);            /* to_host: TRACE_TO_HOST / ipv4_local_delivery */
         if (dep->flags & 1) return OR_TC_ACT_REDIRECT;              /* ENDPOINT_F_HOST: redirect(HOST_IFINDEX) */
@@ -1361,7 +1500,7 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         ps->ct = ct_egress;
         return r;
     }
-    int r = ipv4_l3(skb);                                           /* pass_to_stack */
+    int r = ipv4_l3(skb, NULL, ep->node_mac);                      /* pass_to_stack */
     if (r != OR_TC_ACT_OK) return r;
     update_metrics(dp, len, 2, 0);                                  /* TRACE_TO_STACK */
     return OR_TC_ACT_OK;
@@ -1782,6 +1921,7 @@ void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint
         if (out->nu) out->nu[i] = ps.nu;
         if (out->reason) out->reason[i] = reason;
         if (out->xdp) out->xdp[i] = 0;
+        emit_frame(out, i, frames + (size_t)i * stride, stride, &skb, ret, ps.proxy);
     }
 }
 
@@ -1804,4 +1944,18 @@ uint32_t or_ct_gc(or_map *m, uint32_t time)
     free(keys);
     free(vals);
     return deleted;
+}
+
+/* known-answer access to the checksum restatement (tests/test_oracle_golden.py):
+ * op 0 l3_csum_replace, 1 l4_csum_replace on frame[0..len), 2 csum_diff4 -> *diff */
+int or_csum_apply(uint8_t *frame, uint32_t len, uint32_t op, uint32_t off, uint32_t from, uint32_t to,
+                  uint32_t flags, uint64_t *diff)
+{
+    if (op == 2) { *diff = csum_diff4(from, to, flags); return 0; }
+    or_skb s;
+    skb_init(&s, frame, len, len);
+    int r = op == 0 ? l3_csum_replace(&s, (int)off, from, to, (int)(flags & 0xF))
+                    : l4_csum_replace(&s, (int)off, from, to, flags);
+    memcpy(frame, s.b, s.avail);
+    return r;
 }

@@ -54,6 +54,8 @@ extern "C" {
 #define OR_DROP_INVALID_EXTHDR    -156
 #define OR_DROP_FRAG_NOSUPPORT    -157
 #define OR_DROP_NO_SERVICE        -158
+#define OR_DROP_CSUM_L3 (-153)
+#define OR_DROP_CSUM_L4 (-154)
 #define OR_DROP_WRITE_ERROR       -141
 #define OR_DROP_PROXYMAP_CREATE_FAILED -159
 /* oracle-only: a header byte the reference would read lies beyond the record */
@@ -89,9 +91,9 @@ typedef struct { uint8_t address[16]; uint16_t dport; uint16_t slave; } or_lb6_k
 typedef struct { uint8_t target[16]; uint16_t port; uint16_t count; uint16_t rev_nat_index; uint16_t weight; } or_lb6_service; /* common.h:414-420 */
 #pragma pack(pop)
 
-typedef struct {             /* common.h:165-173, 48 bytes */
-    uint32_t ifindex; uint16_t unused; uint16_t lxc_id; uint32_t flags;
-    uint32_t mac_lo, mac_hi, node_mac_lo, node_mac_hi; uint32_t pad[4];
+typedef struct {             /* common.h:165-173, 48 bytes: mac_t is 8-byte aligned (mac @16) */
+    uint32_t ifindex; uint16_t unused; uint16_t lxc_id; uint32_t flags; uint32_t pad0;
+    uint8_t mac[8], node_mac[8]; uint32_t pad[4];
 } or_endpoint_info;
 typedef struct { uint32_t sec_label; uint32_t tunnel_endpoint; } or_remote_endpoint_info; /* common.h:175-178 */
 typedef struct { uint32_t sec_label; uint16_t dport; uint8_t protocol; uint8_t egress_pad; } or_policy_key; /* common.h:180-186 */
@@ -123,6 +125,9 @@ int      or_map_delete(or_map *m, const void *key);
 uint32_t or_map_count(const or_map *m);
 /* all entries, sorted by key bytes; returns the count written (<= max) */
 uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max);
+/* the kernel checksum helper restatement (known-answer tests) */
+int or_csum_apply(uint8_t *frame, uint32_t len, uint32_t op, uint32_t off, uint32_t from, uint32_t to,
+                  uint32_t flags, uint64_t *diff);
 /* ctmap.GC(GCFilterByTime) on a CT map: delete entries with lifetime < time */
 uint32_t or_ct_gc(or_map *m, uint32_t time);
 void    *or_map_lookup_ptr(or_map *m, const void *key);
@@ -171,6 +176,7 @@ typedef struct or_dp {
     /* node_config.h constants (raw network-order words) */
     uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
     uint8_t  router_ip6[16];
+    uint8_t  host_mac[6];             /* HOST_IFINDEX_MAC */
     uint32_t n_ep;
     or_endpoint_prog ep[OR_MAX_EP];   /* tail-call targets of cilium_policy (maps.h:44-51) */
     uint16_t ep_of_lxc[65536];        /* lxc_id -> index + 1 */
@@ -189,7 +195,7 @@ int    or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_
                              const uint8_t *node_mac, or_map *ct6);
 /* node_config.h: IPV4_CLUSTER_MASK / IPV4_CLUSTER_RANGE / IPV4_LOOPBACK / ROUTER_IP */
 void   or_dp_node_config(or_dp *dp, uint32_t v4_cluster_mask, uint32_t v4_cluster_range, uint32_t v4_loopback,
-                         const uint8_t *router_ip6);
+                         const uint8_t *router_ip6, const uint8_t *host_mac);
 void   or_dp_metrics(const or_dp *dp, uint64_t *out /* [256][4][2] */);
 /* attach a record buffer (NULL detaches); returns and resets nothing: see or_dp_notify_count */
 void   or_dp_notify_attach(or_dp *dp, or_drop_notify *buf, uint32_t cap);
@@ -205,6 +211,8 @@ typedef struct {
     uint8_t  *nl;         /* map lookups performed (algorithmic bytes) */
     uint8_t  *nu;         /* map entry writes performed */
     int32_t  *reason;     /* DROP_* behind a TC_ACT_SHOT, else 0 */
+    uint8_t  *frames_out; /* the frame after the datapath's rewrites (stride bytes per packet;
+                             forwarded IPv4 packets; others: the input frame) */
 } or_out;
 
 /* Config 1: bpf_xdp.c xdp_start over a batch of frames (records of `stride` bytes). */

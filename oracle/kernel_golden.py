@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 
 from cilium_amd import synth  # noqa: E402
 from oracle.bpfasm import (Asm, KMap, insn, prog_load, prog_test_run, PROG_XDP, PROG_SCHED_CLS,  # noqa: E402
-                           BPF_F_NO_PREALLOC, R0, R1, R2, R3, R4, R6, R7, R8, R9, FP)
+                           BPF_F_NO_PREALLOC, R0, R1, R2, R3, R4, R5, R6, R7, R8, R9, FP)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 MAP_LOOKUP = 1
@@ -378,8 +378,93 @@ def gen_map_semantics():
     print("map semantics:", [len(c[1]) for c in cases], "ops")
 
 
+# ------------------------------------------------------------------------
+# checksum helpers: bpf_l3_csum_replace / bpf_l4_csum_replace / bpf_csum_diff
+# (net/core/filter.c on the container's kernel), the arithmetic of every packet
+# rewrite on the path (lb.h lb4_xlate / __lb4_rev_nat, l3.h ipv4_l3 -> ipv4_dec_ttl)
+# ------------------------------------------------------------------------
+CSUM_FRAME = 96          # eth + ipv4 + tcp, params @64, csum_diff result @84
+H_STORE, H_L3, H_L4, H_LOAD, H_DIFF = 9, 10, 11, 26, 28
+
+
+def csum_prog():
+    """op = u32 @64: 0 l3_csum_replace(skb, off, from, to, flags), 1 l4_csum_replace,
+    2 csum_diff(&from, 4, &to, 4, seed) -> u64 stored @84; params off/from/to/flags
+    (seed) as u32 @68/@72/@76/@80."""
+    a = Asm()
+    a.mov(R6, R1)
+    a.mov(R1, R6); a.movi(R2, 64); a.mov(R3, FP); a.addi(R3, -32); a.movi(R4, 20); a.call(H_LOAD)
+    a.jnei(R0, 0, "out")
+    a.ldxw(R7, FP, -32)
+    a.ldxw(R2, FP, -28); a.ldxw(R3, FP, -24); a.ldxw(R4, FP, -20); a.ldxw(R5, FP, -16)
+    a.jeqi(R7, 0, "l3")
+    a.jeqi(R7, 1, "l4")
+    a.mov(R1, FP); a.addi(R1, -24); a.movi(R2, 4); a.mov(R3, FP); a.addi(R3, -20); a.movi(R4, 4)
+    a.call(H_DIFF)
+    a.stxw(FP, -8, R0)
+    a.rshi(R0, 32)
+    a.stxw(FP, -4, R0)
+    a.mov(R1, R6); a.movi(R2, 84); a.mov(R3, FP); a.addi(R3, -8); a.movi(R4, 8); a.movi(R5, 0); a.call(H_STORE)
+    a.ja("out")
+    a.label("l3"); a.mov(R1, R6); a.call(H_L3); a.ja("out")
+    a.label("l4"); a.mov(R1, R6); a.call(H_L4)
+    a.label("out"); a.movi(R0, 0); a.exit()
+    return a
+
+
+def gen_csum(n=6000):
+    from oracle.bpfasm import prog_test_run_out
+    s = synth.Stream(0xC1A0F004)
+    fd = prog_load(PROG_SCHED_CLS, csum_prog().assemble())
+    base = synth.ipv4_frames(np.array([0x0A000001], np.uint32), np.array([0x0A000002], np.uint32),
+                             np.array([6], np.uint8), np.array([1234]), np.array([80]), np.array([0x10]),
+                             np.array([64]))[0]
+    fin = np.zeros((n, CSUM_FRAME), np.uint8)
+    fout = np.zeros((n, CSUM_FRAME), np.uint8)
+    edge = np.array([0x0000, 0xFFFF, 0x0001, 0xFFFE, 0x8000, 0x7FFF], np.uint32)
+    for i in range(n):
+        f = np.zeros(CSUM_FRAME, np.uint8)
+        f[:64] = base
+        op = int(s.choice(1, 3)[0])
+        r = s.u32(6)
+        ck = int(edge[r[0] % len(edge)]) if r[1] % 4 == 0 else int(r[2] & 0xFFFF)
+        if op == 0:
+            off, size = 24, int([0, 2, 4][r[3] % 3])
+            flags = size
+        elif op == 1:
+            udp = r[3] % 2 == 1
+            off = 40 if udp else 50
+            f[23] = 17 if udp else 6
+            size = int([0, 2, 4][(r[3] >> 1) % 3])
+            flags = size | (0x10 if (r[3] >> 3) & 1 else 0) | (0x20 if udp and (r[3] >> 4) & 1 else 0)
+            if udp and (r[3] >> 5) % 4 == 0:
+                ck = 0                                    # UDP without checksum
+        else:
+            off, flags = 0, int(edge[r[4] % len(edge)] * 0x10001) if r[5] % 4 == 0 else int(r[4])
+        frm, to = int(r[4]), int(r[5])
+        if op != 2 and (flags & 0xF) == 2:
+            frm, to = frm & 0xFFFF, to & 0xFFFF
+        if op != 2 and (flags & 0xF) == 0:
+            frm = 0
+        if op != 2:
+            f[off:off + 2] = np.frombuffer(struct.pack(">H", ck), np.uint8)
+        f[64:84] = np.frombuffer(struct.pack("<IIIII", op, off, frm, to, flags & 0xFFFFFFFF), np.uint8)
+        _, out = prog_test_run_out(fd, f.tobytes())
+        fin[i] = f
+        fout[i] = np.frombuffer(out[:CSUM_FRAME], np.uint8)
+    os.close(fd)
+    np.savez_compressed(os.path.join(GOLDEN, "csum_kernel.npz"), frames_in=fin, frames_out=fout)
+    print("csum helpers:", n, "cases;", int((fin != fout).any(axis=1).sum()), "changed frames")
+
+
 if __name__ == "__main__":
     os.makedirs(GOLDEN, exist_ok=True)
-    gen_map_semantics()
-    gen_config1()
-    gen_config2()
+    which = sys.argv[1:] or ["maps", "config1", "config2", "csum"]
+    if "maps" in which:
+        gen_map_semantics()
+    if "config1" in which:
+        gen_config1()
+    if "config2" in which:
+        gen_config2()
+    if "csum" in which:
+        gen_csum()

@@ -59,7 +59,8 @@ def lib():
         L.or_netdev_ingress.argtypes = [vp, vp, u32, vp, vp, u32, u32, i32, vp]
         L.or_ct_create4.argtypes = [vp, vp, u32, i32, vp, u32]
         L.or_dp_endpoint_config.argtypes = [vp, u32, u32, vp, vp, vp, vp]
-        L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp]
+        L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp, vp]
+        L.or_csum_apply.argtypes = [vp, u32, u32, u32, u32, u32, u32, vp]
         L.or_lxc_egress.argtypes = [vp, vp, u32, vp, vp, u32, vp, u32, u32, vp]
         L.or_dp_notify_attach.argtypes = [vp, vp, u32]
         L.or_dp_notify_count.restype = u32
@@ -143,9 +144,12 @@ class Out:
         self.reason = np.zeros(n, np.int32)
 
     FIELDS = ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason")
+    frames_out = None          # set to an (n, stride) uint8 array to receive the rewritten frames
 
     def struct(self):
-        return (C.c_void_p * 8)(*[getattr(self, k).ctypes.data for k in self.FIELDS])
+        ptrs = [getattr(self, k).ctypes.data for k in self.FIELDS]
+        ptrs.append(None if self.frames_out is None else self.frames_out.ctypes.data)
+        return (C.c_void_p * 9)(*ptrs)
 
 
 class ODp:
@@ -182,11 +186,12 @@ class ODp:
         if r:
             raise OSError(-r, "or_dp_endpoint_config")
 
-    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=b"\0" * 16):
+    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=b"\0" * 16, host_mac=b"\0" * 6):
         """node_config.h constants; the v4 words as host-order ints (written in network order)."""
         import struct
         raw = [struct.unpack("<I", struct.pack(">I", v))[0] for v in (cluster_mask, cluster_range, loopback)]
-        lib().or_dp_node_config(self.h, *raw, C.create_string_buffer(bytes(router_ip6), 16))
+        lib().or_dp_node_config(self.h, *raw, C.create_string_buffer(bytes(router_ip6), 16),
+                                C.create_string_buffer(bytes(host_mac), 6))
 
     def notify_attach(self, capacity):
         """Record drop notifications (send_drop_notify) into a host ring."""
@@ -206,9 +211,11 @@ class ODp:
         lib().or_dp_metrics(self.h, m.ctypes.data)
         return m
 
-    def lxc_egress(self, frames, length, src_ep=None, flow_hash=None, now=0, ep0=0):
+    def lxc_egress(self, frames, length, src_ep=None, flow_hash=None, now=0, ep0=0, frames_out=False):
         n = len(length)
         out = Out(n)
+        if frames_out:
+            out.frames_out = np.zeros(np.asarray(frames).shape, np.uint8)
         frames = np.ascontiguousarray(frames, np.uint8)
         length = np.ascontiguousarray(length, np.uint32)
         src_ep = None if src_ep is None else np.ascontiguousarray(src_ep, np.uint16)
@@ -238,9 +245,11 @@ class ODp:
                                 C.byref(s))
         return out
 
-    def netdev_ingress(self, frames, length, mark=None, now=0, with_prefilter=True):
+    def netdev_ingress(self, frames, length, mark=None, now=0, with_prefilter=True, frames_out=False):
         n = len(length)
         out = Out(n)
+        if frames_out:
+            out.frames_out = np.zeros(np.asarray(frames).shape, np.uint8)
         frames = np.ascontiguousarray(frames, np.uint8)
         length = np.ascontiguousarray(length, np.uint32)
         mark = None if mark is None else np.ascontiguousarray(mark, np.uint32)
@@ -254,6 +263,15 @@ class ODp:
             lib().or_dp_free(self.h)
         except Exception:
             pass
+
+
+def csum_apply(frame, op, off, frm, to, flags):
+    """The oracle's restatement of the kernel checksum helpers on one frame (bytes):
+    returns (rc, frame after, csum_diff result)."""
+    b = np.frombuffer(bytes(frame), np.uint8).copy()
+    d = C.c_uint64(0)
+    rc = lib().or_csum_apply(b.ctypes.data, len(b), op, off, frm, to, flags, C.byref(d))
+    return rc, bytes(b), d.value
 
 
 def ref_probe():

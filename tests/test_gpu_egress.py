@@ -27,6 +27,7 @@ def run_egress(ctx, w, dev, lo, hi, now):
     f, l, _ = H.to_dev(w, dev, lo, hi)
     src, fh = H.egress_inputs(w, dev, lo, hi)
     out = H.dev_out(hi - lo, dev)
+    out["frames_out"] = torch.zeros(f.shape, dtype=torch.uint8, device=dev)
     ctx.lxc_egress(f, l, out, now, src_ep=src, flow_hash=fh)
     return H.host_out(out)
 
@@ -40,7 +41,7 @@ def same_table(pm, om, name):
 
 
 def check_egress(w, dev, batches, rounds=2):
-    from tests.test_gpu_parity import same_notifications
+    from tests.test_gpu_parity import same_frames, same_notifications
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)
     ctx.notify_attach(w.n)
@@ -51,7 +52,7 @@ def check_egress(w, dev, batches, rounds=2):
         for lo, hi in zip(cuts[:-1], cuts[1:]):
             o = run_egress(ctx, w, dev, lo, hi, now)
             ref = dp.lxc_egress(w.frames[lo:hi], w.length[lo:hi], w.extra["src_ep"][lo:hi],
-                                w.extra["flow_hash"][lo:hi], now=now)
+                                w.extra["flow_hash"][lo:hi], now=now, frames_out=True)
             for k in FIELDS:
                 bad = np.nonzero(o[k] != getattr(ref, k))[0]
                 if len(bad):
@@ -61,6 +62,7 @@ def check_egress(w, dev, batches, rounds=2):
                           "ct", o["ct"][bad[:12]], ref.ct[bad[:12]], "nl", o["nl"][bad[:12]], ref.nl[bad[:12]])
                 assert len(bad) == 0, (k, rnd, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
             assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
+            same_frames(o["frames_out"], ref.frames_out, w.frames[lo:hi])
     assert (ctx.metrics() == dp.metrics()).all()
     for name in ("ct4", "ct6", "policy"):
         same_table(pm, om, name)
@@ -163,3 +165,17 @@ def test_config5_nat_tuple_readers(dev):
     ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
     assert (ref.ct[-nr:] != 0).any(), "no crafted packet reads a NAT tuple"
     check_egress(w, dev, batches=1, rounds=1)
+
+
+def test_config5_short_l4_checksum_fields(dev):
+    """Packets whose L4 checksum field lies past the packet end (DROP_CSUM_L4 from the
+    lb4_xlate / rev-NAT checksum helpers) or past the 64-B record (E_TRUNC)."""
+    w = synth.config5(1 << 13, n_svc=200, n_ep=64, n_remote=128, family=4, seed=71)
+    s = synth.Stream(5)
+    tcp = (w.frames[:, 23] == 6) & (s.frac(w.n) < 0.3)
+    w.length[tcp] = s.randint(int(tcp.sum()), 38, 52).astype(np.uint32)      # check @50 not in the packet
+    udp = (w.frames[:, 23] == 17) & (s.frac(w.n) < 0.3)
+    w.length[udp] = s.randint(int(udp.sum()), 38, 42).astype(np.uint32)      # check @40
+    dp = check_egress(w, dev, batches=1, rounds=2)
+    ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now + 9)
+    assert (ref.ret == -154).any() or (ref.reason == -154).any()

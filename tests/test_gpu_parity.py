@@ -150,8 +150,17 @@ def test_policy_counters_across_agent_updates(dev):
 def run_ingress(ctx, w, dev, lo, hi, with_prefilter=True):
     f, l, m = H.to_dev(w, dev, lo, hi)
     out = H.dev_out(hi - lo, dev)
+    out["frames_out"] = torch.zeros(f.shape, dtype=torch.uint8, device=dev)
     ctx.netdev_ingress(f, l, out, w.now, mark=m, with_prefilter=with_prefilter)
     return H.host_out(out)
+
+
+def same_frames(got, ref, inp):
+    """The frames after the datapath's rewrites (cv_out.frames_out), byte for byte;
+    at least one frame must differ from its input (the path rewrote something)."""
+    bad = np.nonzero((got != ref).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), bad[:4], got[bad[:2]], ref[bad[:2]], inp[bad[:2]])
+    return int((ref != inp).any(axis=1).sum())
 
 
 def same_notifications(ctx, dp):
@@ -178,10 +187,11 @@ def check_ingress(w, dev, batches, with_prefilter=True):
     for lo, hi in zip(cuts[:-1], cuts[1:]):
         o = run_ingress(ctx, w, dev, lo, hi, with_prefilter)
         ref = dp.netdev_ingress(w.frames[lo:hi], w.length[lo:hi], w.mark[lo:hi], now=w.now,
-                                with_prefilter=with_prefilter)
+                                with_prefilter=with_prefilter, frames_out=True)
         for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
             bad = np.nonzero(o[k] != getattr(ref, k))[0]
             assert len(bad) == 0, (k, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+        same_frames(o["frames_out"], ref.frames_out, w.frames[lo:hi])
         assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
         drops += int((o["reason"] != 0).sum())
     assert drops > 0

@@ -151,3 +151,24 @@ def test_config2_policy_vs_kernel(golden_dir):
     for code in np.unique(g["ret"][g["ret"] < 0]):
         cnt = int((g["ret"] == code).sum())
         assert int(met[-code, 1, 0]) == cnt
+
+
+def test_checksum_helpers_vs_kernel(golden_dir):
+    """bpf_l3_csum_replace / bpf_l4_csum_replace / bpf_csum_diff as the container's
+    kernel computes them (BPF_PROG_TEST_RUN, oracle/kernel_golden.py gen_csum): the
+    arithmetic of every packet rewrite (lb4_xlate, __lb4_rev_nat, ipv4_dec_ttl)."""
+    import struct
+    from oracle.oracle import csum_apply
+    g = np.load(os.path.join(golden_dir, "csum_kernel.npz"))
+    fin, fout = g["frames_in"], g["frames_out"]
+    n = {0: 0, 1: 0, 2: 0}
+    for i in range(len(fin)):
+        op, off, frm, to, flags = struct.unpack("<IIIII", fin[i, 64:84].tobytes())
+        rc, after, diff = csum_apply(fin[i].tobytes(), op, off, frm, to, flags)
+        assert rc == 0, i
+        if op == 2:
+            assert diff == struct.unpack("<Q", fout[i, 84:92].tobytes())[0], i
+        else:
+            assert after[off:off + 2] == fout[i, off:off + 2].tobytes(), (i, op, flags)
+        n[op] += 1
+    assert min(n.values()) > 1000

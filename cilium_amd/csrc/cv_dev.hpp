@@ -1034,8 +1034,27 @@ struct Skb6 {
     uint32_t saddr[4], daddr[4];
     uint32_t len, nexthdr, hoplimit;
     int l4off;                  // ETH_HLEN + ipv6_hdrlen, or the (negative) ipv6_hdrlen error
+    uint32_t avail;             // bytes of the frame in the record
     L4Hdr h;
 };
+
+// csum_l4_offset_and_flags (csum.h:44-64) for an IPv6 packet: TCP 16, UDP 6, ICMPv6 2;
+// other protocols leave it 0 and the IPv6 rewrites (which do not test it) update the
+// field at l4_off + 0
+__device__ __forceinline__ int l4_coff6(uint32_t nexthdr)
+{
+    return nexthdr == 6 ? 16 : nexthdr == 17 ? 6 : nexthdr == 58 ? 2 : 0;
+}
+
+// the L4 checksum access of an IPv6 rewrite (lb6_xlate, __lb6_rev_nat, the rev-NAT
+// index zeroing of ipv6_policy): 0, DROP_CSUM_L4 past the packet, E_TRUNC past the record
+__device__ __forceinline__ int l4_csum_err6(const Skb6 &s)
+{
+    const uint32_t end = (uint32_t)(s.l4off + l4_coff6(s.nexthdr) + 2);
+    if (end > s.len) return DROP_CSUM_L4;
+    if (end > s.avail) return E_TRUNC;
+    return 0;
+}
 
 // ipv6_hdrlen (ipv6.h:61-98): returns the IPv6 header length or a DROP code and
 // the final next header.  The AUTH length is chosen by the type of the header that
@@ -1076,6 +1095,7 @@ __device__ __forceinline__ Skb6 skb6_from(const Rec6 &r)
     const int hl = ipv6_hdrlen(r, nh);
     s.nexthdr = nh;
     s.l4off = hl < 0 ? hl : 14 + hl;
+    s.avail = r.stride;
     if (hl >= 0) s.h = l4_read<54>(r, s.l4off);
     return s;
 }
@@ -1237,6 +1257,120 @@ __device__ __forceinline__ void frame_copy(const uint8_t *in, uint8_t *out, uint
         *reinterpret_cast<uint4 *>(out + k) = *reinterpret_cast<const uint4 *>(in + k);
 }
 
+// ------------------------------------------------------------------ output frames (IPv6)
+// lb6_xlate (lb.h:398-424), __lb6_rev_nat (lb.h:254-290), ipv6_policy's rev-NAT index
+// zeroing (bpf_lxc.c:750-766), ipv6_l3 (l3.h:30-51) and pass_to_stack's
+// ipv6_store_flowlabel (ipv6.h:245-260).  No L3 checksum; the L4 one changes by the
+// 16-byte bpf_csum_diff of the address (pinned by tests/golden/csum16_kernel.npz).
+__device__ __forceinline__ uint32_t csum_diff16(const uint32_t *from, const uint32_t *to, uint32_t seed)
+{
+    uint64_t t = seed;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { t += (uint32_t)~from[j]; t += to[j]; }
+    t = (t & 0xFFFFFFFFu) + (t >> 32);
+    uint32_t x = (uint32_t)t + (uint32_t)(t >> 32);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return (x & 0xFFFFu) + (x >> 16);
+}
+
+struct RevNat6Out {             // a __lb6_rev_nat a program applied
+    bool valid;
+    uint32_t na[4], np;
+};
+
+struct Frame6 {
+    uint32_t saddr[4], daddr[4], w0, hop, sp, dp, l4cs;
+    uint32_t smac[2], dmac[2];
+    uint32_t nexthdr;
+    int l4off, coff;
+    bool mm, ports, csum, smac_set, dmac_set;
+};
+
+template <int NW>
+__device__ __forceinline__ void frame6_init(Frame6 &f, const RecT<NW> &r, int l4off, uint32_t nexthdr,
+                                            const uint8_t *frame)
+{
+    f.saddr[0] = rec_raw32c<22>(r); f.saddr[1] = rec_raw32c<26>(r); f.saddr[2] = rec_raw32c<30>(r); f.saddr[3] = rec_raw32c<34>(r);
+    f.daddr[0] = rec_raw32c<38>(r); f.daddr[1] = rec_raw32c<42>(r); f.daddr[2] = rec_raw32c<46>(r); f.daddr[3] = rec_raw32c<50>(r);
+    f.w0 = rec_raw32c<14>(r);
+    f.hop = rec_u8c<21>(r);
+    f.nexthdr = nexthdr;
+    f.l4off = l4off;
+    f.coff = l4_coff6(nexthdr);
+    f.mm = nexthdr == 17;
+    const uint32_t lim = r.len < r.stride ? r.len : r.stride;
+    f.ports = l4off >= 0 && (uint32_t)l4off + 4 <= lim;
+    f.sp = f.ports ? (uint32_t)frame[l4off] | (uint32_t)frame[l4off + 1] << 8 : 0u;
+    f.dp = f.ports ? (uint32_t)frame[l4off + 2] | (uint32_t)frame[l4off + 3] << 8 : 0u;
+    const int co = l4off + f.coff;
+    f.csum = l4off >= 0 && (uint32_t)co + 2 <= lim;
+    f.l4cs = f.csum ? ((uint32_t)frame[co] | (uint32_t)frame[co + 1] << 8) : 0u;
+    f.smac_set = f.dmac_set = false;
+}
+
+// lb6_xlate: daddr, the L4 checksum by the address diff, then l4_modify_port(TCP_DPORT_OFF)
+__device__ __forceinline__ void frame6_xlate(Frame6 &f, const uint32_t *target, bool port_rw, uint32_t key_dport,
+                                             uint32_t new_port)
+{
+    f.l4cs = l4_replace(f.l4cs, 0, csum_diff16(f.daddr, target, 0), 0, f.mm);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.daddr[j] = target[j];
+    if (port_rw) { f.l4cs = l4_replace(f.l4cs, key_dport, new_port, 2, f.mm); f.dp = new_port; }
+}
+
+// __lb6_rev_nat(flags 0): reverse_map_l4_port, then the packet's saddr and its diff
+__device__ __forceinline__ void frame6_revnat(Frame6 &f, const RevNat6Out &rn)
+{
+    if (rn.np && (f.nexthdr == 6 || f.nexthdr == 17) && rn.np != f.sp) {
+        f.l4cs = l4_replace(f.l4cs, f.sp, rn.np, 2, f.mm);
+        f.sp = rn.np;
+    }
+    f.l4cs = l4_replace(f.l4cs, 0, csum_diff16(f.saddr, rn.na, 0), 0, f.mm);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.saddr[j] = rn.na[j];
+}
+
+// ipv6_policy: rev_nat_index = the low 16 bits of daddr word 3, zeroed in the packet,
+// checksum by csum_diff(&rev_nat_index, 4, &zero, 4, 0) when the L4 has a checksum offset
+__device__ __forceinline__ void frame6_zero_revnat(Frame6 &f)
+{
+    const uint32_t rni = f.daddr[3] & 0xFFFFu;
+    if (!rni) return;
+    f.daddr[3] &= ~0xFFFFu;
+    if (f.coff) f.l4cs = l4_replace(f.l4cs, 0, csum_diff4(rni, 0u, 0u), 0, f.mm);
+}
+
+// ipv6_l3: ipv6_dec_hoplimit, then the MACs (smac optional)
+__device__ __forceinline__ void frame6_l3(Frame6 &f, const uint32_t *smac, const uint32_t *dmac)
+{
+    f.hop = (f.hop - 1) & 0xFFu;
+    if (smac) { f.smac[0] = smac[0]; f.smac[1] = smac[1]; f.smac_set = true; }
+    f.dmac[0] = dmac[0]; f.dmac[1] = dmac[1]; f.dmac_set = true;
+}
+
+// ipv6_store_flowlabel(SECLABEL_NB = htonl(identity)): version 6 | the packet's traffic
+// class | the label (memory-order word)
+__device__ __forceinline__ void frame6_flowlabel(Frame6 &f, uint32_t seclabel)
+{
+    f.w0 = 0x60u | bswap32(seclabel) | (f.w0 & 0x0000F00Fu);
+}
+
+__device__ __forceinline__ void frame6_emit(const Frame6 &f, const uint8_t *in, uint8_t *out, uint32_t stride)
+{
+    for (uint32_t k = 0; k < stride; k += 16)
+        *reinterpret_cast<uint4 *>(out + k) = *reinterpret_cast<const uint4 *>(in + k);
+    auto put16 = [&](int off, uint32_t v) { out[off] = (uint8_t)v; out[off + 1] = (uint8_t)(v >> 8); };
+    auto put32 = [&](int off, uint32_t v) { put16(off, v & 0xFFFFu); put16(off + 2, v >> 16); };
+    if (f.dmac_set) { put32(0, f.dmac[0]); put16(4, f.dmac[1]); }
+    if (f.smac_set) { put32(6, f.smac[0]); put16(10, f.smac[1]); }
+    put32(14, f.w0);
+    out[21] = (uint8_t)f.hop;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { put32(22 + 4 * j, f.saddr[j]); put32(38 + 4 * j, f.daddr[j]); }
+    if (f.ports) { put16(f.l4off, f.sp); put16(f.l4off + 2, f.dp); }
+    if (f.csum) put16(f.l4off + f.coff, f.l4cs);        // after the ports: ICMPv6's field is bytes 2-3
+}
+
 // ------------------------------------------------------------------ endpoint ingress programs
 // ipv4_policy (bpf_lxc.c:865-979) + tail_ipv4_policy (:981-993), LXC_NAT46 off.
 // Returns the final verdict (TC_ACT_*, drops accounted as METRIC_INGRESS) or E_TRUNC.
@@ -1303,7 +1437,8 @@ __device__ __forceinline__ bool eq4(const uint32_t *a, const uint32_t *b)
 // ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862)
 __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m)
+                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m,
+                                           RevNat6Out *rn = nullptr)
 {
     int ret;
     int verdict;
@@ -1318,6 +1453,10 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
     t.nexthdr = s.nexthdr;
     t.dport = t.sport = 0;
     sn.rev_nat = s.daddr[3] & 0xFFFFu;                           // derive reverse NAT index (:750-766)
+    if (sn.rev_nat && l4_coff6(t.nexthdr)) {                     // zeroed in the packet: L4 checksum
+        const int c = l4_csum_err6(s);
+        if (c) { ret = c; goto drop; }
+    }
     ret = ct_lookup<true>(ep.ct6, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a);
     if (ret < 0) goto drop;
     ct_out = (uint8_t)ret;
@@ -1326,6 +1465,9 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
         if (revnat6(p, st.rev_nat, na, np, a)) {
             const int r2 = rev_map_port(s.h, t.nexthdr, np);
             if (r2) { ret = r2; goto drop; }
+            const int r3 = l4_csum_err6(s);                       // __lb6_rev_nat checksum update
+            if (r3) { ret = r3; goto drop; }
+            if (rn) { rn->valid = true; rn->np = np; for (int j = 0; j < 4; ++j) rn->na[j] = na[j]; }
         }
     }
     verdict = policy_ingress<true>(ep.policy, p.flags | (p.ablate << 16), s.len, src_label, t.dport, t.nexthdr, a);
@@ -1372,11 +1514,11 @@ __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep
 
 __device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                               uint32_t ifindex, uint32_t now, uint8_t &ct_out, uint16_t &proxy,
-                                              int32_t &reason, Acct &a, Met &m)
+                                              int32_t &reason, Acct &a, Met &m, RevNat6Out *rn = nullptr)
 {
     int ret;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, false, ifindex, now, ct_out, proxy, reason, a, m);
+    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, false, ifindex, now, ct_out, proxy, reason, a, m, rn);
     else ret = DROP_MISSED_TAIL_CALL;
     m.drop(ret, s.len, METRIC_INGRESS);
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);

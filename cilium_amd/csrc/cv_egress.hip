@@ -424,6 +424,10 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         const uint32_t sport_svc = v[4] & 0xFFFFu;
         st.rev_nat = v[5] & 0xFFFFu;
         uint32_t flags = STAGE_CT | EG_V6 | EG_SVC;
+        {                                                         // lb6_xlate: the L4 checksum update by
+            const int c = l4_csum_err6(s);                        // diff (any offset, ICMP's too)
+            if (c) { ret = c; goto fin; }
+        }
         uint32_t ndport = 0;
         if (sport_svc && key_dport != sport_svc && (t.nexthdr == 6 || t.nexthdr == 17)) {
             if (s.h.c2b) { ret = chk_err(s.h.c2b, DROP_WRITE_ERROR); goto fin; }
@@ -776,6 +780,39 @@ drop:
     eg_final(o, i, res, a);
 }
 
+// The forwarded IPv6 frame of ipv6_l3_from_lxc: lb6_xlate (the LB stage's target and
+// port from the scratch words), the egress reverse NAT, then ipv6_l3 of the exit taken
+// (kind 0 pass_to_stack: dmac NODE_MAC + ipv6_store_flowlabel; 1 to_host: NODE_MAC ->
+// HOST_IFINDEX_MAC; 2 ipv6_local_delivery: the endpoint's node_mac -> mac, then the
+// destination's ipv6_policy: rev-NAT index zeroing and reverse NAT).
+__device__ __noinline__ void eg6_frame(const DpParams &p, const BatchDev &b, const OutDev &o, const uint32_t *eg,
+                                       uint32_t i, const EpDev &ep, const RevNat6Out &rn1, int kind, int64_t lxc_slot,
+                                       const RevNat6Out &rn2)
+{
+    Rec6 r;
+    rec_load(r, b, i, 8);
+    const uint8_t *in = b.frames + (size_t)i * b.stride;
+    uint32_t nh = rec_u8c<20>(r);
+    const int hl = ipv6_hdrlen(r, nh);
+    Frame6 f;
+    frame6_init(f, r, hl < 0 ? hl : 14 + hl, nh, in);
+    if (eg[0] & EG_SVC) frame6_xlate(f, eg + 12, eg[0] & EG_DPORT_RW, eg[2] & 0xFFFFu, eg[2] >> 16);
+    if (rn1.valid) frame6_revnat(f, rn1);
+    if (kind == 0) {
+        frame6_l3(f, nullptr, ep.node_mac);
+        frame6_flowlabel(f, ep.seclabel);
+    } else if (kind == 1) {
+        frame6_l3(f, ep.node_mac, p.host_mac);
+    } else {
+        uint32_t mac[2], nmac[2];
+        lxc_macs(p.lxc6, lxc_slot, mac, nmac);
+        frame6_l3(f, nmac, mac);
+        frame6_zero_revnat(f);
+        if (rn2.valid) frame6_revnat(f, rn2);
+    }
+    frame6_emit(f, in, o.frames + (size_t)i * b.stride, b.stride);
+}
+
 // ipv6_l3_from_lxc (bpf_lxc.c:133-352) from skip_service_lookup on
 __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
                                             const GroupScratch &g, uint32_t i, Met &m)
@@ -804,6 +841,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     uint32_t iv;
     bool lxc_hit = false;
     int64_t lxc_slot = -1;
+    RevNat6Out rn1, rn2;                                          // reverse NATs applied (output frames)
+    rn1.valid = rn2.valid = false;
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     {
@@ -826,8 +865,12 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         if (revnat6(p, st.rev_nat, na, np, a)) {
             const int r2 = rev_map_port(s.h, t.nexthdr, np);
             if (r2) { ret = r2; goto drop; }
+            const int r3 = l4_csum_err6(s);                       // __lb6_rev_nat checksum update
+            if (r3) { ret = r3; goto drop; }
+            rn1.valid = true;
+            rn1.np = np;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s.saddr[j] = na[j];
+            for (int j = 0; j < 4; ++j) { s.saddr[j] = na[j]; rn1.na[j] = na[j]; }
         }
     }
     if (verdict > 0) {                                            // ipv6_redirect_to_host_port + ipv6_l3
@@ -845,18 +888,26 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     if (lxc_hit) {
         if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
         m.fwd(s.len, METRIC_EGRESS);
-        if (iv & (1u << 16)) { res.ret = TC_ACT_REDIRECT; eg_final(o, i, res, a); return; }
+        if (iv & (1u << 16)) {                                    // to_host
+            res.ret = TC_ACT_REDIRECT;
+            if (o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+            eg_final(o, i, res, a);
+            return;
+        }
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
         res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, lxc_ifindex(p.lxc6, lxc_slot, iv), now, ct2,
-                                 res.proxy, res.reason, a, m);
+                                 res.proxy, res.reason, a, m, &rn2);
+        if (o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
+            eg6_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv6_local_delivery
         eg_final(o, i, res, a);
         return;
     }
     if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
     m.fwd(s.len, METRIC_EGRESS);
     res.ret = TC_ACT_OK;
+    if (o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
     return;
 drop:

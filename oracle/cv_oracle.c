@@ -782,15 +782,15 @@ static void skb_init(or_skb *s, const uint8_t *f, uint32_t stride, uint32_t len)
 static inline int sld(const or_skb *s, int off, uint32_t n, void *to) { return ld(s->b, s->avail, s->len, off, n, to); }
 
 /* out->frames_out of packet i: the rewritten frame of a forwarded (TC_ACT_OK / REDIRECT,
- * not to the L7 proxy) IPv4 packet, else the input frame (IPv6 rewrites: a later row) */
+ * not to the L7 proxy) IPv4 or IPv6 packet, else the input frame */
 static void emit_frame(const or_out *out, uint32_t i, const uint8_t *in, uint32_t stride, const or_skb *s,
                        int32_t ret, uint16_t proxy)
 {
     if (!out->frames_out) return;
     uint8_t *o = out->frames_out + (size_t)i * stride;
     memcpy(o, in, stride);
-    const int v4 = stride >= 14 && in[12] == 0x08 && in[13] == 0x00;
-    if (v4 && (ret == OR_TC_ACT_OK || ret == OR_TC_ACT_REDIRECT) && !proxy) memcpy(o, s->b, s->avail);
+    const int ip = stride >= 14 && ((in[12] == 0x08 && in[13] == 0x00) || (in[12] == 0x86 && in[13] == 0xDD));
+    if (ip && (ret == OR_TC_ACT_OK || ret == OR_TC_ACT_REDIRECT) && !proxy) memcpy(o, s->b, s->avail);
 }
 
 /* skb_store_bytes: 0, 1 (beyond len: the helper fails) or OR_E_TRUNC */
@@ -828,6 +828,24 @@ static uint32_t csum_diff4(uint32_t from, uint32_t to, uint32_t seed)
     if (t < (uint64_t)seed) t++;                           /* addq + adcq $0 */
     uint64_t r = (t >> 32) + (t & 0xFFFFFFFFu);            /* add32_with_carry */
     uint32_t x = (uint32_t)r + (uint32_t)(r >> 32);
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return x;
+}
+
+/* bpf_csum_diff(from, 16, to, 16, seed) (the IPv6 address rewrites): the folded
+ * ones-complement sum of seed, the complemented from words and the to words */
+static uint32_t csum_diff16(const uint8_t *from, const uint8_t *to, uint32_t seed)
+{
+    uint64_t t = seed;
+    for (int k = 0; k < 4; k++) {
+        uint32_t f, g;
+        memcpy(&f, from + 4 * k, 4); memcpy(&g, to + 4 * k, 4);
+        t += (uint32_t)~f;
+        t += g;
+    }
+    t = (t & 0xFFFFFFFFu) + (t >> 32);
+    uint32_t x = (uint32_t)t + (uint32_t)(t >> 32);
     x = (x & 0xFFFFu) + (x >> 16);
     x = (x & 0xFFFFu) + (x >> 16);
     return x;
@@ -893,11 +911,9 @@ static int l4_modify_port(or_skb *s, int l4_off, int port_off, uint8_t nexthdr, 
 {
     int coff; uint32_t cfl;
     l4_csum_off(nexthdr, &coff, &cfl);
-    if (coff) {
-        int r = l4_csum_replace(s, l4_off + coff, old_port, port, cfl | 2);
-        if (r) return csum_err(r, OR_DROP_CSUM_L4);
-    }
-    int r = sst(s, l4_off + port_off, 2, &port);
+    int r = l4_csum_replace(s, l4_off + coff, old_port, port, cfl | 2);   /* csum_l4_replace: any offset */
+    if (r) return csum_err(r, OR_DROP_CSUM_L4);
+    r = sst(s, l4_off + port_off, 2, &port);
     return r ? csum_err(r, OR_DROP_WRITE_ERROR) : 0;
 }
 
@@ -1320,13 +1336,6 @@ static int extract_l4_port(const or_skb *skb, uint8_t nexthdr, int l4_off, uint1
     }
 }
 
-/* l4_modify_port (l4.h:50-60) of the destination port; checksum not modelled */
-static int l4_store_dport(or_skb *skb, int l4_off, uint16_t port)
-{
-    int r = sst(skb, l4_off + TCP_DPORT_OFF, 2, &port);
-    return r == OR_E_TRUNC ? r : r ? OR_DROP_WRITE_ERROR : 0;
-}
-
 /* lb4_local (lb.h:700-775) + lb4_xlate (:653-697) */
 static int lb4_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb4_key *key, or_ipv4_ct_tuple *t,
                      or_lb4_service *svc, or_ct_state *st, uint32_t saddr, uint32_t hash, uint32_t now, pkt_state *ps)
@@ -1630,7 +1639,8 @@ static int ct_create6(or_map *ct, const or_ipv6_ct_tuple *t, uint32_t skb_len, i
 }
 
 /* lb6_rev_nat / __lb6_rev_nat (lb.h:254-315), flags = 0 on every caller here:
- * rewrites the source address (and port) of the packet */
+ * rewrites the source address (and port) of the packet, then the L4 checksum by
+ * the 16-byte diff (csum_l4_replace at the nexthdr's offset, 0 for unknown L4) */
 static int lb6_rev_nat(or_dp *dp, or_skb *skb, int l4_off, uint16_t index, const or_ipv6_ct_tuple *t, uint8_t *nl)
 {
     if (!dp->lb6_revnat) return 0;
@@ -1643,9 +1653,8 @@ static int lb6_rev_nat(or_dp *dp, or_skb *skb, int l4_off, uint16_t index, const
         case 6: case 17: {
             uint16_t old;
             if ((r = sld(skb, l4_off + TCP_SPORT_OFF, 2, &old))) return r == OR_E_TRUNC ? r : OR_E_FAULT;
-            if (nat->port != old) {
-                if ((r = sst(skb, l4_off + TCP_SPORT_OFF, 2, &nat->port))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
-            }
+            if (nat->port != old && (r = l4_modify_port(skb, l4_off, TCP_SPORT_OFF, t->nexthdr, nat->port, old)))
+                return r;
             break;
         }
         case 1: case 58: break;
@@ -1655,6 +1664,10 @@ static int lb6_rev_nat(or_dp *dp, or_skb *skb, int l4_off, uint16_t index, const
     uint8_t old[16];
     if ((r = sld(skb, ETH_HLEN + 8, 16, old))) return r == OR_E_TRUNC ? r : OR_DROP_INVALID;   /* ipv6_load_saddr */
     if ((r = sst(skb, ETH_HLEN + 8, 16, nat->address))) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    uint32_t sum = csum_diff16(old, nat->address, 0);
+    int coff; uint32_t cfl;
+    l4_csum_off(t->nexthdr, &coff, &cfl);
+    if ((r = l4_csum_replace(skb, l4_off + coff, 0, sum, cfl | OR_F_PSEUDO_HDR))) return csum_err(r, OR_DROP_CSUM_L4);
     return 0;
 }
 
@@ -1689,22 +1702,40 @@ static int lb6_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb6_key 
     t->flags = flags;
     memcpy(t->daddr, svc->target, 16);
     st->rev_nat_index = svc->rev_nat_index;
-    int r = sst(skb, ETH_HLEN + 24, 16, svc->target);              /* ipv6_store_daddr */
-    if (r) return r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR;
+    int r = sst(skb, ETH_HLEN + 24, 16, svc->target);              /* lb6_xlate: ipv6_store_daddr */
+    if (r == OR_E_TRUNC) return r;
+    int coff; uint32_t cfl;                                         /* csum_off of lb6_extract_key */
+    l4_csum_off(t->nexthdr, &coff, &cfl);
+    r = l4_csum_replace(skb, l4_off + coff, 0, csum_diff16(key->address, svc->target, 0), cfl | OR_F_PSEUDO_HDR);
+    if (r) return csum_err(r, OR_DROP_CSUM_L4);
     if (svc->port && key->dport != svc->port && (t->nexthdr == 6 || t->nexthdr == 17)) {
-        r = l4_store_dport(skb, l4_off, svc->port);
+        r = l4_modify_port(skb, l4_off, TCP_DPORT_OFF, t->nexthdr, svc->port, key->dport);
         if (r) return r;
     }
     return OR_TC_ACT_OK;
 }
 
-/* ipv6_l3 (l3.h:30-51): hop limit <= 1 -> icmp6_send_time_exceeded tail call */
-static int ipv6_l3(or_skb *skb)
+/* ipv6_l3 (l3.h:30-51): ipv6_dec_hoplimit (ipv6.h:178-193; hop limit <= 1 ->
+ * icmp6_send_time_exceeded tail call), then the source MAC (when given) and the
+ * destination MAC */
+static int ipv6_l3(or_skb *skb, const uint8_t *smac, const uint8_t *dmac)
 {
     uint8_t hl = skb->b[21];
     if (hl <= 1) return OR_E_PUNT;
     skb->b[21] = (uint8_t)(hl - 1);
+    if (smac && sst(skb, 6, 6, smac)) return OR_DROP_WRITE_ERROR;
+    if (sst(skb, 0, 6, dmac)) return OR_DROP_WRITE_ERROR;
     return OR_TC_ACT_OK;
+}
+
+/* ipv6_store_flowlabel (ipv6.h:245-260) of pass_to_stack: version 6, the packet's
+ * traffic class, flow label |= SECLABEL_NB (pkg/endpoint/bpf.go:174: htonl(identity)) */
+static void ipv6_store_flowlabel(or_skb *skb, uint32_t seclabel)
+{
+    uint32_t w; memcpy(&w, skb->b + ETH_HLEN, 4);
+    const uint32_t label = __builtin_bswap32(seclabel);
+    w = __builtin_bswap32(0x60000000u) | label | (w & __builtin_bswap32(0x0FF00000u));
+    memcpy(skb->b + ETH_HLEN, &w, 4);
 }
 
 /* ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862) */
@@ -1728,6 +1759,13 @@ static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
         w3 &= ~0xFFFFu;
         int r = sst(skb, ETH_HLEN + 24 + 12, 4, &w3);
         if (r) { ret = r == OR_E_TRUNC ? r : OR_DROP_WRITE_ERROR; goto drop; }
+        int coff; uint32_t cfl;                     /* csum_diff(&rev_nat_index, 4, &zero, 4, 0) */
+        l4_csum_off(t.nexthdr, &coff, &cfl);
+        if (coff && (r = l4_csum_replace(skb, l4_off + coff, 0, csum_diff4(st_new.rev_nat_index, 0, 0),
+                                         cfl | OR_F_PSEUDO_HDR))) {
+            ret = csum_err(r, OR_DROP_CSUM_L4);
+            goto drop;
+        }
     }
     ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_INGRESS, &st, now, dp->flags, &ps->nl, &ps->nu);
     if (ret < 0) goto drop;
@@ -1844,13 +1882,15 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     }
     if (verdict > 0) {
         ps->proxy = (uint16_t)verdict;                              /* ipv6_redirect_to_host_port */
-        int r = ipv6_l3(skb);
+        int r = ipv6_l3(skb, ep->node_mac, dp->host_mac);
         if (r != OR_TC_ACT_OK) return r;
         return OR_TC_ACT_REDIRECT;
     }
     or_endpoint_info *dep = lookup_ip6_endpoint(dp, skb->b + 38, &ps->nl);
     if (dep) {
-        int r = ipv6_l3(skb);
+        /* to_host: ipv6_l3(NODE_MAC, HOST_IFINDEX_MAC); local: ipv6_local_delivery (l3.h:
+         * 71-101) ipv6_l3(endpoint_info.node_mac, endpoint_info.mac) */
+        int r = (dep->flags & 1) ? ipv6_l3(skb, ep->node_mac, dp->host_mac) : ipv6_l3(skb, dep->node_mac, dep->mac);
         if (r != OR_TC_ACT_OK) return r;
         update_metrics(dp, len, 2, 0);
         if (dep->flags & 1) return OR_TC_ACT_REDIRECT;
@@ -1862,8 +1902,9 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         ps->ct = ct_egress;
         return r;
     }
-    int r = ipv6_l3(skb);                                           /* pass_to_stack */
+    int r = ipv6_l3(skb, NULL, ep->node_mac);                       /* pass_to_stack */
     if (r != OR_TC_ACT_OK) return r;
+    ipv6_store_flowlabel(skb, ep->seclabel);
     update_metrics(dp, len, 2, 0);
     return OR_TC_ACT_OK;
 }
@@ -1947,11 +1988,13 @@ uint32_t or_ct_gc(or_map *m, uint32_t time)
 }
 
 /* known-answer access to the checksum restatement (tests/test_oracle_golden.py):
- * op 0 l3_csum_replace, 1 l4_csum_replace on frame[0..len), 2 csum_diff4 -> *diff */
+ * op 0 l3_csum_replace, 1 l4_csum_replace on frame[0..len), 2 csum_diff4 -> *diff,
+ * 3 csum_diff16(frame[0..16), frame[16..32), seed = flags) -> *diff */
 int or_csum_apply(uint8_t *frame, uint32_t len, uint32_t op, uint32_t off, uint32_t from, uint32_t to,
                   uint32_t flags, uint64_t *diff)
 {
     if (op == 2) { *diff = csum_diff4(from, to, flags); return 0; }
+    if (op == 3) { *diff = csum_diff16(frame, frame + 16, flags); return 0; }   /* frame = from16 | to16 */
     or_skb s;
     skb_init(&s, frame, len, len);
     int r = op == 0 ? l3_csum_replace(&s, (int)off, from, to, (int)(flags & 0xF))

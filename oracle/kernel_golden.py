@@ -457,9 +457,66 @@ def gen_csum(n=6000):
     print("csum helpers:", n, "cases;", int((fin != fout).any(axis=1).sum()), "changed frames")
 
 
+CSUM16_FRAME = 112       # from16 @64, to16 @80, seed @96, csum_diff result @104
+
+
+def csum16_prog():
+    """csum_diff(from16, 16, to16, 16, seed) -> u64 stored @104: the sum of the IPv6
+    address rewrites (lb6_xlate lb.h:405, __lb6_rev_nat lb.h:289)."""
+    a = Asm()
+    a.mov(R6, R1)
+    a.mov(R1, R6); a.movi(R2, 64); a.mov(R3, FP); a.addi(R3, -48); a.movi(R4, 36); a.call(H_LOAD)
+    a.jnei(R0, 0, "out")
+    a.ldxw(R5, FP, -16)
+    a.mov(R1, FP); a.addi(R1, -48); a.movi(R2, 16); a.mov(R3, FP); a.addi(R3, -32); a.movi(R4, 16)
+    a.call(H_DIFF)
+    a.stxw(FP, -8, R0)
+    a.rshi(R0, 32)
+    a.stxw(FP, -4, R0)
+    a.mov(R1, R6); a.movi(R2, 104); a.mov(R3, FP); a.addi(R3, -8); a.movi(R4, 8); a.movi(R5, 0); a.call(H_STORE)
+    a.label("out"); a.movi(R0, 0); a.exit()
+    return a
+
+
+def gen_csum16(n=4000):
+    """Golden vectors of the 16-byte bpf_csum_diff: random addresses and seeds, plus
+    edge words (all-zero, all-ones, equal from/to, single-bit differences)."""
+    from oracle.bpfasm import prog_test_run_out
+    s = synth.Stream(0xC1A0F016)
+    fd = prog_load(PROG_SCHED_CLS, csum16_prog().assemble())
+    fin = np.zeros((n, CSUM16_FRAME), np.uint8)
+    fout = np.zeros((n, CSUM16_FRAME), np.uint8)
+    edge = np.array([0, 0xFFFFFFFF, 1, 0xFFFF, 0xFFFF0000, 0x80000000], np.uint32)
+    for i in range(n):
+        f = np.zeros(CSUM16_FRAME, np.uint8)
+        f[12:14] = (0x86, 0xDD)
+        r = s.u32(12)
+        words = r[:8].copy()
+        kind = int(r[8] % 6)
+        if kind == 1:
+            words[:] = edge[r[9] % len(edge)]
+        elif kind == 2:
+            words[4:] = words[:4]                                  # from == to
+        elif kind == 3:
+            words[4:] = words[:4] ^ np.uint32(1 << int(r[9] % 32))   # one bit differs
+        elif kind == 4:
+            words[:4] = edge[r[9] % len(edge)]
+            words[4:] = edge[r[10] % len(edge)]
+        seed = int(edge[r[11] % len(edge)]) if r[10] % 4 == 0 else int(r[11])
+        f[64:100] = np.frombuffer(struct.pack("<8I", *[int(w) for w in words]) + struct.pack("<I", seed), np.uint8)
+        _, out = prog_test_run_out(fd, f.tobytes())
+        fin[i] = f
+        fout[i] = np.frombuffer(out[:CSUM16_FRAME], np.uint8)
+    os.close(fd)
+    np.savez_compressed(os.path.join(GOLDEN, "csum16_kernel.npz"), frames_in=fin, frames_out=fout)
+    print("csum_diff 16:", n, "cases")
+
+
 if __name__ == "__main__":
     os.makedirs(GOLDEN, exist_ok=True)
-    which = sys.argv[1:] or ["maps", "config1", "config2", "csum"]
+    which = sys.argv[1:] or ["maps", "config1", "config2", "csum", "csum16"]
+    if "csum16" in which:
+        gen_csum16()
     if "maps" in which:
         gen_map_semantics()
     if "config1" in which:

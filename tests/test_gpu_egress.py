@@ -179,3 +179,19 @@ def test_config5_short_l4_checksum_fields(dev):
     dp = check_egress(w, dev, batches=1, rounds=2)
     ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now + 9)
     assert (ref.ret == -154).any() or (ref.reason == -154).any()
+
+
+def test_config5_v6_short_l4_checksum_fields(dev):
+    """IPv6 packets whose L4 checksum field (TCP @16, UDP @6, ICMPv6 @2 of the L4
+    header) lies past the packet end: DROP_CSUM_L4 from lb6_xlate, __lb6_rev_nat and the
+    rev-NAT index zeroing of ipv6_policy; frames of the rest byte-exact."""
+    w = synth.config5(1 << 13, n_svc=200, n_ep=64, n_remote=128, family=6, seed=73)
+    s = synth.Stream(6)
+    v6 = (w.frames[:, 12] == 0x86) & (w.frames[:, 13] == 0xDD)
+    tcp = v6 & (w.frames[:, 20] == 6) & (s.frac(w.n) < 0.3)
+    w.length[tcp] = s.randint(int(tcp.sum()), 58, 72).astype(np.uint32)      # check @70 not in the packet
+    udp = v6 & (w.frames[:, 20] == 17) & (s.frac(w.n) < 0.3)
+    w.length[udp] = s.randint(int(udp.sum()), 58, 62).astype(np.uint32)      # check @60
+    dp = check_egress(w, dev, batches=1, rounds=2)
+    ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now + 9)
+    assert (ref.ret == -154).any() or (ref.reason == -154).any()

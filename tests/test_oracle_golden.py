@@ -172,3 +172,18 @@ def test_checksum_helpers_vs_kernel(golden_dir):
             assert after[off:off + 2] == fout[i, off:off + 2].tobytes(), (i, op, flags)
         n[op] += 1
     assert min(n.values()) > 1000
+
+
+def test_csum_diff16_vs_kernel(golden_dir):
+    """bpf_csum_diff over two 16-byte IPv6 addresses as the container's kernel computes
+    it (oracle/kernel_golden.py gen_csum16): the sum of lb6_xlate and __lb6_rev_nat."""
+    import struct
+    from oracle.oracle import csum_apply
+    g = np.load(os.path.join(golden_dir, "csum16_kernel.npz"))
+    fin, fout = g["frames_in"], g["frames_out"]
+    for i in range(len(fin)):
+        seed = struct.unpack("<I", fin[i, 96:100].tobytes())[0]
+        rc, _, diff = csum_apply(fin[i, 64:96].tobytes(), 3, 0, 0, 0, seed)
+        assert rc == 0
+        assert diff == struct.unpack("<Q", fout[i, 104:112].tobytes())[0], (i, fin[i, 64:100].tobytes().hex())
+    assert len(fin) >= 4000

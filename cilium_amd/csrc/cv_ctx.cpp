@@ -169,6 +169,10 @@ struct cv_ctx {
     cv_drop_notify *notify = nullptr;
     uint32_t notify_cap = 0;
     uint32_t *notify_count = nullptr;
+    // trace notification ring (cv_trace_attach)
+    cv_trace_notify *trace = nullptr;
+    uint32_t trace_cap = 0, trace_agg = 0, ingress_ifindex = 0;
+    uint32_t *trace_count = nullptr;
 };
 
 namespace {
@@ -596,6 +600,11 @@ DpParams params(cv_ctx *c)
     p.notify = reinterpret_cast<uint32_t *>(c->notify);
     p.notify_cap = c->notify_cap;
     p.notify_count = c->notify_count;
+    p.trace = reinterpret_cast<uint32_t *>(c->trace);
+    p.trace_cap = c->trace_cap;
+    p.trace_count = c->trace_count;
+    p.trace_agg = c->trace_agg;
+    p.ingress_ifindex = c->ingress_ifindex;
     return p;
 }
 
@@ -1247,6 +1256,21 @@ int cv_notify_attach(cv_ctx *c, cv_drop_notify *records, uint32_t capacity, uint
     c->notify = records;
     c->notify_cap = records ? capacity : 0;
     c->notify_count = records ? count : nullptr;
+    return 0;
+}
+
+// the cilium_events trace stream (TRACE_NOTIFY) into caller-owned device buffers
+int cv_trace_attach(cv_ctx *c, cv_trace_notify *records, uint32_t capacity, uint32_t *count, uint32_t aggregation,
+                    uint32_t ingress_ifindex)
+{
+    if (!c || (records && !count)) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->device >= 0) (void)hipDeviceSynchronize();
+    c->trace = records;
+    c->trace_cap = records ? capacity : 0;
+    c->trace_count = records ? count : nullptr;
+    c->trace_agg = aggregation;
+    c->ingress_ifindex = ingress_ifindex;
     return 0;
 }
 

@@ -337,6 +337,27 @@ __device__ __forceinline__ void notify_drop(const DpParams &p, const Met &m, int
     *reinterpret_cast<uint2 *>(w + 8) = make_uint2(m.pkt, 0u);
 }
 
+// send_trace_notify (bpf/lib/trace.h:96-150): one cv_trace_notify record (10 words)
+// per forwarding step when a ring is attached; FROM_* points hidden at
+// MONITOR_AGGREGATION >= 1, steps without a CT report request at >= 3
+enum : uint32_t { TRACE_TO_LXC = 0, TRACE_TO_PROXY = 1, TRACE_TO_HOST = 2, TRACE_TO_STACK = 3,
+                  TRACE_FROM_LXC = 5, TRACE_FROM_PROXY = 6, TRACE_FROM_HOST = 7, TRACE_FROM_STACK = 8 };
+__device__ __forceinline__ void notify_trace(const DpParams &p, const Met &m, uint32_t obs, uint32_t len,
+                                             uint32_t source, uint32_t src, uint32_t dst, uint32_t dst_id,
+                                             uint32_t ifindex, uint32_t reason, bool monitor)
+{
+    if (!p.trace) return;
+    if (p.trace_agg >= 1 && obs >= TRACE_FROM_LXC) return;
+    if (p.trace_agg >= 3 && !monitor) return;
+    const uint32_t at = wave_append(p.trace_count, true);
+    if (at >= p.trace_cap) return;                                // lost sample (ring full)
+    uint32_t *w = p.trace + (size_t)at * 10;
+    *reinterpret_cast<uint4 *>(w) = make_uint4(4u | obs << 8 | (source & 0xFFFFu) << 16, m.hash, len,
+                                               len < 128 ? len : 128u);
+    *reinterpret_cast<uint4 *>(w + 4) = make_uint4(src, dst, (dst_id & 0xFFFFu) | (reason & 0xFFu) << 16, ifindex);
+    *reinterpret_cast<uint2 *>(w + 8) = make_uint2(m.pkt, 0u);
+}
+
 // ------------------------------------------------------------------ lookups
 struct Acct {
     uint32_t nl, nu;
@@ -699,8 +720,8 @@ __device__ __forceinline__ void ct_store(const HashTable &t, int64_t slot, const
     for (int k = 0; k < 4; ++k) q[k] = make_uint4(e.w[4 * k], e.w[4 * k + 1], e.w[4 * k + 2], e.w[4 * k + 3]);
 }
 
-// __ct_update_timeout (conntrack.h:103-161)
-__device__ __forceinline__ void ct_timeout_raw(CtE &e, uint32_t lifetime, int dir, uint32_t seen, uint32_t now)
+// __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)
+__device__ __forceinline__ bool ct_timeout_raw(CtE &e, uint32_t lifetime, int dir, uint32_t seen, uint32_t now)
 {
     e.w[8] = now + lifetime;
     const int fsh = dir == CT_INGRESS ? 24 : 16;                // rx_flags_seen @43, tx_flags_seen @42
@@ -710,18 +731,20 @@ __device__ __forceinline__ void ct_timeout_raw(CtE &e, uint32_t lifetime, int di
     if (e.w[li] + CT_REPORT_INTERVAL < now || acc != seen) {
         e.w[li] = now;
         e.w[10] = (e.w[10] & ~(0xFFu << fsh)) | (seen << fsh);
+        return true;
     }
+    return false;
 }
 
 // ct_update_timeout (conntrack.h:169-186)
-__device__ __forceinline__ void ct_timeout(CtE &e, bool tcp, int dir, uint32_t seen, uint32_t now)
+__device__ __forceinline__ bool ct_timeout(CtE &e, bool tcp, int dir, uint32_t seen, uint32_t now)
 {
     uint32_t lifetime = CT_LIFETIME_NONTCP;
     if (tcp) {
         if (!(seen & TCPF_SYN)) e.set_bits(e.bits() | CTB_SEEN_NON_SYN);
         lifetime = (e.bits() & CTB_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
     }
-    ct_timeout_raw(e, lifetime, dir, seen, now);
+    return ct_timeout_raw(e, lifetime, dir, seen, now);
 }
 
 __device__ __forceinline__ bool ct_alive(const CtE &e)
@@ -775,29 +798,36 @@ enum { ACTION_UNSPEC = 0, ACTION_CREATE = 1, ACTION_CLOSE = 2 };
 // a hit fills ct_state's rev_nat_index / loopback / slave
 // the entry update of a __ct_lookup hit (conntrack.h:213-258)
 __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
-                                       uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a);
+                                       uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a,
+                                       bool *mon = nullptr);
 
 template <class T>
 __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, int action, int dir, bool tcp,
                                              uint32_t seen, uint32_t len, uint32_t now, uint32_t flags, int64_t &slot,
-                                             CtState *st, Acct &a)
+                                             CtState *st, Acct &a, bool *mon = nullptr)
 {
     uint32_t k[T::KW];
     t.key(k);
     a.nl++;
     slot = dev_find<typename T::Spec>(ct, k, nullptr);
-    if (slot < 0) return CT_NEW;
-    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a);
+    if (slot < 0) {
+        if (mon) *mon = true;
+        return CT_NEW;
+    }
+    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
     return CT_ESTABLISHED;
 }
 
+// *mon: the `monitor` output of __ct_lookup (report requested), left as is when the
+// reference leaves it (a dead entry on a plain lookup)
 __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
-                                       uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a)
+                                       uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a, bool *mon)
 {
     a.nu++;
     CtE e;
     ct_load(ct, slot, e);
-    if (ct_alive(e)) ct_timeout(e, tcp, dir, seen, now);
+    bool m = mon ? *mon : false;
+    if (ct_alive(e)) m = ct_timeout(e, tcp, dir, seen, now);
     if (st) {
         st->rev_nat = e.w[9] >> 16;
         st->loopback = (e.bits() & CTB_LB_LOOPBACK) ? 1u : 0u;
@@ -810,12 +840,14 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
     if (action == ACTION_CREATE) {
         if ((e.bits() & CTB_RX_CLOSING) || (e.bits() & CTB_TX_CLOSING)) {
             e.set_bits(e.bits() & ~(CTB_RX_CLOSING | CTB_TX_CLOSING));
-            ct_timeout(e, tcp, dir, seen, now);
+            m = ct_timeout(e, tcp, dir, seen, now);
         }
     } else if (action == ACTION_CLOSE) {
         e.set_bits(e.bits() | (dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING));
+        m = true;
         if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
     }
+    if (mon) *mon = m;
     if (!(flags & (AB_EG_NO_CTSTORE << 16))) ct_store(ct, slot, e);
 }
 
@@ -866,7 +898,8 @@ __device__ __forceinline__ int ct_l4(T &t, const L4Hdr &h, int dir, uint32_t &se
 // first misses, as the reference's second __ct_lookup).
 template <bool V6, class T>
 __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr &h, int dir, uint32_t len,
-                                         uint32_t now, uint32_t flags, int64_t &slot, CtState *st, Acct &a)
+                                         uint32_t now, uint32_t flags, int64_t &slot, CtState *st, Acct &a,
+                                         bool *mon = nullptr)
 {
     using S = typename T::Spec;
     uint32_t seen;
@@ -874,11 +907,11 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     if (action < 0) return action;
     const bool tcp = t.nexthdr == 6;
 #ifdef CV_NO_ILP
-    int ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a);
+    int ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a, mon);
     if (ret != CT_NEW) return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
     if (dir != CT_SERVICE) {
         t.reverse();
-        ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a);
+        ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a, mon);
     }
     return ret;
 #endif
@@ -893,15 +926,16 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     a.nl++;
     slot = probe_end<S>(p1, ct, k1, nullptr);
     if (slot >= 0) {
-        ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a);
+        ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
         return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
     }
+    if (mon) *mon = true;                                         // the first __ct_lookup missed
     if (dir == CT_SERVICE) return CT_NEW;
     t = t2;
     a.nl++;
     slot = probe_end<S>(p2, ct, k2, nullptr);
     if (slot < 0) return CT_NEW;
-    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a);
+    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
     return CT_ESTABLISHED;
 }
 
@@ -1384,12 +1418,13 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
     Tuple4 t;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
+    bool mon = false;
     if (s.len < 34) { ret = DROP_INVALID; goto drop; }          // revalidate_data
     t.nexthdr = s.nexthdr;
     t.daddr = s.daddr;
     t.saddr = s.saddr;
     t.dport = t.sport = 0;
-    ret = ct_lookup<false>(ep.ct4, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a);
+    ret = ct_lookup<false>(ep.ct4, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     if (ret < 0) goto drop;
     ct_out = (uint8_t)ret;
     if (ret == CT_REPLY && st.rev_nat && !st.loopback) {         // lb4_rev_nat(REV_NAT_F_TUPLE_SADDR)
@@ -1416,10 +1451,12 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
         if (is_err(c)) { ret = c; goto drop; }
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, (uint32_t)ret, mon);
         proxy = (uint16_t)verdict;                                 // ipv4_redirect_to_host_port
         return TC_ACT_REDIRECT;                                    // redirect(HOST_IFINDEX)
     }
     m.fwd(s.len, METRIC_INGRESS);                                  // send_trace_notify(TRACE_TO_LXC)
+    notify_trace(p, m, TRACE_TO_LXC, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex, (uint32_t)ret, mon);
     return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
 drop:
     if (ret == E_TRUNC) return ret;
@@ -1446,6 +1483,7 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
     CtState st{0, 0, 0, 0, 0, 0};
     CtState sn{0, 0, 0, 0, 0, src_label};
     int64_t slot;
+    bool mon = false;
     if (s.len < 54) { ret = DROP_INVALID; goto drop; }
     if (s.l4off < 0) { ret = s.l4off; goto drop; }              // ipv6_hdrlen error
 #pragma unroll
@@ -1457,7 +1495,7 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
         const int c = l4_csum_err6(s);
         if (c) { ret = c; goto drop; }
     }
-    ret = ct_lookup<true>(ep.ct6, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a);
+    ret = ct_lookup<true>(ep.ct6, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     if (ret < 0) goto drop;
     ct_out = (uint8_t)ret;
     if (st.rev_nat) {                                            // lb6_rev_nat(.., 0)
@@ -1482,10 +1520,12 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
         if (is_err(c)) { ret = c; goto drop; }
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, (uint32_t)ret, mon);
         proxy = (uint16_t)verdict;
         return TC_ACT_REDIRECT;
     }
     m.fwd(s.len, METRIC_INGRESS);
+    notify_trace(p, m, TRACE_TO_LXC, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex, (uint32_t)ret, mon);
     return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
 drop:
     if (ret == E_TRUNC) return ret;

@@ -48,6 +48,12 @@ struct DpParams {              // by value as the kernel argument
     uint32_t *notify;
     uint32_t notify_cap;
     uint32_t *notify_count;
+    // trace notifications (cv_trace_attach): cv_trace_notify records of 10 words
+    uint32_t *trace;
+    uint32_t trace_cap;
+    uint32_t *trace_count;
+    uint32_t trace_agg;        // MONITOR_AGGREGATION
+    uint32_t ingress_ifindex;  // skb->ingress_ifindex of from_netdev
 };
 
 // ablation bits: each removes one part of the work to price it (results are wrong)

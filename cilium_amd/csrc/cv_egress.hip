@@ -222,7 +222,9 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
             res.ret = DROP_MISSED_TAIL_CALL;                      // no program for the source: nothing ran
             stage = STAGE_DONE;
         } else {
-            stage = front_one(p, p.eps[e], r, eg, res, a, m);
+            const EpDev &ep = p.eps[e];                           // handle_ingress: send_trace_notify(FROM_LXC)
+            notify_trace(p, m, TRACE_FROM_LXC, r.len, ep.lxc_id, ep.seclabel, 0, 0, 0, 0, true);
+            stage = front_one(p, ep, r, eg, res, a, m);
         }
         eg[0] |= stage;
         g.gslot[i] = NONE;
@@ -698,7 +700,8 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     const uint32_t lxc_key = s.daddr;
     Probe<LxcV4Spec> lxq;
     if (lookups && p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
-    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags | (p.ablate << 16), slot, &st, a);
+    bool mon = false;
+    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags | (p.ablate << 16), slot, &st, a, &mon);
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
@@ -737,6 +740,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         }
     }
     if (verdict > 0) {                                            // ipv4_redirect_to_host_port + ipv4_l3
+        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
         res.proxy = (uint16_t)verdict;
         if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }
         res.ret = TC_ACT_REDIRECT;
@@ -754,6 +758,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
         if (iv & (1u << 16)) {                                    // to_host
             res.ret = TC_ACT_REDIRECT;
+            notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
             if (o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
             eg_final(o, i, res, a);
             return;
@@ -771,6 +776,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }            // pass_to_stack: ipv4_l3
     m.fwd(s.len, METRIC_EGRESS);                                  // TRACE_TO_STACK
+    notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
     res.ret = TC_ACT_OK;
     if (o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
@@ -836,7 +842,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     const uint32_t orig_dip[4] = {t.daddr[0], t.daddr[1], t.daddr[2], t.daddr[3]};
     Probe<LxcV6Spec> lxq;                                         // endpoint lookup of daddr, issued early
     if (p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
-    int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a);
+    bool mon = false;
+    int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
@@ -874,6 +881,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         }
     }
     if (verdict > 0) {                                            // ipv6_redirect_to_host_port + ipv6_l3
+        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
         res.proxy = (uint16_t)verdict;
         if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
         res.ret = TC_ACT_REDIRECT;
@@ -890,6 +898,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         m.fwd(s.len, METRIC_EGRESS);
         if (iv & (1u << 16)) {                                    // to_host
             res.ret = TC_ACT_REDIRECT;
+            notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
             if (o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
             eg_final(o, i, res, a);
             return;
@@ -906,6 +915,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
     m.fwd(s.len, METRIC_EGRESS);
+    notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
     res.ret = TC_ACT_OK;
     if (o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);

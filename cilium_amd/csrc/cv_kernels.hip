@@ -248,6 +248,14 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         uint32_t identity = 0;
         if (pass && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
         ident = identity;
+        if (pass && p.trace) {                                    // from_netdev: send_trace_notify(FROM_*)
+            const uint32_t mg = (b.mark ? b.mark[i] : 0u) & 0xF00u;
+            const uint32_t obs = !(p.flags & F_FROM_HOST) ? TRACE_FROM_STACK
+                                 : (mg == 0xA00u || mg == 0xB00u) ? TRACE_FROM_PROXY : TRACE_FROM_HOST;
+            m.pkt = b.base + i;
+            m.hash = b.hash ? b.hash[i] : 0u;
+            notify_trace(p, m, obs, r.len, 0, identity, 0, 0, p.ingress_ifindex, 0, true);
+        }
         const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
         const bool v4 = pass && eth == 0x0008u && r.len >= 34;   // handle_ipv4 (bpf_netdev.c:357-453)
         const uint32_t nexthdr = rec_u8c<23>(r);

@@ -107,6 +107,7 @@ def load():
         "cv_metrics_device_ptr": (vp, [vp]),
         "cv_metrics_attach": (i32, [vp, vp]),
         "cv_notify_attach": (i32, [vp, vp, u32, vp]),
+        "cv_trace_attach": (i32, [vp, vp, u32, vp, u32, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -135,6 +136,15 @@ DROP_NOTIFY = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"), ("
                         ("len_orig", "<u4"), ("len_cap", "<u4"), ("src_label", "<u4"), ("dst_label", "<u4"),
                         ("dst_id", "<u4"), ("ifindex", "<u4"), ("packet", "<u4"), ("reserved", "<u4")])
 assert DROP_NOTIFY.itemsize == 40
+
+# struct cv_trace_notify (include/cilium_hip.h): bpf/lib/trace.h's struct trace_notify + packet index
+TRACE_NOTIFY = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"), ("hash", "<u4"),
+                         ("len_orig", "<u4"), ("len_cap", "<u4"), ("src_label", "<u4"), ("dst_label", "<u4"),
+                         ("dst_id", "<u2"), ("reason", "u1"), ("pad", "u1"), ("ifindex", "<u4"),
+                         ("packet", "<u4"), ("reserved", "<u4")])
+assert TRACE_NOTIFY.itemsize == 40
+TRACE_TO_LXC, TRACE_TO_PROXY, TRACE_TO_HOST, TRACE_TO_STACK, TRACE_TO_OVERLAY = range(5)
+TRACE_FROM_LXC, TRACE_FROM_PROXY, TRACE_FROM_HOST, TRACE_FROM_STACK, TRACE_FROM_OVERLAY = range(5, 10)
 
 
 class Map:
@@ -305,6 +315,32 @@ class Ctx:
         _check(load().cv_notify_attach(self.h, C.c_void_p(rec.data_ptr()), capacity, C.c_void_p(cnt.data_ptr())),
                "cv_notify_attach")
         return self
+
+    def trace_attach(self, capacity, aggregation=0, ingress_ifindex=0):
+        """Attach a device ring for trace notifications (cv_trace_attach) with the
+        MONITOR_AGGREGATION level; capacity 0 detaches.  Read with trace_drain()."""
+        import torch
+        if not capacity:
+            _check(load().cv_trace_attach(self.h, None, 0, None, 0, 0), "cv_trace_attach")
+            self._trace = None
+            return self
+        dev = f"cuda:{self.device}"
+        rec = torch.zeros(capacity * TRACE_NOTIFY.itemsize, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._trace = (rec, cnt, capacity)
+        _check(load().cv_trace_attach(self.h, C.c_void_p(rec.data_ptr()), capacity, C.c_void_p(cnt.data_ptr()),
+                                      aggregation, ingress_ifindex), "cv_trace_attach")
+        return self
+
+    def trace_drain(self):
+        """(records, count) of the trace ring, as notify_drain."""
+        import torch
+        rec, cnt, cap = self._trace
+        torch.cuda.synchronize(rec.device)
+        n = int(cnt.item())
+        out = rec[: min(n, cap) * TRACE_NOTIFY.itemsize].cpu().numpy().view(TRACE_NOTIFY).copy()
+        cnt.zero_()
+        return out, n
 
     def notify_drain(self):
         """(records, count): the records written since the last drain (structured

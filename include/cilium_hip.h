@@ -221,6 +221,33 @@ typedef struct cv_drop_notify {
 /* device buffers; records NULL detaches (drops are then only counted in cilium_metrics) */
 int cv_notify_attach(cv_ctx *ctx, cv_drop_notify *records, uint32_t capacity, uint32_t *count);
 
+/* ---- trace notifications: send_trace_notify (bpf/lib/trace.h:96-150, TRACE_NOTIFY on)
+ * Every forwarding step of the conntrack paths appends one record: TRACE_FROM_STACK /
+ * FROM_HOST / FROM_PROXY at from_netdev (bpf_netdev.c:478-492; ifindex = the
+ * `ingress_ifindex` given here), TRACE_FROM_LXC at from-container (bpf_lxc.c:681),
+ * TRACE_TO_LXC / TO_PROXY in ipv{4,6}_policy (:828-841, 956-971), TO_HOST / TO_STACK /
+ * TO_PROXY at the from-container exits (:243-354, 542-645).  `aggregation` is
+ * MONITOR_AGGREGATION (pkg/option/monitor.go: 0 none, 1 lowest, 2 low, 3 medium): >= 1
+ * hides the FROM_* points, >= 3 keeps only steps whose conntrack lookup asked for a
+ * report (ct_update_timeout's CT_REPORT_INTERVAL / new-flags logic, conntrack.h:103-161).
+ * Same ring semantics as cv_notify_attach. */
+typedef struct cv_trace_notify {
+    uint8_t  type;        /* CILIUM_NOTIFY_TRACE = 4 */
+    uint8_t  subtype;     /* TRACE_TO_LXC = 0 ... TRACE_FROM_OVERLAY = 9 */
+    uint16_t source;      /* EVENT_SOURCE: LXC_ID of the endpoint program, 0 for bpf_netdev */
+    uint32_t hash;
+    uint32_t len_orig, len_cap;
+    uint32_t src_label, dst_label;
+    uint16_t dst_id;
+    uint8_t  reason;      /* TRACE_REASON_* = the CT result (CT_NEW = 0 ... CT_RELATED = 3) */
+    uint8_t  pad;
+    uint32_t ifindex;
+    uint32_t packet;      /* index in the batch */
+    uint32_t reserved;
+} cv_trace_notify;
+int cv_trace_attach(cv_ctx *ctx, cv_trace_notify *records, uint32_t capacity, uint32_t *count,
+                    uint32_t aggregation, uint32_t ingress_ifindex);
+
 #ifdef __cplusplus
 }
 #endif

@@ -383,6 +383,52 @@ void or_dp_notify_attach(or_dp *dp, or_drop_notify *buf, uint32_t cap)
 
 uint32_t or_dp_notify_count(const or_dp *dp) { return dp->notify_n; }
 
+void or_dp_trace_attach(or_dp *dp, or_trace_notify *buf, uint32_t cap, uint32_t aggregation, uint32_t ingress_ifindex)
+{
+    dp->trace = buf;
+    dp->trace_cap = buf ? cap : 0;
+    dp->trace_n = 0;
+    dp->trace_agg = aggregation;
+    dp->ingress_ifindex = ingress_ifindex;
+}
+
+uint32_t or_dp_trace_count(const or_dp *dp) { return dp->trace_n; }
+
+/* observation points and aggregation levels (bpf/lib/trace.h:38-62) */
+enum { TRACE_TO_LXC, TRACE_TO_PROXY, TRACE_TO_HOST, TRACE_TO_STACK, TRACE_TO_OVERLAY,
+       TRACE_FROM_LXC, TRACE_FROM_PROXY, TRACE_FROM_HOST, TRACE_FROM_STACK, TRACE_FROM_OVERLAY };
+#define TRACE_AGGREGATE_RX 1
+#define TRACE_AGGREGATE_ACTIVE_CT 3
+
+/* send_trace_notify (bpf/lib/trace.h:96-150), TRACE_NOTIFY on (lxc_config.h:36): the
+ * cilium_events record of a forwarding step; the update_metrics half is the caller's.
+ * FROM_* points are hidden at MONITOR_AGGREGATION >= RX, and everything the CT marked
+ * as not worth a report (monitor false) at >= ACTIVE_CT. */
+static void notify_trace(or_dp *dp, uint8_t obs, uint32_t len, uint16_t source, uint32_t src, uint32_t dst,
+                         uint16_t dst_id, uint32_t ifindex, uint8_t reason, int monitor)
+{
+    if (!dp->trace) return;
+    if (dp->trace_agg >= TRACE_AGGREGATE_RX && obs >= TRACE_FROM_LXC) return;
+    if (dp->trace_agg >= TRACE_AGGREGATE_ACTIVE_CT && !monitor) return;
+    const uint32_t at = dp->trace_n++;
+    if (at >= dp->trace_cap) return;
+    or_trace_notify *m = &dp->trace[at];
+    m->type = 4;                                   /* CILIUM_NOTIFY_TRACE (common.h:209-215) */
+    m->subtype = obs;
+    m->source = source;
+    m->hash = dp->cur_hash;
+    m->len_orig = len;
+    m->len_cap = len < 128 ? len : 128;
+    m->src_label = src;
+    m->dst_label = dst;
+    m->dst_id = dst_id;
+    m->reason = reason;
+    m->pad = 0;
+    m->ifindex = ifindex;
+    m->packet = dp->cur_pkt;
+    m->reserved = 0;
+}
+
 /* send_drop_notify (bpf/lib/drop.h:94-108) -> __send_drop_notify (:50-79): the
  * cilium_events record of a drop; cb[1] = src << 16 | (dst & 0xFFFF) is split back into
  * 16-bit labels; subtype = -reason; source = EVENT_SOURCE of the program (LXC_ID in
@@ -627,13 +673,13 @@ static inline int ct_alive(const or_ct_entry *e)   /* conntrack.h:194-197 */
 /* __ct_lookup (conntrack.h:199-263) */
 static int ct_lookup_one(or_map *map, const void *t, int action, int dir, or_ct_state *st,
                          int tcp, uint8_t seen, uint32_t skb_len, uint32_t now, uint32_t flags,
-                         uint8_t *nl, uint8_t *nu)
+                         uint8_t *nl, uint8_t *nu, int *mon)
 {
     (*nl)++;
     or_ct_entry *e = or_map_lookup_ptr(map, t);
-    if (!e) return OR_CT_NEW;
+    if (!e) { *mon = 1; return OR_CT_NEW; }
     (*nu)++;
-    if (ct_alive(e)) ct_update_timeout(e, tcp, dir, seen, now);
+    if (ct_alive(e)) *mon = ct_update_timeout(e, tcp, dir, seen, now);
     if (st) {
         st->rev_nat_index = e->rev_nat_index;
         st->loopback = (e->bits & B_LB_LOOPBACK) ? 1 : 0;
@@ -647,11 +693,12 @@ static int ct_lookup_one(or_map *map, const void *t, int action, int dir, or_ct_
     case ACTION_CREATE:
         if ((e->bits & B_RX_CLOSING) + ((e->bits & B_TX_CLOSING) >> 1) >= 1) {
             e->bits &= (uint16_t)~(B_RX_CLOSING | B_TX_CLOSING);
-            ct_update_timeout(e, tcp, dir, seen, now);
+            *mon = ct_update_timeout(e, tcp, dir, seen, now);
         }
         break;
     case ACTION_CLOSE:
         if (dir == OR_CT_INGRESS) e->bits |= B_RX_CLOSING; else e->bits |= B_TX_CLOSING;
+        *mon = 1;
         if (ct_alive(e)) break;
         ct_update_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
         break;
@@ -667,9 +714,11 @@ static void ct_tuple_reverse4(or_ipv4_ct_tuple *t)
     if (t->flags & TUPLE_F_IN) t->flags &= (uint8_t)~TUPLE_F_IN; else t->flags |= TUPLE_F_IN;
 }
 
-/* ct_lookup4 (conntrack.h:442-562) */
-int or_ct_lookup4(or_map *ct, or_ipv4_ct_tuple *t, const uint8_t *f, uint32_t avail, uint32_t len,
-                  int off, int dir, or_ct_state *st, uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu)
+/* ct_lookup4 (conntrack.h:442-562); *mon = the `monitor` result of the last
+ * __ct_lookup (conntrack.h:199-263) it ran, untouched when none ran */
+static int ct_lookup4m(or_map *ct, or_ipv4_ct_tuple *t, const uint8_t *f, uint32_t avail, uint32_t len,
+                       int off, int dir, or_ct_state *st, uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu,
+                       int *mon)
 {
     int action = ACTION_UNSPEC, r;
     int tcp = t->nexthdr == 6;
@@ -720,14 +769,21 @@ int or_ct_lookup4(or_map *ct, or_ipv4_ct_tuple *t, const uint8_t *f, uint32_t av
         return OR_DROP_CT_UNKNOWN_PROTO;
     }
 
-    int ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, len, now, flags, nl, nu);
+    int ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, len, now, flags, nl, nu, mon);
     if (ret != OR_CT_NEW)
         return (t->flags & TUPLE_F_RELATED) ? OR_CT_RELATED : OR_CT_REPLY;
     if (dir != OR_CT_SERVICE) {
         ct_tuple_reverse4(t);
-        ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, len, now, flags, nl, nu);
+        ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, len, now, flags, nl, nu, mon);
     }
     return ret;
+}
+
+int or_ct_lookup4(or_map *ct, or_ipv4_ct_tuple *t, const uint8_t *f, uint32_t avail, uint32_t len,
+                  int off, int dir, or_ct_state *st, uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu)
+{
+    int mon = 0;
+    return ct_lookup4m(ct, t, f, avail, len, off, dir, st, now, flags, nl, nu, &mon);
 }
 
 /* ct_create4 (conntrack.h:663-744) */
@@ -1006,8 +1062,9 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
     t.nexthdr = f[23];
     memcpy(&t.daddr, f + 30, 4); memcpy(&t.saddr, f + 26, 4);
     int l4_off = ETH_HLEN + (f[14] & 0x0F) * 4;
-    ret = or_ct_lookup4(ep->ct4, &t, skb->b, skb->avail, len, l4_off, OR_CT_INGRESS, &st, now, dp->flags,
-                        &ps->nl, &ps->nu);
+    int mon = 0;                                      /* bool monitor = false */
+    ret = ct_lookup4m(ep->ct4, &t, skb->b, skb->avail, len, l4_off, OR_CT_INGRESS, &st, now, dp->flags,
+                      &ps->nl, &ps->nu, &mon);
     if (ret < 0) goto drop;
     ps->ct = (uint8_t)ret;
     if (ret == OR_CT_REPLY && st.rev_nat_index && !st.loopback) {     /* :904-913 */
@@ -1034,10 +1091,13 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
     if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
         /* ipv4_redirect_to_host_port (lib/lxc.h:97-142): rewrite + proxy-map insert
          * (L7 side effect, out of scope); the verdict redirects to HOST_IFINDEX. */
+        notify_trace(dp, TRACE_TO_PROXY, len, ep->lxc_id, ep->seclabel, 0, 0, HOST_IFINDEX, (uint8_t)ret, mon);
         ps->proxy = (uint16_t)verdict;
         ifindex = HOST_IFINDEX;
     } else {
         update_metrics(dp, len, 1, 0);                /* send_trace_notify(TRACE_TO_LXC) */
+        notify_trace(dp, TRACE_TO_LXC, len, ep->lxc_id, src_label, ep->seclabel, ep->lxc_id, ifindex,
+                     (uint8_t)ret, mon);
     }
     if (ifindex) return OR_TC_ACT_REDIRECT;           /* redirect(ifindex, 0) */
     return OR_TC_ACT_OK;
@@ -1145,7 +1205,14 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
         if (xv == OR_XDP_PASS) {
             /* from_netdev (bpf_netdev.c:470-524) */
             uint32_t identity = 0; int skip_proxy = 0;
-            if (dp->flags & OR_F_FROM_HOST) identity = identity_from_mark(mark ? mark[i] : 0, &skip_proxy);
+            if (dp->flags & OR_F_FROM_HOST) {
+                const uint32_t magic = (mark ? mark[i] : 0) & 0xF00;   /* from_proxy: 0xA00 / 0xB00 */
+                identity = identity_from_mark(mark ? mark[i] : 0, &skip_proxy);
+                notify_trace(dp, magic == 0xA00 || magic == 0xB00 ? TRACE_FROM_PROXY : TRACE_FROM_HOST, L, 0,
+                             identity, 0, 0, dp->ingress_ifindex, 0, 1);
+            } else {
+                notify_trace(dp, TRACE_FROM_STACK, L, 0, 0, 0, 0, dp->ingress_ifindex, 0, 1);
+            }
             uint16_t proto = 0;
             if (skb.avail >= 14) memcpy(&proto, skb.b + 12, 2);      /* skb->protocol */
             ident = identity;
@@ -1446,8 +1513,9 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         }
     }
     uint32_t orig_dip = t.daddr;                                    /* skip_service_lookup: */
-    ret = or_ct_lookup4(ep->ct4, &t, skb->b, skb->avail, len, l4_off, OR_CT_EGRESS, &st, now, dp->flags,
-                        &ps->nl, &ps->nu);
+    int mon = 0;                                      /* bool monitor = false (lb4_local's is its own) */
+    ret = ct_lookup4m(ep->ct4, &t, skb->b, skb->avail, len, l4_off, OR_CT_EGRESS, &st, now, dp->flags,
+                      &ps->nl, &ps->nu, &mon);
     if (ret < 0) return ret;
     ps->ct = (uint8_t)ret;
     /* destination category (:482-494) */
@@ -1486,6 +1554,7 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     if (verdict > 0) {                                              /* redirect_to_proxy */
         /* ipv4_redirect_to_host_port: dport := proxy port, daddr := IPV4_GATEWAY,
          * proxy-map insert (L7 side effect, out of scope) */
+        notify_trace(dp, TRACE_TO_PROXY, len, ep->lxc_id, ep->seclabel, 0, 0, HOST_IFINDEX, ps->ct, mon);
         ps->proxy = (uint16_t)verdict;
         int r = ipv4_l3(skb, ep->node_mac, dp->host_mac);
         if (r != OR_TC_ACT_OK) return r;
@@ -1500,7 +1569,10 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
                                  : ipv4_l3(skb, dep->node_mac, dep->mac);
         if (r != OR_TC_ACT_OK) return r;
         update_metrics(dp, len, 2, 0);            /* to_host: TRACE_TO_HOST / ipv4_local_delivery */
-        if (dep->flags & 1) return OR_TC_ACT_REDIRECT;              /* ENDPOINT_F_HOST: redirect(HOST_IFINDEX) */
+        if (dep->flags & 1) {                                       /* ENDPOINT_F_HOST: redirect(HOST_IFINDEX) */
+            notify_trace(dp, TRACE_TO_HOST, len, ep->lxc_id, ep->seclabel, HOST_ID, 0, HOST_IFINDEX, ps->ct, mon);
+            return OR_TC_ACT_REDIRECT;
+        }
         or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;
         *final = 1;                                                 /* handle_policy -> tail_ipv4_policy */
@@ -1512,6 +1584,7 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     int r = ipv4_l3(skb, NULL, ep->node_mac);                      /* pass_to_stack */
     if (r != OR_TC_ACT_OK) return r;
     update_metrics(dp, len, 2, 0);                                  /* TRACE_TO_STACK */
+    notify_trace(dp, TRACE_TO_STACK, len, ep->lxc_id, ep->seclabel, dst, 0, 0, ps->ct, mon);
     return OR_TC_ACT_OK;
 }
 
@@ -1557,7 +1630,7 @@ static void ct_tuple_reverse6(or_ipv6_ct_tuple *t)
 
 /* ct_lookup6 (conntrack.h:286-412) */
 static int ct_lookup6(or_map *ct, or_ipv6_ct_tuple *t, const or_skb *skb, int off, int dir, or_ct_state *st,
-                      uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu)
+                      uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu, int *mon)
 {
     int action = ACTION_UNSPEC, r;
     int tcp = t->nexthdr == 6;
@@ -1606,11 +1679,11 @@ static int ct_lookup6(or_map *ct, or_ipv6_ct_tuple *t, const or_skb *skb, int of
     default:
         return OR_DROP_CT_UNKNOWN_PROTO;
     }
-    int ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, skb->len, now, flags, nl, nu);
+    int ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, skb->len, now, flags, nl, nu, mon);
     if (ret != OR_CT_NEW) return (t->flags & TUPLE_F_RELATED) ? OR_CT_RELATED : OR_CT_REPLY;
     if (dir != OR_CT_SERVICE) {
         ct_tuple_reverse6(t);
-        ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, skb->len, now, flags, nl, nu);
+        ret = ct_lookup_one(ct, t, action, dir, st, tcp, seen, skb->len, now, flags, nl, nu, mon);
     }
     return ret;
 }
@@ -1676,7 +1749,8 @@ static int lb6_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb6_key 
                      or_lb6_service *svc, or_ct_state *st, uint32_t hash, uint32_t now, pkt_state *ps)
 {
     uint8_t flags = t->flags;
-    int ret = ct_lookup6(ct, t, skb, l4_off, OR_CT_SERVICE, st, now, dp->flags, &ps->nl, &ps->nu);
+    int mon = 0;                                      /* "Deliberately ignored" (lb.h:431) */
+    int ret = ct_lookup6(ct, t, skb, l4_off, OR_CT_SERVICE, st, now, dp->flags, &ps->nl, &ps->nu, &mon);
     if (ret == OR_E_TRUNC) return ret;
     switch (ret) {
     case OR_CT_NEW:
@@ -1767,7 +1841,8 @@ static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
             goto drop;
         }
     }
-    ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_INGRESS, &st, now, dp->flags, &ps->nl, &ps->nu);
+    int mon = 0;
+    ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_INGRESS, &st, now, dp->flags, &ps->nl, &ps->nu, &mon);
     if (ret < 0) goto drop;
     ps->ct = (uint8_t)ret;
     if (st.rev_nat_index) {
@@ -1791,10 +1866,13 @@ static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
         if (IS_ERR(r)) { ret = r; goto drop; }
     }
     if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
+        notify_trace(dp, TRACE_TO_PROXY, len, ep->lxc_id, ep->seclabel, 0, 0, HOST_IFINDEX, (uint8_t)ret, mon);
         ps->proxy = (uint16_t)verdict;                /* ipv6_redirect_to_host_port */
         ifindex = HOST_IFINDEX;
     } else {
         update_metrics(dp, len, 1, 0);                /* TRACE_TO_LXC */
+        notify_trace(dp, TRACE_TO_LXC, len, ep->lxc_id, src_label, ep->seclabel, ep->lxc_id, ifindex,
+                     (uint8_t)ret, mon);
     }
     return ifindex ? OR_TC_ACT_REDIRECT : OR_TC_ACT_OK;
 drop:
@@ -1846,7 +1924,8 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         }
     }
     uint8_t orig_dip[16]; memcpy(orig_dip, t.daddr, 16);
-    ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_EGRESS, &st, now, dp->flags, &ps->nl, &ps->nu);
+    int mon = 0;
+    ret = ct_lookup6(ep->ct6, &t, skb, l4_off, OR_CT_EGRESS, &st, now, dp->flags, &ps->nl, &ps->nu, &mon);
     if (ret < 0) return ret;
     ps->ct = (uint8_t)ret;
     uint32_t dst = WORLD_ID;
@@ -1881,6 +1960,7 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         return OR_DROP_POLICY;
     }
     if (verdict > 0) {
+        notify_trace(dp, TRACE_TO_PROXY, len, ep->lxc_id, ep->seclabel, 0, 0, HOST_IFINDEX, ps->ct, mon);
         ps->proxy = (uint16_t)verdict;                              /* ipv6_redirect_to_host_port */
         int r = ipv6_l3(skb, ep->node_mac, dp->host_mac);
         if (r != OR_TC_ACT_OK) return r;
@@ -1893,7 +1973,10 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         int r = (dep->flags & 1) ? ipv6_l3(skb, ep->node_mac, dp->host_mac) : ipv6_l3(skb, dep->node_mac, dep->mac);
         if (r != OR_TC_ACT_OK) return r;
         update_metrics(dp, len, 2, 0);
-        if (dep->flags & 1) return OR_TC_ACT_REDIRECT;
+        if (dep->flags & 1) {
+            notify_trace(dp, TRACE_TO_HOST, len, ep->lxc_id, ep->seclabel, HOST_ID, 0, HOST_IFINDEX, ps->ct, mon);
+            return OR_TC_ACT_REDIRECT;
+        }
         or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;
         *final = 1;
@@ -1906,6 +1989,7 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     if (r != OR_TC_ACT_OK) return r;
     ipv6_store_flowlabel(skb, ep->seclabel);
     update_metrics(dp, len, 2, 0);
+    notify_trace(dp, TRACE_TO_STACK, len, ep->lxc_id, ep->seclabel, dst, 0, 0, ps->ct, mon);
     return OR_TC_ACT_OK;
 }
 
@@ -1917,6 +2001,7 @@ static int from_container(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t
     uint16_t proto = 0;
     if (skb->avail >= 14) memcpy(&proto, skb->b + 12, 2);           /* skb->protocol */
     int ret, final = 0;
+    notify_trace(dp, TRACE_FROM_LXC, skb->len, ep->lxc_id, ep->seclabel, 0, 0, 0, 0, 1);
     if (dp->flags & OR_F_DROP_ALL) {
         if (proto == 0x0608) return OR_E_PUNT;                      /* ARP responder */
         ret = OR_DROP_POLICY;

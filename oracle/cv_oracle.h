@@ -165,6 +165,16 @@ typedef struct {
     uint32_t hash, len_orig, len_cap, src_label, dst_label, dst_id, ifindex, packet, reserved;
 } or_drop_notify;
 
+/* struct trace_notify (bpf/lib/trace.h:72-82) + the packet's batch index */
+typedef struct {
+    uint8_t  type, subtype;
+    uint16_t source;
+    uint32_t hash, len_orig, len_cap, src_label, dst_label;
+    uint16_t dst_id;
+    uint8_t  reason, pad;
+    uint32_t ifindex, packet, reserved;
+} or_trace_notify;
+
 typedef struct or_dp {
     /* prefilter (bpf_xdp.c); NULL disables the map (filter_config.h) */
     or_map *v4_fix, *v4_dyn, *v6_fix, *v6_dyn;
@@ -184,6 +194,10 @@ typedef struct or_dp {
     /* cilium_events drop notifications (DROP_NOTIFY), when attached */
     or_drop_notify *notify;
     uint32_t notify_cap, notify_n;
+    or_trace_notify *trace;           /* send_trace_notify records (NULL: metrics only) */
+    uint32_t trace_cap, trace_n;
+    uint32_t trace_agg;               /* MONITOR_AGGREGATION (pkg/option/monitor.go levels 0-3) */
+    uint32_t ingress_ifindex;         /* skb->ingress_ifindex of from_netdev */
     uint32_t cur_pkt, cur_hash;       /* the packet being processed and its skb hash */
 } or_dp;
 
@@ -200,6 +214,11 @@ void   or_dp_metrics(const or_dp *dp, uint64_t *out /* [256][4][2] */);
 /* attach a record buffer (NULL detaches); returns and resets nothing: see or_dp_notify_count */
 void   or_dp_notify_attach(or_dp *dp, or_drop_notify *buf, uint32_t cap);
 uint32_t or_dp_notify_count(const or_dp *dp);
+/* attach a trace record buffer (NULL detaches) with the aggregation level and the
+ * netdev's ingress ifindex */
+void   or_dp_trace_attach(or_dp *dp, or_trace_notify *buf, uint32_t cap, uint32_t aggregation,
+                          uint32_t ingress_ifindex);
+uint32_t or_dp_trace_count(const or_dp *dp);
 
 /* per-packet outputs (SoA; any pointer may be NULL) */
 typedef struct {

@@ -65,6 +65,9 @@ def lib():
         L.or_dp_notify_attach.argtypes = [vp, vp, u32]
         L.or_dp_notify_count.restype = u32
         L.or_dp_notify_count.argtypes = [vp]
+        L.or_dp_trace_attach.argtypes = [vp, vp, u32, u32, u32]
+        L.or_dp_trace_count.restype = u32
+        L.or_dp_trace_count.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -199,6 +202,20 @@ class ODp:
         self._nbuf = np.zeros(max(capacity, 1), DROP_NOTIFY)
         self._ncap = capacity
         lib().or_dp_notify_attach(self.h, self._nbuf.ctypes.data if capacity else None, capacity)
+
+    def trace_attach(self, capacity, aggregation=0, ingress_ifindex=0):
+        """Record trace notifications (send_trace_notify) into a host ring."""
+        from cilium_amd.lib import TRACE_NOTIFY
+        self._tbuf = np.zeros(max(capacity, 1), TRACE_NOTIFY)
+        self._tcfg = (capacity, aggregation, ingress_ifindex)
+        lib().or_dp_trace_attach(self.h, self._tbuf.ctypes.data if capacity else None, capacity, aggregation,
+                                 ingress_ifindex)
+
+    def trace_drain(self):
+        n = lib().or_dp_trace_count(self.h)
+        out = self._tbuf[: min(n, self._tcfg[0])].copy()
+        lib().or_dp_trace_attach(self.h, self._tbuf.ctypes.data, *self._tcfg)
+        return out, n
 
     def notify_drain(self):
         n = lib().or_dp_notify_count(self.h)

@@ -40,12 +40,15 @@ def same_table(pm, om, name):
         assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all(), name
 
 
-def check_egress(w, dev, batches, rounds=2):
-    from tests.test_gpu_parity import same_frames, same_notifications
+def check_egress(w, dev, batches, rounds=2, trace_agg=0):
+    from tests.test_gpu_parity import same_frames, same_notifications, same_traces
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)
     ctx.notify_attach(w.n)
     dp.notify_attach(w.n)
+    ctx.trace_attach(3 * w.n, trace_agg)
+    dp.trace_attach(3 * w.n, trace_agg)
+    traces = []
     cuts = np.linspace(0, w.n, batches + 1).astype(int)
     for rnd in range(rounds):
         now = w.now + rnd * 3
@@ -62,7 +65,10 @@ def check_egress(w, dev, batches, rounds=2):
                           "ct", o["ct"][bad[:12]], ref.ct[bad[:12]], "nl", o["nl"][bad[:12]], ref.nl[bad[:12]])
                 assert len(bad) == 0, (k, rnd, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
             assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
+            traces.append(same_traces(ctx, dp, ref.ret))
             same_frames(o["frames_out"], ref.frames_out, w.frames[lo:hi])
+    tr = np.concatenate(traces)
+    assert (tr["subtype"] >= 5).any() == (trace_agg == 0)                    # FROM_LXC hidden at >= 1
     assert (ctx.metrics() == dp.metrics()).all()
     for name in ("ct4", "ct6", "policy"):
         same_table(pm, om, name)
@@ -195,3 +201,12 @@ def test_config5_v6_short_l4_checksum_fields(dev):
     dp = check_egress(w, dev, batches=1, rounds=2)
     ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now + 9)
     assert (ref.ret == -154).any() or (ref.reason == -154).any()
+
+
+@pytest.mark.parametrize("agg", [1, 3])
+def test_config5_traces_aggregated(dev, agg):
+    """send_trace_notify at MONITOR_AGGREGATION lowest (FROM_* hidden) and medium (only
+    the steps whose CT lookup asked for a report: new flows, new TCP flags, or
+    CT_REPORT_INTERVAL elapsed; rounds 3 s apart cross the 5 s interval)."""
+    w = synth.config5(1 << 14, n_svc=500, n_ep=128, n_remote=512, seed=91)
+    check_egress(w, dev, batches=2, rounds=3, trace_agg=agg)

@@ -177,11 +177,31 @@ def same_notifications(ctx, dp):
     return n_got
 
 
-def check_ingress(w, dev, batches, with_prefilter=True):
+def same_traces(ctx, dp, ret):
+    """The trace notification streams (send_trace_notify records) of one call, as sets
+    ordered by (packet, observation point); packets the record did not hold whole
+    (E_TRUNC, no reference counterpart) are left out on both sides."""
+    got, n_got = ctx.trace_drain()
+    ref, n_ref = dp.trace_drain()
+    assert len(got) == n_got and len(ref) == n_ref, "trace ring overflow"
+    trunc = np.nonzero(ret == -1)[0]
+    got = np.sort(got[~np.isin(got["packet"], trunc)], order=["packet", "subtype"])
+    ref = np.sort(ref[~np.isin(ref["packet"], trunc)], order=["packet", "subtype"])
+    assert len(got) == len(ref), (len(got), len(ref))
+    for f in ref.dtype.names:
+        bad = np.nonzero(got[f] != ref[f])[0]
+        assert len(bad) == 0, (f, bad[:5], got[bad[:5]], ref[bad[:5]])
+    return ref
+
+
+def check_ingress(w, dev, batches, with_prefilter=True, trace_agg=0):
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)
     ctx.notify_attach(w.n)
     dp.notify_attach(w.n)
+    ctx.trace_attach(3 * w.n, trace_agg, ingress_ifindex=7)
+    dp.trace_attach(3 * w.n, trace_agg, ingress_ifindex=7)
+    traces = []
     cuts = np.linspace(0, w.n, batches + 1).astype(int)
     drops = 0
     for lo, hi in zip(cuts[:-1], cuts[1:]):
@@ -193,8 +213,12 @@ def check_ingress(w, dev, batches, with_prefilter=True):
             assert len(bad) == 0, (k, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
         same_frames(o["frames_out"], ref.frames_out, w.frames[lo:hi])
         assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
+        traces.append(same_traces(ctx, dp, ref.ret))
         drops += int((o["reason"] != 0).sum())
     assert drops > 0
+    tr = np.concatenate(traces)
+    assert (tr["subtype"] == 0).any()                                        # TRACE_TO_LXC
+    assert (tr["subtype"] >= 5).any() == (trace_agg == 0)                    # FROM_* hidden at >= 1
     assert (ctx.metrics() == dp.metrics()).all()
     check_policy_maps(pm["policy"], om["policy"])
     ck, cv = pm["ct4"].dump()
@@ -297,3 +321,10 @@ def test_chunked_launches_config3(dev, monkeypatch):
     monkeypatch.setenv("CV_MAX_CHUNK", "7001")
     w = synth.config3(1 << 15, 1 << 9, n_ep=64, n_cidrs=1024, n_ids=100, seed=21)
     check_ingress(w, dev, batches=2)
+
+
+def test_config3_traces_aggregated(dev):
+    """send_trace_notify at MONITOR_AGGREGATION medium on the ingress path: established
+    flows of the preloaded CT report only on new TCP flags."""
+    w = synth.config3(1 << 15, 1 << 12, n_ep=64, n_cidrs=1024, n_ids=100, seed=17)
+    check_ingress(w, dev, batches=2, trace_agg=3)

@@ -235,7 +235,11 @@ __device__ __forceinline__ void pol_cache_flush(const LdsPolicy &pc)
         if (pc.key[i] && pc.val[i]) atomicAdd(reinterpret_cast<unsigned long long *>(pc.key[i]), pc.val[i]);
 }
 
-struct Met {
+// EVENTS: the kernel instance that emits the optional outputs (drop / trace records,
+// rewritten frames); the plain instance compiles them out (launchers pick one per call)
+template <bool EVENTS>
+struct MetT {
+    static constexpr bool EV = EVENTS;
     LdsMetrics *lm;
     Fwd f;
     LdsPolicy *pc;             // optional policy counter cache (conntrack stages)
@@ -256,7 +260,8 @@ struct Met {
     }
 };
 
-__device__ __forceinline__ void met_init(Met &m, LdsMetrics &lm)
+template <class M>
+__device__ __forceinline__ void met_init(M &m, LdsMetrics &lm)
 {
     for (int i = threadIdx.x; i < 256 * 4; i += blockDim.x) lm.c[i] = 0;
     m.lm = &lm;
@@ -274,7 +279,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     return v;
 }
 
-__device__ __forceinline__ void met_flush(Met &m, unsigned long long *g)
+template <class M>
+__device__ __forceinline__ void met_flush(M &m, unsigned long long *g)
 {
 #pragma unroll
     for (int d = 0; d < 2; ++d) {
@@ -321,10 +327,12 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred)
 
 // send_drop_notify -> __send_drop_notify (bpf/lib/drop.h:50-108): one cv_drop_notify
 // record (10 words) per drop when a ring is attached; wave-aggregated slot claims
-__device__ __forceinline__ void notify_drop(const DpParams &p, const Met &m, int32_t code, uint32_t len,
+template <class M>
+__device__ __forceinline__ void notify_drop(const DpParams &p, const M &m, int32_t code, uint32_t len,
                                             uint32_t source, uint32_t src, uint32_t dst, uint32_t dst_id,
                                             uint32_t ifindex)
 {
+    if constexpr (!M::EV) return;
     if (!p.notify) return;
     const uint32_t at = wave_append(p.notify_count, true);
     if (at >= p.notify_cap) return;                               // lost sample (ring full)
@@ -342,10 +350,12 @@ __device__ __forceinline__ void notify_drop(const DpParams &p, const Met &m, int
 // MONITOR_AGGREGATION >= 1, steps without a CT report request at >= 3
 enum : uint32_t { TRACE_TO_LXC = 0, TRACE_TO_PROXY = 1, TRACE_TO_HOST = 2, TRACE_TO_STACK = 3,
                   TRACE_FROM_LXC = 5, TRACE_FROM_PROXY = 6, TRACE_FROM_HOST = 7, TRACE_FROM_STACK = 8 };
-__device__ __forceinline__ void notify_trace(const DpParams &p, const Met &m, uint32_t obs, uint32_t len,
+template <class M>
+__device__ __forceinline__ void notify_trace(const DpParams &p, const M &m, uint32_t obs, uint32_t len,
                                              uint32_t source, uint32_t src, uint32_t dst, uint32_t dst_id,
                                              uint32_t ifindex, uint32_t reason, bool monitor)
 {
+    if constexpr (!M::EV) return;
     if (!p.trace) return;
     if (p.trace_agg >= 1 && obs >= TRACE_FROM_LXC) return;
     if (p.trace_agg >= 3 && !monitor) return;
@@ -386,6 +396,16 @@ __device__ __forceinline__ uint32_t lxc_ifindex(const HashTable &t, int64_t slot
 {
     if (t.vals && slot >= 0) return *reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * t.vstride);
     return (ival >> 17) & 1u;
+}
+
+// the ifindex a program hands on: the value itself where a record carries it (the
+// event instances), else only whether it is nonzero (redirect vs TC_ACT_OK), which
+// the inline bit answers without a dependent read of the side array
+template <class M>
+__device__ __forceinline__ uint32_t ifindex_of(const M &, const HashTable &t, int64_t slot, uint32_t ival)
+{
+    if constexpr (M::EV) return lxc_ifindex(t, slot, ival);
+    else return (ival >> 17) & 1u;
 }
 
 // endpoint_info.mac / .node_mac of a matched cilium_lxc entry (words: bytes 0-3, 4-5)
@@ -1408,9 +1428,10 @@ __device__ __forceinline__ void frame6_emit(const Frame6 &f, const uint8_t *in, 
 // ------------------------------------------------------------------ endpoint ingress programs
 // ipv4_policy (bpf_lxc.c:865-979) + tail_ipv4_policy (:981-993), LXC_NAT46 off.
 // Returns the final verdict (TC_ACT_*, drops accounted as METRIC_INGRESS) or E_TRUNC.
+template <class M>
 __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m,
+                                           uint16_t &proxy, int32_t &reason, Acct &a, M &m,
                                            RevNatOut *rn = nullptr)
 {
     int ret;
@@ -1472,9 +1493,10 @@ __device__ __forceinline__ bool eq4(const uint32_t *a, const uint32_t *b)
 }
 
 // ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862)
+template <class M>
 __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                           uint16_t &proxy, int32_t &reason, Acct &a, Met &m,
+                                           uint16_t &proxy, int32_t &reason, Acct &a, M &m,
                                            RevNat6Out *rn = nullptr)
 {
     int ret;
@@ -1537,9 +1559,10 @@ drop:
 
 // handle_policy (bpf_lxc.c:1003-1038) for an IPv4 / IPv6 packet: DROP_ALL drops
 // before any conntrack work; IPv4 needs the endpoint's LXC_IPV4 program.
+template <class M>
 __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                               bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                              uint16_t &proxy, int32_t &reason, Acct &a, Met &m,
+                                              uint16_t &proxy, int32_t &reason, Acct &a, M &m,
                                               RevNatOut *rn = nullptr)
 {
     int ret;
@@ -1552,9 +1575,10 @@ __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep
     return TC_ACT_SHOT;
 }
 
+template <class M>
 __device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                               uint32_t ifindex, uint32_t now, uint8_t &ct_out, uint16_t &proxy,
-                                              int32_t &reason, Acct &a, Met &m, RevNat6Out *rn = nullptr)
+                                              int32_t &reason, Acct &a, M &m, RevNat6Out *rn = nullptr)
 {
     int ret;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;

@@ -69,7 +69,8 @@ __device__ __forceinline__ void eg_final(const OutDev &o, uint32_t i, const EgOu
 }
 
 // tail_handle_ipv{4,6} / handle_ingress: IS_ERR -> send_drop_notify(METRIC_EGRESS)
-__device__ __forceinline__ void eg_drop(const DpParams &p, EgOut &r, int32_t code, uint32_t len, Met &m)
+template <class M>
+__device__ __forceinline__ void eg_drop(const DpParams &p, EgOut &r, int32_t code, uint32_t len, M &m)
 {
     if (code == E_TRUNC || code == E_PUNT) { r.ret = code; return; }
     m.drop(code, len, METRIC_EGRESS);
@@ -86,9 +87,9 @@ __device__ __forceinline__ bool mac_eq(uint32_t w0, uint32_t h1, const uint32_t 
 // ================================================================== front
 // handle_ingress dispatch + the from-container prologue up to lb{4,6}_lookup_service.
 // Returns STAGE_LB (service found), STAGE_CT, or STAGE_DONE with r filled.
-template <int NW>
+template <int NW, class M>
 __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep, const RecT<NW> &r, uint32_t *eg,
-                                              EgOut &res, Acct &a, Met &m)
+                                              EgOut &res, Acct &a, M &m)
 {
     const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
     int ret;
@@ -195,12 +196,13 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
     return STAGE_DONE;
 }
 
-template <int NW>
+template <int NW, bool EV>
 __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
                                                         OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
-    Met m;
+    using M = MetT<EV>;
+    M m;
     met_init(m, lm);
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         RecT<NW> r;
@@ -209,7 +211,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         const uint32_t e = src_ep ? src_ep[i] : ep0;
-        if (o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
+        if (M::EV && o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
         m.pkt = b.base + i;
         m.hash = b.hash ? b.hash[i] : 0u;
         m.src_id = e < p.n_eps ? p.eps[e].lxc_id : 0u;
@@ -256,8 +258,9 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
 // ================================================================== service stage
 // lb4_local (lb.h:700-775) + lb4_xlate (:653-697) of one packet; the packet leaves
 // with its translation in the scratch words, or final.
+template <class M>
 __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, const uint32_t *hash, uint32_t now,
-                                        const OutDev &o, const GroupScratch &g, uint32_t i, Met &m)
+                                        const OutDev &o, const GroupScratch &g, uint32_t i, M &m)
 {
     Rec r;
     rec_load(r, b, i, 4);
@@ -360,8 +363,9 @@ fin:
 }
 
 // lb6_local (lb.h:426-483) + lb6_xlate (:386-424)
+template <class M>
 __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, const uint32_t *hash, uint32_t now,
-                                        const OutDev &o, const GroupScratch &g, uint32_t i, Met &m)
+                                        const OutDev &o, const GroupScratch &g, uint32_t i, M &m)
 {
     Rec6 r;
     rec_load(r, b, i, 8);
@@ -450,12 +454,13 @@ fin:
     eg_final(o, i, res, a);
 }
 
-template <bool V6>
+template <bool V6, bool EV>
 __global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
                                                     OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
-    Met m;
+    using M = MetT<EV>;
+    M m;
     met_init(m, lm);
     for_each_group(g, V6 ? Q_LB6 : Q_LB4, [&](uint32_t, uint32_t head) {
         group_in_order(g, head, 1, [&](uint32_t x) {
@@ -672,8 +677,9 @@ __device__ __noinline__ void eg4_frame(const DpParams &p, const BatchDev &b, con
 }
 
 // handle_ipv4_from_lxc (bpf_lxc.c:464-649) from skip_service_lookup on
+template <class M>
 __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                            const GroupScratch &g, uint32_t i, Met &m)
+                                            const GroupScratch &g, uint32_t i, M &m)
 {
     Rec r;
     rec_load(r, b, i, 4);
@@ -759,7 +765,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (iv & (1u << 16)) {                                    // to_host
             res.ret = TC_ACT_REDIRECT;
             notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
-            if (o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+            if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
             eg_final(o, i, res, a);
             return;
         }
@@ -767,9 +773,9 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
         if (p.ablate & AB_EG_NO_DELIVERY) { res.ret = TC_ACT_OK; eg_final(o, i, res, a); return; }
-        res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, lxc_ifindex(p.lxc4, lxc_slot, iv), now,
+        res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
                                  ct2, res.proxy, res.reason, a, m, &rn2);
-        if (o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
+        if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg4_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv4_local_delivery
         eg_final(o, i, res, a);
         return;
@@ -778,7 +784,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     m.fwd(s.len, METRIC_EGRESS);                                  // TRACE_TO_STACK
     notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
     res.ret = TC_ACT_OK;
-    if (o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
+    if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
     return;
 drop:
@@ -820,8 +826,9 @@ __device__ __noinline__ void eg6_frame(const DpParams &p, const BatchDev &b, con
 }
 
 // ipv6_l3_from_lxc (bpf_lxc.c:133-352) from skip_service_lookup on
+template <class M>
 __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                            const GroupScratch &g, uint32_t i, Met &m)
+                                            const GroupScratch &g, uint32_t i, M &m)
 {
     Rec6 r;
     rec_load(r, b, i, 8);
@@ -899,16 +906,16 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         if (iv & (1u << 16)) {                                    // to_host
             res.ret = TC_ACT_REDIRECT;
             notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
-            if (o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+            if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
             eg_final(o, i, res, a);
             return;
         }
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, lxc_ifindex(p.lxc6, lxc_slot, iv), now, ct2,
+        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
                                  res.proxy, res.reason, a, m, &rn2);
-        if (o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
+        if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg6_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv6_local_delivery
         eg_final(o, i, res, a);
         return;
@@ -917,7 +924,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     m.fwd(s.len, METRIC_EGRESS);
     notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
     res.ret = TC_ACT_OK;
-    if (o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
+    if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
     return;
 drop:
@@ -931,12 +938,13 @@ drop:
 #define CV_EG_OCC
 #endif
 
-template <bool V6>
+template <bool V6, bool EV>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
-    Met m;
+    using M = MetT<EV>;
+    M m;
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
@@ -1015,19 +1023,31 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
 {
     if (!b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
-    if (b.stride >= 128) hipLaunchKernelGGL(k_egress_front<32>, grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-    else hipLaunchKernelGGL(k_egress_front<16>, grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-    hipLaunchKernelGGL(k_lb_stage<false>, grid, blk, 0, s, p, b, flow_hash, now, o, g);
-    if (b.stride >= 128) hipLaunchKernelGGL(k_lb_stage<true>, grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
+    if (b.stride >= 128) {
+        if (ev) hipLaunchKernelGGL((k_egress_front<32, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+        else hipLaunchKernelGGL((k_egress_front<32, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+    } else {
+        if (ev) hipLaunchKernelGGL((k_egress_front<16, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+        else hipLaunchKernelGGL((k_egress_front<16, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+    }
+    if (ev) hipLaunchKernelGGL((k_lb_stage<false, true>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    else hipLaunchKernelGGL((k_lb_stage<false, false>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    if (b.stride >= 128) {
+        if (ev) hipLaunchKernelGGL((k_lb_stage<true, true>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
+        else hipLaunchKernelGGL((k_lb_stage<true, false>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    }
     g.epoch += 1;
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
     if (CV_EG_RUNS) launch_group_runs(g, Q_CT4, grid.x, runs_sched(CV_EG_RUNS), s);
-    hipLaunchKernelGGL(k_egress_ct<false>, grid, blk, 0, s, p, b, now, o, g);
+    if (ev) hipLaunchKernelGGL((k_egress_ct<false, true>), grid, blk, 0, s, p, b, now, o, g);
+    else hipLaunchKernelGGL((k_egress_ct<false, false>), grid, blk, 0, s, p, b, now, o, g);
     if (b.stride >= 128) {
         if (CV_EG_RUNS) launch_group_runs(g, Q_CT6, grid.x, runs_sched(CV_EG_RUNS), s);
-        hipLaunchKernelGGL(k_egress_ct<true>, grid, blk, 0, s, p, b, now, o, g);
+        if (ev) hipLaunchKernelGGL((k_egress_ct<true, true>), grid, blk, 0, s, p, b, now, o, g);
+        else hipLaunchKernelGGL((k_egress_ct<true, false>), grid, blk, 0, s, p, b, now, o, g);
     }
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);

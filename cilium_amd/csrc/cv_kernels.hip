@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
 {
     __shared__ LdsMetrics lm;
     __shared__ uint4 stage[BLOCK / 64][256];
-    Met m;
+    MetT<false> m;
     met_init(m, lm);
     const HashTable pol = p.eps[ep].policy;
     Hit hits[PPT];
@@ -223,13 +223,15 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
 // ================================================================== config 3
 // stage 1: XDP prefilter + from_netdev/handle_ipv4 up to the tail call into the
 // endpoint's policy program; packets reaching it join their address-pair group.
+template <bool EV>
 __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
                                                         int with_prefilter)
 {
     __shared__ LdsMetrics lm;
     __shared__ uint4 stage[BLOCK / 64][256];
     uint4 *st = stage[threadIdx.x >> 6];
-    Met m;
+    using M = MetT<EV>;
+    M m;
     met_init(m, lm);
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < b.n; i0 += gridDim.x * BLOCK) {
@@ -248,7 +250,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         uint32_t identity = 0;
         if (pass && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
         ident = identity;
-        if (pass && p.trace) {                                    // from_netdev: send_trace_notify(FROM_*)
+        if (EV && pass && p.trace) {                              // from_netdev: send_trace_notify(FROM_*)
             const uint32_t mg = (b.mark ? b.mark[i] : 0u) & 0xF00u;
             const uint32_t obs = !(p.flags & F_FROM_HOST) ? TRACE_FROM_STACK
                                  : (mg == 0xA00u || mg == 0xB00u) ? TRACE_FROM_PROXY : TRACE_FROM_HOST;
@@ -297,7 +299,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                         staged = true;                            // -> handle_policy -> tail_ipv4_policy
                         g.secctx[i] = secctx;
                         g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
-                        g.ifx[i] = (uint32_t)lxc_slot;            // -> cb[CB_IFINDEX], MACs (stage 2)
+                        if (EV) g.ifx[i] = (uint32_t)lxc_slot;    // -> cb[CB_IFINDEX], MACs (stage 2)
                     }
                 }
             }
@@ -319,7 +321,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
         }
         if (!live) continue;
-        if (o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
+        if (M::EV && o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
         if (!staged) {
             g.gslot[i] = NONE;
             if (o.ret) o.ret[i] = ret;
@@ -337,8 +339,9 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
     met_flush(m, p.metrics);
 }
 
+template <class M>
 __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b, const OutDev &o,
-                                           const GroupScratch &g, uint32_t i, uint32_t now, Met &m)
+                                           const GroupScratch &g, uint32_t i, uint32_t now, M &m)
 {
     Rec r;
     rec_load(r, b, i, 3);
@@ -349,13 +352,17 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     uint16_t proxy = 0;
     int32_t reason = 0;
     Skb4 s = skb4_from(r);
-    m.pkt = b.base + i;
-    m.hash = b.hash ? b.hash[i] : 0u;
-    const int64_t lslot = (int32_t)g.ifx[i];                     // the destination's cilium_lxc slot
+    int64_t lslot = -1;                                          // the destination's cilium_lxc slot
+    if constexpr (M::EV) {
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+        lslot = (int32_t)g.ifx[i];
+    }
     RevNatOut rn{false, false, 0, 0};
-    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u, lxc_ifindex(p.lxc4, lslot, 0u), now, ct,
-                                   proxy, reason, a, m, &rn);
-    if (o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
+    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u,
+                                   ifindex_of(m, p.lxc4, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
+                                   a, m, &rn);
+    if (M::EV && o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
         // the forwarded frame: ipv4_local_delivery's ipv4_l3 (bpf_netdev handle_ipv4), then
         // the policy program's reverse NAT
         const uint8_t *in = b.frames + (size_t)i * b.stride;
@@ -381,11 +388,12 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 #endif
 
 // stage 2: conntrack + policy, each address-pair group by one lane in packet order
+template <bool EV>
 __global__ void __launch_bounds__(BLOCK) CV_CT_OCC k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
-    Met m;
+    MetT<EV> m;
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
@@ -692,10 +700,13 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
                           const GroupScratch &g, hipStream_t s)
 {
     if (!b.n) return 0;
-    hipLaunchKernelGGL(k_netdev_front, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, with_prefilter);
+    const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
+    if (ev) hipLaunchKernelGGL(k_netdev_front<true>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, with_prefilter);
+    else hipLaunchKernelGGL(k_netdev_front<false>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, with_prefilter);
     if (hipGetLastError() != hipSuccess) return -5;
     if (CV_RUNS_MODE) launch_group_runs(g, Q_NETDEV, grid_for(b.n), runs_sched(CV_RUNS_MODE), s);
-    hipLaunchKernelGGL(k_ct_stage, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, now);
+    if (ev) hipLaunchKernelGGL(k_ct_stage<true>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, now);
+    else hipLaunchKernelGGL(k_ct_stage<false>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, now);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -23,11 +23,12 @@ def dev():
     return "cuda:0"
 
 
-def run_egress(ctx, w, dev, lo, hi, now):
+def run_egress(ctx, w, dev, lo, hi, now, events=True):
     f, l, _ = H.to_dev(w, dev, lo, hi)
     src, fh = H.egress_inputs(w, dev, lo, hi)
     out = H.dev_out(hi - lo, dev)
-    out["frames_out"] = torch.zeros(f.shape, dtype=torch.uint8, device=dev)
+    if events:
+        out["frames_out"] = torch.zeros(f.shape, dtype=torch.uint8, device=dev)
     ctx.lxc_egress(f, l, out, now, src_ep=src, flow_hash=fh)
     return H.host_out(out)
 
@@ -40,22 +41,23 @@ def same_table(pm, om, name):
         assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all(), name
 
 
-def check_egress(w, dev, batches, rounds=2, trace_agg=0):
+def check_egress(w, dev, batches, rounds=2, trace_agg=0, events=True):
     from tests.test_gpu_parity import same_frames, same_notifications, same_traces
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)
-    ctx.notify_attach(w.n)
-    dp.notify_attach(w.n)
-    ctx.trace_attach(3 * w.n, trace_agg)
-    dp.trace_attach(3 * w.n, trace_agg)
+    if events:
+        ctx.notify_attach(w.n)
+        dp.notify_attach(w.n)
+        ctx.trace_attach(3 * w.n, trace_agg)
+        dp.trace_attach(3 * w.n, trace_agg)
     traces = []
     cuts = np.linspace(0, w.n, batches + 1).astype(int)
     for rnd in range(rounds):
         now = w.now + rnd * 3
         for lo, hi in zip(cuts[:-1], cuts[1:]):
-            o = run_egress(ctx, w, dev, lo, hi, now)
+            o = run_egress(ctx, w, dev, lo, hi, now, events)
             ref = dp.lxc_egress(w.frames[lo:hi], w.length[lo:hi], w.extra["src_ep"][lo:hi],
-                                w.extra["flow_hash"][lo:hi], now=now, frames_out=True)
+                                w.extra["flow_hash"][lo:hi], now=now, frames_out=events)
             for k in FIELDS:
                 bad = np.nonzero(o[k] != getattr(ref, k))[0]
                 if len(bad):
@@ -64,11 +66,14 @@ def check_egress(w, dev, batches, rounds=2, trace_agg=0):
                           o["ret"][bad[:12]], o["reason"][bad[:12]], "ref", ref.ret[bad[:12]], ref.reason[bad[:12]],
                           "ct", o["ct"][bad[:12]], ref.ct[bad[:12]], "nl", o["nl"][bad[:12]], ref.nl[bad[:12]])
                 assert len(bad) == 0, (k, rnd, lo, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+            if not events:
+                continue
             assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())   # one record per drop
             traces.append(same_traces(ctx, dp, ref.ret))
             same_frames(o["frames_out"], ref.frames_out, w.frames[lo:hi])
-    tr = np.concatenate(traces)
-    assert (tr["subtype"] >= 5).any() == (trace_agg == 0)                    # FROM_LXC hidden at >= 1
+    if events:
+        tr = np.concatenate(traces)
+        assert (tr["subtype"] >= 5).any() == (trace_agg == 0)                # FROM_LXC hidden at >= 1
     assert (ctx.metrics() == dp.metrics()).all()
     for name in ("ct4", "ct6", "policy"):
         same_table(pm, om, name)
@@ -79,6 +84,12 @@ def check_egress(w, dev, batches, rounds=2, trace_agg=0):
 def test_config5_dual_stack(dev):
     w = synth.config5(1 << 15, n_svc=2000, n_ep=256, n_remote=1024)
     check_egress(w, dev, batches=3)
+
+
+def test_config5_plain_instances(dev):
+    """No rings, no frames: the kernel instances the bench runs."""
+    w = synth.config5(1 << 15, n_svc=2000, n_ep=256, n_remote=1024, seed=23)
+    check_egress(w, dev, batches=2, events=False)
 
 
 def test_config5_v4_records_64(dev):

@@ -21,8 +21,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage",
-            "config5": "k_egress_ct<false>"}
+DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage<false>",
+            "config5": "k_egress_ct<false, false>"}
 
 
 def per_kernel(path):

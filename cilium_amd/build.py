@@ -23,10 +23,21 @@ def needs_build():
 
 
 def build(force=False, verbose=False, out=OUT, defines=()):
-    """Compile every source to an object in parallel, then link the shared library."""
+    """Compile every source to an object in parallel, then link the shared library.
+    Concurrent callers (one process per GPU) serialise on a lock file and re-check, so
+    at most one of them compiles."""
     if not force and out == OUT and not needs_build():
         return out
+    import fcntl
     os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and out == OUT and not needs_build():
+            return out
+        return _build(verbose, out, defines)
+
+
+def _build(verbose, out, defines):
     base = ["/opt/rocm/bin/hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function"] + [f"-D{d}" for d in defines]
     objs, procs = [], []

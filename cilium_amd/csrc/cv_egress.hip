@@ -196,8 +196,13 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
     return STAGE_DONE;
 }
 
+#ifdef CV_EF_WPE               // A/B only
+#define CV_EF_OCC __attribute__((amdgpu_waves_per_eu(CV_EF_WPE, 8)))
+#else
+#define CV_EF_OCC
+#endif
 template <int NW, bool EV>
-__global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
+__global__ void __launch_bounds__(BLOCK) CV_EF_OCC k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
                                                         OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
@@ -454,8 +459,13 @@ fin:
     eg_final(o, i, res, a);
 }
 
+#ifdef CV_LB_WPE               // A/B only
+#define CV_LB_OCC __attribute__((amdgpu_waves_per_eu(CV_LB_WPE, 8)))
+#else
+#define CV_LB_OCC
+#endif
 template <bool V6, bool EV>
-__global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
+__global__ void __launch_bounds__(BLOCK) CV_LB_OCC k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
                                                     OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
@@ -932,11 +942,14 @@ drop:
     eg_final(o, i, res, a);
 }
 
-#ifdef CV_EG_WPE
-#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WPE, 8)))
-#else
-#define CV_EG_OCC
+// Occupancy of the egress conntrack stage: left alone the compiler spends 177 VGPRs
+// (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
+// capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
+// 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
+#ifndef CV_EG_WPE
+#define CV_EG_WPE 4
 #endif
+#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WPE, 8)))
 
 template <bool V6, bool EV>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)

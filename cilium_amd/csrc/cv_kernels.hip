@@ -87,7 +87,12 @@ constexpr int PPT = CV_PPT;
 // short or invalid headers) take part with want = false.  (Holding the results in
 // registers until after the last probe, so the probes' vmcnt waits skip the output
 // stores, measured 3 % slower.)
-__global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
+#ifdef CV_PI_WPE               // A/B only
+#define CV_PI_OCC __attribute__((amdgpu_waves_per_eu(CV_PI_WPE, 8)))
+#else
+#define CV_PI_OCC
+#endif
+__global__ void __launch_bounds__(BLOCK) CV_PI_OCC k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
 {
     __shared__ unsigned long long drops[256 * 2];                 // ingress drops {count, bytes} by reason
 #ifdef CV_POL_PAIR
@@ -223,8 +228,13 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
 // ================================================================== config 3
 // stage 1: XDP prefilter + from_netdev/handle_ipv4 up to the tail call into the
 // endpoint's policy program; packets reaching it join their address-pair group.
+#ifdef CV_NF_WPE               // A/B only
+#define CV_NF_OCC __attribute__((amdgpu_waves_per_eu(CV_NF_WPE, 8)))
+#else
+#define CV_NF_OCC
+#endif
 template <bool EV>
-__global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
+__global__ void __launch_bounds__(BLOCK) CV_NF_OCC k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
                                                         int with_prefilter)
 {
     __shared__ LdsMetrics lm;
@@ -381,8 +391,8 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     store_out(o, i, a);
 }
 
-#ifdef CV_EG_WPE
-#define CV_CT_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WPE, 8)))
+#ifdef CV_CT_WPE               // A/B only: 121 VGPRs give 4 waves/SIMD already; 5 is slower
+#define CV_CT_OCC __attribute__((amdgpu_waves_per_eu(CV_CT_WPE, 8)))
 #else
 #define CV_CT_OCC
 #endif

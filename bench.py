@@ -127,6 +127,22 @@ def cpu_baseline(name, w, min_seconds=10.0):
                       f"({el:.1f} s, {'1 thread, sequential (stateful path)' if seq else 'OpenMP ' + str(threads) + ' threads'})"}
 
 
+def random_access_peak():
+    """SURVEY.md §8(d) denominator 1, measured in this run: random 64-B line reads
+    (4 x dwordx4 per lane) from a 4 GiB table in HBM (tools/gather_probe.hip, built by
+    __graft_entry__.build()), best of 3 launches of 2^26 reads; GB/s of whole lines."""
+    import ctypes as C
+    so = os.path.join(ROOT, "tools", "libgather_probe.so")
+    if not os.path.exists(so):
+        return None
+    L = C.CDLL(so)
+    L.probe_run.restype = C.c_float
+    L.probe_run.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_int, C.c_int]
+    n = 1 << 26
+    ms = L.probe_run(0, 4 << 30, n, 8192, 3)
+    return None if ms <= 0 else round(n * 64 / (ms * 1e-3) / 1e9, 1)
+
+
 def pmc_traffic(name, sha):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary of this exact
     library build (profiles/pmc_<workload>.json), else None."""
@@ -262,6 +278,7 @@ def main():
 
     if rank == 0:
         cpu = None
+        ra_peak = random_access_peak()
         if not args.no_cpu and world == 1:
             log("[rank 0] cpu baseline ...")
             cpu = cpu_baseline(name, w)
@@ -294,6 +311,11 @@ def main():
                 "traffic": traffic,
                 "kernel_ms": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": alg_bytes,
+                # the same achieved rate against the measured random-access peak (64-B lines,
+                # HBM-resident table): > 1 means the tables live in L2 / Infinity Cache
+                "random_access": None if ra_peak is None else {
+                    "peak": ra_peak, "unit": "GB/s", "frac": round(achieved / ra_peak, 4),
+                    "probe": "random 64-B line reads from a 4 GiB HBM table, measured in this run"},
             },
             "cpu_baseline": cpu,
         }

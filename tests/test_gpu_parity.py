@@ -121,6 +121,53 @@ def test_config2_ragged(dev, n):
     check_policy_maps(pm["policy"], om["policy"])
 
 
+def test_ipcache_nested_prefixes(dev):
+    """The v4 LPM layout (DIR-24-8 + /32 front, cv_lpm.hpp) against the oracle's
+    LPM_TRIE semantics: nested prefixes of every length from /0 to /32 inside one /8,
+    addresses at each prefix's first/last address and just outside, then agent deletes
+    and re-inserts between batches (the table is recompiled at the batch boundary)."""
+    w = synth.config2(1 << 12, n_cidrs=512, n_ids=64)
+    base = 0x0A000000
+    plens = np.arange(0, 33)
+    addr = (np.full(33, base + 0x00ABCDEF, np.uint32) & synth.prefix_mask(plens)).astype(np.uint32)
+    ident = (1000 + plens).astype(np.uint32)
+    # a sibling /25 and /31 under the same /24, a /24 whose only longer prefix is a /32
+    addr = np.concatenate([addr, np.array([base + 0x00ABCD00, base + 0x00ABCDF0, base + 0x00123400,
+                                           base + 0x00123477], np.uint32)])
+    plens = np.concatenate([plens, [25, 31, 24, 32]])
+    ident = np.concatenate([ident, [2001, 2002, 2003, 2004]]).astype(np.uint32)
+    w.maps["ipcache"] = synth.MapSpec("cilium_ipcache", synth.MAP_LPM_TRIE, 24, 8, 512000,
+                                      synth.ipcache_keys_v4(addr, plens), synth.remote_endpoint_infos(ident))
+    probes = []
+    for a, pl in zip(addr, plens):
+        span = 1 << (32 - int(pl))
+        lo, hi = int(a), int(a) + span - 1
+        probes += [lo, hi, (lo - 1) & 0xFFFFFFFF, (hi + 1) & 0xFFFFFFFF, lo + span // 2]
+    probes = np.array(probes, np.uint32)
+    n = min(len(probes), w.n)
+    w.frames[:n, 26:30] = synth.be32_bytes(probes[:n])
+    w.mark[:] = 0
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    keys = w.maps["ipcache"].keys
+    for rnd in range(3):
+        ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+        o = run_policy(ctx, w, dev)
+        for k in ("ret", "identity", "nl", "nu"):
+            assert (o[k] == getattr(ref, k)).all(), (rnd, k)
+        assert len(np.unique(o["identity"][:n])) > 10
+        # delete every other nested prefix, then put them back with new identities
+        for j in range(rnd % 2, 33, 2):
+            if rnd == 0:
+                assert pm["ipcache"].delete(keys[j].tobytes()) == 0
+                assert om["ipcache"].delete(keys[j].tobytes()) == 0
+            else:
+                v = synth.remote_endpoint_infos(np.array([3000 + j], np.uint32))[0].tobytes()
+                assert pm["ipcache"].update(keys[j].tobytes(), v) == 0
+                assert om["ipcache"].update(keys[j].tobytes(), v) == 0
+    ctx.close()
+
+
 def test_policy_counters_across_agent_updates(dev):
     w = synth.config2(1 << 14, n_cidrs=2048, n_ids=200)
     dp, om = H.oracle_dp(w)

@@ -282,6 +282,12 @@ def main():
         if not args.no_cpu and world == 1:
             log("[rank 0] cpu baseline ...")
             cpu = cpu_baseline(name, w)
+            if name in ("config1", "config2"):
+                # SURVEY.md §8(d) CPU item (a): the eBPF restatement in the host kernel's
+                # own datapath (JIT + kernel LPM/hash maps) via BPF_PROG_TEST_RUN
+                log("[rank 0] cpu baseline (kernel eBPF) ...")
+                from oracle import kernel_bench
+                cpu["kernel_ebpf"] = kernel_bench.run(name, w)
         line = {
             "metric": METRIC,
             "value": round(value, 2),

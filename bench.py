@@ -165,7 +165,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=1 << 24)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg and the random-access probe (profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -278,7 +278,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        ra_peak = random_access_peak()
+        ra_peak = None if args.no_cpu else random_access_peak()
         if not args.no_cpu and world == 1:
             log("[rank 0] cpu baseline ...")
             cpu = cpu_baseline(name, w)

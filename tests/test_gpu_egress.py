@@ -221,3 +221,28 @@ def test_config5_traces_aggregated(dev, agg):
     CT_REPORT_INTERVAL elapsed; rounds 3 s apart cross the 5 s interval)."""
     w = synth.config5(1 << 14, n_svc=500, n_ep=128, n_remote=512, seed=91)
     check_egress(w, dev, batches=2, rounds=3, trace_agg=agg)
+
+
+def test_empty_batches(dev):
+    """n = 0 at every batch entry point: no launch, no error, no state change; the next
+    real batch still matches the oracle."""
+    w = synth.config5(1 << 12, n_svc=200, n_ep=32, n_remote=64, seed=57)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    f, l, m = H.to_dev(w, dev, 0, 0)
+    src, fh = H.egress_inputs(w, dev, 0, 0)
+    out = H.dev_out(0, dev)
+    ctx.lxc_egress(f, l, out, w.now, src_ep=src, flow_hash=fh)
+    ctx.netdev_ingress(f, l, out, w.now, mark=m)
+    ctx.policy_ingress(0, f, l, out, mark=m)
+    ctx.xdp_prefilter(f, l, out)
+    torch.cuda.synchronize()
+    assert not ctx.metrics().any()
+    assert len(pm["ct4"].dump()[0]) == 0
+    o = run_egress(ctx, w, dev, 0, w.n, w.now)
+    ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    for k in FIELDS:
+        assert (o[k] == getattr(ref, k)).all(), k
+    assert (ctx.metrics() == dp.metrics()).all()
+    same_table(pm, om, "ct4")
+    ctx.close()

@@ -7,7 +7,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from cilium_amd import lib
+from cilium_amd import lib, synth
 
 
 def test_library_exports_header_symbols():
@@ -116,3 +116,54 @@ def test_ct_gc_host_store_vs_oracle():
     assert m.ct_gc(t) == 0                        # idempotent
     assert m.ct_gc(0xFFFFFFFF) == om.ct_gc(0xFFFFFFFF) == len(live) - want   # ctmap.Flush
     assert len(m) == 0
+
+
+def test_concurrent_agent_writers():
+    """SURVEY.md §8(b) threading: agent goroutines update maps concurrently (the C-ABI
+    serialises per context).  8 threads insert, overwrite and delete disjoint key
+    ranges of one hash map and one LPM map at once; the final contents are exactly the
+    union of what each thread left, and the counts agree."""
+    import threading
+    ctx = lib.Ctx(-1)
+    hm = ctx.map_create(lib.MAP_HASH, 8, 24, 1 << 16)
+    lm = ctx.map_create(lib.MAP_LPM_TRIE, 24, 8, 1 << 16, lib.BPF_F_NO_PREALLOC)
+    T, N = 8, 1500
+    errs = []
+
+    def key8(t, i):
+        return np.array([t * 100000 + i, 6 << 16 | 80], np.uint32).tobytes()
+
+    def key24(t, i):
+        return synth.ipcache_keys_v4(np.array([(10 << 24) | (t << 16) | (i << 4)], np.uint32),
+                                     np.array([28]))[0].tobytes()
+
+    def worker(t):
+        try:
+            for i in range(N):
+                assert hm.update(key8(t, i), bytes([t]) * 24) == 0
+                assert lm.update(key24(t, i), np.array([t, i], np.uint32).tobytes()) == 0
+            for i in range(0, N, 3):
+                assert hm.delete(key8(t, i)) == 0
+                assert lm.delete(key24(t, i)) == 0
+            for i in range(1, N, 3):
+                assert hm.update(key8(t, i), bytes([t + 100]) * 24, 2) == 0   # BPF_EXIST
+        except AssertionError as e:  # noqa: PERF203
+            errs.append((t, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    keep = [i for i in range(N) if i % 3]
+    assert len(hm) == T * len(keep) and len(lm) == T * len(keep)
+    for t in range(T):
+        for i in range(N):
+            rc, v = hm.lookup(key8(t, i))
+            if i % 3 == 0:
+                assert rc == -2
+            else:
+                assert rc == 0 and v == bytes([t + 100 if i % 3 == 1 else t]) * 24
+            rc, v = lm.lookup(key24(t, i))
+            assert (rc == -2) if i % 3 == 0 else (rc == 0 and v == np.array([t, i], np.uint32).tobytes())

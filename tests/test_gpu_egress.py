@@ -246,3 +246,43 @@ def test_empty_batches(dev):
     assert (ctx.metrics() == dp.metrics()).all()
     same_table(pm, om, "ct4")
     ctx.close()
+
+
+def _v6_ext_chains(w, seed, frac=0.5):
+    """Rewrite a fraction of the IPv6 records with extension-header chains in front of
+    their L4 header: 0-5 headers from HOPOPTS / ROUTING / DSTOPTS / AUTH (sizes as
+    ipv6_hdrlen computes them, bpf/lib/ipv6.h:61-98, including the AUTH-length quirk),
+    now and then FRAGMENT or NONE, chains that run past skb->len or past the record."""
+    s = synth.Stream(seed)
+    f, ln = w.frames, w.length
+    stride = f.shape[1]
+    rows = np.nonzero((f[:, 12] == 0x86) & (f[:, 13] == 0xDD) & (s.frac(len(ln)) < frac))[0]
+    for i in rows:
+        nh0 = int(f[i, 20])
+        l4off = 62 if nh0 == 0 else 54
+        proto = int(f[i, 54]) if nh0 == 0 else nh0
+        l4 = f[i, l4off:l4off + 24].copy()
+        k = int(s.randint(1, 0, 6)[0])
+        types = [int(t) for t in np.array([0, 43, 60, 51, 51, 43, 44, 59])[s.choice(k, 8)]] if k else []
+        chain = bytearray()
+        for j, t in enumerate(types):
+            nxt = types[j + 1] if j + 1 < k else proto
+            h = int(s.randint(1, 0, 3)[0])
+            size = (h + 2) * 4 if nxt == 51 else (h + 1) * 8
+            hdr = bytearray(size)
+            hdr[0], hdr[1] = nxt, h
+            chain += hdr
+        body = bytes(chain) + l4.tobytes()
+        f[i, 54:] = 0
+        n = min(len(body), stride - 54)
+        f[i, 54:54 + n] = np.frombuffer(body[:n], np.uint8)
+        f[i, 20] = types[0] if k else proto
+        f[i, 18:20] = synth.be16_bytes(np.array([len(body) - 4], np.uint16))
+        r = s.frac(1)[0]
+        ln[i] = 54 + len(body) if r < 0.6 else (90 if r < 0.8 else 54 + len(chain) + 2)
+
+
+def test_config5_v6_extension_headers(dev):
+    w = synth.config5(1 << 13, n_svc=300, n_ep=48, n_remote=96, family=6, seed=58)
+    _v6_ext_chains(w, 0xE7)
+    check_egress(w, dev, batches=2)

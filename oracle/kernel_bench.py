@@ -32,7 +32,9 @@ import time
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.dirname(HERE))
+ROOT = os.path.dirname(HERE)
+RECORDED = os.path.join(ROOT, "profiles", "r01u", "cpu_kernel_ebpf.json")
+sys.path.insert(0, ROOT)
 
 from cilium_amd import synth  # noqa: E402
 from oracle import kernel_golden as K  # noqa: E402
@@ -73,8 +75,15 @@ def run(name, w, threads=None, max_packets=1 << 18, min_seconds=10.0, repeat=REP
             sysctl = open("/proc/sys/kernel/unprivileged_bpf_disabled").read().strip()
         except OSError:
             sysctl = "?"
-        return {"error": f"{type(e).__name__}: {e} (uid {os.getuid()}, kernel.unprivileged_bpf_disabled="
-                         f"{sysctl}); measured where bpf(2) is permitted: profiles/r01u/cpu_kernel_ebpf.json"}
+        out = {"error": f"{type(e).__name__}: {e} (uid {os.getuid()}, kernel.unprivileged_bpf_disabled="
+                        f"{sysctl}); measured where bpf(2) is permitted: {os.path.relpath(RECORDED, ROOT)}"}
+        try:                                  # the committed measurement, labelled as such
+            import json
+            rec = json.load(open(RECORDED))
+            out["recorded_in_build_container"] = {"host": rec.get("host"), name: rec.get(name)}
+        except (OSError, ValueError):
+            pass
+        return out
     load_s = time.perf_counter() - t0
     cpus = sorted(os.sched_getaffinity(0))
     threads = min(threads or len(cpus), len(cpus), 16)           # the GPU box's CPU share is 16

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cilium_hip.h"
@@ -100,10 +101,25 @@ int build_hash(DevHash &d, const std::vector<std::vector<uint32_t>> &keys, const
     return -E2BIG;
 }
 
+struct Pfx {
+    uint32_t prio;       // full prefixlen in the map
+    int plen;            // prefix length within the address
+    uint32_t a[4];       // address words (raw network order)
+    uint32_t value;
+};
+
 struct DevLpm4 {
     DevBuf l1, chunks;
     DevHash full;              // the /32 prefixes (hash front of the trie)
     Lpm4 view{nullptr, nullptr, HashTable{}};
+    // host image for incremental updates (ipcache): the trie as built, the device
+    // chunk capacity, the /17-/31 prefixes per level-1 slot, the map it mirrors
+    bool image = false;
+    Lpm4Builder hb;
+    size_t chunk_cap = 0, chunks_on_dev = 0;
+    std::unordered_map<uint32_t, std::vector<Pfx>> longer;
+    const void *of = nullptr;
+    uint64_t front_live = 0;
 };
 
 struct DevLpm6 {
@@ -121,6 +137,7 @@ struct MapObj {
     bool is_policy = false;
     DevHash pol;
     uint64_t pol_version = 0;
+    uint64_t pol_live = 0;              // live keys in the compiled table
     std::set<std::string> written;      // keys whose value the agent wrote since the last sync
     // conntrack (device-authoritative)
     DevHash ct;
@@ -244,31 +261,43 @@ int compile_cidr_fix(cv_ctx *c, HostMap *m, bool v6)
               : build_hash<Cidr4Spec>(d, keys, none, 0, nullptr, nullptr);
 }
 
-struct Pfx {
-    uint32_t prio;       // full prefixlen in the map
-    int plen;            // prefix length within the address
-    uint32_t a[4];       // address words (raw network order)
-    uint32_t value;
-};
-
-int upload_lpm4(DevLpm4 &d, std::vector<Pfx> &px)
+// `image`: keep the host trie and the /17-/31 index so later writes can be applied
+// incrementally (update_ipcache4), with device room for that many more chunks
+int upload_lpm4(DevLpm4 &d, std::vector<Pfx> &px, bool image = false)
 {
     std::stable_sort(px.begin(), px.end(), [](const Pfx &x, const Pfx &y) { return x.prio < y.prio; });
     Lpm4Builder b;
     std::vector<std::vector<uint32_t>> k32, v32;
+    d.longer.clear();
     for (const Pfx &p : px) {
         if (p.plen == 32) { k32.push_back({p.a[0]}); v32.push_back({p.value}); }   // /32: hash front
         else b.insert(bswap32(p.a[0]), p.plen, p.value);
+        if (image && p.plen > 16 && p.plen < 32) d.longer[bswap32(p.a[0]) >> 16].push_back(p);
     }
+    if (b.chunks.empty()) b.chunks.assign(256, 0);
+    const size_t nch = b.chunks.size() / 256;
+    const size_t cap = image ? nch + std::max<size_t>(nch / 2, 4096) : nch;
     int r = d.l1.upload(b.l1.data(), b.l1.size() * 4);
-    if (!r) {
-        if (b.chunks.empty()) b.chunks.assign(256, 0);
-        r = d.chunks.upload(b.chunks.data(), b.chunks.size() * 4);
-    }
+    if (!r) r = d.chunks.alloc(cap * 1024);
+    if (!r && hipMemcpy(d.chunks.p, b.chunks.data(), b.chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess) r = -EIO;
     if (!r && !k32.empty()) r = build_hash<Host32Spec>(d.full, k32, v32, 0, nullptr, nullptr);
     d.view = r ? Lpm4{nullptr, nullptr, HashTable{}}
                : Lpm4{d.l1.as<uint32_t>(), d.chunks.as<uint32_t>(), k32.empty() ? HashTable{} : d.full.view};
+    d.image = image && !r;
+    d.chunk_cap = cap;
+    d.chunks_on_dev = nch;
+    d.front_live = k32.size();
+    if (d.image) d.hb = std::move(b);
+    else { d.longer.clear(); d.hb = Lpm4Builder{}; d.hb.l1.clear(); d.hb.l1.shrink_to_fit(); }
     return r;
+}
+
+// copy words [lo, hi) of a host array to the same offsets of a device buffer
+int put_words(const DevBuf &dst, const uint32_t *src, size_t lo, size_t hi)
+{
+    if (hi <= lo) return 0;
+    return hipMemcpy(static_cast<uint32_t *>(dst.p) + lo, src + lo, (hi - lo) * 4, hipMemcpyHostToDevice) == hipSuccess
+               ? 0 : -EIO;
 }
 
 int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
@@ -350,9 +379,115 @@ int compile_ipcache(cv_ctx *c, HostMap *m)
         }
     });
     if (err) return err;
-    int r = upload_lpm4(c->ipc4, p4);
+    int r = upload_lpm4(c->ipc4, p4, true);
     if (!r) r = upload_lpm6(c->ipc6, p6);
+    c->ipc4.of = r ? nullptr : m;
+    m->log_clear();
     return r;
+}
+
+// The writes logged since the last compile applied in place (the agent's ipcache
+// churn: one write used to recompile 100k prefixes, ~32 ms at the batch boundary).
+// Each logged key is re-read from the map (present = insert/overwrite, absent =
+// delete): a /32 rewrites its bucket of the hash front; a /17-/31 rebuilds the
+// subtree of its level-1 slot; a /1-/16 the subtrees of the level-1 slots it spans
+// (leaf pushing: a slot's value = the map's longest match for its /16, then the
+// longer prefixes inside it in length order, as the full build inserts them).  New
+// chunks are appended (the old ones become garbage until the next full build).
+// Returns 0 when done, 1 when a full compile is needed, < 0 on error.
+int update_ipcache4(cv_ctx *c, HostMap *m)
+{
+    DevLpm4 &d = c->ipc4;
+    if (!m || !d.image || d.of != m || m->log_full) return 1;
+    std::set<uint32_t> dirty;                  // level-1 slots to rebuild
+    std::vector<uint64_t> front_b;             // front buckets touched
+    HashTable ft{d.full.hb.data(), nullptr, d.full.nb ? d.full.nb - 1 : 0, 0, (uint32_t)Host32Spec::SPB};
+    for (const std::vector<uint8_t> &k : m->log) {
+        const uint32_t plen = rd32(k.data());
+        if (plen < 32) return 1;               // spans the static bits: both families, /0
+        if (k[4] || k[5] || k[6]) continue;    // matches no lookup key
+        if (k[7] == 2) return 1;               // IPv6 (a full compile rebuilds its hash)
+        if (k[7] != 1) continue;
+        if (plen > 64) continue;
+        const int len = (int)plen - 32;
+        const uint32_t raw = rd32(k.data() + 8), addr = bswap32(raw);
+        const uint8_t *v = m->lookup_exact(k.data());
+        if (v && (rd32(v) & 0x80000000u)) return -ERANGE;
+        if (len == 32) {                       // hash front
+            if (!d.full.view.buckets) return 1;
+            if (v) {
+                const uint32_t val = rd32(v);
+                const int64_t sl = host_find<Host32Spec>(ft, &raw);
+                const int64_t s2 = host_upsert<Host32Spec>(ft, &raw, &val);
+                if (s2 < 0) return 1;
+                if (sl < 0 && ++d.front_live * 10 > d.full.nb * Host32Spec::SPB * 8) return 1;   // > 80 % load
+                front_b.push_back((uint64_t)s2 / Host32Spec::SPB);
+            } else {
+                const int64_t sl = host_find<Host32Spec>(ft, &raw);
+                if (sl < 0) continue;
+                const uint64_t b = (uint64_t)sl / Host32Spec::SPB;
+                uint32_t *w = d.full.hb.data() + b * Host32Spec::BW;
+                const int q = (int)(sl % Host32Spec::SPB);
+                uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+                tags = (tags & ~(0xFFULL << (8 * q))) | ((uint64_t)TAG_DEAD << (8 * q));
+                w[0] = (uint32_t)tags; w[1] = (uint32_t)(tags >> 32);
+                front_b.push_back(b);
+                --d.front_live;
+            }
+            continue;
+        }
+        if (len > 16) {
+            const uint32_t x = addr >> 16;
+            std::vector<Pfx> &lv = d.longer[x];
+            lv.erase(std::remove_if(lv.begin(), lv.end(), [&](const Pfx &p) { return p.prio == plen && p.a[0] == raw; }),
+                     lv.end());
+            if (v) {
+                Pfx p{};
+                p.prio = plen; p.plen = len; p.a[0] = raw; p.value = rd32(v);
+                lv.push_back(p);
+            }
+            dirty.insert(x);
+        } else {
+            const uint32_t span = 1u << (16 - len);
+            if (span > 4096) return 1;
+            const uint32_t base = (addr >> 16) & ~(span - 1);
+            for (uint32_t i = 0; i < span; ++i) dirty.insert(base + i);
+        }
+    }
+    // rebuild the dirty level-1 subtrees on the host image
+    uint8_t key[24] = {0};
+    key[0] = 48;                               // prefixlen 32 + 16: the longest match of a /16
+    key[7] = 1;
+    for (const uint32_t x : dirty) {
+        const uint32_t raw16 = bswap32(x << 16);
+        memcpy(key + 8, &raw16, 4);
+        const uint8_t *v0 = m->lookup(key);
+        const uint32_t base = v0 ? rd32(v0) : 0u;
+        if (base & 0x80000000u) return -ERANGE;
+        d.hb.l1[x] = base;
+        auto it = d.longer.find(x);
+        if (it == d.longer.end()) continue;
+        if (it->second.empty()) { d.longer.erase(it); continue; }
+        std::vector<Pfx> lv = it->second;
+        std::stable_sort(lv.begin(), lv.end(), [](const Pfx &a, const Pfx &b) { return a.prio < b.prio; });
+        for (const Pfx &p : lv) d.hb.insert(bswap32(p.a[0]), p.plen, p.value);
+    }
+    const size_t nch = d.hb.chunks.size() / 256;
+    if (nch > d.chunk_cap) return 1;           // out of device room: a full build compacts
+    int r = put_words(d.chunks, d.hb.chunks.data(), d.chunks_on_dev * 256, nch * 256);
+    if (r) return r;
+    d.chunks_on_dev = nch;
+    for (auto it = dirty.begin(); it != dirty.end();) {          // contiguous runs of slots
+        uint32_t lo = *it, hi = lo + 1;
+        for (++it; it != dirty.end() && *it == hi; ++it) ++hi;
+        if ((r = put_words(d.l1, d.hb.l1.data(), lo, hi))) return r;
+    }
+    std::sort(front_b.begin(), front_b.end());
+    front_b.erase(std::unique(front_b.begin(), front_b.end()), front_b.end());
+    for (const uint64_t b : front_b)
+        if ((r = put_words(d.full.buckets, d.full.hb.data(), b * Host32Spec::BW, (b + 1) * Host32Spec::BW))) return r;
+    m->log_clear();
+    return 0;
 }
 
 // policy map -> PolicySpec table (proxy_port inline, so a lookup is one line) + 32-B
@@ -394,6 +529,64 @@ int compile_policy(cv_ctx *c, MapObj *mo)
     if (hipMemset(mo->pol.aux.p, 0, nslots * 8) != hipSuccess) return -EIO;
     mo->pol.view.aux = mo->pol.aux.as<unsigned long long>();
     mo->pol_version = m->version;
+    mo->pol_live = keys.size();
+    m->log_clear();
+    return 0;
+}
+
+// The policy writes logged since the last compile applied in place: a written key's
+// bucket (its inline proxy_port) and 32-B side value {proxy_port, pad, packets, bytes}
+// take the agent's value, its counter-delta word is cleared; a deleted key's slot
+// becomes a tombstone.  Every other entry keeps its device-resident counters, as the
+// full compile carries them over.  0 = done, 1 = a full compile is needed.
+int update_policy(MapObj *mo)
+{
+    HostMap *m = mo->hm.get();
+    DevHash &d = mo->pol;
+    // (three small copies per key: past a few hundred keys one full compile is cheaper)
+    if (!d.view.buckets || m->log_full || d.hb.empty() || m->log.size() > 256) return 1;
+    HashTable t{d.hb.data(), nullptr, d.nb - 1, 32, (uint32_t)PolicySpec::SPB};
+    std::vector<uint64_t> bk;
+    struct Side { int64_t s; uint8_t v[32]; };
+    std::vector<Side> side;
+    for (const std::vector<uint8_t> &k : m->log) {
+        const uint32_t kw[2] = {rd32(k.data()), rd32(k.data() + 4)};
+        const uint8_t *v = m->lookup_exact(k.data());
+        const int64_t old = host_find<PolicySpec>(t, kw);
+        if (v) {
+            const uint32_t px = (uint32_t)v[0] | (uint32_t)v[1] << 8;   // raw be16 bytes, as stored
+            const int64_t sl = host_upsert<PolicySpec>(t, kw, &px);
+            if (sl < 0) return 1;
+            if (old < 0 && ++mo->pol_live * 10 > d.nb * PolicySpec::SPB * 8) return 1;   // > 80 % load
+            Side e{sl, {0}};
+            memcpy(e.v, v, 24);
+            side.push_back(e);
+            bk.push_back((uint64_t)sl / PolicySpec::SPB);
+        } else if (old >= 0) {
+            const uint64_t b = (uint64_t)old / PolicySpec::SPB;
+            uint32_t *w = d.hb.data() + b * PolicySpec::BW;
+            const int q = (int)(old % PolicySpec::SPB);
+            uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            tags = (tags & ~(0xFFULL << (8 * q))) | ((uint64_t)TAG_DEAD << (8 * q));
+            w[0] = (uint32_t)tags; w[1] = (uint32_t)(tags >> 32);
+            bk.push_back(b);
+            --mo->pol_live;
+        }
+    }
+    std::sort(bk.begin(), bk.end());
+    bk.erase(std::unique(bk.begin(), bk.end()), bk.end());
+    int r = 0;
+    for (const uint64_t b : bk)
+        if ((r = put_words(d.buckets, d.hb.data(), b * PolicySpec::BW, (b + 1) * PolicySpec::BW))) return r;
+    const unsigned long long zero = 0;
+    for (const Side &e : side) {          // in log order: the last write of a key wins
+        if (hipMemcpy(d.vals.as<uint8_t>() + (size_t)e.s * 32, e.v, 32, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(d.aux.as<unsigned long long>() + e.s, &zero, 8, hipMemcpyHostToDevice) != hipSuccess)
+            return -EIO;
+    }
+    mo->written.clear();
+    mo->pol_version = m->version;
+    m->log_clear();
     return 0;
 }
 
@@ -519,7 +712,10 @@ int sync_locked(cv_ctx *c)
         case CV_ROLE_CIDR4_DYN: r = compile_cidr_dyn(c, hm, false); break;
         case CV_ROLE_CIDR6_DYN: r = compile_cidr_dyn(c, hm, true); break;
         case CV_ROLE_LXC: r = compile_lxc(c, hm); break;
-        case CV_ROLE_IPCACHE: r = compile_ipcache(c, hm); break;
+        case CV_ROLE_IPCACHE:
+            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_ipcache4(c, hm);
+            if (r == 1) r = compile_ipcache(c, hm);
+            break;
         case CV_ROLE_LB4_SERVICES: r = compile_lb(c, hm, false); break;
         case CV_ROLE_LB6_SERVICES: r = compile_lb(c, hm, true); break;
         case CV_ROLE_LB4_REVNAT: r = compile_revnat(c, hm, false); break;
@@ -533,7 +729,8 @@ int sync_locked(cv_ctx *c)
     for (auto &e : c->eps) {
         MapObj *p = get(c, e.policy);
         if (p && p->hm->version != p->pol_version) {
-            r = compile_policy(c, p);
+            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_policy(p);
+            if (r == 1) r = compile_policy(c, p);
             if (r) return r;
             eps_changed = true;
         }

@@ -93,6 +93,12 @@ class HostMap {
     int type;
     uint32_t ks, vs, max_entries, flags;
     uint64_t version = 1;      // bumped on every successful write
+    // keys written or deleted since the consumer last compiled the map (LPM keys
+    // masked to their prefix length); `log_full` once more than LOG_MAX were noted
+    static constexpr size_t LOG_MAX = 4096;
+    std::vector<std::vector<uint8_t>> log;
+    bool log_full = false;
+    void log_clear() { log.clear(); log_full = false; }
 
     HostMap(int type_, uint32_t ks_, uint32_t vs_, uint32_t max_, uint32_t flags_)
         : type(type_), ks(ks_), vs(vs_), max_entries(max_), flags(flags_)
@@ -137,6 +143,7 @@ class HostMap {
             memcpy(t.val(s), key + 4, ks - 4);
             memcpy(t.val(s) + ks - 4, val, vs);
             version++;
+            note(key, mk.data());
             return 0;
         }
         int64_t s = tab_->find(key);
@@ -149,6 +156,7 @@ class HostMap {
         }
         memcpy(tab_->val(s), val, vs);
         version++;
+        note(key, nullptr);
         return 0;
     }
 
@@ -183,6 +191,7 @@ class HostMap {
             if (s < 0) return -ENOENT;
             tab_->erase(s);
             version++;
+            note(key, nullptr);
             return 0;
         }
         uint32_t plen;
@@ -195,7 +204,22 @@ class HostMap {
         per_len_[plen].erase(s);
         lpm_count_--;
         version++;
+        note(key, mk.data());
         return 0;
+    }
+
+    // value of the exact element (LPM: same prefix length and masked prefix), or null
+    const uint8_t *lookup_exact(const uint8_t *key) const
+    {
+        if (!is_lpm()) return lookup(key);
+        uint32_t plen;
+        memcpy(&plen, key, 4);
+        if (plen > dbits_) return nullptr;
+        std::vector<uint8_t> mk(key + 4, key + ks);
+        mask(mk.data(), plen);
+        const ByteTable &t = per_len_[plen];
+        const int64_t s = t.find(mk.data());
+        return s >= 0 ? t.val(s) + ks - 4 : nullptr;
     }
 
     // Walk every element: f(key bytes (BPF layout), value bytes).
@@ -233,6 +257,14 @@ class HostMap {
         });
         (void)found;
         return done ? 0 : -ENOENT;
+    }
+
+    void note(const uint8_t *key, const uint8_t *masked)
+    {
+        if (log.size() >= LOG_MAX) { log_full = true; return; }
+        std::vector<uint8_t> k(key, key + ks);
+        if (masked) memcpy(k.data() + 4, masked, ks - 4);
+        log.push_back(std::move(k));
     }
 
   private:

@@ -388,3 +388,91 @@ def test_config3_traces_aggregated(dev):
     flows of the preloaded CT report only on new TCP flags."""
     w = synth.config3(1 << 15, 1 << 12, n_ep=64, n_cidrs=1024, n_ids=100, seed=17)
     check_ingress(w, dev, batches=2, trace_agg=3)
+
+
+@pytest.mark.parametrize("incremental", [True, False])
+def test_ipcache_churn_between_batches(dev, monkeypatch, incremental):
+    """Agent ipcache churn between batches (writes visible at the next
+    batch boundary): random inserts, overwrites and deletes of /8-/32 prefixes, a few
+    to a few hundred per round, applied in place (update_ipcache4) or by a full
+    recompile; every round's verdicts, identities and counters equal the oracle's."""
+    if not incremental:
+        monkeypatch.setenv("CV_NO_INCREMENTAL", "1")
+    w = synth.config2(1 << 14, n_cidrs=3000, n_ids=300)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    s = synth.Stream(0xC4)
+    keys = list(w.maps["ipcache"].keys[:-1])           # (keep 0.0.0.0/0)
+    pk = w.frames[:, 26:30].copy()                      # packet saddrs: churn near them
+    for rnd in range(6):
+        ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+        o = run_policy(ctx, w, dev)
+        for k in ("ret", "identity", "proxy", "nl", "nu"):
+            assert (o[k] == getattr(ref, k)).all(), (rnd, k)
+        n_up = [3, 40, 300, 7, 120, 1][rnd]
+        for j in range(n_up):
+            r = float(s.frac(1)[0])
+            if r < 0.35 and keys:                       # delete an existing prefix
+                k = keys.pop(int(s.randint(1, 0, len(keys))[0])).tobytes()
+                assert pm["ipcache"].delete(k) == om["ipcache"].delete(k)   # (a duplicate key: -ENOENT on both)
+                continue
+            if r < 0.5 and keys:                        # overwrite an existing prefix
+                k = keys[int(s.randint(1, 0, len(keys))[0])].tobytes()
+            else:                                       # new prefix around a packet's saddr
+                a = int.from_bytes(pk[int(s.randint(1, 0, len(pk))[0])].tobytes(), "big")
+                plen = int(np.array([8, 12, 16, 17, 20, 24, 24, 25, 28, 31, 32, 32, 32])[s.choice(1, 13)][0])
+                a &= int(synth.prefix_mask(np.array([plen]))[0])
+                kk = synth.ipcache_keys_v4(np.array([a], np.uint32), np.array([plen]))[0]
+                keys.append(kk)
+                k = kk.tobytes()
+            v = synth.remote_endpoint_infos(np.array([int(s.randint(1, 256, 600)[0])], np.uint32))[0].tobytes()
+            assert pm["ipcache"].update(k, v) == 0 and om["ipcache"].update(k, v) == 0
+    assert (ctx.metrics() == dp.metrics()).all()
+    check_policy_maps(pm["policy"], om["policy"])
+    ctx.close()
+
+
+@pytest.mark.parametrize("incremental", [True, False])
+def test_policy_churn_between_batches(dev, monkeypatch, incremental):
+    """Agent policy-map churn between batches, applied in place (update_policy) or by a
+    full recompile: overwrites (new proxy ports, agent-written counters), deletes,
+    inserts of keys the packets hit, insert+delete of one key in the same interval;
+    verdicts and every entry's counters equal the oracle's after each round."""
+    if not incremental:
+        monkeypatch.setenv("CV_NO_INCREMENTAL", "1")
+    w = synth.config2(1 << 14, n_cidrs=2048, n_ids=200)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    s = synth.Stream(0xC5)
+    keys = list(w.maps["policy"].keys)
+    for rnd in range(5):
+        ref = dp.policy_ingress(0, w.frames, w.length, w.mark)
+        o = run_policy(ctx, w, dev)
+        for k in ("ret", "identity", "proxy", "nl", "nu"):
+            assert (o[k] == getattr(ref, k)).all(), (rnd, k)
+        check_policy_maps(pm["policy"], om["policy"])
+        for j in range([5, 60, 400, 1, 30][rnd]):
+            r = float(s.frac(1)[0])
+            if r < 0.3:
+                k = keys.pop(int(s.randint(1, 0, len(keys))[0])).tobytes()
+                assert pm["policy"].delete(k) == om["policy"].delete(k)
+                continue
+            if r < 0.7:
+                k = keys[int(s.randint(1, 0, len(keys))[0])].tobytes()
+            else:                                       # a new L4 / L3 key for a live identity
+                ident = int(s.randint(1, 256, 456)[0])
+                port = int(np.array([80, 443, 53, 8080, 0])[s.choice(1, 5)][0])
+                kk = synth.policy_keys(np.array([ident]), np.array([port]), np.array([6 if port else 0]))[0]
+                keys.append(kk)
+                k = kk.tobytes()
+            v = bytearray(24)
+            if s.frac(1)[0] < 0.3:
+                v[0:2] = int(s.randint(1, 10000, 20000)[0]).to_bytes(2, "big")
+            if s.frac(1)[0] < 0.3:
+                v[8:16] = (5).to_bytes(8, "little")
+            assert pm["policy"].update(k, bytes(v)) == om["policy"].update(k, bytes(v)) == 0
+            if s.frac(1)[0] < 0.05:                     # insert + delete within one interval
+                assert pm["policy"].delete(k) == om["policy"].delete(k) == 0
+                keys = [x for x in keys if x.tobytes() != k]
+    assert (ctx.metrics() == dp.metrics()).all()
+    ctx.close()

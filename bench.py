@@ -46,9 +46,13 @@ def log(*a):
 
 
 def lib_sha():
-    from cilium_amd import lib
-    with open(lib.LIB_PATH, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    """the device code the PMC summaries were taken with (cilium_amd/build.py kernel_sha);
+    an A/B library (CV_LIB) is keyed by its own file hash"""
+    from cilium_amd import build, lib
+    if os.environ.get("CV_LIB"):
+        with open(lib.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    return build.kernel_sha()
 
 
 def make_workload(name, n, rank):
@@ -145,7 +149,7 @@ def random_access_peak():
 
 def pmc_traffic(name, sha):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary of this exact
-    library build (profiles/pmc_<workload>.json), else None."""
+    device code (profiles/pmc_<workload>.json, keyed by build.kernel_sha), else None."""
     p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if not os.path.exists(p):
         return None
@@ -153,7 +157,7 @@ def pmc_traffic(name, sha):
         d = json.load(open(p))
     except Exception:
         return None
-    if d.get("lib_sha") != sha:
+    if d.get("kernel_sha") != sha:
         return None
     return d.get("hbm_bytes_per_launch")
 

@@ -14,6 +14,21 @@ SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip"]
 ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 
 
+DEVICE_SOURCES = ["cv_kernels.hip", "cv_egress.hip", "cv_dev.hpp", "cv_dp.hpp", "cv_hash.hpp", "cv_lpm.hpp",
+                  "cv_common.hpp"]
+
+
+def kernel_sha():
+    """Hash of the device-code sources (the .hip files and the headers they include):
+    what a PMC traffic summary depends on; host-side changes leave it alone."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in DEVICE_SOURCES:
+        with open(os.path.join(SRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def needs_build():
     if not os.path.exists(OUT):
         return True

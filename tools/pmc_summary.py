@@ -60,10 +60,11 @@ def main():
         avg_ns = sum(d) / len(d)
     fetch, write = ctr["FETCH_SIZE"][0], ctr["WRITE_SIZE"][0]
     hit, miss = ctr["TCC_HIT_sum"][0], ctr["TCC_MISS_sum"][0]
-    lib = os.path.join(ROOT, "cilium_amd", "_lib", "libcilium_hip.so")
-    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+    sys.path.insert(0, ROOT)
+    from cilium_amd import build
+    sha = build.kernel_sha()
     out = {
-        "workload": w, "kernel": kname, "tag": tag, "lib_sha": sha,
+        "workload": w, "kernel": kname, "tag": tag, "kernel_sha": sha,
         "dispatches_per_pass": ctr["FETCH_SIZE"][1],
         "rocprof_avg_kernel_ns": avg_ns,
         "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,

@@ -348,7 +348,7 @@ int compile_cidr_dyn(cv_ctx *c, HostMap *m, bool v6)
 }
 
 // cilium_ipcache: a v4 lookup key is {prefixlen 64, pad 0, family 1, ip4, 0...}
-// (eps.h:309-319); it matches stored elements with prefixlen <= 64 whose first
+// (eps.h:68-86); it matches stored elements with prefixlen <= 64 whose first
 // min(prefixlen, 32) bits equal {0, 0, 0, 1}.  Same for v6 with family 2, 160.
 int compile_ipcache(cv_ctx *c, HostMap *m)
 {
@@ -790,6 +790,8 @@ DpParams params(cv_ctx *c)
     memcpy(p.router6, c->node.router_ip6, 16);
     p.host_mac[0] = p.host_mac[1] = 0;
     memcpy(p.host_mac, c->node.host_mac, 6);
+    p.net_mac[0] = p.net_mac[1] = 0;
+    memcpy(p.net_mac, c->node.net_mac, 6);
     const char *rm = getenv("CV_RECMODE");
     p.recmode = rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u;
     const char *ab = getenv("CV_ABLATE");

@@ -416,7 +416,7 @@ __device__ __forceinline__ void lxc_macs(const HashTable &t, int64_t slot, uint3
     node_mac[0] = (v[2] >> 16) | (v[3] << 16); node_mac[1] = v[3] >> 16;
 }
 
-// ipcache_lookup4 (eps.h:309-319) -> remote_endpoint_info.sec_label (0 = none)
+// ipcache_lookup4 (eps.h:68-86) -> remote_endpoint_info.sec_label (0 = none)
 __device__ __forceinline__ uint32_t ipcache4(const DpParams &p, uint32_t addr_raw, Acct &a)
 {
     if (!p.ipc4.l1) return 0;
@@ -433,7 +433,7 @@ __device__ __forceinline__ uint32_t ipcache4_q(const DpParams &p, uint32_t addr_
     return lpm4_lookup_q(p.ipc4, bswap32(addr_raw), want, st);
 }
 
-// ipcache_lookup6 (eps.h:295-305) at /128
+// ipcache_lookup6 (eps.h:54-66) at /128
 __device__ __forceinline__ uint32_t ipcache6(const DpParams &p, const uint32_t *addr, Acct &a)
 {
     if (!p.ipc6.h.buckets) return 0;
@@ -468,7 +468,7 @@ __device__ __forceinline__ void hit_flush(const Hit &h)
     if (h.p) atomicAdd(h.p, h.inc);
 }
 
-// __policy_can_access (policy.h:217-285); cb[CB_POLICY] is 0 on these paths.  With
+// __policy_can_access (policy.h:51-119); cb[CB_POLICY] is 0 on these paths.  With
 // `defer` the counter update is returned instead of issued.
 // With ILP the three keys' buckets are read together (one round trip instead of up
 // to three dependent ones; more lines read when an early step hits).
@@ -606,7 +606,7 @@ __device__ __forceinline__ int policy_ingress_q(const HashTable &pol, uint32_t f
     return r >= TC_ACT_OK ? r : DROP_POLICY;
 }
 
-// policy_can_access_ingress (policy.h:305-329)
+// policy_can_access_ingress (policy.h:139-163)
 template <bool ILP = false>
 __device__ __forceinline__ int policy_ingress(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t src,
                                               uint32_t dport_raw, uint32_t proto, Acct &a, Hit *defer = nullptr)
@@ -801,7 +801,7 @@ struct Tuple6 {                 // struct ipv6_ct_tuple (common.h:338-346), 10 w
         k[8] = (dport & 0xFFFFu) | (sport << 16);
         k[9] = nexthdr | (flags << 8);
     }
-    __device__ void reverse()   // ipv6_ct_tuple_reverse (conntrack.h:264-284)
+    __device__ void reverse()   // ipv6_ct_tuple_reverse (conntrack.h:265-285)
     {
 #pragma unroll
         for (int j = 0; j < 4; ++j) { uint32_t x = saddr[j]; saddr[j] = daddr[j]; daddr[j] = x; }
@@ -1024,7 +1024,7 @@ __device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32
 }
 
 // ------------------------------------------------------------------ reverse NAT
-// cilium_lb4_reverse_nat / cilium_lb6_reverse_nat lookups (lb.h:501-517, 305-315):
+// cilium_lb4_reverse_nat / cilium_lb6_reverse_nat lookups (lb.h:562-576, 305-315):
 // dense tables indexed by the raw u16 key
 __device__ __forceinline__ bool revnat4(const DpParams &p, uint32_t index, uint32_t &addr, uint32_t &port, Acct &a)
 {
@@ -1313,7 +1313,7 @@ __device__ __forceinline__ void frame_copy(const uint8_t *in, uint8_t *out, uint
 
 // ------------------------------------------------------------------ output frames (IPv6)
 // lb6_xlate (lb.h:398-424), __lb6_rev_nat (lb.h:254-290), ipv6_policy's rev-NAT index
-// zeroing (bpf_lxc.c:750-766), ipv6_l3 (l3.h:30-51) and pass_to_stack's
+// zeroing (bpf_lxc.c:754-772), ipv6_l3 (l3.h:30-51) and pass_to_stack's
 // ipv6_store_flowlabel (ipv6.h:245-260).  No L3 checksum; the L4 one changes by the
 // 16-byte bpf_csum_diff of the address (pinned by tests/golden/csum16_kernel.npz).
 __device__ __forceinline__ uint32_t csum_diff16(const uint32_t *from, const uint32_t *to, uint32_t seed)
@@ -1577,12 +1577,12 @@ __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep
 
 template <class M>
 __device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
-                                              uint32_t ifindex, uint32_t now, uint8_t &ct_out, uint16_t &proxy,
-                                              int32_t &reason, Acct &a, M &m, RevNat6Out *rn = nullptr)
+                                              bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
+                                              uint16_t &proxy, int32_t &reason, Acct &a, M &m, RevNat6Out *rn = nullptr)
 {
     int ret;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, false, ifindex, now, ct_out, proxy, reason, a, m, rn);
+    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn);
     else ret = DROP_MISSED_TAIL_CALL;
     m.drop(ret, s.len, METRIC_INGRESS);
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);

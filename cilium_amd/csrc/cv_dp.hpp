@@ -44,6 +44,7 @@ struct DpParams {              // by value as the kernel argument
     uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
     uint32_t router6[4];
     uint32_t host_mac[2];      // HOST_IFINDEX_MAC bytes 0-3 | 4-5
+    uint32_t net_mac[2];       // CILIUM_NET_MAC (rewrite_dmac_to_host, bpf_netdev.c:156-169)
     // drop notifications (cv_notify_attach): cv_drop_notify records of 10 words
     uint32_t *notify;
     uint32_t notify_cap;
@@ -110,6 +111,9 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
 // Queues filled at the same time (the v4 and v6 lists of one stage) live in different
 // banks of `queue`: QSPLIT regions of qregion words each per bank.
 enum : int { Q_NETDEV = 0, Q_LB4 = 1, Q_LB6 = 2, Q_CT4 = 3, Q_CT6 = 4, Q_NAT = 5, NQUEUES = 6 };
+// the netdev path's IPv6 groups (handle_ipv6 -> ipv6_policy) use the CT6 queue, which the
+// egress path alone fills otherwise; it sits in the other bank from Q_NETDEV
+constexpr int Q_NETDEV6 = Q_CT6;
 // Size-sorted runs (k_group_flatten / k_group_schedule): per queue NCLASS group-size
 // classes, each a {count, fill} pair on its own line after the sub-queue counters; cursor[3] is
 // the allocation cursor of the runs in `order` ({size, members...}).
@@ -126,16 +130,6 @@ constexpr int EG_WORDS = 16;
 // sched: 0 runs in queue order (no k_group_schedule), 1 largest size class first,
 // 2 smallest first
 void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStream_t s);
-// how a conntrack stage walks its groups: 0 linked lists (group_in_order), 1 runs
-// largest class first, 2 runs in queue order, 3 runs smallest class first
-// (build-time switches for A/B timing; CV_RUNS_MODE: config 3, CV_EG_RUNS: config 5)
-#ifndef CV_RUNS_MODE
-#define CV_RUNS_MODE 1
-#endif
-#ifndef CV_EG_RUNS
-#define CV_EG_RUNS 2
-#endif
-constexpr int runs_sched(int mode) { return mode == 1 ? 1 : mode == 3 ? 2 : 0; }
 int launch_policy_fold(const HashTable &pol, hipStream_t s);
 int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);

@@ -118,7 +118,7 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
             return STAGE_CT;                                      // DROP_UNKNOWN_L4: skip_service_lookup
         }
         if (!p.lb4.buckets) return STAGE_CT;
-        // lb4_lookup_service (lb.h:590-623), LB_L4 + LB_L3
+        // lb4_lookup_service (lb.h:604-635), LB_L4 + LB_L3
         const uint32_t daddr = rec_raw32c<30>(r);
         uint32_t k[2], v[3];
         if (dport) {
@@ -144,7 +144,7 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
             return STAGE_DONE;
         } else {
             if (!ep.ct6.buckets) { eg_drop(p, res, DROP_MISSED_TAIL_CALL, r.len, m); return STAGE_DONE; }
-            // handle_ipv6 (bpf_lxc.c:354-380) + ipv6_l3_from_lxc (:82-125)
+            // handle_ipv6 (bpf_lxc.c:360-387) + ipv6_l3_from_lxc (:82-125)
             if (r.len < 54) { eg_drop(p, res, DROP_INVALID, r.len, m); return STAGE_DONE; }
             eg[0] |= EG_V6;
             if (rec_u8c<20>(r) == 58) {                          // icmp6_handle (icmp6.h:390-412)
@@ -174,7 +174,7 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
             if (!p.lb6.buckets) return STAGE_CT;
             uint32_t k[5] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r), 0};
             uint32_t v[6];
-            if (dport) {                                          // lb6_lookup_service (lb.h:334-368)
+            if (dport) {                                          // lb6_lookup_service (lb.h:351-380)
                 k[4] = dport;
                 a.nl++;
                 if (dev_find<Lb6Spec>(p.lb6, k, v) >= 0 && (v[4] >> 16)) {
@@ -923,7 +923,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
+        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, false, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
                                  res.proxy, res.reason, a, m, &rn2);
         if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg6_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv6_local_delivery
@@ -961,25 +961,12 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    // AB_EG_ONE_PER_GROUP (timing only): the first member of each group alone
-#if CV_EG_RUNS == 0
-    for_each_group(g, V6 ? Q_CT6 : Q_CT4, [&](uint32_t, uint32_t head) {
-        if (p.ablate & AB_EG_ONE_PER_GROUP) {
-            if constexpr (V6) egress6_one(p, b, now, o, g, head, m);
-            else egress4_one(p, b, now, o, g, head, m);
-            return;
-        }
-        group_in_order(g, head, 2, [&](uint32_t x) {
-            if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
-            else egress4_one(p, b, now, o, g, x, m);
-        });
-    });
-#else
-    for_each_run<CV_EG_RUNS != 2>(g, V6 ? Q_CT6 : Q_CT4, p.ablate & AB_EG_ONE_PER_GROUP, [&](uint32_t x) {
+    // runs in queue order: k_group_flatten without k_group_schedule (measured faster here
+    // than size-class order); AB_EG_ONE_PER_GROUP (timing only): each group's first member
+    for_each_run<false>(g, V6 ? Q_CT6 : Q_CT4, p.ablate & AB_EG_ONE_PER_GROUP, [&](uint32_t x) {
         if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
         else egress4_one(p, b, now, o, g, x, m);
     });
-#endif
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
 }
@@ -1054,11 +1041,11 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
-    if (CV_EG_RUNS) launch_group_runs(g, Q_CT4, grid.x, runs_sched(CV_EG_RUNS), s);
+    launch_group_runs(g, Q_CT4, grid.x, 0, s);
     if (ev) hipLaunchKernelGGL((k_egress_ct<false, true>), grid, blk, 0, s, p, b, now, o, g);
     else hipLaunchKernelGGL((k_egress_ct<false, false>), grid, blk, 0, s, p, b, now, o, g);
     if (b.stride >= 128) {
-        if (CV_EG_RUNS) launch_group_runs(g, Q_CT6, grid.x, runs_sched(CV_EG_RUNS), s);
+        launch_group_runs(g, Q_CT6, grid.x, 0, s);
         if (ev) hipLaunchKernelGGL((k_egress_ct<true, true>), grid, blk, 0, s, p, b, now, o, g);
         else hipLaunchKernelGGL((k_egress_ct<true, false>), grid, blk, 0, s, p, b, now, o, g);
     }

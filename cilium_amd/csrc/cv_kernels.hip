@@ -4,8 +4,8 @@
 // programs (Taeung/cilium v1.1.90) over a batch of frame records in HBM:
 //   k_xdp_prefilter    bpf/bpf_xdp.c:88-184                      (config 1)
 //   k_policy_ingress   bpf/bpf_netdev.c:128-153,357-398 +
-//                      bpf/lib/policy.h:217-329                   (config 2)
-//   k_netdev_front     bpf/bpf_netdev.c:357-524, bpf/lib/l3.h:247-276
+//                      bpf/lib/policy.h:46-163                   (config 2)
+//   k_netdev_front     bpf/bpf_netdev.c:357-524, bpf/lib/l3.h:103-132
 //   k_ct_stage         bpf/bpf_lxc.c:865-1038, bpf/lib/conntrack.h (config 3)
 // The egress path (config 5) is in cv_egress.hip; the shared device functions
 // (map probes, policy, conntrack, metrics, grouping) in cv_dev.hpp.  No MFMA: this
@@ -239,15 +239,67 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
 #endif
 
 // ================================================================== config 3
-// stage 1: XDP prefilter + from_netdev/handle_ipv4 up to the tail call into the
-// endpoint's policy program; packets reaching it join their address-pair group.
-#ifdef CV_NF_WPE               // A/B only
-#define CV_NF_OCC __attribute__((amdgpu_waves_per_eu(CV_NF_WPE, 8)))
-#else
-#define CV_NF_OCC
-#endif
+// handle_ipv6 of bpf_netdev (bpf_netdev.c:172-276; HANDLE_NS, FROM_HOST, no
+// ENCAP_IFINDEX, reverse_proxy6 with an empty cilium_proxy6 map) up to the tail call
+// into the endpoint's policy program.  Per-lane probes (IPv6 is the rare family on
+// this path).  Returns the verdict code of a packet that stops here; *stage: the
+// packet goes on to ipv6_policy; *rw: rewrite_dmac_to_host ran; *ldabs: icmp6_load_type
+// read past the packet, which ends the program with 0 (TC_ACT_OK, no notification).
+template <int NW>
+__device__ __forceinline__ int netdev_ipv6(const DpParams &p, const RecT<NW> &r, uint32_t &identity, Acct &a,
+                                           uint32_t &flowlabel, bool &stage, int64_t &slot, uint32_t &iv, bool &rw,
+                                           bool &ldabs)
+{
+    stage = rw = ldabs = false;
+    slot = -1;
+    iv = 0;
+    if (r.len < 54) return DROP_INVALID;                          // revalidate_data
+    uint32_t nh = rec_u8c<20>(r);
+    const int hl = ipv6_hdrlen(r, nh);
+    if (hl < 0) return hl;
+    const int l4 = 14 + hl;
+    const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
+    const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
+    if (nh == 58) {                                               // icmp6_handle (icmp6.h:390-412)
+        const int c = rec_chk(r, 54, 1);                          // icmp6_load_type: load_byte(ETH_HLEN + 40)
+        if (c == E_TRUNC) return E_TRUNC;
+        if (c) { ldabs = true; return TC_ACT_OK; }
+        const uint32_t type = rec_u8c<54>(r);
+        if (type == 135 || (type == 128 && eq4(da, p.router6))) return E_PUNT;   // NS / echo to the router
+    }
+    if (identity < HEALTH_ID) {                                   // identity_is_reserved (policy.h:46-49)
+        const uint32_t lab = ipcache6(p, sa, a);
+        if (lab && lab != CLUSTER_ID) identity = lab;
+    }
+    flowlabel = WORLD_ID;                                         // derive_sec_ctx (:50-64)
+    if (sa[0] == p.router6[0] && sa[1] == p.router6[1]) flowlabel = bswap32(rec_raw32c<14>(r)) & 0x000FFFFFu;
+    if (p.flags & F_FROM_HOST) {
+        flowlabel = identity;
+        const uint32_t nh0 = rec_u8c<20>(r);                      // reverse_proxy6 gets ip6->nexthdr
+        if (nh0 == 6 || nh0 == 17) {
+            const int c = rec_chk(r, l4, 4);
+            if (c) return chk_err(c, DROP_CT_INVALID_HDR);
+        }
+        rw = true;                                                // rewrite_dmac_to_host
+    }
+    if (!p.lxc6.buckets) return TC_ACT_OK;
+    a.nl++;                                                       // lookup_ip6_endpoint
+    slot = dev_find<LxcV6Spec>(p.lxc6, da, &iv);
+    if (slot < 0 || (iv & (1u << 16))) return TC_ACT_OK;          // not local / ENDPOINT_F_HOST
+    if (rec_u8c<21>(r) <= 1) return E_PUNT;                       // ipv6_l3: icmp6_send_time_exceeded
+    const uint32_t e = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
+    if (!e) return DROP_MISSED_TAIL_CALL;
+    stage = true;                                                 // ipv6_local_delivery -> handle_policy
+    return TC_ACT_OK;
+}
+
+constexpr uint64_t SALT_NETDEV6 = 0x4E45543600000000ULL;
+
+// stage 1: XDP prefilter + from_netdev -> handle_ipv4 / handle_ipv6 up to the tail call
+// into the endpoint's policy program; packets reaching it join their address-pair
+// group (IPv4 in Q_NETDEV, IPv6 in Q_NETDEV6).
 template <bool EV>
-__global__ void __launch_bounds__(BLOCK) CV_NF_OCC k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
+__global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
                                                         int with_prefilter)
 {
     __shared__ LdsMetrics lm;
@@ -266,7 +318,7 @@ __global__ void __launch_bounds__(BLOCK) CV_NF_OCC k_netdev_front(DpParams p, Ba
         uint8_t xv = XDP_PASS;
         int32_t ret = TC_ACT_OK, reason = 0;
         uint32_t ident = 0;
-        bool staged = false;
+        bool staged = false, v6stage = false, dmac_rw = false;
         if (with_prefilter) xv = xdp_verdict_q(p, r, a, live, st);
         const bool pass = live && xv == XDP_PASS;
         bool skip_proxy = false;
@@ -298,13 +350,14 @@ __global__ void __launch_bounds__(BLOCK) CV_NF_OCC k_netdev_front(DpParams p, Ba
                     const int c = rec_chk(r, l4, 4);
                     if (c) h = chk_err(c, DROP_CT_INVALID_HDR);
                 }
+                dmac_rw = h == TC_ACT_OK;                         // rewrite_dmac_to_host (:156-169)
             }
         }
         const bool want_lxc = v4 && h == TC_ACT_OK && p.lxc4.buckets;
         if (want_lxc) a.nl++;                                     // lookup_ip4_endpoint
         uint32_t iv = 0;
         uint32_t daddr = rec_raw32c<30>(r);
-        const int64_t lxc_slot = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv);
+        int64_t lxc_slot = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv);
         const bool lxc_hit = lxc_slot >= 0;
         if (pass && eth == 0x0008u) {
             if (r.len < 34) {
@@ -326,10 +379,24 @@ __global__ void __launch_bounds__(BLOCK) CV_NF_OCC k_netdev_front(DpParams p, Ba
                     }
                 }
             }
-            if (!staged) {
-                if (h == E_TRUNC) ret = h;
-                else if (is_err(h)) {                             // tail_handle_ipv4: send_drop_notify_error
-                    m.drop(h, r.len, METRIC_INGRESS);
+        } else if (pass && eth == 0xDD86u) {                      // handle_ipv6 (bpf_netdev.c:172-276)
+            uint32_t flowlabel = WORLD_ID;
+            bool ldabs;
+            h = netdev_ipv6(p, r, identity, a, flowlabel, v6stage, lxc_slot, iv, dmac_rw, ldabs);
+            ident = identity;
+            if (ldabs) { h = TC_ACT_OK; dmac_rw = false; }
+            if (v6stage) {
+                const uint32_t e = p.ep_of_lxc[iv & 0xFFFFu];
+                g.secctx[i] = flowlabel;
+                g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
+                if (EV) g.ifx[i] = (uint32_t)lxc_slot;
+            }
+        }
+        if ((pass && eth == 0x0008u) || (pass && eth == 0xDD86u)) {
+            if (!staged && !v6stage) {
+                if (h == E_TRUNC || h == E_PUNT) ret = h;
+                else if (is_err(h)) {                             // tail_handle_ipv4 / from_netdev:
+                    m.drop(h, r.len, METRIC_INGRESS);             // send_drop_notify_error
                     m.pkt = b.base + i;
                     m.hash = b.hash ? b.hash[i] : 0u;
                     notify_drop(p, m, h, r.len, 0, 0, 0, 0, 0);
@@ -342,10 +409,24 @@ __global__ void __launch_bounds__(BLOCK) CV_NF_OCC k_netdev_front(DpParams p, Ba
         if (staged) {                                             // group by (CT map, address pair)
             const EpDev &ep = p.eps[g.meta[i] & 0xFFFFu];
             group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
+        } else if (v6stage) {
+            const EpDev &ep = p.eps[g.meta[i] & 0xFFFFu];
+            const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
+            const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
+            group_push(g, group_node(g, pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets)), i,
+                       Q_NETDEV6);
         }
         if (!live) continue;
-        if (M::EV && o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
-        if (!staged) {
+        const bool fwd_here = !staged && !v6stage && ret == TC_ACT_OK;
+        if (M::EV && o.frames) {
+            uint8_t *fo = o.frames + (size_t)i * b.stride;
+            frame_copy(b.frames + (size_t)i * b.stride, fo, b.stride);
+            if (fwd_here && dmac_rw) {                            // the forwarded frame's new dmac
+                *reinterpret_cast<uint32_t *>(fo) = p.net_mac[0];
+                *reinterpret_cast<uint16_t *>(fo + 4) = (uint16_t)p.net_mac[1];
+            }
+        }
+        if (!staged && !v6stage) {
             g.gslot[i] = NONE;
             if (o.ret) o.ret[i] = ret;
             if (o.reason) o.reason[i] = reason;
@@ -404,15 +485,9 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     store_out(o, i, a);
 }
 
-#ifdef CV_CT_WPE               // A/B only: 121 VGPRs give 4 waves/SIMD already; 5 is slower
-#define CV_CT_OCC __attribute__((amdgpu_waves_per_eu(CV_CT_WPE, 8)))
-#else
-#define CV_CT_OCC
-#endif
-
 // stage 2: conntrack + policy, each address-pair group by one lane in packet order
 template <bool EV>
-__global__ void __launch_bounds__(BLOCK) CV_CT_OCC k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+__global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
@@ -420,14 +495,67 @@ __global__ void __launch_bounds__(BLOCK) CV_CT_OCC k_ct_stage(DpParams p, BatchD
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-#if CV_RUNS_MODE == 0
-    for_each_group(g, Q_NETDEV, [&](uint32_t, uint32_t head) {
-        group_in_order(g, head, 0, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
-    });
-#else
-    for_each_run<CV_RUNS_MODE != 2>(g, Q_NETDEV, false, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
-#endif
+    for_each_run<true>(g, Q_NETDEV, false, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
+}
+
+// stage 2 of an IPv6 packet: ipv6_local_delivery's tail call into the endpoint's
+// handle_policy -> tail_ipv6_policy -> ipv6_policy (bpf_lxc.c:721-862, 1003-1038)
+template <class M>
+__device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b, const OutDev &o,
+                                            const GroupScratch &g, uint32_t i, uint32_t now, M &m)
+{
+    Rec6 r;
+    rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
+    const uint32_t meta = g.meta[i];
+    const EpDev &ep = p.eps[meta & 0xFFFFu];
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    uint8_t ct = CT_NONE;
+    uint16_t proxy = 0;
+    int32_t reason = 0;
+    Skb6 s = skb6_from(r);
+    int64_t lslot = -1;                                          // the destination's cilium_lxc slot
+    if constexpr (M::EV) {
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+        lslot = (int32_t)g.ifx[i];
+    }
+    RevNat6Out rn;
+    rn.valid = false;
+    const int ret = handle_policy6(p, ep, s, g.secctx[i], (meta >> 16) & 1u,
+                                   ifindex_of(m, p.lxc6, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
+                                   a, m, &rn);
+    if (M::EV && o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
+        // ipv6_local_delivery's ipv6_l3, then ipv6_policy's rev-NAT index zeroing and reverse NAT
+        const uint8_t *in = b.frames + (size_t)i * b.stride;
+        Frame6 f;
+        frame6_init(f, r, s.l4off, s.nexthdr, in);
+        uint32_t mac[2], nmac[2];
+        lxc_macs(p.lxc6, lslot, mac, nmac);
+        frame6_l3(f, nmac, mac);
+        frame6_zero_revnat(f);
+        if (rn.valid) frame6_revnat(f, rn);
+        frame6_emit(f, in, o.frames + (size_t)i * b.stride, b.stride);
+    }
+    if (o.ret) o.ret[i] = ret;
+    if (o.reason) o.reason[i] = reason;
+    if (o.ct) o.ct[i] = ct;
+    if (o.proxy) o.proxy[i] = proxy;
+    store_out(o, i, a);
+}
+
+template <bool EV>
+__global__ void __launch_bounds__(BLOCK) k_ct_stage6(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+{
+    __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
+    MetT<EV> m;
+    pol_cache_init(pc);
+    met_init(m, lm);
+    m.pc = &pc;
+    for_each_run<true>(g, Q_NETDEV6, false, [&](uint32_t x) { stage2_one6(p, b, o, g, x, now, m); });
+    met_flush(m, p.metrics);
     pol_cache_flush(pc);
 }
 
@@ -724,12 +852,18 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
 {
     if (!b.n) return 0;
     const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
-    if (ev) hipLaunchKernelGGL(k_netdev_front<true>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, with_prefilter);
-    else hipLaunchKernelGGL(k_netdev_front<false>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, with_prefilter);
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
+    if (ev) hipLaunchKernelGGL(k_netdev_front<true>, grid, blk, 0, s, p, b, o, g, with_prefilter);
+    else hipLaunchKernelGGL(k_netdev_front<false>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     if (hipGetLastError() != hipSuccess) return -5;
-    if (CV_RUNS_MODE) launch_group_runs(g, Q_NETDEV, grid_for(b.n), runs_sched(CV_RUNS_MODE), s);
-    if (ev) hipLaunchKernelGGL(k_ct_stage<true>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, now);
-    else hipLaunchKernelGGL(k_ct_stage<false>, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o, g, now);
+    launch_group_runs(g, Q_NETDEV, grid.x, 1, s);
+    if (ev) hipLaunchKernelGGL(k_ct_stage<true>, grid, blk, 0, s, p, b, o, g, now);
+    else hipLaunchKernelGGL(k_ct_stage<false>, grid, blk, 0, s, p, b, o, g, now);
+    // the IPv6 groups after the IPv4 stage: their runs reuse `work` (the two families'
+    // conntrack state is disjoint, so the order between them is free)
+    launch_group_runs(g, Q_NETDEV6, grid.x, 1, s);
+    if (ev) hipLaunchKernelGGL(k_ct_stage6<true>, grid, blk, 0, s, p, b, o, g, now);
+    else hipLaunchKernelGGL(k_ct_stage6<false>, grid, blk, 0, s, p, b, o, g, now);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

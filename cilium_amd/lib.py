@@ -53,7 +53,8 @@ class EndpointCfg(C.Structure):
 
 class NodeCfg(C.Structure):
     _fields_ = [("ipv4_cluster_mask", C.c_uint32), ("ipv4_cluster_range", C.c_uint32),
-                ("ipv4_loopback", C.c_uint32), ("router_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6)]
+                ("ipv4_loopback", C.c_uint32), ("router_ip6", C.c_uint8 * 16), ("host_mac", C.c_uint8 * 6),
+                ("net_mac", C.c_uint8 * 6)]
 
 
 def _raw_be32(v):
@@ -252,10 +253,12 @@ class Ctx:
                           (C.c_uint8 * 6)(*bytes(node_mac)), -1 if ct6 is None else ct6.h)
         _check(load().cv_endpoint_config(self.h, ep, C.byref(cfg)), "cv_endpoint_config")
 
-    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=bytes(16), host_mac=bytes(6)):
+    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=bytes(16), host_mac=bytes(6),
+                    net_mac=bytes(6)):
         """node_config.h constants; the v4 words as host-order ints."""
         cfg = NodeCfg(_raw_be32(cluster_mask), _raw_be32(cluster_range), _raw_be32(loopback),
-                      (C.c_uint8 * 16)(*bytes(router_ip6)), (C.c_uint8 * 6)(*bytes(host_mac)))
+                      (C.c_uint8 * 16)(*bytes(router_ip6)), (C.c_uint8 * 6)(*bytes(host_mac)),
+                      (C.c_uint8 * 6)(*bytes(net_mac)))
         _check(load().cv_node_config(self.h, C.byref(cfg)), "cv_node_config")
 
     def sync(self):

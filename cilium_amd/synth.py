@@ -391,7 +391,13 @@ def ct_entries(n, now, ingress, tcp, src_sec_id, seen_non_syn=False, length=64) 
 
 def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A00003, now0: int = 1_000_000,
             n_cidrs: int = 102400, n_ids: int = 10000, n_ep: int = 4096, ct_max: Optional[int] = None,
-            ttl_low: float = 0.0005) -> Workload:
+            ttl_low: float = 0.0005, v6_frac: float = 0.0, stride: Optional[int] = None,
+            n_flows6: Optional[int] = None) -> Workload:
+    """Ingress through from_netdev into the endpoints' policy programs with conntrack.
+    v6_frac > 0 makes a dual-stack batch: that fraction of the packets becomes IPv6
+    (handle_ipv6 -> ipv6_policy with a global CT6 map, v6 endpoints in cilium_lxc, v6
+    ipcache entries), drawn after every IPv4 draw so the IPv4 part is unchanged;
+    records are then 128 bytes unless `stride` says otherwise."""
     s = Stream(seed)
     c1 = config1(16, n_ep=n_ep)
     c2 = config2(16, n_cidrs=n_cidrs, n_ids=n_ids)
@@ -464,8 +470,147 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     ttl = np.where(s.frac(n_pkts) < ttl_low, 1, 64)
     frames = ipv4_frames(saddr, daddr, proto, sport, dport, flags, ttl)
     eps = [{"lxc_id": int(i), "seclabel": int(0x1000 + i), "ip": int(lxc_ip[i - 1])} for i in ep_ids]
-    return Workload("config3", maps, frames, np.full(n_pkts, 64, np.uint32), np.zeros(n_pkts, np.uint32), eps,
-                    now=now0 + 1, extra={"kind": kind})
+    length = np.full(n_pkts, 64, np.uint32)
+    extra = {"kind": kind, "node": {"router_ip6": ROUTER_IP6, "host_mac": bytes(HOST_IFINDEX_MAC),
+                                    "net_mac": bytes(CILIUM_NET_MAC)}}
+    if v6_frac > 0:
+        stride = stride or 128
+        f6 = np.zeros((n_pkts, stride), np.uint8)
+        f6[:, :64] = frames
+        frames = f6
+        v6 = _config3_v6(s, maps, c2, frames, length, kind, eps, v6_frac, n_flows6 or max(n_flows // 4, 16), n_ep,
+                         now0, ct_max, pp, pr)
+        extra["v6"] = v6
+    elif stride and stride > 64:
+        f6 = np.zeros((n_pkts, stride), np.uint8)
+        f6[:, :64] = frames
+        frames = f6
+    return Workload("config3", maps, frames, length, np.zeros(n_pkts, np.uint32), eps, now=now0 + 1, extra=extra)
+
+
+HOST_IFINDEX_MAC = np.array([0xCE, 0x72, 0xA7, 0x03, 0x88, 0x56], np.uint8)    # bpf/node_config.h:39
+CILIUM_NET_MAC = np.array([0xCE, 0x72, 0xA7, 0x03, 0x88, 0x57], np.uint8)      # bpf/node_config.h:57
+
+
+def ct6_keys(daddr6, saddr6, dport, sport, nexthdr, flags) -> np.ndarray:
+    """struct ipv6_ct_tuple (bpf/lib/common.h:338-346), 40 bytes with 2 zero pad bytes."""
+    n = len(daddr6)
+    k = np.zeros((n, 40), np.uint8)
+    k[:, 0:16] = daddr6
+    k[:, 16:32] = saddr6
+    k[:, 32:34] = be16_bytes(np.asarray(dport, np.uint16))
+    k[:, 34:36] = be16_bytes(np.asarray(sport, np.uint16))
+    k[:, 36] = np.asarray(nexthdr, np.uint8)
+    k[:, 37] = np.asarray(flags, np.uint8)
+    return k
+
+
+def _config3_v6(s, maps, c2, frames, length, kind4, eps, v6_frac, n_flows6, n_ep, now0, ct_max, pp, pr):
+    """The IPv6 half of a dual-stack config 3 (see config3): tables and packets."""
+    n_pkts = len(length)
+    ep_idx = np.arange(n_ep)
+    ep_ip6 = v6_addrs(V6_POD_PREFIX, np.full(n_ep, 0x000A0000), (ep_idx + 0x100).astype(np.uint32) * 0x10001)
+    for e, a in zip(eps, ep_ip6):
+        e["ip6"] = bytes(a)
+    # cilium_lxc: the v6 endpoint addresses (same lxc ids / ifindexes) + the router as HOST
+    lk = maps["lxc"]
+    k6 = np.concatenate([endpoint_keys_v6(ep_ip6), endpoint_keys_v6(np.frombuffer(ROUTER_IP6, np.uint8)[None])])
+    v6v = np.concatenate([lk.vals[:n_ep], endpoint_infos([0], [0], [1])])
+    maps["lxc"] = MapSpec(lk.name, lk.type, 20, 48, lk.max_entries, np.concatenate([lk.keys, k6]),
+                          np.concatenate([lk.vals, v6v]))
+    # ipcache: remote v6 pods /128 and a few /64s -> identities of the config-2 id space
+    n_r6 = 4096
+    remote6 = v6_addrs(bytes([0x20, 0x01, 0x0D, 0xB8, 0, 0, 0, 7]), np.zeros(n_r6), np.arange(n_r6, dtype=np.uint32) + 1)
+    r_id = (256 + s.choice(n_r6, 10000)).astype(np.uint32)
+    nets = v6_addrs(bytes([0x20, 0x01, 0x0D, 0xB8, 0, 0, 0, 0]), np.zeros(64), np.zeros(64))
+    nets[:, 6:8] = be16_bytes(np.arange(64, dtype=np.uint16) + 0x100)
+    n_id = (256 + s.choice(64, 10000)).astype(np.uint32)
+    ik = c2.maps["ipcache"] if "ipcache" not in maps else maps["ipcache"]
+    maps["ipcache"] = MapSpec(ik.name, ik.type, 24, 8, ik.max_entries,
+                              np.concatenate([ik.keys, ipcache_keys_v6(remote6, np.full(n_r6, 128)),
+                                              ipcache_keys_v6(nets, np.full(64, 64))]),
+                              np.concatenate([ik.vals, remote_endpoint_infos(np.concatenate([r_id, n_id]))]))
+    # flows: remote (a /128 pod or an address in a /64) <-> local endpoint, CT6 preloaded
+    F = n_flows6
+    in_net = s.frac(F) < 0.3
+    rem = remote6[s.choice(F, n_r6)].copy()
+    netp = nets[s.choice(F, 64)].copy()
+    netp[:, 8:16] = s.u64(F).astype(">u8").view(np.uint8).reshape(F, 8)
+    rem = np.where(in_net[:, None], netp, rem)
+    epi = s.choice(F, n_ep)
+    loc = ep_ip6[epi]
+    sel = s.choice(F, len(pp))
+    fport = pp[sel].astype(np.int64)
+    fproto = pr[sel].astype(np.uint8)
+    eport = s.randint(F, 1024, 65536)
+    ing = s.frac(F) < 0.75
+    d = np.where(ing[:, None], rem, loc)
+    sa = np.where(ing[:, None], loc, rem)
+    keys = ct6_keys(d, sa, fport, eport, fproto, np.where(ing, 1, 0))
+    tcp = fproto == TCP
+    seclabel = np.array([e["seclabel"] for e in eps], np.uint32)
+    vals = ct_entries(F, now0, ing, tcp, np.where(ing, 0x300, seclabel[epi]), seen_non_syn=tcp, length=90)
+    rk = ct6_keys(d, sa, np.zeros(F), np.zeros(F), np.full(F, ICMPV6), np.where(ing, 3, 2))
+    rv = vals.copy()
+    rv[:, 36] |= 0x10
+    all_k = np.concatenate([keys, rk])
+    uniq, first = np.unique(all_k, axis=0, return_index=True)       # twins of one pair: keep one
+    cap = ct_max or max(1 << 16, 1 << int(np.ceil(np.log2(len(uniq) * 1.25 + n_pkts * v6_frac * 2 + 1))))
+    maps["ct6"] = MapSpec("cilium_ct6_global", MAP_LRU_HASH, 40, 56, cap, all_k[np.sort(first)],
+                          np.concatenate([vals, rv])[np.sort(first)])
+    # packets: which become IPv6, of which kind (forward / reply / new / odd cases)
+    v6 = s.frac(n_pkts) < v6_frac
+    i6 = np.nonzero(v6)[0]
+    m = len(i6)
+    if not m:
+        return v6
+    k = kind4[i6]
+    fi = np.nonzero(ing)[0][s.choice(m, max(int(ing.sum()), 1))] if ing.any() else s.choice(m, F)
+    fe = np.nonzero(~ing)[0][s.choice(m, max(int((~ing).sum()), 1))] if (~ing).any() else fi
+    f = np.where(k == 0, fi, fe)
+    src = rem[f].copy()
+    dst = loc[f].copy()
+    sport = np.where(k == 0, eport[f], fport[f])
+    dport = np.where(k == 0, fport[f], eport[f])
+    proto = fproto[f].copy()
+    new = k == 2
+    nn = int(new.sum())
+    src[new] = remote6[s.choice(nn, n_r6)]
+    dst[new] = ep_ip6[s.choice(nn, n_ep)]
+    sport[new] = s.randint(nn, 1024, 65536)
+    nsel = s.choice(nn, len(pp))
+    dport[new] = np.where(s.frac(nn) < 0.8, pp[nsel], s.randint(nn, 1, 65536))
+    proto[new] = pr[nsel]
+    rf = s.frac(m)
+    tflags = np.where(rf < 0.90, TCP_ACK, np.where(rf < 0.95, TCP_SYN, np.where(rf < 0.98, TCP_FIN | TCP_ACK, TCP_RST)))
+    hop = np.full(m, 64)
+    odd = s.frac(m)
+    icmp_t = np.where(s.frac(m) < 0.5, 128, 129)
+    proto = np.where(odd < 0.04, ICMPV6, proto).astype(np.uint8)                 # ICMPv6 echo / reply
+    ns = (odd >= 0.04) & (odd < 0.045)
+    proto[ns] = ICMPV6
+    icmp_t[ns] = 135                                                              # neighbour solicitation
+    to_rtr = (odd >= 0.045) & (odd < 0.05)
+    proto[to_rtr] = ICMPV6
+    icmp_t[to_rtr] = 128
+    dst[to_rtr] = np.frombuffer(ROUTER_IP6, np.uint8)                             # echo to the router
+    hop[(odd >= 0.05) & (odd < 0.055)] = 1
+    hbh = (odd >= 0.055) & (odd < 0.08)
+    world = (odd >= 0.08) & (odd < 0.10)                                          # not local: to the stack
+    dst[world, 0:2] = [0x20, 0x01]
+    frames[i6, :] = 0
+    full = ipv6_frames(src, dst, proto, sport, dport, tflags, hop, np.broadcast_to(NODE_MAC, (m, 6)),
+                       np.array([0x02, 0, 0, 0, 0, 1], np.uint8)[None].repeat(m, 0), icmp_type=icmp_t, hbh=hbh,
+                       stride=max(128, frames.shape[1]))
+    frames[i6] = full[:, :frames.shape[1]]                                        # (64-B records: truncated)
+    nh_odd = (odd >= 0.10) & (odd < 0.105)                                        # fragment / no-next-header
+    frames[i6[nh_odd], 20] = np.where(s.frac(int(nh_odd.sum())) < 0.5, 44, 59)
+    ln = np.full(m, 90, np.uint32)
+    short = (odd >= 0.105) & (odd < 0.11)
+    ln[short] = s.randint(int(short.sum()), 14, 70).astype(np.uint32)
+    ln[short & (proto == ICMPV6)] = 54                                            # icmp6_load_type past the end
+    length[i6] = ln
+    return v6
 
 
 # --------------------------------------------------------------------------

@@ -60,7 +60,7 @@ typedef struct cv_ctx cv_ctx;
 #define CV_ROLE_LB4_SERVICES 6  /* cilium_lb4_services lb4_key->lb4_service (lb.h:75-81) */
 #define CV_ROLE_LB6_SERVICES 7  /* cilium_lb6_services lb6_key->lb6_service (lb.h:43-49) */
 #define CV_ROLE_LB4_REVNAT  8   /* cilium_lb4_reverse_nat u16->lb4_reverse_nat (lb.h:67-73) */
-#define CV_ROLE_LB6_REVNAT  9   /* cilium_lb6_reverse_nat u16->lb6_reverse_nat (lb.h:37-41) */
+#define CV_ROLE_LB6_REVNAT  9   /* cilium_lb6_reverse_nat u16->lb6_reverse_nat (lb.h:38-44) */
 #define CV_NUM_ROLES        10
 
 /* ---- datapath options (compile-time #defines of the reference) ---- */
@@ -110,7 +110,7 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
 /* conntrack garbage collection: delete every entry of CT map h (ipv4_ct_tuple or
  * ipv6_ct_tuple keys, ct_entry values) whose lifetime < time; *deleted = count.
  * Replaces ctmap.GC(m, name, GCFilterByTime) / doGC4 / doGC6 and, with
- * time = 0xFFFFFFFF, ctmap.Flush (pkg/maps/ctmap/ctmap.go:325-455).  Runs on the GPU
+ * time = 0xFFFFFFFF, ctmap.Flush (pkg/maps/ctmap/ctmap.go:247-448).  Runs on the GPU
  * for a bound CT map, ordered after the batches already submitted. */
 int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
 
@@ -139,6 +139,7 @@ typedef struct {
     uint32_t ipv4_loopback;       /* IPV4_LOOPBACK      */
     uint8_t  router_ip6[16];      /* ROUTER_IP          */
     uint8_t  host_mac[6];         /* HOST_IFINDEX_MAC   */
+    uint8_t  net_mac[6];          /* CILIUM_NET_MAC: bpf_netdev's rewrite_dmac_to_host (FROM_HOST) */
 } cv_node_cfg;
 int cv_node_config(cv_ctx *ctx, const cv_node_cfg *cfg);
 
@@ -172,7 +173,7 @@ typedef struct {              /* any pointer may be NULL */
 /* config 1: bpf_xdp.c xdp_start over the batch */
 int cv_xdp_prefilter(cv_ctx *ctx, const cv_batch *b, cv_out *o, void *stream);
 /* config 2: ingress verdict of a NEW flow at endpoint `ep` (identity resolution of
- * bpf_netdev.c:357-398 + policy_can_access_ingress, policy.h:305-329) */
+ * bpf_netdev.c:357-398 + policy_can_access_ingress, policy.h:139-163) */
 int cv_policy_ingress(cv_ctx *ctx, int ep, const cv_batch *b, cv_out *o, void *stream);
 /* config 3: [xdp_start ->] from_netdev -> handle_ipv4 -> endpoint ipv4_policy with
  * conntrack, in packet order semantics; `now` = bpf_ktime_get_sec() of the batch */

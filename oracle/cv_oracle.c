@@ -356,11 +356,12 @@ int or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_t *
 }
 
 void or_dp_node_config(or_dp *dp, uint32_t mask, uint32_t range, uint32_t loopback, const uint8_t *router_ip6,
-                       const uint8_t *host_mac)
+                       const uint8_t *host_mac, const uint8_t *net_mac)
 {
     dp->v4_cluster_mask = mask; dp->v4_cluster_range = range; dp->v4_loopback = loopback;
     if (router_ip6) memcpy(dp->router_ip6, router_ip6, 16);
     if (host_mac) memcpy(dp->host_mac, host_mac, 6);
+    if (net_mac) memcpy(dp->net_mac, net_mac, 6);
 }
 
 int or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map *policy, or_map *ct4)
@@ -487,7 +488,7 @@ static or_endpoint_info *lookup_ip6_endpoint(or_dp *dp, const uint8_t *daddr, ui
     return or_map_lookup_ptr(dp->lxc, &k);
 }
 
-/* ipcache_lookup4 (bpf/lib/eps.h:309-319) with prefix = V4_CACHE_KEY_LEN (32):
+/* ipcache_lookup4 (bpf/lib/eps.h:68-86) with prefix = V4_CACHE_KEY_LEN (32):
  * key.lpm prefixlen = IPCACHE_PREFIX_LEN(32) = 32 static bits + 32. */
 static or_remote_endpoint_info *ipcache_lookup4(or_dp *dp, uint32_t addr, int prefix, uint8_t *nl)
 {
@@ -500,7 +501,7 @@ static or_remote_endpoint_info *ipcache_lookup4(or_dp *dp, uint32_t addr, int pr
     return or_map_lookup_ptr(dp->ipcache, &k);
 }
 
-/* ipcache_lookup6 (bpf/lib/eps.h:295-305) */
+/* ipcache_lookup6 (bpf/lib/eps.h:54-66) */
 static or_remote_endpoint_info *ipcache_lookup6(or_dp *dp, const uint8_t *addr, int prefix, uint8_t *nl)
 {
     if (!dp->ipcache) return NULL;
@@ -569,7 +570,7 @@ void or_xdp_prefilter(or_dp *dp, const uint8_t *frames, uint32_t stride, const u
 }
 
 /* ===================================================================== */
-/* Policy (bpf/lib/policy.h:217-329)                                      */
+/* Policy (bpf/lib/policy.h:46-200)                                      */
 /* ===================================================================== */
 
 static inline void ctr_add(or_policy_entry *p, uint32_t len)
@@ -578,7 +579,7 @@ static inline void ctr_add(or_policy_entry *p, uint32_t len)
     __atomic_fetch_add(&p->bytes, (uint64_t)len, __ATOMIC_RELAXED);
 }
 
-/* __policy_can_access (policy.h:217-285); cb[CB_POLICY] is always 0 on this path
+/* __policy_can_access (policy.h:51-119); cb[CB_POLICY] is always 0 on this path
  * (policy_clear_mark at bpf_lxc.c:881, bpf_clear_cb at bpf_lxc.c:679). */
 static int policy_can_access(or_map *map, uint32_t flags, uint32_t skb_len, uint32_t identity,
                              uint16_t dport, uint8_t proto, int dir, uint8_t *nl, uint8_t *nu)
@@ -604,7 +605,7 @@ static int policy_can_access(or_map *map, uint32_t flags, uint32_t skb_len, uint
     return OR_DROP_POLICY;
 }
 
-/* policy_can_access_ingress (policy.h:305-329) */
+/* policy_can_access_ingress (policy.h:139-163) */
 static int policy_can_access_ingress(or_map *map, uint32_t flags, uint32_t skb_len, uint32_t src,
                                      uint16_t dport, uint8_t proto, uint8_t *nl, uint8_t *nu)
 {
@@ -1149,7 +1150,7 @@ static int handle_ipv4(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_p
     uint32_t secctx = WORLD_ID;                        /* derive_ipv4_sec_ctx (:278-290) */
     uint8_t nexthdr = f[23];
     uint32_t saddr, daddr; memcpy(&saddr, f + 26, 4); memcpy(&daddr, f + 30, 4);
-    if (src_identity < HEALTH_ID) {                    /* identity_is_reserved (policy.h:212-215) */
+    if (src_identity < HEALTH_ID) {                    /* identity_is_reserved (policy.h:46-49) */
         or_remote_endpoint_info *info = ipcache_lookup4(dp, saddr, 32, &ps->nl);
         if (info && info->sec_label && info->sec_label != CLUSTER_ID && info->sec_label != HOST_ID)
             src_identity = info->sec_label;
@@ -1163,6 +1164,7 @@ static int handle_ipv4(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_p
             if (r == OR_E_TRUNC) return r;
             if (r) return OR_DROP_CT_INVALID_HDR;
         }
+        sst(skb, 0, 6, dp->net_mac);                   /* rewrite_dmac_to_host (:156-169) */
     }
     or_endpoint_info *ep = lookup_ip4_endpoint(dp, daddr, &ps->nl);
     if (ep) {
@@ -1177,6 +1179,9 @@ static int handle_ipv4(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_p
     }
     return OR_TC_ACT_OK;
 }
+
+static int handle_ipv6(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_proxy, uint32_t now,
+                       uint32_t *out_identity, pkt_state *ps, int *final, int32_t *reason);
 
 /* handle_identity_from_host (bpf_netdev.c:128-153) */
 static uint32_t identity_from_mark(uint32_t mark, int *skip_proxy)
@@ -1216,18 +1221,21 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
             uint16_t proto = 0;
             if (skb.avail >= 14) memcpy(&proto, skb.b + 12, 2);      /* skb->protocol */
             ident = identity;
-            if (proto == 0x0008) {
+            if (proto == 0x0008 || proto == 0xDD86) {
                 int final = 0;
-                int r = handle_ipv4(dp, &skb, identity, skip_proxy, now, &ident, &ps, &final, &reason);
-                if (r == OR_E_TRUNC || final) ret = r;
-                else if (IS_ERR(r)) {                        /* tail_handle_ipv4 (:457-466) */
+                /* IPv4: tail_handle_ipv4 (:457-466); IPv6: handle_ipv6 inline (:495-503) */
+                int r = proto == 0x0008 ? handle_ipv4(dp, &skb, identity, skip_proxy, now, &ident, &ps, &final, &reason)
+                                        : handle_ipv6(dp, &skb, identity, skip_proxy, now, &ident, &ps, &final, &reason);
+                if (r == OR_E_LDABS) ret = OR_TC_ACT_OK;         /* the program exited with 0 */
+                else if (r == OR_E_TRUNC || r == OR_E_PUNT || final) ret = r;
+                else if (IS_ERR(r)) {
                     update_metrics(dp, L, 1, (uint8_t)(-r));
                     notify_drop(dp, r, L, 0, 0, 0, 0, 0);        /* send_drop_notify_error */
                     reason = r;
                     ret = OR_TC_ACT_SHOT;
                 } else ret = r;
             } else {
-                ret = OR_TC_ACT_OK;                          /* IPv6 and others: to the stack here */
+                ret = OR_TC_ACT_OK;                          /* unknown traffic to the stack (:518-521) */
             }
         }
         if (out->xdp) out->xdp[i] = xv;
@@ -1354,7 +1362,7 @@ static or_lb4_service *lb4_lookup_slave(or_map *m, or_lb4_key *key, uint16_t sla
  * slave 0 is the master, so (hash % count) + 1; hash = get_hash_recalc(), an input */
 static inline uint16_t lb_select_slave(uint32_t hash, uint16_t count) { return (uint16_t)(hash % count + 1); }
 
-/* lb6_lookup_service (lb.h:334-368) with LB_L4 and LB_L3 (pkg/endpoint/bpf.go:193-194) */
+/* lb6_lookup_service (lb.h:351-380) with LB_L4 and LB_L3 (pkg/endpoint/bpf.go:193-194) */
 static or_lb6_service *lb6_lookup_service(or_map *m, or_lb6_key *key, uint8_t *nl)
 {
     or_lb6_service *svc;
@@ -1371,7 +1379,7 @@ static or_lb6_service *lb6_lookup_service(or_map *m, or_lb6_key *key, uint8_t *n
     return NULL;
 }
 
-/* lb6_lookup_slave (lb.h:370-384) */
+/* lb6_lookup_slave (lb.h:382-396) */
 static or_lb6_service *lb6_lookup_slave(or_map *m, or_lb6_key *key, uint16_t slave, uint8_t *nl)
 {
     key->slave = slave;
@@ -1379,7 +1387,7 @@ static or_lb6_service *lb6_lookup_slave(or_map *m, or_lb6_key *key, uint16_t sla
     return or_map_lookup_ptr(m, key);
 }
 
-/* ct_update4_slave / ct_update6_slave (conntrack.h:573-585, 649-661) */
+/* ct_update4_slave / ct_update6_slave (conntrack.h:572-586, 649-661) */
 static void ct_update_slave(or_map *map, const void *t, const or_ct_state *st, uint8_t *nl, uint8_t *nu)
 {
     (*nl)++;
@@ -1620,7 +1628,7 @@ static int ipv6_hdrlen(const or_skb *skb, int l3_off, uint8_t *nexthdr)
     return OR_DROP_INVALID_EXTHDR;
 }
 
-/* ipv6_ct_tuple_reverse (conntrack.h:264-284) */
+/* ipv6_ct_tuple_reverse (conntrack.h:265-285) */
 static void ct_tuple_reverse6(or_ipv6_ct_tuple *t)
 {
     uint8_t a[16]; memcpy(a, t->saddr, 16); memcpy(t->saddr, t->daddr, 16); memcpy(t->daddr, a, 16);
@@ -1628,7 +1636,7 @@ static void ct_tuple_reverse6(or_ipv6_ct_tuple *t)
     if (t->flags & TUPLE_F_IN) t->flags &= (uint8_t)~TUPLE_F_IN; else t->flags |= TUPLE_F_IN;
 }
 
-/* ct_lookup6 (conntrack.h:286-412) */
+/* ct_lookup6 (conntrack.h:288-412) */
 static int ct_lookup6(or_map *ct, or_ipv6_ct_tuple *t, const or_skb *skb, int off, int dir, or_ct_state *st,
                       uint32_t now, uint32_t flags, uint8_t *nl, uint8_t *nu, int *mon)
 {
@@ -1688,7 +1696,7 @@ static int ct_lookup6(or_map *ct, or_ipv6_ct_tuple *t, const or_skb *skb, int of
     return ret;
 }
 
-/* ct_create6 (conntrack.h:589-639) */
+/* ct_create6 (conntrack.h:588-639) */
 static int ct_create6(or_map *ct, const or_ipv6_ct_tuple *t, uint32_t skb_len, int dir, const or_ct_state *st,
                       uint32_t now)
 {
@@ -1883,7 +1891,64 @@ drop:
     return OR_TC_ACT_SHOT;
 }
 
-/* handle_ipv6 (bpf_lxc.c:354-380) + ipv6_l3_from_lxc (:82-352), direct routing */
+/* handle_ipv6 of bpf_netdev (bpf/bpf_netdev.c:172-276), HANDLE_NS and FROM_HOST as in
+ * netdev_config.h, ENCAP_IFINDEX paths (overlay) disabled, reverse_proxy6 (:66-125)
+ * with an empty cilium_proxy6 map (L7 out of scope).  As handle_ipv4: *final = 1 once
+ * the endpoint's policy program ran (its verdict is final). */
+static int handle_ipv6(or_dp *dp, or_skb *skb, uint32_t src_identity, int skip_proxy, uint32_t now,
+                       uint32_t *out_identity, pkt_state *ps, int *final, int32_t *reason)
+{
+    *final = 0;
+    *out_identity = src_identity;
+    if (skb->len < ETH_HLEN + 40) return OR_DROP_INVALID;          /* revalidate_data */
+    uint8_t nexthdr = skb->b[20];
+    int hdrlen = ipv6_hdrlen(skb, ETH_HLEN, &nexthdr);
+    if (hdrlen < 0) return hdrlen;
+    int l4_off = ETH_HLEN + hdrlen;
+    if (nexthdr == 58) {                                           /* HANDLE_NS: icmp6_handle (icmp6.h:390-412) */
+        uint8_t type;                                              /* icmp6_load_type: load_byte(nh_off + 40) */
+        int r = sld(skb, ETH_HLEN + 40, 1, &type);
+        if (r == OR_E_TRUNC) return r;
+        if (r) return OR_E_LDABS;
+        if (type == 135) return OR_E_PUNT;                         /* icmp6_handle_ns: tail call */
+        if (type == 128 && !memcmp(skb->b + 38, dp->router_ip6, 16)) return OR_E_PUNT;   /* icmp6_send_echo_reply */
+    }
+    if (src_identity < HEALTH_ID) {                                /* identity_is_reserved (policy.h:46-49) */
+        or_remote_endpoint_info *info = ipcache_lookup6(dp, skb->b + 22, 128, &ps->nl);
+        if (info && info->sec_label && info->sec_label != CLUSTER_ID) src_identity = info->sec_label;
+    }
+    *out_identity = src_identity;
+    uint32_t flowlabel = WORLD_ID;                                 /* derive_sec_ctx (:50-64) */
+    if (!memcmp(skb->b + 22, dp->router_ip6, 8)) {                 /* ipv6_match_prefix_64 (ipv6.h:166-175) */
+        uint32_t w; memcpy(&w, skb->b + ETH_HLEN, 4);
+        flowlabel = bswap32(w) & 0x000FFFFFu;                      /* bpf_ntohl(*tmp & IPV6_FLOWLABEL_MASK) */
+    }
+    if (dp->flags & OR_F_FROM_HOST) {
+        flowlabel = src_identity;
+        const uint8_t nh0 = skb->b[20];                            /* reverse_proxy6 gets ip6->nexthdr */
+        if (nh0 == 6 || nh0 == 17) {                               /* port load at l4_off (:79-89) */
+            uint8_t p[4];
+            int r = sld(skb, l4_off, 4, p);
+            if (r == OR_E_TRUNC) return r;
+            if (r) return OR_DROP_CT_INVALID_HDR;
+        }
+        sst(skb, 0, 6, dp->net_mac);                               /* rewrite_dmac_to_host (:156-169) */
+    }
+    or_endpoint_info *ep = lookup_ip6_endpoint(dp, skb->b + 38, &ps->nl);
+    if (ep) {
+        if (ep->flags & 1) return OR_TC_ACT_OK;                    /* ENDPOINT_F_HOST */
+        /* ipv6_local_delivery (l3.h:71-101): ipv6_l3 -> hop limit, MACs */
+        int rl3 = ipv6_l3(skb, ep->node_mac, ep->mac);
+        if (rl3 != OR_TC_ACT_OK) return rl3;
+        or_endpoint_prog *prog = find_ep(dp, ep->lxc_id);
+        if (!prog) return OR_DROP_MISSED_TAIL_CALL;               /* tail_call(cilium_policy, lxc_id) missed */
+        *final = 1;
+        return handle_policy(dp, prog, skb, ep->ifindex, flowlabel, skip_proxy, now, ps, reason);
+    }
+    return OR_TC_ACT_OK;
+}
+
+/* handle_ipv6 (bpf_lxc.c:360-387) + ipv6_l3_from_lxc (:82-352), direct routing */
 static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t hash, uint32_t now,
                                 uint32_t *dst_id, pkt_state *ps, int *final, int32_t *reason)
 {
@@ -1910,7 +1975,7 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     ret = ipv6_hdrlen(skb, ETH_HLEN, &t.nexthdr);
     if (ret < 0) return ret;
     int l4_off = ETH_HLEN + ret;
-    memcpy(key.address, t.daddr, 16);                               /* lb6_extract_key (lb.h:317-332) */
+    memcpy(key.address, t.daddr, 16);                               /* lb6_extract_key (lb.h:334-349) */
     ret = extract_l4_port(skb, t.nexthdr, l4_off, &key.dport);
     if (ret == OR_E_TRUNC) return ret;
     if (IS_ERR(ret)) {

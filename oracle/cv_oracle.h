@@ -63,6 +63,9 @@ extern "C" {
 /* oracle-only: the packet left this path through a tail call into a responder
  * program outside it (ARP / ICMPv6 NS / echo-to-router / hop-limit-exceeded) */
 #define OR_E_PUNT                 -2
+/* oracle-internal, never an output: a load_byte() (BPF_LD_ABS) past the packet ended
+ * the program, which then returns 0 (TC_ACT_OK) with no notification */
+#define OR_E_LDABS                -3
 /* skb_load_bytes() failure as the BPF helper reports it (-EFAULT) */
 #define OR_E_FAULT                -14
 
@@ -181,12 +184,13 @@ typedef struct or_dp {
     or_map *lxc;             /* cilium_lxc  (maps.h:27-33) */
     or_map *ipcache;         /* cilium_ipcache (maps.h:151-158) */
     or_map *lb4_services, *lb6_services;
-    or_map *lb4_revnat, *lb6_revnat;   /* cilium_lb{4,6}_reverse_nat (lb.h:37-65) */
+    or_map *lb4_revnat, *lb6_revnat;   /* cilium_lb{4,6}_reverse_nat (lb.h:37-68) */
     uint32_t flags;
     /* node_config.h constants (raw network-order words) */
     uint32_t v4_cluster_mask, v4_cluster_range, v4_loopback;
     uint8_t  router_ip6[16];
     uint8_t  host_mac[6];             /* HOST_IFINDEX_MAC */
+    uint8_t  net_mac[6];              /* CILIUM_NET_MAC (node_config.h:57): rewrite_dmac_to_host */
     uint32_t n_ep;
     or_endpoint_prog ep[OR_MAX_EP];   /* tail-call targets of cilium_policy (maps.h:44-51) */
     uint16_t ep_of_lxc[65536];        /* lxc_id -> index + 1 */
@@ -207,9 +211,10 @@ int    or_dp_add_endpoint(or_dp *dp, uint16_t lxc_id, uint32_t seclabel, or_map 
 /* the endpoint program's lxc_config.h constants and its CT_MAP6 */
 int    or_dp_endpoint_config(or_dp *dp, uint32_t ep, uint32_t ipv4, const uint8_t *ipv6, const uint8_t *mac,
                              const uint8_t *node_mac, or_map *ct6);
-/* node_config.h: IPV4_CLUSTER_MASK / IPV4_CLUSTER_RANGE / IPV4_LOOPBACK / ROUTER_IP */
+/* node_config.h: IPV4_CLUSTER_MASK / IPV4_CLUSTER_RANGE / IPV4_LOOPBACK / ROUTER_IP /
+ * HOST_IFINDEX_MAC / CILIUM_NET_MAC (NULL macs leave them zero) */
 void   or_dp_node_config(or_dp *dp, uint32_t v4_cluster_mask, uint32_t v4_cluster_range, uint32_t v4_loopback,
-                         const uint8_t *router_ip6, const uint8_t *host_mac);
+                         const uint8_t *router_ip6, const uint8_t *host_mac, const uint8_t *net_mac);
 void   or_dp_metrics(const or_dp *dp, uint64_t *out /* [256][4][2] */);
 /* attach a record buffer (NULL detaches); returns and resets nothing: see or_dp_notify_count */
 void   or_dp_notify_attach(or_dp *dp, or_drop_notify *buf, uint32_t cap);
@@ -239,14 +244,15 @@ void or_xdp_prefilter(or_dp *dp, const uint8_t *frames, uint32_t stride, const u
                       uint32_t n, or_out *out);
 
 /* Config 2: ingress verdict of a NEW flow for one endpoint: netdev identity resolution
- * (bpf_netdev.c:357-398) + policy_can_access_ingress (policy.h:305-329) with the L4
+ * (bpf_netdev.c:357-398) + policy_can_access_ingress (policy.h:139-163) with the L4
  * key as ct_lookup4 leaves it (conntrack.h:442-562) on a CT miss.  Parallel (OpenMP)
  * with atomic policy counters. */
 void or_policy_ingress(or_dp *dp, uint32_t ep_index, const uint8_t *frames, uint32_t stride,
                        const uint32_t *len, const uint32_t *mark, uint32_t n, or_out *out);
 
-/* Config 3: full ingress path: [XDP prefilter] -> from_netdev/handle_ipv4 -> tail call
- * into the endpoint's ipv4_policy (CT lookup/create, policy).  Sequential, as one CPU. */
+/* Config 3: full ingress path: [XDP prefilter] -> from_netdev -> handle_ipv4 (tail call)
+ * or handle_ipv6 -> tail call into the endpoint's ipv{4,6}_policy (CT lookup/create,
+ * policy).  Sequential, as one CPU. */
 void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
                        const uint32_t *mark, uint32_t n, uint32_t now, int with_prefilter, or_out *out);
 

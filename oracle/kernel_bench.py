@@ -4,7 +4,7 @@ INFRASTRUCTURE; only bench.py's cpu_baseline leg calls it).
 SURVEY.md §8(d) "CPU timing on the GPU box, same run", item (a): the hand-assembled
 eBPF restatements of oracle/kernel_golden.py (config 1: bpf_xdp.c:88-184 as an XDP
 program; config 2: the ingress identity + policy verdict, bpf_netdev.c:128-153,375-398
-and policy.h:217-329, as a SCHED_CLS program) are loaded with the bench's full-size
+and policy.h:46-163, as a SCHED_CLS program) are loaded with the bench's full-size
 tables in real kernel maps (LPM_TRIE ipcache / prefilter, HASH policy and cilium_lxc)
 and run by BPF_PROG_TEST_RUN over a bounded sample of the bench's own packets, one
 thread per host core, each pinned and over a disjoint slice.  Reported:

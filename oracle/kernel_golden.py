@@ -11,7 +11,7 @@ tests/golden/.  Three pins for the oracle:
     over synthetic frames with real kernel LPM + HASH + cilium_lxc maps;
   * config 2: a hand-assembled SCHED_CLS restatement of the ingress verdict
     (bpf_netdev.c:128-153 identity from mark, :375-398 ipcache resolution,
-    conntrack.h:471-530 L4 key of a NEW flow, policy.h:217-329 policy with
+    conntrack.h:471-530 L4 key of a NEW flow, policy.h:46-163 policy with
     __sync_fetch_and_add counters) by BPF_PROG_TEST_RUN with skb->mark in ctx_in.
 
 Usage: python -m oracle.kernel_golden   (from the repo root)
@@ -239,7 +239,7 @@ def policy_prog(ipcache, policy, outmap):
     a.stxw(FP, -12, R3)                # save dport
     a.stxw(FP, -16, R4)                # save proto
     a.ldxw(R9, R6, 0)                  # skb->len
-    # __policy_can_access (policy.h:217-285), HAVE_L4_POLICY
+    # __policy_can_access (policy.h:51-119), HAVE_L4_POLICY
     a.ld_map(R1, policy.fd); a.mov(R2, FP); a.addi(R2, -8); a.call(MAP_LOOKUP)
     a.jnei(R0, 0, "hit_l4")
     a.sth(FP, -4, 0); a.stb(FP, -2, 0)

@@ -59,7 +59,7 @@ def lib():
         L.or_netdev_ingress.argtypes = [vp, vp, u32, vp, vp, u32, u32, i32, vp]
         L.or_ct_create4.argtypes = [vp, vp, u32, i32, vp, u32]
         L.or_dp_endpoint_config.argtypes = [vp, u32, u32, vp, vp, vp, vp]
-        L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp, vp]
+        L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp, vp, vp]
         L.or_csum_apply.argtypes = [vp, u32, u32, u32, u32, u32, u32, vp]
         L.or_lxc_egress.argtypes = [vp, vp, u32, vp, vp, u32, vp, u32, u32, vp]
         L.or_dp_notify_attach.argtypes = [vp, vp, u32]
@@ -189,12 +189,13 @@ class ODp:
         if r:
             raise OSError(-r, "or_dp_endpoint_config")
 
-    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=b"\0" * 16, host_mac=b"\0" * 6):
+    def node_config(self, cluster_mask=0, cluster_range=0, loopback=0, router_ip6=b"\0" * 16, host_mac=b"\0" * 6,
+                    net_mac=b"\0" * 6):
         """node_config.h constants; the v4 words as host-order ints (written in network order)."""
         import struct
         raw = [struct.unpack("<I", struct.pack(">I", v))[0] for v in (cluster_mask, cluster_range, loopback)]
         lib().or_dp_node_config(self.h, *raw, C.create_string_buffer(bytes(router_ip6), 16),
-                                C.create_string_buffer(bytes(host_mac), 6))
+                                C.create_string_buffer(bytes(host_mac), 6), C.create_string_buffer(bytes(net_mac), 6))
 
     def notify_attach(self, capacity):
         """Record drop notifications (send_drop_notify) into a host ring."""

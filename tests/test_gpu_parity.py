@@ -275,10 +275,13 @@ def check_ingress(w, dev, batches, with_prefilter=True, trace_agg=0, events=True
         assert (tr["subtype"] >= 5).any() == (trace_agg == 0)                # FROM_* hidden at >= 1
     assert (ctx.metrics() == dp.metrics()).all()
     check_policy_maps(pm["policy"], om["policy"])
-    ck, cv = pm["ct4"].dump()
-    ok, ov = om["ct4"].dump()
-    assert len(ck) == len(ok)
-    assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
+    for name in ("ct4", "ct6"):
+        if name not in pm:
+            continue
+        ck, cv = pm[name].dump()
+        ok, ov = om[name].dump()
+        assert len(ck) == len(ok), name
+        assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), name
     return dp
 
 
@@ -314,6 +317,32 @@ def test_config3_icmp_and_options(dev):
     w.frames[other, 23] = 47
     check_ingress(w, dev, batches=2)
     check_ingress(w, dev, batches=1, with_prefilter=False)
+
+
+def _proxy_marks(w, seed):
+    """FROM_HOST marks: host, proxy-ingress (skip_proxy) and proxy-egress identities"""
+    s = synth.Stream(seed)
+    r = s.frac(w.n)
+    w.mark[:] = np.where(r < 0.03, 0xC00, np.where(r < 0.06, (300 << 16) | 0xA00,
+                                                   np.where(r < 0.08, (301 << 16) | 0xB00, 0)))
+
+
+def test_config3_dual_stack(dev):
+    """from_netdev with IPv6 frames: handle_ipv6 (ipcache6 identity, derive_sec_ctx,
+    reverse_proxy6's port load, rewrite_dmac_to_host, ICMPv6 NS / echo to the router,
+    hop limit, extension headers) -> ipv6_local_delivery -> ipv6_policy with CT6,
+    beside the IPv4 path; CT4 and CT6 tables, frames, notifications compared."""
+    w = synth.config3(1 << 16, 1 << 13, n_ep=256, n_cidrs=4096, n_ids=500, seed=23, v6_frac=0.4)
+    _proxy_marks(w, 5)
+    check_ingress(w, dev, batches=3)
+    check_ingress(w, dev, batches=1, with_prefilter=False, events=False)
+
+
+def test_config3_dual_stack_64b_records(dev):
+    """IPv6 frames in 64-B records: the reads past byte 64 (TCP flags at 67, extension
+    headers) end in E_TRUNC on both sides; UDP / ICMPv6 complete."""
+    w = synth.config3(1 << 15, 1 << 12, n_ep=128, n_cidrs=2048, n_ids=300, seed=29, v6_frac=0.5, stride=64)
+    check_ingress(w, dev, batches=2, with_prefilter=False)
 
 
 def test_ct_map_api_on_device(dev):

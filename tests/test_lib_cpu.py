@@ -88,7 +88,7 @@ def test_bind_checks_layouts():
 
 def test_ct_gc_host_store_vs_oracle():
     """ctmap.GC(GCFilterByTime) on an unbound CT map (host store) against the oracle's
-    restatement of doFiltering (pkg/maps/ctmap/ctmap.go:400-408), then Flush."""
+    restatement of doFiltering (pkg/maps/ctmap/ctmap.go:401-410), then Flush."""
     from cilium_amd import synth
     from oracle.oracle import OMap
     w = synth.config3(256, 4096, n_ep=8, n_cidrs=256, n_ids=20, seed=5)

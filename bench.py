@@ -2,14 +2,24 @@
 """Benchmark of the MI355X batch verdict engine (BASELINE.json metric).
 
 A step = one pass of the verdict path over one batch of synthetic packets already
-resident in HBM.  Default workload = BASELINE.json configs[1] (config 2): ipcache
-LPM (102,401 CIDRs -> identities) + policymap (10k identities x 8 L4 ports + L3 +
-wildcards, 81,055 entries) ingress verdicts on 2^24 64-B IPv4 headers per step, one
-MI355X per rank.  --workload config1 / config3 measure the other paths.
+resident in HBM.  Default workload = config 3, the largest single-GPU 64-B config:
+the full bpf_lxc ingress path (XDP prefilter -> from_netdev -> handle_ipv4 ->
+endpoint ipv4_policy with conntrack) over 2^24 64-B IPv4 headers per step against a
+16M-flow conntrack table, on one MI355X per rank.  --workload config1 / config2 /
+config4 / config5 measure the other paths.
+
+Stateful workloads (conntrack: configs 3, 4, 5) give every step its own batch: step v
+is the batch with fresh client ports on its new flows (synth.port_variant), so every
+timed step creates the conntrack entries the workload's new flows need instead of
+replaying flows an earlier pass created.  The batches are built on the device before
+the timed region; the CT tables are sized for every create of the run.  The
+accounting pass (L(p), U(p) of SURVEY.md §8(d)) is one more such step after the
+timed region.
 
 Multi-GPU (torchrun): tables are replicated, every rank verdicts its own batch
-(weak scaling, no data-path collective); cilium_metrics is summed across ranks
-with one RCCL all_reduce after the timed region.
+(weak scaling, no data-path collective); config 4 shards conntrack by address pair
+(cilium_amd.shard); cilium_metrics is summed across ranks with one RCCL all_reduce
+after the timed region.
 
 Prints ONE JSON line (rank 0).
 """
@@ -19,6 +29,7 @@ import argparse
 import hashlib
 import json
 import os
+import platform
 import sys
 import time
 
@@ -31,14 +42,16 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 T
 METRIC = "Mpps verdicts at 1/2/4/8 GPUs (64B hdrs); achieved HBM GB/s vs peak"
 
 WORKLOADS = {
+    "config3": "full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + ct_lookup4/ct_create4, 16M-flow CT, "
+               "a fresh batch per step (20% new flows)",
     "config2": "ipcache LPM (100k CIDRs->identities) + policymap (10k identities x L4 ports) ingress verdicts",
     "config1": "bpf_xdp.c CIDR deny-list prefilter, 1k IPv4 prefixes + cilium_lxc",
-    "config3": "full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + ct_lookup4/ct_create4, 16M-flow CT",
     "config4": "config 3 per GPU with conntrack sharded by address pair (16M flows per GPU, 128M on 8), "
                "RCCL all_reduce of cilium_metrics",
     "config5": "dual-stack from-container egress: lb4/lb6 (50k services) + CT4/CT6 + egress policy + local delivery "
-               "(v4 64-B and v6 128-B records, 1:1)",
+               "(v4 64-B and v6 128-B records, 1:1), a fresh batch per step (20% of flows new)",
 }
+STATEFUL = ("config3", "config4", "config5")
 
 
 def log(*a):
@@ -46,16 +59,12 @@ def log(*a):
 
 
 def lib_sha():
-    """the device code the PMC summaries were taken with (cilium_amd/build.py kernel_sha);
-    an A/B library (CV_LIB) is keyed by its own file hash"""
-    from cilium_amd import build, lib
-    if os.environ.get("CV_LIB"):
-        with open(lib.LIB_PATH, "rb") as f:
-            return hashlib.sha256(f.read()).hexdigest()[:16]
+    """the device code the PMC summaries were taken with (cilium_amd/build.py kernel_sha)"""
+    from cilium_amd import build
     return build.kernel_sha()
 
 
-def make_workload(name, n, rank):
+def make_workload(name, n, rank, world):
     from cilium_amd import synth
     if name == "config2":
         return synth.config2(n)
@@ -71,17 +80,35 @@ def make_workload(name, n, rank):
     raise SystemExit(f"unknown workload {name}")
 
 
+def size_conntrack(name, w, passes):
+    """max_entries of the CT maps for a run of `passes` fresh batches: today's entries
+    plus every create the run can make (config 3: the tuple and its RELATED twin per
+    new-flow packet; config 5: up to 7 entries per fresh flow over the families), with
+    room, as a power of two."""
+    def p2(x):
+        return 1 << int(np.ceil(np.log2(max(x, 1 << 16))))
+    if name in ("config3", "config4"):
+        nn = int((w.extra["kind"] == 2).sum())
+        ct = w.maps["ct4"]
+        ct.max_entries = p2((len(ct.keys) + 2 * nn * (passes + 1)) * 1.2)
+    elif name == "config5":
+        for fam in ("ct4", "ct6"):
+            w.maps[fam].max_entries = p2(0.9 * w.n + 0.45 * w.n * passes)
+
+
 def split_families(w):
     """config 5: the v4 packets as 64-B records and the v6 packets as 128-B records
-    (two launches per step; v4 and v6 state are disjoint, so order between them is free)."""
-    import numpy as np
+    (two launches per step; v4 and v6 state are disjoint, so order between them is free).
+    Returns the parts and, per packet of w, (part index, row in part)."""
     v6 = w.extra["v6"]
-    parts = []
-    for sel, stride in ((~v6, 64), (v6, 128)):
+    parts, where = [], np.zeros((w.n, 2), np.int64)
+    for k, (sel, stride) in enumerate(((~v6, 64), (v6, 128))):
         idx = np.nonzero(sel)[0]
+        where[idx, 0] = k
+        where[idx, 1] = np.arange(len(idx))
         parts.append({"frames": np.ascontiguousarray(w.frames[idx, :stride]), "length": w.length[idx],
                       "src_ep": w.extra["src_ep"][idx], "flow_hash": w.extra["flow_hash"][idx]})
-    return parts
+    return parts, where
 
 
 def algorithmic_bytes(name, nl, nu, record=64):
@@ -92,43 +119,76 @@ def algorithmic_bytes(name, nl, nu, record=64):
     return n * (R + V) + 64 * (int(nl.astype(np.int64).sum()) + int(nu.astype(np.int64).sum()))
 
 
+def host_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "kernel": platform.release()}
+
+
 def cpu_baseline(name, w, min_seconds=10.0):
-    """The oracle (plain-C restatement) timed on the host cores on a bounded sample
-    of the same workload (>= min_seconds of CPU work): OpenMP over the cores for the
-    stateless paths (configs 1, 2), one thread in packet order for the stateful ones
-    (conntrack: configs 3-5), re-running the sample until the time is reached."""
+    """The oracle (plain-C restatement) timed on the host cores on a bounded sample of
+    the same workload (>= min_seconds of CPU work).  Stateless paths (configs 1, 2):
+    OpenMP over the threads.  Conntrack ingress (configs 3, 4): the sample partitioned
+    by address pair over the threads, one oracle datapath per shard with its CT shard
+    (tests/harness.ShardedOracle; identical results to one sequential run).  Egress
+    (config 5): one thread in packet order.  Stateful samples are re-run as fresh
+    steps (synth.port_variant), as on the GPU."""
+    from cilium_amd import synth
     from tests import harness as H
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    sample = min(w.n, 1 << 21)
-    dp, _ = H.oracle_dp(w)
-    frames, length, mark = w.frames[:sample], w.length[:sample], w.mark[:sample]
-    if name == "config1":
-        run = lambda: dp.xdp_prefilter(frames, length)
-    elif name == "config2":
-        run = lambda: dp.policy_ingress(0, frames, length, mark)
-    elif name == "config5":
-        sample = min(sample, 1 << 18)
-        src, fh = w.extra["src_ep"][:sample], w.extra["flow_hash"][:sample]
-        frames, length = frames[:sample], length[:sample]
-        run = lambda: dp.lxc_egress(frames, length, src, fh, now=w.now)
+    done, busy, v = 0, 0.0, 0
+    if name in ("config1", "config2"):
+        sample = min(w.n, 1 << 21)
+        dp, _ = H.oracle_dp(w)
+        frames, length, mark = w.frames[:sample], w.length[:sample], w.mark[:sample]
+        run = (lambda: dp.xdp_prefilter(frames, length)) if name == "config1" else \
+              (lambda: dp.policy_ingress(0, frames, length, mark))
+        while busy < min_seconds:
+            t0 = time.perf_counter()
+            run()
+            busy += time.perf_counter() - t0
+            done += sample
+        cores, how = threads, f"OpenMP {threads} threads"
     else:
-        sample = min(sample, 1 << 18)
-        frames, length, mark = frames[:sample], length[:sample], mark[:sample]
-        run = lambda: dp.netdev_ingress(frames, length, mark, now=w.now)
-    # stateful paths re-run the same sample: later passes see the flows the first created
-    done, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        done += sample
-        el = time.perf_counter() - t0
-        if el >= min_seconds:
-            break
-    seq = name in ("config3", "config4", "config5")
-    return {"value": round(done / el / 1e6, 3), "unit": "Mpps", "cores": 1 if seq else threads,
-            "kind": "port",
-            "sample": f"oracle/cv_oracle.c over {done} packets of the same synthetic {name} batch "
-                      f"({el:.1f} s, {'1 thread, sequential (stateful path)' if seq else 'OpenMP ' + str(threads) + ' threads'})"}
+        import copy
+        from concurrent.futures import ThreadPoolExecutor
+        sample = min(w.n, 1 << 20 if name != "config5" else 1 << 18)
+        sw = copy.copy(w)
+        sw.frames, sw.length, sw.mark = w.frames[:sample], w.length[:sample], w.mark[:sample]
+        sw.extra = {k: (x[:sample] if isinstance(x, np.ndarray) and len(x) == w.n else x) for k, x in w.extra.items()}
+        if name == "config5":
+            dp, _ = H.oracle_dp(sw)
+            cores, how = 1, "1 thread, sequential (egress conntrack groups are not address pairs)"
+            while busy < min_seconds:
+                v += 1
+                f = H.apply_variant(sw.frames, *synth.port_variant(sw, v))
+                t0 = time.perf_counter()
+                dp.lxc_egress(f, sw.length, sw.extra["src_ep"], sw.extra["flow_hash"], now=w.now + v)
+                busy += time.perf_counter() - t0
+                done += sample
+        else:
+            so = H.ShardedOracle(sw, threads)
+            pool = ThreadPoolExecutor(threads)
+            cores, how = threads, f"{threads} threads, one address-pair CT shard each"
+            while busy < min_seconds:
+                v += 1
+                f = H.apply_variant(sw.frames, *synth.port_variant(sw, v))
+                _, el = so.netdev_ingress(f, now=w.now + v, pool=pool)
+                busy += el
+                done += sample
+            pool.shutdown()
+    return {"value": round(done / busy / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
+            "sample": f"oracle/cv_oracle.c over {done} packets of the synthetic {name} batch ({v or 1} "
+                      f"step{'s' if v > 1 else ''} of {done // max(v, 1)}; {busy:.1f} s; {how})",
+            "host": dict(host_info(), threads_used=cores)}
 
 
 def random_access_peak():
@@ -148,7 +208,7 @@ def random_access_peak():
 
 
 def pmc_traffic(name, sha):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary of this exact
+    """HBM bytes per step from the committed rocprofv3 --pmc summary of this exact
     device code (profiles/pmc_<workload>.json, keyed by build.kernel_sha), else None."""
     p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if not os.path.exists(p):
@@ -159,7 +219,7 @@ def pmc_traffic(name, sha):
         return None
     if d.get("kernel_sha") != sha:
         return None
-    return d.get("hbm_bytes_per_launch")
+    return d.get("hbm_bytes_per_step", d.get("hbm_bytes_per_launch"))
 
 
 def main():
@@ -167,7 +227,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg and the random-access probe (profiling runs)")
     args = ap.parse_args()
@@ -186,12 +246,17 @@ def main():
     torch.cuda.set_device(local)
 
     from cilium_amd import build as cvbuild
+    from cilium_amd import synth
     cvbuild.build()
     from tests import harness as H
 
     name = args.workload
+    stateful = name in STATEFUL
+    passes = args.warmup + args.steps + 1                          # + the accounting step after the timed ones
     t0 = time.time()
-    w = make_workload(name, args.packets, rank)
+    w = make_workload(name, args.packets, rank, world)
+    if stateful:
+        size_conntrack(name, w, passes)
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
     ctx, maps = H.product_ctx(w, device=local)
     log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")
@@ -202,52 +267,64 @@ def main():
            "identity": torch.empty(n, dtype=torch.int32, device=device)}
     if name == "config1":
         out = {"xdp": torch.empty(n, dtype=torch.uint8, device=device)}
-    if name in ("config3", "config4", "config5"):
+    if stateful:
         out["ct"] = torch.empty(n, dtype=torch.uint8, device=device)
+
+    def to_dev(a):
+        if a.dtype == np.uint16:
+            a = a.view(np.int16)
+        elif a.dtype == np.uint32 and a is not None:
+            a = a.view(np.int32)
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+    # the batch of every pass, resident in HBM before anything is timed
     if name == "config5":
-        parts = []
-        for part in split_families(w):
-            t = {}
-            for k, v in part.items():
-                if v.dtype == np.uint16 or (k == "flow_hash" and v.dtype == np.uint32):
-                    v = v.view(np.int16 if v.dtype == np.uint16 else np.int32)
-                t[k] = torch.from_numpy(np.ascontiguousarray(v)).to(device)
-            t["rows"] = len(part["length"])
-            parts.append(t)
-        offs = [0, parts[0]["rows"]]
+        parts, where = split_families(w)
+        dev_parts = [{k: to_dev(v) for k, v in p.items()} for p in parts]
+        offs = [0, len(parts[0]["length"])]
     else:
         frames, length, mark = H.to_dev(w, device)
+    batches = [None] * (passes + 1)
+    if stateful:
+        base = dev_parts if name == "config5" else frames
+        for v in range(1, passes + 1):
+            rows, boff, ports = synth.port_variant(w, v)
+            hi = torch.from_numpy((ports >> 8).astype(np.uint8)).to(device)
+            lo = torch.from_numpy((ports & 0xFF).astype(np.uint8)).to(device)
+            if name == "config5":
+                fv = [p["frames"].clone() for p in base]
+                for k in (0, 1):
+                    sel = where[rows, 0] == k
+                    r = torch.from_numpy(where[rows[sel], 1]).to(device)
+                    o = torch.from_numpy(boff[sel]).to(device)
+                    fv[k][r, o] = hi[torch.from_numpy(sel).to(device)]
+                    fv[k][r, o + 1] = lo[torch.from_numpy(sel).to(device)]
+            else:
+                fv = base.clone()
+                r, o = torch.from_numpy(rows).to(device), torch.from_numpy(boff).to(device)
+                fv[r, o] = hi
+                fv[r, o + 1] = lo
+            batches[v] = fv
+        log(f"[rank {rank}] {passes} step batches built on the device ({time.time() - t0:.1f}s)")
 
-    def step(o):
+    def step(o, v):
         if name == "config1":
             ctx.xdp_prefilter(frames, length, o)
         elif name == "config2":
             ctx.policy_ingress(0, frames, length, o, mark=mark)
         elif name == "config5":
-            for part, off in zip(parts, offs):
-                sub = {k: v[off:off + part["rows"]] for k, v in o.items()}
-                ctx.lxc_egress(part["frames"], part["length"], sub, w.now, src_ep=part["src_ep"],
+            for k, (part, off) in enumerate(zip(dev_parts, offs)):
+                rows = len(part["length"])
+                sub = {kk: t[off:off + rows] for kk, t in o.items()}
+                ctx.lxc_egress(batches[v][k], part["length"], sub, w.now + v, src_ep=part["src_ep"],
                                flow_hash=part["flow_hash"])
         else:
-            ctx.netdev_ingress(frames, length, o, w.now, mark=mark)
+            ctx.netdev_ingress(batches[v], length, o, w.now + v, mark=mark)
 
-    # accounting pass (untimed): L(p), U(p) of the same batch for the algorithmic bytes
-    acct = dict(out)
-    acct["nl"] = torch.zeros(n, dtype=torch.uint8, device=device)
-    acct["nu"] = torch.zeros(n, dtype=torch.uint8, device=device)
-    step(acct)
-    torch.cuda.synchronize()
-    nl, nu = acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy()
-    log(f"[rank {rank}] accounting pass done ({time.time() - t0:.1f}s)")
-    if name == "config5":
-        k4 = offs[1]
-        alg_bytes = algorithmic_bytes(name, nl[:k4], nu[:k4], 64) + algorithmic_bytes(name, nl[k4:], nu[k4:], 128)
-    else:
-        alg_bytes = algorithmic_bytes(name, nl, nu)
-    del acct
-
+    v = 1
     for _ in range(args.warmup):
-        step(out)
+        step(out, v)
+        v += 1
     torch.cuda.synchronize()
     log(f"[rank {rank}] warmup done ({time.time() - t0:.1f}s)")
 
@@ -259,13 +336,31 @@ def main():
     t_start = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        step(out)
+        step(out, v)
         ev[i][1].record(stream)
+        v += 1
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    step_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = float(np.mean(step_ms))
+
+    # accounting step (untimed, after the timed region, in the same regime): L(p), U(p)
+    acct = dict(out)
+    acct["nl"] = torch.zeros(n, dtype=torch.uint8, device=device)
+    acct["nu"] = torch.zeros(n, dtype=torch.uint8, device=device)
+    step(acct, v)
+    torch.cuda.synchronize()
+    nl, nu = acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy()
+    created = int((acct["ct"].cpu().numpy() == 0).sum()) if stateful else 0
+    if name == "config5":
+        k4 = offs[1]
+        alg_bytes = algorithmic_bytes(name, nl[:k4], nu[:k4], 64) + algorithmic_bytes(name, nl[k4:], nu[k4:], 128)
+    else:
+        alg_bytes = algorithmic_bytes(name, nl, nu)
+    del acct
+    log(f"[rank {rank}] accounting step done ({time.time() - t0:.1f}s)")
 
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -309,8 +404,9 @@ def main():
                 "workload": f"{name}: {WORKLOADS[name]}",
                 "packets_per_step_per_gpu": n,
                 "header_bytes": "64 (v4) / 128 (v6)" if name == "config5" else int(w.frames.shape[1]),
-                "parallelism": f"replicated tables, {world} GPU(s), batch per GPU",
-                "tables": {k: len(v) for k, v in w.maps.items()},
+                "parallelism": f"replicated tables, {world} GPU(s), batch per GPU"
+                               + (", conntrack sharded by address pair" if name == "config4" else ""),
+                "tables": {k: len(m) for k, m in w.maps.items()},
             },
             "roofline": {
                 "bound": "hbm",
@@ -320,7 +416,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel_ms": round(kern_ms, 4),
+                "kernel_ms_min_max": [round(min(step_ms), 4), round(max(step_ms), 4)],
                 "algorithmic_bytes_per_launch": alg_bytes,
+                "accounting": "L(p), U(p) from an untimed fresh step after the timed ones"
+                              + (f" ({created} CT_NEW packets)" if stateful else ""),
                 # the same achieved rate against the measured random-access peak (64-B lines,
                 # HBM-resident table): > 1 means the tables live in L2 / Infinity Cache
                 "random_access": None if ra_peak is None else {
@@ -329,6 +428,8 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if stateful:
+            line["config"]["ct_max_entries"] = {k: int(w.maps[k].max_entries) for k in ("ct4", "ct6") if k in w.maps}
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

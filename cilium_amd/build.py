@@ -72,7 +72,24 @@ def _build(verbose, out, defines):
     for o in objs:
         os.remove(o)
     os.replace(out + ".tmp", out)
+    if out == OUT:
+        build_c_caller(verbose)
     return out
+
+
+WALK_SRC = os.path.join(os.path.dirname(HERE), "tests", "ct_walk.c")
+WALK_BIN = os.path.join(os.path.dirname(HERE), "tests", "_bin", "ct_walk")
+
+
+def build_c_caller(verbose=False):
+    """tests/_bin/ct_walk: a plain C caller of the C-ABI (the cgo glue's view), linked
+    against the in-tree library (test tool, not product code)."""
+    os.makedirs(os.path.dirname(WALK_BIN), exist_ok=True)
+    cmd = ["gcc", "-O2", "-Wall", WALK_SRC, "-o", WALK_BIN, "-L" + os.path.dirname(OUT), "-lcilium_hip",
+           "-Wl,-rpath," + os.path.dirname(OUT)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
 
 
 if __name__ == "__main__":

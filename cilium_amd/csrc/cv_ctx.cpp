@@ -142,6 +142,14 @@ struct MapObj {
     // conntrack (device-authoritative)
     DevHash ct;
     uint32_t ct_id = 0;
+    DevBuf live;                        // u64 live-entry count on the device (HashTable::live)
+    uint64_t live_upper = 0;            // an upper bound of it the host plans launches with
+    uint64_t cap = 0;                   // max_entries
+    uint64_t gen = 0;                   // bumped by every device write: batches, map API, GC
+    // GetNextKey walk over the device table: its entries in slot order as of `gen`
+    uint64_t snap_gen = ~0ull;
+    std::vector<uint8_t> snap_keys;
+    std::unordered_map<std::string, size_t> snap_index;
 };
 
 struct Endpoint {
@@ -590,58 +598,52 @@ int update_policy(MapObj *mo)
     return 0;
 }
 
-// CT table sized for max_entries (+ its ICMP-related twins), filled from the host store;
-// v6 tables hold struct ipv6_ct_tuple keys (40 B) in Ct6Spec buckets
+// CT table sized for max_entries at 60 % bucket load, filled on the device from the
+// agent's entries (k_ct_load); v6 tables hold struct ipv6_ct_tuple keys (40 B) in
+// Ct6Spec buckets.  From here on the device copy is authoritative: the host store is
+// emptied and every map operation goes to HBM.
 template <class S>
 int compile_ct_t(cv_ctx *c, MapObj *mo, uint32_t ks, int kind)
 {
     HostMap *m = mo->hm.get();
     if (m->ks != ks || m->vs != 56) return -EINVAL;
-    std::vector<std::vector<uint32_t>> keys;
-    std::vector<uint8_t> vals;
-    m->for_each([&](const uint8_t *k, const uint8_t *v) {
-        uint8_t kk[S::KW * 4] = {0};
-        memcpy(kk, k, ks);
-        std::vector<uint32_t> w(S::KW);
-        memcpy(w.data(), kk, S::KW * 4);
-        keys.push_back(w);
-        size_t o = vals.size();
-        vals.resize(o + 64, 0);
-        memcpy(&vals[o], v, 56);
-    });
-    // capacity: max_entries at 60% bucket load
-    const uint64_t want = std::max<uint64_t>(m->max_entries, keys.size());
+    const uint64_t n = m->count();
     DevHash &d = mo->ct;
-    uint64_t nb = buckets_for(want, S::SPB);
-    if (keys.empty()) {                    // a fresh map: zeroed device buffers, no host image
-        int r = d.buckets.alloc(nb * S::BW * 4);
-        if (!r) r = d.vals.alloc(nb * S::SPB * 64);
-        if (r) return r;
-        if (hipMemset(d.buckets.p, 0, d.buckets.n) != hipSuccess || hipMemset(d.vals.p, 0, d.vals.n) != hipSuccess)
-            return -EIO;
-        d.nb = nb;
-        d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, (uint32_t)S::SPB};
-        mo->kind = kind;
-        mo->ct_id = c->next_ct_id++;
-        return 0;
-    }
-    d.hb.assign(nb * S::BW, 0);
-    HashTable t{d.hb.data(), nullptr, nb - 1, 64, (uint32_t)S::SPB};
-    std::vector<uint8_t> hv(nb * S::SPB * 64, 0);
-    for (size_t i = 0; i < keys.size(); ++i) {
-        int64_t s = host_upsert<S>(t, keys[i].data(), nullptr);
-        if (s < 0) return -E2BIG;
-        memcpy(&hv[(size_t)s * 64], &vals[i * 64], 64);
-    }
-    d.nb = nb;
-    int r = d.buckets.upload(d.hb.data(), d.hb.size() * 4);
-    if (!r) r = d.vals.upload(hv.data(), hv.size());
+    const uint64_t nb = buckets_for(std::max<uint64_t>(m->max_entries, n), S::SPB);
+    int r = d.buckets.alloc(nb * S::BW * 4);
+    if (!r) r = d.vals.alloc(nb * S::SPB * 64);
+    if (!r) r = mo->live.alloc(8);
     if (r) return r;
-    d.hb.clear();
-    d.hb.shrink_to_fit();
-    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, (uint32_t)S::SPB};
+    if (hipMemset(d.buckets.p, 0, d.buckets.n) != hipSuccess || hipMemset(d.vals.p, 0, d.vals.n) != hipSuccess)
+        return -EIO;
+    d.nb = nb;
+    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, (uint32_t)S::SPB, nullptr,
+                       mo->live.as<unsigned long long>(), m->max_entries};
+    if (n) {
+        std::vector<uint32_t> kw((size_t)n * S::KW, 0), vw((size_t)n * 16, 0);
+        size_t i = 0;
+        m->for_each([&](const uint8_t *k, const uint8_t *v) {
+            memcpy(&kw[i * S::KW], k, ks);
+            memcpy(&vw[i * 16], v, 56);
+            ++i;
+        });
+        DevBuf dk, dv, df;
+        if ((r = dk.upload(kw.data(), kw.size() * 4)) || (r = dv.upload(vw.data(), vw.size() * 4)) || (r = df.alloc(4)))
+            return r;
+        uint32_t fail = 0;
+        if (hipMemset(df.p, 0, 4) != hipSuccess) return -EIO;
+        if (launch_ct_load(d.view, kind == MK_CT6, dk.as<uint32_t>(), dv.as<uint32_t>(), n, df.as<uint32_t>(), nullptr))
+            return -EIO;
+        if (hipMemcpy(&fail, df.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+        if (fail) return -E2BIG;
+    }
+    if (hipMemcpy(mo->live.p, &n, 8, hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    mo->live_upper = n;
+    mo->cap = m->max_entries;
+    m->clear();
     mo->kind = kind;
     mo->ct_id = c->next_ct_id++;
+    mo->gen++;
     return 0;
 }
 
@@ -792,10 +794,6 @@ DpParams params(cv_ctx *c)
     memcpy(p.host_mac, c->node.host_mac, 6);
     p.net_mac[0] = p.net_mac[1] = 0;
     memcpy(p.net_mac, c->node.net_mac, 6);
-    const char *rm = getenv("CV_RECMODE");
-    p.recmode = rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u;
-    const char *ab = getenv("CV_ABLATE");
-    p.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
     p.notify = reinterpret_cast<uint32_t *>(c->notify);
     p.notify_cap = c->notify_cap;
     p.notify_count = c->notify_count;
@@ -930,9 +928,22 @@ void group_stats(cv_ctx *c, const char *what, hipStream_t stream)
     }
 }
 
+// Map-API operations on device tables run on the null stream: wait for every batch
+// already submitted (on any stream) first, so they see its writes and do not race it.
+void drain(cv_ctx *c)
+{
+    (void)c;
+    (void)hipDeviceSynchronize();
+}
+
 int ct_io(cv_ctx *c, MapObj *mo, int op, const uint8_t *key, const uint8_t *val, uint8_t *val_out, uint64_t fl)
 {
     const bool v6 = mo->kind == MK_CT6;
+    drain(c);
+    if (op) {
+        mo->gen++;
+        if (op == 1) mo->live_upper++;
+    }
     const uint32_t ks = v6 ? 40 : 14, kw = v6 ? 10 : 4;
     if (!c->ctio.p && c->ctio.alloc(32 * 4)) return -ENOMEM;
     uint32_t io[32] = {0};
@@ -948,35 +959,129 @@ int ct_io(cv_ctx *c, MapObj *mo, int op, const uint8_t *key, const uint8_t *val,
     return rc;
 }
 
-// all (key, value) rows of a device CT table
+// the live-entry count of a device CT map
+int ct_live(cv_ctx *c, MapObj *mo, uint64_t *n)
+{
+    drain(c);
+    return hipMemcpy(n, mo->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -EIO;
+}
+
+// all (key, value) rows of a device CT table, in slot order (the table's walk order)
 int ct_dump(cv_ctx *c, MapObj *mo, std::vector<uint8_t> &keys, std::vector<uint8_t> &vals)
 {
-    (void)c;
     const bool v6 = mo->kind == MK_CT6;
     const uint32_t ks = v6 ? 40 : 14, kw = v6 ? 10 : 4;
-    const uint64_t slots = mo->ct.nb * (v6 ? Ct6Spec::SPB : Ct4Spec::SPB);
-    const uint32_t max = (uint32_t)std::min<uint64_t>(slots, 0xFFFFFFF0ull);
-    DevBuf dk, dv, dc;
-    if (dk.alloc((size_t)max * kw * 4) || dv.alloc((size_t)max * 64) || dc.alloc(4)) return -ENOMEM;
+    uint64_t live = 0;
+    int r = ct_live(c, mo, &live);
+    if (r) return r;
+    const uint32_t max = (uint32_t)std::min<uint64_t>(live + 64, 0xFFFFFFF0ull);
+    DevBuf ds, dk, dv, dc;
+    if (ds.alloc((size_t)max * 8) || dk.alloc((size_t)max * kw * 4) || dv.alloc((size_t)max * 64) || dc.alloc(4))
+        return -ENOMEM;
     (void)hipMemset(dc.p, 0, 4);
-    if (launch_ct_scan(mo->ct.view, v6, mo->ct.nb, dk.as<uint32_t>(), dv.as<uint32_t>(), dc.as<uint32_t>(), max,
-                       nullptr))
+    if (launch_ct_scan(mo->ct.view, v6, mo->ct.nb, ds.as<uint64_t>(), dk.as<uint32_t>(), dv.as<uint32_t>(),
+                       dc.as<uint32_t>(), max, nullptr))
         return -EIO;
     uint32_t n = 0;
     (void)hipMemcpy(&n, dc.p, 4, hipMemcpyDeviceToHost);
-    n = std::min(n, max);
+    if (n > max) return -EIO;                     // the live count lags the table: a bug
+    std::vector<uint64_t> slot(n);
     std::vector<uint8_t> kraw((size_t)n * kw * 4), v64((size_t)n * 64);
     if (n) {
+        (void)hipMemcpy(slot.data(), ds.p, slot.size() * 8, hipMemcpyDeviceToHost);
         (void)hipMemcpy(kraw.data(), dk.p, kraw.size(), hipMemcpyDeviceToHost);
         (void)hipMemcpy(v64.data(), dv.p, v64.size(), hipMemcpyDeviceToHost);
     }
+    std::vector<uint32_t> ord(n);
+    for (uint32_t i = 0; i < n; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return slot[a] < slot[b]; });
     keys.resize((size_t)n * ks);
     vals.resize((size_t)n * 56);
-    for (uint32_t i = 0; i < n; ++i) {
-        memcpy(&keys[(size_t)i * ks], &kraw[(size_t)i * kw * 4], ks);
-        memcpy(&vals[(size_t)i * 56], &v64[(size_t)i * 64], 56);
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t i = ord[j];
+        memcpy(&keys[(size_t)j * ks], &kraw[(size_t)i * kw * 4], ks);
+        memcpy(&vals[(size_t)j * 56], &v64[(size_t)i * 64], 56);
     }
     return (int)n;
+}
+
+// GetNextKey over a device CT map (pkg/bpf/bpf.go:218-245, used by ctmap's dump walk,
+// ctmap.go:196-230): the entry after `key` in slot order, the first one when key is
+// null or absent (kernel/bpf/hashtab.c htab_map_get_next_key).  The walk reads one
+// snapshot of the table, taken once per table generation, so a full walk costs one
+// dump plus O(1) per call; slot order is stable across generations (entries never
+// move), so a walk that spans batches continues where it was.
+int ct_next_key(cv_ctx *c, MapObj *mo, const uint8_t *key, uint8_t *next)
+{
+    const uint32_t ks = mo->kind == MK_CT6 ? 40 : 14;
+    if (mo->snap_gen != mo->gen) {
+        std::vector<uint8_t> vals;
+        mo->snap_keys.clear();
+        mo->snap_index.clear();
+        const int n = ct_dump(c, mo, mo->snap_keys, vals);
+        if (n < 0) return n;
+        mo->snap_index.reserve((size_t)n * 2);
+        for (int i = 0; i < n; ++i) mo->snap_index.emplace(kstr(&mo->snap_keys[(size_t)i * ks], ks), (size_t)i);
+        mo->snap_gen = mo->gen;
+    }
+    size_t pos = 0;
+    if (key) {
+        auto it = mo->snap_index.find(kstr(key, ks));
+        if (it != mo->snap_index.end()) pos = it->second + 1;
+    }
+    if (pos >= mo->snap_index.size()) return -ENOENT;
+    memcpy(next, &mo->snap_keys[pos * ks], ks);
+    return 0;
+}
+
+// The CT maps a batch may write (every endpoint's CT4 / CT6 map), each once
+std::vector<MapObj *> batch_ct_maps(cv_ctx *c)
+{
+    std::vector<MapObj *> v;
+    for (auto &e : c->eps)
+        for (int h : {e.ct4, e.ct6}) {
+            MapObj *m = get(c, h);
+            if (m && m->kind != MK_PLAIN && std::find(v.begin(), v.end(), m) == v.end()) v.push_back(m);
+        }
+    return v;
+}
+
+// Launch-chunk planning against max_entries (ct_live_add, cv_dev.hpp).  A packet
+// creates at most W entries in a map (ingress: the tuple and its ICMP-related twin;
+// egress: a service create, the connection with its NAT tuple, and the delivery's
+// ingress create), so a chunk of n packets fits when every map has W * n free
+// entries.  The host keeps an upper bound of each count, raised by W per packet it
+// launches, and reads the true counts (one sync) only when a bound gets close.  Next
+// to a limit the chunk is one packet with guard = 1: its creates check the count.
+uint32_t ct_plan(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t want, uint32_t W, hipStream_t s,
+                 uint32_t *guard)
+{
+    *guard = 0;
+    auto room = [&]() {
+        uint64_t r = ~0ull;
+        for (MapObj *m : maps) r = std::min(r, m->cap > m->live_upper ? m->cap - m->live_upper : 0);
+        return r;
+    };
+    uint64_t r = room();
+    if (r < (uint64_t)W * want) {
+        (void)hipStreamSynchronize(s);
+        (void)c;
+        for (MapObj *m : maps) {
+            uint64_t v = 0;
+            if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
+        }
+        r = room();
+    }
+    uint64_t n = std::min<uint64_t>(want, r / W);
+    if (n == 0) {
+        n = 1;
+        *guard = 1;
+    }
+    for (MapObj *m : maps) {
+        m->live_upper += W * n;
+        m->gen++;
+    }
+    return (uint32_t)n;
 }
 
 // live policy counters of one key from HBM (device-authoritative)
@@ -1120,7 +1225,10 @@ int cv_map_lookup(cv_ctx *c, int h, const void *key, void *val)
     const uint8_t *v = m->hm->lookup((const uint8_t *)key);
     if (!v) return -ENOENT;
     memcpy(val, v, m->hm->vs);
-    if (m->is_policy) { (void)set_device(c); policy_counters(m, (const uint8_t *)key, (uint8_t *)val); }
+    if (m->is_policy && !set_device(c)) {
+        drain(c);
+        policy_counters(m, (const uint8_t *)key, (uint8_t *)val);
+    }
     return 0;
 }
 
@@ -1152,6 +1260,8 @@ int cv_ct_gc(cv_ctx *c, int h, uint32_t time, uint32_t *deleted)
     uint32_t n = 0;
     if (m->kind != MK_PLAIN) {
         if (set_device(c)) return -ENODEV;
+        drain(c);
+        m->gen++;
         DevBuf d;
         if (d.alloc(4)) return -ENOMEM;
         if (hipMemset(d.p, 0, 4) != hipSuccess) return -EIO;
@@ -1180,19 +1290,8 @@ int cv_map_get_next_key(cv_ctx *c, int h, const void *key, void *next)
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
     if (m->kind != MK_PLAIN) {
-        std::vector<uint8_t> ks, vs;
         if (set_device(c)) return -ENODEV;
-        int n = ct_dump(c, m, ks, vs);
-        if (n < 0) return n;
-        const uint32_t ksz = m->hm->ks;
-        int at = 0;
-        if (key) {
-            for (int i = 0; i < n; ++i)
-                if (!memcmp(&ks[(size_t)i * ksz], key, ksz)) { at = i + 1; break; }
-        }
-        if (at >= n) return -ENOENT;
-        memcpy(next, &ks[(size_t)at * ksz], ksz);
-        return 0;
+        return ct_next_key(c, m, (const uint8_t *)key, (uint8_t *)next);
     }
     return m->hm->next_key((const uint8_t *)key, (uint8_t *)next);
 }
@@ -1204,12 +1303,11 @@ int cv_map_count(cv_ctx *c, int h, uint32_t *count)
     MapObj *m = get(c, h);
     if (!m) return -EBADF;
     if (m->kind != MK_PLAIN) {
-        std::vector<uint8_t> ks, vs;
         if (set_device(c)) return -ENODEV;
-        int n = ct_dump(c, m, ks, vs);
-        if (n < 0) return n;
+        uint64_t n = 0;
+        const int r = ct_live(c, m, &n);
         *count = (uint32_t)n;
-        return 0;
+        return r;
     }
     *count = m->hm->count();
     return 0;
@@ -1233,7 +1331,7 @@ int cv_map_dump(cv_ctx *c, int h, void *keys, void *vals, uint32_t max)
         return (int)w;
     }
     uint32_t w = 0;
-    if (m->is_policy) (void)set_device(c);
+    if (m->is_policy && !set_device(c)) drain(c);
     m->hm->for_each([&](const uint8_t *k, const uint8_t *v) {
         if (w >= max) return;
         if (keys) memcpy((uint8_t *)keys + (size_t)w * ks, k, ks);
@@ -1379,9 +1477,10 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         const HashTable &t = get(c, e.policy)->pol.view;
         if (seen.insert(t.vals).second) pols.push_back(t);
     }
-    const DpParams p = params(c);
-    for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
-        const uint32_t n = std::min(c->chunk, b->n - off);
+    DpParams p = params(c);
+    const std::vector<MapObj *> cts = batch_ct_maps(c);
+    for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
+        n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 2, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
         if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off, b->stride), gs,
                                        (hipStream_t)stream)))
@@ -1410,9 +1509,10 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
         const HashTable &t = get(c, e.policy)->pol.view;
         if (seen.insert(t.vals).second) pols.push_back(t);
     }
-    const DpParams p = params(c);
-    for (uint32_t off = 0; off < b->n; off += c->chunk) {   // sub-batches in packet order
-        const uint32_t n = std::min(c->chunk, b->n - off);
+    DpParams p = params(c);
+    const std::vector<MapObj *> cts = batch_ct_maps(c);
+    for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
+        n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 7, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications

@@ -48,25 +48,6 @@ __device__ __forceinline__ void rec_load(RecT<NW> &r, const BatchDev &b, uint32_
     }
 }
 
-// plain (temporal) per-lane record load, for comparison with the non-temporal one
-template <int NW>
-__device__ __forceinline__ void rec_load_plain(RecT<NW> &r, const BatchDev &b, uint32_t i, int nvec)
-{
-    r.base = b.frames + (size_t)i * b.stride;
-    r.len = b.len[i];
-    r.stride = b.stride;
-    const uint4 *q = reinterpret_cast<const uint4 *>(r.base);
-#pragma unroll
-    for (int k = 0; k < NW / 4; ++k) {
-        if (k < nvec) {
-            const uint4 v = q[k];
-            r.w[4 * k] = v.x; r.w[4 * k + 1] = v.y; r.w[4 * k + 2] = v.z; r.w[4 * k + 3] = v.w;
-        } else {
-            r.w[4 * k] = r.w[4 * k + 1] = r.w[4 * k + 2] = r.w[4 * k + 3] = 0;
-        }
-    }
-}
-
 // Wave-cooperative load of the 64 consecutive 64-B records of a wave (i0 = the
 // wave's first packet): four fully coalesced 1-KiB loads per wave into LDS (`st`,
 // 4 KiB per wave), then every lane takes its own record's first nvec 16-B words.
@@ -485,11 +466,7 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
     const uint32_t kl4[2] = {identity, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
     const uint32_t kl3[2] = {identity, eg << 24};
     const uint32_t kwc[2] = {0, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
-#ifdef CV_NO_ILP
-    if constexpr (false) {
-#else
     if constexpr (ILP) {
-#endif
         const bool have_l4 = flags & F_HAVE_L4_POLICY;
         Probe<PolicySpec> p1, p3;
         if (have_l4) p1 = probe_begin<PolicySpec>(pol, kl4);
@@ -536,19 +513,17 @@ __device__ __forceinline__ int policy_hit(const HashTable &pol, uint32_t flags, 
     if (s < 0) return DROP_POLICY;
     a.nu++;
     uint8_t *v = pol.vals + (size_t)s * pol.vstride;
-    if (!(flags & (AB_NO_POLICY_ATOMICS << 16))) {
-        // __sync_fetch_and_add(packets, 1) and (bytes, len) as ONE 64-bit atomic on the
-        // slot's delta word {count:25 | bytes:39} (launches are chunked to <= 2^24
-        // packets and folded after each chunk, so neither field can overflow)
-        if (len < (1u << 15)) {
-            unsigned long long *d = pol.aux + s;
-            const unsigned long long inc = (1ull << 39) | len;
-            if (defer) *defer = Hit{d, inc};
-            else pol_add(a.pc, d, inc);
-        } else {
-            atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);
-            atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
-        }
+    // __sync_fetch_and_add(packets, 1) and (bytes, len) as ONE 64-bit atomic on the
+    // slot's delta word {count:25 | bytes:39} (launches are chunked to <= 2^24
+    // packets and folded after each chunk, so neither field can overflow)
+    if (len < (1u << 15)) {
+        unsigned long long *d = pol.aux + s;
+        const unsigned long long inc = (1ull << 39) | len;
+        if (defer) *defer = Hit{d, inc};
+        else pol_add(a.pc, d, inc);
+    } else {
+        atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);
+        atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
     }
     return l4 ? (int)proxy_port : TC_ACT_OK;
 }
@@ -568,24 +543,12 @@ __device__ __forceinline__ int policy_access_q(const HashTable &pol, uint32_t fl
     const uint32_t kl4[2] = {identity, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
     const uint32_t kl3[2] = {identity, eg << 24};
     const uint32_t kwc[2] = {0, (dport_raw & 0xFFFFu) | (proto << 16) | (eg << 24)};
-#ifdef CV_POL_PAIR
-    if (have_l4) {                                                // L4 and L3 keys read together
-        int64_t s1, s2;
-        quad_find2<PolicySpec>(pol, kl4, want, kl3, want, st, s1, &v1, s2, &v2);
-        if (want) { a.nl++; s = s1; px = v1; l4 = s1 >= 0; }
-        if (want && s < 0) { a.nl++; s = s2; px = v2; }
-    } else {
-        const int64_t s2 = quad_find<PolicySpec>(pol, kl3, want, st, &v2);
-        if (want) { a.nl++; s = s2; px = v2; }
-    }
-#else
     if (have_l4) {
         const int64_t s1 = quad_find<PolicySpec>(pol, kl4, want, st, &v1);
         if (want) { a.nl++; s = s1; px = v1; l4 = s1 >= 0; }
     }
     const int64_t s2 = quad_find<PolicySpec>(pol, kl3, want && s < 0, st, &v2);
     if (want && s < 0) { a.nl++; s = s2; px = v2; }
-#endif
     if (have_l4) {
         const int64_t s3 = quad_find<PolicySpec>(pol, kwc, want && s < 0, st, &v3);
         if (want && s < 0) { a.nl++; s = s3; px = v3; l4 = s3 >= 0; }
@@ -868,7 +831,7 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
     }
     if (mon) *mon = m;
-    if (!(flags & (AB_EG_NO_CTSTORE << 16))) ct_store(ct, slot, e);
+    ct_store(ct, slot, e);
 }
 
 __device__ __forceinline__ uint8_t dir_flags(int dir)
@@ -926,15 +889,6 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     const int action = ct_l4<V6>(t, h, dir, seen);
     if (action < 0) return action;
     const bool tcp = t.nexthdr == 6;
-#ifdef CV_NO_ILP
-    int ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a, mon);
-    if (ret != CT_NEW) return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
-    if (dir != CT_SERVICE) {
-        t.reverse();
-        ret = ct_lookup_one(ct, t, action, dir, tcp, seen, len, now, flags, slot, st, a, mon);
-    }
-    return ret;
-#endif
     T t2 = t;
     t2.reverse();
     uint32_t k1[T::KW], k2[T::KW];
@@ -959,16 +913,43 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     return CT_ESTABLISHED;
 }
 
+// The live-entry count of a CT map (its max_entries check).  A launch either has room
+// for every create it can make (the host plans launch chunks by the worst case per
+// packet, cv_ctx.cpp ct_plan): creates then only count, summed per workgroup in the
+// LDS counter cache; or it is a guarded one-packet launch next to the limit, where a
+// create of a new key first checks the count, exactly as the kernel's hash map fails
+// an insert past max_entries (-E2BIG -> DROP_CT_CREATE_FAILED).
+__device__ __forceinline__ void ct_live_add(const HashTable &ct, Acct &a, bool guard, long long d)
+{
+    if (!ct.live) return;
+    if (guard) atomicAdd(ct.live, (unsigned long long)d);
+    else pol_add(a.pc, ct.live, (unsigned long long)d);
+}
+
+// map_update_elem(BPF_ANY) of a CT entry (conntrack.h:694,720,740)
 template <class T>
-__device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const CtE &e)
+__device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const CtE &e, Acct &a, bool guard)
 {
     uint32_t k[T::KW];
     t.key(k);
+    if (guard && ct.live && dev_find<typename T::Spec>(ct, k, nullptr) < 0 &&
+        __hip_atomic_load(ct.live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ct.cap)
+        return false;                                             // full: -E2BIG
     bool created;
     const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created);
     if (s < 0) return false;
+    if (created) ct_live_add(ct, a, guard, 1);
     ct_store(ct, s, e);
     return true;
+}
+
+// ct_delete4 / ct_delete6 (conntrack.h:641-647, 564-570) of a found entry
+template <class S>
+__device__ __forceinline__ void ct_kill(const HashTable &ct, int64_t slot, Acct &a, bool guard)
+{
+    dev_kill<S>(ct, slot);
+    ct_live_add(ct, a, guard, -1);
+    a.nu++;
 }
 
 // the entry ct_create4 / ct_create6 write for `t` (conntrack.h:668-690 / 593-612)
@@ -1001,17 +982,17 @@ __device__ __forceinline__ Tuple4 ct_nat_tuple(const Tuple4 &t, int dir, const C
 // later, see k_nat_apply), and the ICMP-RELATED twin
 template <bool V6, class T>
 __device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32_t len, int dir, const CtState &st,
-                                         uint32_t now, Acct &a, bool defer_nat = false)
+                                         uint32_t now, Acct &a, bool guard, bool defer_nat = false)
 {
     CtE e;
     const bool tcp = t.nexthdr == 6;
     ct_entry_new(e, tcp, len, dir, st, now);
     const bool nat = !V6 && st.addr;
     a.nu += nat ? 3 : 2;
-    if (!ct_put(ct, t, e)) return DROP_CT_CREATE_FAILED;
+    if (!ct_put(ct, t, e, a, guard)) return DROP_CT_CREATE_FAILED;
     if constexpr (!V6) {
         if (nat && !defer_nat) {
-            if (!ct_put(ct, ct_nat_tuple(t, dir, st), e)) return DROP_CT_CREATE_FAILED;
+            if (!ct_put(ct, ct_nat_tuple(t, dir, st), e, a, guard)) return DROP_CT_CREATE_FAILED;
         }
     }
     T it = t;
@@ -1019,7 +1000,7 @@ __device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32
     it.sport = 0; it.dport = 0;
     it.flags = t.flags | TUPLE_F_RELATED;
     e.set_bits(e.bits() | CTB_SEEN_NON_SYN);
-    if (!ct_put(ct, it, e)) return DROP_CT_CREATE_FAILED;
+    if (!ct_put(ct, it, e, a, guard)) return DROP_CT_CREATE_FAILED;
     return 0;
 }
 
@@ -1459,16 +1440,16 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
             if (rn) *rn = RevNatOut{true, false, na, np};
         }
     }
-    verdict = policy_ingress<true>(ep.policy, p.flags | (p.ablate << 16), s.len, src_label, t.dport, t.nexthdr, a);
+    verdict = policy_ingress<true>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { dev_kill<Ct4Spec>(ep.ct4, slot); a.nu++; }   // ct_delete4
+        if (ret == CT_ESTABLISHED) ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);   // ct_delete4
         ret = DROP_POLICY;
         goto drop;
     }
     if (skip_proxy) verdict = 0;
     if (ret == CT_NEW) {
         CtState sn{0, 0, 0, 0, 0, src_label};
-        const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a);
+        const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
         if (is_err(c)) { ret = c; goto drop; }
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
@@ -1530,15 +1511,15 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
             if (rn) { rn->valid = true; rn->np = np; for (int j = 0; j < 4; ++j) rn->na[j] = na[j]; }
         }
     }
-    verdict = policy_ingress<true>(ep.policy, p.flags | (p.ablate << 16), s.len, src_label, t.dport, t.nexthdr, a);
+    verdict = policy_ingress<true>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { dev_kill<Ct6Spec>(ep.ct6, slot); a.nu++; }
+        if (ret == CT_ESTABLISHED) ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);   // ct_delete6
         ret = DROP_POLICY;
         goto drop;
     }
     if (skip_proxy) verdict = 0;
     if (ret == CT_NEW) {
-        const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a);
+        const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
         if (is_err(c)) { ret = c; goto drop; }
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {

@@ -34,8 +34,6 @@ struct DpParams {              // by value as the kernel argument
     const EpDev *eps;
     const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
     unsigned long long *metrics;   // [256][4][2]
-    uint32_t ablate;           // timing-only ablations (CV_ABLATE env); 0 in every real run
-    uint32_t recmode;          // record loads: 0 per-lane non-temporal, 1 per-lane plain, 2 wave-cooperative
     // load balancer (lb.h): services and dense reverse-NAT tables indexed by the raw u16 key
     HashTable lb4, lb6;        // Lb4Spec / Lb6Spec
     const uint32_t *revnat4;   // [65536][2]  {address, port | valid << 16}
@@ -55,14 +53,8 @@ struct DpParams {              // by value as the kernel argument
     uint32_t *trace_count;
     uint32_t trace_agg;        // MONITOR_AGGREGATION
     uint32_t ingress_ifindex;  // skb->ingress_ifindex of from_netdev
+    uint32_t ct_guard;         // 1: a one-packet launch next to a CT map's max_entries (exact check per create)
 };
-
-// ablation bits: each removes one part of the work to price it (results are wrong)
-constexpr uint32_t AB_NO_POLICY_ATOMICS = 1, AB_NO_IPCACHE = 2, AB_NO_POLICY = 4, AB_NO_METRICS = 8,
-                   AB_NO_RECORD = 16,
-                   // egress (config 5) timing ablations
-                   AB_EG_NO_DELIVERY = 0x100, AB_EG_NO_POLICY = 0x200, AB_EG_NO_LOOKUPS = 0x400,
-                   AB_EG_NO_CTSTORE = 0x800, AB_EG_ONE_PER_GROUP = 0x1000, AB_EG_NAT_DEFER_ALL = 0x2000;
 
 struct BatchDev {
     const uint8_t *frames;
@@ -144,7 +136,11 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
 int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s);
 // ctmap.GC (GCFilterByTime): mark entries with lifetime < time dead; adds the count
 int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s);
-int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint32_t *out_keys, uint32_t *out_vals, uint32_t *count,
-                   uint32_t max, hipStream_t s);
+// every live entry: slot index (may be null), key words, 16 value words
+int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint64_t *out_slots, uint32_t *out_keys, uint32_t *out_vals,
+                   uint32_t *count, uint32_t max, hipStream_t s);
+// parallel initial fill of an empty CT table with n distinct keys
+int launch_ct_load(const HashTable &t, int v6, const uint32_t *keys, const uint32_t *vals, uint64_t n, uint32_t *fail,
+                   hipStream_t s);
 
 }  // namespace cv

@@ -196,13 +196,8 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
     return STAGE_DONE;
 }
 
-#ifdef CV_EF_WPE               // A/B only
-#define CV_EF_OCC __attribute__((amdgpu_waves_per_eu(CV_EF_WPE, 8)))
-#else
-#define CV_EF_OCC
-#endif
 template <int NW, bool EV>
-__global__ void __launch_bounds__(BLOCK) CV_EF_OCC k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
+__global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
                                                         OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
@@ -275,7 +270,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
     uint32_t key_dport = eg[1] >> 16;
@@ -293,7 +288,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     if (ret == E_TRUNC) goto fin;
     if (ret == CT_NEW) {
         st.slave = hsh % count + 1;                               // lb4_select_slave
-        const int c = ct_create<false>(ep.ct4, t, r.len, CT_SERVICE, st, now, a);
+        const int c = ct_create<false>(ep.ct4, t, r.len, CT_SERVICE, st, now, a, p.ct_guard);
         if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
     } else if (ret < 0) {
         ret = DROP_NO_SERVICE;
@@ -380,7 +375,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u};
+    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
     uint32_t key_dport = eg[1] >> 16;
@@ -398,7 +393,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     if (ret == E_TRUNC) goto fin;
     if (ret == CT_NEW) {
         st.slave = hsh % count + 1;
-        const int c = ct_create<true>(ep.ct6, t, r.len, CT_SERVICE, st, now, a);
+        const int c = ct_create<true>(ep.ct6, t, r.len, CT_SERVICE, st, now, a, p.ct_guard);
         if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
     } else if (ret < 0) {
         ret = DROP_NO_SERVICE;
@@ -459,26 +454,25 @@ fin:
     eg_final(o, i, res, a);
 }
 
-#ifdef CV_LB_WPE               // A/B only
-#define CV_LB_OCC __attribute__((amdgpu_waves_per_eu(CV_LB_WPE, 8)))
-#else
-#define CV_LB_OCC
-#endif
 template <bool V6, bool EV>
-__global__ void __launch_bounds__(BLOCK) CV_LB_OCC k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
+__global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
                                                     OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;                                      // (here: the CT maps' live counts)
     using M = MetT<EV>;
     M m;
+    pol_cache_init(pc);
     met_init(m, lm);
+    m.pc = &pc;
     for_each_group(g, V6 ? Q_LB6 : Q_LB4, [&](uint32_t, uint32_t head) {
         group_in_order(g, head, 1, [&](uint32_t x) {
             if constexpr (V6) lb6_one(p, b, hash, now, o, g, x, m);
             else lb4_one(p, b, hash, now, o, g, x, m);
         });
     });
-    met_flush(m, p.metrics);
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
 }
 
 // ================================================================== egress state of a packet
@@ -632,7 +626,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, Gr
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         if ((eg[0] & (EG_STAGE | EG_V6 | EG_SVC)) != (STAGE_CT | EG_SVC) || !eg[4]) continue;
-        if (p.ablate & AB_EG_NAT_DEFER_ALL) { eg[0] |= EG_NAT_DEFER; continue; }   // timing only
+        if (p.ct_guard) continue;                                 // one-packet launch: written inline, in order
         uint32_t nn;
         if (eg[0] & EG_LOOPBACK) {                                // (client, IPV4_LOOPBACK): by pair
             nn = group_find(g, pair_hash4(eg[4], eg[5], SALT_CT4));
@@ -710,14 +704,13 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     const uint32_t orig_dip = t.daddr;
     // issued ahead of the conntrack probes (independent reads of read-only tables):
     // the ipcache lookup of orig_dip and the endpoint lookup of the packet's daddr
-    const bool lookups = !(p.ablate & AB_EG_NO_LOOKUPS);
     Lpm4Pending ipq;
-    if (lookups && p.ipc4.l1) ipq = lpm4_begin(p.ipc4, bswap32(orig_dip));
+    if (p.ipc4.l1) ipq = lpm4_begin(p.ipc4, bswap32(orig_dip));
     const uint32_t lxc_key = s.daddr;
     Probe<LxcV4Spec> lxq;
-    if (lookups && p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
+    if (p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
     bool mon = false;
-    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags | (p.ablate << 16), slot, &st, a, &mon);
+    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
@@ -725,21 +718,21 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     RevNatOut rn1{false, false, 0, 0}, rn2{false, false, 0, 0};                 // reverse NATs applied (output frames)
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
-    if (lookups) {                                                // destination category (:482-494)
+    {                                                             // destination category (:482-494)
         uint32_t lab = 0;
         if (p.ipc4.l1) { a.nl++; lab = lpm4_end(ipq, p.ipc4); }
         res.dst = lab ? lab : ((orig_dip & p.v4_cluster_mask) == p.v4_cluster_range ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = (p.ablate & AB_EG_NO_POLICY) ? 0 : policy_egress(ep.policy, p.flags | (p.ablate << 16), s.len, res.dst, t.dport, t.nexthdr, a);
+    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { dev_kill<Ct4Spec>(ep.ct4, slot); a.nu++; }   // ct_delete4
+        if (ret == CT_ESTABLISHED) ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);   // ct_delete4
         ret = verdict;
         goto drop;
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
         const bool defer = eg[0] & EG_NAT_DEFER;
-        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, defer);
+        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer);
         if (defer && c != DROP_CT_CREATE_FAILED) g.eg[(size_t)i * EG_WORDS] = eg[0] | EG_NAT_DONE;
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
@@ -763,7 +756,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         eg_final(o, i, res, a);
         return;
     }
-    if (lookups && p.lxc4.buckets) {
+    if (p.lxc4.buckets) {
         a.nl++;                                                   // lookup_ip4_endpoint(ip4)
         lxc_slot = s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv)
                                       : dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv);
@@ -782,7 +775,6 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        if (p.ablate & AB_EG_NO_DELIVERY) { res.ret = TC_ACT_OK; eg_final(o, i, res, a); return; }
         res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
                                  ct2, res.proxy, res.reason, a, m, &rn2);
         if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
@@ -874,15 +866,15 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         res.dst = lab ? lab
                       : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = policy_egress(ep.policy, p.flags | (p.ablate << 16), s.len, res.dst, t.dport, t.nexthdr, a);
+    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) { dev_kill<Ct6Spec>(ep.ct6, slot); a.nu++; }
+        if (ret == CT_ESTABLISHED) ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);   // ct_delete6
         ret = verdict;
         goto drop;
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
-        const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a);
+        const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard);
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
         uint32_t na[4], np;
@@ -946,10 +938,7 @@ drop:
 // (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
 // capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
 // 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
-#ifndef CV_EG_WPE
-#define CV_EG_WPE 4
-#endif
-#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WPE, 8)))
+#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(4, 8)))
 
 template <bool V6, bool EV>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
@@ -962,8 +951,8 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
     met_init(m, lm);
     m.pc = &pc;
     // runs in queue order: k_group_flatten without k_group_schedule (measured faster here
-    // than size-class order); AB_EG_ONE_PER_GROUP (timing only): each group's first member
-    for_each_run<false>(g, V6 ? Q_CT6 : Q_CT4, p.ablate & AB_EG_ONE_PER_GROUP, [&](uint32_t x) {
+    // than size-class order)
+    for_each_run<false>(g, V6 ? Q_CT6 : Q_CT4, false, [&](uint32_t x) {
         if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
         else egress4_one(p, b, now, o, g, x, m);
     });
@@ -987,6 +976,9 @@ __global__ void __launch_bounds__(BLOCK) k_nat_group(BatchDev b, GroupScratch g)
 
 __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uint32_t now, GroupScratch g)
 {
+    __shared__ LdsPolicy pc;                                      // the CT maps' live counts
+    pol_cache_init(pc);
+    __syncthreads();
     for_each_group(g, Q_NAT, [&](uint32_t, uint32_t head) {
         for (uint32_t x = head; x != NONE; x = g.next[x]) {
             Rec r;
@@ -1006,7 +998,8 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
             n.key(k);
             bool created;
             const int64_t sl = dev_upsert<Ct4Spec>(ep.ct4, k, &created);
-            if (sl < 0) continue;                                 // table full: the reference fails the create
+            if (sl < 0) continue;                                 // (probe limit; launches are planned with room)
+            if (created && ep.ct4.live) pol_add(&pc, ep.ct4.live, 1ull);
             uint32_t *v = reinterpret_cast<uint32_t *>(ep.ct4.vals + (size_t)sl * ep.ct4.vstride);
             if (!created && v[15] == g.serial && v[14] > x) continue;
             e.w[14] = x;
@@ -1014,6 +1007,8 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
             ct_store(ep.ct4, sl, e);
         }
     });
+    __syncthreads();
+    pol_cache_flush(pc);
 }
 
 // ================================================================== launcher

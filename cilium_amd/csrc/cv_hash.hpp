@@ -27,6 +27,8 @@ struct HashTable {            // POD view, passed by value to kernels
     uint32_t  vstride;
     uint32_t  spb;
     unsigned long long *aux;  // per-slot 64-bit side words (policy counter deltas), or null
+    unsigned long long *live; // conntrack maps: the live-entry count (device), or null
+    uint64_t  cap;            // conntrack maps: max_entries (a create past it fails, -E2BIG)
 };
 
 template <int KW_, int IVW_, int SPB_, int BW_, int IVH_ = 0>
@@ -91,12 +93,6 @@ __device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets
     const uint4 *q = reinterpret_cast<const uint4 *>(buckets + b * S::BW);
 #pragma unroll
     for (int i = 0; i < S::BW / 4; ++i) {
-#ifdef CV_TIMING_BUCKET_VECS
-        if (S::BW == 16 && i >= CV_TIMING_BUCKET_VECS) {          // timing probe only: wrong answers
-            w[4 * i] = w[4 * i + 1] = w[4 * i + 2] = w[4 * i + 3] = 0;
-            continue;
-        }
-#endif
         uint4 v = q[i];
         w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
@@ -160,13 +156,7 @@ template <class S>
 __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     if (!t.buckets) return -1;
-#ifndef CV_NO_TAGFIRST
-#ifdef CV_TF_ALL
-    if constexpr (true) return dev_find_tf<S>(t, key, ival);
-#else
-    if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);
-#endif
-#endif
+    if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);   // (tag-first 64-B probes: slower)
     const uint64_t h = key_hash<S>(key);
     return dev_find_from<S>(t, key, tag_of(h), h & t.mask, 0, ival);
 }

@@ -113,6 +113,14 @@ class HostMap {
     }
 
     bool is_lpm() const { return type == 11; }
+
+    // drop every element (a CT map whose device copy became authoritative)
+    void clear()
+    {
+        if (is_lpm()) return;
+        tab_.reset(new ByteTable(ks, vs));
+        log_clear();
+    }
     uint32_t data_bits() const { return dbits_; }
 
     uint32_t count() const
@@ -248,6 +256,16 @@ class HostMap {
     // null or absent (kernel/bpf/hashtab.c htab_map_get_next_key).  -ENOENT at end.
     int next_key(const uint8_t *key, uint8_t *out) const
     {
+        if (!is_lpm()) {                                  // the slot after key's, in table order
+            uint64_t s = 0;
+            if (key) {
+                const int64_t at = tab_->find(key);
+                s = at < 0 ? 0 : (uint64_t)at + 1;        // absent key: from the first element
+            }
+            for (; s < tab_->capacity(); ++s)
+                if (tab_->used(s)) { memcpy(out, tab_->key(s), ks); return 0; }
+            return -ENOENT;
+        }
         bool take = key == nullptr, found = false, done = false;
         if (key && !exists_exact(key)) take = true;
         for_each([&](const uint8_t *k, const uint8_t *) {

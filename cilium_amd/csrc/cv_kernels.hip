@@ -22,7 +22,7 @@ namespace cv {
 __device__ __forceinline__ void rec_load_wave(Rec &r, const DpParams &p, const BatchDev &b, uint32_t i0, uint32_t i,
                                               bool live, uint4 *st)
 {
-    if (p.recmode == 2 && b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 4, st);
+    if (b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 4, st);
     else if (!live) { r.len = 0; for (int j = 0; j < 16; ++j) r.w[j] = 0; }
     else rec_load(r, b, i, 4);
 }
@@ -33,11 +33,7 @@ __device__ __forceinline__ void rec_load_wave(Rec &r, const DpParams &p, const B
 template <class T>
 __device__ __forceinline__ void st_out(T *q, T v)
 {
-#ifdef CV_NO_NT_OUT            // A/B only
-    *q = v;
-#else
     __builtin_nontemporal_store(v, q);
-#endif
 }
 
 __global__ void __launch_bounds__(BLOCK) k_xdp_prefilter(DpParams p, BatchDev b, OutDev o)
@@ -88,31 +84,18 @@ __device__ __forceinline__ int l4_key_new_flow(const Rec &r, uint32_t &dport_raw
 
 // PPT packets per lane: lane t of workgroup w takes packets w*PPT*BLOCK + k*BLOCK + t
 // (coalesced per k); its policy counter atomics wait in registers until its last
-// lookup is done.
-#ifndef CV_PPT
-#define CV_PPT 4
-#endif
-constexpr int PPT = CV_PPT;
+// lookup is done (2, 3, 5, 6 and 8 packets per lane measured slower).
+constexpr int PPT = 4;
 
-#ifndef CV_NO_QUAD
-// Quad-probe form: the table probes are quad_find (cv_hash.hpp), so every lane of
-// the wave reaches each probe; lanes without a lookup (past the batch end, non-IPv4,
-// short or invalid headers) take part with want = false.  (Holding the results in
-// registers until after the last probe, so the probes' vmcnt waits skip the output
-// stores, measured 3 % slower.)
-#ifdef CV_PI_WPE               // A/B only
-#define CV_PI_OCC __attribute__((amdgpu_waves_per_eu(CV_PI_WPE, 8)))
-#else
-#define CV_PI_OCC
-#endif
-__global__ void __launch_bounds__(BLOCK) CV_PI_OCC k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
+// The table probes are quad_find (cv_hash.hpp), so every lane of the wave reaches
+// each probe; lanes without a lookup (past the batch end, non-IPv4, short or invalid
+// headers) take part with want = false.  (Holding the results in registers until
+// after the last probe, so the probes' vmcnt waits skip the output stores, measured
+// 3 % slower.)
+__global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
 {
     __shared__ unsigned long long drops[256 * 2];                 // ingress drops {count, bytes} by reason
-#ifdef CV_POL_PAIR
-    __shared__ uint4 stage[BLOCK / 64][512];
-#else
     __shared__ uint4 stage[BLOCK / 64][256];
-#endif
     for (int j = threadIdx.x; j < 256 * 2; j += BLOCK) drops[j] = 0;
     __syncthreads();
     const HashTable pol = p.eps[ep].policy;
@@ -126,9 +109,8 @@ __global__ void __launch_bounds__(BLOCK) CV_PI_OCC k_policy_ingress(DpParams p, 
         if (i0 >= b.n) continue;                                  // the whole wave is past the end
         const bool live = i < b.n;
         Rec r;
-        if (p.recmode == 2 && b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 3, st);
+        if (b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 3, st);
         else if (!live) { r.len = 0; for (int j = 0; j < 16; ++j) r.w[j] = 0; }
-        else if (p.recmode == 1) rec_load_plain(r, b, i, 3);
         else rec_load(r, b, i, 3);
         Acct a{0, 0};
         bool skip_proxy = false;
@@ -136,25 +118,23 @@ __global__ void __launch_bounds__(BLOCK) CV_PI_OCC k_policy_ingress(DpParams p, 
         if (live && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
         const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
         const bool v4 = live && eth == 0x0008u && r.len >= 34;
-        const bool want_ipc = v4 && identity < HEALTH_ID && !(p.ablate & AB_NO_IPCACHE);   // bpf_netdev.c:375-398
+        const bool want_ipc = v4 && identity < HEALTH_ID;         // bpf_netdev.c:375-398
         const uint32_t lab = ipcache4_q(p, rec_raw32c<26>(r), want_ipc, a, st);
         if (want_ipc && lab && lab != CLUSTER_ID && lab != HOST_ID) identity = lab;
         int32_t ret = eth != 0x0008u ? DROP_UNKNOWN_L3 : r.len < 34 ? DROP_INVALID : 0;
         uint32_t dport = 0, proto = 0;
         if (v4) ret = l4_key_new_flow(r, dport, proto);
-        const bool want_pol = v4 && ret == 0 && !(p.ablate & AB_NO_POLICY);
-        const int v = policy_ingress_q(pol, p.flags | (p.ablate << 16), r.len, identity, dport, proto, a, &hits[k],
-                                       want_pol, st);
+        const bool want_pol = v4 && ret == 0;
+        const int v = policy_ingress_q(pol, p.flags, r.len, identity, dport, proto, a, &hits[k], want_pol, st);
         uint16_t proxy = 0;
         if (v4 && ret == 0) {
-            const int vv = (p.ablate & AB_NO_POLICY) ? (int)(identity & 1) : v;
-            if (vv < 0) ret = DROP_POLICY;
-            else if (skip_proxy && vv > 0) ret = 0;
-            else { ret = vv; proxy = vv > 0 ? (uint16_t)vv : 0; }
+            if (v < 0) ret = DROP_POLICY;
+            else if (skip_proxy && v > 0) ret = 0;
+            else { ret = v; proxy = v > 0 ? (uint16_t)v : 0; }
         }
         if (!live) continue;
         const bool dropped = ret < 0 && ret != E_TRUNC;
-        if (dropped && !(p.ablate & AB_NO_METRICS)) {             // send_drop_notify -> cilium_metrics
+        if (dropped) {                                            // send_drop_notify -> cilium_metrics
             const uint32_t rr = (uint8_t)(-ret);
             atomicAdd(&drops[2 * rr], 1ull);
             atomicAdd(&drops[2 * rr + 1], (unsigned long long)r.len);
@@ -176,67 +156,6 @@ __global__ void __launch_bounds__(BLOCK) CV_PI_OCC k_policy_ingress(DpParams p, 
                 atomicAdd(&p.metrics[(j * 4 + METRIC_INGRESS) * 2 + 1], drops[2 * j + 1]);
             }
 }
-#else
-__global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, BatchDev b, OutDev o)
-{
-    __shared__ LdsMetrics lm;
-    __shared__ uint4 stage[BLOCK / 64][256];
-    MetT<false> m;
-    met_init(m, lm);
-    const HashTable pol = p.eps[ep].policy;
-    Hit hits[PPT];
-#pragma unroll
-    for (int k = 0; k < PPT; ++k) {
-        hits[k] = Hit{nullptr, 0};
-        const uint32_t i = blockIdx.x * (PPT * BLOCK) + k * BLOCK + threadIdx.x;
-        const uint32_t i0 = i - (threadIdx.x & 63);
-        Rec r;
-        if (p.recmode == 2 && b.stride == 64 && i0 + 64 <= b.n) rec_load_wave64(r, b, i0, 3, stage[threadIdx.x >> 6]);
-        else if (i >= b.n) continue;
-        else if (p.recmode == 1) rec_load_plain(r, b, i, 3);
-        else rec_load(r, b, i, 3);
-        Acct a{0, 0};
-        bool skip_proxy = false;
-        uint32_t identity = 0;
-        if (p.flags & F_FROM_HOST) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
-        const uint32_t eth = r.len >= 14 ? rec_raw16c<12>(r) : 0u;
-        int32_t ret;
-        uint16_t proxy = 0;
-        if (eth != 0x0008u) {
-            ret = DROP_UNKNOWN_L3;
-        } else if (r.len < 34) {
-            ret = DROP_INVALID;
-        } else {
-            if (identity < HEALTH_ID && !(p.ablate & AB_NO_IPCACHE)) {   // bpf_netdev.c:375-398
-                const uint32_t lab = ipcache4(p, rec_raw32c<26>(r), a);
-                if (lab && lab != CLUSTER_ID && lab != HOST_ID) identity = lab;
-            }
-            uint32_t dport, proto;
-            ret = l4_key_new_flow(r, dport, proto);
-            if (ret == 0) {
-                const int v = (p.ablate & AB_NO_POLICY)
-                                  ? (int)(identity & 1)
-                                  : policy_ingress(pol, p.flags | (p.ablate << 16), r.len, identity, dport, proto, a,
-                                                   &hits[k]);
-                if (v < 0) ret = DROP_POLICY;
-                else if (skip_proxy && v > 0) ret = 0;
-                else { ret = v; proxy = v > 0 ? (uint16_t)v : 0; }
-            }
-        }
-        const bool dropped = ret < 0 && ret != E_TRUNC;
-        if (dropped && !(p.ablate & AB_NO_METRICS)) m.drop(ret, r.len, METRIC_INGRESS);
-        if (o.ret) o.ret[i] = ret;
-        if (o.reason) o.reason[i] = dropped ? ret : 0;
-        if (o.identity) o.identity[i] = identity;
-        if (o.proxy) o.proxy[i] = proxy;
-        if (o.ct) o.ct[i] = CT_NONE;
-        store_out(o, i, a);
-    }
-#pragma unroll
-    for (int k = 0; k < PPT; ++k) hit_flush(hits[k]);
-    met_flush(m, p.metrics);
-}
-#endif
 
 // ================================================================== config 3
 // handle_ipv6 of bpf_netdev (bpf_netdev.c:172-276; HANDLE_NS, FROM_HOST, no
@@ -691,7 +610,9 @@ void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStr
 
 // ------------------------------------------------------------------ CT map API
 // Single-element BPF_MAP_{LOOKUP,UPDATE,DELETE}_ELEM on a device-resident CT table
-// (the agent side of pkg/maps/ctmap: GC deletes, dumps, restores).
+// (the agent side of pkg/maps/ctmap: GC deletes, dumps, restores), with the kernel
+// hash map's errnos: NOEXIST on an existing key -EEXIST, EXIST on a missing one
+// -ENOENT, a new key past max_entries -E2BIG.  Keeps the live-entry count.
 template <class S>
 __device__ void ct_op(HashTable t, int op, uint64_t flags, uint32_t *io)
 {
@@ -710,11 +631,13 @@ __device__ void ct_op(HashTable t, int op, uint64_t flags, uint32_t *io)
     } else if (op == 1) {
         if (s >= 0 && flags == 1) rc = -EEXIST;
         else if (s < 0 && flags == 2) rc = -ENOENT;
+        else if (s < 0 && t.live && *t.live >= t.cap) rc = -E2BIG;
         else {
             bool created;
             s = dev_upsert<S>(t, key, &created);
             if (s < 0) rc = -E2BIG;
             else {
+                if (created && t.live) atomicAdd(t.live, 1ull);
                 CtE e;
                 for (int k = 0; k < 16; ++k) e.w[k] = val[k];
                 ct_store(t, s, e);
@@ -722,7 +645,10 @@ __device__ void ct_op(HashTable t, int op, uint64_t flags, uint32_t *io)
         }
     } else {
         if (s < 0) rc = -ENOENT;
-        else dev_kill<S>(t, s);
+        else {
+            dev_kill<S>(t, s);
+            if (t.live) atomicAdd(t.live, ~0ull);
+        }
     }
     *rcp = (uint32_t)rc;
 }
@@ -734,9 +660,52 @@ __global__ void k_ct_op(HashTable t, int v6, int op, uint64_t flags, uint32_t *i
     else ct_op<Ct4Spec>(t, op, flags, io);
 }
 
-// compact every live entry (tag >= 3) into key/value arrays
+// Initial fill of a CT map from the agent's entries (a restore, or a synthetic table):
+// n distinct keys (KW words each) and ct_entry values (16 words each), inserted in
+// parallel (the CAS slot claim of dev_upsert); *fail counts keys past the probe limit.
 template <class S>
-__device__ void ct_scan(HashTable t, uint64_t nslots, uint32_t *keys, uint32_t *vals, uint32_t *count, uint32_t max)
+__device__ void ct_load_t(HashTable t, const uint32_t *keys, const uint32_t *vals, uint64_t n, uint32_t *fail)
+{
+    for (uint64_t i = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        uint32_t k[S::KW];
+#pragma unroll
+        for (int j = 0; j < S::KW; ++j) k[j] = keys[i * S::KW + j];
+        bool created;
+        const int64_t sl = dev_upsert<S>(t, k, &created);
+        if (sl < 0) { atomicAdd(fail, 1u); continue; }
+        CtE e;
+        const uint4 *q = reinterpret_cast<const uint4 *>(vals + i * 16);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint4 v = q[w];
+            e.w[4 * w] = v.x; e.w[4 * w + 1] = v.y; e.w[4 * w + 2] = v.z; e.w[4 * w + 3] = v.w;
+        }
+        ct_store(t, sl, e);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_ct_load(HashTable t, int v6, const uint32_t *keys, const uint32_t *vals,
+                                                   uint64_t n, uint32_t *fail)
+{
+    if (v6) ct_load_t<Ct6Spec>(t, keys, vals, n, fail);
+    else ct_load_t<Ct4Spec>(t, keys, vals, n, fail);
+}
+
+int launch_ct_load(const HashTable &t, int v6, const uint32_t *keys, const uint32_t *vals, uint64_t n, uint32_t *fail,
+                   hipStream_t s)
+{
+    if (!n) return 0;
+    uint64_t g = (n + BLOCK - 1) / BLOCK;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_ct_load, dim3((uint32_t)g), dim3(BLOCK), 0, s, t, v6, keys, vals, n, fail);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// every live entry (tag >= 3): its slot index, key and value, compacted in no order
+// (the host sorts by slot: the table's walk order, stable while entries stay put)
+template <class S>
+__device__ void ct_scan(HashTable t, uint64_t nslots, uint64_t *slots, uint32_t *keys, uint32_t *vals, uint32_t *count,
+                        uint32_t max)
 {
     for (uint64_t x = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; x < nslots; x += (uint64_t)gridDim.x * BLOCK) {
         const uint64_t b = x / S::SPB;
@@ -746,20 +715,21 @@ __device__ void ct_scan(HashTable t, uint64_t nslots, uint32_t *keys, uint32_t *
         if (tag < 3) continue;
         const uint32_t at = atomicAdd(count, 1u);
         if (at >= max) continue;
+        if (slots) slots[at] = x;
         for (int j = 0; j < S::KW; ++j) keys[(size_t)at * S::KW + j] = bw[S::KEY0 + sl * S::KW + j];
         const uint32_t *v = reinterpret_cast<const uint32_t *>(t.vals + x * t.vstride);
         for (int j = 0; j < 16; ++j) vals[(size_t)at * 16 + j] = v[j];
     }
 }
 
-__global__ void k_ct_scan(HashTable t, int v6, uint64_t nslots, uint32_t *keys, uint32_t *vals, uint32_t *count,
-                          uint32_t max)
+__global__ void k_ct_scan(HashTable t, int v6, uint64_t nslots, uint64_t *slots, uint32_t *keys, uint32_t *vals,
+                          uint32_t *count, uint32_t max)
 {
-    if (v6) ct_scan<Ct6Spec>(t, nslots, keys, vals, count, max);
-    else ct_scan<Ct4Spec>(t, nslots, keys, vals, count, max);
+    if (v6) ct_scan<Ct6Spec>(t, nslots, slots, keys, vals, count, max);
+    else ct_scan<Ct4Spec>(t, nslots, slots, keys, vals, count, max);
 }
 
-// ctmap.GC with GCFilterByTime (pkg/maps/ctmap/ctmap.go:325-432): one pass over the
+// ctmap.GC with GCFilterByTime (pkg/maps/ctmap/ctmap.go:247-448): one pass over the
 // table, a lane per bucket: read the 8 tag bytes, then the lifetime word of every
 // live slot, and mark the expired ones dead (the bucket's tag word rewritten once;
 // the pass runs stream-ordered between batches, so it is the only writer).
@@ -784,7 +754,10 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
         if (out != tags) *reinterpret_cast<uint2 *>(bw) = make_uint2((uint32_t)out, (uint32_t)(out >> 32));
     }
     const unsigned long long tot = wave_sum(mine);
-    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(deleted, (uint32_t)tot);
+    if ((threadIdx.x & 63) == 0 && tot) {
+        atomicAdd(deleted, (uint32_t)tot);
+        if (t.live) atomicAdd(t.live, 0ull - tot);
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_ct_gc(HashTable t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted)
@@ -873,13 +846,14 @@ int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *i
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint32_t *out_keys, uint32_t *out_vals, uint32_t *count,
-                   uint32_t max, hipStream_t s)
+int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint64_t *out_slots, uint32_t *out_keys, uint32_t *out_vals,
+                   uint32_t *count, uint32_t max, hipStream_t s)
 {
     const uint64_t slots = nb * (v6 ? Ct6Spec::SPB : Ct4Spec::SPB);
     uint64_t g = (slots + BLOCK - 1) / BLOCK;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_ct_scan, dim3((uint32_t)g), dim3(BLOCK), 0, s, t, v6, slots, out_keys, out_vals, count, max);
+    hipLaunchKernelGGL(k_ct_scan, dim3((uint32_t)g), dim3(BLOCK), 0, s, t, v6, slots, out_slots, out_keys, out_vals,
+                       count, max);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

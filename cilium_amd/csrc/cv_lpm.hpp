@@ -50,16 +50,9 @@ __device__ __forceinline__ uint32_t lpm4_lookup_q(const Lpm4 &t, uint32_t addr /
 {
     const uint32_t k = bswap32(addr);
     uint32_t v = 0;
-#ifdef CV_L1_PREFETCH
-    const uint32_t l1 = want ? t.l1[addr >> 16] : 0u;             // in flight with the front probe
-#endif
     if (t.full.buckets && quad_find<Host32Spec>(t.full, &k, want, st, &v) >= 0) return v;   // (uniform test)
     if (!want) return 0;
-#ifdef CV_L1_PREFETCH
-    uint32_t e = l1;
-#else
-    uint32_t e = t.l1[addr >> 16];
-#endif
+    uint32_t e = t.l1[addr >> 16];                                // (prefetching it beside the front: +2 %)
     if (e & 0x80000000u) {
         e = t.chunks[((e & 0x7FFFFFFFu) << 8) | ((addr >> 8) & 0xFFu)];
         if (e & 0x80000000u) e = t.chunks[((e & 0x7FFFFFFFu) << 8) | (addr & 0xFFu)];

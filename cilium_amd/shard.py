@@ -45,18 +45,42 @@ def pair_key4(saddr_raw: np.ndarray, daddr_raw: np.ndarray) -> np.ndarray:
     return mix64((lo << np.uint64(32)) | hi)
 
 
+def _be64(a: np.ndarray, off: int) -> np.ndarray:
+    return np.ascontiguousarray(a[:, off:off + 8]).view(">u8").reshape(-1).astype(np.uint64)
+
+
+def pair_key6(a16: np.ndarray, b16: np.ndarray) -> np.ndarray:
+    """Direction-symmetric key of IPv6 address pairs ((n, 16) byte rows): the
+    lexicographically smaller address first, mixed word by word."""
+    ah, al, bh, bl = _be64(a16, 0), _be64(a16, 8), _be64(b16, 0), _be64(b16, 8)
+    a_lt = (ah < bh) | ((ah == bh) & (al < bl))
+    lh, ll = np.where(a_lt, ah, bh), np.where(a_lt, al, bl)
+    hh, hl = np.where(a_lt, bh, ah), np.where(a_lt, bl, al)
+    with np.errstate(over="ignore"):
+        z = mix64(lh ^ np.uint64(0x6A09E667F3BCC908))
+        z = mix64(z ^ ll) + np.uint64(0x9E3779B97F4A7C15)
+        z = mix64(z ^ hh) + np.uint64(0x9E3779B97F4A7C15)
+        return mix64(z ^ hl)
+
+
 def flow_shard(frames: np.ndarray, length: np.ndarray, world: int) -> np.ndarray:
-    """Owner rank of every IPv4 packet of a batch (non-IPv4 / short frames: rank 0,
-    their verdicts touch no conntrack state on the ingress path)."""
+    """Owner rank of every packet of a batch: IPv4 by its address pair, IPv6 by its
+    128-bit address pair (other frames: rank 0, their verdicts touch no conntrack
+    state on the ingress path)."""
     frames = np.asarray(frames, np.uint8)
     n = len(frames)
     out = np.zeros(n, np.int64)
     if world <= 1 or n == 0:
         return out
+    length = np.asarray(length)
     eth = (frames[:, 12].astype(np.uint16) << 8) | frames[:, 13]
-    v4 = (eth == 0x0800) & (np.asarray(length) >= 34)
+    v4 = (eth == 0x0800) & (length >= 34)
     key = pair_key4(_raw32(frames, 26), _raw32(frames, 30))
     out[v4] = (key[v4] % np.uint64(world)).astype(np.int64)
+    v6 = (eth == 0x86DD) & (length >= 54) & (frames.shape[1] >= 54)
+    if v6.any():
+        k6 = pair_key6(frames[v6, 22:38], frames[v6, 38:54])
+        out[v6] = (k6 % np.uint64(world)).astype(np.int64)
     return out
 
 
@@ -69,6 +93,14 @@ def ct4_shard(keys: np.ndarray, world: int) -> np.ndarray:
     return (key % np.uint64(world)).astype(np.int64)
 
 
+def ct6_shard(keys: np.ndarray, world: int) -> np.ndarray:
+    """Owner rank of ipv6_ct_tuple keys (40-B rows: daddr @0, saddr @16)."""
+    keys = np.asarray(keys, np.uint8)
+    if world <= 1 or len(keys) == 0:
+        return np.zeros(len(keys), np.int64)
+    return (pair_key6(keys[:, 16:32], keys[:, 0:16]) % np.uint64(world)).astype(np.int64)
+
+
 def split_workload(w, world: int, rank: int):
     """The rank's share of a synthetic ingress workload: its packets (in their
     original order) and its conntrack shard; the other tables stay whole."""
@@ -76,16 +108,19 @@ def split_workload(w, world: int, rank: int):
     from cilium_amd import synth
     own = np.nonzero(flow_shard(w.frames, w.length, world) == rank)[0]
     maps = dict(w.maps)
-    if "ct4" in maps:
-        ct = maps["ct4"]
-        mine = ct4_shard(ct.keys, world) == rank
-        maps["ct4"] = synth.MapSpec(ct.name, ct.type, ct.key_size, ct.val_size, ct.max_entries,
-                                    ct.keys[mine], ct.vals[mine])
+    for name, fn in (("ct4", ct4_shard), ("ct6", ct6_shard)):
+        if name in maps:
+            ct = maps[name]
+            mine = fn(ct.keys, world) == rank
+            maps[name] = synth.MapSpec(ct.name, ct.type, ct.key_size, ct.val_size, ct.max_entries,
+                                       ct.keys[mine], ct.vals[mine])
     part = copy.copy(w)
     part.maps = maps
     part.frames = w.frames[own]
     part.length = w.length[own]
     part.mark = w.mark[own]
+    if w.extra:
+        part.extra = {k: (v[own] if isinstance(v, np.ndarray) and len(v) == w.n else v) for k, v in w.extra.items()}
     return part, own
 
 

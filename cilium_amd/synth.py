@@ -964,4 +964,55 @@ def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n
                            "node": {"cluster_mask": CLUSTER_V4[1], "cluster_range": CLUSTER_V4[0],
                                     "loopback": IPV4_LOOPBACK, "router_ip6": ROUTER_IP6,
                                     "host_mac": bytes([0x02, 0x00, 0x00, 0x00, 0xFE, 0x01])},
-                           "kind": kind[fi], "reply": rep, "v6": f6})
+                           "kind": kind[fi], "reply": rep, "v6": f6, "flow": fi, "hbh": hbh})
+
+
+# --------------------------------------------------------------------------
+# Benchmark steps of the stateful configs
+# --------------------------------------------------------------------------
+
+def port_variant(w: Workload, v: int, fresh_frac: float = 0.2):
+    """Step v (>= 1) of a stateful benchmark: the batch with fresh client ports on its
+    new flows, so every step creates conntrack entries the way the workload says
+    instead of replaying flows an earlier step created.  Config 3 / 4: every new-flow
+    packet (kind 2) takes source port 1024 + (sport - 1024 + 4099 v) mod 64512.
+    Config 5: the flows whose (flow, v) hash falls under fresh_frac take that client
+    port (the source port of the client's packets, the destination port of the
+    replies); the other flows keep theirs and stay established.  v = 0 is the batch
+    itself.  Returns (rows, byte offsets of the 2-byte port, new port values)."""
+    f = w.frames
+    key = ("_pv", fresh_frac if w.name == "config5" else None)
+    if w.name == "config3" and key in (w.extra or {}):
+        rows, offs, old = w.extra[key]                # (the new-flow rows do not depend on v)
+        rows, offs = (rows[:0], offs[:0]) if v == 0 else (rows, offs)
+        return rows, offs, 1024 + (old[:len(rows)] - 1024 + 4099 * v) % 64512
+    if w.name == "config3":
+        rows = np.nonzero(w.extra["kind"] == 2)[0]
+        v6 = w.extra.get("v6")
+        if v6 is not None:
+            rows = rows[~v6[rows]]
+        proto = f[rows, 23]
+        rows = rows[(proto == TCP) | (proto == UDP)]
+        offs = 14 + 4 * (f[rows, 14] & 0xF).astype(np.int64)
+    elif w.name == "config5":
+        fl = w.extra["flow"].astype(np.uint64)
+        with np.errstate(over="ignore"):
+            h = splitmix64(0x5EED0000 + v, 1)[0] ^ (fl * GOLDEN)
+        h = (h ^ (h >> np.uint64(31))) * np.uint64(0xBF58476D1CE4E5B9)
+        fresh = ((h >> np.uint64(40)).astype(np.float64) / float(1 << 24)) < fresh_frac
+        v6 = w.extra["v6"]
+        l4 = np.where(v6, np.where(w.extra["hbh"], 62, 54), 34)
+        nh6 = f[:, 54] if f.shape[1] > 54 else np.zeros(w.n, np.uint8)
+        proto = np.where(v6, np.where(w.extra["hbh"], nh6, f[:, 20]), f[:, 23])
+        ok = fresh & ((proto == TCP) | (proto == UDP)) & (l4 + 4 <= f.shape[1])
+        rows = np.nonzero(ok)[0]
+        offs = l4[rows] + np.where(w.extra["reply"][rows], 2, 0)
+    else:
+        raise ValueError(w.name)
+    old = (f[rows, offs].astype(np.int64) << 8) | f[rows, offs + 1]
+    if w.name == "config3" and w.extra is not None:
+        w.extra[key] = (rows, offs, old)
+    if v == 0:
+        rows, offs, old = rows[:0], offs[:0], old[:0]
+    new = 1024 + (old - 1024 + 4099 * v) % 64512
+    return rows, offs, new.astype(np.int64)

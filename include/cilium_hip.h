@@ -97,6 +97,9 @@ int cv_map_create(cv_ctx *ctx, int type, uint32_t key_size, uint32_t val_size,
 int cv_map_update(cv_ctx *ctx, int h, const void *key, const void *val, uint64_t flags);
 int cv_map_lookup(cv_ctx *ctx, int h, const void *key, void *val);
 int cv_map_delete(cv_ctx *ctx, int h, const void *key);
+/* GetNextKey: the element after `key` in the map's walk order, the first when key is
+ * NULL or absent, -ENOENT at the end.  O(1) per call (a device CT map walks a snapshot
+ * taken once per table generation, in slot order). */
 int cv_map_get_next_key(cv_ctx *ctx, int h, const void *key, void *next_key);
 int cv_map_close(cv_ctx *ctx, int h);
 /* bulk form of cv_map_update in array order (later writes of a key win);
@@ -111,7 +114,16 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
  * ipv6_ct_tuple keys, ct_entry values) whose lifetime < time; *deleted = count.
  * Replaces ctmap.GC(m, name, GCFilterByTime) / doGC4 / doGC6 and, with
  * time = 0xFFFFFFFF, ctmap.Flush (pkg/maps/ctmap/ctmap.go:247-448).  Runs on the GPU
- * for a bound CT map, ordered after the batches already submitted. */
+ * for a bound CT map after waiting for every batch already submitted, on any stream
+ * (as every map operation on a device-resident table does).
+ *
+ * Conntrack capacity: a CT map holds at most max_entries entries.  The reference's
+ * CT maps are LRU_HASH (bpf_lxc.c:53-75), which evict at capacity in an order the
+ * kernel's per-CPU LRU lists decide; that order is not reproducible, so here a CT map
+ * behaves like a kernel HASH map: a create past max_entries fails (-E2BIG, the
+ * datapath's DROP_CT_CREATE_FAILED), identically in the oracle.  Size max_entries for
+ * the flows the node keeps (HBM: ~137 B per entry at the 60 % bucket load) and run
+ * cv_ct_gc.  A batch next to the limit is processed in exact one-packet launches. */
 int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
 
 /* ---- binding: programs -> maps ---- */

@@ -103,3 +103,59 @@ def sorted_rows(keys, vals):
     rows = np.concatenate([keys, vals], axis=1)
     order = np.lexsort(keys.T[::-1])
     return rows[order]
+
+
+def apply_variant(frames, rows, offs, ports):
+    """frames with the 2-byte big-endian ports of synth.port_variant written in"""
+    out = frames.copy()
+    out[rows, offs] = (ports >> 8).astype(np.uint8)
+    out[rows, offs + 1] = (ports & 0xFF).astype(np.uint8)
+    return out
+
+
+class ShardedOracle:
+    """The ingress oracle run the way the GPU runs it: packets partitioned by
+    direction-symmetric address pair (cilium_amd.shard, the config-4 key), one
+    datapath per shard holding that shard's conntrack entries, shards processed on
+    parallel host threads (ctypes releases the GIL).  Address pairs share no CT
+    entry, so the union equals one sequential run (tests/test_multi_rank.py)."""
+
+    def __init__(self, w: synth.Workload, threads: int):
+        from cilium_amd import shard
+        self.T = max(1, threads)
+        self.w = w
+        self.parts = []
+        for t in range(self.T):
+            part, own = shard.split_workload(w, self.T, t)
+            dp, maps = oracle_dp(part)
+            self.parts.append((own, dp, maps))
+
+    def netdev_ingress(self, frames=None, now=None, pool=None):
+        """verdicts of the whole batch (packet order) and the parallel section's wall time"""
+        import time
+        from concurrent.futures import ThreadPoolExecutor
+        w = self.w
+        frames = w.frames if frames is None else frames
+        now = w.now if now is None else now
+        inputs = [(np.ascontiguousarray(frames[own]), np.ascontiguousarray(w.length[own]),
+                   np.ascontiguousarray(w.mark[own])) for own, _, _ in self.parts]
+        run = lambda t: self.parts[t][1].netdev_ingress(*inputs[t], now=now)
+        ex = pool or ThreadPoolExecutor(self.T)
+        t0 = time.perf_counter()
+        outs = list(ex.map(run, range(self.T)))
+        el = time.perf_counter() - t0
+        if pool is None:
+            ex.shutdown()
+        from oracle import oracle as O
+        res = O.Out(w.n)
+        for (own, _, _), o in zip(self.parts, outs):
+            for k in O.Out.FIELDS:
+                getattr(res, k)[own] = getattr(o, k)
+        return res, el
+
+    def metrics(self):
+        return sum(dp.metrics() for _, dp, _ in self.parts)
+
+    def dump(self, name):
+        ks, vs = zip(*(maps[name].dump() for _, _, maps in self.parts))
+        return np.concatenate(ks), np.concatenate(vs)

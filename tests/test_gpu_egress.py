@@ -286,3 +286,12 @@ def test_config5_v6_extension_headers(dev):
     w = synth.config5(1 << 13, n_svc=300, n_ep=48, n_remote=96, family=6, seed=58)
     _v6_ext_chains(w, 0xE7)
     check_egress(w, dev, batches=2)
+
+
+def test_ct_capacity_egress(dev):
+    """Egress CT4 / CT6 maps reaching max_entries inside a batch: service creates,
+    connection creates with their NAT tuples and the delivery's ingress creates fail
+    past the limit exactly where the sequential oracle's do."""
+    w = synth.config5(1 << 12, n_svc=2000, n_ep=256, n_remote=512, ct_max=1500)
+    dp = check_egress(w, dev, batches=2, rounds=1)
+    assert dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0       # DROP_CT_CREATE_FAILED happened

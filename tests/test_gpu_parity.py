@@ -345,6 +345,19 @@ def test_config3_dual_stack_64b_records(dev):
     check_ingress(w, dev, batches=2, with_prefilter=False)
 
 
+def test_ct_capacity_ingress(dev):
+    """A CT map filled to max_entries: creates past it fail (DROP_CT_CREATE_FAILED,
+    kernel HASH semantics) at the same packets as the oracle, including a tuple that
+    fits while its ICMP-related twin does not; the launches next to the limit are the
+    exact one-packet ones.  Live counts, tables and verdicts compared every batch."""
+    w = synth.config3(1 << 13, 64, n_ep=64, n_cidrs=1024, n_ids=100, seed=31, v6_frac=0.3, n_flows6=16)
+    for name, room in (("ct4", 150), ("ct6", 10)):
+        spec = w.maps[name]
+        spec.max_entries = len(np.unique(spec.keys, axis=0)) + room
+    dp = check_ingress(w, dev, batches=3, with_prefilter=False)
+    assert (dp.metrics()[155, 1, 0]) > 100                              # DROP_CT_CREATE_FAILED happened
+
+
 def test_ct_map_api_on_device(dev):
     w = synth.config3(1 << 10, 256, n_ep=8, n_cidrs=256, n_ids=20, seed=5)
     dp, om = H.oracle_dp(w)
@@ -361,6 +374,24 @@ def test_ct_map_api_on_device(dev):
     assert ct_p.update(keys[0].tobytes(), v, 1) == ct_o.update(keys[0].tobytes(), v, 1)    # EEXIST
     assert ct_p.lookup(keys[0].tobytes()) == (0, v)
     assert len(ct_p) == len(ct_o)
+    # GetNextKey: every key once, then -ENOENT; an absent key restarts at the first
+    seen, k = [], None
+    while True:
+        rc, k = ct_p.next_key(k)
+        if rc:
+            break
+        seen.append(k)
+    assert len(seen) == len(set(seen)) == len(ct_o)
+    assert ct_p.next_key(bytes(14)) == (0, seen[0])
+    # max_entries: an update of a new key into a full map fails like the kernel's (-E2BIG)
+    full = synth.config3(1 << 6, 8, n_ep=4, n_cidrs=64, n_ids=8, seed=6)
+    spec = full.maps["ct4"]
+    spec.max_entries = len(np.unique(spec.keys, axis=0))
+    _, fm = H.product_ctx(full)
+    _, fo = H.oracle_dp(full)
+    assert fm["ct4"].update(bytes(range(14)), v) == fo["ct4"].update(bytes(range(14)), v) == -7   # -E2BIG
+    assert fm["ct4"].delete(spec.keys[0].tobytes()) == 0 == fo["ct4"].delete(spec.keys[0].tobytes())
+    assert fm["ct4"].update(bytes(range(14)), v) == 0 == fo["ct4"].update(bytes(range(14)), v)
     ck, cv = ct_p.dump()
     ok, ov = ct_o.dump()
     assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
@@ -505,3 +536,17 @@ def test_policy_churn_between_batches(dev, monkeypatch, incremental):
                 keys = [x for x in keys if x.tobytes() != k]
     assert (ctx.metrics() == dp.metrics()).all()
     ctx.close()
+
+
+def test_ct_walk_get_next_key_linear(dev):
+    """GetNextKey over a 1M-entry device CT map from a C caller (tests/ct_walk.c, the
+    cgo glue's view of the C-ABI): every key exactly once, then -ENOENT, in well under
+    a second (the dump walk of pkg/maps/ctmap/ctmap.go:196-230)."""
+    import subprocess
+    from cilium_amd import build
+    out = subprocess.run([build.WALK_BIN, str(1 << 20)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    f = out.stdout.split()
+    got = dict(zip(f[0::2], f[1::2]))
+    assert int(got["count"]) == int(got["entries"]) == int(got["visited"]) == int(got["unique"]) == 1 << 20
+    assert float(got["walk_s"]) < 1.0, got

@@ -129,3 +129,24 @@ def test_two_ranks_gloo_hip():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _check(_run(2, use_gpu=True))
+
+
+def test_sharded_oracle_threads_equal_sequential():
+    """bench.py's CPU baseline for the conntrack paths: the oracle partitioned by
+    address pair over host threads (tests/harness.ShardedOracle) gives the sequential
+    run's verdicts, CT4 / CT6 tables and counters, IPv6 pairs included, over two
+    batches (the second one with fresh client ports, synth.port_variant)."""
+    w = synth.config3(1 << 13, 1 << 10, n_ep=64, n_cidrs=1024, n_ids=100, seed=43, v6_frac=0.3)
+    dp, om = H.oracle_dp(w)
+    so = H.ShardedOracle(w, 4)
+    for v in (0, 1):
+        f = H.apply_variant(w.frames, *synth.port_variant(w, v))
+        ref = dp.netdev_ingress(f, w.length, w.mark, now=w.now + v)
+        got, _ = so.netdev_ingress(f, now=w.now + v)
+        for k in ("ret", "identity", "ct", "reason", "nl", "nu", "proxy"):
+            assert (getattr(got, k) == getattr(ref, k)).all(), (v, k)
+    assert (so.metrics() == dp.metrics()).all()
+    for name in ("ct4", "ct6"):
+        ck, cv = so.dump(name)
+        ok, ov = om[name].dump()
+        assert len(ck) == len(ok) and (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), name

@@ -163,7 +163,8 @@ def cpu_baseline(name, w, min_seconds=10.0):
         sample = min(w.n, 1 << 20 if name != "config5" else 1 << 18)
         sw = copy.copy(w)
         sw.frames, sw.length, sw.mark = w.frames[:sample], w.length[:sample], w.mark[:sample]
-        sw.extra = {k: (x[:sample] if isinstance(x, np.ndarray) and len(x) == w.n else x) for k, x in w.extra.items()}
+        sw.extra = {k: (x[:sample] if isinstance(x, np.ndarray) and len(x) == w.n else x) for k, x in w.extra.items()
+                    if not isinstance(k, tuple)}                  # (not port_variant's cache of the full batch)
         if name == "config5":
             dp, _ = H.oracle_dp(sw)
             cores, how = 1, "1 thread, sequential (egress conntrack groups are not address pairs)"

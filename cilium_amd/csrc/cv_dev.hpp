@@ -640,9 +640,11 @@ __device__ __forceinline__ uint8_t xdp_verdict(const DpParams &p, const RecT<NW>
 // xdp_verdict with the IPv4 table probes as quad probes (cv_hash.hpp quad_find):
 // every lane of the wave calls it (`live` false past the batch end); other frames
 // take xdp_verdict's per-lane path, which then does no IPv4 probe.
+// *lxc_slot / *lxc_iv (optional): the cilium_lxc probe of an IPv4 daddr, for a caller
+// that looks the same key up again in the same table (from_netdev's handle_ipv4)
 template <int NW>
 __device__ __forceinline__ uint8_t xdp_verdict_q(const DpParams &p, const RecT<NW> &r, Acct &a, bool live,
-                                                 uint4 *st)
+                                                 uint4 *st, int64_t *lxc_slot = nullptr, uint32_t *lxc_iv = nullptr)
 {
     const bool v4 = live && r.len >= 34 && rec_raw16c<12>(r) == 0x0008u;
     uint32_t saddr = rec_raw32c<26>(r), daddr = rec_raw32c<30>(r);
@@ -659,7 +661,9 @@ __device__ __forceinline__ uint8_t xdp_verdict_q(const DpParams &p, const RecT<N
     uint32_t iv = 0;
     const bool want_lxc = v4 && !drop && p.lxc4.buckets;
     if (want_lxc) a.nl++;
-    const bool hit = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv) >= 0;
+    const int64_t ls = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv);
+    const bool hit = ls >= 0;
+    if (lxc_slot) { *lxc_slot = ls; *lxc_iv = iv; }
     if (v4) return (!drop && hit) ? XDP_PASS : XDP_DROP;
     if (!live) return XDP_PASS;
     return xdp_verdict(p, r, a);

@@ -238,7 +238,9 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         int32_t ret = TC_ACT_OK, reason = 0;
         uint32_t ident = 0;
         bool staged = false, v6stage = false, dmac_rw = false;
-        if (with_prefilter) xv = xdp_verdict_q(p, r, a, live, st);
+        int64_t lxc_slot = -1;
+        uint32_t iv = 0;
+        if (with_prefilter) xv = xdp_verdict_q(p, r, a, live, st, &lxc_slot, &iv);
         const bool pass = live && xv == XDP_PASS;
         bool skip_proxy = false;
         uint32_t identity = 0;
@@ -274,9 +276,11 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         }
         const bool want_lxc = v4 && h == TC_ACT_OK && p.lxc4.buckets;
         if (want_lxc) a.nl++;                                     // lookup_ip4_endpoint
-        uint32_t iv = 0;
         uint32_t daddr = rec_raw32c<30>(r);
-        int64_t lxc_slot = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv);
+        // with the prefilter, an IPv4 packet got here only after check_v4_endpoint
+        // found its daddr in the same table: that probe's answer is reused (read-only
+        // within the launch); without it, one quad probe (wave-uniform branch)
+        if (!with_prefilter) lxc_slot = quad_find<LxcV4Spec>(p.lxc4, &daddr, want_lxc, st, &iv);
         const bool lxc_hit = lxc_slot >= 0;
         if (pass && eth == 0x0008u) {
             if (r.len < 34) {

@@ -120,7 +120,8 @@ def split_workload(w, world: int, rank: int):
     part.length = w.length[own]
     part.mark = w.mark[own]
     if w.extra:
-        part.extra = {k: (v[own] if isinstance(v, np.ndarray) and len(v) == w.n else v) for k, v in w.extra.items()}
+        part.extra = {k: (v[own] if isinstance(v, np.ndarray) and len(v) == w.n else v) for k, v in w.extra.items()
+                      if not isinstance(k, tuple)}
     return part, own
 
 

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session: the -m gpu tests, the bench line, and the rocprofv3 kernel
+# summary of one workload.  Every GPU step has its own time limit and the chain stops
+# at the first failure.
+#   usage: bash tools/gpu_session.sh <tag> <workload> [pytest -k expr | all | -]
+set -u
+TAG=${1:-r02}
+W=${2:-config3}
+K=${3:-all}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() { echo "[$(date +%T)] $*"; }
+if [ "$K" != "-" ]; then
+  step pytest
+  if [ "$K" = "all" ]; then KARG=(); else KARG=(-k "$K"); fi
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${KARG[@]}" \
+      > "$OUT/pytest.log" 2>&1 || { echo "pytest failed rc=$?"; grep -E "FAILED|Error" "$OUT/pytest.log" | head; tail -30 "$OUT/pytest.log"; exit 1; }
+  grep -cE "PASSED" "$OUT/pytest.log"
+fi
+step bench
+timeout -k 10 600 python3 -u bench.py --workload "$W" > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err" \
+    || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$W.err"; exit 1; }
+cat "$OUT/bench_$W.json"
+step rocprof-stats
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$W" -o run --output-format csv \
+    -- python3 bench.py --workload "$W" --steps 10 --warmup 2 --no-cpu > "$OUT/stats_$W.log" 2>&1 \
+    || { echo "rocprof stats failed rc=$?"; tail -20 "$OUT/stats_$W.log"; exit 1; }
+find "$OUT/stats_$W" -name "*kernel_stats.csv" -exec cp {} "$OUT/${W}_kernel_stats.csv" \;
+head -12 "$OUT/${W}_kernel_stats.csv"
+step done

@@ -2,7 +2,8 @@
 
 The product is the C-ABI library ``cilium_amd/_lib/libcilium_hip.so`` (HIP kernels for
 gfx950 + the map store); this package holds its sources (``csrc/``), a thin ctypes
-binding (``lib``) and the host-side mirror of the reference's pkg/maps API (``maps``).
+binding of the C-ABI (``lib``), the synthetic BASELINE workloads (``synth``), the
+address-pair sharding of conntrack over GPUs (``shard``) and the build (``build``).
 Importing the package does not load the library; ``cilium_amd.lib.load()`` does and
 raises if it is missing.
 """

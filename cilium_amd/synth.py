@@ -419,9 +419,13 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     pol_proto = pol[:, 6]
     l4 = pol_proto != 0
     pp, pr = pol_port[l4], pol_proto[l4]
+    ident = c2.maps["ipcache"].vals[pick, 0:4].copy().view("<u4").reshape(-1)
+    # a connection exists because the policy let it in: the service port is one the
+    # remote's identity may reach (its L4 entries; an identity without any: a random one)
     sel = s.choice(n_flows, len(pp))
-    fport = pp[sel].astype(np.int64)
-    fproto = pr[sel].astype(np.uint8)
+    aport, aproto, has = _allowed_l4(pol, ident, s)
+    fport = np.where(has, aport, pp[sel]).astype(np.int64)
+    fproto = np.where(has, aproto, pr[sel]).astype(np.uint8)
     eport = s.randint(n_flows, 1024, 65536)
     ingress_init = s.frac(n_flows) < 0.75
     # CT entries: ingress-initiated {daddr remote, saddr local, dport fport, sport eport, IN}
@@ -431,7 +435,6 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     keys = ct4_keys(d_addr, s_addr, fport, eport, fproto, np.where(ingress_init, 1, 0))
     tcp = fproto == TCP
     seclabel = (0x1000 + ep_ids[epi]).astype(np.uint32)
-    ident = c2.maps["ipcache"].vals[pick, 0:4].copy().view("<u4").reshape(-1)
     vals = ct_entries(n_flows, now0, ingress_init, tcp, np.where(ingress_init, ident, seclabel),
                       seen_non_syn=tcp)
     # ICMP-related twins (conntrack.h:727-741): one per address pair, last writer wins
@@ -463,8 +466,12 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     daddr[new] = lxc_ip[s.choice(nn, n_ep)]
     sport[new] = s.randint(nn, 1024, 65536)
     nsel = s.choice(nn, len(pp))
-    dport[new] = np.where(s.frac(nn) < 0.8, pp[nsel], s.randint(nn, 1, 65536))
-    proto[new] = pr[nsel]
+    nid = c2.maps["ipcache"].vals[npk, 0:4].copy().view("<u4").reshape(-1)
+    nport, nproto, nhas = _allowed_l4(pol, nid, s)
+    r2 = s.frac(nn)                                     # 70% to a port the policy allows
+    allow = nhas & (r2 < 0.7)
+    dport[new] = np.where(allow, nport, np.where(r2 < 0.85, pp[nsel], s.randint(nn, 1, 65536)))
+    proto[new] = np.where(allow, nproto, pr[nsel])
     rf = s.frac(n_pkts)
     flags = np.where(rf < 0.90, TCP_ACK, np.where(rf < 0.95, TCP_SYN, np.where(rf < 0.98, TCP_FIN | TCP_ACK, TCP_RST)))
     ttl = np.where(s.frac(n_pkts) < ttl_low, 1, 64)
@@ -505,6 +512,25 @@ def ct6_keys(daddr6, saddr6, dport, sport, nexthdr, flags) -> np.ndarray:
     return k
 
 
+def _allowed_l4(pol_keys, ident, s):
+    """Per identity of `ident`: one (dport, proto) of its ingress L4 policy entries
+    (policy_key rows), chosen uniformly; `has` false where it has none."""
+    pid = pol_keys[:, 0:4].copy().view("<u4").reshape(-1)
+    port = pol_keys[:, 4:6].copy().view(">u2").reshape(-1).astype(np.int64)
+    proto = pol_keys[:, 6]
+    ok = (pid != 0) & (proto != 0) & (pol_keys[:, 7] == 0)
+    order = np.argsort(pid[ok], kind="stable")
+    ids, ports, protos = pid[ok][order], port[ok][order], proto[ok][order]
+    lo = np.searchsorted(ids, ident, "left")
+    cnt = np.searchsorted(ids, ident, "right") - lo
+    r = (s.u64(len(ident)) % np.maximum(cnt, 1).astype(np.uint64)).astype(np.int64)
+    at = np.minimum(lo + r, max(len(ids) - 1, 0))
+    has = cnt > 0
+    if not len(ids):
+        return np.zeros(len(ident), np.int64), np.zeros(len(ident), np.uint8), has
+    return ports[at], protos[at], has
+
+
 def _config3_v6(s, maps, c2, frames, length, kind4, eps, v6_frac, n_flows6, n_ep, now0, ct_max, pp, pr):
     """The IPv6 half of a dual-stack config 3 (see config3): tables and packets."""
     n_pkts = len(length)
@@ -533,15 +559,19 @@ def _config3_v6(s, maps, c2, frames, length, kind4, eps, v6_frac, n_flows6, n_ep
     # flows: remote (a /128 pod or an address in a /64) <-> local endpoint, CT6 preloaded
     F = n_flows6
     in_net = s.frac(F) < 0.3
-    rem = remote6[s.choice(F, n_r6)].copy()
-    netp = nets[s.choice(F, 64)].copy()
+    ri = s.choice(F, n_r6)
+    ni = s.choice(F, 64)
+    rem = remote6[ri].copy()
+    netp = nets[ni].copy()
     netp[:, 8:16] = s.u64(F).astype(">u8").view(np.uint8).reshape(F, 8)
     rem = np.where(in_net[:, None], netp, rem)
     epi = s.choice(F, n_ep)
     loc = ep_ip6[epi]
     sel = s.choice(F, len(pp))
-    fport = pp[sel].astype(np.int64)
-    fproto = pr[sel].astype(np.uint8)
+    pol = c2.maps["policy"].keys
+    aport, aproto, has = _allowed_l4(pol, np.where(in_net, n_id[ni], r_id[ri]), s)
+    fport = np.where(has, aport, pp[sel]).astype(np.int64)          # flows the policy allows
+    fproto = np.where(has, aproto, pr[sel]).astype(np.uint8)
     eport = s.randint(F, 1024, 65536)
     ing = s.frac(F) < 0.75
     d = np.where(ing[:, None], rem, loc)
@@ -575,12 +605,17 @@ def _config3_v6(s, maps, c2, frames, length, kind4, eps, v6_frac, n_flows6, n_ep
     proto = fproto[f].copy()
     new = k == 2
     nn = int(new.sum())
-    src[new] = remote6[s.choice(nn, n_r6)]
+    nri = s.choice(nn, n_r6)
+    src[new] = remote6[nri]
     dst[new] = ep_ip6[s.choice(nn, n_ep)]
     sport[new] = s.randint(nn, 1024, 65536)
     nsel = s.choice(nn, len(pp))
-    dport[new] = np.where(s.frac(nn) < 0.8, pp[nsel], s.randint(nn, 1, 65536))
-    proto[new] = pr[nsel]
+    nid = r_id[nri]
+    nport, nproto, nhas = _allowed_l4(pol, nid, s)
+    r2 = s.frac(nn)                                     # 70% to a port the policy allows
+    allow = nhas & (r2 < 0.7)
+    dport[new] = np.where(allow, nport, np.where(r2 < 0.85, pp[nsel], s.randint(nn, 1, 65536)))
+    proto[new] = np.where(allow, nproto, pr[nsel])
     rf = s.frac(m)
     tflags = np.where(rf < 0.90, TCP_ACK, np.where(rf < 0.95, TCP_SYN, np.where(rf < 0.98, TCP_FIN | TCP_ACK, TCP_RST)))
     hop = np.full(m, 64)

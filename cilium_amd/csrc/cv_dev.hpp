@@ -15,6 +15,8 @@ namespace cv {
 
 constexpr int BLOCK = 256;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t COMMIT4 = 0xFFFFFFFEu;     // g.gslot marks of a deferred CT create (k_ct_commit)
+constexpr uint32_t COMMIT6 = 0xFFFFFFFDu;
 
 // ------------------------------------------------------------------ records
 // The first 4*NW bytes of a frame record live in NW VGPRs (loaded with 16-B
@@ -1153,6 +1155,43 @@ __device__ __forceinline__ Skb4 skb4_from(const Rec &r)
     return s;
 }
 
+// The stage record of an IPv4 packet that reaches the policy program: the fields
+// tail_ipv4_policy reads, packed by the front kernel into 16 B next to the packet's
+// hand-over words (StageRec), so stage 2 loads one 32-B slot per packet instead of the
+// 64-B record and separate meta / label arrays.  Access outcomes: 2 bits each
+// (0 ok, 1 past the packet, 2 past the record -> E_TRUNC).
+__device__ __forceinline__ uint32_t chk2(int c) { return c == 0 ? 0u : c == E_TRUNC ? 2u : 1u; }
+__device__ __forceinline__ int8_t unchk2(uint32_t v) { return (int8_t)(v == 0 ? 0 : v == 2 ? E_TRUNC : 1); }
+
+__device__ __forceinline__ uint4 skb4_pack(const Skb4 &s, uint32_t &w4, uint32_t &chk)
+{
+    w4 = (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 | (uint32_t)s.l4off << 24;
+    chk = chk2(s.h.c1) | chk2(s.h.c14) << 2 | chk2(s.h.c4) << 4 | chk2(s.h.c2a) << 6 | chk2(s.h.c2b) << 8;
+    return make_uint4(s.saddr, s.daddr, (s.h.p0 & 0xFFFFu) | s.h.p2 << 16, s.len);
+}
+
+__device__ __forceinline__ Skb4 skb4_unpack(const uint4 &a, uint32_t w4, uint32_t chk, uint32_t stride)
+{
+    Skb4 s;
+    s.saddr = a.x;
+    s.daddr = a.y;
+    s.len = a.w;
+    s.nexthdr = w4 & 0xFFu;
+    s.ttl = 0;                                                    // (not read after the front)
+    s.l4off = (int)(w4 >> 24);
+    s.avail = stride;
+    s.h.type = (w4 >> 8) & 0xFFu;
+    s.h.tflags = (w4 >> 16) & 0xFFu;
+    s.h.p0 = a.z & 0xFFFFu;
+    s.h.p2 = a.z >> 16;
+    s.h.c1 = unchk2(chk & 3u);
+    s.h.c14 = unchk2((chk >> 2) & 3u);
+    s.h.c4 = unchk2((chk >> 4) & 3u);
+    s.h.c2a = unchk2((chk >> 6) & 3u);
+    s.h.c2b = unchk2((chk >> 8) & 3u);
+    return s;
+}
+
 // ------------------------------------------------------------------ output frames (IPv4)
 // The frame rewrites of the reference (lb4_xlate lb.h:653-697, __lb4_rev_nat
 // lb.h:485-548, ipv4_l3 l3.h:54-69) replayed on the record's fields with the
@@ -1417,11 +1456,13 @@ template <class M>
 __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                            uint16_t &proxy, int32_t &reason, Acct &a, M &m,
-                                           RevNatOut *rn = nullptr)
+                                           RevNatOut *rn = nullptr, bool *defer = nullptr)
 {
     int ret;
     int verdict;
     Tuple4 t;
+    const bool may_defer = defer && *defer;
+    if (defer) *defer = false;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
     bool mon = false;
@@ -1452,9 +1493,14 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
     }
     if (skip_proxy) verdict = 0;
     if (ret == CT_NEW) {
-        CtState sn{0, 0, 0, 0, 0, src_label};
-        const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
-        if (is_err(c)) { ret = c; goto drop; }
+        if (may_defer) {                                           // k_ct_commit writes it
+            a.nu += 2;
+            *defer = true;
+        } else {
+            CtState sn{0, 0, 0, 0, 0, src_label};
+            const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
+            if (is_err(c)) { ret = c; goto drop; }
+        }
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, (uint32_t)ret, mon);
@@ -1482,11 +1528,13 @@ template <class M>
 __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                            uint16_t &proxy, int32_t &reason, Acct &a, M &m,
-                                           RevNat6Out *rn = nullptr)
+                                           RevNat6Out *rn = nullptr, bool *defer = nullptr)
 {
     int ret;
     int verdict;
     Tuple6 t;
+    const bool may_defer = defer && *defer;
+    if (defer) *defer = false;
     CtState st{0, 0, 0, 0, 0, 0};
     CtState sn{0, 0, 0, 0, 0, src_label};
     int64_t slot;
@@ -1523,8 +1571,13 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
     }
     if (skip_proxy) verdict = 0;
     if (ret == CT_NEW) {
-        const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
-        if (is_err(c)) { ret = c; goto drop; }
+        if (may_defer) {
+            a.nu += 2;
+            *defer = true;
+        } else {
+            const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
+            if (is_err(c)) { ret = c; goto drop; }
+        }
     }
     if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
         notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, (uint32_t)ret, mon);
@@ -1548,11 +1601,13 @@ template <class M>
 __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                               bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                               uint16_t &proxy, int32_t &reason, Acct &a, M &m,
-                                              RevNatOut *rn = nullptr)
+                                              RevNatOut *rn = nullptr, bool *defer = nullptr)
 {
     int ret;
+    if (defer && ((p.flags & F_DROP_ALL) || !ep.ipv4)) *defer = false;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ipv4) return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn);
+    else if (ep.ipv4)
+        return ipv4_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn, defer);
     else ret = DROP_UNKNOWN_L3;
     m.drop(ret, s.len, METRIC_INGRESS);                            // bpf_lxc.c:1032-1035
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
@@ -1563,11 +1618,14 @@ __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep
 template <class M>
 __device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                               bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
-                                              uint16_t &proxy, int32_t &reason, Acct &a, M &m, RevNat6Out *rn = nullptr)
+                                              uint16_t &proxy, int32_t &reason, Acct &a, M &m, RevNat6Out *rn = nullptr,
+                                              bool *defer = nullptr)
 {
     int ret;
+    if (defer && ((p.flags & F_DROP_ALL) || !ep.ct6.buckets)) *defer = false;
     if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ct6.buckets) return ipv6_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn);
+    else if (ep.ct6.buckets)
+        return ipv6_policy(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn, defer);
     else ret = DROP_MISSED_TAIL_CALL;
     m.drop(ret, s.len, METRIC_INGRESS);
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
@@ -1766,7 +1824,7 @@ __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t h
     }
 }
 
-// fn(i) for every member of every scheduled run of queue q, runs in `work` order and
+// fn(i, run size) for every member of every scheduled run of queue q, runs in `work` order and
 // members in packet order; the next member's index is loaded while fn runs
 // (SORTED false: the runs in queue order, when k_group_schedule did not run)
 template <bool SORTED = true, class F>
@@ -1781,7 +1839,7 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
 #pragma unroll 1
         for (uint32_t k = 0; k < cnt; ++k) {
             const uint32_t vn = k + 1 < cnt ? g.order[off + 2 + k] : NONE;
-            fn(v);
+            fn(v, cnt);
             v = vn;
         }
     }

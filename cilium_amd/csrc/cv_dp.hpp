@@ -82,8 +82,11 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t epoch;
     uint32_t *gslot;           // per packet: group slot or ~0
     uint32_t *next;            // per packet: previous inserter in the group or ~0
-    uint32_t *secctx;          // per packet: source label handed to the policy program
-    uint32_t *meta;            // per packet: ep index | skip_proxy << 16 | ifindex != 0 << 17
+    uint4 *srec;               // per packet 2 x 16 B (netdev path, packets handed to the policy
+                               // program): [0] the IPv4 stage record (skb4_pack), [1] {the
+                               // packed protocol word, access bits | nl << 16 | nu << 24,
+                               // meta = ep index | skip_proxy << 16 | ifindex != 0 << 17,
+                               // the source label}
     unsigned long long *parent;// per table slot: epoch << 32 | union-find parent (egress path)
     uint32_t *eg;              // per packet: EG_WORDS words of egress scratch (egress path)
     uint32_t serial;           // launch serial (never reset; tags deferred CT writes)

@@ -952,7 +952,7 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
     m.pc = &pc;
     // runs in queue order: k_group_flatten without k_group_schedule (measured faster here
     // than size-class order)
-    for_each_run<false>(g, V6 ? Q_CT6 : Q_CT4, false, [&](uint32_t x) {
+    for_each_run<false>(g, V6 ? Q_CT6 : Q_CT4, false, [&](uint32_t x, uint32_t) {
         if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
         else egress4_one(p, b, now, o, g, x, m);
     });

@@ -456,10 +456,16 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
 // Conntrack insert (map_update_elem BPF_ANY on an LRU_HASH, conntrack.h:694,720,740).
 // The caller guarantees that no other thread of the launch touches `key` (packets
 // are grouped by address pair), so the only race is for free slots: claim one with
-// an agent-scope CAS of its tag byte (empty/dead -> busy), write the key, release,
-// then publish the fingerprint.  Lookups skip busy slots.  Returns the slot, or -1
-// when the probe limit is hit (-> DROP_CT_CREATE_FAILED); *created tells whether
-// the key was new.
+// an agent-scope CAS of its tag byte (empty/dead -> busy), write the key, then
+// publish the fingerprint.  Lookups skip busy slots.  Returns the slot, or -1 when
+// the probe limit is hit (-> DROP_CT_CREATE_FAILED); *created tells whether the key
+// was new.
+// No release fence between the key and the fingerprint (an agent-scope release is a
+// write-back of the whole XCD L2, microseconds per create): the only thread that
+// looks `key` up in this launch is this one (program order), and any other reader
+// whose fingerprint collides sees either the new key or the zero words every free
+// slot holds (dev_kill clears a key before its slot turns dead), neither of which is
+// its own key.  The kernel boundary publishes the entry to later launches.
 template <class S>
 __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t *key, bool *created)
 {
@@ -486,7 +492,6 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
                                                          __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
                     for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + s * S::KW + j] = key[j];
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     uint32_t c2 = nw;
                     for (;;) {
                         const uint32_t n2 = (c2 & ~(0xFFu << sh)) | (tag << sh);
@@ -504,7 +509,11 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     return -1;
 }
 
-// Conntrack delete (map_delete_elem, conntrack.h:641-647): tag -> dead.
+// Conntrack delete (map_delete_elem, conntrack.h:641-647): key -> zero words, then
+// tag -> dead.  The clearing stores are agent-scope atomics and complete (the
+// workgroup-scope release waits for them, without an L2 write-back) before the tag
+// CAS is issued, so a thread that claims the dead slot later in the launch cannot
+// have its new key overwritten by them.
 template <class S>
 __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
 {
@@ -512,6 +521,11 @@ __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
     const int s = (int)((uint64_t)slot % S::SPB);
     uint32_t *tw = t.buckets + b * S::BW + (s >> 2);
     const int sh = 8 * (s & 3);
+#pragma unroll
+    for (int j = 0; j < S::KW; ++j)
+        __hip_atomic_exchange(t.buckets + b * S::BW + S::KEY0 + s * S::KW + j, 0u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     uint32_t c = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
         const uint32_t n = (c & ~(0xFFu << sh)) | (TAG_DEAD << sh);

@@ -244,6 +244,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         const bool pass = live && xv == XDP_PASS;
         bool skip_proxy = false;
         uint32_t identity = 0;
+        uint32_t smeta = 0, slabel = 0;                           // the hand-over to the policy program
         if (pass && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
         ident = identity;
         if (EV && pass && p.trace) {                              // from_netdev: send_trace_notify(FROM_*)
@@ -296,8 +297,8 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                         h = DROP_MISSED_TAIL_CALL;
                     } else {
                         staged = true;                            // -> handle_policy -> tail_ipv4_policy
-                        g.secctx[i] = secctx;
-                        g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
+                        slabel = secctx;
+                        smeta = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
                         if (EV) g.ifx[i] = (uint32_t)lxc_slot;    // -> cb[CB_IFINDEX], MACs (stage 2)
                     }
                 }
@@ -310,8 +311,8 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             if (ldabs) { h = TC_ACT_OK; dmac_rw = false; }
             if (v6stage) {
                 const uint32_t e = p.ep_of_lxc[iv & 0xFFFFu];
-                g.secctx[i] = flowlabel;
-                g.meta[i] = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
+                slabel = flowlabel;
+                smeta = (e - 1) | (skip_proxy ? 1u << 16 : 0u) | ((iv >> 17) & 1u) << 17;
                 if (EV) g.ifx[i] = (uint32_t)lxc_slot;
             }
         }
@@ -330,10 +331,10 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             }
         }
         if (staged) {                                             // group by (CT map, address pair)
-            const EpDev &ep = p.eps[g.meta[i] & 0xFFFFu];
+            const EpDev &ep = p.eps[smeta & 0xFFFFu];
             group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
         } else if (v6stage) {
-            const EpDev &ep = p.eps[g.meta[i] & 0xFFFFu];
+            const EpDev &ep = p.eps[smeta & 0xFFFFu];
             const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
             const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
             group_push(g, group_node(g, pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets)), i,
@@ -356,9 +357,10 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             if (o.ct) o.ct[i] = CT_NONE;
             if (o.proxy) o.proxy[i] = 0;
             store_out(o, i, a);
-        } else {
-            if (o.nl) o.nl[i] = (uint8_t)a.nl;                  // stage 2 adds its own
-            if (o.nu) o.nu[i] = (uint8_t)a.nu;
+        } else {                                                  // the stage record (stage 2 adds its accounting)
+            uint32_t w4 = 0, chk = 0;
+            if (staged) g.srec[2 * i] = skb4_pack(skb4_from(r), w4, chk);
+            g.srec[2 * i + 1] = make_uint4(w4, chk | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24, smeta, slabel);
         }
         if (o.xdp) o.xdp[i] = xv;
         if (o.identity) o.identity[i] = ident;
@@ -368,17 +370,16 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
 
 template <class M>
 __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b, const OutDev &o,
-                                           const GroupScratch &g, uint32_t i, uint32_t now, M &m)
+                                           const GroupScratch &g, uint32_t i, uint32_t now, M &m, bool single)
 {
-    Rec r;
-    rec_load(r, b, i, 3);
-    const uint32_t meta = g.meta[i];
+    const uint4 s0 = g.srec[2 * i], s1 = g.srec[2 * i + 1];
+    const uint32_t meta = s1.z;
     const EpDev &ep = p.eps[meta & 0xFFFFu];
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
     int32_t reason = 0;
-    Skb4 s = skb4_from(r);
+    Skb4 s = skb4_unpack(s0, s1.x, s1.y & 0x3FFu, b.stride);
     int64_t lslot = -1;                                          // the destination's cilium_lxc slot
     if constexpr (M::EV) {
         m.pkt = b.base + i;
@@ -386,13 +387,17 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
         lslot = (int32_t)g.ifx[i];
     }
     RevNatOut rn{false, false, 0, 0};
-    const int ret = handle_policy4(p, ep, s, g.secctx[i], (meta >> 16) & 1u,
+    bool defer = single && !p.ct_guard;                          // the only packet of its group
+    const int ret = handle_policy4(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc4, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
-                                   a, m, &rn);
+                                   a, m, &rn, &defer);
+    if (defer) g.gslot[i] = COMMIT4;
     if (M::EV && o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
         // the forwarded frame: ipv4_local_delivery's ipv4_l3 (bpf_netdev handle_ipv4), then
         // the policy program's reverse NAT
         const uint8_t *in = b.frames + (size_t)i * b.stride;
+        Rec r;
+        rec_load(r, b, i, 3);
         Frame4 f;
         frame4_init(f, r, in);
         uint32_t mac[2], nmac[2];
@@ -418,7 +423,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutD
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_run<true>(g, Q_NETDEV, false, [&](uint32_t x) { stage2_one(p, b, o, g, x, now, m); });
+    for_each_run<true>(g, Q_NETDEV, false, [&](uint32_t x, uint32_t n) { stage2_one(p, b, o, g, x, now, m, n == 1); });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
 }
@@ -427,13 +432,14 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutD
 // handle_policy -> tail_ipv6_policy -> ipv6_policy (bpf_lxc.c:721-862, 1003-1038)
 template <class M>
 __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b, const OutDev &o,
-                                            const GroupScratch &g, uint32_t i, uint32_t now, M &m)
+                                            const GroupScratch &g, uint32_t i, uint32_t now, M &m, bool single)
 {
     Rec6 r;
     rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
-    const uint32_t meta = g.meta[i];
+    const uint4 s1 = g.srec[2 * i + 1];
+    const uint32_t meta = s1.z;
     const EpDev &ep = p.eps[meta & 0xFFFFu];
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
     int32_t reason = 0;
@@ -446,9 +452,11 @@ __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b
     }
     RevNat6Out rn;
     rn.valid = false;
-    const int ret = handle_policy6(p, ep, s, g.secctx[i], (meta >> 16) & 1u,
+    bool defer = single && !p.ct_guard;
+    const int ret = handle_policy6(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc6, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
-                                   a, m, &rn);
+                                   a, m, &rn, &defer);
+    if (defer) g.gslot[i] = COMMIT6;
     if (M::EV && o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
         // ipv6_local_delivery's ipv6_l3, then ipv6_policy's rev-NAT index zeroing and reverse NAT
         const uint8_t *in = b.frames + (size_t)i * b.stride;
@@ -477,8 +485,56 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage6(DpParams p, BatchDev b, Out
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_run<true>(g, Q_NETDEV6, false, [&](uint32_t x) { stage2_one6(p, b, o, g, x, now, m); });
+    for_each_run<true>(g, Q_NETDEV6, false, [&](uint32_t x, uint32_t n) { stage2_one6(p, b, o, g, x, now, m, n == 1); });
     met_flush(m, p.metrics);
+    pol_cache_flush(pc);
+}
+
+// The creates of singleton groups, deferred by stage 2 (marked in g.gslot): no other
+// packet of the batch can touch the new entry or its ICMP twin (their address pair is
+// the group key), so writing them after the stage equals writing them in place, and
+// the stage's waves no longer wait on the insert chain of their few creating lanes.
+// ct_create4 / ct_create6 (conntrack.h:663-744 / 589-639) with the tuple ct_lookup
+// left (ct_l4's tuple reversed: both directions missed) and the ipv{4,6}_policy state.
+__global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, GroupScratch g, uint32_t now)
+{
+    __shared__ LdsPolicy pc;
+    pol_cache_init(pc);
+    __syncthreads();
+    Acct a{0, 0, &pc};
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint32_t mk = g.gslot[i];
+        if (mk != COMMIT4 && mk != COMMIT6) continue;
+        const uint4 s1 = g.srec[2 * i + 1];
+        const EpDev &ep = p.eps[s1.z & 0xFFFFu];
+        uint32_t seen;
+        if (mk == COMMIT4) {
+            const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
+            Tuple4 t;
+            t.nexthdr = s.nexthdr;
+            t.daddr = s.daddr;
+            t.saddr = s.saddr;
+            t.dport = t.sport = 0;
+            ct_l4<false>(t, s.h, CT_INGRESS, seen);
+            t.reverse();
+            const CtState sn{0, 0, 0, 0, 0, s1.w};
+            ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false);
+        } else {
+            Rec6 r;
+            rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
+            const Skb6 s = skb6_from(r);
+            Tuple6 t;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
+            t.nexthdr = s.nexthdr;
+            t.dport = t.sport = 0;
+            ct_l4<true>(t, s.h, CT_INGRESS, seen);
+            t.reverse();
+            const CtState sn{s.daddr[3] & 0xFFFFu, 0, 0, 0, 0, s1.w};
+            ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, false);
+        }
+    }
+    __syncthreads();
     pol_cache_flush(pc);
 }
 
@@ -752,6 +808,8 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
             const uint32_t life = *reinterpret_cast<const uint32_t *>(t.vals + (b * S::SPB + sl) * t.vstride + 32);
             if (life < time) {
                 out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
+#pragma unroll
+                for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + sl * S::KW + j] = 0;   // free slots hold zero keys
                 ++mine;
             }
         }
@@ -841,6 +899,7 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
     launch_group_runs(g, Q_NETDEV6, grid.x, 1, s);
     if (ev) hipLaunchKernelGGL(k_ct_stage6<true>, grid, blk, 0, s, p, b, o, g, now);
     else hipLaunchKernelGGL(k_ct_stage6<false>, grid, blk, 0, s, p, b, o, g, now);
+    if (!p.ct_guard) hipLaunchKernelGGL(k_ct_commit, grid, blk, 0, s, p, b, g, now);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -2,11 +2,15 @@
 # One GPU-box session: the -m gpu tests, the bench line, and the rocprofv3 kernel
 # summary of one workload.  Every GPU step has its own time limit and the chain stops
 # at the first failure.
-#   usage: bash tools/gpu_session.sh <tag> <workload> [pytest -k expr | all | -]
+#   usage: bash tools/gpu_session.sh <tag> <workload> [pytest -k expr | all | -] [pmc]
+# With "pmc" the counter passes follow (one counter group per rocprofv3 run, each under
+# a hard limit): FETCH_SIZE, WRITE_SIZE, TCC hit/miss, and SQ instruction/wait counts;
+# tools/pmc_summary.py <tag> <workload> turns them into profiles/.
 set -u
 TAG=${1:-r02}
 W=${2:-config3}
 K=${3:-all}
+PMC=${4:-}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -28,4 +32,15 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$W" -o run --o
     || { echo "rocprof stats failed rc=$?"; tail -20 "$OUT/stats_$W.log"; exit 1; }
 find "$OUT/stats_$W" -name "*kernel_stats.csv" -exec cp {} "$OUT/${W}_kernel_stats.csv" \;
 head -12 "$OUT/${W}_kernel_stats.csv"
+if [ "$PMC" = "pmc" ]; then
+  i=0
+  for CTRS in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
+              "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+    i=$((i+1))
+    step "pmc $CTRS"
+    timeout -s KILL 240 rocprofv3 --pmc $CTRS -d "$OUT/pmc${i}_$W" -o run --output-format csv \
+        -- python3 bench.py --workload "$W" --steps 3 --warmup 1 --no-cpu > "$OUT/pmc${i}_$W.log" 2>&1 \
+        || { echo "pmc pass $i failed rc=$?"; tail -20 "$OUT/pmc${i}_$W.log"; exit 1; }
+  done
+fi
 step done

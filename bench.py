@@ -17,9 +17,10 @@ accounting pass (L(p), U(p) of SURVEY.md §8(d)) is one more such step after the
 timed region.
 
 Multi-GPU (torchrun): tables are replicated, every rank verdicts its own batch
-(weak scaling, no data-path collective); config 4 shards conntrack by address pair
-(cilium_amd.shard); cilium_metrics is summed across ranks with one RCCL all_reduce
-after the timed region.
+(weak scaling, no data-path collective); conntrack is sharded by address pair
+(cilium_amd.shard): at N > 1 configs 3 / 4 give each rank 16M flows of one node-wide
+flow set (128M on 8 GPUs) and packets of its own pairs; cilium_metrics is summed
+across ranks with one RCCL all_reduce after the timed region.
 
 Prints ONE JSON line (rank 0).
 """
@@ -42,7 +43,8 @@ HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 T
 METRIC = "Mpps verdicts at 1/2/4/8 GPUs (64B hdrs); achieved HBM GB/s vs peak"
 
 WORKLOADS = {
-    "config3": "full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + ct_lookup4/ct_create4, 16M-flow CT, "
+    "config3": "full bpf_lxc ingress path: prefilter + ipcache + lxc + policy + ct_lookup4/ct_create4, 16M-flow CT "
+               "per GPU (at N > 1 one node-wide flow set sharded by address pair = config 4), "
                "a fresh batch per step (20% new flows)",
     "config2": "ipcache LPM (100k CIDRs->identities) + policymap (10k identities x L4 ports) ingress verdicts",
     "config1": "bpf_xdp.c CIDR deny-list prefilter, 1k IPv4 prefixes + cilium_lxc",
@@ -70,11 +72,12 @@ def make_workload(name, n, rank, world):
         return synth.config2(n)
     if name == "config1":
         return synth.config1(n)
-    if name == "config3":
-        return synth.config3(n, n_flows=1 << 24)
-    if name == "config4":
-        # the rank's shard: flows whose address pair hashes to it (pre-steered by the producer)
-        return synth.config3(n, n_flows=1 << 24, seed=0xC1A00004 + 7919 * rank)
+    if name in ("config3", "config4"):
+        # N > 1: the rank's part of one node-wide flow set (16M flows per rank), the flows
+        # whose address pair it owns, and packets of its own pairs (pre-steered by the
+        # producer): conntrack sharded by address pair, config 4 of BASELINE.json
+        seed = 0xC1A00003 if name == "config3" else 0xC1A00004
+        return synth.config3(n, n_flows=1 << 24, seed=seed, shard=(rank, world) if world > 1 else None)
     if name == "config5":
         return synth.config5(n)
     raise SystemExit(f"unknown workload {name}")
@@ -406,7 +409,8 @@ def main():
                 "packets_per_step_per_gpu": n,
                 "header_bytes": "64 (v4) / 128 (v6)" if name == "config5" else int(w.frames.shape[1]),
                 "parallelism": f"replicated tables, {world} GPU(s), batch per GPU"
-                               + (", conntrack sharded by address pair" if name == "config4" else ""),
+                               + (", conntrack sharded by address pair (16M flows per GPU of one node-wide set)"
+                                  if name in ("config3", "config4") and world > 1 else ""),
                 "tables": {k: len(m) for k, m in w.maps.items()},
             },
             "roofline": {

@@ -934,15 +934,16 @@ __device__ __forceinline__ void ct_live_add(const HashTable &ct, Acct &a, bool g
 
 // map_update_elem(BPF_ANY) of a CT entry (conntrack.h:694,720,740)
 template <class T>
-__device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const CtE &e, Acct &a, bool guard)
+__device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const CtE &e, Acct &a, bool guard,
+                                       bool absent = false)
 {
     uint32_t k[T::KW];
     t.key(k);
-    if (guard && ct.live && dev_find<typename T::Spec>(ct, k, nullptr) < 0 &&
+    if (guard && ct.live && (absent || dev_find<typename T::Spec>(ct, k, nullptr) < 0) &&
         __hip_atomic_load(ct.live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ct.cap)
         return false;                                             // full: -E2BIG
     bool created;
-    const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created);
+    const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent);
     if (s < 0) return false;
     if (created) ct_live_add(ct, a, guard, 1);
     ct_store(ct, s, e);
@@ -985,17 +986,19 @@ __device__ __forceinline__ Tuple4 ct_nat_tuple(const Tuple4 &t, int dir, const C
 
 // ct_create4 / ct_create6 (conntrack.h:663-744 / 589-639): the entry, the NATed
 // tuple when ct_state->addr is set (v4 only; with defer_nat the caller writes it
-// later, see k_nat_apply), and the ICMP-RELATED twin
+// later, see k_nat_apply), and the ICMP-RELATED twin.  absent: `t` is the tuple
+// ct_lookup just missed (both directions), so its insert skips the key compare.
 template <bool V6, class T>
 __device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32_t len, int dir, const CtState &st,
-                                         uint32_t now, Acct &a, bool guard, bool defer_nat = false)
+                                         uint32_t now, Acct &a, bool guard, bool defer_nat = false,
+                                         bool absent = false)
 {
     CtE e;
     const bool tcp = t.nexthdr == 6;
     ct_entry_new(e, tcp, len, dir, st, now);
     const bool nat = !V6 && st.addr;
     a.nu += nat ? 3 : 2;
-    if (!ct_put(ct, t, e, a, guard)) return DROP_CT_CREATE_FAILED;
+    if (!ct_put(ct, t, e, a, guard, absent)) return DROP_CT_CREATE_FAILED;
     if constexpr (!V6) {
         if (nat && !defer_nat) {
             if (!ct_put(ct, ct_nat_tuple(t, dir, st), e, a, guard)) return DROP_CT_CREATE_FAILED;
@@ -1498,7 +1501,7 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
             *defer = true;
         } else {
             CtState sn{0, 0, 0, 0, 0, src_label};
-            const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
+            const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);
             if (is_err(c)) { ret = c; goto drop; }
         }
     }
@@ -1575,7 +1578,7 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
             a.nu += 2;
             *defer = true;
         } else {
-            const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard);
+            const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);
             if (is_err(c)) { ret = c; goto drop; }
         }
     }

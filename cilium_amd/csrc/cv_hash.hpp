@@ -31,9 +31,9 @@ struct HashTable {            // POD view, passed by value to kernels
     uint64_t  cap;            // conntrack maps: max_entries (a create past it fails, -E2BIG)
 };
 
-template <int KW_, int IVW_, int SPB_, int BW_, int IVH_ = 0>
+template <int KW_, int IVW_, int SPB_, int BW_, int IVH_ = 0, int SYM_ = 0>
 struct HashSpec {
-    static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_, IVH = IVH_;
+    static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_, IVH = IVH_, SYM = SYM_;
     static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KW, HVAL0 = 2 * IVAL0;   // HVAL0 in halfwords
     static_assert(IVAL0 + SPB * IVW <= BW, "bucket overflow");
     static_assert(IVH == 0 || (IVW == 0 && IVH == 1 && HVAL0 + SPB <= 2 * BW), "halfword values");
@@ -47,8 +47,8 @@ using LxcV6Spec  = HashSpec<4, 1, 6, 32>;
 using Cidr4Spec  = HashSpec<1, 0, 8, 16>;   // /32 deny set (v4_fix)
 using Cidr6Spec  = HashSpec<4, 0, 7, 32>;   // /128 deny set (v6_fix)
 using PolicySpec = HashSpec<2, 0, 5, 16, 1>; // policy_key (8 B) -> inline proxy_port; side array policy_entry (stride 32)
-using Ct4Spec    = HashSpec<4, 0, 7, 32>;   // ipv4_ct_tuple (14 B + 2 zero) -> side array ct_entry (stride 64)
-using Ct6Spec    = HashSpec<10, 0, 3, 32>;  // ipv6_ct_tuple (40 B) -> side array ct_entry (stride 64)
+using Ct4Spec    = HashSpec<4, 0, 7, 32, 0, 1>;   // ipv4_ct_tuple (14 B + 2 zero) -> side array ct_entry (stride 64)
+using Ct6Spec    = HashSpec<10, 0, 3, 32, 0, 1>;  // ipv6_ct_tuple (40 B) -> side array ct_entry (stride 64)
 using Lb4Spec    = HashSpec<2, 3, 6, 32>;   // lb4_key (8 B) -> lb4_service (12 B) inline
 using Lb6Spec    = HashSpec<5, 6, 4, 64>;   // lb6_key (20 B) -> lb6_service (24 B) inline
 using Lpm6Spec   = HashSpec<5, 1, 5, 32>;   // (masked v6 addr, plen) -> value
@@ -64,6 +64,34 @@ CV_HD uint32_t half_at(const uint32_t *w, int h) { return (w[h >> 1] >> (16 * (h
 
 template <class S>
 CV_HD uint64_t key_hash(const uint32_t *key) { return hash_words<S::KW>(key, HASH_SEED); }
+
+// The home-bucket hash of a key and its fingerprint.  Conntrack tables (SYM) place a
+// tuple by its direction-free form -- the (address, port) endpoints in sorted order,
+// TUPLE_F_IN cleared -- so a tuple and its reverse (the two keys ct_lookup4/6 try,
+// conntrack.h:442-562 / 286-412) share a home bucket and one bucket read answers
+// both; the fingerprint comes from the full key and still tells them apart.
+template <class S>
+CV_HD uint64_t home_hash(const uint32_t *key, uint32_t &tag)
+{
+    const uint64_t h = key_hash<S>(key);
+    tag = tag_of(h);
+    if constexpr (S::SYM != 0) {
+        constexpr int A = S::KW == 4 ? 1 : 4;                    // words per address
+        const uint32_t *da = key, *sa = key + A;
+        const uint32_t ports = key[2 * A], dp = ports & 0xFFFFu, sp = ports >> 16;
+        bool d_lt = dp < sp;                                     // order the (address, port) endpoints
+#pragma unroll
+        for (int j = A - 1; j >= 0; --j)
+            if (da[j] != sa[j]) d_lt = da[j] < sa[j];
+        uint32_t sym[S::KW];
+#pragma unroll
+        for (int j = 0; j < A; ++j) { sym[j] = d_lt ? da[j] : sa[j]; sym[A + j] = d_lt ? sa[j] : da[j]; }
+        sym[2 * A] = d_lt ? (dp | sp << 16) : (sp | dp << 16);
+        sym[2 * A + 1] = key[2 * A + 1] & ~((uint32_t)TUPLE_F_IN << 8);
+        return hash_words<S::KW>(sym, HASH_SEED ^ 0x5CA1AB1E0DDBA11ULL);
+    }
+    return h;
+}
 
 // Match `key` in one bucket snapshot w[BW].  Returns the slot or -1; *stop is set
 // when the bucket has an empty slot (end of the probe chain).
@@ -117,8 +145,8 @@ __device__ __forceinline__ void tag_masks(uint64_t tags, uint32_t tag, uint64_t 
 template <class S>
 __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
-    const uint64_t h = key_hash<S>(key);
-    const uint32_t tag = tag_of(h);
+    uint32_t tag;
+    const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
     for (int p = 0; p < MAX_PROBE; ++p) {
         const uint32_t *bw = t.buckets + b * S::BW;
@@ -157,8 +185,9 @@ __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *
 {
     if (!t.buckets) return -1;
     if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);   // (tag-first 64-B probes: slower)
-    const uint64_t h = key_hash<S>(key);
-    return dev_find_from<S>(t, key, tag_of(h), h & t.mask, 0, ival);
+    uint32_t tag;
+    const uint64_t h = home_hash<S>(key, tag);
+    return dev_find_from<S>(t, key, tag, h & t.mask, 0, ival);
 }
 
 template <class S>
@@ -297,14 +326,15 @@ __device__ __forceinline__ void quad_find2(const HashTable &t, const uint32_t *k
                                            bool want1, uint4 *st, int64_t &s0, uint32_t *iv0, int64_t &s1,
                                            uint32_t *iv1)
 {
-    const uint64_t h0 = key_hash<S>(k0), h1 = key_hash<S>(k1);
+    uint32_t tg0, tg1;
+    const uint64_t h0 = home_hash<S>(k0, tg0), h1 = home_hash<S>(k1, tg1);
     const uint64_t b0 = h0 & t.mask, b1 = h1 & t.mask;
     const uint32_t *bw0 = (want0 && t.buckets) ? t.buckets + b0 * S::BW : nullptr;
     const uint32_t *bw1 = (want1 && t.buckets) ? t.buckets + b1 * S::BW : nullptr;
     uint32_t w0[16], w1[16];
     quad_load64x2(bw0, bw1, st, w0, w1);
-    s0 = bw0 ? quad_match<S>(t, k0, tag_of(h0), b0, w0, iv0) : -1;
-    s1 = bw1 ? quad_match<S>(t, k1, tag_of(h1), b1, w1, iv1) : -1;
+    s0 = bw0 ? quad_match<S>(t, k0, tg0, b0, w0, iv0) : -1;
+    s1 = bw1 ? quad_match<S>(t, k1, tg1, b1, w1, iv1) : -1;
 }
 
 // dev_find for 64-B buckets through quad_load64 (same result); `want` false: no
@@ -314,8 +344,8 @@ __device__ __forceinline__ int64_t quad_find(const HashTable &t, const uint32_t 
                                              uint32_t *ival)
 {
     static_assert(S::BW == 16, "64-B buckets");
-    const uint64_t h = key_hash<S>(key);
-    const uint32_t tag = tag_of(h);
+    uint32_t tag;
+    const uint64_t h = home_hash<S>(key, tag);
     const uint64_t b = h & t.mask;
     const uint32_t *bw = (want && t.buckets) ? t.buckets + b * S::BW : nullptr;
     uint32_t w[16];
@@ -354,8 +384,7 @@ template <class S>
 __device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32_t *key)
 {
     Probe<S> pr;
-    const uint64_t h = key_hash<S>(key);
-    pr.tag = tag_of(h);
+    const uint64_t h = home_hash<S>(key, pr.tag);
     pr.b = h & t.mask;
     pr.bw = t.buckets ? t.buckets + pr.b * S::BW : nullptr;
     if (!pr.bw) return pr;
@@ -455,54 +484,91 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
 
 // Conntrack insert (map_update_elem BPF_ANY on an LRU_HASH, conntrack.h:694,720,740).
 // The caller guarantees that no other thread of the launch touches `key` (packets
-// are grouped by address pair), so the only race is for free slots: claim one with
-// an agent-scope CAS of its tag byte (empty/dead -> busy), write the key, then
-// publish the fingerprint.  Lookups skip busy slots.  Returns the slot, or -1 when
-// the probe limit is hit (-> DROP_CT_CREATE_FAILED); *created tells whether the key
-// was new.
-// No release fence between the key and the fingerprint (an agent-scope release is a
+// are grouped by address pair), so the only race is for free slots.  One pass over
+// the probe chain finds the key or, failing that, the first bucket with a free
+// (empty / dead) slot; the slot is claimed by ONE agent-scope CAS of its tag word
+// that writes the fingerprint (the snapshot the pass read is the CAS's first
+// guess; a lost race returns the current word and the claim moves on), then the key
+// is written.  Returns the slot, or -1 when the probe limit is hit
+// (-> DROP_CT_CREATE_FAILED); *created tells whether the key was new.
+// known_absent: the caller's lookup of `key` missed in this launch (a create right
+// after ct_lookup), so no key compare is needed and the first free slot is taken.
+// No fence between the fingerprint and the key (an agent-scope release is a
 // write-back of the whole XCD L2, microseconds per create): the only thread that
 // looks `key` up in this launch is this one (program order), and any other reader
 // whose fingerprint collides sees either the new key or the zero words every free
-// slot holds (dev_kill clears a key before its slot turns dead), neither of which is
-// its own key.  The kernel boundary publishes the entry to later launches.
-template <class S>
-__device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t *key, bool *created)
+// slot holds (dev_kill and the GC clear a key before its slot turns dead), neither of
+// which is its own key.  The kernel boundary publishes the entry to later launches.
+__device__ __forceinline__ bool claim_in_word(uint32_t *tw, uint32_t cur, int first, int nslots, uint32_t tag,
+                                              int &got)
 {
-    const uint64_t h = key_hash<S>(key);
-    const uint32_t tag = tag_of(h);
-    uint64_t b = h & t.mask;
-    *created = false;
-    {                                               // 1) existing entry?
-        uint32_t none[S::IVW + 1];
-        const int64_t s = dev_find_tf<S>(t, key, none);
-        if (s >= 0) return s;
-    }
-    b = h & t.mask;                                 // 2) claim the first free slot
-    for (int p = 0; p < MAX_PROBE; ++p) {
-        uint32_t *bw = t.buckets + b * S::BW;
-#pragma unroll 1
-        for (int s = 0; s < S::SPB; ++s) {
-            uint32_t *tw = bw + (s >> 2);
-            const int sh = 8 * (s & 3);
-            uint32_t cur = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (((cur >> sh) & 0xFFu) < TAG_BUSY) {
-                const uint32_t nw = (cur & ~(0xFFu << sh)) | (TAG_BUSY << sh);
-                if (__hip_atomic_compare_exchange_strong(tw, &cur, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+    for (;;) {
+        int k = -1;
 #pragma unroll
-                    for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + s * S::KW + j] = key[j];
-                    uint32_t c2 = nw;
-                    for (;;) {
-                        const uint32_t n2 = (c2 & ~(0xFFu << sh)) | (tag << sh);
-                        if (__hip_atomic_compare_exchange_strong(tw, &c2, n2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT))
-                            break;
-                    }
-                    *created = true;
-                    return (int64_t)(b * S::SPB + s);
-                }
-            }
+        for (int q = 3; q >= 0; --q)
+            if (q < nslots && ((cur >> (8 * q)) & 0xFFu) < TAG_BUSY) k = q;
+        if (k < 0) return false;
+        const uint32_t nw = (cur & ~(0xFFu << (8 * k))) | (tag << (8 * k));
+        if (__hip_atomic_compare_exchange_strong(tw, &cur, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+            got = first + k;
+            return true;
+        }
+    }
+}
+
+template <class S>
+__device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t *key, bool *created,
+                                              bool known_absent = false)
+{
+    uint32_t tag;
+    const uint64_t h = home_hash<S>(key, tag);
+    constexpr uint64_t valid = S::SPB >= 8 ? ~0ULL : ((1ULL << (8 * S::SPB)) - 1);
+    constexpr uint64_t ones = 0x0101010101010101ULL, highs = 0x8080808080808080ULL;
+    *created = false;
+    uint64_t b = h & t.mask, fb = 0;
+    uint64_t ftags = 0;
+    bool have_free = false;
+    for (int p = 0; p < MAX_PROBE; ++p) {                          // 1) the key, and the first free slot
+        const uint32_t *bw = t.buckets + b * S::BW;
+        const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
+        const uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
+        uint64_t match;
+        bool empty;
+        tag_masks<S>(tags, tag, match, empty);
+        while (!known_absent && match) {
+            const int sl = (__builtin_ctzll(match) >> 3);
+            match &= match - 1;
+            const uint32_t *kw = bw + S::KEY0 + sl * S::KW;
+            bool eq = true;
+#pragma unroll
+            for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+            if (eq) return (int64_t)(b * S::SPB + sl);
+        }
+        // bytes < TAG_BUSY (empty or dead): high bit of (byte - 2) with the byte's high bit clear
+        const uint64_t fr = ((tags | highs) - 2 * ones) ^ highs;
+        const uint64_t freeb = fr & ~tags & highs & valid;
+        if (!have_free && freeb) { have_free = true; fb = b; ftags = tags; }
+        if (empty || (known_absent && have_free)) break;
+        b = (b + 1) & t.mask;
+    }
+    if (!have_free) return -1;                                     // MAX_PROBE full buckets
+    b = fb;
+    for (int p = 0; p < MAX_PROBE; ++p) {                          // 2) claim (one CAS per try)
+        uint32_t *bw = t.buckets + b * S::BW;
+        uint64_t cur = ftags;
+        if (p > 0) {
+            const uint2 tg = make_uint2(__hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                        __hip_atomic_load(bw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            cur = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
+        }
+        int got = -1;
+        if (claim_in_word(bw, (uint32_t)cur, 0, S::SPB < 4 ? S::SPB : 4, tag, got) ||
+            (S::SPB > 4 && claim_in_word(bw + 1, (uint32_t)(cur >> 32), 4, S::SPB - 4, tag, got))) {
+#pragma unroll
+            for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + got * S::KW + j] = key[j];
+            *created = true;
+            return (int64_t)(b * S::SPB + got);
         }
         b = (b + 1) & t.mask;
     }
@@ -554,8 +620,8 @@ inline void host_set_ival(uint32_t *w, int s, const uint32_t *ival)
 template <class S>
 inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *ival)
 {
-    const uint64_t h = key_hash<S>(key);
-    const uint32_t tag = tag_of(h);
+    uint32_t tag;
+    const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
     int64_t free_slot = -1;
     for (int p = 0; p < MAX_PROBE; ++p) {
@@ -589,8 +655,8 @@ inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *iv
 template <class S>
 inline int64_t host_find(const HashTable &t, const uint32_t *key)
 {
-    const uint64_t h = key_hash<S>(key);
-    const uint32_t tag = tag_of(h);
+    uint32_t tag;
+    const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
     for (int p = 0; p < MAX_PROBE; ++p) {
         const uint32_t *w = t.buckets + b * S::BW;

@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
             ct_l4<false>(t, s.h, CT_INGRESS, seen);
             t.reverse();
             const CtState sn{0, 0, 0, 0, 0, s1.w};
-            ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false);
+            ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
         } else {
             Rec6 r;
             rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
@@ -531,7 +531,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
             ct_l4<true>(t, s.h, CT_INGRESS, seen);
             t.reverse();
             const CtState sn{s.daddr[3] & 0xFFFFu, 0, 0, 0, 0, s1.w};
-            ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, false);
+            ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
         }
     }
     __syncthreads();

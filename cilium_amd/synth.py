@@ -12,7 +12,7 @@ written big-endian (network order) into keys and frames.
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -392,12 +392,17 @@ def ct_entries(n, now, ingress, tcp, src_sec_id, seen_non_syn=False, length=64) 
 def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A00003, now0: int = 1_000_000,
             n_cidrs: int = 102400, n_ids: int = 10000, n_ep: int = 4096, ct_max: Optional[int] = None,
             ttl_low: float = 0.0005, v6_frac: float = 0.0, stride: Optional[int] = None,
-            n_flows6: Optional[int] = None) -> Workload:
+            n_flows6: Optional[int] = None, shard: Optional[Tuple[int, int]] = None) -> Workload:
     """Ingress through from_netdev into the endpoints' policy programs with conntrack.
     v6_frac > 0 makes a dual-stack batch: that fraction of the packets becomes IPv6
     (handle_ipv6 -> ipv6_policy with a global CT6 map, v6 endpoints in cilium_lxc, v6
     ipcache entries), drawn after every IPv4 draw so the IPv4 part is unchanged;
-    records are then 128 bytes unless `stride` says otherwise."""
+    records are then 128 bytes unless `stride` says otherwise.
+    shard = (rank, world): config 4, rank's part of ONE node-wide flow set: every rank
+    draws the same candidate (remote, endpoint) pairs from the same seed and keeps
+    those whose address pair (cilium_amd.shard.pair_key4) it owns, n_flows of them; its
+    packets (existing and new flows) are its own pairs too, as a producer steering by
+    address pair would hand them over.  The ranks' CT shards are disjoint."""
     s = Stream(seed)
     c1 = config1(16, n_ep=n_ep)
     c2 = config2(16, n_cidrs=n_cidrs, n_ids=n_ids)
@@ -410,9 +415,12 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     ipk = c2.maps["ipcache"].keys[:-1]
     cidr_addr = ipk[:, 8:12].copy().view(">u4").reshape(-1).astype(np.uint32)
     cidr_plen = ipk[:, 0:4].copy().view("<u4").reshape(-1).astype(np.int64) - 32
-    pick = s.choice(n_flows, len(cidr_addr))
-    remote = _rand_addrs_in(s, cidr_addr[pick], cidr_plen[pick])
-    epi = s.choice(n_flows, n_ep)
+    if shard is None or shard[1] <= 1:
+        pick = s.choice(n_flows, len(cidr_addr))
+        remote = _rand_addrs_in(s, cidr_addr[pick], cidr_plen[pick])
+        epi = s.choice(n_flows, n_ep)
+    else:
+        pick, remote, epi = _owned_pairs(s, n_flows, shard, cidr_addr, cidr_plen, lxc_ip)
     local = lxc_ip[epi]
     pol = c2.maps["policy"].keys
     pol_port = pol[:, 4:6].copy().view(">u2").reshape(-1)
@@ -461,9 +469,14 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     proto = fproto[f].copy()
     new = kind == 2
     nn = int(new.sum())
-    npk = s.choice(nn, len(cidr_addr))
-    saddr[new] = _rand_addrs_in(s, cidr_addr[npk], cidr_plen[npk])
-    daddr[new] = lxc_ip[s.choice(nn, n_ep)]
+    if shard is None or shard[1] <= 1:
+        npk = s.choice(nn, len(cidr_addr))
+        saddr[new] = _rand_addrs_in(s, cidr_addr[npk], cidr_plen[npk])
+        daddr[new] = lxc_ip[s.choice(nn, n_ep)]
+    else:
+        npk, nrem, nepi = _owned_pairs(s, nn, shard, cidr_addr, cidr_plen, lxc_ip)
+        saddr[new] = nrem
+        daddr[new] = lxc_ip[nepi]
     sport[new] = s.randint(nn, 1024, 65536)
     nsel = s.choice(nn, len(pp))
     nid = c2.maps["ipcache"].vals[npk, 0:4].copy().view("<u4").reshape(-1)
@@ -510,6 +523,25 @@ def ct6_keys(daddr6, saddr6, dport, sport, nexthdr, flags) -> np.ndarray:
     k[:, 36] = np.asarray(nexthdr, np.uint8)
     k[:, 37] = np.asarray(flags, np.uint8)
     return k
+
+
+def _owned_pairs(s, n, shard, cidr_addr, cidr_plen, lxc_ip, chunk=1 << 22):
+    """n (CIDR index, remote address, endpoint index) candidates, drawn in order from
+    stream s, whose (remote, endpoint) address pair belongs to shard = (rank, world).
+    Every rank consumes the same candidate sequence, so the kept sets are disjoint
+    parts of one flow set."""
+    from cilium_amd.shard import pair_key4
+    rank, world = shard
+    picks, rems, epis, got = [], [], [], 0
+    while got < n:
+        pick = s.choice(chunk, len(cidr_addr))
+        rem = _rand_addrs_in(s, cidr_addr[pick], cidr_plen[pick])
+        epi = s.choice(chunk, len(lxc_ip))
+        raw = lambda a: a.astype(np.uint32).byteswap()              # the frame's raw word
+        own = (pair_key4(raw(rem), raw(lxc_ip[epi])) % np.uint64(world)) == np.uint64(rank)
+        picks.append(pick[own]); rems.append(rem[own]); epis.append(epi[own])
+        got += int(own.sum())
+    return (np.concatenate(picks)[:n], np.concatenate(rems)[:n], np.concatenate(epis)[:n])
 
 
 def _allowed_l4(pol_keys, ident, s):

@@ -150,3 +150,22 @@ def test_sharded_oracle_threads_equal_sequential():
         ck, cv = so.dump(name)
         ok, ov = om[name].dump()
         assert len(ck) == len(ok) and (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), name
+
+
+def test_config4_ranks_hold_disjoint_parts_of_one_flow_set():
+    """bench.py's config 3 / 4 at N > 1: every rank draws the same candidate flows and
+    keeps the address pairs it owns, so the CT shards are disjoint, every packet is
+    its rank's, and the union is one flow set (a rank's flows are found in no other
+    rank's shard, reply and RELATED entries included)."""
+    world, n = 3, 1 << 14
+    parts = [synth.config3(n, n, n_ep=64, n_cidrs=1024, n_ids=100, seed=7, shard=(r, world)) for r in range(world)]
+    seen, total = set(), 0
+    for r, w in enumerate(parts):
+        assert (shard.flow_shard(w.frames, w.length, world) == r).all()
+        keys = w.maps["ct4"].keys
+        assert (shard.ct4_shard(keys, world) == r).all()
+        mine = set(map(bytes, keys))                     # (a pair's RELATED twin repeats: one entry)
+        assert not (mine & seen)
+        seen |= mine
+        total += len(mine)
+    assert len(seen) == total

@@ -115,6 +115,40 @@ CV_HD int match_bucket(const uint32_t *w, const uint32_t *key, uint32_t tag, boo
 }
 
 // ---------------------------------------------------------------- device lookup
+// Bucket words of a table the launch also writes (conntrack, S::SYM) are read past
+// the CU's L1 (agent-scope loads, served by the XCD's L2): a lane's own claims and
+// kills are atomics, which drop the line from its L2 but not necessarily from its L1,
+// so a plain re-read of a bucket it just changed could return the old tags or key.
+template <class S>
+__device__ __forceinline__ uint2 ld_tags(const uint32_t *bw)
+{
+    if constexpr (S::SYM != 0) {
+        const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(bw),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+    }
+    return *reinterpret_cast<const uint2 *>(bw);
+}
+
+// the stored key at kw equals key (kw is 8-B aligned: KEY0 = 2 and even KW for SYM specs)
+template <class S>
+__device__ __forceinline__ bool key_eq(const uint32_t *kw, const uint32_t *key)
+{
+    bool eq = true;
+    if constexpr (S::SYM != 0) {
+        static_assert(S::KW % 2 == 0 && S::KEY0 % 2 == 0, "8-B key words");
+#pragma unroll
+        for (int j = 0; j < S::KW; j += 2) {
+            const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(kw + j),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            eq &= ((uint32_t)v == key[j]) & ((uint32_t)(v >> 32) == key[j + 1]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+    }
+    return eq;
+}
 template <class S>
 __device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets, uint64_t b, uint32_t (&w)[S::BW])
 {
@@ -150,7 +184,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
     uint64_t b = h & t.mask;
     for (int p = 0; p < MAX_PROBE; ++p) {
         const uint32_t *bw = t.buckets + b * S::BW;
-        const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
+        const uint2 tg = ld_tags<S>(bw);
         uint64_t match;
         bool empty;
         tag_masks<S>((uint64_t)tg.x | ((uint64_t)tg.y << 32), tag, match, empty);
@@ -158,9 +192,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
             const uint32_t *kw = bw + S::KEY0 + sl * S::KW;
-            bool eq = true;
-#pragma unroll
-            for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+            const bool eq = key_eq<S>(kw, key);
             if (eq) {
 #pragma unroll
                 for (int j = 0; j < S::IVW; ++j) ival[j] = bw[S::IVAL0 + sl * S::IVW + j];
@@ -389,7 +421,7 @@ __device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32
     pr.bw = t.buckets ? t.buckets + pr.b * S::BW : nullptr;
     if (!pr.bw) return pr;
     if constexpr (S::BW >= 32) {
-        const uint2 tg = *reinterpret_cast<const uint2 *>(pr.bw);
+        const uint2 tg = ld_tags<S>(pr.bw);
         pr.w[0] = tg.x; pr.w[1] = tg.y;
     } else {
         const uint4 *q = reinterpret_cast<const uint4 *>(pr.bw);
@@ -415,9 +447,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
             const uint32_t *kw = pr.bw + S::KEY0 + sl * S::KW;
-            bool eq = true;
-#pragma unroll
-            for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+            const bool eq = key_eq<S>(kw, key);
             if (eq) {
 #pragma unroll
                 for (int j = 0; j < S::IVW; ++j) ival[j] = pr.bw[S::IVAL0 + sl * S::IVW + j];
@@ -446,16 +476,14 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
         nx.b = b;
         nx.bw = t.buckets + b * S::BW;
         if constexpr (S::BW >= 32) {
-            const uint2 tg = *reinterpret_cast<const uint2 *>(nx.bw);
+            const uint2 tg = ld_tags<S>(nx.bw);
             uint64_t match;
             tag_masks<S>((uint64_t)tg.x | ((uint64_t)tg.y << 32), pr.tag, match, stop);
             while (match) {
                 const int sl = (__builtin_ctzll(match) >> 3);
                 match &= match - 1;
                 const uint32_t *kw = nx.bw + S::KEY0 + sl * S::KW;
-                bool eq = true;
-#pragma unroll
-                for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+                const bool eq = key_eq<S>(kw, key);
                 if (eq) {
 #pragma unroll
                     for (int j = 0; j < S::IVW; ++j) ival[j] = nx.bw[S::IVAL0 + sl * S::IVW + j];
@@ -531,7 +559,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     bool have_free = false;
     for (int p = 0; p < MAX_PROBE; ++p) {                          // 1) the key, and the first free slot
         const uint32_t *bw = t.buckets + b * S::BW;
-        const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
+        const uint2 tg = ld_tags<S>(bw);
         const uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
         uint64_t match;
         bool empty;
@@ -540,9 +568,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
             const uint32_t *kw = bw + S::KEY0 + sl * S::KW;
-            bool eq = true;
-#pragma unroll
-            for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
+            const bool eq = key_eq<S>(kw, key);
             if (eq) return (int64_t)(b * S::SPB + sl);
         }
         // bytes < TAG_BUSY (empty or dead): high bit of (byte - 2) with the byte's high bit clear
@@ -575,11 +601,13 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     return -1;
 }
 
-// Conntrack delete (map_delete_elem, conntrack.h:641-647): key -> zero words, then
-// tag -> dead.  The clearing stores are agent-scope atomics and complete (the
-// workgroup-scope release waits for them, without an L2 write-back) before the tag
-// CAS is issued, so a thread that claims the dead slot later in the launch cannot
-// have its new key overwritten by them.
+// Conntrack delete (map_delete_elem, conntrack.h:641-647): key and value slot -> zero
+// words, then tag -> dead.  The clearing writes are agent-scope atomics and complete
+// (the workgroup-scope release waits for them, without an L2 write-back) before the
+// tag CAS is issued.  A later claim of the dead slot in the same launch may come from
+// another XCD, whose L2 is not coherent with this one: the atomics leave no dirty
+// copy of the slot's key or value line in this XCD's L2 that the kernel-end write-back
+// could lay over the new owner's entry.
 template <class S>
 __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
 {
@@ -591,6 +619,11 @@ __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
     for (int j = 0; j < S::KW; ++j)
         __hip_atomic_exchange(t.buckets + b * S::BW + S::KEY0 + s * S::KW + j, 0u, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
+    if (t.vals) {
+        unsigned long long *v = reinterpret_cast<unsigned long long *>(t.vals + (size_t)slot * t.vstride);
+        for (uint32_t j = 0; j < t.vstride / 8; ++j)
+            __hip_atomic_store(v + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     uint32_t c = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {

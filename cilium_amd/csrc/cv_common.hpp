@@ -5,6 +5,17 @@
 #include <stdint.h>
 
 #define CV_HD __host__ __device__ __forceinline__
+// Device pointers that come out of memory (the tables of an endpoint, read from the
+// endpoint array) have no address space the compiler can see, so their accesses
+// become flat instructions (the address-space check, and a wait on both the vector
+// and the LDS/scalar counters at every use).  G() states that a pointer is global.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CV_G __attribute__((address_space(1)))
+#else
+#define CV_G
+#endif
+template <class T>
+__host__ __device__ __forceinline__ CV_G T *G(T *p) { return (CV_G T *)p; }
 
 namespace cv {
 

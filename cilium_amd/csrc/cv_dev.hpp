@@ -203,7 +203,7 @@ __device__ __forceinline__ void pol_add(LdsPolicy *pc, unsigned long long *d, un
             return;
         }
     }
-    atomicAdd(d, inc);
+    __hip_atomic_fetch_add(G(d), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void pol_cache_init(LdsPolicy &pc)
@@ -215,7 +215,9 @@ __device__ __forceinline__ void pol_cache_init(LdsPolicy &pc)
 __device__ __forceinline__ void pol_cache_flush(const LdsPolicy &pc)
 {
     for (int i = threadIdx.x; i < PC_N; i += blockDim.x)
-        if (pc.key[i] && pc.val[i]) atomicAdd(reinterpret_cast<unsigned long long *>(pc.key[i]), pc.val[i]);
+        if (pc.key[i] && pc.val[i])
+            __hip_atomic_fetch_add(G(reinterpret_cast<unsigned long long *>(pc.key[i])), pc.val[i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // EVENTS: the kernel instance that emits the optional outputs (drop / trace records,
@@ -377,7 +379,7 @@ __device__ __forceinline__ bool lxc6_find(const DpParams &p, const uint32_t *dad
 // slot); without the side array, the inline nonzero bit
 __device__ __forceinline__ uint32_t lxc_ifindex(const HashTable &t, int64_t slot, uint32_t ival)
 {
-    if (t.vals && slot >= 0) return *reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * t.vstride);
+    if (t.vals && slot >= 0) return *reinterpret_cast<const CV_G uint32_t *>(G(t.vals) + (size_t)slot * t.vstride);
     return (ival >> 17) & 1u;
 }
 
@@ -394,7 +396,7 @@ __device__ __forceinline__ uint32_t ifindex_of(const M &, const HashTable &t, in
 // endpoint_info.mac / .node_mac of a matched cilium_lxc entry (words: bytes 0-3, 4-5)
 __device__ __forceinline__ void lxc_macs(const HashTable &t, int64_t slot, uint32_t *mac, uint32_t *node_mac)
 {
-    const uint32_t *v = reinterpret_cast<const uint32_t *>(t.vals + (size_t)slot * t.vstride);
+    const CV_G uint32_t *v = reinterpret_cast<const CV_G uint32_t *>(G(t.vals) + (size_t)slot * t.vstride);
     mac[0] = v[1]; mac[1] = v[2] & 0xFFFFu;
     node_mac[0] = (v[2] >> 16) | (v[3] << 16); node_mac[1] = v[3] >> 16;
 }
@@ -448,7 +450,7 @@ struct Hit {
 
 __device__ __forceinline__ void hit_flush(const Hit &h)
 {
-    if (h.p) atomicAdd(h.p, h.inc);
+    if (h.p) __hip_atomic_fetch_add(G(h.p), h.inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // __policy_can_access (policy.h:51-119); cb[CB_POLICY] is 0 on these paths.  With
@@ -514,7 +516,7 @@ __device__ __forceinline__ int policy_hit(const HashTable &pol, uint32_t flags, 
 {
     if (s < 0) return DROP_POLICY;
     a.nu++;
-    uint8_t *v = pol.vals + (size_t)s * pol.vstride;
+    CV_G uint8_t *v = G(pol.vals) + (size_t)s * pol.vstride;
     // __sync_fetch_and_add(packets, 1) and (bytes, len) as ONE 64-bit atomic on the
     // slot's delta word {count:25 | bytes:39} (launches are chunked to <= 2^24
     // packets and folded after each chunk, so neither field can overflow)
@@ -524,8 +526,10 @@ __device__ __forceinline__ int policy_hit(const HashTable &pol, uint32_t flags, 
         if (defer) *defer = Hit{d, inc};
         else pol_add(a.pc, d, inc);
     } else {
-        atomicAdd(reinterpret_cast<unsigned long long *>(v + 8), 1ull);
-        atomicAdd(reinterpret_cast<unsigned long long *>(v + 16), (unsigned long long)len);
+        __hip_atomic_fetch_add(reinterpret_cast<CV_G unsigned long long *>(v + 8), 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(reinterpret_cast<CV_G unsigned long long *>(v + 16), (unsigned long long)len,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return l4 ? (int)proxy_port : TC_ACT_OK;
 }
@@ -694,7 +698,7 @@ struct CtState {
 
 __device__ __forceinline__ void ct_load(const HashTable &t, int64_t slot, CtE &e)
 {
-    const uint4 *q = reinterpret_cast<const uint4 *>(t.vals + (size_t)slot * t.vstride);
+    const CV_G uint4 *q = reinterpret_cast<const CV_G uint4 *>(G(t.vals) + (size_t)slot * t.vstride);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         uint4 v = q[k];
@@ -704,7 +708,7 @@ __device__ __forceinline__ void ct_load(const HashTable &t, int64_t slot, CtE &e
 
 __device__ __forceinline__ void ct_store(const HashTable &t, int64_t slot, const CtE &e)
 {
-    uint4 *q = reinterpret_cast<uint4 *>(t.vals + (size_t)slot * t.vstride);
+    CV_G uint4 *q = reinterpret_cast<CV_G uint4 *>(G(t.vals) + (size_t)slot * t.vstride);
 #pragma unroll
     for (int k = 0; k < 4; ++k) q[k] = make_uint4(e.w[4 * k], e.w[4 * k + 1], e.w[4 * k + 2], e.w[4 * k + 3]);
 }
@@ -928,7 +932,7 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
 __device__ __forceinline__ void ct_live_add(const HashTable &ct, Acct &a, bool guard, long long d)
 {
     if (!ct.live) return;
-    if (guard) atomicAdd(ct.live, (unsigned long long)d);
+    if (guard) __hip_atomic_fetch_add(G(ct.live), (unsigned long long)d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else pol_add(a.pc, ct.live, (unsigned long long)d);
 }
 
@@ -940,7 +944,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
     uint32_t k[T::KW];
     t.key(k);
     if (guard && ct.live && (absent || dev_find<typename T::Spec>(ct, k, nullptr) < 0) &&
-        __hip_atomic_load(ct.live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ct.cap)
+        __hip_atomic_load(G(ct.live), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ct.cap)
         return false;                                             // full: -E2BIG
     bool created;
     const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent);

@@ -214,8 +214,8 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         if (M::EV && o.frames) frame_copy(b.frames + (size_t)i * b.stride, o.frames + (size_t)i * b.stride, b.stride);
         m.pkt = b.base + i;
         m.hash = b.hash ? b.hash[i] : 0u;
-        m.src_id = e < p.n_eps ? p.eps[e].lxc_id : 0u;
-        m.src_label = e < p.n_eps ? p.eps[e].seclabel : 0u;
+        m.src_id = e < p.n_eps ? G(p.eps)[e].lxc_id : 0u;
+        m.src_label = e < p.n_eps ? G(p.eps)[e].seclabel : 0u;
         eg[1] = e & 0xFFFFu;
         eg[2] = 0;
         eg[0] = 0;
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
             res.ret = DROP_MISSED_TAIL_CALL;                      // no program for the source: nothing ran
             stage = STAGE_DONE;
         } else {
-            const EpDev &ep = p.eps[e];                           // handle_ingress: send_trace_notify(FROM_LXC)
+            const EpDev ep = G(p.eps)[e];                           // handle_ingress: send_trace_notify(FROM_LXC)
             notify_trace(p, m, TRACE_FROM_LXC, r.len, ep.lxc_id, ep.seclabel, 0, 0, 0, 0, true);
             stage = front_one(p, ep, r, eg, res, a, m);
         }
@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         } else {
             store_out(o, i, a);
             if (stage == STAGE_LB) {                              // join the (source, VIP) service group
-                const EpDev &ep = p.eps[e];
+                const EpDev ep = G(p.eps)[e];
                 uint64_t gh;
                 if (eg[0] & EG_V6) {
                     if constexpr (NW >= 32) {
@@ -265,7 +265,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     Rec r;
     rec_load(r, b, i, 4);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -370,7 +370,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     Rec6 r;
     rec_load(r, b, i, 8);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -537,7 +537,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; continue; }
-        const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+        const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
         Acct na{0, 0};                                            // speculative probes are not accounted
         if (!(eg[0] & EG_V6)) {
             Rec r;
@@ -688,7 +688,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     Rec r;
     rec_load(r, b, i, 4);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -775,7 +775,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy4(p, p.eps[e2 - 1], s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
+        res.ret = handle_policy4(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
                                  ct2, res.proxy, res.reason, a, m, &rn2);
         if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg4_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv4_local_delivery
@@ -835,7 +835,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     Rec6 r;
     rec_load(r, b, i, 8);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -915,7 +915,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy6(p, p.eps[e2 - 1], s, ep.seclabel, false, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
+        res.ret = handle_policy6(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
                                  res.proxy, res.reason, a, m, &rn2);
         if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg6_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv6_local_delivery
@@ -984,7 +984,7 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
             Rec r;
             rec_load(r, b, x, 4);
             const uint32_t *eg = g.eg + (size_t)x * EG_WORDS;
-            const EpDev &ep = p.eps[eg[1] & 0xFFFFu];
+            const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
             Eg4 y;
             eg4_state(r, eg, y);
             uint32_t seen;

@@ -120,26 +120,26 @@ CV_HD int match_bucket(const uint32_t *w, const uint32_t *key, uint32_t tag, boo
 // kills are atomics, which drop the line from its L2 but not necessarily from its L1,
 // so a plain re-read of a bucket it just changed could return the old tags or key.
 template <class S>
-__device__ __forceinline__ uint2 ld_tags(const uint32_t *bw)
+__device__ __forceinline__ uint2 ld_tags(const CV_G uint32_t *bw)
 {
     if constexpr (S::SYM != 0) {
-        const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(bw),
+        const unsigned long long v = __hip_atomic_load(reinterpret_cast<const CV_G unsigned long long *>(bw),
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
     }
-    return *reinterpret_cast<const uint2 *>(bw);
+    return *reinterpret_cast<const CV_G uint2 *>(bw);
 }
 
 // the stored key at kw equals key (kw is 8-B aligned: KEY0 = 2 and even KW for SYM specs)
 template <class S>
-__device__ __forceinline__ bool key_eq(const uint32_t *kw, const uint32_t *key)
+__device__ __forceinline__ bool key_eq(const CV_G uint32_t *kw, const uint32_t *key)
 {
     bool eq = true;
     if constexpr (S::SYM != 0) {
         static_assert(S::KW % 2 == 0 && S::KEY0 % 2 == 0, "8-B key words");
 #pragma unroll
         for (int j = 0; j < S::KW; j += 2) {
-            const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(kw + j),
+            const unsigned long long v = __hip_atomic_load(reinterpret_cast<const CV_G unsigned long long *>(kw + j),
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             eq &= ((uint32_t)v == key[j]) & ((uint32_t)(v >> 32) == key[j + 1]);
         }
@@ -152,7 +152,7 @@ __device__ __forceinline__ bool key_eq(const uint32_t *kw, const uint32_t *key)
 template <class S>
 __device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets, uint64_t b, uint32_t (&w)[S::BW])
 {
-    const uint4 *q = reinterpret_cast<const uint4 *>(buckets + b * S::BW);
+    const CV_G uint4 *q = reinterpret_cast<const CV_G uint4 *>(G(buckets) + b * S::BW);
 #pragma unroll
     for (int i = 0; i < S::BW / 4; ++i) {
         uint4 v = q[i];
@@ -183,7 +183,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
     const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
     for (int p = 0; p < MAX_PROBE; ++p) {
-        const uint32_t *bw = t.buckets + b * S::BW;
+        const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
         const uint2 tg = ld_tags<S>(bw);
         uint64_t match;
         bool empty;
@@ -191,7 +191,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
         while (match) {
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
-            const uint32_t *kw = bw + S::KEY0 + sl * S::KW;
+            const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KW;
             const bool eq = key_eq<S>(kw, key);
             if (eq) {
 #pragma unroll
@@ -406,7 +406,7 @@ __device__ __forceinline__ int64_t quad_find(const HashTable &t, const uint32_t 
 // round trips in flight together: a dependent-latency chain becomes one round trip.
 template <class S>
 struct Probe {
-    const uint32_t *bw;
+    const CV_G uint32_t *bw;
     uint64_t b;
     uint32_t tag;
     uint32_t w[S::BW >= 32 ? 2 : S::BW];
@@ -418,13 +418,13 @@ __device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32
     Probe<S> pr;
     const uint64_t h = home_hash<S>(key, pr.tag);
     pr.b = h & t.mask;
-    pr.bw = t.buckets ? t.buckets + pr.b * S::BW : nullptr;
+    pr.bw = t.buckets ? G(t.buckets) + pr.b * S::BW : nullptr;
     if (!pr.bw) return pr;
     if constexpr (S::BW >= 32) {
         const uint2 tg = ld_tags<S>(pr.bw);
         pr.w[0] = tg.x; pr.w[1] = tg.y;
     } else {
-        const uint4 *q = reinterpret_cast<const uint4 *>(pr.bw);
+        const CV_G uint4 *q = reinterpret_cast<const CV_G uint4 *>(pr.bw);
 #pragma unroll
         for (int i = 0; i < S::BW / 4; ++i) {
             const uint4 v = q[i];
@@ -446,7 +446,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
         while (match) {
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
-            const uint32_t *kw = pr.bw + S::KEY0 + sl * S::KW;
+            const CV_G uint32_t *kw = pr.bw + S::KEY0 + sl * S::KW;
             const bool eq = key_eq<S>(kw, key);
             if (eq) {
 #pragma unroll
@@ -474,7 +474,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
         Probe<S> nx;
         nx.tag = pr.tag;
         nx.b = b;
-        nx.bw = t.buckets + b * S::BW;
+        nx.bw = G(t.buckets) + b * S::BW;
         if constexpr (S::BW >= 32) {
             const uint2 tg = ld_tags<S>(nx.bw);
             uint64_t match;
@@ -482,7 +482,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
             while (match) {
                 const int sl = (__builtin_ctzll(match) >> 3);
                 match &= match - 1;
-                const uint32_t *kw = nx.bw + S::KEY0 + sl * S::KW;
+                const CV_G uint32_t *kw = nx.bw + S::KEY0 + sl * S::KW;
                 const bool eq = key_eq<S>(kw, key);
                 if (eq) {
 #pragma unroll
@@ -527,7 +527,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
 // whose fingerprint collides sees either the new key or the zero words every free
 // slot holds (dev_kill and the GC clear a key before its slot turns dead), neither of
 // which is its own key.  The kernel boundary publishes the entry to later launches.
-__device__ __forceinline__ bool claim_in_word(uint32_t *tw, uint32_t cur, int first, int nslots, uint32_t tag,
+__device__ __forceinline__ bool claim_in_word(CV_G uint32_t *tw, uint32_t cur, int first, int nslots, uint32_t tag,
                                               int &got)
 {
     for (;;) {
@@ -558,7 +558,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     uint64_t ftags = 0;
     bool have_free = false;
     for (int p = 0; p < MAX_PROBE; ++p) {                          // 1) the key, and the first free slot
-        const uint32_t *bw = t.buckets + b * S::BW;
+        const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
         const uint2 tg = ld_tags<S>(bw);
         const uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
         uint64_t match;
@@ -567,7 +567,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
         while (!known_absent && match) {
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
-            const uint32_t *kw = bw + S::KEY0 + sl * S::KW;
+            const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KW;
             const bool eq = key_eq<S>(kw, key);
             if (eq) return (int64_t)(b * S::SPB + sl);
         }
@@ -581,7 +581,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     if (!have_free) return -1;                                     // MAX_PROBE full buckets
     b = fb;
     for (int p = 0; p < MAX_PROBE; ++p) {                          // 2) claim (one CAS per try)
-        uint32_t *bw = t.buckets + b * S::BW;
+        CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
         uint64_t cur = ftags;
         if (p > 0) {
             const uint2 tg = make_uint2(__hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -613,14 +613,14 @@ __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
 {
     const uint64_t b = (uint64_t)slot / S::SPB;
     const int s = (int)((uint64_t)slot % S::SPB);
-    uint32_t *tw = t.buckets + b * S::BW + (s >> 2);
+    CV_G uint32_t *tw = G(t.buckets) + b * S::BW + (s >> 2);
     const int sh = 8 * (s & 3);
 #pragma unroll
     for (int j = 0; j < S::KW; ++j)
-        __hip_atomic_exchange(t.buckets + b * S::BW + S::KEY0 + s * S::KW + j, 0u, __ATOMIC_RELAXED,
+        __hip_atomic_exchange(G(t.buckets) + b * S::BW + S::KEY0 + s * S::KW + j, 0u, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
     if (t.vals) {
-        unsigned long long *v = reinterpret_cast<unsigned long long *>(t.vals + (size_t)slot * t.vstride);
+        CV_G unsigned long long *v = reinterpret_cast<CV_G unsigned long long *>(G(t.vals) + (size_t)slot * t.vstride);
         for (uint32_t j = 0; j < t.vstride / 8; ++j)
             __hip_atomic_store(v + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

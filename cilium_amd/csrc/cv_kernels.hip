@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
     __shared__ uint4 stage[BLOCK / 64][256];
     for (int j = threadIdx.x; j < 256 * 2; j += BLOCK) drops[j] = 0;
     __syncthreads();
-    const HashTable pol = p.eps[ep].policy;
+    const HashTable pol = G(p.eps)[ep].policy;
     uint4 *st = stage[threadIdx.x >> 6];
     Hit hits[PPT];
 #pragma unroll
@@ -331,10 +331,10 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             }
         }
         if (staged) {                                             // group by (CT map, address pair)
-            const EpDev &ep = p.eps[smeta & 0xFFFFu];
+            const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
             group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
         } else if (v6stage) {
-            const EpDev &ep = p.eps[smeta & 0xFFFFu];
+            const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
             const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
             const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
             group_push(g, group_node(g, pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets)), i,
@@ -374,7 +374,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 {
     const uint4 s0 = g.srec[2 * i], s1 = g.srec[2 * i + 1];
     const uint32_t meta = s1.z;
-    const EpDev &ep = p.eps[meta & 0xFFFFu];
+    const EpDev ep = G(p.eps)[meta & 0xFFFFu];
     Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
@@ -438,7 +438,7 @@ __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b
     rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
     const uint4 s1 = g.srec[2 * i + 1];
     const uint32_t meta = s1.z;
-    const EpDev &ep = p.eps[meta & 0xFFFFu];
+    const EpDev ep = G(p.eps)[meta & 0xFFFFu];
     Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
         const uint32_t mk = g.gslot[i];
         if (mk != COMMIT4 && mk != COMMIT6) continue;
         const uint4 s1 = g.srec[2 * i + 1];
-        const EpDev &ep = p.eps[s1.z & 0xFFFFu];
+        const EpDev ep = G(p.eps)[s1.z & 0xFFFFu];
         uint32_t seen;
         if (mk == COMMIT4) {
             const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);

@@ -182,7 +182,7 @@ struct cv_ctx {
     DevBuf eps_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
-    DevBuf gtable, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
+    DevBuf gtable, gnode1, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -857,7 +857,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     uint64_t cap = 1024;
     while (cap < per * cmax || cap < c->gcap) cap <<= 1;
     (void)hipDeviceSynchronize();
-    if (c->gtable.alloc(cap * 16) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
+    if (c->gtable.alloc(cap * 16) || c->gnode1.alloc(cap * 8) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsrec.alloc((size_t)cmax * 32) ||
         c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) || c->gifx.alloc((size_t)cmax * 4) ||
         c->gcursor.alloc(CURSOR_WORDS * 4) ||
@@ -1482,6 +1482,11 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 2, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
+        uint64_t ncap = 1024;                                     // the one-word node table of this launch
+        while (ncap < 2ull * n) ncap <<= 1;
+        gs.node1 = c->gnode1.as<unsigned long long>();
+        gs.cap_mask = (uint32_t)(ncap - 1);
+        (void)hipMemsetAsync(gs.node1, 0, ncap * 8, (hipStream_t)stream);
         if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off, b->stride), gs,
                                        (hipStream_t)stream)))
             return r;

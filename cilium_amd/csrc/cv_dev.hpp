@@ -1696,6 +1696,35 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
     if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;
 }
 
+// The netdev path's node insert: one word per node {tag | the group's latest packet},
+// the table zeroed before the launch, so a packet joins (or opens) its group with one
+// CAS in the common case -- the first try expects an empty word; a lost race returns
+// the word, whose tag says whether to retry on it (same group: swap in this packet)
+// or to move on.  Same result as group_node + group_push.
+__device__ __forceinline__ void group_insert1(const GroupScratch &g, uint64_t gh, uint32_t i, int q)
+{
+    const uint32_t tag = (uint32_t)gh | 1u;
+    const unsigned long long mine = (unsigned long long)tag << 32 | i;
+    uint32_t s = (uint32_t)(gh >> 32) & g.cap_mask;
+    CV_G unsigned long long *nodes = G(g.node1);
+    unsigned long long cur = 0;
+    for (;;) {
+        if (__hip_atomic_compare_exchange_strong(nodes + s, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            break;
+        if ((uint32_t)(cur >> 32) != tag) {                       // another group's node: next slot
+            s = (s + 1) & g.cap_mask;
+            cur = 0;
+        }
+    }
+    const bool first = cur == 0;
+    g.gslot[i] = s;
+    g.next[i] = first ? NONE : (uint32_t)cur;
+    const uint32_t k = blockIdx.x % QSPLIT;
+    const uint32_t at = wave_append(&g.cursor[qctr(q, k)], first);
+    if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;
+}
+
 // ------------------------------------------------------------------ size-sorted runs
 // One lane runs a group's packets one after another, so a wave lasts as long as the
 // largest of its 64 groups.  Before a heavy stage the queue's groups are flattened

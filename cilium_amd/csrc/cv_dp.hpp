@@ -98,6 +98,8 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t qregion;          // words per region
     uint32_t *work;            // per group: `order` offset of its run, in size-class order
     uint32_t *ifx;             // per packet: the destination endpoint's ifindex (netdev path)
+    unsigned long long *node1; // netdev path: one-word nodes {tag32 | head packet}, zeroed per
+                               // launch (cap_mask + 1 words), or null (the epoch-tagged table)
 };
 // GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
 // contention on one counter); blocks b with b % QSPLIT == k hold at most

@@ -332,13 +332,12 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         }
         if (staged) {                                             // group by (CT map, address pair)
             const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
-            group_push(g, group_node(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17)), i, Q_NETDEV);
+            group_insert1(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17), i, Q_NETDEV);
         } else if (v6stage) {
             const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
             const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
             const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
-            group_push(g, group_node(g, pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets)), i,
-                       Q_NETDEV6);
+            group_insert1(g, pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets), i, Q_NETDEV6);
         }
         if (!live) continue;
         const bool fwd_here = !staged && !v6stage && ret == TC_ACT_OK;
@@ -557,7 +556,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q)
         uint32_t m[GMAX];
         if (act) {
             ent = queue_entry(g, q, n, j);
-            head = (uint32_t)g.table[2 * *ent + 1];
+            head = g.node1 ? (uint32_t)g.node1[*ent] : (uint32_t)g.table[2 * *ent + 1];
             for (x = head; x != NONE && cnt < GMAX; x = g.next[x]) {   // insertion into registers
                 int pos = 0;
 #pragma unroll

@@ -116,13 +116,16 @@ CV_HD int match_bucket(const uint32_t *w, const uint32_t *key, uint32_t tag, boo
 
 // ---------------------------------------------------------------- device lookup
 // Bucket words of a table the launch also writes (conntrack, S::SYM) are read past
-// the CU's L1 (agent-scope loads, served by the XCD's L2): a lane's own claims and
-// kills are atomics, which drop the line from its L2 but not necessarily from its L1,
-// so a plain re-read of a bucket it just changed could return the old tags or key.
-template <class S>
+// the CU's L1 (agent-scope loads, served by the XCD's L2) where FRESH: a lane's own
+// claims and kills are atomics, which drop the line from its L2 but not necessarily
+// from its L1, so a plain re-read of a bucket it just changed could return the old
+// tags or key.  Callers that invalidate their L1 after their own (rare) bucket
+// changes read with plain loads instead (FRESH = false): the tags and the key then
+// come from one L1 line fill.
+template <class S, bool FRESH = true>
 __device__ __forceinline__ uint2 ld_tags(const CV_G uint32_t *bw)
 {
-    if constexpr (S::SYM != 0) {
+    if constexpr (S::SYM != 0 && FRESH) {
         const unsigned long long v = __hip_atomic_load(reinterpret_cast<const CV_G unsigned long long *>(bw),
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
@@ -131,11 +134,11 @@ __device__ __forceinline__ uint2 ld_tags(const CV_G uint32_t *bw)
 }
 
 // the stored key at kw equals key (kw is 8-B aligned: KEY0 = 2 and even KW for SYM specs)
-template <class S>
+template <class S, bool FRESH = true>
 __device__ __forceinline__ bool key_eq(const CV_G uint32_t *kw, const uint32_t *key)
 {
     bool eq = true;
-    if constexpr (S::SYM != 0) {
+    if constexpr (S::SYM != 0 && FRESH) {
         static_assert(S::KW % 2 == 0 && S::KEY0 % 2 == 0, "8-B key words");
 #pragma unroll
         for (int j = 0; j < S::KW; j += 2) {
@@ -176,7 +179,7 @@ __device__ __forceinline__ void tag_masks(uint64_t tags, uint32_t tag, uint64_t 
 // keys (and inline values) of slots whose fingerprint matches, so a probe keeps a
 // few registers live instead of the whole bucket.  Same result as the full-bucket
 // match: a key is stored once; the chain ends at a bucket with an empty slot.
-template <class S>
+template <class S, bool FRESH = true>
 __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     uint32_t tag;
@@ -184,7 +187,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
     uint64_t b = h & t.mask;
     for (int p = 0; p < MAX_PROBE; ++p) {
         const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
-        const uint2 tg = ld_tags<S>(bw);
+        const uint2 tg = ld_tags<S, FRESH>(bw);
         uint64_t match;
         bool empty;
         tag_masks<S>((uint64_t)tg.x | ((uint64_t)tg.y << 32), tag, match, empty);
@@ -192,7 +195,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
             const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KW;
-            const bool eq = key_eq<S>(kw, key);
+            const bool eq = key_eq<S, FRESH>(kw, key);
             if (eq) {
 #pragma unroll
                 for (int j = 0; j < S::IVW; ++j) ival[j] = bw[S::IVAL0 + sl * S::IVW + j];
@@ -212,11 +215,11 @@ __device__ __forceinline__ int64_t dev_find_from(const HashTable &t, const uint3
                                                  int p0, uint32_t *ival);
 
 // Returns the slot index (bucket * SPB + slot) or -1; copies the inline value.
-template <class S>
+template <class S, bool FRESH = true>
 __device__ __forceinline__ int64_t dev_find(const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     if (!t.buckets) return -1;
-    if constexpr (S::BW >= 32) return dev_find_tf<S>(t, key, ival);   // (tag-first 64-B probes: slower)
+    if constexpr (S::BW >= 32) return dev_find_tf<S, FRESH>(t, key, ival);   // (tag-first 64-B probes: slower)
     uint32_t tag;
     const uint64_t h = home_hash<S>(key, tag);
     return dev_find_from<S>(t, key, tag, h & t.mask, 0, ival);
@@ -412,7 +415,7 @@ struct Probe {
     uint32_t w[S::BW >= 32 ? 2 : S::BW];
 };
 
-template <class S>
+template <class S, bool FRESH = true>
 __device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32_t *key)
 {
     Probe<S> pr;
@@ -421,7 +424,7 @@ __device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32
     pr.bw = t.buckets ? G(t.buckets) + pr.b * S::BW : nullptr;
     if (!pr.bw) return pr;
     if constexpr (S::BW >= 32) {
-        const uint2 tg = ld_tags<S>(pr.bw);
+        const uint2 tg = ld_tags<S, FRESH>(pr.bw);
         pr.w[0] = tg.x; pr.w[1] = tg.y;
     } else {
         const CV_G uint4 *q = reinterpret_cast<const CV_G uint4 *>(pr.bw);
@@ -434,7 +437,7 @@ __device__ __forceinline__ Probe<S> probe_begin(const HashTable &t, const uint32
     return pr;
 }
 
-template <class S>
+template <class S, bool FRESH = true>
 __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable &t, const uint32_t *key, uint32_t *ival)
 {
     if (!pr.bw) return -1;
@@ -447,7 +450,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
             const CV_G uint32_t *kw = pr.bw + S::KEY0 + sl * S::KW;
-            const bool eq = key_eq<S>(kw, key);
+            const bool eq = key_eq<S, FRESH>(kw, key);
             if (eq) {
 #pragma unroll
                 for (int j = 0; j < S::IVW; ++j) ival[j] = pr.bw[S::IVAL0 + sl * S::IVW + j];
@@ -476,14 +479,14 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
         nx.b = b;
         nx.bw = G(t.buckets) + b * S::BW;
         if constexpr (S::BW >= 32) {
-            const uint2 tg = ld_tags<S>(nx.bw);
+            const uint2 tg = ld_tags<S, FRESH>(nx.bw);
             uint64_t match;
             tag_masks<S>((uint64_t)tg.x | ((uint64_t)tg.y << 32), pr.tag, match, stop);
             while (match) {
                 const int sl = (__builtin_ctzll(match) >> 3);
                 match &= match - 1;
                 const CV_G uint32_t *kw = nx.bw + S::KEY0 + sl * S::KW;
-                const bool eq = key_eq<S>(kw, key);
+                const bool eq = key_eq<S, FRESH>(kw, key);
                 if (eq) {
 #pragma unroll
                     for (int j = 0; j < S::IVW; ++j) ival[j] = nx.bw[S::IVAL0 + sl * S::IVW + j];

@@ -387,7 +387,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     }
     RevNatOut rn{false, false, 0, 0};
     bool defer = single && !p.ct_guard;                          // the only packet of its group
-    const int ret = handle_policy4(p, ep, s, s1.w, (meta >> 16) & 1u,
+    const int ret = handle_policy4<M, false>(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc4, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
                                    a, m, &rn, &defer);
     if (defer) g.gslot[i] = COMMIT4;
@@ -452,7 +452,7 @@ __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b
     RevNat6Out rn;
     rn.valid = false;
     bool defer = single && !p.ct_guard;
-    const int ret = handle_policy6(p, ep, s, s1.w, (meta >> 16) & 1u,
+    const int ret = handle_policy6<M, false>(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc6, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
                                    a, m, &rn, &defer);
     if (defer) g.gslot[i] = COMMIT6;

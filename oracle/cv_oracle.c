@@ -251,6 +251,46 @@ uint32_t or_map_count(const or_map *m)
 static uint32_t g_sort_ks;
 static int cmp_rows(const void *a, const void *b) { return memcmp(a, b, g_sort_ks); }
 
+/* Order-independent digest of a hash map's entries (test infrastructure: compares a
+ * 33M-entry conntrack table with the device's without sorting either dump).  Per
+ * entry: the key then the value, each zero-padded to 8-byte words, chained through
+ * splitmix64's finalizer from a fixed seed; out = {count, sum of the chains mod 2^64,
+ * xor of the chains}.  tests/harness.table_digest is the same function over dumps. */
+static uint64_t dg_mix(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static uint64_t dg_row(const uint8_t *k, uint32_t ks, const uint8_t *v, uint32_t vs)
+{
+    uint64_t h = 0x243F6A8885A308D3ULL;
+    for (int part = 0; part < 2; part++) {
+        const uint8_t *p = part ? v : k;
+        uint32_t n = part ? vs : ks;
+        for (uint32_t o = 0; o < n; o += 8) {
+            uint64_t w = 0;
+            memcpy(&w, p + o, n - o < 8 ? n - o : 8);
+            h = dg_mix(h ^ w);
+        }
+    }
+    return h;
+}
+
+void or_map_digest(const or_map *m, uint64_t out[3])
+{
+    uint64_t cnt = 0, sum = 0, x = 0;
+    if (m->type != OR_MAP_LPM_TRIE) {
+        for (uint32_t i = 0; i < m->h->cap; i++) {
+            if (!m->h->used[i]) continue;
+            const uint64_t h = dg_row(m->h->keys + (size_t)i * m->ks, m->ks, m->h->vals + (size_t)i * m->vs, m->vs);
+            cnt++; sum += h; x ^= h;
+        }
+    }
+    out[0] = cnt; out[1] = sum; out[2] = x;
+}
+
 uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max)
 {
     uint32_t n = or_map_count(m), row = m->ks + m->vs, k = 0;

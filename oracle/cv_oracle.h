@@ -128,6 +128,7 @@ int      or_map_delete(or_map *m, const void *key);
 uint32_t or_map_count(const or_map *m);
 /* all entries, sorted by key bytes; returns the count written (<= max) */
 uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max);
+void or_map_digest(const or_map *m, uint64_t out[3]);   /* test infrastructure */
 /* the kernel checksum helper restatement (known-answer tests) */
 int or_csum_apply(uint8_t *frame, uint32_t len, uint32_t op, uint32_t off, uint32_t from, uint32_t to,
                   uint32_t flags, uint64_t *diff);

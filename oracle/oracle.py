@@ -44,6 +44,8 @@ def lib():
         L.or_map_count.argtypes = [vp]
         L.or_map_dump.restype = u32
         L.or_map_dump.argtypes = [vp, vp, vp, u32]
+        L.or_map_digest.restype = None
+        L.or_map_digest.argtypes = [vp, vp]
         L.or_ct_gc.restype = u32
         L.or_ct_gc.argtypes = [vp, u32]
         L.or_get_prefix.restype = u32
@@ -125,6 +127,12 @@ class OMap:
         vals = np.zeros((max(n, 1), self.vs), np.uint8)
         k = lib().or_map_dump(self.h, _p(keys), _p(vals), n)
         return keys[:k], vals[:k]
+
+    def digest(self):
+        """(count, sum, xor) of the per-entry chains (tests/harness.table_digest)"""
+        out = np.zeros(3, np.uint64)
+        lib().or_map_digest(self.h, out.ctypes.data)
+        return tuple(int(x) for x in out)
 
     def __del__(self):
         try:

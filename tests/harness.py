@@ -159,3 +159,34 @@ class ShardedOracle:
     def dump(self, name):
         ks, vs = zip(*(maps[name].dump() for _, _, maps in self.parts))
         return np.concatenate(ks), np.concatenate(vs)
+
+
+def _dg_mix(z):
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def table_digest(keys, vals, chunk=1 << 22):
+    """(count, sum, xor) of the entries' chains, the same function as the oracle's
+    or_map_digest: key then value, each zero-padded to 8-byte words, chained through
+    splitmix64's finalizer.  Order-independent: compares a full-size table dump with
+    the oracle's without sorting 33M rows."""
+    n = len(keys)
+    tot, x = np.uint64(0), np.uint64(0)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        h = np.full(hi - lo, 0x243F6A8885A308D3, np.uint64)
+        for part in (keys[lo:hi], vals[lo:hi]):
+            w = part.shape[1]
+            pad = np.zeros((hi - lo, (w + 7) // 8 * 8), np.uint8)
+            pad[:, :w] = part
+            words = pad.view("<u8")
+            for j in range(words.shape[1]):
+                h = _dg_mix(h ^ words[:, j])
+        with np.errstate(over="ignore"):
+            tot = tot + np.add.reduce(h, dtype=np.uint64)
+        x ^= np.bitwise_xor.reduce(h)
+    return (n, int(tot), int(x))
+

@@ -169,3 +169,19 @@ def test_config4_ranks_hold_disjoint_parts_of_one_flow_set():
         seen |= mine
         total += len(mine)
     assert len(seen) == total
+
+
+def test_table_digest_matches_oracle():
+    """tests/harness.table_digest (numpy, over a device dump) is the oracle's
+    or_map_digest: the full-size GPU tests compare 33M-entry tables through it."""
+    w = synth.config3(1 << 12, 1 << 12, n_ep=64, n_cidrs=1024, n_ids=100, seed=3)
+    dp, om = H.oracle_dp(w)
+    dp.netdev_ingress(w.frames, w.length, w.mark, now=w.now)
+    for name in ("ct4", "policy"):
+        k, v = om[name].dump()
+        assert om[name].digest() == H.table_digest(k, v)
+        assert om[name].digest()[0] == len(k) > 0
+    k, v = om["ct4"].dump()
+    v2 = v.copy()
+    v2[0, 0] ^= 1
+    assert H.table_digest(k, v2) != H.table_digest(k, v)

@@ -908,7 +908,14 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     t2.key(k2);
     const Probe<S> p1 = probe_begin<S, FRESH>(ct, k1);
     Probe<S> p2;
-    if (dir != CT_SERVICE) p2 = probe_begin<S, FRESH>(ct, k2);
+    if (dir != CT_SERVICE) {
+        if constexpr (S::SYM != 0) {                              // the reverse tuple's home bucket is the
+            p2 = p1;                                              // same (home_hash): one tag read serves both
+            p2.tag = tag_of(key_hash<S>(k2));
+        } else {
+            p2 = probe_begin<S, FRESH>(ct, k2);
+        }
+    }
     a.nl++;
     slot = probe_end<S, FRESH>(p1, ct, k1, nullptr);
     if (slot >= 0) {

@@ -146,6 +146,12 @@ __device__ __forceinline__ bool key_eq(const CV_G uint32_t *kw, const uint32_t *
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             eq &= ((uint32_t)v == key[j]) & ((uint32_t)(v >> 32) == key[j + 1]);
         }
+    } else if constexpr (S::SYM != 0) {
+#pragma unroll
+        for (int j = 0; j < S::KW; j += 2) {
+            const uint2 v = *reinterpret_cast<const CV_G uint2 *>(kw + j);
+            eq &= (v.x == key[j]) & (v.y == key[j + 1]);
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);

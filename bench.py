@@ -141,7 +141,8 @@ def cpu_baseline(name, w, min_seconds=10.0):
     OpenMP over the threads.  Conntrack ingress (configs 3, 4): the sample partitioned
     by address pair over the threads, one oracle datapath per shard with its CT shard
     (tests/harness.ShardedOracle; identical results to one sequential run).  Egress
-    (config 5): one thread in packet order.  Stateful samples are re-run as fresh
+    (config 5): one replica per thread (tables replicated, each with its own
+    conntrack), the way bench.py runs that path on N GPUs.  Stateful samples are re-run as fresh
     steps (synth.port_variant), as on the GPU."""
     from cilium_amd import synth
     from tests import harness as H
@@ -169,15 +170,20 @@ def cpu_baseline(name, w, min_seconds=10.0):
         sw.extra = {k: (x[:sample] if isinstance(x, np.ndarray) and len(x) == w.n else x) for k, x in w.extra.items()
                     if not isinstance(k, tuple)}                  # (not port_variant's cache of the full batch)
         if name == "config5":
-            dp, _ = H.oracle_dp(sw)
-            cores, how = 1, "1 thread, sequential (egress conntrack groups are not address pairs)"
+            # one replica per thread (tables replicated, each its own conntrack and its
+            # own fresh batches), as bench.py runs the GPUs for this path at N > 1
+            pool = ThreadPoolExecutor(threads)
+            dps = list(pool.map(lambda _: H.oracle_dp(sw)[0], range(threads)))
+            cores, how = threads, f"{threads} threads, one replica (tables + own conntrack) each"
             while busy < min_seconds:
                 v += 1
-                f = H.apply_variant(sw.frames, *synth.port_variant(sw, v))
+                fs = [H.apply_variant(sw.frames, *synth.port_variant(sw, v))] * threads
                 t0 = time.perf_counter()
-                dp.lxc_egress(f, sw.length, sw.extra["src_ep"], sw.extra["flow_hash"], now=w.now + v)
+                list(pool.map(lambda t: dps[t].lxc_egress(fs[t], sw.length, sw.extra["src_ep"], sw.extra["flow_hash"],
+                                                          now=w.now + v), range(threads)))
                 busy += time.perf_counter() - t0
-                done += sample
+                done += sample * threads
+            pool.shutdown()
         else:
             so = H.ShardedOracle(sw, threads)
             pool = ThreadPoolExecutor(threads)

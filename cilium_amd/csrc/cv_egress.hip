@@ -21,6 +21,12 @@
 
 namespace cv {
 
+// conntrack reads of the egress stages: plain loads, with the CU's L1 dropped after
+// the lane's own in-place bucket changes (creates, deletes) so that its later lookups
+// see them (see ld_tags); agent-scope loads on every read measured 3-5 % slower
+constexpr bool EGF = false;
+__device__ __forceinline__ void eg_changed() { l1_inv(); }
+
 int grid_for(uint32_t n);
 
 // egress scratch words (GroupScratch::eg, EG_WORDS per packet)
@@ -282,13 +288,14 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     t.daddr = vip; t.saddr = saddr; t.nexthdr = rec_u8c<23>(r); t.dport = t.sport = 0;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
-    int ret = ct_lookup<false>(ep.ct4, t, h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
+    int ret = ct_lookup<false, EGF>(ep.ct4, t, h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
     uint32_t k[2], v[3];
     bool have = false;
     if (ret == E_TRUNC) goto fin;
     if (ret == CT_NEW) {
         st.slave = hsh % count + 1;                               // lb4_select_slave
-        const int c = ct_create<false>(ep.ct4, t, r.len, CT_SERVICE, st, now, a, p.ct_guard);
+        const int c = ct_create<false>(ep.ct4, t, r.len, CT_SERVICE, st, now, a, p.ct_guard, false, true);
+        eg_changed();
         if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
     } else if (ret < 0) {
         ret = DROP_NO_SERVICE;
@@ -312,7 +319,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         uint32_t tk[4];                                           // ct_update4_slave
         t.key(tk);
         a.nl++;
-        const int64_t s2 = dev_find<Ct4Spec>(ep.ct4, tk, nullptr);
+        const int64_t s2 = dev_find<Ct4Spec, EGF>(ep.ct4, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
             ct_load(ep.ct4, s2, e);
@@ -387,13 +394,14 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     t.nexthdr = s.nexthdr; t.dport = t.sport = 0;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
-    int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
+    int ret = ct_lookup<true, EGF>(ep.ct6, t, s.h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
     uint32_t k[5] = {s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3], 0}, v[6];
     bool have = false;
     if (ret == E_TRUNC) goto fin;
     if (ret == CT_NEW) {
         st.slave = hsh % count + 1;
-        const int c = ct_create<true>(ep.ct6, t, r.len, CT_SERVICE, st, now, a, p.ct_guard);
+        const int c = ct_create<true>(ep.ct6, t, r.len, CT_SERVICE, st, now, a, p.ct_guard, false, true);
+        eg_changed();
         if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
     } else if (ret < 0) {
         ret = DROP_NO_SERVICE;
@@ -417,7 +425,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         uint32_t tk[10];                                          // ct_update6_slave
         t.key(tk);
         a.nl++;
-        const int64_t s2 = dev_find<Ct6Spec>(ep.ct6, tk, nullptr);
+        const int64_t s2 = dev_find<Ct6Spec, EGF>(ep.ct6, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
             ct_load(ep.ct6, s2, e);
@@ -572,7 +580,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             if (l4ok && ep.ct4.buckets) {
                 uint32_t k[4];
                 t1.key(k);
-                const int64_t sl = dev_find<Ct4Spec>(ep.ct4, k, nullptr);
+                const int64_t sl = dev_find<Ct4Spec, false>(ep.ct4, k, nullptr);   // (no CT writes here)
                 if (sl >= 0) {
                     CtE e;
                     ct_load(ep.ct4, sl, e);
@@ -599,7 +607,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             if (x.s.l4off >= 0 && ct_l4<true>(t1, x.s.h, CT_EGRESS, seen) >= 0) {
                 uint32_t k[10];
                 t1.key(k);
-                const int64_t sl = dev_find<Ct6Spec>(ep.ct6, k, nullptr);
+                const int64_t sl = dev_find<Ct6Spec, false>(ep.ct6, k, nullptr);
                 if (sl >= 0) {
                     CtE e;
                     ct_load(ep.ct6, sl, e);
@@ -710,7 +718,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     Probe<LxcV4Spec> lxq;
     if (p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
     bool mon = false;
-    int ret = ct_lookup<false>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
+    int ret = ct_lookup<false, EGF>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
@@ -725,14 +733,18 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);   // ct_delete4
+        if (ret == CT_ESTABLISHED) {
+            ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);       // ct_delete4
+            eg_changed();
+        }
         ret = verdict;
         goto drop;
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
         const bool defer = eg[0] & EG_NAT_DEFER;
-        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer);
+        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer, true);
+        eg_changed();
         if (defer && c != DROP_CT_CREATE_FAILED) g.eg[(size_t)i * EG_WORDS] = eg[0] | EG_NAT_DONE;
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
@@ -775,7 +787,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy4(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
+        res.ret = handle_policy4<M, EGF>(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
                                  ct2, res.proxy, res.reason, a, m, &rn2);
         if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg4_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv4_local_delivery
@@ -852,7 +864,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     Probe<LxcV6Spec> lxq;                                         // endpoint lookup of daddr, issued early
     if (p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
     bool mon = false;
-    int ret = ct_lookup<true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
+    int ret = ct_lookup<true, EGF>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;
@@ -868,13 +880,17 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);   // ct_delete6
+        if (ret == CT_ESTABLISHED) {
+            ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);       // ct_delete6
+            eg_changed();
+        }
         ret = verdict;
         goto drop;
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
-        const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard);
+        const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, false, true);
+        eg_changed();
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
         uint32_t na[4], np;
@@ -915,7 +931,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
         uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy6(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
+        res.ret = handle_policy6<M, EGF>(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
                                  res.proxy, res.reason, a, m, &rn2);
         if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
             eg6_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv6_local_delivery

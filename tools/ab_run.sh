@@ -1,6 +1,6 @@
 #!/bin/bash
 # timing-only A/B of library variants on config 3 (variants may give wrong answers)
-#   usage: bash tools/dbg/ab_run.sh <tag> <variant>...   (variant "main" = cilium_amd/_lib)
+#   usage: bash tools/ab_run.sh <tag> <variant>...   (variant "main" = cilium_amd/_lib)
 T=$1; shift
 OUT=gpurun_out/$T; mkdir -p $OUT; export TMPDIR=/tmp
 for v in "$@"; do

@@ -182,7 +182,7 @@ struct cv_ctx {
     DevBuf eps_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
-    DevBuf gtable, gnode1, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
+    DevBuf gtable, gnode1, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -857,7 +857,8 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     uint64_t cap = 1024;
     while (cap < per * cmax || cap < c->gcap) cap <<= 1;
     (void)hipDeviceSynchronize();
-    if (c->gtable.alloc(cap * 16) || c->gnode1.alloc(cap * 8) || c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
+    if (c->gtable.alloc(cap * 16) || c->gnode1.alloc(cap * 8) || c->gsingle.alloc((size_t)cmax * 4) ||
+        c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsrec.alloc((size_t)cmax * 32) ||
         c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) || c->gifx.alloc((size_t)cmax * 4) ||
         c->gcursor.alloc(CURSOR_WORDS * 4) ||
@@ -887,7 +888,8 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsrec.as<uint4>(),
                     c->gparent.as<unsigned long long>(), c->geg.as<uint32_t>(),
                     ++c->serial, c->gorder.as<uint32_t>(), c->gcursor.as<uint32_t>(), c->gqueue.as<uint32_t>(),
-                    (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>()};
+                    (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>(), nullptr,
+                    c->gsingle.as<uint32_t>()};
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;

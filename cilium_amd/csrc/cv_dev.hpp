@@ -15,6 +15,7 @@ namespace cv {
 
 constexpr int BLOCK = 256;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t SINGLE_RUN = 0x80000000u; // a flattened queue word naming a singleton's packet
 constexpr uint32_t COMMIT4 = 0xFFFFFFFEu;     // g.gslot marks of a deferred CT create (k_ct_commit)
 constexpr uint32_t COMMIT6 = 0xFFFFFFFDu;
 
@@ -1884,16 +1885,18 @@ __device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t h
     }
 }
 
-// fn(i, run size) for every member of every scheduled run of queue q, runs in `work` order and
-// members in packet order; the next member's index is loaded while fn runs
-// (SORTED false: the runs in queue order, when k_group_schedule did not run)
+// fn(i, run size) for every member of every scheduled run of queue q, runs in `work`
+// order and members in packet order, then every singleton group (k_group_flatten
+// lists their packets densely in `single`); the next member's index is loaded while
+// fn runs.  (SORTED false: the queue in order when k_group_schedule did not run, the
+// queue word of a singleton naming its packet, SINGLE_RUN-tagged.)
 template <bool SORTED = true, class F>
 __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool first_only, F &&fn)
 {
     uint32_t n[QSPLIT];
     const uint32_t total = queue_sizes(g, q, n);
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
-        const uint32_t off = SORTED ? g.work[j] : *queue_entry(g, q, n, j);
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    auto run = [&](uint32_t off) {
         const uint32_t cnt = first_only ? 1u : g.order[off];
         uint32_t v = g.order[off + 1];
 #pragma unroll 1
@@ -1901,6 +1904,20 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
             const uint32_t vn = k + 1 < cnt ? g.order[off + 2 + k] : NONE;
             fn(v, cnt);
             v = vn;
+        }
+    };
+    if constexpr (SORTED) {
+        uint32_t multi = 0;                                       // scheduled runs: classes >= 1
+#pragma unroll
+        for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
+        for (uint32_t j = tid; j < multi; j += stride) run(g.work[j]);
+        const uint32_t singles = g.cursor[SINGLE_WORD0 + q];
+        for (uint32_t j = tid; j < singles; j += stride) fn(g.single[j], 1u);
+    } else {
+        for (uint32_t j = tid; j < total; j += stride) {
+            const uint32_t e = *queue_entry(g, q, n, j);
+            if (e & SINGLE_RUN) fn(e & ~SINGLE_RUN, 1u);
+            else run(e);
         }
     }
 }

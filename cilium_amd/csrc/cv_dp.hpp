@@ -100,6 +100,8 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *ifx;             // per packet: the destination endpoint's ifindex (netdev path)
     unsigned long long *node1; // netdev path: one-word nodes {tag32 | head packet}, zeroed per
                                // launch (cap_mask + 1 words), or null (the epoch-tagged table)
+    uint32_t *single;          // the packets of singleton groups, dense (k_group_flatten with a
+                               // schedule; cursor[SINGLE_WORD0 + q] of them)
 };
 // GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
 // contention on one counter); blocks b with b % QSPLIT == k hold at most
@@ -121,6 +123,7 @@ __host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT +
 __host__ __device__ constexpr int qcls(int q, int c) { return CLS0 + (q * NCLASS + c) * 32; }
 constexpr int RUN_CURSOR = 3;
 constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (k_group_flatten)
+constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
 constexpr int EG_WORDS = 16;
 
 // flatten + schedule the groups of queue q (before the stage that runs them)

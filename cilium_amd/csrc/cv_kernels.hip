@@ -542,9 +542,9 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
 // in `order` (one block-aggregated allocation per 256 groups); the queue word is
 // replaced by the run's offset; per-class counts.  Block-uniform loop (the scans use
 // every lane).
-__global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q)
+__global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, bool dense)
 {
-    __shared__ uint32_t hist[NCLASS], wsum[BLOCK / 64], bbase;
+    __shared__ uint32_t hist[NCLASS], wsum[BLOCK / 64], ssum[BLOCK / 64], bbase, sbase;
     if (threadIdx.x < NCLASS) hist[threadIdx.x] = 0;
     uint32_t n[QSPLIT];
     const uint32_t total = queue_sizes(g, q, n);
@@ -570,22 +570,35 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q)
             }
             for (uint32_t y = x; y != NONE; y = g.next[y]) ++cnt;
         }
-        const uint32_t need = act ? cnt + 1 : 0;
+        const uint32_t need = act && cnt > 1 ? cnt + 1 : 0;      // singletons need no run
+        const bool one = act && cnt == 1;
         uint32_t incl = need;                                     // wave inclusive scan
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t t = __shfl_up(incl, d, 64);
             if (lane >= (uint32_t)d) incl += t;
         }
+        const unsigned long long ones = __ballot(one);            // singletons' rank in the wave
+        const uint32_t srank = __popcll(ones & ((1ull << lane) - 1));
         if (lane == 63) wsum[wv] = incl;
+        if (lane == 0) ssum[wv] = __popcll(ones);
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (int w = 0; w < BLOCK / 64; ++w) { const uint32_t t = wsum[w]; wsum[w] = acc; acc += t; }
+            uint32_t acc = 0, sacc = 0;
+            for (int w = 0; w < BLOCK / 64; ++w) {
+                const uint32_t t = wsum[w], u = ssum[w];
+                wsum[w] = acc; acc += t;
+                ssum[w] = sacc; sacc += u;
+            }
             bbase = acc ? atomicAdd(&g.cursor[RUN_CURSOR], acc) : 0;
+            sbase = dense && sacc ? atomicAdd(&g.cursor[SINGLE_WORD0 + q], sacc) : 0;
         }
         __syncthreads();
-        if (act) {
+        if (one) {                                                // no run: the packet itself
+            if (dense) g.single[sbase + ssum[wv] + srank] = head;
+            *ent = head | SINGLE_RUN;                             // (k_group_schedule skips it)
+            atomicAdd(&hist[0], 1u);
+        } else if (act) {
             const uint32_t off = bbase + wsum[wv] + incl - need;
             uint32_t *o = g.order + off;
             o[0] = cnt;
@@ -642,8 +655,9 @@ __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q,
 #pragma unroll
         for (int u = 0; u < SCHED_PER_THREAD; ++u) {
             const uint32_t j = base + u * BLOCK + threadIdx.x;
-            if (j < total) {
-                off[u] = *queue_entry(g, q, n, j);
+            off[u] = SINGLE_RUN;
+            if (j < total) off[u] = *queue_entry(g, q, n, j);
+            if (!(off[u] & SINGLE_RUN)) {                         // (singletons are not scheduled)
                 cls[u] = size_class(g.order[off[u]]);
                 rank[u] = atomicAdd(&lcnt[cls[u]], 1u);
             }
@@ -655,7 +669,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q,
 #pragma unroll
         for (int u = 0; u < SCHED_PER_THREAD; ++u) {
             const uint32_t j = base + u * BLOCK + threadIdx.x;
-            if (j < total) g.work[cbase[cls[u]] + lbase[cls[u]] + rank[u]] = off[u];
+            if (!(off[u] & SINGLE_RUN)) g.work[cbase[cls[u]] + lbase[cls[u]] + rank[u]] = off[u];
         }
         __syncthreads();
     }
@@ -663,7 +677,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q,
 
 void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_group_flatten, dim3(grid), dim3(BLOCK), 0, s, g, q);
+    hipLaunchKernelGGL(k_group_flatten, dim3(grid), dim3(BLOCK), 0, s, g, q, sched != 0);
     if (sched) hipLaunchKernelGGL(k_group_schedule, dim3(grid), dim3(BLOCK), 0, s, g, q, sched == 1);
 }
 

@@ -179,7 +179,7 @@ struct cv_ctx {
     cv_node_cfg node{};
     std::vector<Endpoint> eps;
     bool eps_dirty = true;
-    DevBuf eps_dev, ep_of_lxc;
+    DevBuf eps_dev, ephot_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gnode1, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
@@ -739,6 +739,7 @@ int sync_locked(cv_ctx *c)
     }
     if (eps_changed) {
         std::vector<EpDev> ev;
+        std::vector<EpHot> hot;
         std::vector<uint16_t> of(65536, 0);
         for (size_t i = 0; i < c->eps.size(); ++i) {
             const Endpoint &e = c->eps[i];
@@ -755,10 +756,17 @@ int sync_locked(cv_ctx *c)
             for (int j = 0; j < 4; ++j) d.ipv6[j] = e.ipv6[j];
             for (int j = 0; j < 2; ++j) { d.mac[j] = e.mac[j]; d.node_mac[j] = e.node_mac[j]; }
             ev.push_back(d);
+            EpHot h{d.policy.buckets, d.policy.vals, d.policy.aux, d.ct4.buckets, d.ct4.vals, d.ct4.live,
+                    (uint32_t)d.policy.mask, (uint32_t)d.ct4.mask, d.ipv4, d.ct_id};
+            if ((d.policy.buckets && d.policy.vstride != 32) || (d.ct4.buckets && d.ct4.vstride != 64) ||
+                d.policy.mask > 0xFFFFFFFFull || d.ct4.mask > 0xFFFFFFFFull)
+                return -EINVAL;                                   // (EpHot's fixed strides and 32-bit masks)
+            hot.push_back(h);
             of[e.lxc_id] = (uint16_t)(i + 1);
         }
-        if (ev.empty()) ev.push_back(EpDev{});
+        if (ev.empty()) { ev.push_back(EpDev{}); hot.push_back(EpHot{}); }
         r = c->eps_dev.upload(ev.data(), ev.size() * sizeof(EpDev));
+        if (!r) r = c->ephot_dev.upload(hot.data(), hot.size() * sizeof(EpHot));
         if (!r) r = c->ep_of_lxc.upload(of.data(), of.size() * 2);
         if (r) return r;
         c->eps_dirty = false;
@@ -780,6 +788,7 @@ DpParams params(cv_ctx *c)
     p.ipc4 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc4.view : Lpm4{nullptr, nullptr, HashTable{}};
     p.ipc6 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc6.view : Lpm6{};
     p.eps = c->eps_dev.as<EpDev>();
+    p.ephot = c->ephot_dev.as<EpHot>();
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
     p.lb4 = c->role[CV_ROLE_LB4_SERVICES] >= 0 ? c->lb4.view : HashTable{};

@@ -1467,6 +1467,23 @@ __device__ __forceinline__ void frame6_emit(const Frame6 &f, const uint8_t *in, 
 }
 
 // ------------------------------------------------------------------ endpoint ingress programs
+// The endpoint program's tables for the IPv4 conntrack stages from its EpHot line
+// (one 64-B read); the full EpDev where the event records need its constants or a
+// guarded launch needs the CT map's max_entries.
+template <bool FULL>
+__device__ __forceinline__ EpDev ep_stage4(const DpParams &p, uint32_t idx)
+{
+    if constexpr (FULL) return G(p.eps)[idx];
+    const EpHot h = G(p.ephot)[idx];
+    EpDev e{};
+    e.policy = HashTable{h.pol_buckets, h.pol_vals, h.pol_mask, 32u, (uint32_t)PolicySpec::SPB, h.pol_aux, nullptr, 0};
+    e.ct4 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, 64u, (uint32_t)Ct4Spec::SPB, nullptr, h.ct_live, 0};
+    if (p.ct_guard) e.ct4.cap = G(p.eps)[idx].ct4.cap;
+    e.ipv4 = h.ipv4;
+    e.ct_id = h.ct_id;
+    return e;
+}
+
 // After a lane changed conntrack buckets in place (create, delete) on a path that
 // reads them with plain loads (FRESH = false): drop this CU's L1 copy, so the lane's
 // next lookups see its own change (the atomics that made it bypass L1).

@@ -25,6 +25,21 @@ struct EpDev {                 // one endpoint program (bpf_lxc.c), its maps and
     uint32_t node_mac[2];      // NODE_MAC
 };
 
+// The fields the IPv4 conntrack stages read per packet, in one 64-B line per endpoint
+// (policy and CT4 tables; value strides are fixed: 32-B policy_entry slots, 64-B
+// ct_entry slots), so a lane reads one line instead of three table structs' fields.
+struct EpHot {
+    uint32_t *pol_buckets;
+    uint8_t *pol_vals;
+    unsigned long long *pol_aux;
+    uint32_t *ct_buckets;
+    uint8_t *ct_vals;
+    unsigned long long *ct_live;
+    uint32_t pol_mask, ct_mask;    // bucket counts - 1 (< 2^32)
+    uint32_t ipv4, ct_id;
+};
+static_assert(sizeof(EpHot) == 64, "one line per endpoint");
+
 struct DpParams {              // by value as the kernel argument
     uint32_t flags;
     uint32_t n_eps;
@@ -32,6 +47,7 @@ struct DpParams {              // by value as the kernel argument
     Lpm4 cidr4_dyn, ipc4;
     Lpm6 cidr6_dyn, ipc6;
     const EpDev *eps;
+    const EpHot *ephot;        // per endpoint, same index as eps
     const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
     unsigned long long *metrics;   // [256][4][2]
     // load balancer (lb.h): services and dense reverse-NAT tables indexed by the raw u16 key

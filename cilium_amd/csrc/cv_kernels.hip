@@ -331,8 +331,8 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             }
         }
         if (staged) {                                             // group by (CT map, address pair)
-            const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
-            group_insert1(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ep.ct_id << 17), i, Q_NETDEV);
+            const uint32_t ct_id = G(p.ephot)[smeta & 0xFFFFu].ct_id;
+            group_insert1(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ct_id << 17), i, Q_NETDEV);
         } else if (v6stage) {
             const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
             const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
@@ -373,7 +373,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 {
     const uint4 s0 = g.srec[2 * i], s1 = g.srec[2 * i + 1];
     const uint32_t meta = s1.z;
-    const EpDev ep = G(p.eps)[meta & 0xFFFFu];
+    const EpDev ep = ep_stage4<M::EV>(p, meta & 0xFFFFu);
     Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
@@ -505,9 +505,9 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
         const uint32_t mk = g.gslot[i];
         if (mk != COMMIT4 && mk != COMMIT6) continue;
         const uint4 s1 = g.srec[2 * i + 1];
-        const EpDev ep = G(p.eps)[s1.z & 0xFFFFu];
         uint32_t seen;
         if (mk == COMMIT4) {
+            const EpDev ep = ep_stage4<false>(p, s1.z & 0xFFFFu);
             const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
             Tuple4 t;
             t.nexthdr = s.nexthdr;
@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
             ct_l4<true>(t, s.h, CT_INGRESS, seen);
             t.reverse();
             const CtState sn{s.daddr[3] & 0xFFFFu, 0, 0, 0, 0, s1.w};
-            ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
+            ct_create<true>(G(p.eps)[s1.z & 0xFFFFu].ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
         }
     }
     __syncthreads();

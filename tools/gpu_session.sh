@@ -42,5 +42,9 @@ if [ "$PMC" = "pmc" ]; then
         -- python3 bench.py --workload "$W" --steps 3 --warmup 1 --no-cpu > "$OUT/pmc${i}_$W.log" 2>&1 \
         || { echo "pmc pass $i failed rc=$?"; tail -20 "$OUT/pmc${i}_$W.log"; exit 1; }
   done
+  step "pmc calibration (random 64-B lines)"
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_cal" -o run --output-format csv \
+      -- python3 tools/pmc_calibrate.py > "$OUT/pmc_cal.log" 2>&1 \
+      || { echo "pmc calibration failed rc=$?"; tail -20 "$OUT/pmc_cal.log"; exit 1; }
 fi
 step done

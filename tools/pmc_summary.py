@@ -40,16 +40,22 @@ def main():
     shutil.copy(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv"), os.path.join(dst, f"{w}_kernel_stats.csv"))
     shutil.copy(os.path.join(src, f"bench_{w}.json"), os.path.join(dst, f"bench_{w}.json"))
     kname = DOMINANT[w]
-    ctr = {}
+    setup = ("k_ct_load", "k_ct_scan", "k_ct_op", "k_ct_gc")      # table loads / map API, not the step
+    ctr, step = {}, defaultdict(float)
     for i in (1, 2, 3):
         p = os.path.join(src, f"pmc{i}_{w}", "run_counter_collection.csv")
         for name, cs in per_kernel(p).items():
+            if not name.startswith(("cv::", "void cv::")) or any(f"::{x}(" in name for x in setup):
+                continue
+            for c, v in cs.items():
+                step[c] += sum(v)                                 # every dispatch of the step's kernels
             if f"::{kname}(" in name:
                 for c, v in cs.items():
                     # config 5's v6 launch also runs the v4 stage kernels on empty
                     # queues: such near-empty dispatches are not launches of the path
                     v = [x for x in v if x >= 0.01 * max(v)] or v
                     ctr[c] = (sum(v) / len(v), len(v))
+    steps = ctr["FETCH_SIZE"][1]                                  # one dominant-kernel launch per step
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv")))}
     avg_ns = next(float(r["AverageNs"]) for n, r in stats.items() if f"::{kname}(" in n)
     tp = os.path.join(src, f"stats_{w}", "run_kernel_trace.csv")
@@ -65,13 +71,24 @@ def main():
     sha = build.kernel_sha()
     out = {
         "workload": w, "kernel": kname, "tag": tag, "kernel_sha": sha,
-        "dispatches_per_pass": ctr["FETCH_SIZE"][1],
+        "dispatches_per_pass": steps,
         "rocprof_avg_kernel_ns": avg_ns,
         "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
         "TCC_HIT_sum": hit, "TCC_MISS_sum": miss, "l2_hit_rate": round(hit / (hit + miss), 4),
         "hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
-        "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section); memory-side bytes incl. Infinity-Cache hits",
+        "step_FETCH_SIZE_KiB": step["FETCH_SIZE"] / steps, "step_WRITE_SIZE_KiB": step["WRITE_SIZE"] / steps,
+        "hbm_bytes_per_step": int((2 * step["FETCH_SIZE"] + step["WRITE_SIZE"]) * 1024 / steps),
+        "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section); memory-side bytes incl. "
+                      "Infinity-Cache hits; per launch of the dominant kernel, and per step = every cv:: kernel "
+                      "of the step (table loads excluded) / steps in the pass",
     }
+    cal = os.path.join(src, "pmc_cal", "run_counter_collection.csv")
+    if os.path.exists(cal):                                       # known bytes / counter, random 64-B lines
+        fs = [v for cs in per_kernel(cal).values() for v in cs.get("FETCH_SIZE", [])]
+        if fs:
+            out["fetch_calibration_random64"] = round((1 << 26) * 64 / (max(fs) * 1024), 3)
+            out["hbm_bytes_per_step_calibrated"] = int((out["fetch_calibration_random64"] * step["FETCH_SIZE"]
+                                                        + step["WRITE_SIZE"]) * 1024 / steps)
     json.dump(out, open(os.path.join(ROOT, "profiles", f"pmc_{w}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 

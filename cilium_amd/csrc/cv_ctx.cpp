@@ -611,13 +611,13 @@ int compile_ct_t(cv_ctx *c, MapObj *mo, uint32_t ks, int kind)
     DevHash &d = mo->ct;
     const uint64_t nb = buckets_for(std::max<uint64_t>(m->max_entries, n), S::SPB);
     int r = d.buckets.alloc(nb * S::BW * 4);
-    if (!r) r = d.vals.alloc(nb * S::SPB * 64);
+    if (!r) r = d.vals.alloc(nb * S::SPB * CT_COLD);          // side slots (the hot words sit in the buckets)
     if (!r) r = mo->live.alloc(8);
     if (r) return r;
     if (hipMemset(d.buckets.p, 0, d.buckets.n) != hipSuccess || hipMemset(d.vals.p, 0, d.vals.n) != hipSuccess)
         return -EIO;
     d.nb = nb;
-    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, 64, (uint32_t)S::SPB, nullptr,
+    d.view = HashTable{d.buckets.as<uint32_t>(), d.vals.as<uint8_t>(), nb - 1, CT_COLD, (uint32_t)S::SPB, nullptr,
                        mo->live.as<unsigned long long>(), m->max_entries};
     if (n) {
         std::vector<uint32_t> kw((size_t)n * S::KW, 0), vw((size_t)n * 16, 0);
@@ -758,7 +758,7 @@ int sync_locked(cv_ctx *c)
             ev.push_back(d);
             EpHot h{d.policy.buckets, d.policy.vals, d.policy.aux, d.ct4.buckets, d.ct4.vals, d.ct4.live,
                     (uint32_t)d.policy.mask, (uint32_t)d.ct4.mask, d.ipv4, d.ct_id};
-            if ((d.policy.buckets && d.policy.vstride != 32) || (d.ct4.buckets && d.ct4.vstride != 64) ||
+            if ((d.policy.buckets && d.policy.vstride != 32) || (d.ct4.buckets && d.ct4.vstride != CT_COLD) ||
                 d.policy.mask > 0xFFFFFFFFull || d.ct4.mask > 0xFFFFFFFFull)
                 return -EINVAL;                                   // (EpHot's fixed strides and 32-bit masks)
             hot.push_back(h);

@@ -699,21 +699,82 @@ struct CtState {
     uint32_t addr, svc_addr, src_sec_id;
 };
 
-__device__ __forceinline__ void ct_load(const HashTable &t, int64_t slot, CtE &e)
+// Storage of a struct ct_entry (CtE words: w0-7 rx/tx packets/bytes as u64 pairs,
+// w8 lifetime, w9 flags | rev_nat << 16, w10 slave | tx/rx_flags_seen, w11 src_sec_id,
+// w12/w13 last tx/rx report, w14/15 the slot padding k_nat_apply tags).  A lookup hit
+// touches the hot half, kept in the bucket right after the slot's key (CT_HOTW words:
+// w8-w13 and the low words of the four counters), so the key and the entry share
+// one line; the counters' high words and w14/15 sit in a 32-B side slot, written
+// only when a low word carries, at a create, or by the map API.
+
+template <class S>
+__device__ __forceinline__ CV_G uint32_t *ct_hot(const HashTable &t, int64_t slot)
 {
-    const CV_G uint4 *q = reinterpret_cast<const CV_G uint4 *>(G(t.vals) + (size_t)slot * t.vstride);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint4 v = q[k];
-        e.w[4 * k] = v.x; e.w[4 * k + 1] = v.y; e.w[4 * k + 2] = v.z; e.w[4 * k + 3] = v.w;
-    }
+    static_assert(S::KS >= S::KW + CT_HOTW, "slot holds the hot words");
+    return G(t.buckets) + (uint64_t)slot / S::SPB * S::BW + S::KEY0 + (uint32_t)((uint64_t)slot % S::SPB) * S::KS +
+           S::KW;
 }
 
-__device__ __forceinline__ void ct_store(const HashTable &t, int64_t slot, const CtE &e)
+template <class S>
+__device__ __forceinline__ CV_G uint32_t *ct_cold(const HashTable &t, int64_t slot)
 {
-    CV_G uint4 *q = reinterpret_cast<CV_G uint4 *>(G(t.vals) + (size_t)slot * t.vstride);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = make_uint4(e.w[4 * k], e.w[4 * k + 1], e.w[4 * k + 2], e.w[4 * k + 3]);
+    return reinterpret_cast<CV_G uint32_t *>(G(t.vals) + (size_t)slot * CT_COLD);
+}
+
+// hot words <-> CtE (the hot run is 8-B aligned: KEY0, KW and KS are even)
+template <class S>
+__device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, CtE &e)
+{
+    const CV_G uint2 *h = reinterpret_cast<const CV_G uint2 *>(ct_hot<S>(t, slot));
+    const uint2 a = h[0], b = h[1], c = h[2], d = h[3], f = h[4];
+    e.w[8] = a.x; e.w[9] = a.y; e.w[10] = b.x; e.w[11] = b.y; e.w[12] = c.x; e.w[13] = c.y;
+    e.w[0] = d.x; e.w[2] = d.y; e.w[4] = f.x; e.w[6] = f.y;
+}
+
+template <class S>
+__device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, const CtE &e)
+{
+    CV_G uint2 *h = reinterpret_cast<CV_G uint2 *>(ct_hot<S>(t, slot));
+    h[0] = make_uint2(e.w[8], e.w[9]);
+    h[1] = make_uint2(e.w[10], e.w[11]);
+    h[2] = make_uint2(e.w[12], e.w[13]);
+    h[3] = make_uint2(e.w[0], e.w[2]);
+    h[4] = make_uint2(e.w[4], e.w[6]);
+}
+
+template <class S>
+__device__ __forceinline__ void ct_load(const HashTable &t, int64_t slot, CtE &e)
+{
+    ct_load_hot<S>(t, slot, e);
+    const CV_G uint4 *c = reinterpret_cast<const CV_G uint4 *>(ct_cold<S>(t, slot));
+    const uint4 u = c[0], v = c[1];
+    e.w[1] = u.x; e.w[3] = u.y; e.w[5] = u.z; e.w[7] = u.w;
+    e.w[14] = v.x; e.w[15] = v.y;
+}
+
+// cold_known_zero: the slot was just claimed (free slots hold zero side words, see
+// dev_kill and k_ct_gc) and e's cold words are zero, so only the bucket line changes
+template <class S>
+__device__ __forceinline__ void ct_store(const HashTable &t, int64_t slot, const CtE &e, bool cold_known_zero = false)
+{
+    ct_store_hot<S>(t, slot, e);
+    if (cold_known_zero && !(e.w[1] | e.w[3] | e.w[5] | e.w[7] | e.w[14] | e.w[15])) return;
+    CV_G uint4 *c = reinterpret_cast<CV_G uint4 *>(ct_cold<S>(t, slot));
+    c[0] = make_uint4(e.w[1], e.w[3], e.w[5], e.w[7]);
+    c[1] = make_uint4(e.w[14], e.w[15], 0u, 0u);
+}
+
+// counter k (0 rx_packets, 2 rx_bytes, 4 tx_packets, 6 tx_bytes) += v on an entry whose
+// hot words are loaded: the low word in place, a carry into the side slot's high word
+template <class S>
+__device__ __forceinline__ void ct_count(const HashTable &t, int64_t slot, CtE &e, int k, uint32_t v)
+{
+    const uint32_t lo = e.w[k] + v;
+    if (lo < e.w[k]) {
+        CV_G uint32_t *hi = ct_cold<S>(t, slot) + (k >> 1);
+        *hi = *hi + 1u;
+    }
+    e.w[k] = lo;
 }
 
 // __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)
@@ -793,6 +854,7 @@ enum { ACTION_UNSPEC = 0, ACTION_CREATE = 1, ACTION_CLOSE = 2 };
 // __ct_lookup (conntrack.h:199-263) -> CT_NEW / CT_ESTABLISHED; *slot = hit slot;
 // a hit fills ct_state's rev_nat_index / loopback / slave
 // the entry update of a __ct_lookup hit (conntrack.h:213-258)
+template <class S>
 __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
                                        uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a,
                                        bool *mon = nullptr);
@@ -810,18 +872,20 @@ __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, in
         if (mon) *mon = true;
         return CT_NEW;
     }
-    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
+    ct_hit<typename T::Spec>(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
     return CT_ESTABLISHED;
 }
 
 // *mon: the `monitor` output of __ct_lookup (report requested), left as is when the
-// reference leaves it (a dead entry on a plain lookup)
+// reference leaves it (a dead entry on a plain lookup).  Reads and writes the hot
+// words only (the bucket line the lookup just read).
+template <class S>
 __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
                                        uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a, bool *mon)
 {
     a.nu++;
     CtE e;
-    ct_load(ct, slot, e);
+    ct_load_hot<S>(ct, slot, e);
     bool m = mon ? *mon : false;
     if (ct_alive(e)) m = ct_timeout(e, tcp, dir, seen, now);
     if (st) {
@@ -830,8 +894,8 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         st->slave = e.w[10] & 0xFFFFu;
     }
     if (flags & F_CT_ACCOUNTING) {
-        if (dir == CT_INGRESS) { e.add64(0, 1); e.add64(2, len); }
-        else                   { e.add64(4, 1); e.add64(6, len); }
+        if (dir == CT_INGRESS) { ct_count<S>(ct, slot, e, 0, 1u); ct_count<S>(ct, slot, e, 2, len); }
+        else                   { ct_count<S>(ct, slot, e, 4, 1u); ct_count<S>(ct, slot, e, 6, len); }
     }
     if (action == ACTION_CREATE) {
         if ((e.bits() & CTB_RX_CLOSING) || (e.bits() & CTB_TX_CLOSING)) {
@@ -844,7 +908,7 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
     }
     if (mon) *mon = m;
-    ct_store(ct, slot, e);
+    ct_store_hot<S>(ct, slot, e);
 }
 
 __device__ __forceinline__ uint8_t dir_flags(int dir)
@@ -920,7 +984,7 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     a.nl++;
     slot = probe_end<S, FRESH>(p1, ct, k1, nullptr);
     if (slot >= 0) {
-        ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
+        ct_hit<S>(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
         return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
     }
     if (mon) *mon = true;                                         // the first __ct_lookup missed
@@ -929,7 +993,7 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     a.nl++;
     slot = probe_end<S, FRESH>(p2, ct, k2, nullptr);
     if (slot < 0) return CT_NEW;
-    ct_hit(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
+    ct_hit<S>(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
     return CT_ESTABLISHED;
 }
 
@@ -960,7 +1024,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
     const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent);
     if (s < 0) return false;
     if (created) ct_live_add(ct, a, guard, 1);
-    ct_store(ct, s, e);
+    ct_store<typename T::Spec>(ct, s, e, created);
     return true;
 }
 
@@ -1477,7 +1541,8 @@ __device__ __forceinline__ EpDev ep_stage4(const DpParams &p, uint32_t idx)
     const EpHot h = G(p.ephot)[idx];
     EpDev e{};
     e.policy = HashTable{h.pol_buckets, h.pol_vals, h.pol_mask, 32u, (uint32_t)PolicySpec::SPB, h.pol_aux, nullptr, 0};
-    e.ct4 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, 64u, (uint32_t)Ct4Spec::SPB, nullptr, h.ct_live, 0};
+    e.ct4 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, (uint32_t)CT_COLD, (uint32_t)Ct4Spec::SPB, nullptr, h.ct_live,
+                      0};
     if (p.ct_guard) e.ct4.cap = G(p.eps)[idx].ct4.cap;
     e.ipv4 = h.ipv4;
     e.ct_id = h.ct_id;

@@ -26,8 +26,8 @@ struct EpDev {                 // one endpoint program (bpf_lxc.c), its maps and
 };
 
 // The fields the IPv4 conntrack stages read per packet, in one 64-B line per endpoint
-// (policy and CT4 tables; value strides are fixed: 32-B policy_entry slots, 64-B
-// ct_entry slots), so a lane reads one line instead of three table structs' fields.
+// (policy and CT4 tables; value strides are fixed: 32-B policy_entry slots, 32-B
+// ct_entry side slots), so a lane reads one line instead of three table structs' fields.
 struct EpHot {
     uint32_t *pol_buckets;
     uint8_t *pol_vals;

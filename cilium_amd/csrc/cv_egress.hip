@@ -322,9 +322,9 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         const int64_t s2 = dev_find<Ct4Spec, EGF>(ep.ct4, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
-            ct_load(ep.ct4, s2, e);
+            ct_load_hot<Ct4Spec>(ep.ct4, s2, e);                  // (w10: a hot word)
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
-            ct_store(ep.ct4, s2, e);
+            ct_store_hot<Ct4Spec>(ep.ct4, s2, e);
             a.nu++;
         }
     }
@@ -428,9 +428,9 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         const int64_t s2 = dev_find<Ct6Spec, EGF>(ep.ct6, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
-            ct_load(ep.ct6, s2, e);
+            ct_load_hot<Ct6Spec>(ep.ct6, s2, e);
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
-            ct_store(ep.ct6, s2, e);
+            ct_store_hot<Ct6Spec>(ep.ct6, s2, e);
             a.nu++;
         }
     }
@@ -583,7 +583,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
                 const int64_t sl = dev_find<Ct4Spec, false>(ep.ct4, k, nullptr);   // (no CT writes here)
                 if (sl >= 0) {
                     CtE e;
-                    ct_load(ep.ct4, sl, e);
+                    ct_load_hot<Ct4Spec>(ep.ct4, sl, e);
                     uint32_t na4, np;
                     if ((e.w[9] >> 16) && revnat4(p, e.w[9] >> 16, na4, np, na)) {
                         const bool lb = e.bits() & CTB_LB_LOOPBACK;
@@ -610,7 +610,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
                 const int64_t sl = dev_find<Ct6Spec, false>(ep.ct6, k, nullptr);
                 if (sl >= 0) {
                     CtE e;
-                    ct_load(ep.ct6, sl, e);
+                    ct_load_hot<Ct6Spec>(ep.ct6, sl, e);
                     uint32_t na6[4], np;
                     if ((e.w[9] >> 16) && revnat6(p, e.w[9] >> 16, na6, np, na)) {
                         uf_union(g, P, group_node(g, pair_hash6(na6, x.s.daddr, SALT_CT6)));
@@ -1016,11 +1016,11 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
             const int64_t sl = dev_upsert<Ct4Spec>(ep.ct4, k, &created);
             if (sl < 0) continue;                                 // (probe limit; launches are planned with room)
             if (created && ep.ct4.live) pol_add(&pc, ep.ct4.live, 1ull);
-            uint32_t *v = reinterpret_cast<uint32_t *>(ep.ct4.vals + (size_t)sl * ep.ct4.vstride);
-            if (!created && v[15] == g.serial && v[14] > x) continue;
+            const CV_G uint32_t *v = ct_cold<Ct4Spec>(ep.ct4, sl);  // w14 / w15: side words 4 / 5
+            if (!created && v[5] == g.serial && v[4] > x) continue;
             e.w[14] = x;
             e.w[15] = g.serial;
-            ct_store(ep.ct4, sl, e);
+            ct_store<Ct4Spec>(ep.ct4, sl, e, created);
         }
     });
     __syncthreads();

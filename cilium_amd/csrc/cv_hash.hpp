@@ -6,7 +6,9 @@
 // (0 empty, 1 dead, 2 busy, 3..255 hash fingerprint); then SPB keys of KW words;
 // then SPB inline values of IVW words, or of one 16-bit halfword each (IVH = 1, the
 // policy table's proxy_port).  Larger values live in a side array indexed
-// by slot (bucket * SPB + slot) with a fixed byte stride.  Tag 2 marks a slot a
+// by slot (bucket * SPB + slot) with a fixed byte stride.  Conntrack buckets (KS >
+// KW) interleave each slot's key with the hot words of its entry (cv_dev.hpp
+// ct_hot), so a hit reads one line.  Tag 2 marks a slot a
 // device thread is claiming (skipped by lookups, never matched).  Linear probing over
 // buckets; a lookup ends at the first bucket holding an empty slot, so one probe
 // is one line read in the common case.  The same code runs on the host (table
@@ -31,10 +33,11 @@ struct HashTable {            // POD view, passed by value to kernels
     uint64_t  cap;            // conntrack maps: max_entries (a create past it fails, -E2BIG)
 };
 
-template <int KW_, int IVW_, int SPB_, int BW_, int IVH_ = 0, int SYM_ = 0>
+template <int KW_, int IVW_, int SPB_, int BW_, int IVH_ = 0, int SYM_ = 0, int KS_ = 0>
 struct HashSpec {
     static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_, IVH = IVH_, SYM = SYM_;
-    static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KW, HVAL0 = 2 * IVAL0;   // HVAL0 in halfwords
+    static constexpr int KS = KS_ ? KS_ : KW_;                   // words from one slot's key to the next
+    static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KS, HVAL0 = 2 * IVAL0;   // HVAL0 in halfwords
     static_assert(IVAL0 + SPB * IVW <= BW, "bucket overflow");
     static_assert(IVH == 0 || (IVW == 0 && IVH == 1 && HVAL0 + SPB <= 2 * BW), "halfword values");
     static_assert(SPB <= 8, "eight tag bytes");
@@ -47,8 +50,10 @@ using LxcV6Spec  = HashSpec<4, 1, 6, 32>;
 using Cidr4Spec  = HashSpec<1, 0, 8, 16>;   // /32 deny set (v4_fix)
 using Cidr6Spec  = HashSpec<4, 0, 7, 32>;   // /128 deny set (v6_fix)
 using PolicySpec = HashSpec<2, 0, 5, 16, 1>; // policy_key (8 B) -> inline proxy_port; side array policy_entry (stride 32)
-using Ct4Spec    = HashSpec<4, 0, 7, 32, 0, 1>;   // ipv4_ct_tuple (14 B + 2 zero) -> side array ct_entry (stride 64)
-using Ct6Spec    = HashSpec<10, 0, 3, 32, 0, 1>;  // ipv6_ct_tuple (40 B) -> side array ct_entry (stride 64)
+// conntrack: {key, 10 hot words of struct ct_entry} per slot, the rest in 32-B side slots
+using Ct4Spec    = HashSpec<4, 0, 2, 32, 0, 1, 14>;   // ipv4_ct_tuple (14 B + 2 zero): 2 slots per 128 B
+using Ct6Spec    = HashSpec<10, 0, 3, 64, 0, 1, 20>;  // ipv6_ct_tuple (40 B): 3 slots per 256 B
+constexpr int CT_HOTW = 10, CT_COLD = 32;   // hot words per CT slot; bytes per CT side slot
 using Lb4Spec    = HashSpec<2, 3, 6, 32>;   // lb4_key (8 B) -> lb4_service (12 B) inline
 using Lb6Spec    = HashSpec<5, 6, 4, 64>;   // lb6_key (20 B) -> lb6_service (24 B) inline
 using Lpm6Spec   = HashSpec<5, 1, 5, 32>;   // (masked v6 addr, plen) -> value
@@ -107,7 +112,7 @@ CV_HD int match_bucket(const uint32_t *w, const uint32_t *key, uint32_t tag, boo
         empty |= (t == TAG_EMPTY);
         bool eq = (t == tag);
 #pragma unroll
-        for (int j = 0; j < S::KW; ++j) eq &= (w[S::KEY0 + s * S::KW + j] == key[j]);
+        for (int j = 0; j < S::KW; ++j) eq &= (w[S::KEY0 + s * S::KS + j] == key[j]);
         hit = eq ? s : hit;
     }
     *stop = empty;
@@ -200,7 +205,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
         while (match) {
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
-            const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KW;
+            const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KS;
             const bool eq = key_eq<S, FRESH>(kw, key);
             if (eq) {
 #pragma unroll
@@ -455,7 +460,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
         while (match) {
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
-            const CV_G uint32_t *kw = pr.bw + S::KEY0 + sl * S::KW;
+            const CV_G uint32_t *kw = pr.bw + S::KEY0 + sl * S::KS;
             const bool eq = key_eq<S, FRESH>(kw, key);
             if (eq) {
 #pragma unroll
@@ -491,7 +496,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
             while (match) {
                 const int sl = (__builtin_ctzll(match) >> 3);
                 match &= match - 1;
-                const CV_G uint32_t *kw = nx.bw + S::KEY0 + sl * S::KW;
+                const CV_G uint32_t *kw = nx.bw + S::KEY0 + sl * S::KS;
                 const bool eq = key_eq<S, FRESH>(kw, key);
                 if (eq) {
 #pragma unroll
@@ -576,7 +581,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
         while (!known_absent && match) {
             const int sl = (__builtin_ctzll(match) >> 3);
             match &= match - 1;
-            const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KW;
+            const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KS;
             const bool eq = key_eq<S>(kw, key);
             if (eq) return (int64_t)(b * S::SPB + sl);
         }
@@ -601,7 +606,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
         if (claim_in_word(bw, (uint32_t)cur, 0, S::SPB < 4 ? S::SPB : 4, tag, got) ||
             (S::SPB > 4 && claim_in_word(bw + 1, (uint32_t)(cur >> 32), 4, S::SPB - 4, tag, got))) {
 #pragma unroll
-            for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + got * S::KW + j] = key[j];
+            for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + got * S::KS + j] = key[j];
             *created = true;
             return (int64_t)(b * S::SPB + got);
         }
@@ -625,8 +630,8 @@ __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
     CV_G uint32_t *tw = G(t.buckets) + b * S::BW + (s >> 2);
     const int sh = 8 * (s & 3);
 #pragma unroll
-    for (int j = 0; j < S::KW; ++j)
-        __hip_atomic_exchange(G(t.buckets) + b * S::BW + S::KEY0 + s * S::KW + j, 0u, __ATOMIC_RELAXED,
+    for (int j = 0; j < S::KS; ++j)                               // the key, and a CT slot's hot words
+        __hip_atomic_exchange(G(t.buckets) + b * S::BW + S::KEY0 + s * S::KS + j, 0u, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
     if (t.vals) {
         CV_G unsigned long long *v = reinterpret_cast<CV_G unsigned long long *>(G(t.vals) + (size_t)slot * t.vstride);
@@ -686,7 +691,7 @@ inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *iv
     uint64_t fb = (uint64_t)free_slot / S::SPB;
     int q = (int)((uint64_t)free_slot % S::SPB);
     uint32_t *w = host_bucket<S>(t, fb);
-    for (int j = 0; j < S::KW; ++j) w[S::KEY0 + q * S::KW + j] = key[j];
+    for (int j = 0; j < S::KW; ++j) w[S::KEY0 + q * S::KS + j] = key[j];
     host_set_ival<S>(w, q, ival);
     uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
     tags = (tags & ~(0xFFULL << (8 * q))) | ((uint64_t)tag << (8 * q));

@@ -698,7 +698,7 @@ __device__ void ct_op(HashTable t, int op, uint64_t flags, uint32_t *io)
         if (s < 0) rc = -ENOENT;
         else {
             CtE e;
-            ct_load(t, s, e);
+            ct_load<S>(t, s, e);
             for (int k = 0; k < 16; ++k) val[k] = e.w[k];
         }
     } else if (op == 1) {
@@ -713,7 +713,7 @@ __device__ void ct_op(HashTable t, int op, uint64_t flags, uint32_t *io)
                 if (created && t.live) atomicAdd(t.live, 1ull);
                 CtE e;
                 for (int k = 0; k < 16; ++k) e.w[k] = val[k];
-                ct_store(t, s, e);
+                ct_store<S>(t, s, e);
             }
         }
     } else {
@@ -753,7 +753,7 @@ __device__ void ct_load_t(HashTable t, const uint32_t *keys, const uint32_t *val
             const uint4 v = q[w];
             e.w[4 * w] = v.x; e.w[4 * w + 1] = v.y; e.w[4 * w + 2] = v.z; e.w[4 * w + 3] = v.w;
         }
-        ct_store(t, sl, e);
+        ct_store<S>(t, sl, e, created);
     }
 }
 
@@ -789,9 +789,10 @@ __device__ void ct_scan(HashTable t, uint64_t nslots, uint64_t *slots, uint32_t 
         const uint32_t at = atomicAdd(count, 1u);
         if (at >= max) continue;
         if (slots) slots[at] = x;
-        for (int j = 0; j < S::KW; ++j) keys[(size_t)at * S::KW + j] = bw[S::KEY0 + sl * S::KW + j];
-        const uint32_t *v = reinterpret_cast<const uint32_t *>(t.vals + x * t.vstride);
-        for (int j = 0; j < 16; ++j) vals[(size_t)at * 16 + j] = v[j];
+        for (int j = 0; j < S::KW; ++j) keys[(size_t)at * S::KW + j] = bw[S::KEY0 + sl * S::KS + j];
+        CtE e;
+        ct_load<S>(t, (int64_t)x, e);
+        for (int j = 0; j < 16; ++j) vals[(size_t)at * 16 + j] = e.w[j];
     }
 }
 
@@ -818,11 +819,13 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
         for (int sl = 0; sl < S::SPB; ++sl) {
             const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
             if (tag < 3) continue;
-            const uint32_t life = *reinterpret_cast<const uint32_t *>(t.vals + (b * S::SPB + sl) * t.vstride + 32);
+            const uint32_t life = *ct_hot<S>(t, (int64_t)(b * S::SPB + sl));   // lifetime: hot word 0
             if (life < time) {
                 out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
 #pragma unroll
-                for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + sl * S::KW + j] = 0;   // free slots hold zero keys
+                for (int j = 0; j < S::KS; ++j) bw[S::KEY0 + sl * S::KS + j] = 0;   // free slots hold zero keys,
+                uint4 *c = reinterpret_cast<uint4 *>(t.vals + (b * S::SPB + sl) * CT_COLD);   // hot and side words
+                c[0] = c[1] = make_uint4(0, 0, 0, 0);
                 ++mine;
             }
         }

@@ -956,7 +956,10 @@ __device__ __forceinline__ int ct_l4(T &t, const L4Hdr &h, int dir, uint32_t &se
 // Both lookup keys are known before the first probe, so the reverse-direction
 // probe is issued together with the first one (its result is used only when the
 // first misses, as the reference's second __ct_lookup).
-template <bool V6, bool FRESH = true, class T>
+// ONE: a single call site for the entry update (the lanes of a wave take different
+// branches; the update's loads and stores then issue once for all of them): measured
+// 7 % faster in the IPv6 egress stage, 2 % slower in the netdev policy stage.
+template <bool V6, bool FRESH = true, bool ONE = false, class T>
 __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr &h, int dir, uint32_t len,
                                          uint32_t now, uint32_t flags, int64_t &slot, CtState *st, Acct &a,
                                          bool *mon = nullptr)
@@ -983,6 +986,20 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     }
     a.nl++;
     slot = probe_end<S, FRESH>(p1, ct, k1, nullptr);
+    if constexpr (ONE) {
+        const bool first = slot >= 0;
+        if (!first) {
+            if (mon) *mon = true;                                 // the first __ct_lookup missed
+            if (dir == CT_SERVICE) return CT_NEW;
+            t = t2;
+            a.nl++;
+            slot = probe_end<S, FRESH>(p2, ct, k2, nullptr);
+            if (slot < 0) return CT_NEW;
+        }
+        ct_hit<S>(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
+        if (!first) return CT_ESTABLISHED;
+        return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+    }
     if (slot >= 0) {
         ct_hit<S>(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
         return (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;

@@ -864,7 +864,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     Probe<LxcV6Spec> lxq;                                         // endpoint lookup of daddr, issued early
     if (p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
     bool mon = false;
-    int ret = ct_lookup<true, EGF>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
+    int ret = ct_lookup<true, EGF, true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
     uint32_t iv;
     bool lxc_hit = false;

@@ -668,7 +668,6 @@ __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q,
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < SCHED_PER_THREAD; ++u) {
-            const uint32_t j = base + u * BLOCK + threadIdx.x;
             if (!(off[u] & SINGLE_RUN)) g.work[cbase[cls[u]] + lbase[cls[u]] + rank[u]] = off[u];
         }
         __syncthreads();

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libcilium_hip.so")
-SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip"]
+SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip", "cv_agent.cpp"]
 ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 
 

@@ -1,4 +1,4 @@
-"""ctypes binding of the product library (include/cilium_hip.h).
+"""ctypes binding of the product library (include/cilium_hip.h, include/cilium_agent.h).
 
 The library is the HIP path; there is no CPU fallback.  ``load()`` raises when
 ``cilium_amd/_lib/libcilium_hip.so`` is missing (build it with
@@ -16,6 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CV_LIB") or os.path.join(HERE, "_lib", "libcilium_hip.so")   # CV_LIB: A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "cilium_hip.h")
+HEADERS = [HEADER, os.path.join(os.path.dirname(HERE), "include", "cilium_agent.h")]
 
 MAP_HASH, MAP_LRU_HASH, MAP_LPM_TRIE, MAP_PERCPU_HASH = 1, 9, 11, 5
 BPF_F_NO_PREALLOC = 1
@@ -64,10 +65,12 @@ def _raw_be32(v):
 
 
 def header_functions():
-    """Names of the functions include/cilium_hip.h declares."""
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(cv_[a-z0-9_]+)\s*\(", src)))
+    """Names of the functions include/*.h declare."""
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(cv_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def load():
@@ -109,6 +112,18 @@ def load():
         "cv_metrics_attach": (i32, [vp, vp]),
         "cv_notify_attach": (i32, [vp, vp, u32, vp]),
         "cv_trace_attach": (i32, [vp, vp, u32, vp, u32, u32]),
+        "cv_prefilter_new": (i32, [vp, u32, C.POINTER(vp)]),
+        "cv_prefilter_free": (None, [vp]),
+        "cv_prefilter_insert": (i32, [vp, C.c_int64, vp, u32, C.c_char_p, u32]),
+        "cv_prefilter_delete": (i32, [vp, C.c_int64, vp, u32, C.c_char_p, u32]),
+        "cv_prefilter_dump": (i32, [vp, vp, u32, C.POINTER(C.c_int64)]),
+        "cv_prefilter_write_config": (i32, [vp, C.c_char_p, u32]),
+        "cv_prefilter_map": (i32, [vp, i32]),
+        "cv_policy_sync_new": (i32, [C.POINTER(vp)]),
+        "cv_policy_sync_free": (None, [vp]),
+        "cv_policy_sync_set_desired": (i32, [vp, vp, vp, u32]),
+        "cv_policy_sync_run": (i32, [vp, vp, i32, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]),
+        "cv_policy_sync_realized": (i32, [vp, vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("CV_LIB") and not hasattr(L, name):
@@ -358,3 +373,120 @@ class Ctx:
         out = rec[: min(n, cap) * DROP_NOTIFY.itemsize].cpu().numpy().view(DROP_NOTIFY).copy()
         cnt.zero_()
         return out, n
+
+
+# ---------------------------------------------------------------- agent side (include/cilium_agent.h)
+PF_V4_DYN, PF_V4_FIX, PF_V6_DYN, PF_V6_FIX = 0, 1, 2, 3
+PF_DYN4, PF_FIX4, PF_DYN6, PF_FIX6 = 1, 2, 4, 8
+PF_DEFAULT = PF_FIX4 | PF_FIX6
+
+
+class Cidr(C.Structure):
+    _fields_ = [("family", C.c_uint8), ("prefixlen", C.c_uint8), ("pad", C.c_uint8 * 2), ("addr", C.c_uint8 * 16)]
+
+
+def cidrs_to_c(cidrs):
+    """["10.0.0.0/8", "fd00::/64", ...] (net.ParseCIDR's network addresses) -> cv_cidr[]"""
+    import ipaddress
+    arr = (Cidr * max(len(cidrs), 1))()
+    for i, c in enumerate(cidrs):
+        net = ipaddress.ip_network(c, strict=False)
+        arr[i].family = net.version
+        arr[i].prefixlen = net.prefixlen
+        raw = net.network_address.packed
+        for j, b in enumerate(raw):
+            arr[i].addr[j] = b
+    return arr
+
+
+def cidr_str(c):
+    import ipaddress
+    raw = bytes(c.addr[:4] if c.family == 4 else c.addr[:16])
+    a = ipaddress.ip_address(raw)
+    return f"{a}/{c.prefixlen}"
+
+
+class PreFilter:
+    """pkg/policy/prefilter.go's PreFilter over the engine (cv_prefilter_*): Insert /
+    Delete raise CvError with the reference's message on failure."""
+
+    def __init__(self, ctx, config=PF_DEFAULT):
+        self.L, self.ctx = load(), ctx
+        h = C.c_void_p()
+        _check(self.L.cv_prefilter_new(ctx.h, config, C.byref(h)), "cv_prefilter_new")
+        self.h = h
+
+    def _op(self, fn, revision, cidrs):
+        arr = cidrs_to_c(cidrs)
+        err = C.create_string_buffer(512)
+        rc = fn(self.h, revision, arr, len(cidrs), err, 512)
+        if rc < 0:
+            raise CvError(-rc, err.value.decode())
+
+    def insert(self, revision, cidrs):
+        self._op(self.L.cv_prefilter_insert, revision, cidrs)
+
+    def delete(self, revision, cidrs):
+        self._op(self.L.cv_prefilter_delete, revision, cidrs)
+
+    def dump(self):
+        rev = C.c_int64()
+        n = _check(self.L.cv_prefilter_dump(self.h, None, 0, C.byref(rev)), "cv_prefilter_dump")
+        arr = (Cidr * max(n, 1))()
+        n = _check(self.L.cv_prefilter_dump(self.h, arr, n, C.byref(rev)), "cv_prefilter_dump")
+        return [cidr_str(arr[i]) for i in range(n)], rev.value
+
+    def write_config(self):
+        n = _check(self.L.cv_prefilter_write_config(self.h, None, 0), "cv_prefilter_write_config")
+        buf = C.create_string_buffer(n + 1)
+        self.L.cv_prefilter_write_config(self.h, buf, n + 1)
+        return buf.value.decode()
+
+    def map_handle(self, which):
+        return self.L.cv_prefilter_map(self.h, which)
+
+    def close(self):
+        if self.h:
+            self.L.cv_prefilter_free(self.h)
+            self.h = None
+
+
+class PolicyKey(C.Structure):
+    _fields_ = [("identity", C.c_uint32), ("dport", C.c_uint16), ("nexthdr", C.c_uint8), ("direction", C.c_uint8)]
+
+
+class PolicySync:
+    """Endpoint.syncPolicyMap's desired / realized state (cv_policy_sync_*); keys are
+    (identity, dport, nexthdr, direction) in host byte order, values proxy ports."""
+
+    def __init__(self):
+        self.L = load()
+        h = C.c_void_p()
+        _check(self.L.cv_policy_sync_new(C.byref(h)), "cv_policy_sync_new")
+        self.h = h
+
+    def set_desired(self, desired):
+        items = sorted(desired.items())
+        keys = (PolicyKey * max(len(items), 1))()
+        proxy = (C.c_uint16 * max(len(items), 1))()
+        for i, ((ident, dport, nh, d), pp) in enumerate(items):
+            keys[i] = PolicyKey(ident, dport, nh, d)
+            proxy[i] = pp
+        _check(self.L.cv_policy_sync_set_desired(self.h, keys, proxy, len(items)), "cv_policy_sync_set_desired")
+
+    def run(self, ctx, policy_map):
+        d, a, f = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        rc = self.L.cv_policy_sync_run(self.h, ctx.h, policy_map.h, C.byref(d), C.byref(a), C.byref(f))
+        return rc, d.value, a.value, f.value
+
+    def realized(self):
+        n = _check(self.L.cv_policy_sync_realized(self.h, None, None, 0), "cv_policy_sync_realized")
+        keys = (PolicyKey * max(n, 1))()
+        proxy = (C.c_uint16 * max(n, 1))()
+        n = self.L.cv_policy_sync_realized(self.h, keys, proxy, n)
+        return {(k.identity, k.dport, k.nexthdr, k.direction): int(proxy[i]) for i, k in enumerate(keys[:n])}
+
+    def close(self):
+        if self.h:
+            self.L.cv_policy_sync_free(self.h)
+            self.h = None

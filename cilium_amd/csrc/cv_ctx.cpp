@@ -866,7 +866,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     uint64_t cap = 1024;
     while (cap < per * cmax || cap < c->gcap) cap <<= 1;
     (void)hipDeviceSynchronize();
-    if (c->gtable.alloc(cap * 16) || c->gnode1.alloc(cap * 8) || c->gsingle.alloc((size_t)cmax * 4) ||
+    if (c->gtable.alloc(cap * 16) || c->gnode1.alloc(cap * 4) || c->gsingle.alloc((size_t)cmax * 4) ||
         c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsrec.alloc((size_t)cmax * 32) ||
         c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) || c->gifx.alloc((size_t)cmax * 4) ||
@@ -1495,9 +1495,9 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
         uint64_t ncap = 1024;                                     // the one-word node table of this launch
         while (ncap < 2ull * n) ncap <<= 1;
-        gs.node1 = c->gnode1.as<unsigned long long>();
+        gs.node1 = c->gnode1.as<uint32_t>();
         gs.cap_mask = (uint32_t)(ncap - 1);
-        (void)hipMemsetAsync(gs.node1, 0, ncap * 8, (hipStream_t)stream);
+        (void)hipMemsetAsync(gs.node1, 0, ncap * 4, (hipStream_t)stream);
         if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off, b->stride), gs,
                                        (hipStream_t)stream)))
             return r;

@@ -1820,30 +1820,37 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
     if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;
 }
 
-// The netdev path's node insert: one word per node {tag | the group's latest packet},
-// the table zeroed before the launch, so a packet joins (or opens) its group with one
-// CAS in the common case -- the first try expects an empty word; a lost race returns
-// the word, whose tag says whether to retry on it (same group: swap in this packet)
-// or to move on.  Same result as group_node + group_push.
+// The netdev path's node insert: one 32-bit word per node {tag:7 | multi:1 | the
+// group's latest packet:24} (packet indexes < MAX_CHUNK = 2^24; tag 2..127, so a used
+// word is never 0; its low bit is the queue, IPv4 or IPv6), the table zeroed before
+// the launch: a packet opens its group with one CAS expecting an empty word, or joins
+// it by swapping in its own index with the multi bit set; a lost race returns the
+// word, whose tag says whether to retry on it or to move on.  Two groups of one queue
+// whose pairs share a slot chain and a tag merge into one (about 1 in 63 collisions):
+// a coarser grouping, equally exact -- a group's packets run in packet order on one
+// lane either way.  4-B words keep the table at 128 MiB
+// for 2^24 packets, and the multi bit tells k_group_flatten a singleton from the node
+// word alone.
+constexpr uint32_t NODE_MULTI = 1u << 24, NODE_IDX = NODE_MULTI - 1;
 __device__ __forceinline__ void group_insert1(const GroupScratch &g, uint64_t gh, uint32_t i, int q)
 {
-    const uint32_t tag = (uint32_t)gh | 1u;
-    const unsigned long long mine = (unsigned long long)tag << 32 | i;
+    const uint32_t tag = (1u + (uint32_t)(gh % 63u)) << 1 | (q == Q_NETDEV ? 0u : 1u);   // (queues never merge)
+    const uint32_t first_w = tag << 25 | i, join_w = first_w | NODE_MULTI;
     uint32_t s = (uint32_t)(gh >> 32) & g.cap_mask;
-    CV_G unsigned long long *nodes = G(g.node1);
-    unsigned long long cur = 0;
+    CV_G uint32_t *nodes = G(g.node1);
+    uint32_t cur = 0;
     for (;;) {
-        if (__hip_atomic_compare_exchange_strong(nodes + s, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
+        if (__hip_atomic_compare_exchange_strong(nodes + s, &cur, cur ? join_w : first_w, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             break;
-        if ((uint32_t)(cur >> 32) != tag) {                       // another group's node: next slot
+        if ((cur >> 25) != tag) {                                 // another group's node: next slot
             s = (s + 1) & g.cap_mask;
             cur = 0;
         }
     }
     const bool first = cur == 0;
     g.gslot[i] = s;
-    g.next[i] = first ? NONE : (uint32_t)cur;
+    g.next[i] = first ? NONE : (cur & NODE_IDX);
     const uint32_t k = blockIdx.x % QSPLIT;
     const uint32_t at = wave_append(&g.cursor[qctr(q, k)], first);
     if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;

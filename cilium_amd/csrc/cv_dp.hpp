@@ -114,8 +114,9 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t qregion;          // words per region
     uint32_t *work;            // per group: `order` offset of its run, in size-class order
     uint32_t *ifx;             // per packet: the destination endpoint's ifindex (netdev path)
-    unsigned long long *node1; // netdev path: one-word nodes {tag32 | head packet}, zeroed per
-                               // launch (cap_mask + 1 words), or null (the epoch-tagged table)
+    uint32_t *node1;           // netdev path: one-word nodes {tag:7 | multi:1 | head packet:24},
+                               // zeroed per launch (cap_mask + 1 words), or null (the
+                               // epoch-tagged table)
     uint32_t *single;          // the packets of singleton groups, dense (k_group_flatten with a
                                // schedule; cursor[SINGLE_WORD0 + q] of them)
 };

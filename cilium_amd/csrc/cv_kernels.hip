@@ -556,8 +556,18 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, 
         uint32_t m[GMAX];
         if (act) {
             ent = queue_entry(g, q, n, j);
-            head = g.node1 ? (uint32_t)g.node1[*ent] : (uint32_t)g.table[2 * *ent + 1];
-            for (x = head; x != NONE && cnt < GMAX; x = g.next[x]) {   // insertion into registers
+            uint32_t nw = NODE_MULTI;
+            if (g.node1) {
+                nw = g.node1[*ent];
+                head = nw & NODE_IDX;
+            } else {
+                head = (uint32_t)g.table[2 * *ent + 1];
+            }
+            if (!(nw & NODE_MULTI)) {                             // a netdev singleton: no list walk
+                m[0] = head;
+                cnt = 1;
+            }
+            for (x = (nw & NODE_MULTI) ? head : NONE; x != NONE && cnt < GMAX; x = g.next[x]) {   // insertion into registers
                 int pos = 0;
 #pragma unroll
                 for (int t = 0; t < GMAX; ++t) pos += (t < (int)cnt && m[t] < x) ? 1 : 0;
@@ -632,7 +642,9 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, 
     if (threadIdx.x < NCLASS && hist[threadIdx.x]) atomicAdd(&g.cursor[qcls(q, threadIdx.x)], hist[threadIdx.x]);
 }
 
-// k_group_schedule: `work` lists the runs class by class, largest class first
+// k_group_schedule: `work` lists the runs class by class, largest class first (or
+// smallest first).  Class 0, the singletons, is not scheduled: it takes no room in
+// `work`, so the runs fill work[0 .. runs) as for_each_run reads them in either order.
 constexpr int SCHED_PER_THREAD = 4;
 __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q, bool largest_first)
 {
@@ -642,7 +654,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q,
         for (int k = 0; k < NCLASS; ++k) {
             const int c = largest_first ? NCLASS - 1 - k : k;
             cbase[c] = acc;
-            acc += g.cursor[qcls(q, c)];
+            if (c) acc += g.cursor[qcls(q, c)];
         }
     }
     uint32_t n[QSPLIT];

@@ -539,59 +539,82 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
 
 // ------------------------------------------------------------------ size-sorted runs
 // k_group_flatten: every queued group of q becomes a run {size, members ascending}
-// in `order` (one block-aggregated allocation per 256 groups); the queue word is
-// replaced by the run's offset; per-class counts.  Block-uniform loop (the scans use
-// every lane).
+// in `order`; the queue word is replaced by the run's offset (a singleton's by its
+// packet, SINGLE_RUN-tagged, and with `dense` the packet is listed in `single`);
+// per-class counts.  A thread takes FLAT_PER_THREAD groups per pass and walks their
+// member lists in lockstep (independent dependent-load chains in flight together);
+// a block allocates its runs and singleton slots with one atomic per counter per pass
+// of BLOCK * FLAT_PER_THREAD groups (returning atomics on one word serialise at about
+// 90 per microsecond chip-wide, so the per-pass count is what bounds the kernel).
+// Block-uniform loop (the scans use every lane).
+constexpr int FLAT_PER_THREAD = 4;
 __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, bool dense)
 {
+    constexpr int U = FLAT_PER_THREAD;
     __shared__ uint32_t hist[NCLASS], wsum[BLOCK / 64], ssum[BLOCK / 64], bbase, sbase;
     if (threadIdx.x < NCLASS) hist[threadIdx.x] = 0;
     uint32_t n[QSPLIT];
     const uint32_t total = queue_sizes(g, q, n);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (uint32_t base = blockIdx.x * BLOCK; base < total; base += gridDim.x * BLOCK) {
-        const uint32_t j = base + threadIdx.x;
-        const bool act = j < total;
-        uint32_t *ent = nullptr, cnt = 0, x = NONE, head = NONE;
-        uint32_t m[GMAX];
-        if (act) {
-            ent = queue_entry(g, q, n, j);
+    constexpr uint32_t SPAN = BLOCK * U;
+    for (uint32_t base = blockIdx.x * SPAN; base < total; base += gridDim.x * SPAN) {
+        uint32_t *ent[U], cnt[U], head[U], x[U];
+        uint32_t m[U][GMAX];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = base + u * BLOCK + threadIdx.x;
+            ent[u] = nullptr;
+            cnt[u] = 0;
+            head[u] = x[u] = NONE;
+            if (j >= total) continue;
+            ent[u] = queue_entry(g, q, n, j);
             uint32_t nw = NODE_MULTI;
             if (g.node1) {
-                nw = g.node1[*ent];
-                head = nw & NODE_IDX;
+                nw = g.node1[*ent[u]];
+                head[u] = nw & NODE_IDX;
             } else {
-                head = (uint32_t)g.table[2 * *ent + 1];
+                head[u] = (uint32_t)g.table[2 * *ent[u] + 1];
             }
-            if (!(nw & NODE_MULTI)) {                             // a netdev singleton: no list walk
-                m[0] = head;
-                cnt = 1;
+            if (nw & NODE_MULTI) {
+                x[u] = head[u];
+            } else {                                              // a netdev singleton: no list walk
+                m[u][0] = head[u];
+                cnt[u] = 1;
             }
-            for (x = (nw & NODE_MULTI) ? head : NONE; x != NONE && cnt < GMAX; x = g.next[x]) {   // insertion into registers
-                int pos = 0;
+        }
+        for (bool more = true; more;) {                           // the member lists, in lockstep
+            more = false;
 #pragma unroll
-                for (int t = 0; t < GMAX; ++t) pos += (t < (int)cnt && m[t] < x) ? 1 : 0;
+            for (int u = 0; u < U; ++u) {
+                if (x[u] == NONE || cnt[u] >= GMAX) continue;
+                const uint32_t v = x[u];
+                int pos = 0;                                      // insertion into registers
+#pragma unroll
+                for (int t = 0; t < GMAX; ++t) pos += (t < (int)cnt[u] && m[u][t] < v) ? 1 : 0;
 #pragma unroll
                 for (int t = GMAX - 1; t >= 0; --t) {
-                    const uint32_t left = t > 0 ? m[t - 1] : 0u;
-                    m[t] = (t < pos) ? m[t] : (t == pos ? x : left);
+                    const uint32_t left = t > 0 ? m[u][t - 1] : 0u;
+                    m[u][t] = (t < pos) ? m[u][t] : (t == pos ? v : left);
                 }
-                ++cnt;
+                ++cnt[u];
+                x[u] = g.next[v];
+                more = true;
             }
-            for (uint32_t y = x; y != NONE; y = g.next[y]) ++cnt;
         }
-        const uint32_t need = act && cnt > 1 ? cnt + 1 : 0;      // singletons need no run
-        const bool one = act && cnt == 1;
-        uint32_t incl = need;                                     // wave inclusive scan
+        uint32_t tneed = 0, tone = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            for (uint32_t y = x[u]; y != NONE; y = g.next[y]) ++cnt[u];   // (groups past GMAX: count)
+            tneed += cnt[u] > 1 ? cnt[u] + 1 : 0;                 // singletons need no run
+            tone += cnt[u] == 1 ? 1 : 0;
+        }
+        uint32_t incl = tneed, sincl = tone;                      // wave inclusive scans
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(incl, d, 64);
-            if (lane >= (uint32_t)d) incl += t;
+            const uint32_t t = __shfl_up(incl, d, 64), ts = __shfl_up(sincl, d, 64);
+            if (lane >= (uint32_t)d) { incl += t; sincl += ts; }
         }
-        const unsigned long long ones = __ballot(one);            // singletons' rank in the wave
-        const uint32_t srank = __popcll(ones & ((1ull << lane) - 1));
-        if (lane == 63) wsum[wv] = incl;
-        if (lane == 0) ssum[wv] = __popcll(ones);
+        if (lane == 63) { wsum[wv] = incl; ssum[wv] = sincl; }
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t acc = 0, sacc = 0;
@@ -604,37 +627,46 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, 
             sbase = dense && sacc ? atomicAdd(&g.cursor[SINGLE_WORD0 + q], sacc) : 0;
         }
         __syncthreads();
-        if (one) {                                                // no run: the packet itself
-            if (dense) g.single[sbase + ssum[wv] + srank] = head;
-            *ent = head | SINGLE_RUN;                             // (k_group_schedule skips it)
-            atomicAdd(&hist[0], 1u);
-        } else if (act) {
-            const uint32_t off = bbase + wsum[wv] + incl - need;
-            uint32_t *o = g.order + off;
-            o[0] = cnt;
-            if (cnt <= GMAX) {
+        // singleton slots in (wave, u, lane) order: consecutive lanes list consecutive
+        // queue entries, as the stage reads them
+        uint32_t off = bbase + wsum[wv] + incl - tneed, so = sbase + ssum[wv], big = 0;
 #pragma unroll
-                for (int t = 0; t < GMAX; ++t)
-                    if (t < (int)cnt) o[1 + t] = m[t];
-            } else {                                              // large group: copy, shell sort
-                uint32_t k = 1;
-                for (uint32_t y = head; y != NONE; y = g.next[y]) o[k++] = y;
-                ++o;
-                for (uint32_t gap = cnt / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {
-                    for (uint32_t i = gap; i < cnt; ++i) {
-                        const uint32_t v = o[i];
-                        uint32_t t = i;
-                        for (; t >= gap && o[t - gap] > v; t -= gap) o[t] = o[t - gap];
-                        o[t] = v;
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = cnt[u];
+            const unsigned long long ones = __ballot(c == 1);
+            big = max(big, c);
+            if (c == 1) {                                         // no run: the packet itself
+                if (dense) g.single[so + __popcll(ones & ((1ull << lane) - 1))] = head[u];
+                *ent[u] = head[u] | SINGLE_RUN;                   // (k_group_schedule skips it)
+                atomicAdd(&hist[0], 1u);
+            } else if (c) {
+                uint32_t *o = g.order + off;
+                o[0] = c;
+                if (c <= GMAX) {
+#pragma unroll
+                    for (int t = 0; t < GMAX; ++t)
+                        if (t < (int)c) o[1 + t] = m[u][t];
+                } else {                                          // large group: copy, shell sort
+                    uint32_t k = 1;
+                    for (uint32_t y = head[u]; y != NONE; y = g.next[y]) o[k++] = y;
+                    ++o;
+                    for (uint32_t gap = c / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {
+                        for (uint32_t i = gap; i < c; ++i) {
+                            const uint32_t v = o[i];
+                            uint32_t t = i;
+                            for (; t >= gap && o[t - gap] > v; t -= gap) o[t] = o[t - gap];
+                            o[t] = v;
+                        }
                     }
                 }
+                *ent[u] = off;
+                off += c + 1;
+                atomicAdd(&hist[size_class(c)], 1u);
             }
-            *ent = off;
-            atomicAdd(&hist[size_class(cnt)], 1u);
+            so += __popcll(ones);
         }
-        uint32_t big = cnt;                                       // the largest group (diagnostics)
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) big = max(big, (uint32_t)__shfl_xor(big, d, 64));
+        for (int d = 32; d >= 1; d >>= 1) big = max(big, (uint32_t)__shfl_xor(big, d, 64));   // (diagnostics)
         if (lane == 0 && big > 8) atomicMax(&g.cursor[GMAX_WORD0 + q], big);
         __syncthreads();                                          // wsum / bbase reuse
     }

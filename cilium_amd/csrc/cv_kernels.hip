@@ -495,43 +495,73 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage6(DpParams p, BatchDev b, Out
 // the stage's waves no longer wait on the insert chain of their few creating lanes.
 // ct_create4 / ct_create6 (conntrack.h:663-744 / 589-639) with the tuple ct_lookup
 // left (ct_l4's tuple reversed: both directions missed) and the ipv{4,6}_policy state.
+// A block gathers the marked packets of a span of COMMIT_SPAN packets into LDS (a
+// ballot and one LDS atomic per wave) and then creates them with every lane busy:
+// about one packet in seven carries a create, and a lane-per-packet pass would keep
+// six lanes of seven idle while the seventh walks its insert chains.
+constexpr uint32_t COMMIT_SPAN = BLOCK * 8;
+__device__ __forceinline__ void commit_one(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
+                                           bool v6, uint32_t now, Acct &a)
+{
+    const uint4 s1 = g.srec[2 * i + 1];
+    uint32_t seen;
+    if (!v6) {
+        const EpDev ep = ep_stage4<false>(p, s1.z & 0xFFFFu);
+        const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
+        Tuple4 t;
+        t.nexthdr = s.nexthdr;
+        t.daddr = s.daddr;
+        t.saddr = s.saddr;
+        t.dport = t.sport = 0;
+        ct_l4<false>(t, s.h, CT_INGRESS, seen);
+        t.reverse();
+        const CtState sn{0, 0, 0, 0, 0, s1.w};
+        ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
+    } else {
+        Rec6 r;
+        rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
+        const Skb6 s = skb6_from(r);
+        Tuple6 t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
+        t.nexthdr = s.nexthdr;
+        t.dport = t.sport = 0;
+        ct_l4<true>(t, s.h, CT_INGRESS, seen);
+        t.reverse();
+        const CtState sn{s.daddr[3] & 0xFFFFu, 0, 0, 0, 0, s1.w};
+        ct_create<true>(G(p.eps)[s1.z & 0xFFFFu].ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, GroupScratch g, uint32_t now)
 {
     __shared__ LdsPolicy pc;
+    __shared__ uint32_t list[COMMIT_SPAN], lcount;
     pol_cache_init(pc);
-    __syncthreads();
     Acct a{0, 0, &pc};
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
-        const uint32_t mk = g.gslot[i];
-        if (mk != COMMIT4 && mk != COMMIT6) continue;
-        const uint4 s1 = g.srec[2 * i + 1];
-        uint32_t seen;
-        if (mk == COMMIT4) {
-            const EpDev ep = ep_stage4<false>(p, s1.z & 0xFFFFu);
-            const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
-            Tuple4 t;
-            t.nexthdr = s.nexthdr;
-            t.daddr = s.daddr;
-            t.saddr = s.saddr;
-            t.dport = t.sport = 0;
-            ct_l4<false>(t, s.h, CT_INGRESS, seen);
-            t.reverse();
-            const CtState sn{0, 0, 0, 0, 0, s1.w};
-            ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
-        } else {
-            Rec6 r;
-            rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
-            const Skb6 s = skb6_from(r);
-            Tuple6 t;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * COMMIT_SPAN; base < b.n; base += gridDim.x * COMMIT_SPAN) {
+        if (threadIdx.x == 0) lcount = 0;
+        __syncthreads();
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
-            t.nexthdr = s.nexthdr;
-            t.dport = t.sport = 0;
-            ct_l4<true>(t, s.h, CT_INGRESS, seen);
-            t.reverse();
-            const CtState sn{s.daddr[3] & 0xFFFFu, 0, 0, 0, 0, s1.w};
-            ct_create<true>(G(p.eps)[s1.z & 0xFFFFu].ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
+        for (uint32_t u = 0; u < COMMIT_SPAN / BLOCK; ++u) {
+            const uint32_t i = base + u * BLOCK + threadIdx.x;
+            const uint32_t mk = i < b.n ? g.gslot[i] : NONE;
+            const bool want = mk == COMMIT4 || mk == COMMIT6;
+            const unsigned long long w = __ballot(want);
+            if (!w) continue;
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(&lcount, (uint32_t)__popcll(w));
+            at = __shfl(at, 0, 64);
+            if (want) list[at + __popcll(w & ((1ull << lane) - 1))] = i | (mk == COMMIT6 ? 0x80000000u : 0u);
         }
+        __syncthreads();
+        const uint32_t cnt = lcount;
+        for (uint32_t k = threadIdx.x; k < cnt; k += BLOCK) {
+            const uint32_t e = list[k];
+            commit_one(p, b, g, e & 0x7FFFFFFFu, e >> 31, now, a);
+        }
+        __syncthreads();                                          // (list / lcount reuse)
     }
     __syncthreads();
     pol_cache_flush(pc);

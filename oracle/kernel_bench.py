@@ -33,7 +33,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-RECORDED = os.path.join(ROOT, "profiles", "r01u", "cpu_kernel_ebpf.json")
+RECORDED = os.path.join(ROOT, "profiles", "cpu_kernel_ebpf.json")   # (profiles/r0*/ stay off the GPU box)
 sys.path.insert(0, ROOT)
 
 from cilium_amd import synth  # noqa: E402

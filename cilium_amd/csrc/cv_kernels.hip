@@ -707,7 +707,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, 
 // k_group_schedule: `work` lists the runs class by class, largest class first (or
 // smallest first).  Class 0, the singletons, is not scheduled: it takes no room in
 // `work`, so the runs fill work[0 .. runs) as for_each_run reads them in either order.
-constexpr int SCHED_PER_THREAD = 4;
+constexpr int SCHED_PER_THREAD = 16;   // (class-counter atomics per 4 096 runs: 62 -> 33 us per call vs 4)
 __global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q, bool largest_first)
 {
     __shared__ uint32_t cbase[NCLASS], lcnt[NCLASS], lbase[NCLASS];

@@ -1832,6 +1832,7 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
 // for 2^24 packets, and the multi bit tells k_group_flatten a singleton from the node
 // word alone.
 constexpr uint32_t NODE_MULTI = 1u << 24, NODE_IDX = NODE_MULTI - 1;
+static_assert(MAX_CHUNK <= NODE_MULTI, "a launch's packet indexes must fit the node word's 24 bits");
 __device__ __forceinline__ void group_insert1(const GroupScratch &g, uint64_t gh, uint32_t i, int q)
 {
     const uint32_t tag = (1u + (uint32_t)(gh % 63u)) << 1 | (q == Q_NETDEV ? 0u : 1u);   // (queues never merge)

@@ -181,10 +181,16 @@ struct Fwd {
 // before.  Flushed once per workgroup: hot entries (one L3 rule hit by most packets)
 // see one global atomic per workgroup instead of one per packet.  Sums commute, so
 // the folded counters equal the per-packet updates.
-constexpr int PC_N = 256;
+// The conntrack maps' live-entry counts (one word per map, added to by every create
+// and delete of the launch) get slots of their own: in the shared table a policy
+// entry holding their slot would send every create of the workgroup to that one
+// global word, where returning and non-returning atomics alike serialise.
+constexpr int PC_N = 256, PC_LIVE = 8;
 struct LdsPolicy {
     unsigned long long key[PC_N];
     unsigned long long val[PC_N];
+    unsigned long long lkey[PC_LIVE];
+    unsigned long long lval[PC_LIVE];
 };
 
 __device__ __forceinline__ void pol_add(LdsPolicy *pc, unsigned long long *d, unsigned long long inc)
@@ -207,9 +213,32 @@ __device__ __forceinline__ void pol_add(LdsPolicy *pc, unsigned long long *d, un
     __hip_atomic_fetch_add(G(d), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void live_add(LdsPolicy *pc, unsigned long long *d, unsigned long long inc)
+{
+    if (pc) {
+        const unsigned long long k = reinterpret_cast<uintptr_t>(d);
+#pragma unroll
+        for (int i = 0; i < PC_LIVE; ++i) {
+            unsigned long long cur = pc->lkey[i];
+            if (cur == 0) {
+                unsigned long long exp = 0;
+                __hip_atomic_compare_exchange_strong(&pc->lkey[i], &exp, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                cur = exp == 0 ? k : exp;
+            }
+            if (cur == k) {
+                __hip_atomic_fetch_add(&pc->lval[i], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return;
+            }
+        }
+    }
+    pol_add(pc, d, inc);
+}
+
 __device__ __forceinline__ void pol_cache_init(LdsPolicy &pc)
 {
     for (int i = threadIdx.x; i < PC_N; i += blockDim.x) pc.key[i] = 0, pc.val[i] = 0;
+    if (threadIdx.x < PC_LIVE) pc.lkey[threadIdx.x] = 0, pc.lval[threadIdx.x] = 0;
 }
 
 // after a __syncthreads that follows the workgroup's last pol_add
@@ -219,6 +248,9 @@ __device__ __forceinline__ void pol_cache_flush(const LdsPolicy &pc)
         if (pc.key[i] && pc.val[i])
             __hip_atomic_fetch_add(G(reinterpret_cast<unsigned long long *>(pc.key[i])), pc.val[i], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < PC_LIVE && pc.lkey[threadIdx.x] && pc.lval[threadIdx.x])
+        __hip_atomic_fetch_add(G(reinterpret_cast<unsigned long long *>(pc.lkey[threadIdx.x])), pc.lval[threadIdx.x],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // EVENTS: the kernel instance that emits the optional outputs (drop / trace records,
@@ -1024,7 +1056,7 @@ __device__ __forceinline__ void ct_live_add(const HashTable &ct, Acct &a, bool g
 {
     if (!ct.live) return;
     if (guard) __hip_atomic_fetch_add(G(ct.live), (unsigned long long)d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else pol_add(a.pc, ct.live, (unsigned long long)d);
+    else live_add(a.pc, ct.live, (unsigned long long)d);
 }
 
 // map_update_elem(BPF_ANY) of a CT entry (conntrack.h:694,720,740)

@@ -1015,7 +1015,7 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
             bool created;
             const int64_t sl = dev_upsert<Ct4Spec>(ep.ct4, k, &created);
             if (sl < 0) continue;                                 // (probe limit; launches are planned with room)
-            if (created && ep.ct4.live) pol_add(&pc, ep.ct4.live, 1ull);
+            if (created && ep.ct4.live) live_add(&pc, ep.ct4.live, 1ull);
             const CV_G uint32_t *v = ct_cold<Ct4Spec>(ep.ct4, sl);  // w14 / w15: side words 4 / 5
             if (!created && v[5] == g.serial && v[4] > x) continue;
             e.w[14] = x;

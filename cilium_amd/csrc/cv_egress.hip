@@ -555,8 +555,10 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             const uint32_t S = x.t.saddr;
             const uint32_t P = group_node(g, pair_hash4(S, x.t.daddr, SALT_CT4));
             g.gslot[i] = P;
-            // local delivery sees the packet after the service / loopback rewrites
-            uf_union(g, P, group_node(g, pair_hash4(x.s.saddr, x.s.daddr, SALT_CT4)));
+            // local delivery sees the packet after the service / loopback rewrites; that
+            // pair is P itself unless a loopback rewrite changed it (its node is P's)
+            const bool same = (x.s.saddr == S && x.s.daddr == x.t.daddr) || (x.s.saddr == x.t.daddr && x.s.daddr == S);
+            if (!same) uf_union(g, P, group_node(g, pair_hash4(x.s.saddr, x.s.daddr, SALT_CT4)));
             uint32_t na4, np;                                     // a loopback NAT entry's reply rev-NAT target
             if (x.stn.addr && x.stn.loopback && revnat4(p, x.stn.rev_nat, na4, np, na))
                 uf_union(g, P, group_node(g, pair_hash4(na4, S, SALT_CT4)));

@@ -33,9 +33,16 @@ int grid_for(uint32_t n);
 enum : uint32_t {
     EG_STAGE = 0x3u, EG_V6 = 0x4u, EG_LOOPBACK = 0x8u, EG_SVC = 0x10u, EG_DPORT_RW = 0x20u,
     EG_NAT_DEFER = 0x40u,       // the NATed tuple's pair is read by no packet of the launch
-    EG_NAT_DONE = 0x80u,        // ... and ct_create4 reached it: k_nat_apply writes it
 };
 enum : uint32_t { STAGE_DONE = 0, STAGE_LB = 1, STAGE_CT = 2 };
+
+// A dense word per packet (GroupScratch::ifx, which otherwise only the netdev path
+// uses) with what the grouping passes after k_egress_pairs test on every packet,
+// so they stream 4 B per packet instead of its 64-B scratch line: the conntrack queue
+// (IPv6), a NAT-tuple writer to place (k_egress_nat), a deferred NAT write made
+// (k_nat_group).  Written by k_egress_pairs for every packet, BIT_NAT_DONE by the
+// packet's own lane in k_egress_ct.
+enum : uint32_t { BIT_V6 = 1, BIT_NAT_CAND = 2, BIT_NAT_DONE = 4 };
 constexpr uint64_t SALT_SVC4 = 0x5356433400000000ULL, SALT_SVC6 = 0x5356433600000000ULL,
                    SALT_CT4 = 0x4354340000000000ULL, SALT_CT6 = 0x4354360000000000ULL,
                    SALT_NAT = 0x4E41540000000000ULL, SALT_SELF = 0x53454C4600000000ULL;
@@ -544,7 +551,9 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-        if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; continue; }
+        if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; g.ifx[i] = 0; continue; }
+        g.ifx[i] = ((eg[0] & EG_V6) ? BIT_V6 : 0u) |
+                   ((eg[0] & (EG_V6 | EG_SVC)) == EG_SVC && eg[4] ? BIT_NAT_CAND : 0u);
         const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
         Acct na{0, 0};                                            // speculative probes are not accounted
         if (!(eg[0] & EG_V6)) {
@@ -634,9 +643,9 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
 __global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, GroupScratch g)
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
-        uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-        if ((eg[0] & (EG_STAGE | EG_V6 | EG_SVC)) != (STAGE_CT | EG_SVC) || !eg[4]) continue;
+        if (!(g.ifx[i] & BIT_NAT_CAND)) continue;                // (STAGE_CT, IPv4 service, a NATed tuple)
         if (p.ct_guard) continue;                                 // one-packet launch: written inline, in order
+        uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         uint32_t nn;
         if (eg[0] & EG_LOOPBACK) {                                // (client, IPV4_LOOPBACK): by pair
             nn = group_find(g, pair_hash4(eg[4], eg[5], SALT_CT4));
@@ -654,7 +663,7 @@ __global__ void __launch_bounds__(BLOCK) k_group_link(BatchDev b, GroupScratch g
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         const uint32_t s = g.gslot[i];
         if (s == NONE) { g.next[i] = NONE; continue; }
-        group_push(g, uf_find(g, s), i, (g.eg[(size_t)i * EG_WORDS] & EG_V6) ? Q_CT6 : Q_CT4);
+        group_push(g, uf_find(g, s), i, (g.ifx[i] & BIT_V6) ? Q_CT6 : Q_CT4);
     }
 }
 
@@ -747,7 +756,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         const bool defer = eg[0] & EG_NAT_DEFER;
         const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer, true);
         eg_changed();
-        if (defer && c != DROP_CT_CREATE_FAILED) g.eg[(size_t)i * EG_WORDS] = eg[0] | EG_NAT_DONE;
+        if (defer && c != DROP_CT_CREATE_FAILED) g.ifx[i] |= BIT_NAT_DONE;
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
         uint32_t na, np;
@@ -986,8 +995,8 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
 __global__ void __launch_bounds__(BLOCK) k_nat_group(BatchDev b, GroupScratch g)
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        if (!(g.ifx[i] & BIT_NAT_DONE)) { g.gslot[i] = NONE; continue; }
         const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-        if (!(eg[0] & EG_NAT_DONE)) { g.gslot[i] = NONE; continue; }
         group_push(g, group_node(g, pair_hash4(eg[4], eg[6], SALT_NAT)), i, Q_NAT);
     }
 }

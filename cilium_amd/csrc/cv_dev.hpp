@@ -526,18 +526,21 @@ __device__ __forceinline__ int policy_access(const HashTable &pol, uint32_t flag
             l4 = s >= 0;
         }
     } else {
+        // tag-first probes: the 16-B part with the fingerprints, then the matching
+        // key's part (2-3 line requests instead of the whole 64-B bucket's 4 per
+        // lane; the config-3 stage 1.5 % faster)
         if (flags & F_HAVE_L4_POLICY) {
             a.nl++;
-            s = dev_find<PolicySpec>(pol, kl4, px);
+            s = dev_find_tf<PolicySpec, true>(pol, kl4, px);
             l4 = s >= 0;
         }
         if (s < 0) {
             a.nl++;
-            s = dev_find<PolicySpec>(pol, kl3, px);
+            s = dev_find_tf<PolicySpec, true>(pol, kl3, px);
         }
         if (s < 0 && (flags & F_HAVE_L4_POLICY)) {
             a.nl++;
-            s = dev_find<PolicySpec>(pol, kwc, px);
+            s = dev_find_tf<PolicySpec, true>(pol, kwc, px);
             l4 = s >= 0;
         }
     }

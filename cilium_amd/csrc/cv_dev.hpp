@@ -624,13 +624,16 @@ __device__ __forceinline__ int policy_ingress(const HashTable &pol, uint32_t fla
     return r >= TC_ACT_OK ? r : DROP_POLICY;
 }
 
-// policy_can_egress (policy.h:181-200), POLICY_EGRESS && LXC_ID
+// policy_can_egress (policy.h:181-200), POLICY_EGRESS && LXC_ID.  ILP: the three keys'
+// buckets read together; the IPv6 egress stage measured 3.5 % faster with the
+// sequential tag-first probes, the IPv4 one 1 % slower.
+template <bool ILP = true>
 __device__ __forceinline__ int policy_egress(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
                                              uint32_t dport_raw, uint32_t proto, Acct &a)
 {
     if (!(flags & F_POLICY_EGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
     if (flags & F_DROP_ALL) return DROP_POLICY;
-    int r = policy_access<true>(pol, flags, len, identity, dport_raw, proto, CT_EGRESS, a);
+    int r = policy_access<ILP>(pol, flags, len, identity, dport_raw, proto, CT_EGRESS, a);
     return r >= 0 ? r : DROP_POLICY;
 }
 

@@ -889,7 +889,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         res.dst = lab ? lab
                       : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+    verdict = policy_egress<false>(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);       // ct_delete6

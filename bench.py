@@ -132,7 +132,35 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count(), "kernel": platform.release()}
+    share = cpu_share()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "kernel": platform.release(), **share}
+
+
+_OMP_ENV = os.environ.get("OMP_NUM_THREADS")
+
+
+def cpu_share():
+    """The host CPUs this process may use: its affinity mask, the cgroup CPU quota
+    (cpu.max) and the lease's OMP_NUM_THREADS, whichever is smallest.  nproc counts the
+    whole machine; a GPU lease grants a share of it."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    env = int(_OMP_ENV) if _OMP_ENV and _OMP_ENV.isdigit() else None
+    use = min(x for x in (aff, quota, env) if x)
+    return {"cpus_affinity": aff, "cpus_cgroup_quota": quota, "omp_num_threads_env": env, "threads_used": use}
+
+
+def allowed_cpus():
+    return cpu_share()["threads_used"]
 
 
 def cpu_baseline(name, w, min_seconds=10.0):
@@ -146,8 +174,8 @@ def cpu_baseline(name, w, min_seconds=10.0):
     steps (synth.port_variant), as on the GPU."""
     from cilium_amd import synth
     from tests import harness as H
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    threads = allowed_cpus()
+    os.environ["OMP_NUM_THREADS"] = str(threads)
     done, busy, v = 0, 0.0, 0
     if name in ("config1", "config2"):
         sample = min(w.n, 1 << 21)
@@ -416,7 +444,9 @@ def main():
                 "header_bytes": "64 (v4) / 128 (v6)" if name == "config5" else int(w.frames.shape[1]),
                 "parallelism": f"replicated tables, {world} GPU(s), batch per GPU"
                                + (", conntrack sharded by address pair (16M flows per GPU of one node-wide set)"
-                                  if name in ("config3", "config4") and world > 1 else ""),
+                                  if name in ("config3", "config4") and world > 1 else "")
+                               + (", independent CT per rank (N separate nodes: replicas, DESIGN.md §7)"
+                                  if name == "config5" and world > 1 else ""),
                 "tables": {k: len(m) for k, m in w.maps.items()},
             },
             "roofline": {

@@ -73,7 +73,10 @@ def _build(verbose, out, defines):
         os.remove(o)
     os.replace(out + ".tmp", out)
     if out == OUT:
-        build_c_caller(verbose)
+        try:
+            build_c_caller(verbose)
+        except (OSError, subprocess.CalledProcessError) as e:   # a test tool: never fails the product build
+            print(f"[cilium_amd.build] tests/_bin/ct_walk not built: {e}", file=sys.stderr)
     return out
 
 

@@ -104,25 +104,38 @@ def ct6_shard(keys: np.ndarray, world: int) -> np.ndarray:
 def split_workload(w, world: int, rank: int):
     """The rank's share of a synthetic ingress workload: its packets (in their
     original order) and its conntrack shard; the other tables stay whole."""
+    return split_workload_all(w, world, ranks=[rank])[0]
+
+
+def split_workload_all(w, world: int, ranks=None):
+    """split_workload for several ranks at once: the packets' and the CT entries'
+    owners are computed once (one pass over a 2^24-packet batch and a 33M-entry table
+    instead of one per rank)."""
     import copy
     from cilium_amd import synth
-    own = np.nonzero(flow_shard(w.frames, w.length, world) == rank)[0]
-    maps = dict(w.maps)
-    for name, fn in (("ct4", ct4_shard), ("ct6", ct6_shard)):
-        if name in maps:
+    ranks = range(world) if ranks is None else ranks
+    pkt_owner = flow_shard(w.frames, w.length, world)
+    ct_owner = {name: fn(w.maps[name].keys, world) for name, fn in (("ct4", ct4_shard), ("ct6", ct6_shard))
+                if name in w.maps}
+    out = []
+    for rank in ranks:
+        own = np.nonzero(pkt_owner == rank)[0]
+        maps = dict(w.maps)
+        for name, owner in ct_owner.items():
             ct = maps[name]
-            mine = fn(ct.keys, world) == rank
+            mine = owner == rank
             maps[name] = synth.MapSpec(ct.name, ct.type, ct.key_size, ct.val_size, ct.max_entries,
                                        ct.keys[mine], ct.vals[mine])
-    part = copy.copy(w)
-    part.maps = maps
-    part.frames = w.frames[own]
-    part.length = w.length[own]
-    part.mark = w.mark[own]
-    if w.extra:
-        part.extra = {k: (v[own] if isinstance(v, np.ndarray) and len(v) == w.n else v) for k, v in w.extra.items()
-                      if not isinstance(k, tuple)}
-    return part, own
+        part = copy.copy(w)
+        part.maps = maps
+        part.frames = w.frames[own]
+        part.length = w.length[own]
+        part.mark = w.mark[own]
+        if w.extra:
+            part.extra = {k: (v[own] if isinstance(v, np.ndarray) and len(v) == w.n else v)
+                          for k, v in w.extra.items() if not isinstance(k, tuple)}
+        out.append((part, own))
+    return out
 
 
 def allreduce_counters(t, group=None):

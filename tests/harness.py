@@ -121,14 +121,14 @@ class ShardedOracle:
     entry, so the union equals one sequential run (tests/test_multi_rank.py)."""
 
     def __init__(self, w: synth.Workload, threads: int):
+        from concurrent.futures import ThreadPoolExecutor
         from cilium_amd import shard
         self.T = max(1, threads)
         self.w = w
-        self.parts = []
-        for t in range(self.T):
-            part, own = shard.split_workload(w, self.T, t)
-            dp, maps = oracle_dp(part)
-            self.parts.append((own, dp, maps))
+        split = shard.split_workload_all(w, self.T)
+        with ThreadPoolExecutor(self.T) as ex:                     # (the C loads release the GIL)
+            dps = list(ex.map(lambda po: oracle_dp(po[0]), split))
+        self.parts = [(own, dp, maps) for (_, own), (dp, maps) in zip(split, dps)]
 
     def netdev_ingress(self, frames=None, now=None, pool=None):
         """verdicts of the whole batch (packet order) and the parallel section's wall time"""
@@ -159,6 +159,33 @@ class ShardedOracle:
     def dump(self, name):
         ks, vs = zip(*(maps[name].dump() for _, _, maps in self.parts))
         return np.concatenate(ks), np.concatenate(vs)
+
+    def digest(self, name):
+        """table_digest of the union of the shards' tables (disjoint key sets)"""
+        cnt, tot, x = 0, 0, 0
+        for _, _, maps in self.parts:
+            c, s, y = maps[name].digest()
+            cnt, tot, x = cnt + c, (tot + s) & 0xFFFFFFFFFFFFFFFF, x ^ y
+        return (cnt, tot, x)
+
+    def policy_rows(self, name="policy"):
+        """the policy map as one node's: every shard's packets / bytes counters summed
+        (the agent sums per-rank counters), key-sorted rows"""
+        base = None
+        tot = None
+        for _, _, maps in self.parts:
+            rows = sorted_rows(*maps[name].dump())
+            if base is None:
+                base = rows.copy()
+                tot = np.zeros((len(rows), 2), np.uint64)
+            assert (rows[:, :16] == base[:, :16]).all()
+            tot += rows[:, 16:32].copy().view("<u8").reshape(-1, 2)
+        spec = self.w.maps[name]
+        init = sorted_rows(spec.keys, spec.vals)[:, 16:32].copy().view("<u8").reshape(-1, 2)
+        with np.errstate(over="ignore"):
+            tot -= init * np.uint64(len(self.parts) - 1)
+        base[:, 16:32] = tot.view(np.uint8).reshape(-1, 16)
+        return base
 
 
 def _dg_mix(z):

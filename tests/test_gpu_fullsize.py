@@ -76,6 +76,85 @@ def test_config4_rank_shards(dev):
         ctx.close()
 
 
+@pytest.fixture
+def say(capsys):
+    """progress lines past pytest's capture (a minutes-long test stays visibly alive)"""
+    import time
+    t0 = time.time()
+
+    def f(msg):
+        with capsys.disabled():
+            print(f"  [{time.time() - t0:6.1f}s] {msg}", flush=True)
+    return f
+
+
+def _bench_steps(w, dev, steps, say, threads, ct_check=None):
+    """bench.py's timed regime on the device and on the address-pair-sharded oracle:
+    step v = the batch with fresh client ports on its new flows (synth.port_variant),
+    built on the device as bench.py builds it, `now + v`; after each step every
+    per-packet output, cilium_metrics, the node's policy counters and the CT table
+    digest against the oracle."""
+    from cilium_amd import synth
+    so = H.ShardedOracle(w, threads)
+    say(f"oracle: {threads} address-pair shards loaded")
+    ctx, pm = H.product_ctx(w)
+    frames, length, mark = H.to_dev(w, dev)
+    out = H.dev_out(w.n, dev)
+    say("device tables compiled")
+    for v in steps:
+        rows, boff, ports = synth.port_variant(w, v)
+        fv = frames.clone()
+        r, o = torch.from_numpy(rows).to(dev), torch.from_numpy(boff).to(dev)
+        fv[r, o] = torch.from_numpy((ports >> 8).astype(np.uint8)).to(dev)
+        fv[r, o + 1] = torch.from_numpy((ports & 0xFF).astype(np.uint8)).to(dev)
+        ctx.netdev_ingress(fv, length, out, w.now + v, mark=mark)
+        got = H.host_out(out)
+        del fv
+        ref, el = so.netdev_ingress(H.apply_variant(w.frames, rows, boff, ports), now=w.now + v)
+        say(f"step {v}: device done, oracle {el:.1f}s")
+        for k in FIELDS:
+            bad = np.nonzero(got[k] != getattr(ref, k))[0]
+            assert len(bad) == 0, (v, k, bad[:5], got[k][bad[:5]], getattr(ref, k)[bad[:5]])
+        assert (ctx.metrics() == so.metrics()).all()
+        pk, pv = pm["policy"].dump()
+        assert (H.sorted_rows(pk, pv) == so.policy_rows()).all()
+        want = so.digest("ct4")
+        ck, cv = pm["ct4"].dump()
+        assert H.table_digest(ck, cv) == want, v
+        if ct_check is not None:
+            assert ct_check(ck)
+        say(f"step {v}: outputs, metrics, policy counters and the {want[0]}-entry CT bit-exact "
+            f"({int((got['ct'] == 0).sum())} CT_NEW)")
+        del ck, cv
+    ctx.close()
+    return so
+
+
+def test_config3_bench_regime(dev, say):
+    """The regime bench.py times (verdict r02 item 1): the 2^24-packet config-3 batch
+    on the 16M-flow table with the CT sized by bench.size_conntrack for a default run,
+    two consecutive fresh steps (2.58M creates each), bit-exact against the oracle."""
+    import bench
+    w = bench.make_workload("config3", 1 << 24, 0, 1)
+    bench.size_conntrack("config3", w, passes=3 + 20 + 1)
+    say(f"workload: {w.n} packets, {len(w.maps['ct4'].keys)} CT entries, max_entries {w.maps['ct4'].max_entries}")
+    _bench_steps(w, dev, (1, 2), say, bench.allowed_cpus())
+
+
+def test_config4_rank_shard_full_size(dev, say):
+    """Config 4 at BASELINE's size: rank 0 of 8's part of the 128M-flow node-wide set
+    (16M flows, 33.5M CT entries) and packets of its own address pairs, two fresh
+    steps bit-exact against the oracle; every CT entry stays on its rank."""
+    import bench
+    w = synth.config3(1 << 22, 1 << 24, seed=0xC1A00004, shard=(0, 8))
+    assert (shard.flow_shard(w.frames, w.length, 8) == 0).all()
+    assert (shard.ct4_shard(w.maps["ct4"].keys, 8) == 0).all()
+    bench.size_conntrack("config4", w, passes=3)
+    say(f"workload: rank 0 of 8, {w.n} packets, {len(w.maps['ct4'].keys)} CT entries")
+    _bench_steps(w, dev, (1, 2), say, bench.allowed_cpus(),
+                 ct_check=lambda keys: (shard.ct4_shard(keys, 8) == 0).all())      # creates stay on the rank
+
+
 def test_config5_full_services(dev):
     from tests.test_gpu_egress import run_egress
     w = synth.config5(1 << 17)                                    # 50k services, 4096 endpoints

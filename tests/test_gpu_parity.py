@@ -122,7 +122,7 @@ def test_config2_ragged(dev, n):
 
 
 def test_ipcache_nested_prefixes(dev):
-    """The v4 LPM layout (DIR-24-8 + /32 front, cv_lpm.hpp) against the oracle's
+    """The v4 LPM layout (16-8-8 trie + /32 hash front, cv_lpm.hpp) against the oracle's
     LPM_TRIE semantics: nested prefixes of every length from /0 to /32 inside one /8,
     addresses at each prefix's first/last address and just outside, then agent deletes
     and re-inserts between batches (the table is recompiled at the batch boundary)."""
@@ -542,8 +542,11 @@ def test_ct_walk_get_next_key_linear(dev):
     """GetNextKey over a 1M-entry device CT map from a C caller (tests/ct_walk.c, the
     cgo glue's view of the C-ABI): every key exactly once, then -ENOENT, in well under
     a second (the dump walk of pkg/maps/ctmap/ctmap.go:196-230)."""
+    import os
     import subprocess
     from cilium_amd import build
+    if not os.path.exists(build.WALK_BIN):
+        build.build_c_caller()                                    # (the library build skips it without gcc)
     out = subprocess.run([build.WALK_BIN, str(1 << 20)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     f = out.stdout.split()

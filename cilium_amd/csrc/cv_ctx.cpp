@@ -149,7 +149,8 @@ struct MapObj {
     // GetNextKey walk over the device table: its entries in slot order as of `gen`
     uint64_t snap_gen = ~0ull;
     std::vector<uint8_t> snap_keys;
-    std::unordered_map<std::string, size_t> snap_index;
+    size_t snap_last = ~(size_t)0;                     // position of the key the last call returned
+    std::unordered_map<std::string, size_t> snap_index;   // built only for walks that jump
 };
 
 struct Endpoint {
@@ -1022,26 +1023,43 @@ int ct_dump(cv_ctx *c, MapObj *mo, std::vector<uint8_t> &keys, std::vector<uint8
 // snapshot of the table, taken once per table generation, so a full walk costs one
 // dump plus O(1) per call; slot order is stable across generations (entries never
 // move), so a walk that spans batches continues where it was.
+// A walk that continues (key = the key the previous call returned) keeps reading its
+// snapshot even when batches ran in between: a GetNextKey walk over a changing kernel
+// hash map likewise may or may not see entries added or removed meanwhile.  The
+// snapshot is retaken when a walk (re)starts -- a null key, or a key that is not the
+// one just returned and not in the snapshot -- and the table changed since.  The
+// common call (the previous result) is found in O(1) without any index; a key index
+// is built only for a walk that jumps.
 int ct_next_key(cv_ctx *c, MapObj *mo, const uint8_t *key, uint8_t *next)
 {
     const uint32_t ks = mo->kind == MK_CT6 ? 40 : 14;
-    if (mo->snap_gen != mo->gen) {
+    const size_t n = mo->snap_keys.size() / ks;
+    size_t pos = 0;
+    bool found = false;
+    if (key && mo->snap_last < n && !memcmp(&mo->snap_keys[mo->snap_last * ks], key, ks)) {
+        pos = mo->snap_last + 1;
+        found = true;
+    } else if (key && mo->snap_gen == mo->gen) {
+        if (mo->snap_index.empty() && n) {
+            mo->snap_index.reserve(n * 2);
+            for (size_t i = 0; i < n; ++i) mo->snap_index.emplace(kstr(&mo->snap_keys[i * ks], ks), i);
+        }
+        auto it = mo->snap_index.find(kstr(key, ks));
+        if (it != mo->snap_index.end()) { pos = it->second + 1; found = true; }
+    }
+    if (!found && mo->snap_gen != mo->gen) {              // a walk (re)starts on a changed table
         std::vector<uint8_t> vals;
         mo->snap_keys.clear();
         mo->snap_index.clear();
-        const int n = ct_dump(c, mo, mo->snap_keys, vals);
-        if (n < 0) return n;
-        mo->snap_index.reserve((size_t)n * 2);
-        for (int i = 0; i < n; ++i) mo->snap_index.emplace(kstr(&mo->snap_keys[(size_t)i * ks], ks), (size_t)i);
+        mo->snap_last = ~(size_t)0;
+        const int r = ct_dump(c, mo, mo->snap_keys, vals);
+        if (r < 0) return r;
         mo->snap_gen = mo->gen;
+        return ct_next_key(c, mo, key, next);
     }
-    size_t pos = 0;
-    if (key) {
-        auto it = mo->snap_index.find(kstr(key, ks));
-        if (it != mo->snap_index.end()) pos = it->second + 1;
-    }
-    if (pos >= mo->snap_index.size()) return -ENOENT;
+    if (pos >= mo->snap_keys.size() / ks) return -ENOENT;
     memcpy(next, &mo->snap_keys[pos * ks], ks);
+    mo->snap_last = pos;
     return 0;
 }
 
@@ -1075,8 +1093,10 @@ uint32_t ct_plan(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t want, ui
     };
     uint64_t r = room();
     if (r < (uint64_t)W * want) {
-        (void)hipStreamSynchronize(s);
-        (void)c;
+        // every batch already submitted, on any stream, has finished (a batch on another
+        // stream against the same CT maps holds a reservation this read would drop)
+        (void)s;
+        drain(c);
         for (MapObj *m : maps) {
             uint64_t v = 0;
             if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
@@ -1274,8 +1294,8 @@ int cv_ct_gc(cv_ctx *c, int h, uint32_t time, uint32_t *deleted)
         drain(c);
         m->gen++;
         DevBuf d;
-        if (d.alloc(4)) return -ENOMEM;
-        if (hipMemset(d.p, 0, 4) != hipSuccess) return -EIO;
+        if (d.alloc(8)) return -ENOMEM;
+        if (hipMemset(d.p, 0, 8) != hipSuccess) return -EIO;
         if (launch_ct_gc(m->ct.view, m->kind == MK_CT6, m->ct.nb, time, d.as<uint32_t>(), nullptr)) return -EIO;
         if (hipMemcpy(&n, d.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
     } else {
@@ -1292,6 +1312,23 @@ int cv_ct_gc(cv_ctx *c, int h, uint32_t time, uint32_t *deleted)
     }
     if (deleted) *deleted = n;
     return 0;
+}
+
+// slot occupancy of a device CT map: out[0] empty, out[1] dead (tombstones), out[2] live
+int cv_ct_slots(cv_ctx *c, int h, uint64_t out[3])
+{
+    if (!c || !out) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    MapObj *m = get(c, h);
+    if (!m) return -EBADF;
+    if (m->kind == MK_PLAIN) return -EINVAL;
+    if (set_device(c)) return -ENODEV;
+    drain(c);
+    DevBuf d;
+    if (d.alloc(24)) return -ENOMEM;
+    if (hipMemset(d.p, 0, 24) != hipSuccess) return -EIO;
+    if (launch_ct_tags(m->ct.view, m->kind == MK_CT6, m->ct.nb, d.as<unsigned long long>(), nullptr)) return -EIO;
+    return hipMemcpy(out, d.p, 24, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -EIO;
 }
 
 int cv_map_get_next_key(cv_ctx *c, int h, const void *key, void *next)

@@ -161,6 +161,7 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
 int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s);
 // ctmap.GC (GCFilterByTime): mark entries with lifetime < time dead; adds the count
 int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s);
+int launch_ct_tags(const HashTable &t, int v6, uint64_t nb, unsigned long long *out, hipStream_t s);
 // every live entry: slot index (may be null), key words, 16 value words
 int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint64_t *out_slots, uint32_t *out_keys, uint32_t *out_vals,
                    uint32_t *count, uint32_t max, hipStream_t s);

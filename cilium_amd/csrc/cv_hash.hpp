@@ -19,7 +19,15 @@
 namespace cv {
 
 constexpr uint32_t TAG_EMPTY = 0, TAG_DEAD = 1, TAG_BUSY = 2;
-constexpr int MAX_PROBE = 64;
+constexpr int MAX_PROBE = 64;        // probe limit (buckets) of the host-built tables: a longer chain grows the table
+// Conntrack tables (filled on the device, never rebuilt) probe up to CT_MAX_PROBE
+// buckets: a create fails below max_entries only when that many consecutive buckets
+// hold live entries and nothing else.  The tables are sized for max_entries at 60 %
+// slot load (buckets_for), where a run of k full 2-slot buckets has probability about
+// e^(-0.22 k): e^-900 for k = 4096, so a create below max_entries never fails -- the
+// kernel hash map's behaviour -- while a lookup miss still ends at the first bucket
+// with an empty slot (k_ct_gc turns tombstones back into empty slots).
+constexpr int CT_MAX_PROBE = 4096;
 constexpr uint64_t HASH_SEED = 0x243F6A8885A308D3ULL;
 
 struct HashTable {            // POD view, passed by value to kernels
@@ -38,6 +46,7 @@ struct HashSpec {
     static constexpr int KW = KW_, IVW = IVW_, SPB = SPB_, BW = BW_, IVH = IVH_, SYM = SYM_;
     static constexpr int KS = KS_ ? KS_ : KW_;                   // words from one slot's key to the next
     static constexpr int KEY0 = 2, IVAL0 = 2 + SPB * KS, HVAL0 = 2 * IVAL0;   // HVAL0 in halfwords
+    static constexpr int MAXP = SYM ? CT_MAX_PROBE : MAX_PROBE;           // probe limit in buckets
     static_assert(IVAL0 + SPB * IVW <= BW, "bucket overflow");
     static_assert(IVH == 0 || (IVW == 0 && IVH == 1 && HVAL0 + SPB <= 2 * BW), "halfword values");
     static_assert(SPB <= 8, "eight tag bytes");
@@ -196,7 +205,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
     uint32_t tag;
     const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
-    for (int p = 0; p < MAX_PROBE; ++p) {
+    for (int p = 0; p < S::MAXP; ++p) {
         const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
         const uint2 tg = ld_tags<S, FRESH>(bw);
         uint64_t match;
@@ -220,7 +229,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
     return -1;
 }
 
-// the full-bucket probe chain from bucket b (probe number p0 of MAX_PROBE)
+// the full-bucket probe chain from bucket b (probe number p0 of S::MAXP)
 template <class S>
 __device__ __forceinline__ int64_t dev_find_from(const HashTable &t, const uint32_t *key, uint32_t tag, uint64_t b,
                                                  int p0, uint32_t *ival);
@@ -240,7 +249,7 @@ template <class S>
 __device__ __forceinline__ int64_t dev_find_from(const HashTable &t, const uint32_t *key, uint32_t tag, uint64_t b,
                                                  int p0, uint32_t *ival)
 {
-    for (int p = p0; p < MAX_PROBE; ++p) {
+    for (int p = p0; p < S::MAXP; ++p) {
         uint32_t w[S::BW];
         load_bucket<S>(t.buckets, b, w);
         bool stop;
@@ -483,7 +492,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
     }
     if (stop) return -1;
     // rare: the home bucket is full, continue the chain from the next bucket
-    for (int p = 1; p < MAX_PROBE; ++p) {
+    for (int p = 1; p < S::MAXP; ++p) {
         b = (b + 1) & t.mask;
         Probe<S> nx;
         nx.tag = pr.tag;
@@ -571,7 +580,7 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
     uint64_t b = h & t.mask, fb = 0;
     uint64_t ftags = 0;
     bool have_free = false;
-    for (int p = 0; p < MAX_PROBE; ++p) {                          // 1) the key, and the first free slot
+    for (int p = 0; p < S::MAXP; ++p) {                          // 1) the key, and the first free slot
         const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
         const uint2 tg = ld_tags<S>(bw);
         const uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
@@ -592,9 +601,9 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
         if (empty || (known_absent && have_free)) break;
         b = (b + 1) & t.mask;
     }
-    if (!have_free) return -1;                                     // MAX_PROBE full buckets
+    if (!have_free) return -1;                                     // S::MAXP full buckets
     b = fb;
-    for (int p = 0; p < MAX_PROBE; ++p) {                          // 2) claim (one CAS per try)
+    for (int p = 0; p < S::MAXP; ++p) {                          // 2) claim (one CAS per try)
         CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
         uint64_t cur = ftags;
         if (p > 0) {
@@ -663,7 +672,7 @@ inline void host_set_ival(uint32_t *w, int s, const uint32_t *ival)
 }
 
 // Insert or overwrite on a host copy.  Returns slot, or -1 when the chain is longer
-// than MAX_PROBE (caller grows the table).
+// than S::MAXP (caller grows the table).
 template <class S>
 inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *ival)
 {
@@ -671,7 +680,7 @@ inline int64_t host_upsert(HashTable &t, const uint32_t *key, const uint32_t *iv
     const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
     int64_t free_slot = -1;
-    for (int p = 0; p < MAX_PROBE; ++p) {
+    for (int p = 0; p < S::MAXP; ++p) {
         uint32_t *w = host_bucket<S>(t, b);
         bool stop;
         int s = match_bucket<S>(w, key, tag, &stop);
@@ -705,7 +714,7 @@ inline int64_t host_find(const HashTable &t, const uint32_t *key)
     uint32_t tag;
     const uint64_t h = home_hash<S>(key, tag);
     uint64_t b = h & t.mask;
-    for (int p = 0; p < MAX_PROBE; ++p) {
+    for (int p = 0; p < S::MAXP; ++p) {
         const uint32_t *w = t.buckets + b * S::BW;
         bool stop;
         int s = match_bucket<S>(w, key, tag, &stop);

@@ -386,11 +386,13 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
         lslot = (int32_t)g.ifx[i];
     }
     RevNatOut rn{false, false, 0, 0};
-    bool defer = single && !p.ct_guard;                          // the only packet of its group
+    // the only packet of its group defers its create to k_ct_commit (not with event
+    // records, whose TRACE_TO_LXC would have to be withdrawn if the create failed)
+    bool defer = single && !p.ct_guard && !M::EV;
     const int ret = handle_policy4<M, false>(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc4, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
                                    a, m, &rn, &defer);
-    if (defer) g.gslot[i] = COMMIT4;
+    if (defer) g.gslot[i] = proxy ? COMMIT4 - COMMIT_PROXY : COMMIT4;
     if (M::EV && o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
         // the forwarded frame: ipv4_local_delivery's ipv4_l3 (bpf_netdev handle_ipv4), then
         // the policy program's reverse NAT
@@ -451,11 +453,11 @@ __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b
     }
     RevNat6Out rn;
     rn.valid = false;
-    bool defer = single && !p.ct_guard;
+    bool defer = single && !p.ct_guard && !M::EV;
     const int ret = handle_policy6<M, false>(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc6, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
                                    a, m, &rn, &defer);
-    if (defer) g.gslot[i] = COMMIT6;
+    if (defer) g.gslot[i] = proxy ? COMMIT6 - COMMIT_PROXY : COMMIT6;
     if (M::EV && o.frames && (ret == TC_ACT_OK || ret == TC_ACT_REDIRECT) && !proxy) {
         // ipv6_local_delivery's ipv6_l3, then ipv6_policy's rev-NAT index zeroing and reverse NAT
         const uint8_t *in = b.frames + (size_t)i * b.stride;
@@ -499,9 +501,18 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage6(DpParams p, BatchDev b, Out
 // ballot and one LDS atomic per wave) and then creates them with every lane busy:
 // about one packet in seven carries a create, and a lane-per-packet pass would keep
 // six lanes of seven idle while the seventh walks its insert chains.
+//
+// A deferred create cannot fail on capacity (launches that could reach max_entries
+// run guarded and do not defer) and fails on the probe limit only when CT_MAX_PROBE
+// consecutive buckets hold live entries (cv_hash.hpp).  Should one fail anyway, the
+// packet's outcome is rewritten to the reference's: ipv{4,6}_policy returns
+// DROP_CT_CREATE_FAILED, tail_ipv{4,6}_policy sends the drop notification
+// (bpf_lxc.c:946-949, 985-990) -- the forward metric the stage counted (a proxy
+// redirect counts none) moves to the drop reason; the entries written before the
+// failing one stay, as in the reference.
 constexpr uint32_t COMMIT_SPAN = BLOCK * 8;
-__device__ __forceinline__ void commit_one(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
-                                           bool v6, uint32_t now, Acct &a)
+__device__ __forceinline__ int commit_one(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
+                                          bool v6, uint32_t now, Acct &a, uint32_t &len)
 {
     const uint4 s1 = g.srec[2 * i + 1];
     uint32_t seen;
@@ -515,8 +526,9 @@ __device__ __forceinline__ void commit_one(const DpParams &p, const BatchDev &b,
         t.dport = t.sport = 0;
         ct_l4<false>(t, s.h, CT_INGRESS, seen);
         t.reverse();
+        len = s.len;
         const CtState sn{0, 0, 0, 0, 0, s1.w};
-        ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
+        return ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
     } else {
         Rec6 r;
         rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
@@ -528,12 +540,28 @@ __device__ __forceinline__ void commit_one(const DpParams &p, const BatchDev &b,
         t.dport = t.sport = 0;
         ct_l4<true>(t, s.h, CT_INGRESS, seen);
         t.reverse();
+        len = s.len;
         const CtState sn{s.daddr[3] & 0xFFFFu, 0, 0, 0, 0, s1.w};
-        ct_create<true>(G(p.eps)[s1.z & 0xFFFFu].ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
+        return ct_create<true>(G(p.eps)[s1.z & 0xFFFFu].ct6, t, s.len, CT_INGRESS, sn, now, a, false, false, true);
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, GroupScratch g, uint32_t now)
+__device__ __noinline__ void commit_failed(const DpParams &p, const OutDev &o, uint32_t i, uint32_t len, bool proxied)
+{
+    if (o.ret) o.ret[i] = TC_ACT_SHOT;
+    if (o.reason) o.reason[i] = DROP_CT_CREATE_FAILED;
+    if (o.proxy) o.proxy[i] = 0;
+    if (!p.metrics) return;
+    const uint32_t r = (uint8_t)(-DROP_CT_CREATE_FAILED);
+    atomicAdd(&p.metrics[(r * 4 + METRIC_INGRESS) * 2], 1ull);
+    atomicAdd(&p.metrics[(r * 4 + METRIC_INGRESS) * 2 + 1], (unsigned long long)len);
+    if (!proxied) {
+        atomicAdd(&p.metrics[(0 * 4 + METRIC_INGRESS) * 2], ~0ull);
+        atomicAdd(&p.metrics[(0 * 4 + METRIC_INGRESS) * 2 + 1], 0ull - len);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
 {
     __shared__ LdsPolicy pc;
     __shared__ uint32_t list[COMMIT_SPAN], lcount;
@@ -547,19 +575,23 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Gro
         for (uint32_t u = 0; u < COMMIT_SPAN / BLOCK; ++u) {
             const uint32_t i = base + u * BLOCK + threadIdx.x;
             const uint32_t mk = i < b.n ? g.gslot[i] : NONE;
-            const bool want = mk == COMMIT4 || mk == COMMIT6;
+            const bool want = mk >= COMMIT6 - COMMIT_PROXY && mk <= COMMIT4;
             const unsigned long long w = __ballot(want);
             if (!w) continue;
             uint32_t at = 0;
             if (lane == 0) at = atomicAdd(&lcount, (uint32_t)__popcll(w));
             at = __shfl(at, 0, 64);
-            if (want) list[at + __popcll(w & ((1ull << lane) - 1))] = i | (mk == COMMIT6 ? 0x80000000u : 0u);
+            const uint32_t v6 = (mk == COMMIT6 || mk == COMMIT6 - COMMIT_PROXY) ? 0x80000000u : 0u;
+            const uint32_t px = mk <= COMMIT4 - COMMIT_PROXY ? 0x40000000u : 0u;
+            if (want) list[at + __popcll(w & ((1ull << lane) - 1))] = i | v6 | px;
         }
         __syncthreads();
         const uint32_t cnt = lcount;
         for (uint32_t k = threadIdx.x; k < cnt; k += BLOCK) {
-            const uint32_t e = list[k];
-            commit_one(p, b, g, e & 0x7FFFFFFFu, e >> 31, now, a);
+            const uint32_t e = list[k], i = e & 0x3FFFFFFFu;
+            uint32_t len;
+            if (commit_one(p, b, g, i, e >> 31, now, a, len) == DROP_CT_CREATE_FAILED)
+                commit_failed(p, o, i, len, (e >> 30) & 1u);
         }
         __syncthreads();                                          // (list / lcount reuse)
     }
@@ -880,17 +912,29 @@ __global__ void k_ct_scan(HashTable t, int v6, uint64_t nslots, uint64_t *slots,
 // table, a lane per bucket: read the 8 tag bytes, then the lifetime word of every
 // live slot, and mark the expired ones dead (the bucket's tag word rewritten once;
 // the pass runs stream-ordered between batches, so it is the only writer).
+//
+// Tombstones: a lookup walks past dead slots until a bucket with an empty one, so the
+// bucket's dead slots (old deletes and this pass's) become empty again when no probe
+// chain needs to pass through bucket b.  Invariant: a live key stored in bucket s with
+// home h has no empty slot in [h, s).  If bucket b+1 has an empty slot, no key beyond
+// b+1 has its home at or before b+1; if every live key of b+1 also has its home in
+// b+1, no key past b has its home at or before b, and b's dead slots may empty.  The
+// check reads b+1 while its own lane may change it; those changes only delete keys or
+// add empty slots, which keeps the conclusion true (a key read half-deleted looks
+// displaced: the bucket then just keeps its tombstones this pass).
 template <class S>
-__device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted)
+__device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted, uint32_t *freed)
 {
-    uint32_t mine = 0;
+    uint32_t mine = 0, cleared = 0;
     for (uint64_t b = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BLOCK) {
         uint32_t *bw = t.buckets + b * S::BW;
         const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
         uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32), out = tags;
+        bool dead = false;
 #pragma unroll
         for (int sl = 0; sl < S::SPB; ++sl) {
             const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
+            if (tag == TAG_DEAD) dead = true;
             if (tag < 3) continue;
             const uint32_t life = *ct_hot<S>(t, (int64_t)(b * S::SPB + sl));   // lifetime: hot word 0
             if (life < time) {
@@ -900,10 +944,34 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
                 uint4 *c = reinterpret_cast<uint4 *>(t.vals + (b * S::SPB + sl) * CT_COLD);   // hot and side words
                 c[0] = c[1] = make_uint4(0, 0, 0, 0);
                 ++mine;
+                dead = true;
+            }
+        }
+        if (dead) {
+            const uint64_t nx = (b + 1) & t.mask;
+            const volatile uint32_t *nw = t.buckets + nx * S::BW;
+            const uint64_t ntags = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
+            bool has_empty = false, displaced = false;
+#pragma unroll
+            for (int sl = 0; sl < S::SPB; ++sl) {
+                const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
+                has_empty |= tag == TAG_EMPTY;
+                if (tag < 3) continue;
+                uint32_t key[S::KW], tg2;
+#pragma unroll
+                for (int j = 0; j < S::KW; ++j) key[j] = nw[S::KEY0 + sl * S::KS + j];
+                displaced |= (home_hash<S>(key, tg2) & t.mask) != nx;
+            }
+            if (has_empty && !displaced) {
+#pragma unroll
+                for (int sl = 0; sl < S::SPB; ++sl)
+                    if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) { out &= ~(0xFFull << (8 * sl)); ++cleared; }
             }
         }
         if (out != tags) *reinterpret_cast<uint2 *>(bw) = make_uint2((uint32_t)out, (uint32_t)(out >> 32));
     }
+    const unsigned long long fr = wave_sum(cleared);
+    if ((threadIdx.x & 63) == 0 && fr && freed) atomicAdd(freed, (uint32_t)fr);
     const unsigned long long tot = wave_sum(mine);
     if ((threadIdx.x & 63) == 0 && tot) {
         atomicAdd(deleted, (uint32_t)tot);
@@ -913,15 +981,50 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
 
 __global__ void __launch_bounds__(BLOCK) k_ct_gc(HashTable t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted)
 {
-    if (v6) ct_gc<Ct6Spec>(t, nb, time, deleted);
-    else ct_gc<Ct4Spec>(t, nb, time, deleted);
+    if (v6) ct_gc<Ct6Spec>(t, nb, time, deleted, deleted + 1);
+    else ct_gc<Ct4Spec>(t, nb, time, deleted, deleted + 1);
 }
 
+// deleted[0]: entries the pass deleted, deleted[1]: tombstones it turned back into empty slots
 int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s)
 {
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_gc, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, time, deleted);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// slots by tag class: out[0] empty, out[1] dead (tombstones), out[2] live
+template <class S>
+__device__ void ct_tags(HashTable t, uint64_t nb, unsigned long long *out)
+{
+    uint32_t c[3] = {0, 0, 0};
+    for (uint64_t b = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BLOCK) {
+        const uint32_t w = t.buckets[b * S::BW];
+#pragma unroll
+        for (int sl = 0; sl < S::SPB; ++sl) {
+            const uint32_t tag = (w >> (8 * sl)) & 0xFFu;
+            c[tag == TAG_EMPTY ? 0 : tag == TAG_DEAD ? 1 : 2]++;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const unsigned long long v = wave_sum(c[k]);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&out[k], v);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_ct_tags(HashTable t, int v6, uint64_t nb, unsigned long long *out)
+{
+    if (v6) ct_tags<Ct6Spec>(t, nb, out);
+    else ct_tags<Ct4Spec>(t, nb, out);
+}
+
+int launch_ct_tags(const HashTable &t, int v6, uint64_t nb, unsigned long long *out, hipStream_t s)
+{
+    uint64_t g = (nb + BLOCK - 1) / BLOCK;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_ct_tags, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, out);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -988,7 +1091,7 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
     launch_group_runs(g, Q_NETDEV6, grid.x, 1, s);
     if (ev) hipLaunchKernelGGL(k_ct_stage6<true>, grid, blk, 0, s, p, b, o, g, now);
     else hipLaunchKernelGGL(k_ct_stage6<false>, grid, blk, 0, s, p, b, o, g, now);
-    if (!p.ct_guard) hipLaunchKernelGGL(k_ct_commit, grid, blk, 0, s, p, b, g, now);
+    if (!p.ct_guard) hipLaunchKernelGGL(k_ct_commit, grid, blk, 0, s, p, b, o, g, now);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

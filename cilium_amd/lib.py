@@ -97,6 +97,7 @@ def load():
         "cv_map_count": (i32, [vp, i32, C.POINTER(u32)]),
         "cv_map_dump": (i32, [vp, i32, vp, vp, u32]),
         "cv_ct_gc": (i32, [vp, i32, u32, C.POINTER(u32)]),
+        "cv_ct_slots": (i32, [vp, i32, vp]),
         "cv_bind": (i32, [vp, i32, i32]),
         "cv_endpoint_add": (i32, [vp, C.c_uint16, u32, i32, i32]),
         "cv_sync": (i32, [vp]),
@@ -210,6 +211,12 @@ class Map:
         n = C.c_uint32(0)
         _check(load().cv_ct_gc(self.ctx.h, self.h, time, C.byref(n)), "cv_ct_gc")
         return n.value
+
+    def ct_slots(self):
+        """(empty, tombstone, live) slot counts of a device CT map"""
+        out = np.zeros(3, np.uint64)
+        _check(load().cv_ct_slots(self.ctx.h, self.h, out.ctypes.data), "cv_ct_slots")
+        return tuple(int(x) for x in out)
 
     def dump(self):
         n = len(self)

@@ -125,6 +125,10 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
  * the flows the node keeps (HBM: ~137 B per entry at the 60 % bucket load) and run
  * cv_ct_gc.  A batch next to the limit is processed in exact one-packet launches. */
 int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
+/* Slot occupancy of a device CT map (diagnostics, no reference counterpart): out[0]
+ * empty slots, out[1] tombstones (deleted entries not yet reclaimed by cv_ct_gc),
+ * out[2] live entries. */
+int cv_ct_slots(cv_ctx *ctx, int h, uint64_t out[3]);
 
 /* ---- binding: programs -> maps ---- */
 int cv_bind(cv_ctx *ctx, int role, int map_handle /* -1 unbinds */);

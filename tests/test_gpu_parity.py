@@ -424,6 +424,42 @@ def test_ct_gc_on_device(dev, flush):
     assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
 
 
+def test_ct_churn_fill_gc_refill(dev):
+    """Conntrack churn at about 50 % slot load: every round a fresh batch creates ~26k
+    entries (lifetime now + 60), then ctmap.GC at the next `now` deletes the previous
+    round's; six rounds against the oracle (verdicts, GC counts, live counts, the
+    table).  No create fails below max_entries (the kernel HASH map never does), and
+    k_ct_gc hands the tombstones back as empty slots, so lookup misses keep ending
+    after a bucket or two instead of walking ever-longer chains of deleted slots."""
+    w = synth.config3(1 << 16, 1 << 12, n_ep=64, n_cidrs=1024, n_ids=100, seed=41)
+    spec = w.maps["ct4"]
+    spec.max_entries = len(np.unique(spec.keys, axis=0)) + 60000       # two rounds' creates fit
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    deleted = 0
+    for v in range(1, 7):
+        now = w.now + 70 * v
+        f = H.apply_variant(w.frames, *synth.port_variant(w, v))
+        wv = synth.Workload(w.name, w.maps, f, w.length, w.mark, w.endpoints, now=now, extra=w.extra)
+        o = run_ingress(ctx, wv, dev, 0, w.n, events=False)       # (the deferred-create path)
+        ref = dp.netdev_ingress(f, w.length, w.mark, now=now)
+        for k in ("ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
+            assert (o[k] == getattr(ref, k)).all(), (v, k)
+        assert (ctx.metrics() == dp.metrics()).all()
+        assert dp.metrics()[155, 1, 0] == 0                        # no DROP_CT_CREATE_FAILED
+        g = pm["ct4"].ct_gc(now)
+        assert g == om["ct4"].ct_gc(now) > 0
+        deleted += g
+        empty, dead, live = pm["ct4"].ct_slots()
+        assert live == len(om["ct4"]) == len(pm["ct4"])
+        print(f"round {v}: gc deleted {g}, slots empty {empty} dead {dead} live {live}")
+        assert dead < deleted // 4, (dead, deleted)                # tombstones are reclaimed
+    ck, cv = pm["ct4"].dump()
+    ok, ov = om["ct4"].dump()
+    assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
+    ctx.close()
+
+
 def test_chunked_launches_config2(dev, monkeypatch):
     # batches larger than one launch chunk: per-chunk delta fold keeps counters exact
     monkeypatch.setenv("CV_MAX_CHUNK", "10007")

@@ -268,6 +268,9 @@ def main():
     ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg and the random-access probe (profiling runs)")
+    ap.add_argument("--ct-room", type=int, default=None,
+                    help="configs 3/4: max_entries = the preloaded entries + this many (0: a full table, every "
+                         "create fails; the exact-admission regime) instead of room for every create of the run")
     args = ap.parse_args()
 
     import torch
@@ -295,6 +298,8 @@ def main():
     w = make_workload(name, args.packets, rank, world)
     if stateful:
         size_conntrack(name, w, passes)
+        if args.ct_room is not None and name in ("config3", "config4"):
+            w.maps["ct4"].max_entries = len(np.unique(w.maps["ct4"].keys, axis=0)) + args.ct_room
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
     ctx, maps = H.product_ctx(w, device=local)
     log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")

@@ -183,7 +183,9 @@ struct cv_ctx {
     DevBuf eps_dev, ephot_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
-    DevBuf gtable, gnode1, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
+    DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
+    DevBuf gpkey, gent, gbig, gcnt, gwork6;   // the netdev path's binned grouping
+    DevBuf adm_ib, adm_pre, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -779,6 +781,8 @@ DpParams params(cv_ctx *c)
 {
     DpParams p{};
     p.flags = c->flags;
+    p.win_lo = 0;
+    p.win_span = ~0u;
     p.n_eps = (uint32_t)c->eps.size();
     p.cidr4_fix = c->role[CV_ROLE_CIDR4_FIX] >= 0 ? c->cidr4_fix.view : HashTable{};
     p.cidr6_fix = c->role[CV_ROLE_CIDR6_FIX] >= 0 ? c->cidr6_fix.view : HashTable{};
@@ -867,7 +871,9 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     uint64_t cap = 1024;
     while (cap < per * cmax || cap < c->gcap) cap <<= 1;
     (void)hipDeviceSynchronize();
-    if (c->gtable.alloc(cap * 16) || c->gnode1.alloc(cap * 4) || c->gsingle.alloc((size_t)cmax * 4) ||
+    if (c->gtable.alloc(cap * 16) || c->gsingle.alloc((size_t)cmax * 4) ||
+        c->gpkey.alloc((size_t)cmax * 8) || c->gent.alloc((size_t)cmax * 8) || c->gbig.alloc((size_t)cmax * 16) ||
+        c->gcnt.alloc(((size_t)GBIN_MAX * GBLK + 1 + 1024) * 4) || c->gwork6.alloc((size_t)cmax * 4) ||
         c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsrec.alloc((size_t)cmax * 32) ||
         c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) || c->gifx.alloc((size_t)cmax * 4) ||
@@ -898,8 +904,10 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     c->gslot.as<uint32_t>(), c->gnext.as<uint32_t>(), c->gsrec.as<uint4>(),
                     c->gparent.as<unsigned long long>(), c->geg.as<uint32_t>(),
                     ++c->serial, c->gorder.as<uint32_t>(), c->gcursor.as<uint32_t>(), c->gqueue.as<uint32_t>(),
-                    (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>(), nullptr,
-                    c->gsingle.as<uint32_t>()};
+                    (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>(),
+                    c->gsingle.as<uint32_t>(), c->gpkey.as<unsigned long long>(), c->gent.as<uint2>(),
+                    c->gcnt.as<uint32_t>(), c->gbig.as<unsigned long long>(), 4, c->gnext.as<uint32_t>(),
+                    c->gwork6.as<uint32_t>()};
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1113,6 +1121,81 @@ uint32_t ct_plan(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t want, ui
         m->gen++;
     }
     return (uint32_t)n;
+}
+
+// Whether a launch of n packets (each creating at most W entries per map) surely
+// fits every map's room; reads the exact live counts (after every batch already
+// submitted) when the running upper bound says it may not.  A launch that fits is
+// reserved: the bound rises by W * n.
+bool ct_fits(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t n, uint32_t W)
+{
+    auto room = [&]() {
+        uint64_t r = ~0ull;
+        for (MapObj *m : maps) r = std::min(r, m->cap > m->live_upper ? m->cap - m->live_upper : 0);
+        return r;
+    };
+    if (room() < (uint64_t)W * n) {
+        drain(c);
+        for (MapObj *m : maps) {
+            uint64_t v = 0;
+            if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
+        }
+        if (room() < (uint64_t)W * n) return false;
+    }
+    for (MapObj *m : maps) {
+        m->live_upper += (uint64_t)W * n;
+        m->gen++;
+    }
+    return true;
+}
+
+// A netdev launch next to max_entries, exact (cv_kernels.hip "conntrack admission"):
+// the front and the grouping once, k_ct_intent's bounds, then the conntrack stages in
+// windows, each planned on the device from the exact live counts as it starts.
+int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, uint32_t now, int with_prefilter,
+                 const GroupScratch &gs, const std::vector<MapObj *> &cts, hipStream_t s)
+{
+    const uint32_t n = bc.n;
+    Admit a{};
+    a.nmaps = (uint32_t)cts.size();
+    for (size_t k = 0; k < cts.size(); ++k) a.maps[k] = cts[k]->ct.view.buckets;
+    const size_t need_pre = (size_t)2 * a.nmaps * n * 4;
+    if ((c->adm_ib.n < n && c->adm_ib.alloc(n)) || (c->adm_pre.n < need_pre && c->adm_pre.alloc(need_pre)) ||
+        (!c->adm_tsum.p && c->adm_tsum.alloc(4096 * 4)) || (!c->adm_win.p && c->adm_win.alloc(8)))
+        return -ENOMEM;
+    a.ib = c->adm_ib.as<uint8_t>();
+    a.pre = c->adm_pre.as<uint32_t>();
+    a.tsum = c->adm_tsum.as<uint32_t>();
+    a.win = c->adm_win.as<uint32_t>();
+    int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
+    if (!r) r = launch_ct_intent(p, bc, gs, a, s);
+    if (r) return r;
+    uint32_t windows = 0;
+    for (uint32_t lo = 0; lo < n; ++windows) {
+        drain(c);
+        Rooms rm{};
+        for (size_t k = 0; k < cts.size(); ++k) {
+            uint64_t v = 0;
+            if (hipMemcpy(&v, cts[k]->live.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+            cts[k]->live_upper = v;
+            rm.r[k] = cts[k]->cap > v ? cts[k]->cap - v : 0;
+        }
+        uint32_t w[2];
+        if ((r = launch_window(a, n, lo, rm, s))) return r;
+        if (hipMemcpy(w, a.win, 8, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+        DpParams pw = p;
+        pw.win_lo = lo;
+        pw.win_span = w[0] - lo;
+        pw.ct_guard = w[1];
+        if ((r = launch_netdev_stages(pw, bc, now, oc, gs, s))) return r;
+        lo = w[0];
+    }
+    for (MapObj *m : cts) {
+        m->live_upper = m->cap;                                   // (re-read when the next launch plans)
+        m->gen++;
+    }
+    if (getenv("CV_ADMIT_STATS")) fprintf(stderr, "[cv admit] %u packets in %u windows\n", n, windows);
+    return 0;
 }
 
 // live policy counters of one key from HBM (device-authoritative)
@@ -1528,16 +1611,25 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
-        n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 2, (hipStream_t)stream, &p.ct_guard);
+        // a launch whose creates (at most the tuple and its ICMP twin per packet) fit runs
+        // at full width; one that may reach a CT map's max_entries runs admitted
+        // (run_admitted), or, with more CT maps than Admit holds, in one-packet guarded launches
+        n = std::min(c->chunk, b->n - off);
+        const bool fits = ct_fits(c, cts, n, 2);
+        if (!fits && cts.size() > (size_t)ADMIT_MAPS)
+            n = ct_plan(c, cts, n, 2, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
-        uint64_t ncap = 1024;                                     // the one-word node table of this launch
-        while (ncap < 2ull * n) ncap <<= 1;
-        gs.node1 = c->gnode1.as<uint32_t>();
-        gs.cap_mask = (uint32_t)(ncap - 1);
-        (void)hipMemsetAsync(gs.node1, 0, ncap * 4, (hipStream_t)stream);
-        if ((r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off, b->stride), gs,
-                                       (hipStream_t)stream)))
-            return r;
+        gs.gbits = 4;                                             // bins of ~2048 packets (at most GBIN_MAX)
+        while (gs.gbits < 13 && (1ull << (gs.gbits + 11)) < n) ++gs.gbits;
+        if (!fits && cts.size() <= (size_t)ADMIT_MAPS) {
+            r = run_admitted(c, p, chunk(b, off, n), chunk(o, off, b->stride), now, with_prefilter, gs, cts,
+                             (hipStream_t)stream);
+        } else {
+            r = launch_netdev_ingress(p, chunk(b, off, n), now, with_prefilter, chunk(o, off, b->stride), gs,
+                                      (hipStream_t)stream);
+        }
+        p.ct_guard = 0;
+        if (r) return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "netdev", (hipStream_t)stream);

@@ -625,6 +625,23 @@ __device__ __forceinline__ int policy_ingress(const HashTable &pol, uint32_t fla
     return r >= TC_ACT_OK ? r : DROP_POLICY;
 }
 
+// policy_can_access_ingress's verdict alone (no counter update, no accounting): true
+// when it returns DROP_POLICY
+__device__ __forceinline__ bool policy_ingress_denies(const HashTable &pol, uint32_t flags, uint32_t src,
+                                                      uint32_t dport_raw, uint32_t proto)
+{
+    if (!(flags & F_POLICY_INGRESS)) return (flags & F_DROP_ALL) != 0;
+    if (flags & F_DROP_ALL) return true;
+    uint32_t px[1];
+    const uint32_t kl4[2] = {src, (dport_raw & 0xFFFFu) | (proto << 16)};
+    const uint32_t kl3[2] = {src, 0u};
+    const uint32_t kwc[2] = {0u, (dport_raw & 0xFFFFu) | (proto << 16)};
+    const bool l4 = flags & F_HAVE_L4_POLICY;
+    if (l4 && dev_find_tf<PolicySpec, true>(pol, kl4, px) >= 0) return false;
+    if (dev_find_tf<PolicySpec, true>(pol, kl3, px) >= 0) return false;
+    return !(l4 && dev_find_tf<PolicySpec, true>(pol, kwc, px) >= 0);
+}
+
 // policy_can_egress (policy.h:181-200), POLICY_EGRESS && LXC_ID.  ILP: the three keys'
 // buckets read together; the IPv6 egress stage measured 3.5 % faster with the
 // sequential tag-first probes, the IPv4 one 1 % slower.
@@ -1854,43 +1871,6 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
     g.gslot[i] = s;
     const bool first = (uint32_t)(prev >> 32) != g.epoch;
     g.next[i] = first ? NONE : (uint32_t)prev;
-    const uint32_t k = blockIdx.x % QSPLIT;
-    const uint32_t at = wave_append(&g.cursor[qctr(q, k)], first);
-    if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;
-}
-
-// The netdev path's node insert: one 32-bit word per node {tag:7 | multi:1 | the
-// group's latest packet:24} (packet indexes < MAX_CHUNK = 2^24; tag 2..127, so a used
-// word is never 0; its low bit is the queue, IPv4 or IPv6), the table zeroed before
-// the launch: a packet opens its group with one CAS expecting an empty word, or joins
-// it by swapping in its own index with the multi bit set; a lost race returns the
-// word, whose tag says whether to retry on it or to move on.  Two groups of one queue
-// whose pairs share a slot chain and a tag merge into one (about 1 in 63 collisions):
-// a coarser grouping, equally exact -- a group's packets run in packet order on one
-// lane either way.  4-B words keep the table at 128 MiB
-// for 2^24 packets, and the multi bit tells k_group_flatten a singleton from the node
-// word alone.
-constexpr uint32_t NODE_MULTI = 1u << 24, NODE_IDX = NODE_MULTI - 1;
-static_assert(MAX_CHUNK <= NODE_MULTI, "a launch's packet indexes must fit the node word's 24 bits");
-__device__ __forceinline__ void group_insert1(const GroupScratch &g, uint64_t gh, uint32_t i, int q)
-{
-    const uint32_t tag = (1u + (uint32_t)(gh % 63u)) << 1 | (q == Q_NETDEV ? 0u : 1u);   // (queues never merge)
-    const uint32_t first_w = tag << 25 | i, join_w = first_w | NODE_MULTI;
-    uint32_t s = (uint32_t)(gh >> 32) & g.cap_mask;
-    CV_G uint32_t *nodes = G(g.node1);
-    uint32_t cur = 0;
-    for (;;) {
-        if (__hip_atomic_compare_exchange_strong(nodes + s, &cur, cur ? join_w : first_w, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            break;
-        if ((cur >> 25) != tag) {                                 // another group's node: next slot
-            s = (s + 1) & g.cap_mask;
-            cur = 0;
-        }
-    }
-    const bool first = cur == 0;
-    g.gslot[i] = s;
-    g.next[i] = first ? NONE : (cur & NODE_IDX);
     const uint32_t k = blockIdx.x % QSPLIT;
     const uint32_t at = wave_append(&g.cursor[qctr(q, k)], first);
     if (first) g.queue[((size_t)qbank(q) * QSPLIT + k) * g.qregion + at] = s;

@@ -69,8 +69,24 @@ struct DpParams {              // by value as the kernel argument
     uint32_t *trace_count;
     uint32_t trace_agg;        // MONITOR_AGGREGATION
     uint32_t ingress_ifindex;  // skb->ingress_ifindex of from_netdev
-    uint32_t ct_guard;         // 1: a one-packet launch next to a CT map's max_entries (exact check per create)
+    uint32_t ct_guard;         // 1: creates check the CT map's live count against max_entries (cv_ctx.cpp admission)
+    uint32_t win_lo, win_span; // the conntrack stages run the packets in [win_lo, win_lo + win_span) (admission
+                               // windows; 0, ~0 otherwise)
 };
+
+// Exact conntrack admission next to max_entries (cv_ctx.cpp, k_ct_intent): per packet
+// of a launch an upper bound of the entries it creates (U) and deletes (D) in its CT
+// map, and per map their inclusive prefix sums over the launch.
+constexpr int ADMIT_MAPS = 4;
+struct Admit {
+    const uint32_t *maps[ADMIT_MAPS];  // bucket arrays of the launch's CT maps (map index = position)
+    uint32_t nmaps;
+    uint8_t *ib;                       // per packet: U | D << 2 | map << 3
+    uint32_t *pre;                     // [2 * map + (0: U, 1: D)] * n + i: inclusive prefix sums
+    uint32_t *tsum;                    // scan tile sums
+    uint32_t *win;                     // k_window out: {hi, guarded}
+};
+struct Rooms { unsigned long long r[ADMIT_MAPS]; };
 
 struct BatchDev {
     const uint8_t *frames;
@@ -114,12 +130,21 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t qregion;          // words per region
     uint32_t *work;            // per group: `order` offset of its run, in size-class order
     uint32_t *ifx;             // per packet: the destination endpoint's ifindex (netdev path)
-    uint32_t *node1;           // netdev path: one-word nodes {tag:7 | multi:1 | head packet:24},
-                               // zeroed per launch (cap_mask + 1 words), or null (the
-                               // epoch-tagged table)
     uint32_t *single;          // the packets of singleton groups, dense (k_group_flatten with a
-                               // schedule; cursor[SINGLE_WORD0 + q] of them)
+                               // schedule, k_gbin_group; cursor[SINGLE_WORD0 + q] of them)
+    // netdev path (k_gkey_hist / k_gkey_scatter / k_gbin_group): groups by binning
+    unsigned long long *pkey;  // per packet: the address-pair key of a staged packet, 0 if none
+    uint2 *gent;               // staged packets binned by key: {packet, key low word}
+    uint32_t *gcnt;            // per (bin, count block) counts, scanned into offsets in place;
+                               // [nbins * GBLK] = the staged total
+    unsigned long long *gbig;  // sort space of bins too large for LDS: 2 words per packet
+    uint32_t gbits;            // log2 of the number of bins
+    uint32_t *single6;         // the singleton packets of the IPv6 queue (Q_NETDEV6)
+    uint32_t *work6;           // the IPv6 queue's schedule (`work` of Q_NETDEV6)
 };
+// binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
+// the most bins (2^gbits) a launch uses
+constexpr uint32_t GBLK = 256, GBIN_MAX = 1u << 13;
 // GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
 // contention on one counter); blocks b with b % QSPLIT == k hold at most
 // n / QSPLIT + BLOCK + QSPLIT packets (grids are multiples of QSPLIT or one block per 256
@@ -152,6 +177,16 @@ int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, 
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter,
                           const OutDev &o, const GroupScratch &g, hipStream_t s);
+// the same in parts: front + grouping + schedules, then (per admission window) the
+// conntrack stages and the commit of deferred creates
+int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter, const OutDev &o,
+                        const GroupScratch &g, hipStream_t s);
+int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, const GroupScratch &g,
+                         hipStream_t s);
+// admission: U / D per packet and their prefix sums per map (after launch_netdev_front)
+int launch_ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s);
+// the admission window from packet lo: out {hi, guarded} in a.win
+int launch_window(const Admit &a, uint32_t n, uint32_t lo, const Rooms &r, hipStream_t s);
 // config 5: from-container of the packets' source endpoints (src_ep[i], or ep0)
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s);

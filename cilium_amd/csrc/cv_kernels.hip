@@ -330,16 +330,22 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
                 else ret = h;
             }
         }
-        if (staged) {                                             // group by (CT map, address pair)
+        // the group key (CT map, address pair) of a packet handed to the policy program:
+        // bit 0 = its queue (0 IPv4, 1 IPv6), bit 1 set (never 0); k_gbin_group bins and
+        // groups by it
+        unsigned long long gkey = 0;
+        if (staged) {
             const uint32_t ct_id = G(p.ephot)[smeta & 0xFFFFu].ct_id;
-            group_insert1(g, pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ct_id << 17), i, Q_NETDEV);
+            gkey = (pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ct_id << 17) & ~3ull) | 2ull;
         } else if (v6stage) {
             const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
             const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
             const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
-            group_insert1(g, pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets), i, Q_NETDEV6);
+            gkey = (pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets) & ~3ull) | 3ull;
         }
         if (!live) continue;
+        g.pkey[i] = gkey;
+        g.gslot[i] = NONE;
         const bool fwd_here = !staged && !v6stage && ret == TC_ACT_OK;
         if (M::EV && o.frames) {
             uint8_t *fo = o.frames + (size_t)i * b.stride;
@@ -350,7 +356,6 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
             }
         }
         if (!staged && !v6stage) {
-            g.gslot[i] = NONE;
             if (o.ret) o.ret[i] = ret;
             if (o.reason) o.reason[i] = reason;
             if (o.ct) o.ct[i] = CT_NONE;
@@ -424,7 +429,9 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutD
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_run<true>(g, Q_NETDEV, false, [&](uint32_t x, uint32_t n) { stage2_one(p, b, o, g, x, now, m, n == 1); });
+    for_each_run<true>(g, Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
+        if (x - p.win_lo < p.win_span) stage2_one(p, b, o, g, x, now, m, n == 1);     // (admission windows)
+    });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
 }
@@ -486,7 +493,9 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage6(DpParams p, BatchDev b, Out
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_run<true>(g, Q_NETDEV6, false, [&](uint32_t x, uint32_t n) { stage2_one6(p, b, o, g, x, now, m, n == 1); });
+    for_each_run<true>(g, Q_NETDEV6, false, [&](uint32_t x, uint32_t n) {
+        if (x - p.win_lo < p.win_span) stage2_one6(p, b, o, g, x, now, m, n == 1);
+    });
     met_flush(m, p.metrics);
     pol_cache_flush(pc);
 }
@@ -574,7 +583,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Out
 #pragma unroll
         for (uint32_t u = 0; u < COMMIT_SPAN / BLOCK; ++u) {
             const uint32_t i = base + u * BLOCK + threadIdx.x;
-            const uint32_t mk = i < b.n ? g.gslot[i] : NONE;
+            const uint32_t mk = i < b.n && i - p.win_lo < p.win_span ? g.gslot[i] : NONE;
             const bool want = mk >= COMMIT6 - COMMIT_PROXY && mk <= COMMIT4;
             const unsigned long long w = __ballot(want);
             if (!w) continue;
@@ -630,19 +639,8 @@ __global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, 
             head[u] = x[u] = NONE;
             if (j >= total) continue;
             ent[u] = queue_entry(g, q, n, j);
-            uint32_t nw = NODE_MULTI;
-            if (g.node1) {
-                nw = g.node1[*ent[u]];
-                head[u] = nw & NODE_IDX;
-            } else {
-                head[u] = (uint32_t)g.table[2 * *ent[u] + 1];
-            }
-            if (nw & NODE_MULTI) {
-                x[u] = head[u];
-            } else {                                              // a netdev singleton: no list walk
-                m[u][0] = head[u];
-                cnt[u] = 1;
-            }
+            head[u] = (uint32_t)g.table[2 * *ent[u] + 1];
+            x[u] = head[u];
         }
         for (bool more = true; more;) {                           // the member lists, in lockstep
             more = false;
@@ -784,6 +782,255 @@ void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStr
 {
     hipLaunchKernelGGL(k_group_flatten, dim3(grid), dim3(BLOCK), 0, s, g, q, sched != 0);
     if (sched) hipLaunchKernelGGL(k_group_schedule, dim3(grid), dim3(BLOCK), 0, s, g, q, sched == 1);
+}
+
+// ------------------------------------------------------------------ binned grouping
+// The netdev path groups its packets by (CT map, address pair) without an atomic per
+// packet: k_netdev_front writes each staged packet's 64-bit key (0: not staged);
+// k_gkey_hist counts the keys per (bin = the key's top gbits bits, binning block) in
+// LDS; three small kernels scan the counts into offsets; k_gkey_scatter writes every
+// staged packet as {packet, key low word} into its bin's slice; k_gbin_group sorts each
+// bin by (key low word, packet) -- in LDS, or for a bin past LCAP entries (a hot
+// address pair) in global memory -- so a group's members end up contiguous and in packet
+// order, and emits the runs {size, members} and the singletons exactly as
+// k_group_flatten does for the node-table queues (k_group_schedule and the stages read
+// them unchanged).  Keys that share the bin bits and the low word merge into one group
+// (about 2^-32 per pair of groups in a bin): a coarser grouping, equally exact.
+// Measured against the node-table join it replaces (one CAS per packet into a 128 MiB
+// table at the device's atomic rate, k_group_flatten's list walks, the table memset):
+// see DESIGN.md §5.
+constexpr uint32_t SCAN_TILE = 4096;                             // entries per scan block (1024 x 4)
+constexpr uint32_t LCAP = 4096;                                  // bin entries sorted in LDS
+
+__device__ __forceinline__ uint32_t gkey_bin(unsigned long long k, uint32_t bits)
+{
+    return (uint32_t)(k >> (64 - bits));
+}
+
+// exclusive scan of one value per thread over a block of up to 1024 threads
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, uint32_t &total)
+{
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += t;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t w = 0; w < nw; ++w) { const uint32_t t = wsum[w]; wsum[w] = acc; acc += t; }
+        wsum[16] = acc;
+    }
+    __syncthreads();
+    total = wsum[16];
+    const uint32_t r = wsum[wv] + incl - v;
+    __syncthreads();                                              // (wsum reuse)
+    return r;
+}
+
+__global__ void __launch_bounds__(1024) k_gkey_hist(GroupScratch g, uint32_t n)
+{
+    extern __shared__ uint32_t hist[];                           // one counter per bin
+    const uint32_t nb = 1u << g.gbits;
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[j] = 0;
+    __syncthreads();
+    const uint32_t tile = (n + GBLK - 1) / GBLK, lo = blockIdx.x * tile, hi = min(n, lo + tile);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const unsigned long long k = g.pkey[i];
+        if (k) atomicAdd(&hist[gkey_bin(k, g.gbits)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) g.gcnt[j * GBLK + blockIdx.x] = hist[j];
+}
+
+// Scan of L u32 values in place (the bin-major counts here, the admission prefixes
+// below): tile sums (SCAN_TILE values per block), their exclusive scan (+ the total)
+// by one block, then each tile scanned with its offset, exclusive or inclusive.
+__global__ void __launch_bounds__(1024) k_scan_tiles(const uint32_t *c, uint32_t L, uint32_t *tsum)
+{
+    __shared__ uint32_t wsum[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; ++k) v += j + k < L ? c[j + k] : 0u;
+    uint32_t total;
+    block_excl_scan(v, wsum, total);
+    if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_top(uint32_t *tsum, uint32_t tiles, uint32_t *total_out)
+{
+    __shared__ uint32_t wsum[17];
+    uint32_t v[4], sum = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t t = threadIdx.x * 4 + k;
+        v[k] = t < tiles ? tsum[t] : 0u;
+        sum += v[k];
+    }
+    uint32_t total;
+    uint32_t e = block_excl_scan(sum, wsum, total);
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t t = threadIdx.x * 4 + k;
+        if (t < tiles) tsum[t] = e;
+        e += v[k];
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = total;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_apply(uint32_t *c, uint32_t L, const uint32_t *tsum, int inclusive)
+{
+    __shared__ uint32_t wsum[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    uint32_t v[4], sum = 0;
+    for (uint32_t k = 0; k < 4; ++k) { v[k] = j + k < L ? c[j + k] : 0u; sum += v[k]; }
+    uint32_t total;
+    uint32_t e = block_excl_scan(sum, wsum, total) + tsum[blockIdx.x];
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (j + k < L) c[j + k] = inclusive ? e + v[k] : e;
+        e += v[k];
+    }
+}
+
+// in-place scan of c[0, L) (L <= SCAN_TILE * 4096); tsum: ceil(L / SCAN_TILE) words
+void launch_scan(uint32_t *c, uint32_t L, uint32_t *tsum, uint32_t *total_out, bool inclusive, hipStream_t s)
+{
+    const uint32_t tiles = (L + SCAN_TILE - 1) / SCAN_TILE;
+    if (!tiles) return;
+    hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(1024), 0, s, c, L, tsum);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tsum, tiles, total_out);
+    hipLaunchKernelGGL(k_scan_apply, dim3(tiles), dim3(1024), 0, s, c, L, tsum, inclusive ? 1 : 0);
+}
+
+__global__ void __launch_bounds__(1024) k_gkey_scatter(GroupScratch g, uint32_t n)
+{
+    extern __shared__ uint32_t pos[];                            // the block's next slot per bin
+    const uint32_t nb = 1u << g.gbits;
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) pos[j] = g.gcnt[j * GBLK + blockIdx.x];
+    __syncthreads();
+    const uint32_t tile = (n + GBLK - 1) / GBLK, lo = blockIdx.x * tile, hi = min(n, lo + tile);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const unsigned long long k = g.pkey[i];
+        if (!k) continue;
+        const uint32_t at = atomicAdd(&pos[gkey_bin(k, g.gbits)], 1u);
+        g.gent[at] = make_uint2(i, (uint32_t)k);
+    }
+}
+
+// ascending bitonic sort of v[0, p), p a power of two, by the block's threads
+template <class P>
+__device__ __forceinline__ void bitonic_sort(P v, uint32_t p)
+{
+    for (uint32_t k = 2; k <= p; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < p / 2; t += blockDim.x) {
+                const uint32_t i = 2 * j * (t / j) + (t % j), l = i + j;
+                const unsigned long long a = v[i], b = v[l];
+                if ((a > b) == ((i & k) == 0)) { v[i] = b; v[l] = a; }
+            }
+            __syncthreads();
+        }
+}
+
+// a sub-queue region of queue q with room for cnt more entries (starting at sub-queue
+// k0): returns the region and the first entry (regions hold n / QSPLIT + 512 words and
+// the queue at most n / 2 runs, so one always has room)
+__device__ __forceinline__ uint32_t *queue_reserve(const GroupScratch &g, int q, uint32_t k0, uint32_t cnt)
+{
+    for (uint32_t t = 0; t < QSPLIT; ++t) {
+        const uint32_t k = (k0 + t) % QSPLIT;
+        uint32_t *ctr = &g.cursor[qctr(q, k)];
+        uint32_t cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (cur + cnt <= g.qregion) {
+            if (__hip_atomic_compare_exchange_strong(ctr, &cur, cur + cnt, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                return g.queue + ((size_t)qbank(q) * QSPLIT + k) * g.qregion + cur;
+        }
+    }
+    return nullptr;                                               // (unreachable, see above)
+}
+
+__global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
+{
+    __shared__ unsigned long long lv[LCAP];
+    __shared__ uint32_t tot[5], fill[5], hist[2][NCLASS], big[2];
+    __shared__ uint32_t *qbase[2];
+    __shared__ uint32_t base[3];
+    const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
+    const uint32_t start = g.gcnt[b * GBLK], end = b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m];
+    const uint32_t nb = end - start;
+    if (!nb) return;                                              // (block-uniform)
+    uint32_t p = 64;
+    while (p < nb) p <<= 1;
+    if (threadIdx.x < 5) tot[threadIdx.x] = fill[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * NCLASS) hist[threadIdx.x / NCLASS][threadIdx.x % NCLASS] = 0;
+    if (threadIdx.x < 2) big[threadIdx.x] = 0;
+    // composite {key low word, packet}: sorted, a group's members are contiguous and ascending
+    unsigned long long *gv = g.gbig + 2 * (size_t)start;          // (a bin past LCAP: 2 words per entry)
+    const bool in_lds = nb <= LCAP;
+    for (uint32_t j = threadIdx.x; j < p; j += blockDim.x) {
+        unsigned long long x = ~0ull;
+        if (j < nb) { const uint2 e = g.gent[start + j]; x = (unsigned long long)e.y << 32 | e.x; }
+        if (in_lds) lv[j] = x; else gv[j] = x;
+    }
+    __syncthreads();
+    if (in_lds) bitonic_sort(lv, p); else bitonic_sort(gv, p);
+    const unsigned long long *v = in_lds ? lv : gv;
+    // pass 1: sizes -> totals
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        const uint32_t key = (uint32_t)(v[j] >> 32);
+        if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;     // not a group's first member
+        uint32_t c = 1;
+        while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
+        const int q6 = key & 1u;
+        if (c == 1) atomicAdd(&tot[1 + q6], 1u);
+        else { atomicAdd(&tot[0], c + 1); atomicAdd(&tot[3 + q6], 1u); atomicMax(&big[q6], c); }
+        atomicAdd(&hist[q6][size_class(c)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        base[0] = tot[0] ? atomicAdd(&g.cursor[RUN_CURSOR], tot[0]) : 0u;
+        base[1] = tot[1] ? atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV], tot[1]) : 0u;
+        base[2] = tot[2] ? atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV6], tot[2]) : 0u;
+        qbase[0] = tot[3] ? queue_reserve(g, Q_NETDEV, b % QSPLIT, tot[3]) : nullptr;
+        qbase[1] = tot[4] ? queue_reserve(g, Q_NETDEV6, b % QSPLIT, tot[4]) : nullptr;
+    }
+    if (threadIdx.x < 2 * NCLASS) {
+        const int q6 = threadIdx.x / NCLASS, c = threadIdx.x % NCLASS;
+        const uint32_t h = hist[q6][c];
+        if (h) atomicAdd(&g.cursor[qcls(q6 ? Q_NETDEV6 : Q_NETDEV, c)], h);
+    }
+    if (threadIdx.x < 2 && big[threadIdx.x] > 8)
+        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : Q_NETDEV)], big[threadIdx.x]);
+    __syncthreads();
+    // pass 2: write the singletons, the runs and their queue entries
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        const uint32_t key = (uint32_t)(v[j] >> 32);
+        if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;
+        uint32_t c = 1;
+        while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
+        const int q6 = key & 1u;
+        if (c == 1) {
+            uint32_t *single = q6 ? g.single6 : g.single;
+            single[base[1 + q6] + atomicAdd(&fill[1 + q6], 1u)] = (uint32_t)v[j];
+        } else {
+            const uint32_t off = base[0] + atomicAdd(&fill[0], c + 1);
+            uint32_t *o = g.order + off;
+            o[0] = c;
+            for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
+            qbase[q6][atomicAdd(&fill[3 + q6], 1u)] = off;
+        }
+    }
+}
+
+void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
+{
+    const uint32_t nb = 1u << g.gbits, m = nb * GBLK;
+    hipLaunchKernelGGL(k_gkey_hist, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
+    launch_scan(g.gcnt, m, g.gcnt + m + 1, g.gcnt + m, false, s);
+    hipLaunchKernelGGL(k_gkey_scatter, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
+    hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g);
 }
 
 // ------------------------------------------------------------------ CT map API
@@ -1074,8 +1321,8 @@ int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const Ou
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter, const OutDev &o,
-                          const GroupScratch &g, hipStream_t s)
+int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter, const OutDev &o,
+                        const GroupScratch &g, hipStream_t s)
 {
     if (!b.n) return 0;
     const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
@@ -1083,15 +1330,180 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
     if (ev) hipLaunchKernelGGL(k_netdev_front<true>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     else hipLaunchKernelGGL(k_netdev_front<false>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     if (hipGetLastError() != hipSuccess) return -5;
-    launch_group_runs(g, Q_NETDEV, grid.x, 1, s);
+    launch_gbin_groups(g, b.n, s);                                // both families' runs and singletons
+    hipLaunchKernelGGL(k_group_schedule, grid, blk, 0, s, g, Q_NETDEV, true);
+    GroupScratch g6 = g;
+    g6.work = g.work6;
+    hipLaunchKernelGGL(k_group_schedule, grid, blk, 0, s, g6, Q_NETDEV6, true);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// the IPv4 runs, then the IPv6 runs (the two families' conntrack state is disjoint, so
+// the order between them is free), then the deferred creates
+int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, const GroupScratch &g,
+                         hipStream_t s)
+{
+    if (!b.n) return 0;
+    const bool ev = o.frames || p.notify || p.trace;
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
     if (ev) hipLaunchKernelGGL(k_ct_stage<true>, grid, blk, 0, s, p, b, o, g, now);
     else hipLaunchKernelGGL(k_ct_stage<false>, grid, blk, 0, s, p, b, o, g, now);
-    // the IPv6 groups after the IPv4 stage: their runs reuse `work` (the two families'
-    // conntrack state is disjoint, so the order between them is free)
-    launch_group_runs(g, Q_NETDEV6, grid.x, 1, s);
-    if (ev) hipLaunchKernelGGL(k_ct_stage6<true>, grid, blk, 0, s, p, b, o, g, now);
-    else hipLaunchKernelGGL(k_ct_stage6<false>, grid, blk, 0, s, p, b, o, g, now);
+    GroupScratch g6 = g;
+    g6.single = g.single6;
+    g6.work = g.work6;
+    if (ev) hipLaunchKernelGGL(k_ct_stage6<true>, grid, blk, 0, s, p, b, o, g6, now);
+    else hipLaunchKernelGGL(k_ct_stage6<false>, grid, blk, 0, s, p, b, o, g6, now);
     if (!p.ct_guard) hipLaunchKernelGGL(k_ct_commit, grid, blk, 0, s, p, b, o, g, now);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter, const OutDev &o,
+                          const GroupScratch &g, hipStream_t s)
+{
+    const int r = launch_netdev_front(p, b, with_prefilter, o, g, s);
+    return r ? r : launch_netdev_stages(p, b, now, o, g, s);
+}
+
+// ------------------------------------------------------------------ conntrack admission
+// Next to a CT map's max_entries the batch result depends on the order of creates and
+// deletes across groups (a create fails once the count reaches max_entries, a delete
+// makes room).  The host then runs a launch in windows of packets that are exact under
+// parallel execution (cv_ctx.cpp run_admitted): a window whose creates all fit in
+// every map's room runs unguarded; one whose maps without room see no delete runs
+// guarded (each create checks the count: the count cannot move inside the window, so
+// every create into a full map fails, the others succeed, in any order); otherwise one
+// packet.  What a packet can create or delete comes from k_ct_intent, read-only against
+// the tables as the launch starts: ipv4_policy / ipv6_policy (bpf_lxc.c:865-979,
+// 721-849) create the tuple and its ICMP twin (U = 2) only on CT_NEW with an allowing
+// verdict and delete (D = 1) only on CT_ESTABLISHED with a denying one; a packet after a
+// group member that may have changed the table gets U = 2, D = 1 (its lookup may
+// differ from the launch-start table's).
+template <bool V6>
+__device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
+                                              bool hist, const uint32_t *&map)
+{
+    const uint4 s1 = g.srec[2 * i + 1];
+    const uint32_t meta = s1.z, src = s1.w;
+    uint32_t seen;
+    if constexpr (!V6) {
+        const EpDev ep = ep_stage4<false>(p, meta & 0xFFFFu);
+        map = ep.ct4.buckets;
+        if ((p.flags & F_DROP_ALL) || !ep.ipv4) return 0;
+        const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
+        if (s.len < 34) return 0;
+        Tuple4 t;
+        t.nexthdr = s.nexthdr; t.daddr = s.daddr; t.saddr = s.saddr; t.dport = t.sport = 0;
+        if (ct_l4<false>(t, s.h, CT_INGRESS, seen) < 0) return 0;
+        if (hist) return 2u | 4u;
+        Tuple4 t2 = t;
+        t2.reverse();
+        uint32_t k1[Tuple4::KW], k2[Tuple4::KW];
+        t.key(k1);
+        t2.key(k2);
+        if (dev_find<Ct4Spec>(ep.ct4, k1, nullptr) >= 0) return 0;          // CT_REPLY / CT_RELATED
+        const bool est = dev_find<Ct4Spec>(ep.ct4, k2, nullptr) >= 0;
+        const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
+        return est ? (deny ? 4u : 0u) : (deny ? 0u : 2u);
+    } else {
+        const EpDev ep = G(p.eps)[meta & 0xFFFFu];
+        map = ep.ct6.buckets;
+        if (p.flags & F_DROP_ALL) return 0;
+        Rec6 r;
+        rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
+        const Skb6 s = skb6_from(r);
+        if (s.len < 54 || s.l4off < 0) return 0;
+        Tuple6 t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
+        t.nexthdr = s.nexthdr;
+        t.dport = t.sport = 0;
+        if (ct_l4<true>(t, s.h, CT_INGRESS, seen) < 0) return 0;
+        if (hist) return 2u | 4u;
+        Tuple6 t2 = t;
+        t2.reverse();
+        uint32_t k1[Tuple6::KW], k2[Tuple6::KW];
+        t.key(k1);
+        t2.key(k2);
+        if (dev_find<Ct6Spec>(ep.ct6, k1, nullptr) >= 0) return 0;
+        const bool est = dev_find<Ct6Spec>(ep.ct6, k2, nullptr) >= 0;
+        const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
+        return est ? (deny ? 4u : 0u) : (deny ? 0u : 2u);
+    }
+}
+
+template <bool V6>
+__global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, GroupScratch g, Admit a)
+{
+    bool hist = false;
+    uint32_t left = 0;                                            // members of the current run still to come
+    for_each_run<true>(g, V6 ? Q_NETDEV6 : Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
+        if (!left) { left = n; hist = false; }                    // (a lane's runs come one after another)
+        --left;
+        const uint32_t *map = nullptr;
+        const uint32_t ud = ct_intent<V6>(p, b, g, x, hist, map);
+        uint32_t mi = 0;
+#pragma unroll
+        for (int k = 0; k < ADMIT_MAPS; ++k)
+            if ((uint32_t)k < a.nmaps && a.maps[k] == map) mi = k;
+        a.ib[x] = (uint8_t)(ud | mi << 3);
+        hist = hist || ud;
+    });
+}
+__global__ void __launch_bounds__(BLOCK) k_admit_extract(Admit a, uint32_t n)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint32_t v = a.ib[i], mi = v >> 3;
+        for (uint32_t m = 0; m < a.nmaps; ++m) {
+            a.pre[(size_t)(2 * m) * n + i] = m == mi ? (v & 3u) : 0u;
+            a.pre[(size_t)(2 * m + 1) * n + i] = m == mi ? (v >> 2) & 1u : 0u;
+        }
+    }
+}
+
+int launch_ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s)
+{
+    if (!b.n) return 0;
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
+    (void)hipMemsetAsync(a.ib, 0, b.n, s);
+    hipLaunchKernelGGL(k_ct_intent<false>, grid, blk, 0, s, p, b, g, a);
+    GroupScratch g6 = g;
+    g6.single = g.single6;
+    g6.work = g.work6;
+    hipLaunchKernelGGL(k_ct_intent<true>, grid, blk, 0, s, p, b, g6, a);
+    hipLaunchKernelGGL(k_admit_extract, grid, blk, 0, s, a, b.n);
+    for (uint32_t k = 0; k < 2 * a.nmaps; ++k) launch_scan(a.pre + (size_t)k * b.n, b.n, a.tsum, nullptr, true, s);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// The next window [lo, hi) (one thread: binary searches over the prefix sums).  A map
+// with room bounds the window by its possible creates (their sum must fit the room); a
+// full map by its first possible delete, and makes the window guarded.
+__global__ void k_window(Admit a, uint32_t n, uint32_t lo, Rooms r)
+{
+    if (threadIdx.x || blockIdx.x) return;
+    uint32_t hi = n, guarded = 0;
+    for (uint32_t m = 0; m < a.nmaps; ++m) {
+        const uint32_t *pu = a.pre + (size_t)(2 * m) * n, *pd = pu + n;
+        const uint32_t *pre = r.r[m] ? pu : pd;
+        const unsigned long long lim = r.r[m] ? r.r[m] : 0ull;  // the window's sum may reach lim
+        guarded |= r.r[m] ? 0u : 1u;
+        const uint32_t base = lo ? pre[lo - 1] : 0u;
+        if ((unsigned long long)(pre[n - 1] - base) <= lim) continue;
+        uint32_t L = lo, R = n - 1;                              // first p with pre[p] - base > lim
+        while (L < R) {
+            const uint32_t mid = L + (R - L) / 2;
+            if ((unsigned long long)(pre[mid] - base) > lim) R = mid; else L = mid + 1;
+        }
+        hi = min(hi, L);
+    }
+    if (hi <= lo) { hi = lo + 1; guarded = 1; }
+    a.win[0] = hi;
+    a.win[1] = guarded;
+}
+
+int launch_window(const Admit &a, uint32_t n, uint32_t lo, const Rooms &r, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_window, dim3(1), dim3(64), 0, s, a, n, lo, r);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

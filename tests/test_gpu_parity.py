@@ -424,6 +424,40 @@ def test_ct_gc_on_device(dev, flush):
     assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all()
 
 
+def test_ct_capacity_admission_full_width(dev):
+    """A 2^20-packet config-3 batch that crosses max_entries half way (exact admission,
+    cv_ctx.cpp run_admitted): DROP_CT_CREATE_FAILED at exactly the oracle's packets, in
+    a handful of windows instead of one launch per packet; then a batch into the full
+    table after the agent removed policy entries, so established flows are denied and
+    their deletes make room that later packets' creates take, in packet order."""
+    w = synth.config3(1 << 20, 1 << 16, n_ep=256, n_cidrs=4096, n_ids=400, seed=51)
+    spec = w.maps["ct4"]
+    spec.max_entries = len(np.unique(spec.keys, axis=0)) + 200_000
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    for v in (0, 1):
+        if v == 1:                                                 # deny a third of the L4 entries
+            keys = w.maps["policy"].keys
+            for k in keys[(keys[:, 6] != 0)][::3]:
+                assert pm["policy"].delete(k.tobytes()) == 0 == om["policy"].delete(k.tobytes())
+        f = H.apply_variant(w.frames, *synth.port_variant(w, v))
+        wv = synth.Workload(w.name, w.maps, f, w.length, w.mark, w.endpoints, now=w.now + v, extra=w.extra)
+        o = run_ingress(ctx, wv, dev, 0, w.n, events=False)
+        ref = dp.netdev_ingress(f, w.length, w.mark, now=w.now + v)
+        for k in ("ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
+            bad = np.nonzero(o[k] != getattr(ref, k))[0]
+            assert len(bad) == 0, (v, k, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+        assert (ctx.metrics() == dp.metrics()).all()
+        assert len(pm["ct4"]) == len(om["ct4"]) == spec.max_entries or v == 1
+        ck, cv = pm["ct4"].dump()
+        assert H.table_digest(ck, cv) == om["ct4"].digest()
+        check_policy_maps(pm["policy"], om["policy"])
+    m = dp.metrics()
+    assert m[155, 1, 0] > 50_000                                   # DROP_CT_CREATE_FAILED happened
+    assert m[133, 1, 0] > 0                                        # DROP_POLICY
+    ctx.close()
+
+
 def test_ct_churn_fill_gc_refill(dev):
     """Conntrack churn at about 50 % slot load: every round a fresh batch creates ~26k
     entries (lifetime now + 60), then ctmap.GC at the next `now` deletes the previous

@@ -124,9 +124,13 @@ struct DevLpm4 {
 
 struct DevLpm6 {
     DevHash h;
-    DevBuf lens;
+    DevBuf lens;                 // LENS_CAP bytes: the distinct prefix lengths, descending
     Lpm6 view{};
+    // host side for incremental updates (ipcache): live entries, entries per length
+    uint64_t live = 0;
+    std::map<int, uint32_t> lens_cnt;
 };
+constexpr size_t LENS_CAP = 160;
 
 enum MapKind { MK_PLAIN = 0, MK_CT4 = 1, MK_CT6 = 2 };
 
@@ -161,6 +165,38 @@ struct Endpoint {
     uint32_t ipv4 = 0;         // LXC_IPV4 (raw); set by cv_endpoint_config
     uint32_t ipv6[4] = {0, 0, 0, 0};
     uint32_t mac[2] = {0, 0}, node_mac[2] = {0, 0};
+};
+
+// Stream-ordered publication of the agent's incremental table writes: the changed
+// words are gathered on the host while the writes are applied to the host images, then
+// at the batch boundary one pinned staging buffer goes to the device (one async copy)
+// and k_patch writes every run of words into its table, in the stream of the batch
+// about to run: batches already submitted see the old words, later ones the new --
+// the kernel's RCU per-element visibility at batch granularity, without waiting for
+// the device.
+struct PatchQueue {
+    std::vector<PatchRec> recs;
+    std::vector<uint32_t> words;
+    void add(void *dst, const void *src, size_t nwords)
+    {
+        if (!nwords) return;
+        recs.push_back(PatchRec{reinterpret_cast<unsigned long long>(dst), (uint32_t)nwords, (uint32_t)words.size()});
+        const uint32_t *w = static_cast<const uint32_t *>(src);
+        words.insert(words.end(), w, w + nwords);
+    }
+    size_t mark() const { return recs.size(); }
+    void undo(size_t m)                        // (a role falling back to a full compile)
+    {
+        if (m >= recs.size()) return;
+        words.resize(recs[m].src);
+        recs.resize(m);
+    }
+};
+
+struct Staging {                               // pinned host + device staging of one publication
+    void *host = nullptr, *dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;                 // recorded after its k_patch
 };
 
 }  // namespace
@@ -201,6 +237,13 @@ struct cv_ctx {
     cv_trace_notify *trace = nullptr;
     uint32_t trace_cap = 0, trace_agg = 0, ingress_ifindex = 0;
     uint32_t *trace_count = nullptr;
+    // table publication (PatchQueue) and batch ordering across streams
+    PatchQueue pq;
+    std::vector<Staging> staging;
+    hipEvent_t last_ev = nullptr;              // the last batch's (or publication's) completion
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
+    uint64_t publications = 0, full_compiles = 0;
 };
 
 namespace {
@@ -303,12 +346,13 @@ int upload_lpm4(DevLpm4 &d, std::vector<Pfx> &px, bool image = false)
     return r;
 }
 
-// copy words [lo, hi) of a host array to the same offsets of a device buffer
-int put_words(const DevBuf &dst, const uint32_t *src, size_t lo, size_t hi)
+// words [lo, hi) of a host image to the same offsets of its device buffer, published
+// at the batch boundary (PatchQueue)
+int put_words(PatchQueue &pq, const DevBuf &dst, const uint32_t *src, size_t lo, size_t hi)
 {
     if (hi <= lo) return 0;
-    return hipMemcpy(static_cast<uint32_t *>(dst.p) + lo, src + lo, (hi - lo) * 4, hipMemcpyHostToDevice) == hipSuccess
-               ? 0 : -EIO;
+    pq.add(static_cast<uint32_t *>(dst.p) + lo, src + lo, hi - lo);
+    return 0;
 }
 
 int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
@@ -329,11 +373,17 @@ int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
         lens.insert(p.plen);
     }
     std::vector<std::vector<uint32_t>> keys, vals;
-    for (auto &kv : uniq) { keys.push_back(kv.first); vals.push_back({kv.second}); }
+    d.lens_cnt.clear();
+    for (auto &kv : uniq) {
+        keys.push_back(kv.first);
+        vals.push_back({kv.second});
+        d.lens_cnt[(int)kv.first[4]]++;
+    }
     int r = build_hash<Lpm6Spec>(d.h, keys, vals, 0, nullptr, nullptr);
     if (r) return r;
-    std::vector<uint8_t> l(lens.rbegin(), lens.rend());
-    if (l.empty()) l.push_back(0);
+    d.live = keys.size();
+    std::vector<uint8_t> l(LENS_CAP, 0);
+    std::copy(lens.rbegin(), lens.rend(), l.begin());
     r = d.lens.upload(l.data(), l.size());
     d.view = Lpm6{d.h.view, d.lens.as<uint8_t>(), (uint32_t)lens.size()};
     return r;
@@ -417,8 +467,7 @@ int update_ipcache4(cv_ctx *c, HostMap *m)
         const uint32_t plen = rd32(k.data());
         if (plen < 32) return 1;               // spans the static bits: both families, /0
         if (k[4] || k[5] || k[6]) continue;    // matches no lookup key
-        if (k[7] == 2) return 1;               // IPv6 (a full compile rebuilds its hash)
-        if (k[7] != 1) continue;
+        if (k[7] != 1) continue;               // (IPv6: update_ipcache6)
         if (plen > 64) continue;
         const int len = (int)plen - 32;
         const uint32_t raw = rd32(k.data() + 8), addr = bswap32(raw);
@@ -485,20 +534,95 @@ int update_ipcache4(cv_ctx *c, HostMap *m)
     }
     const size_t nch = d.hb.chunks.size() / 256;
     if (nch > d.chunk_cap) return 1;           // out of device room: a full build compacts
-    int r = put_words(d.chunks, d.hb.chunks.data(), d.chunks_on_dev * 256, nch * 256);
-    if (r) return r;
+    PatchQueue &pq = c->pq;
+    put_words(pq, d.chunks, d.hb.chunks.data(), d.chunks_on_dev * 256, nch * 256);
     d.chunks_on_dev = nch;
     for (auto it = dirty.begin(); it != dirty.end();) {          // contiguous runs of slots
         uint32_t lo = *it, hi = lo + 1;
         for (++it; it != dirty.end() && *it == hi; ++it) ++hi;
-        if ((r = put_words(d.l1, d.hb.l1.data(), lo, hi))) return r;
+        put_words(pq, d.l1, d.hb.l1.data(), lo, hi);
     }
     std::sort(front_b.begin(), front_b.end());
     front_b.erase(std::unique(front_b.begin(), front_b.end()), front_b.end());
-    for (const uint64_t b : front_b)
-        if ((r = put_words(d.full.buckets, d.full.hb.data(), b * Host32Spec::BW, (b + 1) * Host32Spec::BW))) return r;
-    m->log_clear();
+    for (const uint64_t b : front_b) put_words(pq, d.full.buckets, d.full.hb.data(), b * Host32Spec::BW, (b + 1) * Host32Spec::BW);
     return 0;
+}
+
+// The IPv6 ipcache writes logged since the last compile applied in place: a prefix
+// is one entry of the per-length hash (Lpm6Spec: the masked address and the length),
+// so an insert, overwrite or delete rewrites one bucket; a length that appears or
+// disappears rewrites the descending length list the lookup walks.  0 = done, 1 = a
+// full compile is needed.
+int update_ipcache6(cv_ctx *c, HostMap *m)
+{
+    DevLpm6 &d = c->ipc6;
+    bool any = false;
+    for (const std::vector<uint8_t> &k : m->log)
+        if (!k[4] && !k[5] && !k[6] && k[7] == 2) { any = true; break; }
+    if (!any) return 0;
+    if (!d.h.nb || d.h.hb.empty() || !d.lens.p) return 1;
+    HashTable t{d.h.hb.data(), nullptr, d.h.nb - 1, 0, (uint32_t)Lpm6Spec::SPB};
+    std::vector<uint64_t> bk;
+    bool lens_changed = false;
+    for (const std::vector<uint8_t> &k : m->log) {
+        const uint32_t plen = rd32(k.data());
+        if (plen < 32) return 1;               // spans the static bits: both families, /0
+        if (k[4] || k[5] || k[6] || k[7] != 2 || plen > 160) continue;
+        const int len = (int)plen - 32;
+        uint32_t key[5];
+        for (int w = 0; w < 4; ++w) {
+            const int bits = len - 32 * w;
+            const uint32_t msk = bits <= 0 ? 0u : bits >= 32 ? 0xFFFFFFFFu : bswap32(0xFFFFFFFFu << (32 - bits));
+            key[w] = rd32(k.data() + 8 + 4 * w) & msk;
+        }
+        key[4] = (uint32_t)len;
+        const uint8_t *v = m->lookup_exact(k.data());
+        const int64_t old = host_find<Lpm6Spec>(t, key);
+        if (v) {
+            const uint32_t val = rd32(v);
+            if (val & 0x80000000u) return -ERANGE;
+            const int64_t sl = host_upsert<Lpm6Spec>(t, key, &val);
+            if (sl < 0) return 1;
+            if (old < 0) {
+                if (++d.live * 10 > d.h.nb * Lpm6Spec::SPB * 8) return 1;   // > 80 % load
+                if (d.lens_cnt[len]++ == 0) lens_changed = true;
+            }
+            bk.push_back((uint64_t)sl / Lpm6Spec::SPB);
+        } else if (old >= 0) {
+            const uint64_t b = (uint64_t)old / Lpm6Spec::SPB;
+            uint32_t *w = d.h.hb.data() + b * Lpm6Spec::BW;
+            const int q = (int)(old % Lpm6Spec::SPB);
+            uint64_t tags = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            tags = (tags & ~(0xFFULL << (8 * q))) | ((uint64_t)TAG_DEAD << (8 * q));
+            w[0] = (uint32_t)tags; w[1] = (uint32_t)(tags >> 32);
+            bk.push_back(b);
+            --d.live;
+            if (--d.lens_cnt[len] == 0) { d.lens_cnt.erase(len); lens_changed = true; }
+        }
+    }
+    std::sort(bk.begin(), bk.end());
+    bk.erase(std::unique(bk.begin(), bk.end()), bk.end());
+    for (const uint64_t b : bk) put_words(c->pq, d.h.buckets, d.h.hb.data(), b * Lpm6Spec::BW, (b + 1) * Lpm6Spec::BW);
+    if (lens_changed) {
+        uint32_t lw[LENS_CAP / 4] = {0};
+        uint8_t *l = reinterpret_cast<uint8_t *>(lw);
+        size_t n = 0;
+        for (auto it = d.lens_cnt.rbegin(); it != d.lens_cnt.rend(); ++it) l[n++] = (uint8_t)it->first;
+        c->pq.add(d.lens.p, lw, LENS_CAP / 4);
+        d.view.nlens = (uint32_t)n;
+    }
+    return 0;
+}
+
+// both families' incremental ipcache writes, or 1 (a full compile; nothing published)
+int update_ipcache(cv_ctx *c, HostMap *m)
+{
+    const size_t mk = c->pq.mark();
+    int r = update_ipcache4(c, m);
+    if (!r) r = update_ipcache6(c, m);
+    if (r) c->pq.undo(mk);
+    else m->log_clear();
+    return r;
 }
 
 // policy map -> PolicySpec table (proxy_port inline, so a lookup is one line) + 32-B
@@ -550,12 +674,11 @@ int compile_policy(cv_ctx *c, MapObj *mo)
 // take the agent's value, its counter-delta word is cleared; a deleted key's slot
 // becomes a tombstone.  Every other entry keeps its device-resident counters, as the
 // full compile carries them over.  0 = done, 1 = a full compile is needed.
-int update_policy(MapObj *mo)
+int update_policy(cv_ctx *c, MapObj *mo)
 {
     HostMap *m = mo->hm.get();
     DevHash &d = mo->pol;
-    // (three small copies per key: past a few hundred keys one full compile is cheaper)
-    if (!d.view.buckets || m->log_full || d.hb.empty() || m->log.size() > 256) return 1;
+    if (!d.view.buckets || m->log_full || d.hb.empty()) return 1;
     HashTable t{d.hb.data(), nullptr, d.nb - 1, 32, (uint32_t)PolicySpec::SPB};
     std::vector<uint64_t> bk;
     struct Side { int64_t s; uint8_t v[32]; };
@@ -586,14 +709,11 @@ int update_policy(MapObj *mo)
     }
     std::sort(bk.begin(), bk.end());
     bk.erase(std::unique(bk.begin(), bk.end()), bk.end());
-    int r = 0;
-    for (const uint64_t b : bk)
-        if ((r = put_words(d.buckets, d.hb.data(), b * PolicySpec::BW, (b + 1) * PolicySpec::BW))) return r;
-    const unsigned long long zero = 0;
+    for (const uint64_t b : bk) put_words(c->pq, d.buckets, d.hb.data(), b * PolicySpec::BW, (b + 1) * PolicySpec::BW);
+    const uint32_t zero[2] = {0, 0};
     for (const Side &e : side) {          // in log order: the last write of a key wins
-        if (hipMemcpy(d.vals.as<uint8_t>() + (size_t)e.s * 32, e.v, 32, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(d.aux.as<unsigned long long>() + e.s, &zero, 8, hipMemcpyHostToDevice) != hipSuccess)
-            return -EIO;
+        c->pq.add(d.vals.as<uint8_t>() + (size_t)e.s * 32, e.v, 8);
+        c->pq.add(d.aux.as<unsigned long long>() + e.s, zero, 2);
     }
     mo->written.clear();
     mo->pol_version = m->version;
@@ -690,7 +810,67 @@ int compile_revnat(cv_ctx *c, HostMap *m, bool v6)
     return d.upload(tab.data(), tab.size() * 4);
 }
 
-int sync_locked(cv_ctx *c)
+void drain(cv_ctx *c);
+
+// The stream of the batch about to be submitted waits (on the device) for the last
+// batch or publication of this context, whatever stream that was on: a context's
+// batches and table publications are totally ordered, so a publication never races a
+// batch of another stream and the per-launch group scratch is never shared by two
+// batches in flight.  No host wait.
+void order_stream(cv_ctx *c, hipStream_t s)
+{
+    if (c->have_last && c->last_stream != s) (void)hipStreamWaitEvent(s, c->last_ev, 0);
+}
+
+void mark_stream(cv_ctx *c, hipStream_t s)
+{
+    if (!c->last_ev && hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming) != hipSuccess) return;
+    (void)hipEventRecord(c->last_ev, s);
+    c->last_stream = s;
+    c->have_last = true;
+}
+
+// The queued table patches to the device, in stream s: pinned staging (a buffer whose
+// previous publication has completed, else a new one), one async copy, k_patch.
+int publish(cv_ctx *c, hipStream_t s)
+{
+    PatchQueue &pq = c->pq;
+    if (pq.recs.empty()) return 0;
+    const size_t rb = pq.recs.size() * sizeof(PatchRec), bytes = rb + pq.words.size() * 4;
+    Staging *st = nullptr;
+    for (Staging &x : c->staging)
+        if (x.cap >= bytes && (!x.done || hipEventQuery(x.done) == hipSuccess)) { st = &x; break; }
+    if (!st) {
+        Staging x;
+        x.cap = std::max<size_t>(bytes, 1 << 16);
+        if (hipHostMalloc(&x.host, x.cap, hipHostMallocDefault) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&x.dev, x.cap) != hipSuccess) { (void)hipHostFree(x.host); return -ENOMEM; }
+        if (hipEventCreateWithFlags(&x.done, hipEventDisableTiming) != hipSuccess) return -ENOMEM;
+        c->staging.push_back(x);
+        st = &c->staging.back();
+    }
+    memcpy(st->host, pq.recs.data(), rb);
+    memcpy(static_cast<uint8_t *>(st->host) + rb, pq.words.data(), pq.words.size() * 4);
+    order_stream(c, s);
+    if (hipMemcpyAsync(st->dev, st->host, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+    const int r = launch_patches(static_cast<const PatchRec *>(st->dev), (uint32_t)pq.recs.size(),
+                                 reinterpret_cast<const uint32_t *>(static_cast<uint8_t *>(st->dev) + rb), s);
+    if (r) return r;
+    (void)hipEventRecord(st->done, s);
+    mark_stream(c, s);
+    pq.recs.clear();
+    pq.words.clear();
+    ++c->publications;
+    return 0;
+}
+
+// Apply the agent's writes since the last batch boundary to the device tables, for a
+// batch about to run on stream s.  Incremental writes (ipcache v4 and v6 prefixes,
+// policy entries) are published in stream order (PatchQueue): no device wait.  A
+// table that has to be rebuilt (other roles, endpoint changes, a write the incremental
+// path cannot apply) replaces device buffers: only then does the boundary wait for
+// the batches already submitted.
+int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
 {
     bool dirty = c->eps_dirty;
     for (int r = 0; r < CV_NUM_ROLES; ++r) {
@@ -705,27 +885,33 @@ int sync_locked(cv_ctx *c)
     if (!dirty) return 0;
     int r = set_device(c);
     if (r) return r;
-    (void)hipDeviceSynchronize();          // no batch may still read a table we replace
+    bool drained = false;
+    auto rebuild = [&]() {                     // no batch may still read a table we replace
+        if (!drained) { drain(c); drained = true; }
+        ++c->full_compiles;
+    };
     for (int role = 0; role < CV_NUM_ROLES; ++role) {
         MapObj *m = get(c, c->role[role]);
         uint64_t v = m ? m->hm->version : 0;
         if (v == c->role_version[role]) continue;
         HostMap *hm = m ? m->hm.get() : nullptr;
-        switch (role) {
-        case CV_ROLE_CIDR4_FIX: r = compile_cidr_fix(c, hm, false); break;
-        case CV_ROLE_CIDR6_FIX: r = compile_cidr_fix(c, hm, true); break;
-        case CV_ROLE_CIDR4_DYN: r = compile_cidr_dyn(c, hm, false); break;
-        case CV_ROLE_CIDR6_DYN: r = compile_cidr_dyn(c, hm, true); break;
-        case CV_ROLE_LXC: r = compile_lxc(c, hm); break;
-        case CV_ROLE_IPCACHE:
-            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_ipcache4(c, hm);
-            if (r == 1) r = compile_ipcache(c, hm);
-            break;
-        case CV_ROLE_LB4_SERVICES: r = compile_lb(c, hm, false); break;
-        case CV_ROLE_LB6_SERVICES: r = compile_lb(c, hm, true); break;
-        case CV_ROLE_LB4_REVNAT: r = compile_revnat(c, hm, false); break;
-        case CV_ROLE_LB6_REVNAT: r = compile_revnat(c, hm, true); break;
-        default: r = 0; break;
+        if (role == CV_ROLE_IPCACHE) {
+            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_ipcache(c, hm);
+            if (r == 1) { rebuild(); r = compile_ipcache(c, hm); }
+        } else {
+            rebuild();
+            switch (role) {
+            case CV_ROLE_CIDR4_FIX: r = compile_cidr_fix(c, hm, false); break;
+            case CV_ROLE_CIDR6_FIX: r = compile_cidr_fix(c, hm, true); break;
+            case CV_ROLE_CIDR4_DYN: r = compile_cidr_dyn(c, hm, false); break;
+            case CV_ROLE_CIDR6_DYN: r = compile_cidr_dyn(c, hm, true); break;
+            case CV_ROLE_LXC: r = compile_lxc(c, hm); break;
+            case CV_ROLE_LB4_SERVICES: r = compile_lb(c, hm, false); break;
+            case CV_ROLE_LB6_SERVICES: r = compile_lb(c, hm, true); break;
+            case CV_ROLE_LB4_REVNAT: r = compile_revnat(c, hm, false); break;
+            case CV_ROLE_LB6_REVNAT: r = compile_revnat(c, hm, true); break;
+            default: r = 0; break;
+            }
         }
         if (r) return r;
         c->role_version[role] = v;
@@ -734,13 +920,14 @@ int sync_locked(cv_ctx *c)
     for (auto &e : c->eps) {
         MapObj *p = get(c, e.policy);
         if (p && p->hm->version != p->pol_version) {
-            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_policy(p);
-            if (r == 1) r = compile_policy(c, p);
+            const size_t mk = c->pq.mark();
+            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_policy(c, p);
+            if (r == 1) { c->pq.undo(mk); rebuild(); r = compile_policy(c, p); eps_changed = true; }
             if (r) return r;
-            eps_changed = true;
         }
     }
     if (eps_changed) {
+        rebuild();
         std::vector<EpDev> ev;
         std::vector<EpHot> hot;
         std::vector<uint16_t> of(65536, 0);
@@ -774,7 +961,7 @@ int sync_locked(cv_ctx *c)
         if (r) return r;
         c->eps_dirty = false;
     }
-    return 0;
+    return publish(c, stream);
 }
 
 DpParams params(cv_ctx *c)
@@ -1150,45 +1337,48 @@ bool ct_fits(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t n, uint32_t 
 }
 
 // A netdev launch next to max_entries, exact (cv_kernels.hip "conntrack admission"):
-// the front and the grouping once, k_ct_intent's bounds, then the conntrack stages in
-// windows, each planned on the device from the exact live counts as it starts.
+// the front and the grouping once, then windows: k_ct_intent's creates and deletes of
+// every packet not yet run, the budgets, the conntrack stages over the window (up to
+// the first packet whose creates depend on an earlier create of its group in the same
+// window: the next window sees it exactly).  One host read per window (its end).
 int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, uint32_t now, int with_prefilter,
                  const GroupScratch &gs, const std::vector<MapObj *> &cts, hipStream_t s)
 {
     const uint32_t n = bc.n;
     Admit a{};
     a.nmaps = (uint32_t)cts.size();
-    for (size_t k = 0; k < cts.size(); ++k) a.maps[k] = cts[k]->ct.view.buckets;
-    const size_t need_pre = (size_t)2 * a.nmaps * n * 4;
-    if ((c->adm_ib.n < n && c->adm_ib.alloc(n)) || (c->adm_pre.n < need_pre && c->adm_pre.alloc(need_pre)) ||
+    for (size_t k = 0; k < cts.size(); ++k) {
+        a.maps[k] = cts[k]->ct.view.buckets;
+        a.live[k] = cts[k]->live.as<unsigned long long>();
+        a.cap[k] = cts[k]->cap;
+    }
+    const size_t need_scan = (size_t)a.nmaps * n * 4;
+    if ((c->adm_ib.n < (size_t)n * 2 && c->adm_ib.alloc((size_t)n * 2)) ||
+        (c->adm_pre.n < 2 * need_scan && c->adm_pre.alloc(2 * need_scan)) ||
         (!c->adm_tsum.p && c->adm_tsum.alloc(4096 * 4)) || (!c->adm_win.p && c->adm_win.alloc(8)))
         return -ENOMEM;
     a.ib = c->adm_ib.as<uint8_t>();
-    a.pre = c->adm_pre.as<uint32_t>();
+    a.budget = a.ib + n;
+    a.sum = c->adm_pre.as<int32_t>();
+    a.pmin = a.sum + (size_t)a.nmaps * n;
     a.tsum = c->adm_tsum.as<uint32_t>();
-    a.win = c->adm_win.as<uint32_t>();
+    a.hi = c->adm_win.as<uint32_t>();
     int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
-    if (!r) r = launch_ct_intent(p, bc, gs, a, s);
     if (r) return r;
     uint32_t windows = 0;
     for (uint32_t lo = 0; lo < n; ++windows) {
-        drain(c);
-        Rooms rm{};
-        for (size_t k = 0; k < cts.size(); ++k) {
-            uint64_t v = 0;
-            if (hipMemcpy(&v, cts[k]->live.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
-            cts[k]->live_upper = v;
-            rm.r[k] = cts[k]->cap > v ? cts[k]->cap - v : 0;
-        }
-        uint32_t w[2];
-        if ((r = launch_window(a, n, lo, rm, s))) return r;
-        if (hipMemcpy(w, a.win, 8, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+        a.lo = lo;
+        if ((r = launch_admission(p, bc, gs, a, s))) return r;
+        uint32_t hi = n;
+        if (hipMemcpyAsync(&hi, a.hi, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        if (hi <= lo || hi > n) return -EIO;                      // (the first packet not run is never unsure)
         DpParams pw = p;
         pw.win_lo = lo;
-        pw.win_span = w[0] - lo;
-        pw.ct_guard = w[1];
+        pw.win_span = hi - lo;
+        pw.budget = a.budget;
         if ((r = launch_netdev_stages(pw, bc, now, oc, gs, s))) return r;
-        lo = w[0];
+        lo = hi;
     }
     for (MapObj *m : cts) {
         m->live_upper = m->cap;                                   // (re-read when the next launch plans)
@@ -1252,6 +1442,12 @@ void cv_close(cv_ctx *c)
     if (c->device >= 0) {
         (void)hipSetDevice(c->device);
         (void)hipDeviceSynchronize();
+        for (Staging &x : c->staging) {
+            (void)hipHostFree(x.host);
+            (void)hipFree(x.dev);
+            (void)hipEventDestroy(x.done);
+        }
+        if (c->last_ev) (void)hipEventDestroy(c->last_ev);
     }
     delete c;
 }
@@ -1557,11 +1753,22 @@ int cv_node_config(cv_ctx *c, const cv_node_cfg *cfg)
     return 0;
 }
 
+// how the agent's writes reached the device so far: stream-ordered publications of
+// incremental changes, and table rebuilds (a boundary that waited for the device)
+int cv_publish_stats(cv_ctx *c, uint64_t *publications, uint64_t *rebuilds)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (publications) *publications = c->publications;
+    if (rebuilds) *rebuilds = c->full_compiles;
+    return 0;
+}
+
 int cv_sync(cv_ctx *c)
 {
     if (!c) return -EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    return sync_locked(c);
+    return sync_locked(c, nullptr);
 }
 
 int cv_xdp_prefilter(cv_ctx *c, const cv_batch *b, cv_out *o, void *stream)
@@ -1570,8 +1777,11 @@ int cv_xdp_prefilter(cv_ctx *c, const cv_batch *b, cv_out *o, void *stream)
     int r = check_batch(b);
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
-    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
-    return launch_xdp_prefilter(params(c), to_dev(b), to_dev(o), (hipStream_t)stream);
+    if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
+    order_stream(c, (hipStream_t)stream);
+    r = launch_xdp_prefilter(params(c), to_dev(b), to_dev(o), (hipStream_t)stream);
+    mark_stream(c, (hipStream_t)stream);
+    return r;
 }
 
 int cv_policy_ingress(cv_ctx *c, int ep, const cv_batch *b, cv_out *o, void *stream)
@@ -1581,15 +1791,17 @@ int cv_policy_ingress(cv_ctx *c, int ep, const cv_batch *b, cv_out *o, void *str
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
     if (ep < 0 || (size_t)ep >= c->eps.size() || c->eps[ep].policy < 0) return -EINVAL;
-    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
+    order_stream(c, (hipStream_t)stream);
     const DpParams p = params(c);
     const HashTable pol = get(c, c->eps[ep].policy)->pol.view;
-    for (uint32_t off = 0; off < b->n; off += c->chunk) {
+    for (uint32_t off = 0; off < b->n && !r; off += c->chunk) {
         const uint32_t n = std::min(c->chunk, b->n - off);
-        if ((r = launch_policy_ingress(p, ep, chunk(b, off, n), chunk(o, off), (hipStream_t)stream))) return r;
-        if ((r = launch_policy_fold(pol, (hipStream_t)stream))) return r;
+        r = launch_policy_ingress(p, ep, chunk(b, off, n), chunk(o, off), (hipStream_t)stream);
+        if (!r) r = launch_policy_fold(pol, (hipStream_t)stream);
     }
-    return 0;
+    mark_stream(c, (hipStream_t)stream);
+    return r;
 }
 
 int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefilter, cv_out *o, void *stream)
@@ -1599,7 +1811,8 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
     for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
-    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
+    order_stream(c, (hipStream_t)stream);
     const uint32_t cmax = std::min(b->n, c->chunk);
     if ((r = ensure_groups(c, cmax, false))) return r;
     std::set<const void *> seen;
@@ -1634,6 +1847,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "netdev", (hipStream_t)stream);
     }
+    mark_stream(c, (hipStream_t)stream);
     return 0;
 }
 
@@ -1645,7 +1859,8 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
     for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
-    if ((r = set_device(c)) || (r = sync_locked(c))) return r;
+    if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
+    order_stream(c, (hipStream_t)stream);
     const uint32_t cmax = std::min(b->n, c->chunk);
     if ((r = ensure_groups(c, cmax, true))) return r;
     std::set<const void *> seen;
@@ -1669,6 +1884,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream);
     }
+    mark_stream(c, (hipStream_t)stream);
     return 0;
 }
 

@@ -391,6 +391,7 @@ __device__ __forceinline__ void notify_trace(const DpParams &p, const M &m, uint
 struct Acct {
     uint32_t nl, nu;
     LdsPolicy *pc = nullptr;   // policy counter cache of the workgroup, if any
+    uint32_t budget = ~0u;     // admission windows: creates of new CT entries that may still succeed
 };
 
 // lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
@@ -1093,6 +1094,10 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
     if (guard && ct.live && (absent || dev_find<typename T::Spec>(ct, k, nullptr) < 0) &&
         __hip_atomic_load(G(ct.live), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ct.cap)
         return false;                                             // full: -E2BIG
+    if (a.budget != ~0u && (absent || dev_find<typename T::Spec>(ct, k, nullptr) < 0)) {
+        if (!a.budget) return false;                              // admission: the map is full here (-E2BIG)
+        --a.budget;
+    }
     bool created;
     const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent);
     if (s < 0) return false;

@@ -72,21 +72,25 @@ struct DpParams {              // by value as the kernel argument
     uint32_t ct_guard;         // 1: creates check the CT map's live count against max_entries (cv_ctx.cpp admission)
     uint32_t win_lo, win_span; // the conntrack stages run the packets in [win_lo, win_lo + win_span) (admission
                                // windows; 0, ~0 otherwise)
+    const uint8_t *budget;     // admission: per packet the creates of new CT entries that succeed, or null
 };
 
-// Exact conntrack admission next to max_entries (cv_ctx.cpp, k_ct_intent): per packet
-// of a launch an upper bound of the entries it creates (U) and deletes (D) in its CT
-// map, and per map their inclusive prefix sums over the launch.
+// Exact conntrack admission next to max_entries (cv_kernels.hip "conntrack
+// admission", cv_ctx.cpp run_admitted).
 constexpr int ADMIT_MAPS = 4;
 struct Admit {
     const uint32_t *maps[ADMIT_MAPS];  // bucket arrays of the launch's CT maps (map index = position)
+    unsigned long long *live[ADMIT_MAPS];
+    unsigned long long cap[ADMIT_MAPS];
     uint32_t nmaps;
-    uint8_t *ib;                       // per packet: U | D << 2 | map << 3
-    uint32_t *pre;                     // [2 * map + (0: U, 1: D)] * n + i: inclusive prefix sums
-    uint32_t *tsum;                    // scan tile sums
-    uint32_t *win;                     // k_window out: {hi, guarded}
+    uint32_t lo;                       // the first packet not yet run
+    uint8_t *ib;                       // per packet: creates A | deletes D << 2 | map << 3 | unsure << 6
+    int32_t *sum, *pmin;               // per map m: [m * (n - lo) + j] inclusive sum of D - A over packets
+                                       // lo .. lo + j, and the prefix minimum of that sum
+    uint8_t *budget;                   // per packet: how many of its creates of new entries succeed
+    uint32_t *tsum;                    // scan tile aggregates
+    uint32_t *hi;                      // the first unsure packet (the window's end)
 };
-struct Rooms { unsigned long long r[ADMIT_MAPS]; };
 
 struct BatchDev {
     const uint8_t *frames;
@@ -183,13 +187,19 @@ int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter
                         const GroupScratch &g, hipStream_t s);
 int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, const GroupScratch &g,
                          hipStream_t s);
-// admission: U / D per packet and their prefix sums per map (after launch_netdev_front)
-int launch_ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s);
-// the admission window from packet lo: out {hi, guarded} in a.win
-int launch_window(const Admit &a, uint32_t n, uint32_t lo, const Rooms &r, hipStream_t s);
+// admission, per window from packet a.lo (after launch_netdev_front): every later
+// packet's creates and deletes, the window's end (*a.hi) and the budgets
+int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s);
 // config 5: from-container of the packets' source endpoints (src_ep[i], or ep0)
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s);
+// one run of words the agent's writes changed in a device table (cv_ctx.cpp PatchQueue)
+struct PatchRec {
+    unsigned long long dst;    // device address of the first word
+    uint32_t words, src;       // run length, offset in the staged word array
+};
+// k_patch: copy every run from the staged words (recs then words, in one device buffer)
+int launch_patches(const PatchRec *recs, uint32_t n, const uint32_t *words, hipStream_t s);
 // single-element operations on a device-resident conntrack table (map API path):
 // op 0 lookup, 1 update (BPF_ANY/NOEXIST/EXIST in flags), 2 delete; v6 selects the
 // ipv6_ct_tuple table.  io = {key[KW words], value[16 words], rc}

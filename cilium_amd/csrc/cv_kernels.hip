@@ -10,6 +10,8 @@
 // The egress path (config 5) is in cv_egress.hip; the shared device functions
 // (map probes, policy, conntrack, metrics, grouping) in cv_dev.hpp.  No MFMA: this
 // is integer gather work, HBM/L2 bound.
+#include <type_traits>
+
 #include "cv_dev.hpp"
 
 namespace cv {
@@ -391,9 +393,11 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
         lslot = (int32_t)g.ifx[i];
     }
     RevNatOut rn{false, false, 0, 0};
+    if (p.budget) a.budget = p.budget[i];                        // (admission windows)
     // the only packet of its group defers its create to k_ct_commit (not with event
-    // records, whose TRACE_TO_LXC would have to be withdrawn if the create failed)
-    bool defer = single && !p.ct_guard && !M::EV;
+    // records, whose TRACE_TO_LXC would have to be withdrawn if the create failed, nor
+    // with a budget short of the tuple and its twin)
+    bool defer = single && !p.ct_guard && !M::EV && a.budget >= 2;
     const int ret = handle_policy4<M, false>(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc4, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
                                    a, m, &rn, &defer);
@@ -460,7 +464,8 @@ __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b
     }
     RevNat6Out rn;
     rn.valid = false;
-    bool defer = single && !p.ct_guard && !M::EV;
+    if (p.budget) a.budget = p.budget[i];
+    bool defer = single && !p.ct_guard && !M::EV && a.budget >= 2;
     const int ret = handle_policy6<M, false>(p, ep, s, s1.w, (meta >> 16) & 1u,
                                    ifindex_of(m, p.lxc6, lslot, ((meta >> 17) & 1u) << 17), now, ct, proxy, reason,
                                    a, m, &rn, &defer);
@@ -1366,144 +1371,272 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
 
 // ------------------------------------------------------------------ conntrack admission
 // Next to a CT map's max_entries the batch result depends on the order of creates and
-// deletes across groups (a create fails once the count reaches max_entries, a delete
-// makes room).  The host then runs a launch in windows of packets that are exact under
-// parallel execution (cv_ctx.cpp run_admitted): a window whose creates all fit in
-// every map's room runs unguarded; one whose maps without room see no delete runs
-// guarded (each create checks the count: the count cannot move inside the window, so
-// every create into a full map fails, the others succeed, in any order); otherwise one
-// packet.  What a packet can create or delete comes from k_ct_intent, read-only against
-// the tables as the launch starts: ipv4_policy / ipv6_policy (bpf_lxc.c:865-979,
-// 721-849) create the tuple and its ICMP twin (U = 2) only on CT_NEW with an allowing
-// verdict and delete (D = 1) only on CT_ESTABLISHED with a denying one; a packet after a
-// group member that may have changed the table gets U = 2, D = 1 (its lookup may
-// differ from the launch-start table's).
+// deletes across groups: the kernel hash map fails an insert of a new key once the
+// count is at max_entries (-E2BIG: DROP_CT_CREATE_FAILED) and a delete makes room.  In
+// packet order, with r the map's room, a delete makes r + 1 and a packet that tries A
+// creates of new entries (its tuple, then its ICMP twin only if the tuple went in)
+// gets min(A, r) of them, r - that: a walk reflected at 0, so r after packet j is
+// x_j - min(0, min_{q <= j} x_q) with x_j = r_start + the sum of (D - A) up to j --
+// two scans.  What each packet creates and deletes comes from k_ct_intent, against
+// the table as the window starts: ipv4_policy / ipv6_policy (bpf_lxc.c:865-979,
+// 721-849) delete only on CT_ESTABLISHED with a denying verdict and create only on
+// CT_NEW with an allowing one, the tuple (absent: the lookup just missed) and the twin
+// if it is absent.  A packet whose lookups touch a key an earlier member of its group
+// created or deleted in this window is "unsure" (the earlier create may fail): the
+// window ends before the first one, which the next window (run_admitted) sees exactly.
+// The stage then runs the window with each packet's budget (Acct::budget in ct_put):
+// exactly the sequential run's successes and failures, at full width.
+template <class T>
+__device__ __forceinline__ bool seen_key(const uint64_t *ch, int nch, const T &t)
+{
+    uint32_t k[T::KW];
+    t.key(k);
+    const uint64_t h = key_hash<typename T::Spec>(k);
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hit |= j < nch && ch[j] == h;
+    return hit;
+}
+
+template <class T>
+__device__ __forceinline__ uint64_t key_h(const T &t)
+{
+    uint32_t k[T::KW];
+    t.key(k);
+    return key_hash<typename T::Spec>(k);
+}
+
+template <class T>
+__device__ __forceinline__ bool present(const HashTable &ct, const T &t)
+{
+    uint32_t k[T::KW];
+    t.key(k);
+    return dev_find<typename T::Spec>(ct, k, nullptr) >= 0;
+}
+
+// one packet's creates (bits 0-1), delete (bit 2) and unsure flag (bit 6); ch / nch:
+// the keys earlier members of the run changed in this window (nch > 4: too many)
 template <bool V6>
 __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
-                                              bool hist, const uint32_t *&map)
+                                              uint64_t *ch, int &nch, const uint32_t *&map)
 {
+    using T = typename std::conditional<V6, Tuple6, Tuple4>::type;
     const uint4 s1 = g.srec[2 * i + 1];
     const uint32_t meta = s1.z, src = s1.w;
     uint32_t seen;
+    T t;
+    EpDev ep;
     if constexpr (!V6) {
-        const EpDev ep = ep_stage4<false>(p, meta & 0xFFFFu);
+        ep = ep_stage4<false>(p, meta & 0xFFFFu);
         map = ep.ct4.buckets;
         if ((p.flags & F_DROP_ALL) || !ep.ipv4) return 0;
         const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
         if (s.len < 34) return 0;
-        Tuple4 t;
         t.nexthdr = s.nexthdr; t.daddr = s.daddr; t.saddr = s.saddr; t.dport = t.sport = 0;
         if (ct_l4<false>(t, s.h, CT_INGRESS, seen) < 0) return 0;
-        if (hist) return 2u | 4u;
-        Tuple4 t2 = t;
-        t2.reverse();
-        uint32_t k1[Tuple4::KW], k2[Tuple4::KW];
-        t.key(k1);
-        t2.key(k2);
-        if (dev_find<Ct4Spec>(ep.ct4, k1, nullptr) >= 0) return 0;          // CT_REPLY / CT_RELATED
-        const bool est = dev_find<Ct4Spec>(ep.ct4, k2, nullptr) >= 0;
-        const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
-        return est ? (deny ? 4u : 0u) : (deny ? 0u : 2u);
     } else {
-        const EpDev ep = G(p.eps)[meta & 0xFFFFu];
+        ep = G(p.eps)[meta & 0xFFFFu];
         map = ep.ct6.buckets;
         if (p.flags & F_DROP_ALL) return 0;
         Rec6 r;
         rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
         const Skb6 s = skb6_from(r);
         if (s.len < 54 || s.l4off < 0) return 0;
-        Tuple6 t;
 #pragma unroll
         for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
         t.nexthdr = s.nexthdr;
         t.dport = t.sport = 0;
         if (ct_l4<true>(t, s.h, CT_INGRESS, seen) < 0) return 0;
-        if (hist) return 2u | 4u;
-        Tuple6 t2 = t;
-        t2.reverse();
-        uint32_t k1[Tuple6::KW], k2[Tuple6::KW];
-        t.key(k1);
-        t2.key(k2);
-        if (dev_find<Ct6Spec>(ep.ct6, k1, nullptr) >= 0) return 0;
-        const bool est = dev_find<Ct6Spec>(ep.ct6, k2, nullptr) >= 0;
-        const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
-        return est ? (deny ? 4u : 0u) : (deny ? 0u : 2u);
     }
+    const HashTable &ct = V6 ? ep.ct6 : ep.ct4;
+    T t2 = t;
+    t2.reverse();
+    T tw = t2;                                                    // the ICMP twin of a create (ct_create)
+    tw.nexthdr = V6 ? 58u : 1u;
+    tw.sport = 0; tw.dport = 0;
+    tw.flags = t2.flags | TUPLE_F_RELATED;
+    if (nch > 4 || seen_key(ch, nch, t) || seen_key(ch, nch, t2) || seen_key(ch, nch, tw)) return 64u;
+    if (present(ct, t)) return 0;                                 // CT_REPLY / CT_RELATED
+    const bool est = present(ct, t2);
+    const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
+    if (est) {
+        if (!deny) return 0;
+        if (nch < 4) ch[nch] = key_h(t2);
+        ++nch;
+        return 4u;                                                // ct_delete
+    }
+    if (deny) return 0;
+    const uint32_t A = present(ct, tw) ? 1u : 2u;                 // (an existing twin is overwritten)
+    if (nch < 4) ch[nch] = key_h(t2);
+    ++nch;
+    if (nch < 4) ch[nch] = key_h(tw);
+    ++nch;
+    return A;
 }
 
 template <bool V6>
 __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, GroupScratch g, Admit a)
 {
-    bool hist = false;
+    uint64_t ch[4];
+    int nch = 0;
     uint32_t left = 0;                                            // members of the current run still to come
     for_each_run<true>(g, V6 ? Q_NETDEV6 : Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
-        if (!left) { left = n; hist = false; }                    // (a lane's runs come one after another)
+        if (!left) { left = n; nch = 0; }                         // (a lane's runs come one after another)
         --left;
+        if (x < a.lo) return;                                     // run by an earlier window
         const uint32_t *map = nullptr;
-        const uint32_t ud = ct_intent<V6>(p, b, g, x, hist, map);
+        const uint32_t v = ct_intent<V6>(p, b, g, x, ch, nch, map);
         uint32_t mi = 0;
 #pragma unroll
         for (int k = 0; k < ADMIT_MAPS; ++k)
             if ((uint32_t)k < a.nmaps && a.maps[k] == map) mi = k;
-        a.ib[x] = (uint8_t)(ud | mi << 3);
-        hist = hist || ud;
+        a.ib[x] = (uint8_t)(v | mi << 3);
+        if (v & 64u) atomicMin(a.hi, x);
     });
 }
+
+__global__ void k_admit_init(Admit a, uint32_t n)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) *a.hi = n;
+}
+
+// per map m: D - A of the packets lo.. (others 0)
 __global__ void __launch_bounds__(BLOCK) k_admit_extract(Admit a, uint32_t n)
 {
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        const uint32_t v = a.ib[i], mi = v >> 3;
-        for (uint32_t m = 0; m < a.nmaps; ++m) {
-            a.pre[(size_t)(2 * m) * n + i] = m == mi ? (v & 3u) : 0u;
-            a.pre[(size_t)(2 * m + 1) * n + i] = m == mi ? (v >> 2) & 1u : 0u;
-        }
+    const uint32_t L = n - a.lo;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < L; j += gridDim.x * BLOCK) {
+        const uint32_t v = a.ib[a.lo + j], mi = (v >> 3) & 7u;
+        const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
+        for (uint32_t m = 0; m < a.nmaps; ++m) a.sum[(size_t)m * L + j] = m == mi ? d : 0;
     }
 }
 
-int launch_ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s)
+// the budgets from the scans (the reflected walk above), for every packet from lo with creates
+__global__ void __launch_bounds__(BLOCK) k_admit_budget(Admit a, uint32_t n)
 {
-    if (!b.n) return 0;
+    const uint32_t L = n - a.lo;
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < L; j += gridDim.x * BLOCK) {
+        const uint32_t v = a.ib[a.lo + j], mi = (v >> 3) & 7u, A = v & 3u;
+        if (!A) { a.budget[a.lo + j] = 0; continue; }
+        const unsigned long long live = __hip_atomic_load(a.live[mi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long long r0 = live < a.cap[mi] ? (long long)(a.cap[mi] - live) : 0;
+        long long r = r0;                                         // the room before packet j
+        if (j) {
+            const long long S = a.sum[(size_t)mi * L + j - 1], PM = a.pmin[(size_t)mi * L + j - 1];
+            const long long lowest = r0 + PM < 0 ? r0 + PM : 0;
+            r = r0 + S - lowest;
+        }
+        a.budget[a.lo + j] = (uint8_t)(r < (long long)A ? r : (long long)A);
+    }
+}
+
+// prefix minimum of int32 values in place (the same three phases as launch_scan)
+__device__ __forceinline__ int32_t block_incl_min(int32_t v, int32_t *wmin)
+{
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t t = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl = min(incl, t);
+    }
+    if (lane == 63) wmin[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t acc = INT32_MAX;
+        for (uint32_t w = 0; w < nw; ++w) { const int32_t t = wmin[w]; wmin[w] = acc; acc = min(acc, t); }
+        wmin[16] = acc;
+    }
+    __syncthreads();
+    const int32_t r = min(wmin[wv], incl);
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(1024) k_min_tiles(const int32_t *c, uint32_t L, int32_t *tmin)
+{
+    __shared__ int32_t wmin[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    int32_t v = INT32_MAX;
+    for (uint32_t k = 0; k < 4; ++k) if (j + k < L) v = min(v, c[j + k]);
+    block_incl_min(v, wmin);
+    if (threadIdx.x == 0) tmin[blockIdx.x] = wmin[16];
+}
+
+__global__ void __launch_bounds__(1024) k_min_top(int32_t *tmin, uint32_t tiles)
+{
+    __shared__ int32_t wmin[17];
+    int32_t v[4], m = INT32_MAX;
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t t = threadIdx.x * 4 + k;
+        v[k] = t < tiles ? tmin[t] : INT32_MAX;
+        m = min(m, v[k]);
+    }
+    const int32_t incl = block_incl_min(m, wmin);
+    const int32_t before = __shfl_up(incl, 1, 64);               // exclusive: the minimum before this thread
+    int32_t e = (threadIdx.x & 63) ? before : (threadIdx.x >> 6 ? wmin[threadIdx.x >> 6] : INT32_MAX);
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t t = threadIdx.x * 4 + k;
+        if (t < tiles) tmin[t] = e;                               // (the minimum of the tiles before t)
+        e = min(e, v[k]);
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_min_apply(const int32_t *c, int32_t *out, uint32_t L, const int32_t *tmin)
+{
+    __shared__ int32_t wmin[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    int32_t v[4], m = INT32_MAX;
+    for (uint32_t k = 0; k < 4; ++k) { v[k] = j + k < L ? c[j + k] : INT32_MAX; m = min(m, v[k]); }
+    const int32_t incl = block_incl_min(m, wmin);
+    const int32_t before = __shfl_up(incl, 1, 64);
+    int32_t e = (threadIdx.x & 63) ? before : (threadIdx.x >> 6 ? wmin[threadIdx.x >> 6] : INT32_MAX);
+    e = min(e, tmin[blockIdx.x]);
+    for (uint32_t k = 0; k < 4; ++k) {
+        e = min(e, v[k]);
+        if (j + k < L) out[j + k] = e;
+    }
+}
+
+int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s)
+{
+    if (!b.n || a.lo >= b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
-    (void)hipMemsetAsync(a.ib, 0, b.n, s);
+    const uint32_t L = b.n - a.lo, tiles = (L + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(k_admit_init, dim3(1), dim3(64), 0, s, a, b.n);
     hipLaunchKernelGGL(k_ct_intent<false>, grid, blk, 0, s, p, b, g, a);
     GroupScratch g6 = g;
     g6.single = g.single6;
     g6.work = g.work6;
     hipLaunchKernelGGL(k_ct_intent<true>, grid, blk, 0, s, p, b, g6, a);
     hipLaunchKernelGGL(k_admit_extract, grid, blk, 0, s, a, b.n);
-    for (uint32_t k = 0; k < 2 * a.nmaps; ++k) launch_scan(a.pre + (size_t)k * b.n, b.n, a.tsum, nullptr, true, s);
+    for (uint32_t m = 0; m < a.nmaps; ++m) {
+        uint32_t *sm = reinterpret_cast<uint32_t *>(a.sum + (size_t)m * L);
+        launch_scan(sm, L, a.tsum, nullptr, true, s);
+        int32_t *tm = reinterpret_cast<int32_t *>(a.tsum);
+        hipLaunchKernelGGL(k_min_tiles, dim3(tiles), dim3(1024), 0, s, a.sum + (size_t)m * L, L, tm);
+        hipLaunchKernelGGL(k_min_top, dim3(1), dim3(1024), 0, s, tm, tiles);
+        hipLaunchKernelGGL(k_min_apply, dim3(tiles), dim3(1024), 0, s, a.sum + (size_t)m * L, a.pmin + (size_t)m * L,
+                           L, tm);
+    }
+    hipLaunchKernelGGL(k_admit_budget, grid, blk, 0, s, a, b.n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// The next window [lo, hi) (one thread: binary searches over the prefix sums).  A map
-// with room bounds the window by its possible creates (their sum must fit the room); a
-// full map by its first possible delete, and makes the window guarded.
-__global__ void k_window(Admit a, uint32_t n, uint32_t lo, Rooms r)
+// the agent's staged table writes (cv_ctx.cpp PatchQueue): a block per run of words
+__global__ void __launch_bounds__(BLOCK) k_patch(const PatchRec *recs, uint32_t n, const uint32_t *words)
 {
-    if (threadIdx.x || blockIdx.x) return;
-    uint32_t hi = n, guarded = 0;
-    for (uint32_t m = 0; m < a.nmaps; ++m) {
-        const uint32_t *pu = a.pre + (size_t)(2 * m) * n, *pd = pu + n;
-        const uint32_t *pre = r.r[m] ? pu : pd;
-        const unsigned long long lim = r.r[m] ? r.r[m] : 0ull;  // the window's sum may reach lim
-        guarded |= r.r[m] ? 0u : 1u;
-        const uint32_t base = lo ? pre[lo - 1] : 0u;
-        if ((unsigned long long)(pre[n - 1] - base) <= lim) continue;
-        uint32_t L = lo, R = n - 1;                              // first p with pre[p] - base > lim
-        while (L < R) {
-            const uint32_t mid = L + (R - L) / 2;
-            if ((unsigned long long)(pre[mid] - base) > lim) R = mid; else L = mid + 1;
-        }
-        hi = min(hi, L);
+    for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const PatchRec pr = recs[r];
+        uint32_t *dst = reinterpret_cast<uint32_t *>(pr.dst);
+        for (uint32_t w = threadIdx.x; w < pr.words; w += BLOCK) dst[w] = words[pr.src + w];
     }
-    if (hi <= lo) { hi = lo + 1; guarded = 1; }
-    a.win[0] = hi;
-    a.win[1] = guarded;
 }
 
-int launch_window(const Admit &a, uint32_t n, uint32_t lo, const Rooms &r, hipStream_t s)
+int launch_patches(const PatchRec *recs, uint32_t n, const uint32_t *words, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_window, dim3(1), dim3(64), 0, s, a, n, lo, r);
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_patch, dim3(n < 4096 ? n : 4096), dim3(BLOCK), 0, s, recs, n, words);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -101,6 +101,7 @@ def load():
         "cv_bind": (i32, [vp, i32, i32]),
         "cv_endpoint_add": (i32, [vp, C.c_uint16, u32, i32, i32]),
         "cv_sync": (i32, [vp]),
+        "cv_publish_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
         "cv_xdp_prefilter": (i32, [vp, C.POINTER(Batch), C.POINTER(Out), vp]),
         "cv_policy_ingress": (i32, [vp, i32, C.POINTER(Batch), C.POINTER(Out), vp]),
         "cv_netdev_ingress": (i32, [vp, C.POINTER(Batch), u32, i32, C.POINTER(Out), vp]),
@@ -285,6 +286,12 @@ class Ctx:
 
     def sync(self):
         _check(load().cv_sync(self.h), "cv_sync")
+
+    def publish_stats(self):
+        """(stream-ordered publications of incremental writes, table rebuilds) so far"""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        _check(load().cv_publish_stats(self.h, C.byref(a), C.byref(b)), "cv_publish_stats")
+        return a.value, b.value
 
     # ---- batches (torch tensors on this device) ----
     @staticmethod

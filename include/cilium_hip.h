@@ -159,8 +159,18 @@ typedef struct {
 } cv_node_cfg;
 int cv_node_config(cv_ctx *ctx, const cv_node_cfg *cfg);
 
-/* make every pending map write visible to the next batch */
+/* Make every pending map write visible to the next batch.  Every batch call does this
+ * itself first (RCU-like visibility at batch granularity): the
+ * agent's writes since the last batch are applied to the host images of the device
+ * tables and the changed words published in the stream of the batch about to run
+ * (batches already submitted see the old tables, later ones the new) -- ipcache v4
+ * and v6 prefixes and policy entries without waiting for the device.  A write the
+ * incremental path cannot apply (other maps, endpoint changes, /0, a table past 80 %
+ * load) rebuilds the table after the submitted batches finish.  A context's batches
+ * are ordered across streams on the device (no host wait). */
 int cv_sync(cv_ctx *ctx);
+/* publications of incremental writes so far, and rebuilds (boundaries that waited) */
+int cv_publish_stats(cv_ctx *ctx, uint64_t *publications, uint64_t *rebuilds);
 
 /* ---- batches ---- */
 typedef struct {

@@ -220,7 +220,7 @@ struct cv_ctx {
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
-    DevBuf gpkey, gent, gbig, gcnt, gwork6;   // the netdev path's binned grouping
+    DevBuf gpkey, gent, gbig, gcnt, gwork6, ghcls, ghoff, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_pre, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
@@ -1061,6 +1061,8 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     if (c->gtable.alloc(cap * 16) || c->gsingle.alloc((size_t)cmax * 4) ||
         c->gpkey.alloc((size_t)cmax * 8) || c->gent.alloc((size_t)cmax * 8) || c->gbig.alloc((size_t)cmax * 16) ||
         c->gcnt.alloc(((size_t)GBIN_MAX * GBLK + 1 + 1024) * 4) || c->gwork6.alloc((size_t)cmax * 4) ||
+        c->ghcls.alloc((size_t)cmax) || c->ghoff.alloc((size_t)cmax * 4) ||
+        c->ghcnt.alloc(((size_t)32 * (cmax / 4096 + 1) + 1 + 1024) * 4) ||
         c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsrec.alloc((size_t)cmax * 32) ||
         c->gorder.alloc((size_t)cmax * 8) || c->gwork.alloc((size_t)cmax * 4) || c->gifx.alloc((size_t)cmax * 4) ||
@@ -1094,7 +1096,8 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>(),
                     c->gsingle.as<uint32_t>(), c->gpkey.as<unsigned long long>(), c->gent.as<uint2>(),
                     c->gcnt.as<uint32_t>(), c->gbig.as<unsigned long long>(), 4, c->gnext.as<uint32_t>(),
-                    c->gwork6.as<uint32_t>()};
+                    c->gwork6.as<uint32_t>(), c->ghcls.as<uint8_t>(), c->ghoff.as<uint32_t>(),
+                    c->ghcnt.as<uint32_t>()};
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;

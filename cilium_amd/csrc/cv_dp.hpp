@@ -145,6 +145,9 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t gbits;            // log2 of the number of bins
     uint32_t *single6;         // the singleton packets of the IPv6 queue (Q_NETDEV6)
     uint32_t *work6;           // the IPv6 queue's schedule (`work` of Q_NETDEV6)
+    uint8_t *hcls;             // per packet: 1 + its list if it is a group's first packet (k_heads_place), else 0
+    uint32_t *hoff;            // per first packet of a multi-packet group: its run's offset in `order`
+    uint32_t *hcnt;            // per (list, tile) head counts -> positions (k_heads_count / place)
 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses

@@ -347,6 +347,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         }
         if (!live) continue;
         g.pkey[i] = gkey;
+        g.hcls[i] = 0;
         g.gslot[i] = NONE;
         const bool fwd_here = !staged && !v6stage && ret == TC_ACT_OK;
         if (M::EV && o.frames) {
@@ -938,37 +939,19 @@ __device__ __forceinline__ void bitonic_sort(P v, uint32_t p)
         }
 }
 
-// a sub-queue region of queue q with room for cnt more entries (starting at sub-queue
-// k0): returns the region and the first entry (regions hold n / QSPLIT + 512 words and
-// the queue at most n / 2 runs, so one always has room)
-__device__ __forceinline__ uint32_t *queue_reserve(const GroupScratch &g, int q, uint32_t k0, uint32_t cnt)
-{
-    for (uint32_t t = 0; t < QSPLIT; ++t) {
-        const uint32_t k = (k0 + t) % QSPLIT;
-        uint32_t *ctr = &g.cursor[qctr(q, k)];
-        uint32_t cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (cur + cnt <= g.qregion) {
-            if (__hip_atomic_compare_exchange_strong(ctr, &cur, cur + cnt, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT))
-                return g.queue + ((size_t)qbank(q) * QSPLIT + k) * g.qregion + cur;
-        }
-    }
-    return nullptr;                                               // (unreachable, see above)
-}
-
 __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
 {
     __shared__ unsigned long long lv[LCAP];
-    __shared__ uint32_t tot[5], fill[5], hist[2][NCLASS], big[2];
-    __shared__ uint32_t *qbase[2];
-    __shared__ uint32_t base[3];
+    __shared__ uint32_t tot[3], fill, hist[2][NCLASS], big[2];
+    __shared__ uint32_t base;
     const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
     const uint32_t start = g.gcnt[b * GBLK], end = b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m];
     const uint32_t nb = end - start;
     if (!nb) return;                                              // (block-uniform)
     uint32_t p = 64;
     while (p < nb) p <<= 1;
-    if (threadIdx.x < 5) tot[threadIdx.x] = fill[threadIdx.x] = 0;
+    if (threadIdx.x < 3) tot[threadIdx.x] = 0;
+    if (threadIdx.x == 0) fill = 0;
     if (threadIdx.x < 2 * NCLASS) hist[threadIdx.x / NCLASS][threadIdx.x % NCLASS] = 0;
     if (threadIdx.x < 2) big[threadIdx.x] = 0;
     // composite {key low word, packet}: sorted, a group's members are contiguous and ascending
@@ -982,7 +965,7 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
     __syncthreads();
     if (in_lds) bitonic_sort(lv, p); else bitonic_sort(gv, p);
     const unsigned long long *v = in_lds ? lv : gv;
-    // pass 1: sizes -> totals
+    // pass 1: sizes -> run words, singletons and size classes per queue
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
         const uint32_t key = (uint32_t)(v[j] >> 32);
         if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;     // not a group's first member
@@ -990,16 +973,14 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
         while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
         const int q6 = key & 1u;
         if (c == 1) atomicAdd(&tot[1 + q6], 1u);
-        else { atomicAdd(&tot[0], c + 1); atomicAdd(&tot[3 + q6], 1u); atomicMax(&big[q6], c); }
+        else { atomicAdd(&tot[0], c + 1); atomicMax(&big[q6], c); }
         atomicAdd(&hist[q6][size_class(c)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        base[0] = tot[0] ? atomicAdd(&g.cursor[RUN_CURSOR], tot[0]) : 0u;
-        base[1] = tot[1] ? atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV], tot[1]) : 0u;
-        base[2] = tot[2] ? atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV6], tot[2]) : 0u;
-        qbase[0] = tot[3] ? queue_reserve(g, Q_NETDEV, b % QSPLIT, tot[3]) : nullptr;
-        qbase[1] = tot[4] ? queue_reserve(g, Q_NETDEV6, b % QSPLIT, tot[4]) : nullptr;
+        base = tot[0] ? atomicAdd(&g.cursor[RUN_CURSOR], tot[0]) : 0u;
+        if (tot[1]) atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV], tot[1]);
+        if (tot[2]) atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV6], tot[2]);
     }
     if (threadIdx.x < 2 * NCLASS) {
         const int q6 = threadIdx.x / NCLASS, c = threadIdx.x % NCLASS;
@@ -1009,23 +990,61 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
     if (threadIdx.x < 2 && big[threadIdx.x] > 8)
         atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : Q_NETDEV)], big[threadIdx.x]);
     __syncthreads();
-    // pass 2: write the singletons, the runs and their queue entries
+    // pass 2: the runs into `order`; every group's first packet marked with its list
+    // (k_heads_place lists them in packet order, class by class)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
         const uint32_t key = (uint32_t)(v[j] >> 32);
         if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;
         uint32_t c = 1;
         while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
-        const int q6 = key & 1u;
-        if (c == 1) {
-            uint32_t *single = q6 ? g.single6 : g.single;
-            single[base[1 + q6] + atomicAdd(&fill[1 + q6], 1u)] = (uint32_t)v[j];
-        } else {
-            const uint32_t off = base[0] + atomicAdd(&fill[0], c + 1);
+        const uint32_t q6 = key & 1u, x = (uint32_t)v[j];
+        uint32_t list = 15;                                       // 15: singletons
+        if (c > 1) {
+            const uint32_t off = base + atomicAdd(&fill, c + 1);
             uint32_t *o = g.order + off;
             o[0] = c;
             for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
-            qbase[q6][atomicAdd(&fill[3 + q6], 1u)] = off;
+            g.hoff[x] = off;
+            list = 15 - (uint32_t)size_class(c);                  // largest class first
         }
+        g.hcls[x] = (uint8_t)(1 + q6 * 16 + list);
+    }
+}
+
+// The groups' first packets listed in packet order, list by list (IPv4 runs class
+// 15 .. 1, IPv4 singletons, the same for IPv6): per tile of HTILE packets a count per
+// list, one scan, then each tile places its heads (ranks within a tile by LDS atomics:
+// a wave's lanes still take packets of one tile).  The stage's first members then
+// read their stage records and write their verdicts along the batch instead of at
+// random.
+constexpr uint32_t HTILE = 4096;
+__global__ void __launch_bounds__(1024) k_heads_count(GroupScratch g, uint32_t n, uint32_t tiles)
+{
+    __shared__ uint32_t c[32];
+    if (threadIdx.x < 32) c[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t k = 0; k < HTILE / 1024; ++k) {
+        const uint32_t x = blockIdx.x * HTILE + k * 1024 + threadIdx.x;
+        const uint32_t h = x < n ? g.hcls[x] : 0u;
+        if (h) atomicAdd(&c[h - 1], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) g.hcnt[threadIdx.x * tiles + blockIdx.x] = c[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n, uint32_t tiles)
+{
+    __shared__ uint32_t pos[32], start[4];
+    if (threadIdx.x < 32) pos[threadIdx.x] = g.hcnt[threadIdx.x * tiles + blockIdx.x];
+    if (threadIdx.x < 4) start[threadIdx.x] = g.hcnt[(threadIdx.x >> 1) * 16 * tiles + (threadIdx.x & 1) * 15 * tiles];
+    __syncthreads();
+    for (uint32_t k = 0; k < HTILE / 1024; ++k) {
+        const uint32_t x = blockIdx.x * HTILE + k * 1024 + threadIdx.x;
+        const uint32_t h = x < n ? g.hcls[x] : 0u;
+        if (!h) continue;
+        const uint32_t key = h - 1, q6 = key >> 4, at = atomicAdd(&pos[key], 1u);
+        if ((key & 15u) == 15u) (q6 ? g.single6 : g.single)[at - start[q6 * 2 + 1]] = x;
+        else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = g.hoff[x];
     }
 }
 
@@ -1036,6 +1055,10 @@ void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
     launch_scan(g.gcnt, m, g.gcnt + m + 1, g.gcnt + m, false, s);
     hipLaunchKernelGGL(k_gkey_scatter, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
     hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g);
+    const uint32_t tiles = (n + HTILE - 1) / HTILE;
+    hipLaunchKernelGGL(k_heads_count, dim3(tiles), dim3(1024), 0, s, g, n, tiles);
+    launch_scan(g.hcnt, 32 * tiles, g.hcnt + 32 * tiles + 1, g.hcnt + 32 * tiles, false, s);
+    hipLaunchKernelGGL(k_heads_place, dim3(tiles), dim3(1024), 0, s, g, n, tiles);
 }
 
 // ------------------------------------------------------------------ CT map API
@@ -1335,11 +1358,7 @@ int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter
     if (ev) hipLaunchKernelGGL(k_netdev_front<true>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     else hipLaunchKernelGGL(k_netdev_front<false>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     if (hipGetLastError() != hipSuccess) return -5;
-    launch_gbin_groups(g, b.n, s);                                // both families' runs and singletons
-    hipLaunchKernelGGL(k_group_schedule, grid, blk, 0, s, g, Q_NETDEV, true);
-    GroupScratch g6 = g;
-    g6.work = g.work6;
-    hipLaunchKernelGGL(k_group_schedule, grid, blk, 0, s, g6, Q_NETDEV6, true);
+    launch_gbin_groups(g, b.n, s);                                // both families' runs and singletons, listed
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

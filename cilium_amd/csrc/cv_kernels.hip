@@ -798,10 +798,11 @@ void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStr
 // staged packet as {packet, key low word} into its bin's slice; k_gbin_group sorts each
 // bin by (key low word, packet) -- in LDS, or for a bin past LCAP entries (a hot
 // address pair) in global memory -- so a group's members end up contiguous and in packet
-// order, and emits the runs {size, members} and the singletons exactly as
-// k_group_flatten does for the node-table queues (k_group_schedule and the stages read
-// them unchanged).  Keys that share the bin bits and the low word merge into one group
-// (about 2^-32 per pair of groups in a bin): a coarser grouping, equally exact.
+// order, and writes the runs {size, members} into `order`; k_heads_count / k_heads_place
+// list the groups' first packets in packet order, size class by size class (the
+// `work` and `single` lists for_each_run reads).  Keys that share the bin bits and the
+// low word merge into one group (about 2^-32 per pair of groups in a bin): a coarser
+// grouping, equally exact.
 // Measured against the node-table join it replaces (one CAS per packet into a 128 MiB
 // table at the device's atomic rate, k_group_flatten's list walks, the table memset):
 // see DESIGN.md §5.

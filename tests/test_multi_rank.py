@@ -185,3 +185,95 @@ def test_table_digest_matches_oracle():
     v2 = v.copy()
     v2[0, 0] ^= 1
     assert H.table_digest(k, v2) != H.table_digest(k, v)
+
+
+# ---------------------------------------------------------------- config 5: replicas
+# bench.py --workload config5 at N > 1 runs N independent nodes (an
+# exact conntrack sharding of the egress path needs cross-rank ordering): every rank
+# holds the replicated tables and its own conntrack, verdicts its own batch (here rank
+# r: the batch with fresh client ports, synth.port_variant(w, r + 1)), and the one
+# collective sums cilium_metrics.
+
+def _c5_workload():
+    return synth.config5(1 << 12, n_svc=400, n_ep=64)
+
+
+def _c5_batch(w, rank):
+    return H.apply_variant(w.frames, *synth.port_variant(w, rank + 1))
+
+
+def _c5_rank_main(rank, world, port, use_gpu, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = _c5_workload()
+        frames = _c5_batch(w, rank)
+        wr = synth.Workload(w.name, w.maps, frames, w.length, w.mark, w.endpoints, now=w.now, extra=w.extra)
+        if use_gpu:
+            from tests.test_gpu_egress import run_egress
+            ctx, maps = H.product_ctx(wr, device=0)
+            o = run_egress(ctx, wr, "cuda:0", 0, wr.n, wr.now, events=False)
+            res = {k: o[k] for k in ("ret", "identity", "ct", "reason")}
+            met = ctx.metrics()
+        else:
+            dp, maps = H.oracle_dp(wr)
+            ref = dp.lxc_egress(frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+            res = {k: getattr(ref, k) for k in ("ret", "identity", "ct", "reason")}
+            met = dp.metrics()
+        mine = torch.from_numpy(met.astype(np.int64).reshape(-1))
+        t = mine.clone()
+        shard.allreduce_counters(t)                      # the one cross-rank collective
+        ct = [maps[n].dump() for n in ("ct4", "ct6")]
+        gathered = [None] * world
+        dist.all_gather_object(gathered, {"res": res, "ct": ct, "met": mine.numpy()})
+        if rank == 0:
+            q.put({"metrics": t.numpy().reshape(256, 4, 2), "ranks": gathered})
+        if use_gpu:
+            ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _c5_check(out, world):
+    w = _c5_workload()
+    total = np.zeros((256, 4, 2), np.int64)
+    for rank, got in enumerate(out["ranks"]):
+        dp, om = H.oracle_dp(w)                          # the rank's own node: fresh tables and conntrack
+        ref = dp.lxc_egress(_c5_batch(w, rank), w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+        for k in ("ret", "identity", "ct", "reason"):
+            assert (got["res"][k] == getattr(ref, k)).all(), (rank, k)
+        for name, (ck, cv) in zip(("ct4", "ct6"), got["ct"]):
+            ok, ov = om[name].dump()
+            assert len(ck) == len(ok) and (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), (rank, name)
+        assert (got["met"].reshape(256, 4, 2) == dp.metrics().astype(np.int64)).all()
+        total += dp.metrics().astype(np.int64)
+    assert (out["metrics"] == total).all()               # the all_reduce = the nodes' sum
+
+
+def _c5_run(world, use_gpu):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_rank_main, args=(r, world, port, use_gpu, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+def test_config5_replicas_gloo_oracle():
+    _c5_check(_c5_run(2, use_gpu=False), 2)
+
+
+@pytest.mark.gpu
+def test_config5_replicas_gloo_hip():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _c5_check(_c5_run(2, use_gpu=True), 2)

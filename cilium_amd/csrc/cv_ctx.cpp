@@ -838,8 +838,15 @@ int publish(cv_ctx *c, hipStream_t s)
     if (pq.recs.empty()) return 0;
     const size_t rb = pq.recs.size() * sizeof(PatchRec), bytes = rb + pq.words.size() * 4;
     Staging *st = nullptr;
-    for (Staging &x : c->staging)
-        if (x.cap >= bytes && (!x.done || hipEventQuery(x.done) == hipSuccess)) { st = &x; break; }
+    for (Staging &x : c->staging) {
+        if (x.cap < bytes) continue;
+        if (x.done && hipEventQuery(x.done) != hipSuccess) {
+            (void)hipGetLastError();              // (hipErrorNotReady is sticky: the next launch check would see it)
+            continue;
+        }
+        st = &x;
+        break;
+    }
     if (!st) {
         Staging x;
         x.cap = std::max<size_t>(bytes, 1 << 16);

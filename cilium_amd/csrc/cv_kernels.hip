@@ -940,9 +940,14 @@ __device__ __forceinline__ void bitonic_sort(P v, uint32_t p)
         }
 }
 
+constexpr uint32_t SUBMAX = 48;                                  // largest sub-bin sorted by insertion
+__device__ __forceinline__ uint32_t sub_of(unsigned long long composite) { return (uint32_t)(composite >> 34) & 255u; }
+
 __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
 {
     __shared__ unsigned long long lv[LCAP];
+    __shared__ uint16_t perm[LCAP];
+    __shared__ uint32_t sub_cnt[256], sub_off[256], sub_max, wsum[17];
     __shared__ uint32_t tot[3], fill, hist[2][NCLASS], big[2];
     __shared__ uint32_t base;
     const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
@@ -964,7 +969,56 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
         if (in_lds) lv[j] = x; else gv[j] = x;
     }
     __syncthreads();
-    if (in_lds) bitonic_sort(lv, p); else bitonic_sort(gv, p);
+    if (in_lds) {
+        // counting sort by 8 more key bits (sub-bins of ~8 entries), then an insertion
+        // sort of each sub-bin by one thread; a bin with a sub-bin past SUBMAX (a hot
+        // address pair) takes the bitonic sort instead
+        uint32_t *cnt = sub_cnt, *off = sub_off;
+        cnt[threadIdx.x] = 0;
+        if (threadIdx.x == 0) sub_max = 0;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) atomicAdd(&cnt[sub_of(lv[j])], 1u);
+        __syncthreads();
+        uint32_t total;
+        const uint32_t mine = cnt[threadIdx.x];
+        off[threadIdx.x] = block_excl_scan(mine, wsum, total);
+        atomicMax(&sub_max, mine);
+        cnt[threadIdx.x] = 0;                                     // (reused as the fill counters)
+        __syncthreads();
+        if (sub_max > SUBMAX) {
+            bitonic_sort(lv, p);
+        } else {
+            for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+                const uint32_t sb = sub_of(lv[j]);
+                perm[off[sb] + atomicAdd(&cnt[sb], 1u)] = (uint16_t)j;
+            }
+            __syncthreads();
+            const uint32_t o = off[threadIdx.x];
+            for (uint32_t a = 1; a < mine; ++a) {                 // this thread's sub-bin
+                const uint16_t x = perm[o + a];
+                const unsigned long long xv = lv[x];
+                uint32_t t = a;
+                for (; t > 0 && lv[perm[o + t - 1]] > xv; --t) perm[o + t] = perm[o + t - 1];
+                perm[o + t] = x;
+            }
+            __syncthreads();
+            unsigned long long r[LCAP / 256];
+#pragma unroll
+            for (uint32_t k = 0; k < LCAP / 256; ++k) {
+                const uint32_t j = threadIdx.x + k * 256;
+                if (j < nb) r[k] = lv[perm[j]];
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t k = 0; k < LCAP / 256; ++k) {
+                const uint32_t j = threadIdx.x + k * 256;
+                if (j < nb) lv[j] = r[k];
+            }
+            __syncthreads();
+        }
+    } else {
+        bitonic_sort(gv, p);
+    }
     const unsigned long long *v = in_lds ? lv : gv;
     // pass 1: sizes -> run words, singletons and size classes per queue
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
@@ -1406,41 +1460,69 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
 // window ends before the first one, which the next window (run_admitted) sees exactly.
 // The stage then runs the window with each packet's budget (Acct::budget in ct_put):
 // exactly the sequential run's successes and failures, at full width.
+// What earlier members of a run changed in this window: keys they try to create (the
+// creates may fail: a later member touching one is unsure), by hash; keys they deleted
+// (deletes always happen: later lookups of them miss), exactly.
 template <class T>
-__device__ __forceinline__ bool seen_key(const uint64_t *ch, int nch, const T &t)
-{
-    uint32_t k[T::KW];
-    t.key(k);
-    const uint64_t h = key_hash<typename T::Spec>(k);
-    bool hit = false;
+struct Changed {
+    uint64_t ch[4];
+    int nch = 0;
+    uint32_t dk[2][T::KW];
+    int ndk = 0;
+    __device__ void reset() { nch = ndk = 0; }
+    __device__ bool created(const T &t) const
+    {
+        uint32_t k[T::KW];
+        t.key(k);
+        const uint64_t h = key_hash<typename T::Spec>(k);
+        bool hit = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) hit |= j < nch && ch[j] == h;
-    return hit;
-}
+        for (int j = 0; j < 4; ++j) hit |= j < nch && ch[j] == h;
+        return hit;
+    }
+    __device__ bool deleted(const T &t) const
+    {
+        uint32_t k[T::KW];
+        t.key(k);
+        bool hit = false;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            bool eq = d < ndk;
+#pragma unroll
+            for (int w = 0; w < T::KW; ++w) eq &= dk[d][w] == k[w];
+            hit |= eq;
+        }
+        return hit;
+    }
+    __device__ void add_create(const T &t)
+    {
+        uint32_t k[T::KW];
+        t.key(k);
+        if (nch < 4) ch[nch] = key_hash<typename T::Spec>(k);
+        ++nch;
+    }
+    __device__ void add_delete(const T &t)
+    {
+        if (ndk < 2) t.key(dk[ndk]);
+        ++ndk;
+    }
+    __device__ bool overflow() const { return nch > 4 || ndk > 2; }
+};
 
 template <class T>
-__device__ __forceinline__ uint64_t key_h(const T &t)
+__device__ __forceinline__ bool present(const HashTable &ct, const T &t, const Changed<T> &cg)
 {
-    uint32_t k[T::KW];
-    t.key(k);
-    return key_hash<typename T::Spec>(k);
-}
-
-template <class T>
-__device__ __forceinline__ bool present(const HashTable &ct, const T &t)
-{
+    if (cg.deleted(t)) return false;
     uint32_t k[T::KW];
     t.key(k);
     return dev_find<typename T::Spec>(ct, k, nullptr) >= 0;
 }
 
-// one packet's creates (bits 0-1), delete (bit 2) and unsure flag (bit 6); ch / nch:
-// the keys earlier members of the run changed in this window (nch > 4: too many)
-template <bool V6>
+// one packet's creates (bits 0-1), delete (bit 2) and unsure flag (bit 6)
+template <bool V6, class T>
 __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
-                                              uint64_t *ch, int &nch, const uint32_t *&map)
+                                              Changed<T> &cg, const uint32_t *&map)
 {
-    using T = typename std::conditional<V6, Tuple6, Tuple4>::type;
     const uint4 s1 = g.srec[2 * i + 1];
     const uint32_t meta = s1.z, src = s1.w;
     uint32_t seen;
@@ -1475,37 +1557,34 @@ __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev 
     tw.nexthdr = V6 ? 58u : 1u;
     tw.sport = 0; tw.dport = 0;
     tw.flags = t2.flags | TUPLE_F_RELATED;
-    if (nch > 4 || seen_key(ch, nch, t) || seen_key(ch, nch, t2) || seen_key(ch, nch, tw)) return 64u;
-    if (present(ct, t)) return 0;                                 // CT_REPLY / CT_RELATED
-    const bool est = present(ct, t2);
+    if (cg.overflow() || cg.created(t) || cg.created(t2) || cg.created(tw)) return 64u;
+    if (present(ct, t, cg)) return 0;                             // CT_REPLY / CT_RELATED
+    const bool est = present(ct, t2, cg);
     const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
     if (est) {
         if (!deny) return 0;
-        if (nch < 4) ch[nch] = key_h(t2);
-        ++nch;
+        cg.add_delete(t2);
         return 4u;                                                // ct_delete
     }
     if (deny) return 0;
-    const uint32_t A = present(ct, tw) ? 1u : 2u;                 // (an existing twin is overwritten)
-    if (nch < 4) ch[nch] = key_h(t2);
-    ++nch;
-    if (nch < 4) ch[nch] = key_h(tw);
-    ++nch;
+    const uint32_t A = present(ct, tw, cg) ? 1u : 2u;             // (an existing twin is overwritten)
+    cg.add_create(t2);
+    cg.add_create(tw);
     return A;
 }
 
 template <bool V6>
 __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, GroupScratch g, Admit a)
 {
-    uint64_t ch[4];
-    int nch = 0;
+    using T = typename std::conditional<V6, Tuple6, Tuple4>::type;
+    Changed<T> cg;
     uint32_t left = 0;                                            // members of the current run still to come
     for_each_run<true>(g, V6 ? Q_NETDEV6 : Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
-        if (!left) { left = n; nch = 0; }                         // (a lane's runs come one after another)
+        if (!left) { left = n; cg.reset(); }                      // (a lane's runs come one after another)
         --left;
         if (x < a.lo) return;                                     // run by an earlier window
         const uint32_t *map = nullptr;
-        const uint32_t v = ct_intent<V6>(p, b, g, x, ch, nch, map);
+        const uint32_t v = ct_intent<V6>(p, b, g, x, cg, map);
         uint32_t mi = 0;
 #pragma unroll
         for (int k = 0; k < ADMIT_MAPS; ++k)

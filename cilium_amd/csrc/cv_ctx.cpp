@@ -220,7 +220,7 @@ struct cv_ctx {
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
-    DevBuf gpkey, gent, gbig, gcnt, gwork6, ghcls, ghoff, ghcnt;   // the netdev path's binned grouping
+    DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_pre, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
@@ -1068,7 +1068,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     if (c->gtable.alloc(cap * 16) || c->gsingle.alloc((size_t)cmax * 4) ||
         c->gpkey.alloc((size_t)cmax * 8) || c->gent.alloc((size_t)cmax * 8) || c->gbig.alloc((size_t)cmax * 16) ||
         c->gcnt.alloc(((size_t)GBIN_MAX * GBLK + 1 + 1024) * 4) || c->gwork6.alloc((size_t)cmax * 4) ||
-        c->ghcls.alloc((size_t)cmax) || c->ghoff.alloc((size_t)cmax * 4) ||
+        c->ghword.alloc((size_t)cmax * 4) ||
         c->ghcnt.alloc(((size_t)32 * (cmax / 4096 + 1) + 1 + 1024) * 4) ||
         c->gslot.alloc((size_t)cmax * 4) || c->gnext.alloc((size_t)cmax * 4) ||
         c->gsrec.alloc((size_t)cmax * 32) ||
@@ -1103,8 +1103,7 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>(),
                     c->gsingle.as<uint32_t>(), c->gpkey.as<unsigned long long>(), c->gent.as<uint2>(),
                     c->gcnt.as<uint32_t>(), c->gbig.as<unsigned long long>(), 4, c->gnext.as<uint32_t>(),
-                    c->gwork6.as<uint32_t>(), c->ghcls.as<uint8_t>(), c->ghoff.as<uint32_t>(),
-                    c->ghcnt.as<uint32_t>()};
+                    c->gwork6.as<uint32_t>(), c->ghword.as<uint32_t>(), c->ghcnt.as<uint32_t>()};
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1380,9 +1379,16 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
         a.lo = lo;
         if ((r = launch_admission(p, bc, gs, a, s))) return r;
         uint32_t hi = n;
-        if (hipMemcpyAsync(&hi, a.hi, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        hipError_t e = hipMemcpyAsync(&hi, a.hi, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[cv] admission window at %u: %s\n", lo, hipGetErrorString(e));
             return -EIO;
-        if (hi <= lo || hi > n) return -EIO;                      // (the first packet not run is never unsure)
+        }
+        if (hi <= lo || hi > n) {                                 // (the first packet not run is never unsure)
+            fprintf(stderr, "[cv] admission window [%u, %u) of %u\n", lo, hi, n);
+            return -EPROTO;
+        }
         DpParams pw = p;
         pw.win_lo = lo;
         pw.win_span = hi - lo;
@@ -1842,8 +1848,8 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         if (!fits && cts.size() > (size_t)ADMIT_MAPS)
             n = ct_plan(c, cts, n, 2, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
-        gs.gbits = 4;                                             // bins of ~2048 packets (at most GBIN_MAX)
-        while (gs.gbits < 13 && (1ull << (gs.gbits + 11)) < n) ++gs.gbits;
+        gs.gbits = 4;                                             // bins of ~1024 packets (at most GBIN_MAX)
+        while (gs.gbits < 14 && (1ull << (gs.gbits + 10)) < n) ++gs.gbits;
         if (!fits && cts.size() <= (size_t)ADMIT_MAPS) {
             r = run_admitted(c, p, chunk(b, off, n), chunk(o, off, b->stride), now, with_prefilter, gs, cts,
                              (hipStream_t)stream);

@@ -145,13 +145,13 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t gbits;            // log2 of the number of bins
     uint32_t *single6;         // the singleton packets of the IPv6 queue (Q_NETDEV6)
     uint32_t *work6;           // the IPv6 queue's schedule (`work` of Q_NETDEV6)
-    uint8_t *hcls;             // per packet: 1 + its list if it is a group's first packet (k_heads_place), else 0
-    uint32_t *hoff;            // per first packet of a multi-packet group: its run's offset in `order`
+    uint32_t *hword;           // per packet: 0, or for a group's first packet (1 + its list) << 26 | its run's
+                               // offset in `order` (k_gbin_group -> k_heads_place)
     uint32_t *hcnt;            // per (list, tile) head counts -> positions (k_heads_count / place)
 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses
-constexpr uint32_t GBLK = 256, GBIN_MAX = 1u << 13;
+constexpr uint32_t GBLK = 256, GBIN_MAX = 1u << 14;
 // GroupScratch queues: appends go to one of QSPLIT sub-queues by block index (less
 // contention on one counter); blocks b with b % QSPLIT == k hold at most
 // n / QSPLIT + BLOCK + QSPLIT packets (grids are multiples of QSPLIT or one block per 256

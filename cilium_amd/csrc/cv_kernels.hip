@@ -16,6 +16,15 @@
 
 namespace cv {
 
+// the status of the launches just made: 0, or -EIO with the HIP error on stderr
+static int launch_status(const char *where)
+{
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    fprintf(stderr, "[cv] %s: %s\n", where, hipGetErrorString(e));
+    return -5;
+}
+
 // ================================================================== config 1
 // A wave's record load and probes: wave-cooperative 1-KiB record loads through LDS
 // when the wave's 64 records are all in the batch (64-B stride), quad probes
@@ -347,7 +356,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         }
         if (!live) continue;
         g.pkey[i] = gkey;
-        g.hcls[i] = 0;
+        g.hword[i] = 0;
         g.gslot[i] = NONE;
         const bool fwd_here = !staged && !v6stage && ret == TC_ACT_OK;
         if (M::EV && o.frames) {
@@ -807,7 +816,7 @@ void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStr
 // table at the device's atomic rate, k_group_flatten's list walks, the table memset):
 // see DESIGN.md §5.
 constexpr uint32_t SCAN_TILE = 4096;                             // entries per scan block (1024 x 4)
-constexpr uint32_t LCAP = 4096;                                  // bin entries sorted in LDS
+constexpr uint32_t LCAP = 2048;                                  // bin entries sorted in LDS
 
 __device__ __forceinline__ uint32_t gkey_bin(unsigned long long k, uint32_t bits)
 {
@@ -947,18 +956,14 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
 {
     __shared__ unsigned long long lv[LCAP];
     __shared__ uint16_t perm[LCAP];
-    __shared__ uint32_t sub_cnt[256], sub_off[256], sub_max, wsum[17];
-    __shared__ uint32_t tot[3], fill, hist[2][NCLASS], big[2];
-    __shared__ uint32_t base;
+    __shared__ uint32_t sub_cnt[256], sub_off[256], sub_max, wsum[17], fill, big[2];
     const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
     const uint32_t start = g.gcnt[b * GBLK], end = b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m];
     const uint32_t nb = end - start;
     if (!nb) return;                                              // (block-uniform)
     uint32_t p = 64;
     while (p < nb) p <<= 1;
-    if (threadIdx.x < 3) tot[threadIdx.x] = 0;
     if (threadIdx.x == 0) fill = 0;
-    if (threadIdx.x < 2 * NCLASS) hist[threadIdx.x / NCLASS][threadIdx.x % NCLASS] = 0;
     if (threadIdx.x < 2) big[threadIdx.x] = 0;
     // composite {key low word, packet}: sorted, a group's members are contiguous and ascending
     unsigned long long *gv = g.gbig + 2 * (size_t)start;          // (a bin past LCAP: 2 words per entry)
@@ -970,7 +975,7 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
     }
     __syncthreads();
     if (in_lds) {
-        // counting sort by 8 more key bits (sub-bins of ~8 entries), then an insertion
+        // counting sort by 8 more key bits (sub-bins of a few entries), then an insertion
         // sort of each sub-bin by one thread; a bin with a sub-bin past SUBMAX (a hot
         // address pair) takes the bitonic sort instead
         uint32_t *cnt = sub_cnt, *off = sub_off;
@@ -1020,58 +1025,37 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
         bitonic_sort(gv, p);
     }
     const unsigned long long *v = in_lds ? lv : gv;
-    // pass 1: sizes -> run words, singletons and size classes per queue
+    // one pass: the runs into the bin's own region of `order` (2 words per entry: a run
+    // of c members takes c + 1 <= 2c; no allocation atomics), and every group's first
+    // packet marked with its list and run (k_heads_place lists them in packet order)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
         const uint32_t key = (uint32_t)(v[j] >> 32);
         if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;     // not a group's first member
         uint32_t c = 1;
         while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
-        const int q6 = key & 1u;
-        if (c == 1) atomicAdd(&tot[1 + q6], 1u);
-        else { atomicAdd(&tot[0], c + 1); atomicMax(&big[q6], c); }
-        atomicAdd(&hist[q6][size_class(c)], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        base = tot[0] ? atomicAdd(&g.cursor[RUN_CURSOR], tot[0]) : 0u;
-        if (tot[1]) atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV], tot[1]);
-        if (tot[2]) atomicAdd(&g.cursor[SINGLE_WORD0 + Q_NETDEV6], tot[2]);
-    }
-    if (threadIdx.x < 2 * NCLASS) {
-        const int q6 = threadIdx.x / NCLASS, c = threadIdx.x % NCLASS;
-        const uint32_t h = hist[q6][c];
-        if (h) atomicAdd(&g.cursor[qcls(q6 ? Q_NETDEV6 : Q_NETDEV, c)], h);
-    }
-    if (threadIdx.x < 2 && big[threadIdx.x] > 8)
-        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : Q_NETDEV)], big[threadIdx.x]);
-    __syncthreads();
-    // pass 2: the runs into `order`; every group's first packet marked with its list
-    // (k_heads_place lists them in packet order, class by class)
-    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
-        const uint32_t key = (uint32_t)(v[j] >> 32);
-        if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;
-        uint32_t c = 1;
-        while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
         const uint32_t q6 = key & 1u, x = (uint32_t)v[j];
-        uint32_t list = 15;                                       // 15: singletons
+        uint32_t list = 15, off = 0;                              // 15: singletons
         if (c > 1) {
-            const uint32_t off = base + atomicAdd(&fill, c + 1);
+            off = 2 * start + atomicAdd(&fill, c + 1);
             uint32_t *o = g.order + off;
             o[0] = c;
             for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
-            g.hoff[x] = off;
             list = 15 - (uint32_t)size_class(c);                  // largest class first
+            if (c > 8) atomicMax(&big[q6], c);
         }
-        g.hcls[x] = (uint8_t)(1 + q6 * 16 + list);
+        g.hword[x] = (1u + q6 * 16 + list) << 26 | off;
     }
+    __syncthreads();
+    if (threadIdx.x < 2 && big[threadIdx.x])                      // (diagnostics: the largest group)
+        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : Q_NETDEV)], big[threadIdx.x]);
 }
 
 // The groups' first packets listed in packet order, list by list (IPv4 runs class
 // 15 .. 1, IPv4 singletons, the same for IPv6): per tile of HTILE packets a count per
 // list, one scan, then each tile places its heads (ranks within a tile by LDS atomics:
-// a wave's lanes still take packets of one tile).  The stage's first members then
-// read their stage records and write their verdicts along the batch instead of at
-// random.
+// a wave's lanes still take packets of one tile) and the lists' lengths go to the
+// cursor words for_each_run reads.  The stage's first members then read their stage
+// records and write their verdicts along the batch instead of at random.
 constexpr uint32_t HTILE = 4096;
 __global__ void __launch_bounds__(1024) k_heads_count(GroupScratch g, uint32_t n, uint32_t tiles)
 {
@@ -1080,7 +1064,7 @@ __global__ void __launch_bounds__(1024) k_heads_count(GroupScratch g, uint32_t n
     __syncthreads();
     for (uint32_t k = 0; k < HTILE / 1024; ++k) {
         const uint32_t x = blockIdx.x * HTILE + k * 1024 + threadIdx.x;
-        const uint32_t h = x < n ? g.hcls[x] : 0u;
+        const uint32_t h = x < n ? g.hword[x] >> 26 : 0u;
         if (h) atomicAdd(&c[h - 1], 1u);
     }
     __syncthreads();
@@ -1092,14 +1076,20 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
     __shared__ uint32_t pos[32], start[4];
     if (threadIdx.x < 32) pos[threadIdx.x] = g.hcnt[threadIdx.x * tiles + blockIdx.x];
     if (threadIdx.x < 4) start[threadIdx.x] = g.hcnt[(threadIdx.x >> 1) * 16 * tiles + (threadIdx.x & 1) * 15 * tiles];
+    if (blockIdx.x == 0 && threadIdx.x < 32) {                    // list lengths -> the cursor words
+        const uint32_t key = threadIdx.x, q = key >> 4 ? Q_NETDEV6 : Q_NETDEV, list = key & 15u;
+        const uint32_t cnt = g.hcnt[(key + 1) * tiles] - g.hcnt[key * tiles];   // ([32 * tiles] = the total)
+        if (list == 15) g.cursor[SINGLE_WORD0 + q] = cnt;
+        g.cursor[qcls(q, list == 15 ? 0 : 15 - list)] = cnt;
+    }
     __syncthreads();
     for (uint32_t k = 0; k < HTILE / 1024; ++k) {
         const uint32_t x = blockIdx.x * HTILE + k * 1024 + threadIdx.x;
-        const uint32_t h = x < n ? g.hcls[x] : 0u;
+        const uint32_t hw = x < n ? g.hword[x] : 0u, h = hw >> 26;
         if (!h) continue;
         const uint32_t key = h - 1, q6 = key >> 4, at = atomicAdd(&pos[key], 1u);
         if ((key & 15u) == 15u) (q6 ? g.single6 : g.single)[at - start[q6 * 2 + 1]] = x;
-        else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = g.hoff[x];
+        else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = hw & ((1u << 26) - 1);
     }
 }
 
@@ -1206,7 +1196,7 @@ int launch_ct_load(const HashTable &t, int v6, const uint32_t *keys, const uint3
     uint64_t g = (n + BLOCK - 1) / BLOCK;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_load, dim3((uint32_t)g), dim3(BLOCK), 0, s, t, v6, keys, vals, n, fail);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 // every live entry (tag >= 3): its slot index, key and value, compacted in no order
@@ -1321,7 +1311,7 @@ int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_gc, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, time, deleted);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 // slots by tag class: out[0] empty, out[1] dead (tombstones), out[2] live
@@ -1355,7 +1345,7 @@ int launch_ct_tags(const HashTable &t, int v6, uint64_t nb, unsigned long long *
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_tags, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, out);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 // ------------------------------------------------------------------ host launchers
@@ -1370,7 +1360,7 @@ int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, 
 {
     if (!b.n) return 0;
     hipLaunchKernelGGL(k_xdp_prefilter, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, o);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 // fold the per-chunk delta words into policy_entry.packets / .bytes
@@ -1393,7 +1383,7 @@ int launch_policy_fold(const HashTable &pol, hipStream_t s)
     uint64_t g = (slots + BLOCK - 1) / BLOCK;
     if (g > 2048) g = 2048;
     hipLaunchKernelGGL(k_policy_fold, dim3((uint32_t)g), dim3(BLOCK), 0, s, pol, slots);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s)
@@ -1401,7 +1391,7 @@ int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const Ou
     if (!b.n) return 0;
     const uint32_t grid = (b.n + PPT * BLOCK - 1) / (PPT * BLOCK);
     hipLaunchKernelGGL(k_policy_ingress, dim3(grid), dim3(BLOCK), 0, s, p, ep, b, o);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter, const OutDev &o,
@@ -1412,9 +1402,9 @@ int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     if (ev) hipLaunchKernelGGL(k_netdev_front<true>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     else hipLaunchKernelGGL(k_netdev_front<false>, grid, blk, 0, s, p, b, o, g, with_prefilter);
-    if (hipGetLastError() != hipSuccess) return -5;
+    if (const int r = launch_status(__func__)) return r;
     launch_gbin_groups(g, b.n, s);                                // both families' runs and singletons, listed
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 // the IPv4 runs, then the IPv6 runs (the two families' conntrack state is disjoint, so
@@ -1433,7 +1423,7 @@ int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, con
     if (ev) hipLaunchKernelGGL(k_ct_stage6<true>, grid, blk, 0, s, p, b, o, g6, now);
     else hipLaunchKernelGGL(k_ct_stage6<false>, grid, blk, 0, s, p, b, o, g6, now);
     if (!p.ct_guard) hipLaunchKernelGGL(k_ct_commit, grid, blk, 0, s, p, b, o, g, now);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, int with_prefilter, const OutDev &o,
@@ -1719,7 +1709,7 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
                            L, tm);
     }
     hipLaunchKernelGGL(k_admit_budget, grid, blk, 0, s, a, b.n);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 // the agent's staged table writes (cv_ctx.cpp PatchQueue): a block per run of words
@@ -1736,13 +1726,13 @@ int launch_patches(const PatchRec *recs, uint32_t n, const uint32_t *words, hipS
 {
     if (!n) return 0;
     hipLaunchKernelGGL(k_patch, dim3(n < 4096 ? n : 4096), dim3(BLOCK), 0, s, recs, n, words);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *io_dev, hipStream_t s)
 {
     hipLaunchKernelGGL(k_ct_op, dim3(1), dim3(64), 0, s, t, v6, op, flags, io_dev);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint64_t *out_slots, uint32_t *out_keys, uint32_t *out_vals,
@@ -1753,7 +1743,7 @@ int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint64_t *out_slots,
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_ct_scan, dim3((uint32_t)g), dim3(BLOCK), 0, s, t, v6, slots, out_slots, out_keys, out_vals,
                        count, max);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
+    return launch_status(__func__);
 }
 
 }  // namespace cv

@@ -348,8 +348,9 @@ def test_config3_dual_stack_64b_records(dev):
 def test_ct_capacity_ingress(dev):
     """A CT map filled to max_entries: creates past it fail (DROP_CT_CREATE_FAILED,
     kernel HASH semantics) at the same packets as the oracle, including a tuple that
-    fits while its ICMP-related twin does not; the launches next to the limit are the
-    exact one-packet ones.  Live counts, tables and verdicts compared every batch."""
+    fits while its ICMP-related twin does not; the launches next to the limit run
+    admitted (exact budgets per packet, cv_ctx.cpp run_admitted).  Live counts, tables
+    and verdicts compared every batch."""
     w = synth.config3(1 << 13, 64, n_ep=64, n_cidrs=1024, n_ids=100, seed=31, v6_frac=0.3, n_flows6=16)
     for name, room in (("ct4", 150), ("ct6", 10)):
         spec = w.maps[name]

@@ -1374,6 +1374,9 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     a.hi = c->adm_win.as<uint32_t>();
     int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
     if (r) return r;
+    // packets that reach no conntrack stage keep 0 (no creates, no deletes, map 0);
+    // k_ct_intent rewrites the others every window
+    if (hipMemsetAsync(a.ib, 0, n, s) != hipSuccess) return -EIO;
     uint32_t windows = 0;
     for (uint32_t lo = 0; lo < n; ++windows) {
         a.lo = lo;

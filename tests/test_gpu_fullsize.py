@@ -8,7 +8,12 @@
   order-independent digest (tests/harness.table_digest = the oracle's or_map_digest);
 * config 4: one rank's part of the node-wide flow set (bench.py at N > 1, two ranks'
   shards here, each against its own oracle: shards share no conntrack state);
-* config 5: the 50k-service dual-stack egress tables.
+* config 5: the 50k-service dual-stack egress tables;
+* bench.py's own timed regime (round 3): two consecutive fresh 2^24-packet config-3
+  steps on the 16M-flow table with the CT sized as bench.py sizes it, and rank 0 of 8's
+  config-4 shard at BASELINE size (16M flows), against the address-pair-sharded oracle
+  (tests/harness.ShardedOracle): every per-packet output, metrics, the node's policy
+  counters and the CT digest after each step.
 """
 import numpy as np
 import pytest

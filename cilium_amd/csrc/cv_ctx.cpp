@@ -1392,6 +1392,12 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
             fprintf(stderr, "[cv] admission window [%u, %u) of %u\n", lo, hi, n);
             return -EPROTO;
         }
+        if (getenv("CV_ADMIT_STATS") && hi < n) {                 // why the window ends: the unsure packet
+            uint8_t why = 0;
+            (void)hipMemcpy(&why, a.ib + hi, 1, hipMemcpyDeviceToHost);
+            fprintf(stderr, "[cv admit] window [%u, %u): packet %u unsure (%s)\n", lo, hi, hi,
+                    (why & 128) ? "too many changed keys" : (why & 4) ? "twin" : "tuple created earlier");
+        }
         DpParams pw = p;
         pw.win_lo = lo;
         pw.win_span = hi - lo;

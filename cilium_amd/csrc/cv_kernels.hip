@@ -1547,7 +1547,8 @@ __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev 
     tw.nexthdr = V6 ? 58u : 1u;
     tw.sport = 0; tw.dport = 0;
     tw.flags = t2.flags | TUPLE_F_RELATED;
-    if (cg.overflow() || cg.created(t) || cg.created(t2)) return 64u;
+    if (cg.overflow()) return 64u | 128u;                         // (bit 7: diagnostics, CV_ADMIT_STATS)
+    if (cg.created(t) || cg.created(t2)) return 64u;
     if (present(ct, t, cg)) return 0;                             // CT_REPLY / CT_RELATED
     const bool est = present(ct, t2, cg);
     const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
@@ -1557,7 +1558,7 @@ __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev 
         return 4u;                                                // ct_delete
     }
     if (deny) return 0;
-    if (cg.created(tw)) return 64u;                               // (the twin exists iff that create went in)
+    if (cg.created(tw)) return 64u | 4u;                          // (the twin exists iff that create went in)
     const uint32_t A = present(ct, tw, cg) ? 1u : 2u;             // (an existing twin is overwritten)
     cg.add_create(t2);
     cg.add_create(tw);

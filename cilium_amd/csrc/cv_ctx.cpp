@@ -1103,7 +1103,8 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     (uint32_t)(c->gn / QSPLIT + 512), c->gwork.as<uint32_t>(), c->gifx.as<uint32_t>(),
                     c->gsingle.as<uint32_t>(), c->gpkey.as<unsigned long long>(), c->gent.as<uint2>(),
                     c->gcnt.as<uint32_t>(), c->gbig.as<unsigned long long>(), 4, c->gnext.as<uint32_t>(),
-                    c->gwork6.as<uint32_t>(), c->ghword.as<uint32_t>(), c->ghcnt.as<uint32_t>()};
+                    c->gwork6.as<uint32_t>(), c->ghword.as<uint32_t>(), c->ghcnt.as<uint32_t>(), (uint32_t)Q_NETDEV,
+                    0};
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1899,6 +1900,8 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 7, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
+        gs.gbits = 4;                                             // (the binned grouping of the components)
+        while (gs.gbits < 14 && (1ull << (gs.gbits + 10)) < n) ++gs.gbits;
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
         if ((r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0,

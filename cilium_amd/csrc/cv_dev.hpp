@@ -2053,6 +2053,28 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
     }
 }
 
+// fn(i, run size) for every member of every group of queue q listed flat by the
+// binned grouping (g.flat: one list, the groups' first packets in packet order; a
+// singleton's entry is its packet, SINGLE_RUN-tagged)
+template <class F>
+__device__ __forceinline__ void for_each_flat(const GroupScratch &g, int q, F &&fn)
+{
+    const uint32_t total = g.cursor[qcls(q, 0)];
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    for (uint32_t j = tid; j < total; j += stride) {
+        const uint32_t e = g.work[j];
+        if (e & SINGLE_RUN) { fn(e & ~SINGLE_RUN, 1u); continue; }
+        const uint32_t cnt = g.order[e];
+        uint32_t v = g.order[e + 1];
+#pragma unroll 1
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t vn = k + 1 < cnt ? g.order[e + 2 + k] : NONE;
+            fn(v, cnt);
+            v = vn;
+        }
+    }
+}
+
 // node key of an unordered address pair (v4 words or v6 4-word addresses), mixed
 // with a salt that separates families / stages
 __device__ __forceinline__ uint64_t pair_hash4(uint32_t a, uint32_t b, uint64_t salt)

@@ -148,6 +148,8 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *hword;           // per packet: 0, or for a group's first packet (1 + its list) << 26 | its run's
                                // offset in `order` (k_gbin_group -> k_heads_place)
     uint32_t *hcnt;            // per (list, tile) head counts -> positions (k_heads_count / place)
+    uint32_t q4;               // the IPv4 queue the binned grouping fills (Q_NETDEV, or Q_CT4 on egress)
+    uint32_t flat;             // 1: one list per queue, every group's first packet in packet order (egress)
 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses
@@ -175,6 +177,9 @@ constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (
 constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
 constexpr int EG_WORDS = 16;
 
+// the binned grouping of the packets whose g.pkey is set (cv_kernels.hip): runs, and the
+// lists of the groups' first packets (g.flat: one per queue)
+void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s);
 // flatten + schedule the groups of queue q (before the stage that runs them)
 // sched: 0 runs in queue order (no k_group_schedule), 1 largest size class first,
 // 2 smallest first

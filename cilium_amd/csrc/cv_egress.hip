@@ -15,7 +15,8 @@
 //     the address pairs a packet can touch — its egress tuple, the NATed tuple a
 //     service create writes, the pair its local delivery sees after rewrites and the
 //     pairs a reverse-NAT of an entry it reads or creates can lead to — built by
-//     k_egress_pairs (lock-free union-find) and linked by k_group_link.
+//     k_egress_pairs (lock-free union-find), keyed by component in k_group_link and
+//     grouped by binning (launch_gbin_groups).
 // Within a group packets run in packet order; groups share no entry.
 #include "cv_dev.hpp"
 
@@ -658,12 +659,17 @@ __global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, Gr
     }
 }
 
+// Every packet of a conntrack stage keyed by its component (the union-find root of its
+// address-pair node) for the binned grouping (k_gbin_group, flat lists: the groups'
+// first packets in packet order, about the order the node-table queue used to have)
 __global__ void __launch_bounds__(BLOCK) k_group_link(BatchDev b, GroupScratch g)
 {
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         const uint32_t s = g.gslot[i];
-        if (s == NONE) { g.next[i] = NONE; continue; }
-        group_push(g, uf_find(g, s), i, (g.ifx[i] & BIT_V6) ? Q_CT6 : Q_CT4);
+        g.hword[i] = 0;
+        if (s == NONE) { g.pkey[i] = 0; continue; }
+        const uint64_t root = uf_find(g, s);
+        g.pkey[i] = (mix64(root ^ 0xC0FFEE0000000000ULL) & ~3ull) | 2ull | ((g.ifx[i] & BIT_V6) ? 1ull : 0ull);
     }
 }
 
@@ -977,9 +983,8 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    // runs in queue order: k_group_flatten without k_group_schedule (measured faster here
-    // than size-class order)
-    for_each_run<false>(g, V6 ? Q_CT6 : Q_CT4, false, [&](uint32_t x, uint32_t) {
+    // runs in the order of their first packets (measured faster here than size-class order)
+    for_each_flat(g, V6 ? Q_CT6 : Q_CT4, [&](uint32_t x, uint32_t) {
         if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
         else egress4_one(p, b, now, o, g, x, m);
     });
@@ -1063,13 +1068,16 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
-    launch_group_runs(g, Q_CT4, grid.x, 0, s);
+    g.q4 = Q_CT4;
+    g.flat = 1;
+    launch_gbin_groups(g, b.n, s);
     if (ev) hipLaunchKernelGGL((k_egress_ct<false, true>), grid, blk, 0, s, p, b, now, o, g);
     else hipLaunchKernelGGL((k_egress_ct<false, false>), grid, blk, 0, s, p, b, now, o, g);
     if (b.stride >= 128) {
-        launch_group_runs(g, Q_CT6, grid.x, 0, s);
-        if (ev) hipLaunchKernelGGL((k_egress_ct<true, true>), grid, blk, 0, s, p, b, now, o, g);
-        else hipLaunchKernelGGL((k_egress_ct<true, false>), grid, blk, 0, s, p, b, now, o, g);
+        GroupScratch g6 = g;
+        g6.work = g.work6;
+        if (ev) hipLaunchKernelGGL((k_egress_ct<true, true>), grid, blk, 0, s, p, b, now, o, g6);
+        else hipLaunchKernelGGL((k_egress_ct<true, false>), grid, blk, 0, s, p, b, now, o, g6);
     }
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);

@@ -1034,20 +1034,20 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
         uint32_t c = 1;
         while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
         const uint32_t q6 = key & 1u, x = (uint32_t)v[j];
-        uint32_t list = 15, off = 0;                              // 15: singletons
+        uint32_t list = g.flat ? 0u : 15u, off = 1u << 25;        // 15: singletons (bit 25: a singleton)
         if (c > 1) {
             off = 2 * start + atomicAdd(&fill, c + 1);
             uint32_t *o = g.order + off;
             o[0] = c;
             for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
-            list = 15 - (uint32_t)size_class(c);                  // largest class first
+            if (!g.flat) list = 15 - (uint32_t)size_class(c);     // largest class first
             if (c > 8) atomicMax(&big[q6], c);
         }
         g.hword[x] = (1u + q6 * 16 + list) << 26 | off;
     }
     __syncthreads();
     if (threadIdx.x < 2 && big[threadIdx.x])                      // (diagnostics: the largest group)
-        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : Q_NETDEV)], big[threadIdx.x]);
+        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : g.q4)], big[threadIdx.x]);
 }
 
 // The groups' first packets listed in packet order, list by list (IPv4 runs class
@@ -1077,10 +1077,14 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
     if (threadIdx.x < 32) pos[threadIdx.x] = g.hcnt[threadIdx.x * tiles + blockIdx.x];
     if (threadIdx.x < 4) start[threadIdx.x] = g.hcnt[(threadIdx.x >> 1) * 16 * tiles + (threadIdx.x & 1) * 15 * tiles];
     if (blockIdx.x == 0 && threadIdx.x < 32) {                    // list lengths -> the cursor words
-        const uint32_t key = threadIdx.x, q = key >> 4 ? Q_NETDEV6 : Q_NETDEV, list = key & 15u;
+        const uint32_t key = threadIdx.x, q = key >> 4 ? Q_NETDEV6 : g.q4, list = key & 15u;
         const uint32_t cnt = g.hcnt[(key + 1) * tiles] - g.hcnt[key * tiles];   // ([32 * tiles] = the total)
-        if (list == 15) g.cursor[SINGLE_WORD0 + q] = cnt;
-        g.cursor[qcls(q, list == 15 ? 0 : 15 - list)] = cnt;
+        if (g.flat) {
+            if (list == 0) g.cursor[qcls(q, 0)] = cnt;            // (for_each_flat)
+        } else {
+            if (list == 15) g.cursor[SINGLE_WORD0 + q] = cnt;
+            g.cursor[qcls(q, list == 15 ? 0 : 15 - list)] = cnt;
+        }
     }
     __syncthreads();
     for (uint32_t k = 0; k < HTILE / 1024; ++k) {
@@ -1088,8 +1092,9 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
         const uint32_t hw = x < n ? g.hword[x] : 0u, h = hw >> 26;
         if (!h) continue;
         const uint32_t key = h - 1, q6 = key >> 4, at = atomicAdd(&pos[key], 1u);
-        if ((key & 15u) == 15u) (q6 ? g.single6 : g.single)[at - start[q6 * 2 + 1]] = x;
-        else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = hw & ((1u << 26) - 1);
+        if (g.flat) (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = (hw & (1u << 25)) ? (x | SINGLE_RUN) : (hw & ((1u << 25) - 1));
+        else if ((key & 15u) == 15u) (q6 ? g.single6 : g.single)[at - start[q6 * 2 + 1]] = x;
+        else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = hw & ((1u << 25) - 1);
     }
 }
 

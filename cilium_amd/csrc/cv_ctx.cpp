@@ -68,9 +68,9 @@ struct DevHash {
 
 template <class S>
 int build_hash(DevHash &d, const std::vector<std::vector<uint32_t>> &keys, const std::vector<std::vector<uint32_t>> &ivals,
-               uint32_t vstride, const std::vector<uint8_t> *vals, std::vector<int64_t> *slots)
+               uint32_t vstride, const std::vector<uint8_t> *vals, std::vector<int64_t> *slots, size_t room = 0)
 {
-    uint64_t nb = buckets_for(keys.size(), S::SPB);
+    uint64_t nb = buckets_for(keys.size() + room, S::SPB);   // (room: entries later writes may add in place)
     for (int attempt = 0; attempt < 8; ++attempt, nb <<= 1) {
         d.hb.assign(nb * S::BW, 0);
         HashTable t{d.hb.data(), nullptr, nb - 1, vstride, (uint32_t)S::SPB};
@@ -334,14 +334,17 @@ int upload_lpm4(DevLpm4 &d, std::vector<Pfx> &px, bool image = false)
     int r = d.l1.upload(b.l1.data(), b.l1.size() * 4);
     if (!r) r = d.chunks.alloc(cap * 1024);
     if (!r && hipMemcpy(d.chunks.p, b.chunks.data(), b.chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess) r = -EIO;
-    if (!r && !k32.empty()) r = build_hash<Host32Spec>(d.full, k32, v32, 0, nullptr, nullptr);
+    // (an image keeps a /32 front with room for as many more, even an empty one)
+    const bool front = !k32.empty() || image;
+    if (!r && front)
+        r = build_hash<Host32Spec>(d.full, k32, v32, 0, nullptr, nullptr, image ? std::max<size_t>(k32.size(), 4096) : 0);
     d.view = r ? Lpm4{nullptr, nullptr, HashTable{}}
-               : Lpm4{d.l1.as<uint32_t>(), d.chunks.as<uint32_t>(), k32.empty() ? HashTable{} : d.full.view};
+               : Lpm4{d.l1.as<uint32_t>(), d.chunks.as<uint32_t>(), front ? d.full.view : HashTable{}};
     d.image = image && !r;
     d.chunk_cap = cap;
     d.chunks_on_dev = nch;
     d.front_live = k32.size();
-    if (d.image) d.hb = std::move(b);
+    if (d.image) { d.hb = std::move(b); d.hb.touched.clear(); }
     else { d.longer.clear(); d.hb = Lpm4Builder{}; d.hb.l1.clear(); d.hb.l1.shrink_to_fit(); }
     return r;
 }
@@ -355,7 +358,7 @@ int put_words(PatchQueue &pq, const DevBuf &dst, const uint32_t *src, size_t lo,
     return 0;
 }
 
-int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
+int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px, size_t room = 0)
 {
     std::stable_sort(px.begin(), px.end(), [](const Pfx &x, const Pfx &y) { return x.prio < y.prio; });
     // later (higher priority) entries win for identical (masked addr, plen)
@@ -379,7 +382,7 @@ int upload_lpm6(DevLpm6 &d, std::vector<Pfx> &px)
         vals.push_back({kv.second});
         d.lens_cnt[(int)kv.first[4]]++;
     }
-    int r = build_hash<Lpm6Spec>(d.h, keys, vals, 0, nullptr, nullptr);
+    int r = build_hash<Lpm6Spec>(d.h, keys, vals, 0, nullptr, nullptr, room ? std::max(keys.size(), room) : 0);
     if (r) return r;
     d.live = keys.size();
     std::vector<uint8_t> l(LENS_CAP, 0);
@@ -441,7 +444,7 @@ int compile_ipcache(cv_ctx *c, HostMap *m)
     });
     if (err) return err;
     int r = upload_lpm4(c->ipc4, p4, true);
-    if (!r) r = upload_lpm6(c->ipc6, p6);
+    if (!r) r = upload_lpm6(c->ipc6, p6, 4096);
     c->ipc4.of = r ? nullptr : m;
     m->log_clear();
     return r;
@@ -456,16 +459,24 @@ int compile_ipcache(cv_ctx *c, HostMap *m)
 // longer prefixes inside it in length order, as the full build inserts them).  New
 // chunks are appended (the old ones become garbage until the next full build).
 // Returns 0 when done, 1 when a full compile is needed, < 0 on error.
+// why the last incremental update needed a full compile (CV_REBUILD_WHY prints it)
+static const char *rebuild_why = "";
+#define NEED_FULL(why)          \
+    do {                        \
+        rebuild_why = why;      \
+        return 1;               \
+    } while (0)
+
 int update_ipcache4(cv_ctx *c, HostMap *m)
 {
     DevLpm4 &d = c->ipc4;
-    if (!m || !d.image || d.of != m || m->log_full) return 1;
+    if (!m || !d.image || d.of != m || m->log_full) NEED_FULL("no image of this map");
     std::set<uint32_t> dirty;                  // level-1 slots to rebuild
     std::vector<uint64_t> front_b;             // front buckets touched
     HashTable ft{d.full.hb.data(), nullptr, d.full.nb ? d.full.nb - 1 : 0, 0, (uint32_t)Host32Spec::SPB};
     for (const std::vector<uint8_t> &k : m->log) {
         const uint32_t plen = rd32(k.data());
-        if (plen < 32) return 1;               // spans the static bits: both families, /0
+        if (plen < 32) NEED_FULL("a /0 key");               // spans the static bits: both families, /0
         if (k[4] || k[5] || k[6]) continue;    // matches no lookup key
         if (k[7] != 1) continue;               // (IPv6: update_ipcache6)
         if (plen > 64) continue;
@@ -474,13 +485,13 @@ int update_ipcache4(cv_ctx *c, HostMap *m)
         const uint8_t *v = m->lookup_exact(k.data());
         if (v && (rd32(v) & 0x80000000u)) return -ERANGE;
         if (len == 32) {                       // hash front
-            if (!d.full.view.buckets) return 1;
+            if (!d.full.view.buckets) NEED_FULL("no /32 front");
             if (v) {
                 const uint32_t val = rd32(v);
                 const int64_t sl = host_find<Host32Spec>(ft, &raw);
                 const int64_t s2 = host_upsert<Host32Spec>(ft, &raw, &val);
-                if (s2 < 0) return 1;
-                if (sl < 0 && ++d.front_live * 10 > d.full.nb * Host32Spec::SPB * 8) return 1;   // > 80 % load
+                if (s2 < 0) NEED_FULL("/32 front probe limit");
+                if (sl < 0 && ++d.front_live * 10 > d.full.nb * Host32Spec::SPB * 8) NEED_FULL("/32 front over 80% load");   // > 80 % load
                 front_b.push_back((uint64_t)s2 / Host32Spec::SPB);
             } else {
                 const int64_t sl = host_find<Host32Spec>(ft, &raw);
@@ -509,7 +520,7 @@ int update_ipcache4(cv_ctx *c, HostMap *m)
             dirty.insert(x);
         } else {
             const uint32_t span = 1u << (16 - len);
-            if (span > 4096) return 1;
+            if (span > 4096) NEED_FULL("a prefix shorter than /4");
             const uint32_t base = (addr >> 16) & ~(span - 1);
             for (uint32_t i = 0; i < span; ++i) dirty.insert(base + i);
         }
@@ -524,6 +535,7 @@ int update_ipcache4(cv_ctx *c, HostMap *m)
         const uint8_t *v0 = m->lookup(key);
         const uint32_t base = v0 ? rd32(v0) : 0u;
         if (base & 0x80000000u) return -ERANGE;
+        d.hb.release(d.hb.l1[x]);
         d.hb.l1[x] = base;
         auto it = d.longer.find(x);
         if (it == d.longer.end()) continue;
@@ -533,9 +545,18 @@ int update_ipcache4(cv_ctx *c, HostMap *m)
         for (const Pfx &p : lv) d.hb.insert(bswap32(p.a[0]), p.plen, p.value);
     }
     const size_t nch = d.hb.chunks.size() / 256;
-    if (nch > d.chunk_cap) return 1;           // out of device room: a full build compacts
+    if (nch > d.chunk_cap) NEED_FULL("out of device chunk room");           // out of device room: a full build compacts
     PatchQueue &pq = c->pq;
-    put_words(pq, d.chunks, d.hb.chunks.data(), d.chunks_on_dev * 256, nch * 256);
+    std::vector<uint32_t> &tc = d.hb.touched;  // new and reused chunks (batches before this
+    std::sort(tc.begin(), tc.end());           // publication no longer run: stream order)
+    tc.erase(std::unique(tc.begin(), tc.end()), tc.end());
+    for (size_t i = 0; i < tc.size();) {
+        size_t j = i + 1;
+        while (j < tc.size() && tc[j] == tc[j - 1] + 1) ++j;
+        put_words(pq, d.chunks, d.hb.chunks.data(), (size_t)tc[i] * 256, ((size_t)tc[j - 1] + 1) * 256);
+        i = j;
+    }
+    tc.clear();
     d.chunks_on_dev = nch;
     for (auto it = dirty.begin(); it != dirty.end();) {          // contiguous runs of slots
         uint32_t lo = *it, hi = lo + 1;
@@ -560,13 +581,13 @@ int update_ipcache6(cv_ctx *c, HostMap *m)
     for (const std::vector<uint8_t> &k : m->log)
         if (!k[4] && !k[5] && !k[6] && k[7] == 2) { any = true; break; }
     if (!any) return 0;
-    if (!d.h.nb || d.h.hb.empty() || !d.lens.p) return 1;
+    if (!d.h.nb || d.h.hb.empty() || !d.lens.p) NEED_FULL("no v6 table");
     HashTable t{d.h.hb.data(), nullptr, d.h.nb - 1, 0, (uint32_t)Lpm6Spec::SPB};
     std::vector<uint64_t> bk;
     bool lens_changed = false;
     for (const std::vector<uint8_t> &k : m->log) {
         const uint32_t plen = rd32(k.data());
-        if (plen < 32) return 1;               // spans the static bits: both families, /0
+        if (plen < 32) NEED_FULL("a /0 key");               // spans the static bits: both families, /0
         if (k[4] || k[5] || k[6] || k[7] != 2 || plen > 160) continue;
         const int len = (int)plen - 32;
         uint32_t key[5];
@@ -582,9 +603,9 @@ int update_ipcache6(cv_ctx *c, HostMap *m)
             const uint32_t val = rd32(v);
             if (val & 0x80000000u) return -ERANGE;
             const int64_t sl = host_upsert<Lpm6Spec>(t, key, &val);
-            if (sl < 0) return 1;
+            if (sl < 0) NEED_FULL("v6 probe limit");
             if (old < 0) {
-                if (++d.live * 10 > d.h.nb * Lpm6Spec::SPB * 8) return 1;   // > 80 % load
+                if (++d.live * 10 > d.h.nb * Lpm6Spec::SPB * 8) NEED_FULL("v6 table over 80% load");   // > 80 % load
                 if (d.lens_cnt[len]++ == 0) lens_changed = true;
             }
             bk.push_back((uint64_t)sl / Lpm6Spec::SPB);
@@ -904,6 +925,7 @@ int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
         HostMap *hm = m ? m->hm.get() : nullptr;
         if (role == CV_ROLE_IPCACHE) {
             r = getenv("CV_NO_INCREMENTAL") ? 1 : update_ipcache(c, hm);
+            if (r == 1 && getenv("CV_REBUILD_WHY")) fprintf(stderr, "[cv] ipcache rebuild: %s\n", rebuild_why);
             if (r == 1) { rebuild(); r = compile_ipcache(c, hm); }
         } else {
             rebuild();
@@ -1347,13 +1369,17 @@ bool ct_fits(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t n, uint32_t 
 }
 
 // A netdev launch next to max_entries, exact (cv_kernels.hip "conntrack admission"):
-// the front and the grouping once, then windows: k_ct_intent's creates and deletes of
-// every packet not yet run, the budgets, the conntrack stages over the window (up to
-// the first packet whose creates depend on an earlier create of its group in the same
-// window: the next window sees it exactly).  One host read per window (its end).
+// the front and the grouping once, then windows.  A window repeats k_ct_intent + the
+// budget scans over every packet not yet run until the intents stop changing (each
+// pass reads the previous one's budgets for creates of earlier group members: the
+// fixed point is the sequential answer), then runs the conntrack stages over it.  A
+// window ends early at a packet whose run changed more keys than Changed holds, or,
+// after MAX_PASSES, just past the last packet the passes have settled.  One host read
+// per pass (three words).
 int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, uint32_t now, int with_prefilter,
                  const GroupScratch &gs, const std::vector<MapObj *> &cts, hipStream_t s)
 {
+    constexpr int MAX_PASSES = 12;
     const uint32_t n = bc.n;
     Admit a{};
     a.nmaps = (uint32_t)cts.size();
@@ -1365,7 +1391,7 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     const size_t need_scan = (size_t)a.nmaps * n * 4;
     if ((c->adm_ib.n < (size_t)n * 2 && c->adm_ib.alloc((size_t)n * 2)) ||
         (c->adm_pre.n < 2 * need_scan && c->adm_pre.alloc(2 * need_scan)) ||
-        (!c->adm_tsum.p && c->adm_tsum.alloc(4096 * 4)) || (!c->adm_win.p && c->adm_win.alloc(8)))
+        (!c->adm_tsum.p && c->adm_tsum.alloc(4096 * 4)) || (!c->adm_win.p && c->adm_win.alloc(16)))
         return -ENOMEM;
     a.ib = c->adm_ib.as<uint8_t>();
     a.budget = a.ib + n;
@@ -1376,41 +1402,51 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
     if (r) return r;
     // packets that reach no conntrack stage keep 0 (no creates, no deletes, map 0);
-    // k_ct_intent rewrites the others every window
-    if (hipMemsetAsync(a.ib, 0, n, s) != hipSuccess) return -EIO;
-    uint32_t windows = 0;
+    // k_ct_intent rewrites the others every pass.  The first pass assumes that earlier
+    // creates fail (budget 0).
+    if (hipMemsetAsync(a.ib, 0, (size_t)n * 2, s) != hipSuccess) return -EIO;
+    const bool stats = getenv("CV_ADMIT_STATS") != nullptr;
+    uint32_t windows = 0, passes = 0;
     for (uint32_t lo = 0; lo < n; ++windows) {
         a.lo = lo;
-        if ((r = launch_admission(p, bc, gs, a, s))) return r;
-        uint32_t hi = n;
-        hipError_t e = hipMemcpyAsync(&hi, a.hi, 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) {
-            fprintf(stderr, "[cv] admission window at %u: %s\n", lo, hipGetErrorString(e));
-            return -EIO;
+        uint32_t end = lo, w[3] = {n, n, n};
+        for (int pass = 0;; ++pass) {
+            if ((r = launch_admission(p, bc, gs, a, s))) return r;
+            ++passes;
+            hipError_t e = hipMemcpyAsync(w, a.hi, 12, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) {
+                fprintf(stderr, "[cv] admission pass at %u: %s\n", lo, hipGetErrorString(e));
+                return -EIO;
+            }
+            const uint32_t hi = w[0], chg = w[1], used = w[2];
+            if (hi <= lo || hi > n || (pass && chg <= lo) || used <= lo) {   // (the window's first packet is exact)
+                fprintf(stderr, "[cv] admission window at %u: %u %u %u of %u\n", lo, hi, chg, used, n);
+                return -EPROTO;
+            }
+            // exact: every packet before the first that read a budget (pass 0), or, once
+            // the budgets come from the previous pass, up to the first that changed
+            if (used >= hi || (pass && chg >= hi)) { end = hi; break; }
+            if (pass + 1 == MAX_PASSES) { end = pass ? std::max(chg + 1, used) : used; break; }
         }
-        if (hi <= lo || hi > n) {                                 // (the first packet not run is never unsure)
-            fprintf(stderr, "[cv] admission window [%u, %u) of %u\n", lo, hi, n);
-            return -EPROTO;
-        }
-        if (getenv("CV_ADMIT_STATS") && hi < n) {                 // why the window ends: the unsure packet
+        if (stats && end < n) {                                   // why the window ends
             uint8_t why = 0;
-            (void)hipMemcpy(&why, a.ib + hi, 1, hipMemcpyDeviceToHost);
-            fprintf(stderr, "[cv admit] window [%u, %u): packet %u unsure (%s)\n", lo, hi, hi,
-                    (why & 128) ? "too many changed keys" : (why & 4) ? "twin" : "tuple created earlier");
+            (void)hipMemcpy(&why, a.ib + end, 1, hipMemcpyDeviceToHost);
+            fprintf(stderr, "[cv admit] window [%u, %u) (%u passes so far): %s\n", lo, end, passes,
+                    (why & 64) ? "too many changed keys in a run" : "intents still changing");
         }
         DpParams pw = p;
         pw.win_lo = lo;
-        pw.win_span = hi - lo;
+        pw.win_span = end - lo;
         pw.budget = a.budget;
         if ((r = launch_netdev_stages(pw, bc, now, oc, gs, s))) return r;
-        lo = hi;
+        lo = end;
     }
     for (MapObj *m : cts) {
         m->live_upper = m->cap;                                   // (re-read when the next launch plans)
         m->gen++;
     }
-    if (getenv("CV_ADMIT_STATS")) fprintf(stderr, "[cv admit] %u packets in %u windows\n", n, windows);
+    if (stats) fprintf(stderr, "[cv admit] %u packets in %u windows, %u passes\n", n, windows, passes);
     return 0;
 }
 

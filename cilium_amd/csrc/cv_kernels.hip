@@ -1450,123 +1450,163 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
 // the table as the window starts: ipv4_policy / ipv6_policy (bpf_lxc.c:865-979,
 // 721-849) delete only on CT_ESTABLISHED with a denying verdict and create only on
 // CT_NEW with an allowing one, the tuple (absent: the lookup just missed) and the twin
-// if it is absent.  A packet whose lookups touch a key an earlier member of its group
-// created or deleted in this window is "unsure" (the earlier create may fail): the
-// window ends before the first one, which the next window (run_admitted) sees exactly.
-// The stage then runs the window with each packet's budget (Acct::budget in ct_put):
-// exactly the sequential run's successes and failures, at full width.
-// What earlier members of a run changed in this window: keys they try to create (the
-// creates may fail: a later member touching one is unsure), by hash; keys they deleted
-// (deletes always happen: later lookups of them miss), exactly.
+// if it is absent.  A key an earlier member of the packet's group created in this
+// window exists iff that member's budget covered it -- a budget the scans compute from
+// the intents: k_ct_intent reads the previous pass's budgets and run_admitted repeats
+// the pass until no intent changes (a fixed point; the dependencies only point back in
+// packet order, so it is the sequential answer, and a pass that changes packet c
+// leaves every packet up to c exact).  The stage then runs the window with each
+// packet's budget (Acct::budget in ct_put): exactly the sequential run's successes and
+// failures, at full width.
+// What earlier members of a run did in this window, in packet order: each event a key
+// (by hash; a hit is confirmed against the member's key re-derived from its record),
+// the member, and its kind: 0 a delete (certain), 1 / 2 a create that went in iff the
+// member's budget reaches 1 (its tuple) / 2 (its ICMP twin, tried second).
 template <class T>
 struct Changed {
-    uint64_t ch[4];
-    int nch = 0;
-    uint32_t dk[2][T::KW];
-    int ndk = 0;
-    __device__ void reset() { nch = ndk = 0; }
-    __device__ bool created(const T &t) const
+    static constexpr int N = 6;
+    uint64_t h[N];
+    uint32_t ev[N];                                               // member | kind << 30
+    int n = 0;
+    __device__ void reset() { n = 0; }
+    __device__ bool overflow() const { return n > N; }
+    __device__ void add(const T &t, uint32_t member, uint32_t kind)
     {
         uint32_t k[T::KW];
         t.key(k);
-        const uint64_t h = key_hash<typename T::Spec>(k);
-        bool hit = false;
+        const uint64_t hk = key_hash<typename T::Spec>(k);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) hit |= j < nch && ch[j] == h;
-        return hit;
+        for (int j = 0; j < N; ++j)
+            if (j == n) { h[j] = hk; ev[j] = member | kind << 30; }
+        ++n;
     }
-    __device__ bool deleted(const T &t) const
-    {
-        uint32_t k[T::KW];
-        t.key(k);
-        bool hit = false;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            bool eq = d < ndk;
-#pragma unroll
-            for (int w = 0; w < T::KW; ++w) eq &= dk[d][w] == k[w];
-            hit |= eq;
-        }
-        return hit;
-    }
-    __device__ void add_create(const T &t)
-    {
-        uint32_t k[T::KW];
-        t.key(k);
-        if (nch < 4) ch[nch] = key_hash<typename T::Spec>(k);
-        ++nch;
-    }
-    __device__ void add_delete(const T &t)
-    {
-        if (ndk < 2) t.key(dk[ndk]);
-        ++ndk;
-    }
-    __device__ bool overflow() const { return nch > 4 || ndk > 2; }
 };
 
-template <class T>
-__device__ __forceinline__ bool present(const HashTable &ct, const T &t, const Changed<T> &cg)
-{
-    if (cg.deleted(t)) return false;
-    uint32_t k[T::KW];
-    t.key(k);
-    return dev_find<typename T::Spec>(ct, k, nullptr) >= 0;
-}
-
-// one packet's creates (bits 0-1), delete (bit 2) and unsure flag (bit 6)
+// the conntrack tuple packet i looks up in ipv4_policy / ipv6_policy (false: none)
 template <bool V6, class T>
-__device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
-                                              Changed<T> &cg, const uint32_t *&map)
+__device__ __forceinline__ bool intent_tuple(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
+                                             T &t, EpDev &ep, uint32_t &src)
 {
     const uint4 s1 = g.srec[2 * i + 1];
-    const uint32_t meta = s1.z, src = s1.w;
+    const uint32_t meta = s1.z;
     uint32_t seen;
-    T t;
-    EpDev ep;
+    src = s1.w;
     if constexpr (!V6) {
         ep = ep_stage4<false>(p, meta & 0xFFFFu);
-        map = ep.ct4.buckets;
-        if ((p.flags & F_DROP_ALL) || !ep.ipv4) return 0;
+        if ((p.flags & F_DROP_ALL) || !ep.ipv4) return false;
         const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
-        if (s.len < 34) return 0;
+        if (s.len < 34) return false;
         t.nexthdr = s.nexthdr; t.daddr = s.daddr; t.saddr = s.saddr; t.dport = t.sport = 0;
-        if (ct_l4<false>(t, s.h, CT_INGRESS, seen) < 0) return 0;
+        return ct_l4<false>(t, s.h, CT_INGRESS, seen) >= 0;
     } else {
         ep = G(p.eps)[meta & 0xFFFFu];
-        map = ep.ct6.buckets;
-        if (p.flags & F_DROP_ALL) return 0;
+        if (p.flags & F_DROP_ALL) return false;
         Rec6 r;
         rec_load(r, b, i, b.stride >= 128 ? 8 : (int)(b.stride >> 4));
         const Skb6 s = skb6_from(r);
-        if (s.len < 54 || s.l4off < 0) return 0;
+        if (s.len < 54 || s.l4off < 0) return false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
         t.nexthdr = s.nexthdr;
         t.dport = t.sport = 0;
-        if (ct_l4<true>(t, s.h, CT_INGRESS, seen) < 0) return 0;
+        return ct_l4<true>(t, s.h, CT_INGRESS, seen) >= 0;
     }
-    const HashTable &ct = V6 ? ep.ct6 : ep.ct4;
-    T t2 = t;
-    t2.reverse();
-    T tw = t2;                                                    // the ICMP twin of a create (ct_create)
+}
+
+// the ICMP twin ct_create makes beside a new entry (conntrack.h ct_create4 / ct_create6)
+template <bool V6, class T>
+__device__ __forceinline__ T twin_of(const T &t2)
+{
+    T tw = t2;
     tw.nexthdr = V6 ? 58u : 1u;
     tw.sport = 0; tw.dport = 0;
     tw.flags = t2.flags | TUPLE_F_RELATED;
-    if (cg.overflow()) return 64u | 128u;                         // (bit 7: diagnostics, CV_ADMIT_STATS)
-    if (cg.created(t) || cg.created(t2)) return 64u;
-    if (present(ct, t, cg)) return 0;                             // CT_REPLY / CT_RELATED
-    const bool est = present(ct, t2, cg);
+    return tw;
+}
+
+// What the earlier members' events say of keys ks[0..2] (the packet's tuple, its reverse,
+// the reverse's ICMP twin): st[q] = 0 absent, 1 present, 2 untouched in this window
+// (the table as the window started decides).  The latest confirmed event on a key
+// counts: a delete leaves it absent, a create present iff the member's budget covered
+// it (a failed create leaves it absent, as it was).  *used: a state came from a budget.
+template <bool V6, class T>
+__device__ __forceinline__ void changed_state(const DpParams &p, const BatchDev &b, const GroupScratch &g,
+                                              const Changed<T> &cg, const uint32_t (&ks)[3][T::KW],
+                                              const uint8_t *budget, uint32_t (&st)[3], bool &used)
+{
+    uint32_t hit[3], all = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        st[q] = 2;
+        const uint64_t hk = key_hash<typename T::Spec>(ks[q]);
+        hit[q] = 0;
+#pragma unroll
+        for (int j = 0; j < Changed<T>::N; ++j) hit[q] |= (j < cg.n && cg.h[j] == hk) ? 1u << j : 0u;
+        all |= hit[q];
+    }
+    while (all) {                                                 // latest first
+        const int j = 31 - __clz(all);
+        all &= ~(1u << j);
+        uint32_t e = 0;
+#pragma unroll
+        for (int q = 0; q < Changed<T>::N; ++q) e = q == j ? cg.ev[q] : e;
+        const uint32_t m = e & 0x3FFFFFFFu, kind = e >> 30;
+        T te;
+        EpDev ep;
+        uint32_t src;
+        if (!intent_tuple<V6>(p, b, g, m, te, ep, src)) continue;
+        te.reverse();
+        if (kind == 2) te = twin_of<V6>(te);
+        uint32_t km[T::KW];
+        te.key(km);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (st[q] != 2 || !((hit[q] >> j) & 1u)) continue;
+            bool eq = true;
+#pragma unroll
+            for (int w = 0; w < T::KW; ++w) eq &= km[w] == ks[q][w];
+            if (!eq) continue;                                    // (a hash collision)
+            if (kind) used = true;
+            st[q] = kind ? (budget[m] >= kind ? 1u : 0u) : 0u;
+        }
+    }
+}
+
+// one packet's creates (bits 0-1), delete (bit 2) and unsure flag (bit 6, bit 7 the
+// reason: too many changed keys in its run for Changed to hold)
+template <bool V6, class T>
+__device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
+                                              Changed<T> &cg, const uint8_t *budget, const uint32_t *&map, bool &used)
+{
+    T t;
+    EpDev ep;
+    uint32_t src;
+    const bool any = intent_tuple<V6>(p, b, g, i, t, ep, src);
+    map = V6 ? ep.ct6.buckets : ep.ct4.buckets;
+    if (!any) return 0;
+    if (cg.overflow()) return 64u | 128u;
+    const HashTable &ct = V6 ? ep.ct6 : ep.ct4;
+    T t2 = t;
+    t2.reverse();
+    const T tw = twin_of<V6>(t2);
+    uint32_t ks[3][T::KW], st[3];
+    t.key(ks[0]);
+    t2.key(ks[1]);
+    tw.key(ks[2]);
+    changed_state<V6>(p, b, g, cg, ks, budget, st, used);
+    auto present = [&](int q) { return st[q] == 2 ? dev_find<typename T::Spec>(ct, ks[q], nullptr) >= 0 : st[q] == 1; };
+    if (present(0)) return 0;                                     // CT_REPLY / CT_RELATED
+    const bool est = present(1);
     const bool deny = policy_ingress_denies(ep.policy, p.flags, src, t2.dport, t2.nexthdr);
     if (est) {
         if (!deny) return 0;
-        cg.add_delete(t2);
+        cg.add(t2, i, 0);
         return 4u;                                                // ct_delete
     }
     if (deny) return 0;
-    if (cg.created(tw)) return 64u | 4u;                          // (the twin exists iff that create went in)
-    const uint32_t A = present(ct, tw, cg) ? 1u : 2u;             // (an existing twin is overwritten)
-    cg.add_create(t2);
-    cg.add_create(tw);
+    const uint32_t A = present(2) ? 1u : 2u;                      // (an existing twin is overwritten)
+    cg.add(t2, i, 1);
+    if (A == 2) cg.add(tw, i, 2);
     return A;
 }
 
@@ -1581,19 +1621,23 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
         --left;
         if (x < a.lo) return;                                     // run by an earlier window
         const uint32_t *map = nullptr;
-        const uint32_t v = ct_intent<V6>(p, b, g, x, cg, map);
+        bool used = false;
+        const uint32_t v = ct_intent<V6>(p, b, g, x, cg, a.budget, map, used);
         uint32_t mi = 0;
 #pragma unroll
         for (int k = 0; k < ADMIT_MAPS; ++k)
             if ((uint32_t)k < a.nmaps && a.maps[k] == map) mi = k;
-        a.ib[x] = (uint8_t)(v | mi << 3);
+        const uint8_t nv = (uint8_t)(v | mi << 3), old = a.ib[x];
+        a.ib[x] = nv;
         if (v & 64u) atomicMin(a.hi, x);
+        if (nv != old) atomicMin(a.hi + 1, x);
+        if (used) atomicMin(a.hi + 2, x);
     });
 }
 
 __global__ void k_admit_init(Admit a, uint32_t n)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) *a.hi = n;
+    if (threadIdx.x < 3 && blockIdx.x == 0) a.hi[threadIdx.x] = n;
 }
 
 // per map m: D - A of the packets lo.. (others 0)

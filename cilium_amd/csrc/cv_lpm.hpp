@@ -97,12 +97,34 @@ __device__ __forceinline__ uint32_t lpm4_end(const Lpm4Pending &q, const Lpm4 &t
 struct Lpm4Builder {
     std::vector<uint32_t> l1 = std::vector<uint32_t>(65536, 0);
     std::vector<uint32_t> chunks;
+    std::vector<uint32_t> free_chunks;         // chunks of rebuilt subtrees, reused first
+    std::vector<uint32_t> touched;             // chunks written since the last take_touched()
 
     uint32_t new_chunk(uint32_t fill)
     {
-        uint32_t idx = (uint32_t)(chunks.size() / 256);
-        chunks.insert(chunks.end(), 256, fill);
+        uint32_t idx;
+        if (!free_chunks.empty()) {
+            idx = free_chunks.back();
+            free_chunks.pop_back();
+            std::fill(chunks.begin() + (size_t)idx * 256, chunks.begin() + (size_t)idx * 256 + 256, fill);
+        } else {
+            idx = (uint32_t)(chunks.size() / 256);
+            chunks.insert(chunks.end(), 256, fill);
+        }
+        touched.push_back(idx);
         return idx;
+    }
+
+    // the chunks under a level-1 slot to the free list (the slot is about to be rebuilt)
+    void release(uint32_t e)
+    {
+        if (!(e & 0x80000000u)) return;
+        const uint32_t c2 = e & 0x7FFFFFFFu;
+        for (uint32_t i = 0; i < 256; ++i) {
+            const uint32_t e2 = chunks[((size_t)c2 << 8) + i];
+            if (e2 & 0x80000000u) free_chunks.push_back(e2 & 0x7FFFFFFFu);
+        }
+        free_chunks.push_back(c2);
     }
 
     // value must be < 2^31 (0 = no match)

@@ -630,6 +630,7 @@ def test_agent_writes_stream_without_stall(dev):
     batch latency under the writes stays within 1 ms of the quiet one."""
     import threading
     import time
+    os.environ["CV_REBUILD_WHY"] = "1"                                 # (stderr: why a write needed a rebuild)
     w = synth.config2(1 << 16, n_cidrs=4096, n_ids=300)
     dp, om = H.oracle_dp(w)
     ctx, pm = H.product_ctx(w)

@@ -221,7 +221,7 @@ struct cv_ctx {
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
-    DevBuf adm_ib, adm_pre, adm_tsum, adm_win;  // conntrack admission next to max_entries
+    DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -1388,15 +1388,11 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
         a.live[k] = cts[k]->live.as<unsigned long long>();
         a.cap[k] = cts[k]->cap;
     }
-    const size_t need_scan = (size_t)a.nmaps * n * 4;
     if ((c->adm_ib.n < (size_t)n * 2 && c->adm_ib.alloc((size_t)n * 2)) ||
-        (c->adm_pre.n < 2 * need_scan && c->adm_pre.alloc(2 * need_scan)) ||
-        (!c->adm_tsum.p && c->adm_tsum.alloc(4096 * 4)) || (!c->adm_win.p && c->adm_win.alloc(16)))
+        (!c->adm_tsum.p && c->adm_tsum.alloc((size_t)ADMIT_MAPS * 4096 * 8)) || (!c->adm_win.p && c->adm_win.alloc(16)))
         return -ENOMEM;
     a.ib = c->adm_ib.as<uint8_t>();
     a.budget = a.ib + n;
-    a.sum = c->adm_pre.as<int32_t>();
-    a.pmin = a.sum + (size_t)a.nmaps * n;
     a.tsum = c->adm_tsum.as<uint32_t>();
     a.hi = c->adm_win.as<uint32_t>();
     int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
@@ -1411,6 +1407,7 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
         a.lo = lo;
         uint32_t end = lo, w[3] = {n, n, n};
         for (int pass = 0;; ++pass) {
+            a.pass = (uint32_t)pass;
             if ((r = launch_admission(p, bc, gs, a, s))) return r;
             ++passes;
             hipError_t e = hipMemcpyAsync(w, a.hi, 12, hipMemcpyDeviceToHost, s);

@@ -84,13 +84,12 @@ struct Admit {
     unsigned long long cap[ADMIT_MAPS];
     uint32_t nmaps;
     uint32_t lo;                       // the first packet not yet run
-    uint8_t *ib;                       // per packet: creates A | deletes D << 2 | map << 3 | unsure << 6
-                                       // (unsure: bit 7 = too many changed keys in its run)
-    int32_t *sum, *pmin;               // per map m: [m * (n - lo) + j] inclusive sum of D - A over packets
-                                       // lo .. lo + j, and the prefix minimum of that sum
+    uint32_t pass;                     // the pass over this window (0: every packet from lo)
+    uint8_t *ib;                       // per packet: creates A | deletes D << 2 | map << 3 | read a
+                                       // budget << 5 | unsure << 6 (bit 7: too many changed keys in its run)
     uint8_t *budget;                   // per packet: how many of its creates of new entries succeed (the
                                        // previous pass's: what k_ct_intent assumes of earlier creates)
-    uint32_t *tsum;                    // scan tile aggregates
+    uint32_t *tsum;                    // per map and scan tile: the (sum, prefix minimum) of D - A
     uint32_t *hi;                      // [0] the first unsure packet (the window's end), [1] the first
                                        // packet whose intent changed from the previous pass, [2] the first
                                        // packet whose intent rests on an earlier member's budget

@@ -1610,16 +1610,21 @@ __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev 
     return A;
 }
 
+// ib bits besides A / D / map: 32 the intent read an earlier member's budget, 64 unsure,
+// 128 (with 64) the reason: too many changed keys in the run
+constexpr uint32_t IB_USED = 32u, IB_UNSURE = 64u;
+
+// Pass 0 of a window replays every packet from a.lo; a later pass (a.pass) only the
+// runs with a member whose intent read a budget (or that was unsure) in the previous
+// one: the other intents cannot change (singletons never read one).
 template <bool V6>
 __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, GroupScratch g, Admit a)
 {
     using T = typename std::conditional<V6, Tuple6, Tuple4>::type;
+    const int q = V6 ? Q_NETDEV6 : Q_NETDEV;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     Changed<T> cg;
-    uint32_t left = 0;                                            // members of the current run still to come
-    for_each_run<true>(g, V6 ? Q_NETDEV6 : Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
-        if (!left) { left = n; cg.reset(); }                      // (a lane's runs come one after another)
-        --left;
-        if (x < a.lo) return;                                     // run by an earlier window
+    auto one = [&](uint32_t x) {
         const uint32_t *map = nullptr;
         bool used = false;
         const uint32_t v = ct_intent<V6>(p, b, g, x, cg, a.budget, map, used);
@@ -1627,12 +1632,39 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
 #pragma unroll
         for (int k = 0; k < ADMIT_MAPS; ++k)
             if ((uint32_t)k < a.nmaps && a.maps[k] == map) mi = k;
-        const uint8_t nv = (uint8_t)(v | mi << 3), old = a.ib[x];
-        a.ib[x] = nv;
-        if (v & 64u) atomicMin(a.hi, x);
-        if (nv != old) atomicMin(a.hi + 1, x);
+        const uint32_t nv = v | mi << 3 | (used ? IB_USED : 0u), old = a.ib[x];
+        a.ib[x] = (uint8_t)nv;
+        if (v & IB_UNSURE) atomicMin(a.hi, x);
+        if ((nv ^ old) & ~IB_USED) atomicMin(a.hi + 1, x);
         if (used) atomicMin(a.hi + 2, x);
-    });
+    };
+    uint32_t multi = 0;                                           // scheduled runs: classes >= 1
+#pragma unroll
+    for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
+    for (uint32_t j = tid; j < multi; j += stride) {
+        const uint32_t off = g.work[j], cnt = g.order[off];
+        if (a.pass) {
+            bool redo = false;
+            for (uint32_t k = 0; k < cnt && !redo; ++k) {
+                const uint32_t x = g.order[off + 1 + k];
+                redo = x >= a.lo && (a.ib[x] & (IB_USED | IB_UNSURE));
+            }
+            if (!redo) continue;
+        }
+        cg.reset();
+#pragma unroll 1
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t x = g.order[off + 1 + k];
+            if (x >= a.lo) one(x);                                // (below: run by an earlier window)
+        }
+    }
+    if (a.pass) return;
+    const uint32_t singles = g.cursor[SINGLE_WORD0 + q];
+    for (uint32_t j = tid; j < singles; j += stride) {
+        const uint32_t x = g.single[j];
+        cg.reset();
+        if (x >= a.lo) one(x);
+    }
 }
 
 __global__ void k_admit_init(Admit a, uint32_t n)
@@ -1640,102 +1672,138 @@ __global__ void k_admit_init(Admit a, uint32_t n)
     if (threadIdx.x < 3 && blockIdx.x == 0) a.hi[threadIdx.x] = n;
 }
 
-// per map m: D - A of the packets lo.. (others 0)
-__global__ void __launch_bounds__(BLOCK) k_admit_extract(Admit a, uint32_t n)
+// The reflected walk's two scans as one, over the monoid of (sum, prefix minimum) pairs:
+// (s1, m1) then (s2, m2) = (s1 + s2, min(m1, s1 + m2)); a packet of map m contributes
+// (D - A, D - A) to m's walk and the identity (0, +inf) to the others.  Three kernels
+// for all maps: tile aggregates, their exclusive scan, and a pass that rescans each tile
+// and writes the budgets directly (no per-packet sums in HBM).
+struct SumMin {
+    int32_t s, m;
+};
+constexpr int32_t SM_INF = 1 << 30;                               // (|sums| <= 2^25: no overflow)
+
+__device__ __forceinline__ SumMin sm_comb(SumMin l, SumMin r) { return {l.s + r.s, min(l.m, l.s + r.m)}; }
+
+__device__ __forceinline__ SumMin sm_shfl_up(SumMin v, int d)
 {
-    const uint32_t L = n - a.lo;
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < L; j += gridDim.x * BLOCK) {
-        const uint32_t v = a.ib[a.lo + j], mi = (v >> 3) & 7u;
-        const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
-        for (uint32_t m = 0; m < a.nmaps; ++m) a.sum[(size_t)m * L + j] = m == mi ? d : 0;
-    }
+    return {__shfl_up(v.s, d, 64), __shfl_up(v.m, d, 64)};
 }
 
-// the budgets from the scans (the reflected walk above), for every packet from lo with creates
-__global__ void __launch_bounds__(BLOCK) k_admit_budget(Admit a, uint32_t n)
-{
-    const uint32_t L = n - a.lo;
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < L; j += gridDim.x * BLOCK) {
-        const uint32_t v = a.ib[a.lo + j], mi = (v >> 3) & 7u, A = v & 3u;
-        if (!A) { a.budget[a.lo + j] = 0; continue; }
-        const unsigned long long live = __hip_atomic_load(a.live[mi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const long long r0 = live < a.cap[mi] ? (long long)(a.cap[mi] - live) : 0;
-        long long r = r0;                                         // the room before packet j
-        if (j) {
-            const long long S = a.sum[(size_t)mi * L + j - 1], PM = a.pmin[(size_t)mi * L + j - 1];
-            const long long lowest = r0 + PM < 0 ? r0 + PM : 0;
-            r = r0 + S - lowest;
-        }
-        a.budget[a.lo + j] = (uint8_t)(r < (long long)A ? r : (long long)A);
-    }
-}
-
-// prefix minimum of int32 values in place (the same three phases as launch_scan)
-__device__ __forceinline__ int32_t block_incl_min(int32_t v, int32_t *wmin)
+// exclusive scan of one SumMin per thread over a block of 1024 (16 waves); *total: the
+// block's aggregate
+__device__ __forceinline__ SumMin block_excl_summin(SumMin v, SumMin *lds, SumMin *total)
 {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int32_t incl = v;
+    SumMin incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const int32_t t = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl = min(incl, t);
+        const SumMin t = sm_shfl_up(incl, d);
+        if (lane >= (uint32_t)d) incl = sm_comb(t, incl);
     }
-    if (lane == 63) wmin[wv] = incl;
+    if (lane == 63) lds[wv] = incl;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int32_t acc = INT32_MAX;
-        for (uint32_t w = 0; w < nw; ++w) { const int32_t t = wmin[w]; wmin[w] = acc; acc = min(acc, t); }
-        wmin[16] = acc;
+        SumMin acc{0, SM_INF};
+        for (uint32_t w = 0; w < nw; ++w) { const SumMin t = lds[w]; lds[w] = acc; acc = sm_comb(acc, t); }
+        lds[16] = acc;
     }
     __syncthreads();
-    const int32_t r = min(wmin[wv], incl);
+    SumMin ex = sm_shfl_up(incl, 1);
+    if (!lane) ex = SumMin{0, SM_INF};
+    const SumMin r = sm_comb(lds[wv], ex);
+    if (total) *total = lds[16];
     __syncthreads();
     return r;
 }
 
-__global__ void __launch_bounds__(1024) k_min_tiles(const int32_t *c, uint32_t L, int32_t *tmin)
+// this thread's 4 packets (lo + tile * SCAN_TILE + 4 * thread ..): their ib bytes
+__device__ __forceinline__ uint32_t adm_ib4(const Admit &a, uint32_t L, uint32_t j)
 {
-    __shared__ int32_t wmin[17];
-    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-    int32_t v = INT32_MAX;
-    for (uint32_t k = 0; k < 4; ++k) if (j + k < L) v = min(v, c[j + k]);
-    block_incl_min(v, wmin);
-    if (threadIdx.x == 0) tmin[blockIdx.x] = wmin[16];
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (j + k < L) w |= (uint32_t)a.ib[a.lo + j + k] << (8 * k);
+    return w;
 }
 
-__global__ void __launch_bounds__(1024) k_min_top(int32_t *tmin, uint32_t tiles)
+__device__ __forceinline__ SumMin adm_elem(uint32_t v, uint32_t m)
 {
-    __shared__ int32_t wmin[17];
-    int32_t v[4], m = INT32_MAX;
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t t = threadIdx.x * 4 + k;
-        v[k] = t < tiles ? tmin[t] : INT32_MAX;
-        m = min(m, v[k]);
-    }
-    const int32_t incl = block_incl_min(m, wmin);
-    const int32_t before = __shfl_up(incl, 1, 64);               // exclusive: the minimum before this thread
-    int32_t e = (threadIdx.x & 63) ? before : (threadIdx.x >> 6 ? wmin[threadIdx.x >> 6] : INT32_MAX);
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t t = threadIdx.x * 4 + k;
-        if (t < tiles) tmin[t] = e;                               // (the minimum of the tiles before t)
-        e = min(e, v[k]);
+    if (((v >> 3) & 3u) != m) return SumMin{0, SM_INF};
+    const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
+    return SumMin{d, d};
+}
+
+__global__ void __launch_bounds__(1024) k_adm_tiles(Admit a, uint32_t n, uint32_t tiles)
+{
+    __shared__ SumMin lds[17];
+    const uint32_t L = n - a.lo, j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    const uint32_t w = adm_ib4(a, L, j);
+    SumMin *agg = reinterpret_cast<SumMin *>(a.tsum);
+    for (uint32_t m = 0; m < a.nmaps; ++m) {
+        SumMin t{0, SM_INF};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (j + k < L) t = sm_comb(t, adm_elem(w >> (8 * k) & 0xFFu, m));
+        SumMin tot;
+        block_excl_summin(t, lds, &tot);
+        if (threadIdx.x == 0) agg[m * tiles + blockIdx.x] = tot;
     }
 }
 
-__global__ void __launch_bounds__(1024) k_min_apply(const int32_t *c, int32_t *out, uint32_t L, const int32_t *tmin)
+// one block: each map's tile aggregates -> exclusive prefixes, in place
+__global__ void __launch_bounds__(1024) k_adm_top(Admit a, uint32_t tiles)
 {
-    __shared__ int32_t wmin[17];
-    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-    int32_t v[4], m = INT32_MAX;
-    for (uint32_t k = 0; k < 4; ++k) { v[k] = j + k < L ? c[j + k] : INT32_MAX; m = min(m, v[k]); }
-    const int32_t incl = block_incl_min(m, wmin);
-    const int32_t before = __shfl_up(incl, 1, 64);
-    int32_t e = (threadIdx.x & 63) ? before : (threadIdx.x >> 6 ? wmin[threadIdx.x >> 6] : INT32_MAX);
-    e = min(e, tmin[blockIdx.x]);
-    for (uint32_t k = 0; k < 4; ++k) {
-        e = min(e, v[k]);
-        if (j + k < L) out[j + k] = e;
+    __shared__ SumMin lds[17];
+    SumMin *agg = reinterpret_cast<SumMin *>(a.tsum);
+    for (uint32_t m = 0; m < a.nmaps; ++m) {
+        SumMin v[4], t{0, SM_INF};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = threadIdx.x * 4 + k;
+            v[k] = q < tiles ? agg[m * tiles + q] : SumMin{0, SM_INF};
+            t = sm_comb(t, v[k]);
+        }
+        SumMin e = block_excl_summin(t, lds, nullptr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = threadIdx.x * 4 + k;
+            if (q < tiles) agg[m * tiles + q] = e;
+            e = sm_comb(e, v[k]);
+        }
     }
+}
+
+// the budgets: the room before packet j is r0 + S - min(0, r0 + M) with (S, M) the
+// walk's (sum, prefix minimum) over lo .. j - 1 of j's map (r0 before lo)
+__global__ void __launch_bounds__(1024) k_adm_apply(Admit a, uint32_t n, uint32_t tiles)
+{
+    __shared__ SumMin lds[17];
+    const uint32_t L = n - a.lo, j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    const uint32_t w = adm_ib4(a, L, j);
+    const SumMin *agg = reinterpret_cast<const SumMin *>(a.tsum);
+    uint32_t out = 0;
+    for (uint32_t m = 0; m < a.nmaps; ++m) {
+        SumMin t{0, SM_INF};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (j + k < L) t = sm_comb(t, adm_elem(w >> (8 * k) & 0xFFu, m));
+        SumMin P = sm_comb(agg[m * tiles + blockIdx.x], block_excl_summin(t, lds, nullptr));
+        const unsigned long long live = __hip_atomic_load(a.live[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long long r0 = live < a.cap[m] ? (long long)(a.cap[m] - live) : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t v = w >> (8 * k) & 0xFFu, A = v & 3u;
+            if (((v >> 3) & 3u) == m && A) {
+                const long long lowest = r0 + P.m < 0 ? r0 + P.m : 0;
+                const long long r = r0 + P.s - lowest;
+                out |= (uint32_t)(r < (long long)A ? r : (long long)A) << (8 * k);
+            }
+            P = sm_comb(P, adm_elem(v, m));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (j + k < L) a.budget[a.lo + j + k] = (uint8_t)(out >> (8 * k));
 }
 
 int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s)
@@ -1743,23 +1811,16 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     if (!b.n || a.lo >= b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     const uint32_t L = b.n - a.lo, tiles = (L + SCAN_TILE - 1) / SCAN_TILE;
+    if (tiles > 4096 || a.nmaps > ADMIT_MAPS) return -EINVAL;
     hipLaunchKernelGGL(k_admit_init, dim3(1), dim3(64), 0, s, a, b.n);
     hipLaunchKernelGGL(k_ct_intent<false>, grid, blk, 0, s, p, b, g, a);
     GroupScratch g6 = g;
     g6.single = g.single6;
     g6.work = g.work6;
     hipLaunchKernelGGL(k_ct_intent<true>, grid, blk, 0, s, p, b, g6, a);
-    hipLaunchKernelGGL(k_admit_extract, grid, blk, 0, s, a, b.n);
-    for (uint32_t m = 0; m < a.nmaps; ++m) {
-        uint32_t *sm = reinterpret_cast<uint32_t *>(a.sum + (size_t)m * L);
-        launch_scan(sm, L, a.tsum, nullptr, true, s);
-        int32_t *tm = reinterpret_cast<int32_t *>(a.tsum);
-        hipLaunchKernelGGL(k_min_tiles, dim3(tiles), dim3(1024), 0, s, a.sum + (size_t)m * L, L, tm);
-        hipLaunchKernelGGL(k_min_top, dim3(1), dim3(1024), 0, s, tm, tiles);
-        hipLaunchKernelGGL(k_min_apply, dim3(tiles), dim3(1024), 0, s, a.sum + (size_t)m * L, a.pmin + (size_t)m * L,
-                           L, tm);
-    }
-    hipLaunchKernelGGL(k_admit_budget, grid, blk, 0, s, a, b.n);
+    hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
+    hipLaunchKernelGGL(k_adm_top, dim3(1), dim3(1024), 0, s, a, tiles);
+    hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
     return launch_status(__func__);
 }
 

@@ -123,7 +123,11 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
  * behaves like a kernel HASH map: a create past max_entries fails (-E2BIG, the
  * datapath's DROP_CT_CREATE_FAILED), identically in the oracle.  Size max_entries for
  * the flows the node keeps (HBM: ~137 B per entry at the 60 % bucket load) and run
- * cv_ct_gc.  A batch next to the limit is processed in exact one-packet launches. */
+ * cv_ct_gc.  A from-netdev batch next to the limit runs at full width with exact
+ * admission: every packet's creates and deletes are resolved against the map's room
+ * in packet order first (DESIGN.md §2 "Admission"); other entry points (egress, or
+ * more CT maps in one launch than admission tracks) fall back to launches of as many
+ * packets as surely fit, and one-packet launches at the limit. */
 int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
 /* Slot occupancy of a device CT map (diagnostics, no reference counterpart): out[0]
  * empty slots, out[1] tombstones (deleted entries not yet reclaimed by cv_ct_gc),

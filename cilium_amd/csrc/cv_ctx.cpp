@@ -1132,14 +1132,16 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
     return gs;
 }
 
-// diagnostics (CV_GROUP_STATS): per queue, groups per size class and the largest group
-void group_stats(cv_ctx *c, const char *what, hipStream_t stream)
+// diagnostics (CV_GROUP_STATS): per node-table queue (services, NAT writers) groups per
+// size class; per binned conntrack queue (flat: egress components, else netdev runs)
+// runs by size (powers of two), packets in runs past 64, the largest run
+void group_stats(cv_ctx *c, const char *what, hipStream_t stream, bool flat)
 {
     std::vector<uint32_t> cur(CURSOR_WORDS);
     (void)hipStreamSynchronize(stream);
     (void)hipMemcpy(cur.data(), c->gcursor.p, CURSOR_WORDS * 4, hipMemcpyDeviceToHost);
     static const char *qn[NQUEUES] = {"netdev", "lb4", "lb6", "ct4", "ct6", "nat"};
-    for (int q = 0; q < NQUEUES; ++q) {
+    for (int q : {(int)Q_LB4, (int)Q_LB6, (int)Q_NAT}) {
         uint64_t groups = 0;
         for (int k = 0; k < QSPLIT; ++k) groups += cur[qctr(q, k)];
         if (!groups) continue;
@@ -1147,22 +1149,42 @@ void group_stats(cv_ctx *c, const char *what, hipStream_t stream)
                 (unsigned long long)groups, cur[GMAX_WORD0 + q]);
         for (int k = 0; k < NCLASS; ++k) fprintf(stderr, " %u", cur[qcls(q, k)]);
         fprintf(stderr, "\n");
-        if (q != Q_CT4 && q != Q_CT6 && q != Q_NETDEV) continue;
-        // members of the largest run (queue words hold run offsets after k_group_flatten)
-        std::vector<uint32_t> order((size_t)c->gn * 2);
-        (void)hipMemcpy(order.data(), c->gorder.p, order.size() * 4, hipMemcpyDeviceToHost);
-        const uint32_t qr = (uint32_t)(c->gn / QSPLIT + 512);
-        std::vector<uint32_t> qw((size_t)qr * QSPLIT);
-        (void)hipMemcpy(qw.data(), c->gqueue.as<uint32_t>() + (size_t)qbank(q) * QSPLIT * qr, qw.size() * 4,
-                        hipMemcpyDeviceToHost);
-        uint32_t best = 0, boff = 0;
-        for (int k = 0; k < QSPLIT; ++k)
-            for (uint32_t j = 0; j < cur[qctr(q, k)]; ++j) {
-                const uint32_t off = qw[(size_t)k * qr + j];
-                if (off < order.size() && order[off] > best) { best = order[off]; boff = off; }
-            }
-        fprintf(stderr, "[cv groups] %s %s largest run (%u):", what, qn[q], best);
-        for (uint32_t j = 0; j < best && j < 24; ++j) fprintf(stderr, " %u", order[boff + 1 + j]);
+    }
+    std::vector<uint32_t> order((size_t)c->gn * 2);
+    (void)hipMemcpy(order.data(), c->gorder.p, order.size() * 4, hipMemcpyDeviceToHost);
+    const int q4 = flat ? (int)Q_CT4 : (int)Q_NETDEV, q6 = flat ? (int)Q_CT6 : (int)Q_NETDEV6;
+    for (int fam = 0; fam < 2; ++fam) {
+        const int q = fam ? q6 : q4;
+        const DevBuf &wb = fam ? c->gwork6 : c->gwork;
+        uint32_t nw = 0;
+        uint64_t singles = 0;
+        if (flat) {
+            nw = cur[qcls(q, 0)];
+        } else {
+            for (int k = 1; k < NCLASS; ++k) nw += cur[qcls(q, k)];
+            singles = cur[SINGLE_WORD0 + q];
+        }
+        std::vector<uint32_t> w(nw);
+        if (nw) (void)hipMemcpy(w.data(), wb.p, (size_t)nw * 4, hipMemcpyDeviceToHost);
+        uint64_t hist[33] = {0}, big = 0, pk = 0;
+        uint32_t best = 0;
+        for (uint32_t e : w) {
+            uint32_t sz = 1;
+            if (!(e & SINGLE_RUN) && e < order.size()) sz = order[e];
+            if (sz == 1) { ++singles; continue; }
+            int lg = 0;
+            while ((2u << lg) <= sz) ++lg;
+            ++hist[lg];
+            pk += sz;
+            if (sz > 64) big += sz;
+            best = std::max(best, sz);
+        }
+        if (!nw && !singles) continue;
+        fprintf(stderr, "[cv groups] %s %s: %llu singletons, %llu packets in runs, largest %u, %llu in runs > 64; "
+                "runs by size 2^k:", what, fam ? "v6" : "v4", (unsigned long long)singles, (unsigned long long)pk, best,
+                (unsigned long long)big);
+        for (int k = 1; k < 33; ++k)
+            if (hist[k]) fprintf(stderr, " [%d]%llu", k, (unsigned long long)hist[k]);
         fprintf(stderr, "\n");
     }
 }
@@ -1904,7 +1926,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         if (r) return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
-        if (getenv("CV_GROUP_STATS")) group_stats(c, "netdev", (hipStream_t)stream);
+        if (getenv("CV_GROUP_STATS")) group_stats(c, "netdev", (hipStream_t)stream, false);
     }
     mark_stream(c, (hipStream_t)stream);
     return 0;
@@ -1943,7 +1965,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
             return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
-        if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream);
+        if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream, true);
     }
     mark_stream(c, (hipStream_t)stream);
     return 0;

@@ -15,7 +15,6 @@ namespace cv {
 
 constexpr int BLOCK = 256;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint32_t SINGLE_RUN = 0x80000000u; // a flattened queue word naming a singleton's packet
 constexpr uint32_t COMMIT4 = 0xFFFFFFFEu;     // g.gslot marks of a deferred CT create (k_ct_commit)
 constexpr uint32_t COMMIT6 = 0xFFFFFFFDu;
 constexpr uint32_t COMMIT_PROXY = 2u;         // COMMIT4/6 - 2: the packet went to the proxy (no forward metric)

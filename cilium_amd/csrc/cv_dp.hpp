@@ -177,6 +177,7 @@ __host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT +
 __host__ __device__ constexpr int qcls(int q, int c) { return CLS0 + (q * NCLASS + c) * 32; }
 constexpr int RUN_CURSOR = 3;
 constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (k_group_flatten)
+constexpr uint32_t SINGLE_RUN = 0x80000000u; // a flattened queue word naming a singleton's packet
 constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
 constexpr int EG_WORDS = 16;
 

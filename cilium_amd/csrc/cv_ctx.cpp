@@ -220,6 +220,7 @@ struct cv_ctx {
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
+    DevBuf gdel;                  // egress: local-delivery records (DEL_SLOTS x 16 B per packet)
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
@@ -1100,7 +1101,9 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
         return -ENOMEM;
     (void)hipMemset(c->gtable.p, 0, cap * 16);
     if (egress || c->g_egress) {
-        if (c->gparent.alloc(cap * 8) || c->geg.alloc((size_t)cmax * EG_WORDS * 4)) return -ENOMEM;
+        if (c->gparent.alloc(cap * 8) || c->geg.alloc((size_t)cmax * EG_WORDS * 4) ||
+            c->gdel.alloc((size_t)cmax * DEL_SLOTS * 16))
+            return -ENOMEM;
         (void)hipMemset(c->gparent.p, 0, cap * 8);
         c->g_egress = true;
     }
@@ -1127,6 +1130,7 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     c->gcnt.as<uint32_t>(), c->gbig.as<unsigned long long>(), 4, c->gnext.as<uint32_t>(),
                     c->gwork6.as<uint32_t>(), c->ghword.as<uint32_t>(), c->ghcnt.as<uint32_t>(), (uint32_t)Q_NETDEV,
                     0};
+    gs.del = c->gdel.as<uint4>();
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1149,6 +1153,15 @@ void group_stats(cv_ctx *c, const char *what, hipStream_t stream, bool flat)
                 (unsigned long long)groups, cur[GMAX_WORD0 + q]);
         for (int k = 0; k < NCLASS; ++k) fprintf(stderr, " %u", cur[qcls(q, k)]);
         fprintf(stderr, "\n");
+    }
+    if (flat) {                                   // egress: the position lists' lengths
+        for (int q : {(int)Q_CT4, (int)Q_CT6}) {
+            fprintf(stderr, "[cv groups] %s %s: largest %u; packets per member position:", what, qn[q],
+                    cur[GMAX_WORD0 + q]);
+            for (uint32_t k = 0; k < NPOS; ++k) fprintf(stderr, " %u", cur[qcls(q, (int)k)]);
+            fprintf(stderr, " (the last: groups continued)\n");
+        }
+        return;
     }
     std::vector<uint32_t> order((size_t)c->gn * 2);
     (void)hipMemcpy(order.data(), c->gorder.p, order.size() * 4, hipMemcpyDeviceToHost);

@@ -2052,25 +2052,22 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
     }
 }
 
-// fn(i, run size) for every member of every group of queue q listed flat by the
-// binned grouping (g.flat: one list, the groups' first packets in packet order; a
-// singleton's entry is its packet, SINGLE_RUN-tagged)
+// fn(i) for member `pos` of every group of queue q (position lists, g.flat), in packet
+// order; the last list (pos = NPOS - 1) names runs: fn for their members from pos on.
+// One call site of fn.
 template <class F>
-__device__ __forceinline__ void for_each_flat(const GroupScratch &g, int q, F &&fn)
+__device__ __forceinline__ void for_each_at(const GroupScratch &g, int q, uint32_t pos, F &&fn)
 {
-    const uint32_t total = g.cursor[qcls(q, 0)];
+    uint32_t base = 0;
+    for (uint32_t l = 0; l < pos; ++l) base += g.cursor[qcls(q, l)];
+    const uint32_t total = g.cursor[qcls(q, pos)];
+    const bool runs = pos + 1 == NPOS;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t j = tid; j < total; j += stride) {
-        const uint32_t e = g.work[j];
-        if (e & SINGLE_RUN) { fn(e & ~SINGLE_RUN, 1u); continue; }
-        const uint32_t cnt = g.order[e];
-        uint32_t v = g.order[e + 1];
+        const uint32_t e = g.work[base + j];
+        const uint32_t k1 = runs ? g.order[e] : pos + 1;
 #pragma unroll 1
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const uint32_t vn = k + 1 < cnt ? g.order[e + 2 + k] : NONE;
-            fn(v, cnt);
-            v = vn;
-        }
+        for (uint32_t k = pos; k < k1; ++k) fn(runs ? g.order[e + 1 + k] : e);
     }
 }
 

@@ -152,7 +152,12 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
                                // offset in `order` (k_gbin_group -> k_heads_place)
     uint32_t *hcnt;            // per (list, tile) head counts -> positions (k_heads_count / place)
     uint32_t q4;               // the IPv4 queue the binned grouping fills (Q_NETDEV, or Q_CT4 on egress)
-    uint32_t flat;             // 1: one list per queue, every group's first packet in packet order (egress)
+    uint32_t flat;             // 1: position lists (egress): list t < NPOS - 1 holds member t of every
+                               // group, list NPOS - 1 the runs of groups past NPOS - 1 members, in
+                               // packet order (k_gbin_group -> k_heads_place)
+    uint32_t pos;              // egress: the member position of the current launch pair
+    uint4 *del;                // egress: per packet DEL_SLOTS x 16 B, the local-delivery record
+                               // k_egress_ct hands to k_egress_deliver (listed in `single`)
 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses
@@ -180,6 +185,13 @@ constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (
 constexpr uint32_t SINGLE_RUN = 0x80000000u; // a flattened queue word naming a singleton's packet
 constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
 constexpr int EG_WORDS = 16;
+// position lists of the egress conntrack stage: one launch per member position, the last
+// one continuing the few groups past NPOS - 1 members (<= 16: the lists are k_heads' 16)
+constexpr uint32_t NPOS = 8;
+constexpr uint32_t DEL_SLOTS = 6;
+// the local-delivery list counter of a position (the netdev queue's sub-queue counters,
+// which the egress path does not use)
+__host__ __device__ constexpr int del_ctr(bool v6, uint32_t pos) { return 32 + (int)((v6 ? 8u : 0u) + pos) * 32; }
 
 // the binned grouping of the packets whose g.pkey is set (cv_kernels.hip): runs, and the
 // lists of the groups' first packets (g.flat: one per queue)

@@ -28,7 +28,36 @@ namespace cv {
 constexpr bool EGF = false;
 __device__ __forceinline__ void eg_changed() { l1_inv(); }
 
+// the endpoint lookup of daddr issued ahead of the conntrack probes (its 64-B bucket then
+// stays in registers across them), or at its use
+#ifdef CV_AB_EARLY_LXC
+constexpr bool EG_EARLY_LXC = true;
+#else
+constexpr bool EG_EARLY_LXC = false;
+#endif
+
 int grid_for(uint32_t n);
+
+#ifdef CV_AB_TIMING
+// timing-only instrumentation (A/B builds): per member position and checkpoint the summed
+// wall-clock time since the previous checkpoint of sampled packets, and their count
+__device__ unsigned long long g_tdbg[NPOS][32];
+#define TCK(k) do { if (tsamp) { __builtin_amdgcn_s_waitcnt(0); const long long tn_ = wall_clock64(); \
+    atomicAdd(&g_tdbg[g.pos][k], (unsigned long long)(tn_ - tprev)); atomicAdd(&g_tdbg[g.pos][16 + (k)], 1ull); \
+    tprev = tn_; } } while (0)
+__global__ void k_tdbg_dump()
+{
+    for (uint32_t q = 0; q < NPOS; ++q) {
+        printf("[tdbg] pos %u:", q);
+        for (int k = 0; k < 16; ++k)
+            if (g_tdbg[q][16 + k]) printf(" %d:%.2fus/%llu", k, g_tdbg[q][k] * 0.01 / g_tdbg[q][16 + k], g_tdbg[q][16 + k]);
+        printf("\n");
+        for (int k = 0; k < 32; ++k) g_tdbg[q][k] = 0;
+    }
+}
+#else
+#define TCK(k) do { } while (0)
+#endif
 
 // egress scratch words (GroupScratch::eg, EG_WORDS per packet)
 enum : uint32_t {
@@ -80,6 +109,22 @@ __device__ __forceinline__ void eg_final(const OutDev &o, uint32_t i, const EgOu
     if (o.proxy) o.proxy[i] = r.proxy;
     if (o.xdp) o.xdp[i] = 0;
     store_out(o, i, a);
+}
+
+template <bool FULL>
+__device__ __forceinline__ EpDev eg_src4(const DpParams &p, uint32_t idx)
+{
+    if constexpr (FULL) return G(p.eps)[idx];
+    EpDev e = ep_stage4<false>(p, idx);
+    e.seclabel = G(p.eps)[idx].seclabel;
+    return e;
+}
+
+// a local delivery handed over to k_egress_deliver (see there)
+__device__ __forceinline__ void del_list(const GroupScratch &g, bool v6, uint32_t i)
+{
+    const uint32_t at = wave_append(&g.cursor[del_ctr(v6, g.pos)], true);
+    g.single[at] = i;
 }
 
 // tail_handle_ipv{4,6} / handle_ingress: IS_ERR -> send_drop_notify(METRIC_EGRESS)
@@ -705,15 +750,30 @@ __device__ __noinline__ void eg4_frame(const DpParams &p, const BatchDev &b, con
     frame4_emit(f, in, o.frames + (size_t)i * b.stride, b.stride, r.len);
 }
 
-// handle_ipv4_from_lxc (bpf_lxc.c:464-649) from skip_service_lookup on
 template <class M>
+__device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                             const GroupScratch &g, uint32_t i, M &m);
+template <class M>
+__device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                             const GroupScratch &g, uint32_t i, M &m);
+
+// handle_ipv4_from_lxc (bpf_lxc.c:464-649) from skip_service_lookup on.  INL: the local
+// delivery runs inline (the continuation list, whose lanes run several members of a
+// group in one launch), else it is handed to k_egress_deliver.
+template <bool INL, class M>
 __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
                                             const GroupScratch &g, uint32_t i, M &m)
 {
+#ifdef CV_AB_TIMING
+    const bool tsamp = (i & 15) == 0;
+    long long tprev = wall_clock64();
+#endif
     Rec r;
     rec_load(r, b, i, 4);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
+    // the source endpoint's tables from its EpHot line (table constants folded: fewer
+    // live registers); the full EpDev where the event records need its constants
+    const EpDev ep = eg_src4<M::EV>(p, eg[1] & 0xFFFFu);
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -722,6 +782,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Eg4 x;
     eg4_state(r, eg, x);
+    TCK(0);
     Skb4 &s = x.s;
     Tuple4 &t = x.t;
     CtState st{0, 0, 0, 0, 0, 0};
@@ -733,7 +794,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     if (p.ipc4.l1) ipq = lpm4_begin(p.ipc4, bswap32(orig_dip));
     const uint32_t lxc_key = s.daddr;
     Probe<LxcV4Spec> lxq;
-    if (p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
+    if (EG_EARLY_LXC && p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
     bool mon = false;
     int ret = ct_lookup<false, EGF>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
@@ -741,6 +802,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     bool lxc_hit = false;
     int64_t lxc_slot = -1;
     RevNatOut rn1{false, false, 0, 0}, rn2{false, false, 0, 0};                 // reverse NATs applied (output frames)
+    TCK(1);
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     {                                                             // destination category (:482-494)
@@ -748,7 +810,13 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (p.ipc4.l1) { a.nl++; lab = lpm4_end(ipq, p.ipc4); }
         res.dst = lab ? lab : ((orig_dip & p.v4_cluster_mask) == p.v4_cluster_range ? CLUSTER_ID : WORLD_ID);
     }
+    TCK(2);
+#ifdef CV_AB_NOPOL
+    verdict = 0;
+#else
     verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+#endif
+    TCK(3);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);       // ct_delete4
@@ -760,8 +828,12 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
         const bool defer = eg[0] & EG_NAT_DEFER;
+#ifdef CV_AB_NOCREATE
+        const int c = 0;
+#else
         const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer, true);
         eg_changed();
+#endif
         if (defer && c != DROP_CT_CREATE_FAILED) g.ifx[i] |= BIT_NAT_DONE;
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
@@ -777,6 +849,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
             s.saddr = na;
         }
     }
+    TCK(4);
     if (verdict > 0) {                                            // ipv4_redirect_to_host_port + ipv4_l3
         notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
         res.proxy = (uint16_t)verdict;
@@ -787,10 +860,14 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     if (p.lxc4.buckets) {
         a.nl++;                                                   // lookup_ip4_endpoint(ip4)
-        lxc_slot = s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv)
+        lxc_slot = EG_EARLY_LXC && s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv)
                                       : dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv);
         lxc_hit = lxc_slot >= 0;
     }
+    TCK(5);
+#ifdef CV_AB_NODELIV
+    lxc_hit = false;
+#endif
     if (lxc_hit) {
         if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
         m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
@@ -803,12 +880,18 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         }
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
-        uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy4<M, EGF>(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc4, lxc_slot, iv), now,
-                                 ct2, res.proxy, res.reason, a, m, &rn2);
-        if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
-            eg4_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv4_local_delivery
-        eg_final(o, i, res, a);
+        // ipv4_local_delivery -> the destination's handle_policy: k_egress_deliver
+        uint32_t w4, chk;
+        uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+        d[0] = skb4_pack(s, w4, chk);
+        d[1] = make_uint4(w4, chk | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24,
+                          (e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u) | (rn1.loopback ? 1u << 26 : 0u),
+                          ep.seclabel);
+        d[2] = make_uint4(ifindex_of(m, p.lxc4, lxc_slot, iv), res.dst, (uint32_t)lxc_slot, rn1.na);
+        if (M::EV) d[3] = make_uint4(rn1.np, 0, 0, 0);
+        if constexpr (INL) deliver4_one(p, b, now, o, g, i, m);
+        else del_list(g, false, i);
+        TCK(6);
         return;
     }
     if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }            // pass_to_stack: ipv4_l3
@@ -817,6 +900,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     res.ret = TC_ACT_OK;
     if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
+    TCK(8);
     return;
 drop:
     eg_drop(p, res, ret, s.len, m);
@@ -857,7 +941,7 @@ __device__ __noinline__ void eg6_frame(const DpParams &p, const BatchDev &b, con
 }
 
 // ipv6_l3_from_lxc (bpf_lxc.c:133-352) from skip_service_lookup on
-template <class M>
+template <bool INL, class M>
 __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
                                             const GroupScratch &g, uint32_t i, M &m)
 {
@@ -879,7 +963,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     int64_t slot;
     const uint32_t orig_dip[4] = {t.daddr[0], t.daddr[1], t.daddr[2], t.daddr[3]};
     Probe<LxcV6Spec> lxq;                                         // endpoint lookup of daddr, issued early
-    if (p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
+    if (EG_EARLY_LXC && p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
     bool mon = false;
     int ret = ct_lookup<true, EGF, true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
@@ -895,7 +979,11 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         res.dst = lab ? lab
                       : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
     }
+#ifdef CV_AB_NOPOL
+    verdict = 0;
+#else
     verdict = policy_egress<false>(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
+#endif
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);       // ct_delete6
@@ -906,8 +994,12 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
+#ifdef CV_AB_NOCREATE
+        const int c = 0;
+#else
         const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, false, true);
         eg_changed();
+#endif
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
         uint32_t na[4], np;
@@ -932,9 +1024,13 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     if (p.lxc6.buckets) {                                         // lookup_ip6_endpoint (the daddr is unchanged)
         a.nl++;
-        lxc_slot = probe_end<LxcV6Spec>(lxq, p.lxc6, s.daddr, &iv);
+        lxc_slot = EG_EARLY_LXC ? probe_end<LxcV6Spec>(lxq, p.lxc6, s.daddr, &iv)
+                                : dev_find<LxcV6Spec>(p.lxc6, s.daddr, &iv);
         lxc_hit = lxc_slot >= 0;
     }
+#ifdef CV_AB_NODELIV
+    lxc_hit = false;
+#endif
     if (lxc_hit) {
         if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
         m.fwd(s.len, METRIC_EGRESS);
@@ -947,12 +1043,23 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         }
         const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
         if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
-        uint8_t ct2 = CT_NONE;
-        res.ret = handle_policy6<M, EGF>(p, EpDev(G(p.eps)[e2 - 1]), s, ep.seclabel, false, ifindex_of(m, p.lxc6, lxc_slot, iv), now, ct2,
-                                 res.proxy, res.reason, a, m, &rn2);
-        if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy)
-            eg6_frame(p, b, o, eg, i, ep, rn1, 2, lxc_slot, rn2);   // ipv6_local_delivery
-        eg_final(o, i, res, a);
+        // ipv6_local_delivery -> the destination's handle_policy: k_egress_deliver
+        uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+        d[0] = make_uint4(s.saddr[0], s.saddr[1], s.saddr[2], s.saddr[3]);
+        d[1] = make_uint4(s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3]);
+        d[2] = make_uint4(s.len, (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 |
+                                     ((uint32_t)s.l4off & 0xFFu) << 24,
+                          (s.h.p0 & 0xFFFFu) | s.h.p2 << 16,
+                          chk2(s.h.c1) | chk2(s.h.c14) << 2 | chk2(s.h.c4) << 4 | chk2(s.h.c2a) << 6 | chk2(s.h.c2b) << 8 |
+                              (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24);
+        d[3] = make_uint4((e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u), ep.seclabel,
+                          ifindex_of(m, p.lxc6, lxc_slot, iv), res.dst);
+        if (M::EV) {
+            d[4] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
+            d[5] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
+        }
+        if constexpr (INL) deliver6_one(p, b, now, o, g, i, m);
+        else del_list(g, true, i);
         return;
     }
     if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
@@ -967,14 +1074,85 @@ drop:
     eg_final(o, i, res, a);
 }
 
-// Occupancy of the egress conntrack stage: left alone the compiler spends 177 VGPRs
-// (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
-// capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
-// 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
-#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(4, 8)))
+// ================================================================== local delivery
+// A packet k_egress_ct forwards to a local endpoint leaves its state after the egress
+// program in a delivery record (g.del) and joins the position's delivery list; the
+// destination's policy program (handle_policy -> ipv{4,6}_policy) runs for the whole
+// list in k_egress_deliver, right after the k_egress_ct launch of the same position.
+// The packets of one position belong to different groups (no common conntrack entry),
+// so running all their egress halves before all their delivery halves equals running
+// each packet whole; the next position's launch follows both.  The split keeps the
+// delivery path out of the egress kernel's registers (it spilled over a hundred VGPRs
+// to scratch) and runs the deliveries with every lane on the same path.
+template <class M>
+__device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                             const GroupScratch &g, uint32_t i, M &m)
+{
+    const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+    const uint4 d0 = d[0], d1 = d[1], d2 = d[2];
+    Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
+    Acct a{(d1.y >> 16) & 0xFFu, d1.y >> 24, m.pc};
+    EgOut res{TC_ACT_OK, 0, d2.y, (uint8_t)(d1.z >> 16), 0};
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    RevNatOut rn2{false, false, 0, 0};
+    uint8_t ct2 = CT_NONE;
+    res.ret = handle_policy4<M, EGF>(p, G(p.eps)[d1.z & 0xFFFFu], s, d1.w, false, d2.x, now, ct2, res.proxy,
+                                     res.reason, a, m, &rn2);
+    if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy) {
+        const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        const RevNatOut rn1{(d1.z >> 25) & 1u ? true : false, (d1.z >> 26) & 1u ? true : false, d2.w, d[3].x};
+        eg4_frame(p, b, o, eg, i, G(p.eps)[eg[1] & 0xFFFFu], rn1, 2, (int64_t)d2.z, rn2);   // ipv4_local_delivery
+    }
+    eg_final(o, i, res, a);
+}
+
+template <class M>
+__device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                             const GroupScratch &g, uint32_t i, M &m)
+{
+    const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+    const uint4 d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+    Skb6 s;
+    s.saddr[0] = d0.x; s.saddr[1] = d0.y; s.saddr[2] = d0.z; s.saddr[3] = d0.w;
+    s.daddr[0] = d1.x; s.daddr[1] = d1.y; s.daddr[2] = d1.z; s.daddr[3] = d1.w;
+    s.len = d2.x;
+    s.nexthdr = d2.y & 0xFFu;
+    s.hoplimit = 0;                                               // (checked before the hand-over)
+    s.l4off = (int)(d2.y >> 24);
+    s.avail = b.stride;
+    s.h.type = (d2.y >> 8) & 0xFFu;
+    s.h.tflags = (d2.y >> 16) & 0xFFu;
+    s.h.p0 = d2.z & 0xFFFFu;
+    s.h.p2 = d2.z >> 16;
+    s.h.c1 = unchk2(d2.w & 3u);
+    s.h.c14 = unchk2((d2.w >> 2) & 3u);
+    s.h.c4 = unchk2((d2.w >> 4) & 3u);
+    s.h.c2a = unchk2((d2.w >> 6) & 3u);
+    s.h.c2b = unchk2((d2.w >> 8) & 3u);
+    Acct a{(d2.w >> 16) & 0xFFu, d2.w >> 24, m.pc};
+    EgOut res{TC_ACT_OK, 0, d3.w, (uint8_t)(d3.x >> 16), 0};
+    m.pkt = b.base + i;
+    m.hash = b.hash ? b.hash[i] : 0u;
+    RevNat6Out rn2;
+    rn2.valid = false;
+    uint8_t ct2 = CT_NONE;
+    res.ret = handle_policy6<M, EGF>(p, G(p.eps)[d3.x & 0xFFFFu], s, d3.y, false, d3.z, now, ct2, res.proxy,
+                                     res.reason, a, m, &rn2);
+    if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy) {
+        const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        const uint4 d4 = d[4], d5 = d[5];
+        RevNat6Out rn1;
+        rn1.valid = (d3.x >> 25) & 1u;
+        rn1.np = d4.y;
+        rn1.na[0] = d5.x; rn1.na[1] = d5.y; rn1.na[2] = d5.z; rn1.na[3] = d5.w;
+        eg6_frame(p, b, o, eg, i, G(p.eps)[eg[1] & 0xFFFFu], rn1, 2, (int64_t)d4.x, rn2);   // ipv6_local_delivery
+    }
+    eg_final(o, i, res, a);
+}
 
 template <bool V6, bool EV>
-__global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
+__global__ void __launch_bounds__(BLOCK) k_egress_deliver(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
@@ -983,10 +1161,37 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    // runs in the order of their first packets (measured faster here than size-class order)
-    for_each_flat(g, V6 ? Q_CT6 : Q_CT4, [&](uint32_t x, uint32_t) {
-        if constexpr (V6) egress6_one(p, b, now, o, g, x, m);
-        else egress4_one(p, b, now, o, g, x, m);
+    const uint32_t total = g.cursor[del_ctr(V6, g.pos)];
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < total; j += gridDim.x * BLOCK) {
+        const uint32_t i = g.single[j];
+        if constexpr (V6) deliver6_one(p, b, now, o, g, i, m);
+        else deliver4_one(p, b, now, o, g, i, m);
+    }
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
+}
+
+// Occupancy of the egress conntrack stage: left alone the compiler spends 177 VGPRs
+// (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
+// capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
+// 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
+#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(4, 8)))
+
+template <bool V6, bool EV, bool INL>
+__global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g,
+                                                                uint32_t pos)
+{
+    __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
+    using M = MetT<EV>;
+    M m;
+    pol_cache_init(pc);
+    met_init(m, lm);
+    m.pc = &pc;
+    // member `pos` of every group, in packet order (one launch per position)
+    for_each_at(g, V6 ? Q_CT6 : Q_CT4, pos, [&](uint32_t x) {
+        if constexpr (V6) egress6_one<INL>(p, b, now, o, g, x, m);
+        else egress4_one<INL>(p, b, now, o, g, x, m);
     });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
@@ -1071,14 +1276,50 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     g.q4 = Q_CT4;
     g.flat = 1;
     launch_gbin_groups(g, b.n, s);
-    if (ev) hipLaunchKernelGGL((k_egress_ct<false, true>), grid, blk, 0, s, p, b, now, o, g);
-    else hipLaunchKernelGGL((k_egress_ct<false, false>), grid, blk, 0, s, p, b, now, o, g);
-    if (b.stride >= 128) {
-        GroupScratch g6 = g;
+    // one launch per member position (the kernel boundary orders a group's members); a
+    // list's length is at most n / (pos + 1)
+    // and each followed by the local deliveries it handed over; the last (continuation)
+    // list delivers inline
+    for (uint32_t k = 0; k < NPOS; ++k) {
+        const dim3 gk(grid_for(b.n / (k + 1)));
+        GroupScratch gp = g, g6 = g;
+        gp.pos = g6.pos = k;
         g6.work = g.work6;
-        if (ev) hipLaunchKernelGGL((k_egress_ct<true, true>), grid, blk, 0, s, p, b, now, o, g6);
-        else hipLaunchKernelGGL((k_egress_ct<true, false>), grid, blk, 0, s, p, b, now, o, g6);
+        const bool last = k + 1 == NPOS;
+        for (int v6 = 0; v6 < (b.stride >= 128 ? 2 : 1); ++v6) {
+            const GroupScratch &gv = v6 ? g6 : gp;
+            if (last) {
+                if (v6) {
+                    if (ev) hipLaunchKernelGGL((k_egress_ct<true, true, true>), gk, blk, 0, s, p, b, now, o, gv, k);
+                    else hipLaunchKernelGGL((k_egress_ct<true, false, true>), gk, blk, 0, s, p, b, now, o, gv, k);
+                } else {
+                    if (ev) hipLaunchKernelGGL((k_egress_ct<false, true, true>), gk, blk, 0, s, p, b, now, o, gv, k);
+                    else hipLaunchKernelGGL((k_egress_ct<false, false, true>), gk, blk, 0, s, p, b, now, o, gv, k);
+                }
+                continue;
+            }
+            if (v6) {
+                if (ev) {
+                    hipLaunchKernelGGL((k_egress_ct<true, true, false>), gk, blk, 0, s, p, b, now, o, gv, k);
+                    hipLaunchKernelGGL((k_egress_deliver<true, true>), gk, blk, 0, s, p, b, now, o, gv);
+                } else {
+                    hipLaunchKernelGGL((k_egress_ct<true, false, false>), gk, blk, 0, s, p, b, now, o, gv, k);
+                    hipLaunchKernelGGL((k_egress_deliver<true, false>), gk, blk, 0, s, p, b, now, o, gv);
+                }
+            } else {
+                if (ev) {
+                    hipLaunchKernelGGL((k_egress_ct<false, true, false>), gk, blk, 0, s, p, b, now, o, gv, k);
+                    hipLaunchKernelGGL((k_egress_deliver<false, true>), gk, blk, 0, s, p, b, now, o, gv);
+                } else {
+                    hipLaunchKernelGGL((k_egress_ct<false, false, false>), gk, blk, 0, s, p, b, now, o, gv, k);
+                    hipLaunchKernelGGL((k_egress_deliver<false, false>), gk, blk, 0, s, p, b, now, o, gv);
+                }
+            }
+        }
     }
+#ifdef CV_AB_TIMING
+    hipLaunchKernelGGL(k_tdbg_dump, dim3(1), dim3(1), 0, s);
+#endif
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);

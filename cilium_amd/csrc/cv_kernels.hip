@@ -817,6 +817,7 @@ void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStr
 // see DESIGN.md §5.
 constexpr uint32_t SCAN_TILE = 4096;                             // entries per scan block (1024 x 4)
 constexpr uint32_t LCAP = 2048;                                  // bin entries sorted in LDS
+constexpr uint32_t GUNROLL = 8;                                  // keys loaded ahead per thread
 
 __device__ __forceinline__ uint32_t gkey_bin(unsigned long long k, uint32_t bits)
 {
@@ -854,9 +855,18 @@ __global__ void __launch_bounds__(1024) k_gkey_hist(GroupScratch g, uint32_t n)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[j] = 0;
     __syncthreads();
     const uint32_t tile = (n + GBLK - 1) / GBLK, lo = blockIdx.x * tile, hi = min(n, lo + tile);
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const unsigned long long k = g.pkey[i];
-        if (k) atomicAdd(&hist[gkey_bin(k, g.gbits)], 1u);
+    // GUNROLL keys in flight per thread (one block per CU: a load per iteration left
+    // the kernel latency-bound)
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += GUNROLL * blockDim.x) {
+        unsigned long long k[GUNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            k[u] = i < hi ? __builtin_nontemporal_load(&g.pkey[i]) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u)
+            if (k[u]) atomicAdd(&hist[gkey_bin(k[u], g.gbits)], 1u);
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) g.gcnt[j * GBLK + blockIdx.x] = hist[j];
@@ -926,11 +936,19 @@ __global__ void __launch_bounds__(1024) k_gkey_scatter(GroupScratch g, uint32_t 
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) pos[j] = g.gcnt[j * GBLK + blockIdx.x];
     __syncthreads();
     const uint32_t tile = (n + GBLK - 1) / GBLK, lo = blockIdx.x * tile, hi = min(n, lo + tile);
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const unsigned long long k = g.pkey[i];
-        if (!k) continue;
-        const uint32_t at = atomicAdd(&pos[gkey_bin(k, g.gbits)], 1u);
-        g.gent[at] = make_uint2(i, (uint32_t)k);
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += GUNROLL * blockDim.x) {
+        unsigned long long k[GUNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            k[u] = i < hi ? __builtin_nontemporal_load(&g.pkey[i]) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            if (!k[u]) continue;
+            const uint32_t at = atomicAdd(&pos[gkey_bin(k[u], g.gbits)], 1u);
+            g.gent[at] = make_uint2(i0 + u * blockDim.x, (uint32_t)k[u]);
+        }
     }
 }
 
@@ -1034,13 +1052,27 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
         uint32_t c = 1;
         while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
         const uint32_t q6 = key & 1u, x = (uint32_t)v[j];
-        uint32_t list = g.flat ? 0u : 15u, off = 1u << 25;        // 15: singletons (bit 25: a singleton)
+        if (g.flat) {                                             // position lists (egress)
+            uint32_t off = 0;
+            if (c >= NPOS) {                                      // the continuation list needs the run
+                off = 2 * start + atomicAdd(&fill, c + 1);
+                uint32_t *o = g.order + off;
+                o[0] = c;
+                for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
+            }
+            if (c > 8) atomicMax(&big[q6], c);
+            const uint32_t m = c < NPOS ? c : NPOS;
+            for (uint32_t t = 0; t < m; ++t)
+                g.hword[(uint32_t)v[j + t]] = (1u + q6 * 16 + t) << 26 | (t + 1 == NPOS ? off : 0u);
+            continue;
+        }
+        uint32_t list = 15u, off = 1u << 25;                      // 15: singletons (bit 25: a singleton)
         if (c > 1) {
             off = 2 * start + atomicAdd(&fill, c + 1);
             uint32_t *o = g.order + off;
             o[0] = c;
             for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
-            if (!g.flat) list = 15 - (uint32_t)size_class(c);     // largest class first
+            list = 15 - (uint32_t)size_class(c);                  // largest class first
             if (c > 8) atomicMax(&big[q6], c);
         }
         g.hword[x] = (1u + q6 * 16 + list) << 26 | off;
@@ -1080,7 +1112,7 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
         const uint32_t key = threadIdx.x, q = key >> 4 ? Q_NETDEV6 : g.q4, list = key & 15u;
         const uint32_t cnt = g.hcnt[(key + 1) * tiles] - g.hcnt[key * tiles];   // ([32 * tiles] = the total)
         if (g.flat) {
-            if (list == 0) g.cursor[qcls(q, 0)] = cnt;            // (for_each_flat)
+            g.cursor[qcls(q, list)] = cnt;                        // position list lengths (for_each_at)
         } else {
             if (list == 15) g.cursor[SINGLE_WORD0 + q] = cnt;
             g.cursor[qcls(q, list == 15 ? 0 : 15 - list)] = cnt;
@@ -1092,7 +1124,7 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
         const uint32_t hw = x < n ? g.hword[x] : 0u, h = hw >> 26;
         if (!h) continue;
         const uint32_t key = h - 1, q6 = key >> 4, at = atomicAdd(&pos[key], 1u);
-        if (g.flat) (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = (hw & (1u << 25)) ? (x | SINGLE_RUN) : (hw & ((1u << 25) - 1));
+        if (g.flat) (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = (key & 15u) + 1 == NPOS ? (hw & ((1u << 25) - 1)) : x;
         else if ((key & 15u) == 15u) (q6 ? g.single6 : g.single)[at - start[q6 * 2 + 1]] = x;
         else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = hw & ((1u << 25) - 1);
     }

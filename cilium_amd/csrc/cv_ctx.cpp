@@ -220,7 +220,8 @@ struct cv_ctx {
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
-    DevBuf gdel;                  // egress: local-delivery records (DEL_SLOTS x 16 B per packet)
+    DevBuf gdel, gest;            // egress: local-delivery records (DEL_SLOTS x 16 B per packet),
+                                  // the conntrack stage's input states (64 B per packet)
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
@@ -1102,7 +1103,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     (void)hipMemset(c->gtable.p, 0, cap * 16);
     if (egress || c->g_egress) {
         if (c->gparent.alloc(cap * 8) || c->geg.alloc((size_t)cmax * EG_WORDS * 4) ||
-            c->gdel.alloc((size_t)cmax * DEL_SLOTS * 16))
+            c->gdel.alloc((size_t)cmax * DEL_SLOTS * 16) || c->gest.alloc((size_t)cmax * 64))
             return -ENOMEM;
         (void)hipMemset(c->gparent.p, 0, cap * 8);
         c->g_egress = true;
@@ -1131,6 +1132,7 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     c->gwork6.as<uint32_t>(), c->ghword.as<uint32_t>(), c->ghcnt.as<uint32_t>(), (uint32_t)Q_NETDEV,
                     0};
     gs.del = c->gdel.as<uint4>();
+    gs.est = c->gest.as<uint4>();
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;

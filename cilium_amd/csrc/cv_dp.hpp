@@ -158,6 +158,8 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t pos;              // egress: the member position of the current launch pair
     uint4 *del;                // egress: per packet DEL_SLOTS x 16 B, the local-delivery record
                                // k_egress_ct hands to k_egress_deliver (listed in `single`)
+    uint4 *est;                // egress: per packet 64 B, the conntrack stage's packed input state
+                               // (k_egress_pairs -> k_egress_ct)
 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses

@@ -72,7 +72,7 @@ enum : uint32_t { STAGE_DONE = 0, STAGE_LB = 1, STAGE_CT = 2 };
 // (IPv6), a NAT-tuple writer to place (k_egress_nat), a deferred NAT write made
 // (k_nat_group).  Written by k_egress_pairs for every packet, BIT_NAT_DONE by the
 // packet's own lane in k_egress_ct.
-enum : uint32_t { BIT_V6 = 1, BIT_NAT_CAND = 2, BIT_NAT_DONE = 4 };
+enum : uint32_t { BIT_V6 = 1, BIT_NAT_CAND = 2, BIT_NAT_DONE = 4, BIT_NAT_DEFER = 8 };
 constexpr uint64_t SALT_SVC4 = 0x5356433400000000ULL, SALT_SVC6 = 0x5356433600000000ULL,
                    SALT_CT4 = 0x4354340000000000ULL, SALT_CT6 = 0x4354360000000000ULL,
                    SALT_NAT = 0x4E41540000000000ULL, SALT_SELF = 0x53454C4600000000ULL;
@@ -324,7 +324,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     Rec r;
     rec_load(r, b, i, 4);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
+    const EpDev ep = eg_src4<M::EV>(p, eg[1] & 0xFFFFu);
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -564,6 +564,39 @@ __device__ __forceinline__ void eg4_state(const Rec &r, const uint32_t *eg, Eg4 
     }
 }
 
+// The IPv4 egress state of a packet the conntrack stage runs, packed by k_egress_pairs
+// (which derives it from the record and the LB stage's scratch words anyway) into the
+// packet's 64-B line of g.est (written whole: partial lines cost the writer a read):
+// the stage then loads it with four 16-B loads instead of the 64-B record plus the
+// scratch words behind data-dependent branches.
+//   d0 skb4_pack(s)   d1 {w4, chk | ttl << 16 | flags << 24, ep | rev_nat << 16, slave}
+//   d2 {tuple daddr, ct_state addr, ct_state svc_addr, 0}   d3 0
+enum : uint32_t { ES_LOOPBACK = 1 };
+
+__device__ __forceinline__ void eg4_pack(const Eg4 &x, uint32_t ep, uint4 *d)
+{
+    uint32_t w4, chk;
+    d[0] = skb4_pack(x.s, w4, chk);
+    d[1] = make_uint4(w4, chk | (x.s.ttl & 0xFFu) << 16 | (x.stn.loopback ? ES_LOOPBACK : 0u) << 24,
+                      (ep & 0xFFFFu) | (x.stn.rev_nat & 0xFFFFu) << 16, x.stn.slave);
+    d[2] = make_uint4(x.t.daddr, x.stn.addr, x.stn.svc_addr, 0u);
+    d[3] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+__device__ __forceinline__ void eg4_unpack(const uint4 *d, uint32_t stride, Eg4 &x, uint32_t &ep, uint32_t &fl)
+{
+    const uint4 d0 = d[0], d1 = d[1], d2 = d[2];
+    x.s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, stride);
+    x.s.ttl = (d1.y >> 16) & 0xFFu;
+    fl = d1.y >> 24;
+    ep = d1.z & 0xFFFFu;
+    x.stn = CtState{d1.z >> 16, (fl & ES_LOOPBACK) ? 1u : 0u, d1.w, d2.y, d2.z, 0u};
+    x.t.nexthdr = x.s.nexthdr;
+    x.t.saddr = (fl & ES_LOOPBACK) ? d2.z : x.s.saddr;            // (a loopback skb carries IPV4_LOOPBACK)
+    x.t.daddr = d2.x;
+    x.t.dport = x.t.sport = 0;
+}
+
 struct Eg6 {
     Skb6 s;
     Tuple6 t;
@@ -584,6 +617,51 @@ __device__ __forceinline__ void eg6_state(const Rec6 &r, const uint32_t *eg, Eg6
     x.t.dport = x.t.sport = 0;
     x.stn = CtState{eg[3] & 0xFFFFu, 0, eg[3] >> 16, 0, 0, 0};
     if (!(eg[0] & EG_SVC)) x.stn = CtState{0, 0, 0, 0, 0, 0};
+}
+
+// The IPv6 egress state, packed the same way into the packet's line of g.est:
+//   d0 saddr  d1 daddr (after lb6_xlate)  d2 {len, nexthdr | type << 8 | tflags << 16 |
+//   l4off << 24, ports, chk | hoplimit << 16}  d3 {ep, the service stage's rev_nat | slave
+//   << 16 (0 without a service), 0, 0}
+__device__ __forceinline__ void eg6_pack(const Eg6 &x, uint32_t ep, uint32_t svc, uint4 *d)
+{
+    const Skb6 &s = x.s;
+    d[0] = make_uint4(s.saddr[0], s.saddr[1], s.saddr[2], s.saddr[3]);
+    d[1] = make_uint4(s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3]);
+    d[2] = make_uint4(s.len, (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 |
+                                 ((uint32_t)s.l4off & 0xFFu) << 24,
+                      (s.h.p0 & 0xFFFFu) | s.h.p2 << 16,
+                      chk2(s.h.c1) | chk2(s.h.c14) << 2 | chk2(s.h.c4) << 4 | chk2(s.h.c2a) << 6 | chk2(s.h.c2b) << 8 |
+                          (s.hoplimit & 0xFFu) << 16);
+    d[3] = make_uint4(ep & 0xFFFFu, svc, 0u, 0u);
+}
+
+__device__ __forceinline__ void eg6_unpack(const uint4 *d, uint32_t stride, Eg6 &x, uint32_t &ep)
+{
+    const uint4 d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+    Skb6 &s = x.s;
+    s.saddr[0] = d0.x; s.saddr[1] = d0.y; s.saddr[2] = d0.z; s.saddr[3] = d0.w;
+    s.daddr[0] = d1.x; s.daddr[1] = d1.y; s.daddr[2] = d1.z; s.daddr[3] = d1.w;
+    s.len = d2.x;
+    s.nexthdr = d2.y & 0xFFu;
+    s.l4off = (int)(d2.y >> 24);
+    s.avail = stride;
+    s.h.type = (d2.y >> 8) & 0xFFu;
+    s.h.tflags = (d2.y >> 16) & 0xFFu;
+    s.h.p0 = d2.z & 0xFFFFu;
+    s.h.p2 = d2.z >> 16;
+    s.h.c1 = unchk2(d2.w & 3u);
+    s.h.c14 = unchk2((d2.w >> 2) & 3u);
+    s.h.c4 = unchk2((d2.w >> 4) & 3u);
+    s.h.c2a = unchk2((d2.w >> 6) & 3u);
+    s.h.c2b = unchk2((d2.w >> 8) & 3u);
+    s.hoplimit = (d2.w >> 16) & 0xFFu;
+    ep = d3.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x.t.daddr[j] = s.daddr[j]; x.t.saddr[j] = s.saddr[j]; }
+    x.t.nexthdr = s.nexthdr;
+    x.t.dport = x.t.sport = 0;
+    x.stn = CtState{d3.y & 0xFFFFu, 0, d3.y >> 16, 0, 0, 0};
 }
 
 // ================================================================== pairs -> components
@@ -607,6 +685,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             rec_load(r, b, i, 4);
             Eg4 x;
             eg4_state(r, eg, x);
+            eg4_pack(x, eg[1], g.est + (size_t)i * 4);
             const uint32_t S = x.t.saddr;
             const uint32_t P = group_node(g, pair_hash4(S, x.t.daddr, SALT_CT4));
             g.gslot[i] = P;
@@ -656,6 +735,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             rec_load(r, b, i, 8);
             Eg6 x;
             eg6_state(r, eg, x);
+            eg6_pack(x, eg[1], (eg[0] & EG_SVC) ? eg[3] : 0u, g.est + (size_t)i * 4);
             const uint32_t P = group_node(g, pair_hash6(x.t.saddr, x.t.daddr, SALT_CT6));
             g.gslot[i] = P;
             uint32_t xs[4] = {x.s.saddr[0], x.s.saddr[1], x.s.saddr[2], x.s.saddr[3]};
@@ -699,8 +779,12 @@ __global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, Gr
             nn = group_find(g, self_hash(eg[4], eg[9], eg[10]));
             if (nn == NONE) nn = group_find(g, self_hash(eg[4], 0, 0x100));
         }
-        if (nn != NONE) uf_union(g, g.gslot[i], nn);
-        else eg[0] |= EG_NAT_DEFER;
+        if (nn != NONE) {
+            uf_union(g, g.gslot[i], nn);
+        } else {
+            eg[0] |= EG_NAT_DEFER;
+            g.ifx[i] |= BIT_NAT_DEFER;
+        }
     }
 }
 
@@ -768,20 +852,19 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     const bool tsamp = (i & 15) == 0;
     long long tprev = wall_clock64();
 #endif
-    Rec r;
-    rec_load(r, b, i, 4);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+    Eg4 x;
+    uint32_t epi, fl;
+    eg4_unpack(g.est + (size_t)i * 4, b.stride, x, epi, fl);
     // the source endpoint's tables from its EpHot line (table constants folded: fewer
     // live registers); the full EpDev where the event records need its constants
-    const EpDev ep = eg_src4<M::EV>(p, eg[1] & 0xFFFFu);
+    const EpDev ep = eg_src4<M::EV>(p, epi);
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
-    Eg4 x;
-    eg4_state(r, eg, x);
     TCK(0);
     Skb4 &s = x.s;
     Tuple4 &t = x.t;
@@ -827,7 +910,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
-        const bool defer = eg[0] & EG_NAT_DEFER;
+        const bool defer = g.ifx[i] & BIT_NAT_DEFER;
 #ifdef CV_AB_NOCREATE
         const int c = 0;
 #else
@@ -945,18 +1028,17 @@ template <bool INL, class M>
 __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
                                             const GroupScratch &g, uint32_t i, M &m)
 {
-    Rec6 r;
-    rec_load(r, b, i, 8);
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
+    Eg6 x;
+    uint32_t epi;
+    eg6_unpack(g.est + (size_t)i * 4, b.stride, x, epi);
+    const EpDev ep = G(p.eps)[epi];
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
-    Eg6 x;
-    eg6_state(r, eg, x);
     Skb6 &s = x.s;
     Tuple6 &t = x.t;
     CtState st{0, 0, 0, 0, 0, 0};

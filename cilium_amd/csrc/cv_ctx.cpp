@@ -1114,6 +1114,20 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     return 0;
 }
 
+// log2 of the bins of a binned grouping of n packets: bins of about 2^GBIN_LOG entries
+// (CV_GBIN_LOG overrides, for measurements), at most GBIN_MAX bins
+uint32_t gbin_bits(uint32_t n)
+{
+    static const int lg = [] {
+        const char *e = getenv("CV_GBIN_LOG");
+        const int v = e ? atoi(e) : 10;
+        return v >= 8 && v <= 12 ? v : 10;
+    }();
+    uint32_t b = 4;
+    while (b < 14 && (1ull << (b + lg)) < n) ++b;
+    return b;
+}
+
 // the scratch view for the next launch, which uses `epochs` fresh epochs
 GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
 {
@@ -1133,6 +1147,7 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     0};
     gs.del = c->gdel.as<uint4>();
     gs.est = c->gest.as<uint4>();
+    gs.q6 = (uint32_t)Q_NETDEV6;
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1157,7 +1172,7 @@ void group_stats(cv_ctx *c, const char *what, hipStream_t stream, bool flat)
         fprintf(stderr, "\n");
     }
     if (flat) {                                   // egress: the position lists' lengths
-        for (int q : {(int)Q_CT4, (int)Q_CT6}) {
+        for (int q : {(int)Q_LB4, (int)Q_LB6, (int)Q_CT4, (int)Q_CT6}) {
             fprintf(stderr, "[cv groups] %s %s: largest %u; packets per member position:", what, qn[q],
                     cur[GMAX_WORD0 + q]);
             for (uint32_t k = 0; k < NPOS; ++k) fprintf(stderr, " %u", cur[qcls(q, (int)k)]);
@@ -1928,8 +1943,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         if (!fits && cts.size() > (size_t)ADMIT_MAPS)
             n = ct_plan(c, cts, n, 2, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
-        gs.gbits = 4;                                             // bins of ~1024 packets (at most GBIN_MAX)
-        while (gs.gbits < 14 && (1ull << (gs.gbits + 10)) < n) ++gs.gbits;
+        gs.gbits = gbin_bits(n);
         if (!fits && cts.size() <= (size_t)ADMIT_MAPS) {
             r = run_admitted(c, p, chunk(b, off, n), chunk(o, off, b->stride), now, with_prefilter, gs, cts,
                              (hipStream_t)stream);
@@ -1970,8 +1984,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 7, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
-        gs.gbits = 4;                                             // (the binned grouping of the components)
-        while (gs.gbits < 14 && (1ull << (gs.gbits + 10)) < n) ++gs.gbits;
+        gs.gbits = gbin_bits(n);                                  // (the binned grouping of the components)
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
         if ((r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0,

@@ -1963,57 +1963,7 @@ __device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint
     }
 }
 
-constexpr int GMAX = 8;
-
-// Run fn(i) for every member of the group whose list starts at `head`, in
-// ascending packet order: <= GMAX members are sorted in registers; larger groups
-// are copied to a slice of g.order (cursor `cur`) and shell-sorted there.  One call
-// site of fn, so its (large) body is inlined once.
-template <class F>
-__device__ __forceinline__ void group_in_order(const GroupScratch &g, uint32_t head, int cur, F &&fn)
-{
-    uint32_t m[GMAX];
-    uint32_t cnt = 0;
-    uint32_t x = head;
-    for (; x != NONE && cnt < GMAX; x = g.next[x]) {
-        int pos = 0;
-#pragma unroll
-        for (int j = 0; j < GMAX; ++j) pos += (j < (int)cnt && m[j] < x) ? 1 : 0;
-#pragma unroll
-        for (int j = GMAX - 1; j >= 0; --j) {
-            const uint32_t left = j > 0 ? m[j - 1] : 0u;
-            m[j] = (j < pos) ? m[j] : (j == pos ? x : left);
-        }
-        ++cnt;
-    }
-    uint32_t *o = nullptr;
-    if (x != NONE) {                                              // large group
-        for (uint32_t y = x; y != NONE; y = g.next[y]) ++cnt;
-        o = g.order + atomicAdd(&g.cursor[cur], cnt);
-        uint32_t k = 0;
-        for (uint32_t y = head; y != NONE; y = g.next[y]) o[k++] = y;
-        for (uint32_t gap = cnt / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {   // shell sort
-            for (uint32_t i = gap; i < cnt; ++i) {
-                const uint32_t v = o[i];
-                uint32_t j = i;
-                for (; j >= gap && o[j - gap] > v; j -= gap) o[j] = o[j - gap];
-                o[j] = v;
-            }
-        }
-    }
-#pragma unroll 1
-    for (uint32_t j = 0; j < cnt; ++j) {
-        uint32_t v;
-        if (o) {
-            v = o[j];
-        } else {
-            v = m[0];
-#pragma unroll
-            for (int q = 1; q < GMAX; ++q) v = (q == (int)j) ? m[q] : v;
-        }
-        fn(v);
-    }
-}
+constexpr int GMAX = 8;        // group members k_group_flatten sorts in registers
 
 // fn(i, run size) for every member of every scheduled run of queue q, runs in `work`
 // order and members in packet order, then every singleton group (k_group_flatten

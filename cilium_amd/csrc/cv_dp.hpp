@@ -130,7 +130,7 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *eg;              // per packet: EG_WORDS words of egress scratch (egress path)
     uint32_t serial;           // launch serial (never reset; tags deferred CT writes)
     uint32_t *order;           // 2 words per packet: members of large groups sorted in place
-                               // (group_in_order), or the runs {size, members} of k_group_flatten
+                               // (k_group_flatten past GMAX), or the runs {size, members} of the grouping passes
     uint32_t *cursor;          // [CURSOR_WORDS] zeroed per launch: [0..2] cursors into `order`,
                                // [qctr(q, k)] length of sub-queue k of queue q (one 128-B line each)
     uint32_t *queue;           // dense lists of group slots (one lane per group), QSPLIT regions
@@ -151,7 +151,7 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *hword;           // per packet: 0, or for a group's first packet (1 + its list) << 26 | its run's
                                // offset in `order` (k_gbin_group -> k_heads_place)
     uint32_t *hcnt;            // per (list, tile) head counts -> positions (k_heads_count / place)
-    uint32_t q4;               // the IPv4 queue the binned grouping fills (Q_NETDEV, or Q_CT4 on egress)
+    uint32_t q4;               // the IPv4 queue the binned grouping fills (Q_NETDEV, or Q_LB4 / Q_CT4 on egress)
     uint32_t flat;             // 1: position lists (egress): list t < NPOS - 1 holds member t of every
                                // group, list NPOS - 1 the runs of groups past NPOS - 1 members, in
                                // packet order (k_gbin_group -> k_heads_place)
@@ -160,6 +160,7 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
                                // k_egress_ct hands to k_egress_deliver (listed in `single`)
     uint4 *est;                // egress: per packet 64 B, the conntrack stage's packed input state
                                // (k_egress_pairs -> k_egress_ct)
+    uint32_t q6;               // the IPv6 queue the binned grouping fills (Q_NETDEV6, or Q_LB6 / Q_CT6)
 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses

@@ -289,27 +289,30 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         }
         eg[0] |= stage;
         g.gslot[i] = NONE;
+        g.hword[i] = 0;
+        unsigned long long gk = 0;                                // the service group key (binned grouping)
         if (stage == STAGE_DONE) {
             eg_final(o, i, res, a);
         } else {
             store_out(o, i, a);
-            if (stage == STAGE_LB) {                              // join the (source, VIP) service group
-                const EpDev ep = G(p.eps)[e];
+            if (stage == STAGE_LB) {                              // the (source, VIP) service group
+                const uint32_t ct_id = G(p.eps)[e].ct_id;
                 uint64_t gh;
                 if (eg[0] & EG_V6) {
                     if constexpr (NW >= 32) {
                         const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
                         const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
-                        gh = pair_hash6(sa, da, SALT_SVC6 ^ ep.ct_id);
+                        gh = pair_hash6(sa, da, SALT_SVC6 ^ ct_id);
                     } else {
                         gh = 0;
                     }
                 } else {
-                    gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ep.ct_id);
+                    gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ct_id);
                 }
-                group_push(g, group_node(g, gh), i, (eg[0] & EG_V6) ? Q_LB6 : Q_LB4);
+                gk = (gh & ~3ull) | 2ull | ((eg[0] & EG_V6) ? 1ull : 0ull);
             }
         }
+        g.pkey[i] = gk;
     }
     met_flush(m, p.metrics);
 }
@@ -515,9 +518,11 @@ fin:
     eg_final(o, i, res, a);
 }
 
+// the service groups by member position, as the conntrack stage (position lists of the
+// binned grouping; one launch per position)
 template <bool V6, bool EV>
 __global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
-                                                    OutDev o, GroupScratch g)
+                                                    OutDev o, GroupScratch g, uint32_t pos)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;                                      // (here: the CT maps' live counts)
@@ -526,11 +531,9 @@ __global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, cons
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_group(g, V6 ? Q_LB6 : Q_LB4, [&](uint32_t, uint32_t head) {
-        group_in_order(g, head, 1, [&](uint32_t x) {
-            if constexpr (V6) lb6_one(p, b, hash, now, o, g, x, m);
-            else lb4_one(p, b, hash, now, o, g, x, m);
-        });
+    for_each_at(g, V6 ? Q_LB6 : Q_LB4, pos, [&](uint32_t x) {
+        if constexpr (V6) lb6_one(p, b, hash, now, o, g, x, m);
+        else lb4_one(p, b, hash, now, o, g, x, m);
     });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
@@ -1345,17 +1348,31 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
         if (ev) hipLaunchKernelGGL((k_egress_front<16, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
         else hipLaunchKernelGGL((k_egress_front<16, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
     }
-    if (ev) hipLaunchKernelGGL((k_lb_stage<false, true>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
-    else hipLaunchKernelGGL((k_lb_stage<false, false>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
-    if (b.stride >= 128) {
-        if (ev) hipLaunchKernelGGL((k_lb_stage<true, true>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
-        else hipLaunchKernelGGL((k_lb_stage<true, false>), grid, blk, 0, s, p, b, flow_hash, now, o, g);
+    // the service groups (source, VIP) by binning, then one LB launch per member position
+    {
+        GroupScratch gl = g;
+        gl.q4 = Q_LB4;
+        gl.q6 = Q_LB6;
+        gl.flat = 1;
+        launch_gbin_groups(gl, b.n, s);
+        GroupScratch gl6 = gl;
+        gl6.work = g.work6;
+        for (uint32_t k = 0; k < NPOS; ++k) {
+            const dim3 gk(grid_for(b.n / (k + 1)));
+            if (ev) hipLaunchKernelGGL((k_lb_stage<false, true>), gk, blk, 0, s, p, b, flow_hash, now, o, gl, k);
+            else hipLaunchKernelGGL((k_lb_stage<false, false>), gk, blk, 0, s, p, b, flow_hash, now, o, gl, k);
+            if (b.stride >= 128) {
+                if (ev) hipLaunchKernelGGL((k_lb_stage<true, true>), gk, blk, 0, s, p, b, flow_hash, now, o, gl6, k);
+                else hipLaunchKernelGGL((k_lb_stage<true, false>), gk, blk, 0, s, p, b, flow_hash, now, o, gl6, k);
+            }
+        }
     }
     g.epoch += 1;
     hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
     g.q4 = Q_CT4;
+    g.q6 = Q_CT6;
     g.flat = 1;
     launch_gbin_groups(g, b.n, s);
     // one launch per member position (the kernel boundary orders a group's members); a

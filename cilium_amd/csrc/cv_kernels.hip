@@ -1079,7 +1079,7 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
     }
     __syncthreads();
     if (threadIdx.x < 2 && big[threadIdx.x])                      // (diagnostics: the largest group)
-        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? Q_NETDEV6 : g.q4)], big[threadIdx.x]);
+        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? g.q6 : g.q4)], big[threadIdx.x]);
 }
 
 // The groups' first packets listed in packet order, list by list (IPv4 runs class
@@ -1109,7 +1109,7 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
     if (threadIdx.x < 32) pos[threadIdx.x] = g.hcnt[threadIdx.x * tiles + blockIdx.x];
     if (threadIdx.x < 4) start[threadIdx.x] = g.hcnt[(threadIdx.x >> 1) * 16 * tiles + (threadIdx.x & 1) * 15 * tiles];
     if (blockIdx.x == 0 && threadIdx.x < 32) {                    // list lengths -> the cursor words
-        const uint32_t key = threadIdx.x, q = key >> 4 ? Q_NETDEV6 : g.q4, list = key & 15u;
+        const uint32_t key = threadIdx.x, q = key >> 4 ? g.q6 : g.q4, list = key & 15u;
         const uint32_t cnt = g.hcnt[(key + 1) * tiles] - g.hcnt[key * tiles];   // ([32 * tiles] = the total)
         if (g.flat) {
             g.cursor[qcls(q, list)] = cnt;                        // position list lengths (for_each_at)

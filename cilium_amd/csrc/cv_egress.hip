@@ -28,36 +28,9 @@ namespace cv {
 constexpr bool EGF = false;
 __device__ __forceinline__ void eg_changed() { l1_inv(); }
 
-// the endpoint lookup of daddr issued ahead of the conntrack probes (its 64-B bucket then
-// stays in registers across them), or at its use
-#ifdef CV_AB_EARLY_LXC
-constexpr bool EG_EARLY_LXC = true;
-#else
-constexpr bool EG_EARLY_LXC = false;
-#endif
 
 int grid_for(uint32_t n);
 
-#ifdef CV_AB_TIMING
-// timing-only instrumentation (A/B builds): per member position and checkpoint the summed
-// wall-clock time since the previous checkpoint of sampled packets, and their count
-__device__ unsigned long long g_tdbg[NPOS][32];
-#define TCK(k) do { if (tsamp) { __builtin_amdgcn_s_waitcnt(0); const long long tn_ = wall_clock64(); \
-    atomicAdd(&g_tdbg[g.pos][k], (unsigned long long)(tn_ - tprev)); atomicAdd(&g_tdbg[g.pos][16 + (k)], 1ull); \
-    tprev = tn_; } } while (0)
-__global__ void k_tdbg_dump()
-{
-    for (uint32_t q = 0; q < NPOS; ++q) {
-        printf("[tdbg] pos %u:", q);
-        for (int k = 0; k < 16; ++k)
-            if (g_tdbg[q][16 + k]) printf(" %d:%.2fus/%llu", k, g_tdbg[q][k] * 0.01 / g_tdbg[q][16 + k], g_tdbg[q][16 + k]);
-        printf("\n");
-        for (int k = 0; k < 32; ++k) g_tdbg[q][k] = 0;
-    }
-}
-#else
-#define TCK(k) do { } while (0)
-#endif
 
 // egress scratch words (GroupScratch::eg, EG_WORDS per packet)
 enum : uint32_t {
@@ -851,10 +824,6 @@ template <bool INL, class M>
 __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
                                             const GroupScratch &g, uint32_t i, M &m)
 {
-#ifdef CV_AB_TIMING
-    const bool tsamp = (i & 15) == 0;
-    long long tprev = wall_clock64();
-#endif
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     Eg4 x;
     uint32_t epi, fl;
@@ -868,19 +837,17 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
-    TCK(0);
     Skb4 &s = x.s;
     Tuple4 &t = x.t;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
     const uint32_t orig_dip = t.daddr;
-    // issued ahead of the conntrack probes (independent reads of read-only tables):
-    // the ipcache lookup of orig_dip and the endpoint lookup of the packet's daddr
+    // the ipcache lookup of orig_dip issued ahead of the conntrack probes (independent
+    // reads of a read-only table); the endpoint lookup of daddr waits for its use (issued
+    // early, its 64-B bucket stayed in registers across the probes: no faster, and it
+    // spilled)
     Lpm4Pending ipq;
     if (p.ipc4.l1) ipq = lpm4_begin(p.ipc4, bswap32(orig_dip));
-    const uint32_t lxc_key = s.daddr;
-    Probe<LxcV4Spec> lxq;
-    if (EG_EARLY_LXC && p.lxc4.buckets) lxq = probe_begin<LxcV4Spec>(p.lxc4, &lxc_key);
     bool mon = false;
     int ret = ct_lookup<false, EGF>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
@@ -888,7 +855,6 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     bool lxc_hit = false;
     int64_t lxc_slot = -1;
     RevNatOut rn1{false, false, 0, 0}, rn2{false, false, 0, 0};                 // reverse NATs applied (output frames)
-    TCK(1);
     if (ret < 0) goto drop;
     res.ct = (uint8_t)ret;
     {                                                             // destination category (:482-494)
@@ -896,13 +862,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (p.ipc4.l1) { a.nl++; lab = lpm4_end(ipq, p.ipc4); }
         res.dst = lab ? lab : ((orig_dip & p.v4_cluster_mask) == p.v4_cluster_range ? CLUSTER_ID : WORLD_ID);
     }
-    TCK(2);
-#ifdef CV_AB_NOPOL
-    verdict = 0;
-#else
     verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
-#endif
-    TCK(3);
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);       // ct_delete4
@@ -914,12 +874,8 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
         const bool defer = g.ifx[i] & BIT_NAT_DEFER;
-#ifdef CV_AB_NOCREATE
-        const int c = 0;
-#else
         const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer, true);
         eg_changed();
-#endif
         if (defer && c != DROP_CT_CREATE_FAILED) g.ifx[i] |= BIT_NAT_DONE;
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
@@ -935,7 +891,6 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
             s.saddr = na;
         }
     }
-    TCK(4);
     if (verdict > 0) {                                            // ipv4_redirect_to_host_port + ipv4_l3
         notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
         res.proxy = (uint16_t)verdict;
@@ -946,14 +901,9 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     }
     if (p.lxc4.buckets) {
         a.nl++;                                                   // lookup_ip4_endpoint(ip4)
-        lxc_slot = EG_EARLY_LXC && s.daddr == lxc_key ? probe_end<LxcV4Spec>(lxq, p.lxc4, &lxc_key, &iv)
-                                      : dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv);
+        lxc_slot = dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv);
         lxc_hit = lxc_slot >= 0;
     }
-    TCK(5);
-#ifdef CV_AB_NODELIV
-    lxc_hit = false;
-#endif
     if (lxc_hit) {
         if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
         m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
@@ -977,7 +927,6 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         if (M::EV) d[3] = make_uint4(rn1.np, 0, 0, 0);
         if constexpr (INL) deliver4_one(p, b, now, o, g, i, m);
         else del_list(g, false, i);
-        TCK(6);
         return;
     }
     if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }            // pass_to_stack: ipv4_l3
@@ -986,7 +935,6 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     res.ret = TC_ACT_OK;
     if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
     eg_final(o, i, res, a);
-    TCK(8);
     return;
 drop:
     eg_drop(p, res, ret, s.len, m);
@@ -1047,8 +995,6 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
     const uint32_t orig_dip[4] = {t.daddr[0], t.daddr[1], t.daddr[2], t.daddr[3]};
-    Probe<LxcV6Spec> lxq;                                         // endpoint lookup of daddr, issued early
-    if (EG_EARLY_LXC && p.lxc6.buckets) lxq = probe_begin<LxcV6Spec>(p.lxc6, s.daddr);
     bool mon = false;
     int ret = ct_lookup<true, EGF, true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
     int verdict;
@@ -1064,11 +1010,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         res.dst = lab ? lab
                       : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
     }
-#ifdef CV_AB_NOPOL
-    verdict = 0;
-#else
     verdict = policy_egress<false>(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
-#endif
     if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
         if (ret == CT_ESTABLISHED) {
             ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);       // ct_delete6
@@ -1079,12 +1021,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     if (ret == CT_NEW) {
         x.stn.src_sec_id = ep.seclabel;
-#ifdef CV_AB_NOCREATE
-        const int c = 0;
-#else
         const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, false, true);
         eg_changed();
-#endif
         if (is_err(c)) { ret = c; goto drop; }
     } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
         uint32_t na[4], np;
@@ -1109,13 +1047,9 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     }
     if (p.lxc6.buckets) {                                         // lookup_ip6_endpoint (the daddr is unchanged)
         a.nl++;
-        lxc_slot = EG_EARLY_LXC ? probe_end<LxcV6Spec>(lxq, p.lxc6, s.daddr, &iv)
-                                : dev_find<LxcV6Spec>(p.lxc6, s.daddr, &iv);
+        lxc_slot = dev_find<LxcV6Spec>(p.lxc6, s.daddr, &iv);
         lxc_hit = lxc_slot >= 0;
     }
-#ifdef CV_AB_NODELIV
-    lxc_hit = false;
-#endif
     if (lxc_hit) {
         if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
         m.fwd(s.len, METRIC_EGRESS);
@@ -1260,7 +1194,10 @@ __global__ void __launch_bounds__(BLOCK) k_egress_deliver(DpParams p, BatchDev b
 // (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
 // capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
 // 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
-#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(4, 8)))
+#ifndef CV_EG_WAVES
+#define CV_EG_WAVES 4
+#endif
+#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WAVES, 8)))
 
 template <bool V6, bool EV, bool INL>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g,
@@ -1416,9 +1353,6 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
             }
         }
     }
-#ifdef CV_AB_TIMING
-    hipLaunchKernelGGL(k_tdbg_dump, dim3(1), dim3(1), 0, s);
-#endif
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);

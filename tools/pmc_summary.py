@@ -22,7 +22,10 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage<false>",
-            "config5": "k_egress_ct<false, false>"}
+            "config5": "k_egress_ct<true, false, false>"}
+# launches of the dominant kernel per step (config 5: the IPv6 stage's member positions
+# before the continuation list, cv_egress.hip NPOS - 1)
+LAUNCHES = {"config5": 7}
 
 
 def per_kernel(path):
@@ -55,7 +58,7 @@ def main():
                     # queues: such near-empty dispatches are not launches of the path
                     v = [x for x in v if x >= 0.01 * max(v)] or v
                     ctr[c] = (sum(v) / len(v), len(v))
-    steps = ctr["FETCH_SIZE"][1]                                  # one dominant-kernel launch per step
+    steps = ctr["FETCH_SIZE"][1] / LAUNCHES.get(w, 1)            # dominant-kernel launches per step
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv")))}
     avg_ns = next(float(r["AverageNs"]) for n, r in stats.items() if f"::{kname}(" in n)
     tp = os.path.join(src, f"stats_{w}", "run_kernel_trace.csv")

@@ -23,9 +23,9 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage<false>",
             "config5": "k_egress_ct<true, false, false>"}
-# launches of the dominant kernel per step (config 5: the IPv6 stage's member positions
-# before the continuation list, cv_egress.hip NPOS - 1)
-LAUNCHES = {"config5": 7}
+# a kernel launched exactly once per step (counts the steps of a pass)
+STEP_KERNEL = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_netdev_front<false>",
+               "config5": "k_egress_front<32, false>"}
 
 
 def per_kernel(path):
@@ -45,9 +45,12 @@ def main():
     kname = DOMINANT[w]
     setup = ("k_ct_load", "k_ct_scan", "k_ct_op", "k_ct_gc")      # table loads / map API, not the step
     ctr, step = {}, defaultdict(float)
+    nsteps = 0
     for i in (1, 2, 3):
         p = os.path.join(src, f"pmc{i}_{w}", "run_counter_collection.csv")
         for name, cs in per_kernel(p).items():
+            if i == 1 and f"::{STEP_KERNEL[w]}(" in name:
+                nsteps = len(next(iter(cs.values())))
             if not name.startswith(("cv::", "void cv::")) or any(f"::{x}(" in name for x in setup):
                 continue
             for c, v in cs.items():
@@ -58,7 +61,7 @@ def main():
                     # queues: such near-empty dispatches are not launches of the path
                     v = [x for x in v if x >= 0.01 * max(v)] or v
                     ctr[c] = (sum(v) / len(v), len(v))
-    steps = ctr["FETCH_SIZE"][1] / LAUNCHES.get(w, 1)            # dominant-kernel launches per step
+    steps = nsteps or ctr["FETCH_SIZE"][1]
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv")))}
     avg_ns = next(float(r["AverageNs"]) for n, r in stats.items() if f"::{kname}(" in n)
     tp = os.path.join(src, f"stats_{w}", "run_kernel_trace.csv")

@@ -85,6 +85,50 @@ __device__ __forceinline__ void rec_load_wave64(Rec &r, const BatchDev &b, uint3
     __builtin_amdgcn_wave_barrier();
 }
 
+// The same for records of any register width (NW / 4 16-B parts, stride 4 * NW): the
+// wave's 64 consecutive records in NW / 4 fully coalesced 1-KiB loads through LDS
+// (`st`: 16 * NW uint4 per wave).  All 64 lanes, wave-uniform, i0 + 64 <= b.n.
+template <int NW>
+__device__ __forceinline__ void rec_load_coop(RecT<NW> &r, const BatchDev &b, uint32_t i0, uint4 *st)
+{
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int P = NW / 4;
+    const int lane = threadIdx.x & 63;
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(b.frames + (size_t)i0 * (4 * NW));
+#pragma unroll
+    for (int c = 0; c < P; ++c) {
+        const u32x4 v = __builtin_nontemporal_load(src + c * 64 + lane);
+        const int chunk = c * 64 + lane;                          // record chunk / P, part chunk % P
+        st[(chunk % P) * 64 + chunk / P] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t i = i0 + lane;
+    r.base = b.frames + (size_t)i * (4 * NW);
+    r.len = b.len[i];
+    r.stride = 4 * NW;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const uint4 v = st[k * 64 + lane];
+        r.w[4 * k] = v.x; r.w[4 * k + 1] = v.y; r.w[4 * k + 2] = v.z; r.w[4 * k + 3] = v.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the first 16 words of a wider record (an IPv4 packet in a 128-B record)
+template <int NW>
+__device__ __forceinline__ Rec rec_head(const RecT<NW> &w)
+{
+    Rec r;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) r.w[j] = w.w[j];
+    r.base = w.base;
+    r.len = w.len;
+    r.stride = w.stride;
+    return r;
+}
+
 template <int O, int NW>
 __device__ __forceinline__ uint32_t rec_u8c(const RecT<NW> &r)
 {

@@ -233,12 +233,18 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
                                                         OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
+    __shared__ uint4 stage[BLOCK / 64][16 * NW];                  // cooperative record loads
+    uint4 *st = stage[threadIdx.x >> 6];
     using M = MetT<EV>;
     M m;
     met_init(m, lm);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < b.n; i0 += gridDim.x * BLOCK) {
+        const uint32_t i = i0 + lane;
         RecT<NW> r;
-        rec_load(r, b, i, NW / 4);
+        if (i0 + 64 <= b.n && b.stride == 4 * NW) rec_load_coop(r, b, i0, st);   // (wave-uniform)
+        else if (i < b.n) rec_load(r, b, i, NW / 4);
+        if (i >= b.n) continue;
         Acct a{0, 0};
         EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
@@ -647,21 +653,26 @@ __device__ __forceinline__ void eg6_unpack(const uint4 *d, uint32_t stride, Eg6 
 // = backend), is a blind write: k_egress_nat merges it into the component only
 // when some packet reads its pair, else its write is deferred to k_nat_apply, which
 // resolves writers of one key last-writer-wins, as the sequential run does.
-__global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
+// one packet of k_egress_pairs: its record `rw` (loaded when `have`), its packed conntrack
+// input state left in es[0..3] (zero for a packet that reaches no conntrack stage)
+template <int NW>
+__device__ __forceinline__ void pairs_one(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
+                                          const RecT<NW> &rw, bool have, uint4 *es)
 {
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+    {
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-        if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; g.ifx[i] = 0; continue; }
+        if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; g.ifx[i] = 0; return; }
         g.ifx[i] = ((eg[0] & EG_V6) ? BIT_V6 : 0u) |
                    ((eg[0] & (EG_V6 | EG_SVC)) == EG_SVC && eg[4] ? BIT_NAT_CAND : 0u);
         const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
         Acct na{0, 0};                                            // speculative probes are not accounted
         if (!(eg[0] & EG_V6)) {
             Rec r;
-            rec_load(r, b, i, 4);
+            if (have) r = rec_head(rw);
+            else rec_load(r, b, i, 4);
             Eg4 x;
             eg4_state(r, eg, x);
-            eg4_pack(x, eg[1], g.est + (size_t)i * 4);
+            eg4_pack(x, eg[1], es);
             const uint32_t S = x.t.saddr;
             const uint32_t P = group_node(g, pair_hash4(S, x.t.daddr, SALT_CT4));
             g.gslot[i] = P;
@@ -708,10 +719,15 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
             }
         } else {
             Rec6 r;
-            rec_load(r, b, i, 8);
+            if constexpr (NW >= 32) {
+                if (have) r = rw;
+                else rec_load(r, b, i, 8);
+            } else {
+                rec_load(r, b, i, 8);                             // (a 64-B batch holds no IPv6 stage packet)
+            }
             Eg6 x;
             eg6_state(r, eg, x);
-            eg6_pack(x, eg[1], (eg[0] & EG_SVC) ? eg[3] : 0u, g.est + (size_t)i * 4);
+            eg6_pack(x, eg[1], (eg[0] & EG_SVC) ? eg[3] : 0u, es);
             const uint32_t P = group_node(g, pair_hash6(x.t.saddr, x.t.daddr, SALT_CT6));
             g.gslot[i] = P;
             uint32_t xs[4] = {x.s.saddr[0], x.s.saddr[1], x.s.saddr[2], x.s.saddr[3]};
@@ -738,6 +754,44 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
                 uf_union(g, P, group_node(g, pair_hash6(na6, x.t.saddr, SALT_CT6)));
                 uf_union(g, P, group_node(g, pair_hash6(na6, xs, SALT_CT6)));
             }
+        }
+    }
+}
+
+// The records come in through LDS (a wave's 64 consecutive records in coalesced 1-KiB
+// loads) and the packed input states leave the same way, one 64-B line per packet.
+template <int NW>
+__global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
+{
+    __shared__ uint4 stage[BLOCK / 64][16 * NW];
+    uint4 *st = stage[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < b.n; i0 += gridDim.x * BLOCK) {
+        const uint32_t i = i0 + lane;
+        const bool full = i0 + 64 <= b.n && b.stride == 4 * NW;  // (wave-uniform)
+        RecT<NW> rw;
+        if (full) rec_load_coop(rw, b, i0, st);
+        uint4 es[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) es[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < b.n) pairs_one<NW>(p, b, g, i, rw, full, es);
+        if (full) {
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) st[k * 64 + lane] = es[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint4 *dst = g.est + (size_t)i0 * 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int chunk = c * 64 + (int)lane;             // packet chunk / 4, part chunk % 4
+                dst[chunk] = st[(chunk & 3) * 64 + (chunk >> 2)];
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else if (i < b.n) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g.est[(size_t)i * 4 + k] = es[k];
         }
     }
 }
@@ -1305,7 +1359,8 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
         }
     }
     g.epoch += 1;
-    hipLaunchKernelGGL(k_egress_pairs, grid, blk, 0, s, p, b, g);
+    if (b.stride >= 128) hipLaunchKernelGGL(k_egress_pairs<32>, grid, blk, 0, s, p, b, g);
+    else hipLaunchKernelGGL(k_egress_pairs<16>, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_egress_nat, grid, blk, 0, s, p, b, g);
     hipLaunchKernelGGL(k_group_link, grid, blk, 0, s, b, g);
     g.q4 = Q_CT4;

@@ -177,6 +177,14 @@ __device__ __forceinline__ int rec_chk(const RecT<NW> &r, int off, int n)
     return 0;
 }
 
+// rec_chk on a packet known only by its length and record stride
+__device__ __forceinline__ int len_chk(uint32_t len, uint32_t stride, int off, int n)
+{
+    if (off < 0 || (uint32_t)(off + n) > len) return 1;
+    if ((uint32_t)(off + n) > stride) return E_TRUNC;
+    return 0;
+}
+
 // The L4 bytes the programs read, with the outcome of each load the reference
 // does: [off,1) ICMP type, [off+12,2) TCP flags, [off,4) ports, [off,2) sport,
 // [off+2,2) dport.  Rewrites (lb xlate, rev-NAT) update p0 / p2 in place, as the

@@ -93,6 +93,68 @@ __device__ __forceinline__ EpDev eg_src4(const DpParams &p, uint32_t idx)
     return e;
 }
 
+// The service stage's input state of a packet (the front parsed it anyway), in the
+// packet's 64-B line of g.est (k_egress_pairs later overwrites it with the conntrack
+// stage's): IPv4 d0 skb4_pack(s), d1 {w4, chk, 0, 0}; IPv6 d0 saddr, d1 daddr, d2 {len,
+// nexthdr | type << 8 | tflags << 16 | l4off << 24, ports, chk}; both d3 {eg[1], eg[2]}
+__device__ __forceinline__ void lb_pack4(const Skb4 &s, uint32_t e1, uint32_t e2, uint4 *d)
+{
+    uint32_t w4, chk;
+    d[0] = skb4_pack(s, w4, chk);
+    d[1] = make_uint4(w4, chk, 0u, 0u);
+    d[3] = make_uint4(e1, e2, 0u, 0u);
+}
+
+__device__ __forceinline__ void lb_pack6(const Skb6 &s, uint32_t e1, uint32_t e2, uint4 *d)
+{
+    d[0] = make_uint4(s.saddr[0], s.saddr[1], s.saddr[2], s.saddr[3]);
+    d[1] = make_uint4(s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3]);
+    d[2] = make_uint4(s.len, (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 |
+                                 ((uint32_t)s.l4off & 0xFFu) << 24,
+                      (s.h.p0 & 0xFFFFu) | s.h.p2 << 16,
+                      chk2(s.h.c1) | chk2(s.h.c14) << 2 | chk2(s.h.c4) << 4 | chk2(s.h.c2a) << 6 | chk2(s.h.c2b) << 8);
+    d[3] = make_uint4(e1, e2, 0u, 0u);
+}
+
+__device__ __forceinline__ void skb6_unpack(const uint4 &d0, const uint4 &d1, const uint4 &d2, uint32_t stride, Skb6 &s)
+{
+    s.saddr[0] = d0.x; s.saddr[1] = d0.y; s.saddr[2] = d0.z; s.saddr[3] = d0.w;
+    s.daddr[0] = d1.x; s.daddr[1] = d1.y; s.daddr[2] = d1.z; s.daddr[3] = d1.w;
+    s.len = d2.x;
+    s.nexthdr = d2.y & 0xFFu;
+    s.l4off = (int)(d2.y >> 24);
+    s.avail = stride;
+    s.h.type = (d2.y >> 8) & 0xFFu;
+    s.h.tflags = (d2.y >> 16) & 0xFFu;
+    s.h.p0 = d2.z & 0xFFFFu;
+    s.h.p2 = d2.z >> 16;
+    s.h.c1 = unchk2(d2.w & 3u);
+    s.h.c14 = unchk2((d2.w >> 2) & 3u);
+    s.h.c4 = unchk2((d2.w >> 4) & 3u);
+    s.h.c2a = unchk2((d2.w >> 6) & 3u);
+    s.h.c2b = unchk2((d2.w >> 8) & 3u);
+    s.hoplimit = (d2.w >> 16) & 0xFFu;
+}
+
+// a lane's 64 B at dst + 64 * lane (the wave's 64 consecutive lines) through LDS as four
+// coalesced 1-KiB stores; all 64 lanes, wave-uniform (`st`: 256 uint4)
+__device__ __forceinline__ void wave_store64(uint4 *dst, const uint4 *v, uint4 *st)
+{
+    const int lane = threadIdx.x & 63;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[k * 64 + lane] = v[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int chunk = c * 64 + lane;                          // line chunk / 4, part chunk % 4
+        dst[chunk] = st[(chunk & 3) * 64 + (chunk >> 2)];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // a local delivery handed over to k_egress_deliver (see there)
 __device__ __forceinline__ void del_list(const GroupScratch &g, bool v6, uint32_t i)
 {
@@ -242,9 +304,13 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
     for (uint32_t i0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < b.n; i0 += gridDim.x * BLOCK) {
         const uint32_t i = i0 + lane;
         RecT<NW> r;
-        if (i0 + 64 <= b.n && b.stride == 4 * NW) rec_load_coop(r, b, i0, st);   // (wave-uniform)
+        const bool full = i0 + 64 <= b.n && b.stride == 4 * NW;  // (wave-uniform)
+        if (full) rec_load_coop(r, b, i0, st);
         else if (i < b.n) rec_load(r, b, i, NW / 4);
         if (i >= b.n) continue;
+        uint4 es[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) es[k] = make_uint4(0u, 0u, 0u, 0u);
         Acct a{0, 0};
         EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
@@ -289,9 +355,20 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
                     gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ct_id);
                 }
                 gk = (gh & ~3ull) | 2ull | ((eg[0] & EG_V6) ? 1ull : 0ull);
+                // the service stage's input: the parsed skb and the scratch words it reads
+                if (eg[0] & EG_V6) {
+                    if constexpr (NW >= 32) lb_pack6(skb6_from(r), eg[1], eg[2], es);
+                } else {
+                    lb_pack4(skb4_from(rec_head(r)), eg[1], eg[2], es);
+                }
             }
         }
         g.pkey[i] = gk;
+        if (!full && stage == STAGE_LB) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g.est[(size_t)i * 4 + k] = es[k];
+        }
+        if (full) wave_store64(g.est + (size_t)i0 * 4, es, st);
     }
     met_flush(m, p.metrics);
 }
@@ -303,10 +380,11 @@ template <class M>
 __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, const uint32_t *hash, uint32_t now,
                                         const OutDev &o, const GroupScratch &g, uint32_t i, M &m)
 {
-    Rec r;
-    rec_load(r, b, i, 4);
+    const uint4 *d = g.est + (size_t)i * 4;
+    const uint4 d0 = d[0], d1 = d[1], d3 = d[3];
+    const Skb4 sk = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev ep = eg_src4<M::EV>(p, eg[1] & 0xFFFFu);
+    const EpDev ep = eg_src4<M::EV>(p, d3.x & 0xFFFFu);
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -314,13 +392,14 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
-    uint32_t key_dport = eg[1] >> 16;
-    const uint32_t count = eg[2] & 0xFFFFu;
-    const uint32_t saddr = rec_raw32c<26>(r), vip = rec_raw32c<30>(r);
-    const int off = 14 + (int)(rec_u8c<14>(r) & 0xFu) * 4;
-    L4Hdr h = l4_read<34>(r, off);
+    uint32_t key_dport = d3.x >> 16;
+    const uint32_t count = d3.y & 0xFFFFu;
+    const uint32_t saddr = sk.saddr, vip = sk.daddr;
+    const int off = sk.l4off;
+    L4Hdr h = sk.h;
+    struct { uint32_t len; } r{sk.len};
     Tuple4 t;
-    t.daddr = vip; t.saddr = saddr; t.nexthdr = rec_u8c<23>(r); t.dport = t.sport = 0;
+    t.daddr = vip; t.saddr = saddr; t.nexthdr = sk.nexthdr; t.dport = t.sport = 0;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
     int ret = ct_lookup<false, EGF>(ep.ct4, t, h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
@@ -378,7 +457,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         uint32_t flags = STAGE_CT | EG_SVC | (st.loopback ? EG_LOOPBACK : 0u);
         const int coff = t.nexthdr == 6 ? 16 : t.nexthdr == 17 ? 6 : 0;   // lb4_xlate: the L4 checksum
         if (coff) {                                               // update by diff (pseudo header)
-            const int c = rec_chk(r, off + coff, 2);
+            const int c = len_chk(sk.len, b.stride, off + coff, 2);
             if (c) { ret = chk_err(c, DROP_CSUM_L4); goto fin; }
         }
         uint32_t ndport = 0;
@@ -409,10 +488,13 @@ template <class M>
 __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, const uint32_t *hash, uint32_t now,
                                         const OutDev &o, const GroupScratch &g, uint32_t i, M &m)
 {
-    Rec6 r;
-    rec_load(r, b, i, 8);
+    const uint4 *d = g.est + (size_t)i * 4;
+    const uint4 d3 = d[3];
+    Skb6 s;
+    skb6_unpack(d[0], d[1], d[2], b.stride, s);
+    struct { uint32_t len; } r{s.len};
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
+    const EpDev ep = G(p.eps)[d3.x & 0xFFFFu];
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -420,9 +502,8 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
-    uint32_t key_dport = eg[1] >> 16;
-    const uint32_t count = eg[2] & 0xFFFFu;
-    Skb6 s = skb6_from(r);
+    uint32_t key_dport = d3.x >> 16;
+    const uint32_t count = d3.y & 0xFFFFu;
     Tuple6 t;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
@@ -776,19 +857,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, 
         for (int k = 0; k < 4; ++k) es[k] = make_uint4(0u, 0u, 0u, 0u);
         if (i < b.n) pairs_one<NW>(p, b, g, i, rw, full, es);
         if (full) {
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int k = 0; k < 4; ++k) st[k * 64 + lane] = es[k];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint4 *dst = g.est + (size_t)i0 * 4;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int chunk = c * 64 + (int)lane;             // packet chunk / 4, part chunk % 4
-                dst[chunk] = st[(chunk & 3) * 64 + (chunk >> 2)];
-            }
-            __builtin_amdgcn_wave_barrier();
+            wave_store64(g.est + (size_t)i0 * 4, es, st);
         } else if (i < b.n) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) g.est[(size_t)i * 4 + k] = es[k];

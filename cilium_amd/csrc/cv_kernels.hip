@@ -993,9 +993,11 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
     }
     __syncthreads();
     if (in_lds) {
-        // counting sort by 8 more key bits (sub-bins of a few entries), then an insertion
-        // sort of each sub-bin by one thread; a bin with a sub-bin past SUBMAX (a hot
-        // address pair) takes the bitonic sort instead
+        // counting sort by 8 more key bits (sub-bins of a few entries), then every entry
+        // ranked within its sub-bin by its own thread (a rank sort: m compares per entry,
+        // all entries at once; one insertion sort per sub-bin and thread spent m^2 steps
+        // on its largest sub-bin); a bin with a sub-bin past SUBMAX (a hot address pair)
+        // takes the bitonic sort instead
         uint32_t *cnt = sub_cnt, *off = sub_off;
         cnt[threadIdx.x] = 0;
         if (threadIdx.x == 0) sub_max = 0;
@@ -1016,26 +1018,25 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
                 perm[off[sb] + atomicAdd(&cnt[sb], 1u)] = (uint16_t)j;
             }
             __syncthreads();
-            const uint32_t o = off[threadIdx.x];
-            for (uint32_t a = 1; a < mine; ++a) {                 // this thread's sub-bin
-                const uint16_t x = perm[o + a];
-                const unsigned long long xv = lv[x];
-                uint32_t t = a;
-                for (; t > 0 && lv[perm[o + t - 1]] > xv; --t) perm[o + t] = perm[o + t - 1];
-                perm[o + t] = x;
-            }
-            __syncthreads();
-            unsigned long long r[LCAP / 256];
+            uint32_t dst[LCAP / 256];
+            unsigned long long val[LCAP / 256];
 #pragma unroll
             for (uint32_t k = 0; k < LCAP / 256; ++k) {
                 const uint32_t j = threadIdx.x + k * 256;
-                if (j < nb) r[k] = lv[perm[j]];
+                if (j < nb) {
+                    const unsigned long long xv = lv[j];
+                    const uint32_t sb = sub_of(xv), o = off[sb], c = cnt[sb];
+                    uint32_t rank = 0;
+                    for (uint32_t q = o; q < o + c; ++q) rank += lv[perm[q]] < xv ? 1u : 0u;   // (composites differ)
+                    dst[k] = o + rank;
+                    val[k] = xv;
+                }
             }
             __syncthreads();
 #pragma unroll
             for (uint32_t k = 0; k < LCAP / 256; ++k) {
                 const uint32_t j = threadIdx.x + k * 256;
-                if (j < nb) lv[j] = r[k];
+                if (j < nb) lv[dst[k]] = val[k];
             }
             __syncthreads();
         }

@@ -320,9 +320,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         m.hash = b.hash ? b.hash[i] : 0u;
         m.src_id = e < p.n_eps ? G(p.eps)[e].lxc_id : 0u;
         m.src_label = e < p.n_eps ? G(p.eps)[e].seclabel : 0u;
-        eg[1] = e & 0xFFFFu;
-        eg[2] = 0;
-        eg[0] = 0;
+        uint32_t egl[3] = {0u, e & 0xFFFFu, 0u};                 // eg[0..2], stored once below
         uint32_t stage;
         if (e >= p.n_eps) {
             res.ret = DROP_MISSED_TAIL_CALL;                      // no program for the source: nothing ran
@@ -330,9 +328,10 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         } else {
             const EpDev ep = G(p.eps)[e];                           // handle_ingress: send_trace_notify(FROM_LXC)
             notify_trace(p, m, TRACE_FROM_LXC, r.len, ep.lxc_id, ep.seclabel, 0, 0, 0, 0, true);
-            stage = front_one(p, ep, r, eg, res, a, m);
+            stage = front_one(p, ep, r, egl, res, a, m);
         }
-        eg[0] |= stage;
+        egl[0] |= stage;
+        reinterpret_cast<uint4 *>(eg)[0] = make_uint4(egl[0], egl[1], egl[2], 0u);
         g.gslot[i] = NONE;
         g.hword[i] = 0;
         unsigned long long gk = 0;                                // the service group key (binned grouping)
@@ -343,7 +342,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
             if (stage == STAGE_LB) {                              // the (source, VIP) service group
                 const uint32_t ct_id = G(p.eps)[e].ct_id;
                 uint64_t gh;
-                if (eg[0] & EG_V6) {
+                if (egl[0] & EG_V6) {
                     if constexpr (NW >= 32) {
                         const uint32_t sa[4] = {rec_raw32c<22>(r), rec_raw32c<26>(r), rec_raw32c<30>(r), rec_raw32c<34>(r)};
                         const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
@@ -354,12 +353,12 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
                 } else {
                     gh = pair_hash4(rec_raw32c<26>(r), rec_raw32c<30>(r), SALT_SVC4 ^ ct_id);
                 }
-                gk = (gh & ~3ull) | 2ull | ((eg[0] & EG_V6) ? 1ull : 0ull);
+                gk = (gh & ~3ull) | 2ull | ((egl[0] & EG_V6) ? 1ull : 0ull);
                 // the service stage's input: the parsed skb and the scratch words it reads
-                if (eg[0] & EG_V6) {
-                    if constexpr (NW >= 32) lb_pack6(skb6_from(r), eg[1], eg[2], es);
+                if (egl[0] & EG_V6) {
+                    if constexpr (NW >= 32) lb_pack6(skb6_from(r), egl[1], egl[2], es);
                 } else {
-                    lb_pack4(skb4_from(rec_head(r)), eg[1], eg[2], es);
+                    lb_pack4(skb4_from(rec_head(r)), egl[1], egl[2], es);
                 }
             }
         }
@@ -466,13 +465,11 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
             ndport = sport_svc;
             flags |= EG_DPORT_RW;
         }
-        eg[0] = flags;
-        eg[2] = ndport << 16 | (key_dport & 0xFFFFu);                // (the final lb4_key.dport)
-        eg[3] = (st.rev_nat & 0xFFFFu) | st.slave << 16;
-        eg[4] = st.addr;
-        eg[5] = st.svc_addr;
-        eg[6] = tdaddr;
-        eg[7] = target;                                           // skb daddr after lb4_xlate
+        // eg[2]: the final lb4_key.dport | the rewritten port; eg[7]: the skb daddr after
+        // lb4_xlate (three wide stores; eg[1] rewritten unchanged)
+        uint4 *e4 = reinterpret_cast<uint4 *>(eg);
+        e4[0] = make_uint4(flags, d3.x, ndport << 16 | (key_dport & 0xFFFFu), (st.rev_nat & 0xFFFFu) | st.slave << 16);
+        e4[1] = make_uint4(st.addr, st.svc_addr, tdaddr, target);
         eg[8] = skb_saddr;
         store_out(o, i, a);
         return;
@@ -564,11 +561,10 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
             ndport = sport_svc;
             flags |= EG_DPORT_RW;
         }
-        eg[0] = flags;
-        eg[2] = ndport << 16 | (key_dport & 0xFFFFu);                // (the final lb4_key.dport)
-        eg[3] = (st.rev_nat & 0xFFFFu) | st.slave << 16;
+        uint4 *e4 = reinterpret_cast<uint4 *>(eg);                // (eg[2]: the final lb6_key.dport)
+        e4[0] = make_uint4(flags, d3.x, ndport << 16 | (key_dport & 0xFFFFu), (st.rev_nat & 0xFFFFu) | st.slave << 16);
         eg[4] = 0; eg[5] = 0;
-        eg[12] = v[0]; eg[13] = v[1]; eg[14] = v[2]; eg[15] = v[3];   // tuple daddr = skb daddr = target
+        e4[3] = make_uint4(v[0], v[1], v[2], v[3]);               // tuple daddr = skb daddr = target
         store_out(o, i, a);
         return;
     }
@@ -741,8 +737,17 @@ __device__ __forceinline__ void pairs_one(const DpParams &p, const BatchDev &b, 
                                           const RecT<NW> &rw, bool have, uint4 *es)
 {
     {
-        uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
+        uint32_t *egp = g.eg + (size_t)i * EG_WORDS;
+        const uint4 *e4 = reinterpret_cast<const uint4 *>(egp);
+        uint32_t eg[EG_WORDS];                                    // the scratch words, four wide loads
+        const uint4 e0 = e4[0];
+        eg[0] = e0.x; eg[1] = e0.y; eg[2] = e0.z; eg[3] = e0.w;
         if ((eg[0] & EG_STAGE) != STAGE_CT) { g.gslot[i] = NONE; g.ifx[i] = 0; return; }
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const uint4 v = e4[k];
+            eg[4 * k] = v.x; eg[4 * k + 1] = v.y; eg[4 * k + 2] = v.z; eg[4 * k + 3] = v.w;
+        }
         g.ifx[i] = ((eg[0] & EG_V6) ? BIT_V6 : 0u) |
                    ((eg[0] & (EG_V6 | EG_SVC)) == EG_SVC && eg[4] ? BIT_NAT_CAND : 0u);
         const EpDev ep = G(p.eps)[eg[1] & 0xFFFFu];
@@ -770,6 +775,8 @@ __device__ __forceinline__ void pairs_one(const DpParams &p, const BatchDev &b, 
             const bool l4ok = ct_l4<false>(t1, x.s.h, CT_EGRESS, seen) >= 0;
             eg[9] = port_sig(t1);                                 // the key signature of this packet's
             eg[10] = t1.nexthdr;                                  // create (and NAT) tuples
+            egp[9] = eg[9];
+            egp[10] = eg[10];
             if (l4ok && S == x.t.daddr)                           // self-pair egress lookup keys
                 uf_union(g, P, group_node(g, self_hash(S, eg[9], t1.nexthdr)));
             if (x.s.saddr == x.s.daddr) {                         // self-pair keys of the delivery lookups

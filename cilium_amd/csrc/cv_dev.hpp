@@ -1934,10 +1934,9 @@ __device__ __forceinline__ void group_push(const GroupScratch &g, uint32_t s, ui
 
 // ------------------------------------------------------------------ size-sorted runs
 // One lane runs a group's packets one after another, so a wave lasts as long as the
-// largest of its 64 groups.  Before a heavy stage the queue's groups are flattened
-// into runs {size, members in packet order} in `order` (k_group_flatten) and listed
-// in `work` by size class, largest first (k_group_schedule): the groups of one wave
-// then have about the same size and its lanes stay busy.
+// largest of its 64 groups.  The binned grouping (k_gbin_group, k_heads_place) lists
+// the runs {size, members in packet order} of the netdev path in `work` by size class,
+// largest first: the groups of one wave then have about the same size.
 __host__ __device__ constexpr int size_class(uint32_t n)
 {
     return n <= 8 ? (n ? (int)n - 1 : 0) : n <= 12 ? 8 : n <= 16 ? 9 : n <= 24 ? 10 : n <= 32 ? 11
@@ -2015,18 +2014,12 @@ __device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint
     }
 }
 
-constexpr int GMAX = 8;        // group members k_group_flatten sorts in registers
-
-// fn(i, run size) for every member of every scheduled run of queue q, runs in `work`
-// order and members in packet order, then every singleton group (k_group_flatten
-// lists their packets densely in `single`); the next member's index is loaded while
-// fn runs.  (SORTED false: the queue in order when k_group_schedule did not run, the
-// queue word of a singleton naming its packet, SINGLE_RUN-tagged.)
-template <bool SORTED = true, class F>
+// fn(i, run size) for every member of every listed run of queue q, runs in `work`
+// order and members in packet order, then every singleton group (listed densely in
+// `single`); the next member's index is loaded while fn runs.
+template <class F>
 __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool first_only, F &&fn)
 {
-    uint32_t n[QSPLIT];
-    const uint32_t total = queue_sizes(g, q, n);
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     auto run = [&](uint32_t off) {
         const uint32_t cnt = first_only ? 1u : g.order[off];
@@ -2038,20 +2031,12 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
             v = vn;
         }
     };
-    if constexpr (SORTED) {
-        uint32_t multi = 0;                                       // scheduled runs: classes >= 1
+    uint32_t multi = 0;                                           // listed runs: classes >= 1
 #pragma unroll
-        for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
-        for (uint32_t j = tid; j < multi; j += stride) run(g.work[j]);
-        const uint32_t singles = g.cursor[SINGLE_WORD0 + q];
-        for (uint32_t j = tid; j < singles; j += stride) fn(g.single[j], 1u);
-    } else {
-        for (uint32_t j = tid; j < total; j += stride) {
-            const uint32_t e = *queue_entry(g, q, n, j);
-            if (e & SINGLE_RUN) fn(e & ~SINGLE_RUN, 1u);
-            else run(e);
-        }
-    }
+    for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
+    for (uint32_t j = tid; j < multi; j += stride) run(g.work[j]);
+    const uint32_t singles = g.cursor[SINGLE_WORD0 + q];
+    for (uint32_t j = tid; j < singles; j += stride) fn(g.single[j], 1u);
 }
 
 // fn(i) for member `pos` of every group of queue q (position lists, g.flat), in packet

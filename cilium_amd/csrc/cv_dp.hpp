@@ -129,16 +129,15 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     unsigned long long *parent;// per table slot: epoch << 32 | union-find parent (egress path)
     uint32_t *eg;              // per packet: EG_WORDS words of egress scratch (egress path)
     uint32_t serial;           // launch serial (never reset; tags deferred CT writes)
-    uint32_t *order;           // 2 words per packet: members of large groups sorted in place
-                               // (k_group_flatten past GMAX), or the runs {size, members} of the grouping passes
+    uint32_t *order;           // 2 words per packet: the runs {size, members} of the binned grouping
     uint32_t *cursor;          // [CURSOR_WORDS] zeroed per launch: [0..2] cursors into `order`,
                                // [qctr(q, k)] length of sub-queue k of queue q (one 128-B line each)
     uint32_t *queue;           // dense lists of group slots (one lane per group), QSPLIT regions
     uint32_t qregion;          // words per region
     uint32_t *work;            // per group: `order` offset of its run, in size-class order
     uint32_t *ifx;             // per packet: the destination endpoint's ifindex (netdev path)
-    uint32_t *single;          // the packets of singleton groups, dense (k_group_flatten with a
-                               // schedule, k_gbin_group; cursor[SINGLE_WORD0 + q] of them)
+    uint32_t *single;          // the packets of singleton groups, dense (k_gbin_group ->
+                               // k_heads_place; cursor[SINGLE_WORD0 + q] of them)
     // netdev path (k_gkey_hist / k_gkey_scatter / k_gbin_group): groups by binning
     unsigned long long *pkey;  // per packet: the address-pair key of a staged packet, 0 if none
     uint2 *gent;               // staged packets binned by key: {packet, key low word}
@@ -175,17 +174,15 @@ enum : int { Q_NETDEV = 0, Q_LB4 = 1, Q_LB6 = 2, Q_CT4 = 3, Q_CT6 = 4, Q_NAT = 5
 // the netdev path's IPv6 groups (handle_ipv6 -> ipv6_policy) use the CT6 queue, which the
 // egress path alone fills otherwise; it sits in the other bank from Q_NETDEV
 constexpr int Q_NETDEV6 = Q_CT6;
-// Size-sorted runs (k_group_flatten / k_group_schedule): per queue NCLASS group-size
-// classes, each a {count, fill} pair on its own line after the sub-queue counters; cursor[3] is
-// the allocation cursor of the runs in `order` ({size, members...}).
+// Size-sorted runs (k_heads_place): per queue NCLASS group-size classes, each a count on
+// its own line after the sub-queue counters.
 constexpr int QSPLIT = 16, QBANKS = 2, NCLASS = 16;
 constexpr int CLS0 = 32 + NQUEUES * QSPLIT * 32, CURSOR_WORDS = CLS0 + NQUEUES * NCLASS * 32;
 __host__ __device__ constexpr int qbank(int q) { return (q == Q_LB6 || q == Q_CT6) ? 1 : 0; }
 __host__ __device__ constexpr int qctr(int q, int k) { return 32 + (q * QSPLIT + k) * 32; }
 __host__ __device__ constexpr int qcls(int q, int c) { return CLS0 + (q * NCLASS + c) * 32; }
-constexpr int RUN_CURSOR = 3;
-constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (k_group_flatten)
-constexpr uint32_t SINGLE_RUN = 0x80000000u; // a flattened queue word naming a singleton's packet
+constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (diagnostics)
+constexpr uint32_t SINGLE_RUN = 0x80000000u; // a list word naming a singleton's packet (diagnostics)
 constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
 constexpr int EG_WORDS = 16;
 // position lists of the egress conntrack stage: one launch per member position, the last
@@ -199,10 +196,6 @@ __host__ __device__ constexpr int del_ctr(bool v6, uint32_t pos) { return 32 + (
 // the binned grouping of the packets whose g.pkey is set (cv_kernels.hip): runs, and the
 // lists of the groups' first packets (g.flat: one per queue)
 void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s);
-// flatten + schedule the groups of queue q (before the stage that runs them)
-// sched: 0 runs in queue order (no k_group_schedule), 1 largest size class first,
-// 2 smallest first
-void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStream_t s);
 int launch_policy_fold(const HashTable &pol, hipStream_t s);
 int launch_xdp_prefilter(const DpParams &p, const BatchDev &b, const OutDev &o, hipStream_t s);
 int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const OutDev &o, hipStream_t s);

@@ -396,18 +396,17 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     const uint32_t saddr = sk.saddr, vip = sk.daddr;
     const int off = sk.l4off;
     L4Hdr h = sk.h;
-    struct { uint32_t len; } r{sk.len};
     Tuple4 t;
     t.daddr = vip; t.saddr = saddr; t.nexthdr = sk.nexthdr; t.dport = t.sport = 0;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
-    int ret = ct_lookup<false, EGF>(ep.ct4, t, h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
+    int ret = ct_lookup<false, EGF>(ep.ct4, t, h, CT_SERVICE, sk.len, now, p.flags, slot, &st, a);
     uint32_t k[2], v[3];
     bool have = false;
     if (ret == E_TRUNC) goto fin;
     if (ret == CT_NEW) {
         st.slave = hsh % count + 1;                               // lb4_select_slave
-        const int c = ct_create<false>(ep.ct4, t, r.len, CT_SERVICE, st, now, a, p.ct_guard, false, true);
+        const int c = ct_create<false>(ep.ct4, t, sk.len, CT_SERVICE, st, now, a, p.ct_guard, false, true);
         eg_changed();
         if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
     } else if (ret < 0) {
@@ -476,7 +475,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     }
 fin:
     eg[0] = STAGE_DONE;
-    eg_drop(p, res, ret, r.len, m);
+    eg_drop(p, res, ret, sk.len, m);
     eg_final(o, i, res, a);
 }
 
@@ -489,7 +488,6 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     const uint4 d3 = d[3];
     Skb6 s;
     skb6_unpack(d[0], d[1], d[2], b.stride, s);
-    struct { uint32_t len; } r{s.len};
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
     const EpDev ep = G(p.eps)[d3.x & 0xFFFFu];
     m.pkt = b.base + i;
@@ -507,13 +505,13 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     t.nexthdr = s.nexthdr; t.dport = t.sport = 0;
     CtState st{0, 0, 0, 0, 0, 0};
     int64_t slot;
-    int ret = ct_lookup<true, EGF>(ep.ct6, t, s.h, CT_SERVICE, r.len, now, p.flags, slot, &st, a);
+    int ret = ct_lookup<true, EGF>(ep.ct6, t, s.h, CT_SERVICE, s.len, now, p.flags, slot, &st, a);
     uint32_t k[5] = {s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3], 0}, v[6];
     bool have = false;
     if (ret == E_TRUNC) goto fin;
     if (ret == CT_NEW) {
         st.slave = hsh % count + 1;
-        const int c = ct_create<true>(ep.ct6, t, r.len, CT_SERVICE, st, now, a, p.ct_guard, false, true);
+        const int c = ct_create<true>(ep.ct6, t, s.len, CT_SERVICE, st, now, a, p.ct_guard, false, true);
         eg_changed();
         if (is_err(c)) { ret = DROP_NO_SERVICE; goto fin; }
     } else if (ret < 0) {
@@ -570,7 +568,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     }
 fin:
     eg[0] = STAGE_DONE;
-    eg_drop(p, res, ret, r.len, m);
+    eg_drop(p, res, ret, s.len, m);
     eg_final(o, i, res, a);
 }
 

@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutD
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_run<true>(g, Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
+    for_each_run(g, Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
         if (x - p.win_lo < p.win_span) stage2_one(p, b, o, g, x, now, m, n == 1);     // (admission windows)
     });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
@@ -508,7 +508,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage6(DpParams p, BatchDev b, Out
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    for_each_run<true>(g, Q_NETDEV6, false, [&](uint32_t x, uint32_t n) {
+    for_each_run(g, Q_NETDEV6, false, [&](uint32_t x, uint32_t n) {
         if (x - p.win_lo < p.win_span) stage2_one6(p, b, o, g, x, now, m, n == 1);
     });
     met_flush(m, p.metrics);
@@ -623,182 +623,6 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Out
     pol_cache_flush(pc);
 }
 
-// ------------------------------------------------------------------ size-sorted runs
-// k_group_flatten: every queued group of q becomes a run {size, members ascending}
-// in `order`; the queue word is replaced by the run's offset (a singleton's by its
-// packet, SINGLE_RUN-tagged, and with `dense` the packet is listed in `single`);
-// per-class counts.  A thread takes FLAT_PER_THREAD groups per pass and walks their
-// member lists in lockstep (independent dependent-load chains in flight together);
-// a block allocates its runs and singleton slots with one atomic per counter per pass
-// of BLOCK * FLAT_PER_THREAD groups (returning atomics on one word serialise at about
-// 90 per microsecond chip-wide, so the per-pass count is what bounds the kernel).
-// Block-uniform loop (the scans use every lane).
-constexpr int FLAT_PER_THREAD = 4;
-__global__ void __launch_bounds__(BLOCK) k_group_flatten(GroupScratch g, int q, bool dense)
-{
-    constexpr int U = FLAT_PER_THREAD;
-    __shared__ uint32_t hist[NCLASS], wsum[BLOCK / 64], ssum[BLOCK / 64], bbase, sbase;
-    if (threadIdx.x < NCLASS) hist[threadIdx.x] = 0;
-    uint32_t n[QSPLIT];
-    const uint32_t total = queue_sizes(g, q, n);
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr uint32_t SPAN = BLOCK * U;
-    for (uint32_t base = blockIdx.x * SPAN; base < total; base += gridDim.x * SPAN) {
-        uint32_t *ent[U], cnt[U], head[U], x[U];
-        uint32_t m[U][GMAX];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = base + u * BLOCK + threadIdx.x;
-            ent[u] = nullptr;
-            cnt[u] = 0;
-            head[u] = x[u] = NONE;
-            if (j >= total) continue;
-            ent[u] = queue_entry(g, q, n, j);
-            head[u] = (uint32_t)g.table[2 * *ent[u] + 1];
-            x[u] = head[u];
-        }
-        for (bool more = true; more;) {                           // the member lists, in lockstep
-            more = false;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (x[u] == NONE || cnt[u] >= GMAX) continue;
-                const uint32_t v = x[u];
-                int pos = 0;                                      // insertion into registers
-#pragma unroll
-                for (int t = 0; t < GMAX; ++t) pos += (t < (int)cnt[u] && m[u][t] < v) ? 1 : 0;
-#pragma unroll
-                for (int t = GMAX - 1; t >= 0; --t) {
-                    const uint32_t left = t > 0 ? m[u][t - 1] : 0u;
-                    m[u][t] = (t < pos) ? m[u][t] : (t == pos ? v : left);
-                }
-                ++cnt[u];
-                x[u] = g.next[v];
-                more = true;
-            }
-        }
-        uint32_t tneed = 0, tone = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            for (uint32_t y = x[u]; y != NONE; y = g.next[y]) ++cnt[u];   // (groups past GMAX: count)
-            tneed += cnt[u] > 1 ? cnt[u] + 1 : 0;                 // singletons need no run
-            tone += cnt[u] == 1 ? 1 : 0;
-        }
-        uint32_t incl = tneed, sincl = tone;                      // wave inclusive scans
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(incl, d, 64), ts = __shfl_up(sincl, d, 64);
-            if (lane >= (uint32_t)d) { incl += t; sincl += ts; }
-        }
-        if (lane == 63) { wsum[wv] = incl; ssum[wv] = sincl; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0, sacc = 0;
-            for (int w = 0; w < BLOCK / 64; ++w) {
-                const uint32_t t = wsum[w], u = ssum[w];
-                wsum[w] = acc; acc += t;
-                ssum[w] = sacc; sacc += u;
-            }
-            bbase = acc ? atomicAdd(&g.cursor[RUN_CURSOR], acc) : 0;
-            sbase = dense && sacc ? atomicAdd(&g.cursor[SINGLE_WORD0 + q], sacc) : 0;
-        }
-        __syncthreads();
-        // singleton slots in (wave, u, lane) order: consecutive lanes list consecutive
-        // queue entries, as the stage reads them
-        uint32_t off = bbase + wsum[wv] + incl - tneed, so = sbase + ssum[wv], big = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = cnt[u];
-            const unsigned long long ones = __ballot(c == 1);
-            big = max(big, c);
-            if (c == 1) {                                         // no run: the packet itself
-                if (dense) g.single[so + __popcll(ones & ((1ull << lane) - 1))] = head[u];
-                *ent[u] = head[u] | SINGLE_RUN;                   // (k_group_schedule skips it)
-                atomicAdd(&hist[0], 1u);
-            } else if (c) {
-                uint32_t *o = g.order + off;
-                o[0] = c;
-                if (c <= GMAX) {
-#pragma unroll
-                    for (int t = 0; t < GMAX; ++t)
-                        if (t < (int)c) o[1 + t] = m[u][t];
-                } else {                                          // large group: copy, shell sort
-                    uint32_t k = 1;
-                    for (uint32_t y = head[u]; y != NONE; y = g.next[y]) o[k++] = y;
-                    ++o;
-                    for (uint32_t gap = c / 2; gap > 0; gap = gap == 2 ? 1 : gap * 5 / 11) {
-                        for (uint32_t i = gap; i < c; ++i) {
-                            const uint32_t v = o[i];
-                            uint32_t t = i;
-                            for (; t >= gap && o[t - gap] > v; t -= gap) o[t] = o[t - gap];
-                            o[t] = v;
-                        }
-                    }
-                }
-                *ent[u] = off;
-                off += c + 1;
-                atomicAdd(&hist[size_class(c)], 1u);
-            }
-            so += __popcll(ones);
-        }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) big = max(big, (uint32_t)__shfl_xor(big, d, 64));   // (diagnostics)
-        if (lane == 0 && big > 8) atomicMax(&g.cursor[GMAX_WORD0 + q], big);
-        __syncthreads();                                          // wsum / bbase reuse
-    }
-    __syncthreads();
-    if (threadIdx.x < NCLASS && hist[threadIdx.x]) atomicAdd(&g.cursor[qcls(q, threadIdx.x)], hist[threadIdx.x]);
-}
-
-// k_group_schedule: `work` lists the runs class by class, largest class first (or
-// smallest first).  Class 0, the singletons, is not scheduled: it takes no room in
-// `work`, so the runs fill work[0 .. runs) as for_each_run reads them in either order.
-constexpr int SCHED_PER_THREAD = 16;   // (class-counter atomics per 4 096 runs: 62 -> 33 us per call vs 4)
-__global__ void __launch_bounds__(BLOCK) k_group_schedule(GroupScratch g, int q, bool largest_first)
-{
-    __shared__ uint32_t cbase[NCLASS], lcnt[NCLASS], lbase[NCLASS];
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int k = 0; k < NCLASS; ++k) {
-            const int c = largest_first ? NCLASS - 1 - k : k;
-            cbase[c] = acc;
-            if (c) acc += g.cursor[qcls(q, c)];
-        }
-    }
-    uint32_t n[QSPLIT];
-    const uint32_t total = queue_sizes(g, q, n);
-    constexpr uint32_t SPAN = BLOCK * SCHED_PER_THREAD;
-    for (uint32_t base = blockIdx.x * SPAN; base < total; base += gridDim.x * SPAN) {
-        if (threadIdx.x < NCLASS) lcnt[threadIdx.x] = 0;
-        __syncthreads();
-        uint32_t off[SCHED_PER_THREAD], cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD];
-#pragma unroll
-        for (int u = 0; u < SCHED_PER_THREAD; ++u) {
-            const uint32_t j = base + u * BLOCK + threadIdx.x;
-            off[u] = SINGLE_RUN;
-            if (j < total) off[u] = *queue_entry(g, q, n, j);
-            if (!(off[u] & SINGLE_RUN)) {                         // (singletons are not scheduled)
-                cls[u] = size_class(g.order[off[u]]);
-                rank[u] = atomicAdd(&lcnt[cls[u]], 1u);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < NCLASS && lcnt[threadIdx.x])
-            lbase[threadIdx.x] = atomicAdd(&g.cursor[qcls(q, threadIdx.x) + 1], lcnt[threadIdx.x]);
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < SCHED_PER_THREAD; ++u) {
-            if (!(off[u] & SINGLE_RUN)) g.work[cbase[cls[u]] + lbase[cls[u]] + rank[u]] = off[u];
-        }
-        __syncthreads();
-    }
-}
-
-void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_group_flatten, dim3(grid), dim3(BLOCK), 0, s, g, q, sched != 0);
-    if (sched) hipLaunchKernelGGL(k_group_schedule, dim3(grid), dim3(BLOCK), 0, s, g, q, sched == 1);
-}
-
 // ------------------------------------------------------------------ binned grouping
 // The netdev path groups its packets by (CT map, address pair) without an atomic per
 // packet: k_netdev_front writes each staged packet's 64-bit key (0: not staged);
@@ -812,9 +636,8 @@ void launch_group_runs(const GroupScratch &g, int q, int grid, int sched, hipStr
 // `work` and `single` lists for_each_run reads).  Keys that share the bin bits and the
 // low word merge into one group (about 2^-32 per pair of groups in a bin): a coarser
 // grouping, equally exact.
-// Measured against the node-table join it replaces (one CAS per packet into a 128 MiB
-// table at the device's atomic rate, k_group_flatten's list walks, the table memset):
-// see DESIGN.md §5.
+// Measured against the node-table join it replaced (one CAS per packet into a 128 MiB
+// table at the device's atomic rate, then list walks to flatten the groups): DESIGN.md §5.
 constexpr uint32_t SCAN_TILE = 4096;                             // entries per scan block (1024 x 4)
 constexpr uint32_t LCAP = 2048;                                  // bin entries sorted in LDS
 constexpr uint32_t GUNROLL = 8;                                  // keys loaded ahead per thread

@@ -839,28 +839,15 @@ __device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, Ct
     e.w[0] = d.x; e.w[2] = d.y; e.w[4] = f.x; e.w[6] = f.y;
 }
 
-// NT: the update of a lookup hit, written with non-temporal stores: a conntrack bucket
-// line is touched once per packet and step, and marked for early eviction it leaves the
-// L2 to the policy tables and endpoint descriptors (config-3 stage -5 %, config 5
-// unchanged; the creates' writes stay plain: non-temporal, k_ct_commit took 12 % longer)
-template <class S, bool NT = false>
+template <class S>
 __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, const CtE &e)
 {
-    if constexpr (NT) {
-        CV_G unsigned long long *h = reinterpret_cast<CV_G unsigned long long *>(ct_hot<S>(t, slot));
-        __builtin_nontemporal_store((unsigned long long)e.w[8] | (unsigned long long)e.w[9] << 32, h + 0);
-        __builtin_nontemporal_store((unsigned long long)e.w[10] | (unsigned long long)e.w[11] << 32, h + 1);
-        __builtin_nontemporal_store((unsigned long long)e.w[12] | (unsigned long long)e.w[13] << 32, h + 2);
-        __builtin_nontemporal_store((unsigned long long)e.w[0] | (unsigned long long)e.w[2] << 32, h + 3);
-        __builtin_nontemporal_store((unsigned long long)e.w[4] | (unsigned long long)e.w[6] << 32, h + 4);
-    } else {
-        CV_G uint2 *h = reinterpret_cast<CV_G uint2 *>(ct_hot<S>(t, slot));
-        h[0] = make_uint2(e.w[8], e.w[9]);
-        h[1] = make_uint2(e.w[10], e.w[11]);
-        h[2] = make_uint2(e.w[12], e.w[13]);
-        h[3] = make_uint2(e.w[0], e.w[2]);
-        h[4] = make_uint2(e.w[4], e.w[6]);
-    }
+    CV_G uint2 *h = reinterpret_cast<CV_G uint2 *>(ct_hot<S>(t, slot));
+    h[0] = make_uint2(e.w[8], e.w[9]);
+    h[1] = make_uint2(e.w[10], e.w[11]);
+    h[2] = make_uint2(e.w[12], e.w[13]);
+    h[3] = make_uint2(e.w[0], e.w[2]);
+    h[4] = make_uint2(e.w[4], e.w[6]);
 }
 
 template <class S>
@@ -1029,7 +1016,7 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
     }
     if (mon) *mon = m;
-    ct_store_hot<S, true>(ct, slot, e);
+    ct_store_hot<S>(ct, slot, e);
 }
 
 __device__ __forceinline__ uint8_t dir_flags(int dir)

@@ -245,6 +245,7 @@ struct cv_ctx {
     hipEvent_t last_ev = nullptr;              // the last batch's (or publication's) completion
     hipStream_t last_stream = nullptr;
     bool have_last = false;
+    bool force_full = false;                   // a publication was lost: compile ipcache / policies in full
     uint64_t publications = 0, full_compiles = 0;
 };
 
@@ -853,6 +854,16 @@ void mark_stream(cv_ctx *c, hipStream_t s)
     c->have_last = true;
 }
 
+// order_stream now, mark_stream on every exit (error returns included: kernels of a
+// partly submitted launch are still queued on s, and the next publication or batch on
+// another stream must wait for them)
+struct StreamScope {
+    cv_ctx *c;
+    hipStream_t s;
+    StreamScope(cv_ctx *cc, hipStream_t ss) : c(cc), s(ss) { order_stream(c, s); }
+    ~StreamScope() { mark_stream(c, s); }
+};
+
 // The queued table patches to the device, in stream s: pinned staging (a buffer whose
 // previous publication has completed, else a new one), one async copy, k_patch.
 int publish(cv_ctx *c, hipStream_t s)
@@ -894,14 +905,54 @@ int publish(cv_ctx *c, hipStream_t s)
     return 0;
 }
 
+// Queued patches hold raw addresses of the device buffers live now.  They go out before
+// any buffer is replaced (a rebuild) and on every error exit of a boundary, so no patch
+// outlives the buffer it targets (a later sync could free and reallocate it).  A
+// publication that fails drops the queue and makes the next boundary compile the
+// incremental tables in full, so the host images and the device agree again.
+int flush_patches(cv_ctx *c, hipStream_t s)
+{
+    if (c->pq.recs.empty()) return 0;
+    const int r = publish(c, s);
+    if (r) {
+        c->pq.recs.clear();
+        c->pq.words.clear();
+        c->force_full = true;
+    }
+    return r;
+}
+
+// the test hook CV_INJECT_COMPILE_FAIL=<role>: that role's next full compile fails
+bool injected_failure(int role)
+{
+    const char *e = getenv("CV_INJECT_COMPILE_FAIL");
+    return e && atoi(e) == role;
+}
+
+int sync_body(cv_ctx *c, hipStream_t stream);
+
 // Apply the agent's writes since the last batch boundary to the device tables, for a
 // batch about to run on stream s.  Incremental writes (ipcache v4 and v6 prefixes,
 // policy entries) are published in stream order (PatchQueue): no device wait.  A
 // table that has to be rebuilt (other roles, endpoint changes, a write the incremental
 // path cannot apply) replaces device buffers: only then does the boundary wait for
-// the batches already submitted.
+// the batches already submitted.  All or nothing per table: a table whose compile fails
+// keeps its old version (the next boundary retries it), and the patches already queued
+// for other tables are published against the buffers they were made for.
 int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
 {
+    const int r = sync_body(c, stream);
+    if (r) (void)flush_patches(c, stream);
+    return r;
+}
+
+int sync_body(cv_ctx *c, hipStream_t stream)
+{
+    if (c->force_full) {                       // a lost publication: recompile the incremental tables
+        c->role_version[CV_ROLE_IPCACHE] = ~0ull;
+        for (auto &e : c->eps)
+            if (MapObj *p = get(c, e.policy)) p->pol_version = ~0ull;
+    }
     bool dirty = c->eps_dirty;
     for (int r = 0; r < CV_NUM_ROLES; ++r) {
         MapObj *m = get(c, c->role[r]);
@@ -917,20 +968,24 @@ int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
     if (r) return r;
     bool drained = false;
     auto rebuild = [&]() {                     // no batch may still read a table we replace
+        int e = flush_patches(c, stream);      // (queued patches target the buffers live now)
         if (!drained) { drain(c); drained = true; }
         ++c->full_compiles;
+        return e;
     };
+    const bool full = c->force_full || getenv("CV_NO_INCREMENTAL");
     for (int role = 0; role < CV_NUM_ROLES; ++role) {
         MapObj *m = get(c, c->role[role]);
         uint64_t v = m ? m->hm->version : 0;
         if (v == c->role_version[role]) continue;
         HostMap *hm = m ? m->hm.get() : nullptr;
         if (role == CV_ROLE_IPCACHE) {
-            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_ipcache(c, hm);
+            r = full ? 1 : update_ipcache(c, hm);
             if (r == 1 && getenv("CV_REBUILD_WHY")) fprintf(stderr, "[cv] ipcache rebuild: %s\n", rebuild_why);
-            if (r == 1) { rebuild(); r = compile_ipcache(c, hm); }
+            if (r == 1 && !(r = rebuild())) r = injected_failure(role) ? -EIO : compile_ipcache(c, hm);
         } else {
-            rebuild();
+            if ((r = rebuild())) return r;
+            if (injected_failure(role)) return -EIO;
             switch (role) {
             case CV_ROLE_CIDR4_FIX: r = compile_cidr_fix(c, hm, false); break;
             case CV_ROLE_CIDR6_FIX: r = compile_cidr_fix(c, hm, true); break;
@@ -952,13 +1007,18 @@ int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
         MapObj *p = get(c, e.policy);
         if (p && p->hm->version != p->pol_version) {
             const size_t mk = c->pq.mark();
-            r = getenv("CV_NO_INCREMENTAL") ? 1 : update_policy(c, p);
-            if (r == 1) { c->pq.undo(mk); rebuild(); r = compile_policy(c, p); eps_changed = true; }
+            r = full ? 1 : update_policy(c, p);
+            if (r == 1) {
+                c->pq.undo(mk);
+                if ((r = rebuild())) return r;
+                r = compile_policy(c, p);
+                eps_changed = true;
+            }
             if (r) return r;
         }
     }
     if (eps_changed) {
-        rebuild();
+        if ((r = rebuild())) return r;
         std::vector<EpDev> ev;
         std::vector<EpHot> hot;
         std::vector<uint16_t> of(65536, 0);
@@ -992,7 +1052,8 @@ int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
         if (r) return r;
         c->eps_dirty = false;
     }
-    return publish(c, stream);
+    c->force_full = false;
+    return flush_patches(c, stream);
 }
 
 DpParams params(cv_ctx *c)
@@ -1447,6 +1508,8 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     a.budget = a.ib + n;
     a.tsum = c->adm_tsum.as<uint32_t>();
     a.hi = c->adm_win.as<uint32_t>();
+    const char *inj = getenv("CV_ADMIT_INJECT");
+    a.inject = inj ? (uint32_t)strtoul(inj, nullptr, 0) : ~0u;
     int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
     if (r) return r;
     // packets that reach no conntrack stage keep 0 (no creates, no deletes, map 0);
@@ -1457,16 +1520,20 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     uint32_t windows = 0, passes = 0;
     for (uint32_t lo = 0; lo < n; ++windows) {
         a.lo = lo;
-        uint32_t end = lo, w[3] = {n, n, n};
+        uint32_t end = lo, w[4] = {n, n, n, 0};
         for (int pass = 0;; ++pass) {
             a.pass = (uint32_t)pass;
             if ((r = launch_admission(p, bc, gs, a, s))) return r;
             ++passes;
-            hipError_t e = hipMemcpyAsync(w, a.hi, 12, hipMemcpyDeviceToHost, s);
+            hipError_t e = hipMemcpyAsync(w, a.hi, 16, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) {
                 fprintf(stderr, "[cv] admission pass at %u: %s\n", lo, hipGetErrorString(e));
                 return -EIO;
+            }
+            if (w[3]) {                                           // a stale or corrupt intent byte
+                fprintf(stderr, "[cv] admission pass at %u: intent error %#x\n", lo, w[3]);
+                return -EPROTO;
             }
             const uint32_t hi = w[0], chg = w[1], used = w[2];
             if (hi <= lo || hi > n || (pass && chg <= lo) || used <= lo) {   // (the window's first packet is exact)
@@ -1889,9 +1956,8 @@ int cv_xdp_prefilter(cv_ctx *c, const cv_batch *b, cv_out *o, void *stream)
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
     if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
-    order_stream(c, (hipStream_t)stream);
+    StreamScope scope(c, (hipStream_t)stream);
     r = launch_xdp_prefilter(params(c), to_dev(b), to_dev(o), (hipStream_t)stream);
-    mark_stream(c, (hipStream_t)stream);
     return r;
 }
 
@@ -1903,7 +1969,7 @@ int cv_policy_ingress(cv_ctx *c, int ep, const cv_batch *b, cv_out *o, void *str
     std::lock_guard<std::mutex> g(c->mu);
     if (ep < 0 || (size_t)ep >= c->eps.size() || c->eps[ep].policy < 0) return -EINVAL;
     if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
-    order_stream(c, (hipStream_t)stream);
+    StreamScope scope(c, (hipStream_t)stream);
     const DpParams p = params(c);
     const HashTable pol = get(c, c->eps[ep].policy)->pol.view;
     for (uint32_t off = 0; off < b->n && !r; off += c->chunk) {
@@ -1911,7 +1977,6 @@ int cv_policy_ingress(cv_ctx *c, int ep, const cv_batch *b, cv_out *o, void *str
         r = launch_policy_ingress(p, ep, chunk(b, off, n), chunk(o, off), (hipStream_t)stream);
         if (!r) r = launch_policy_fold(pol, (hipStream_t)stream);
     }
-    mark_stream(c, (hipStream_t)stream);
     return r;
 }
 
@@ -1923,7 +1988,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     std::lock_guard<std::mutex> g(c->mu);
     for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
     if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
-    order_stream(c, (hipStream_t)stream);
+    StreamScope scope(c, (hipStream_t)stream);
     const uint32_t cmax = std::min(b->n, c->chunk);
     if ((r = ensure_groups(c, cmax, false))) return r;
     std::set<const void *> seen;
@@ -1957,7 +2022,6 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "netdev", (hipStream_t)stream, false);
     }
-    mark_stream(c, (hipStream_t)stream);
     return 0;
 }
 
@@ -1970,7 +2034,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     std::lock_guard<std::mutex> g(c->mu);
     for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
     if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
-    order_stream(c, (hipStream_t)stream);
+    StreamScope scope(c, (hipStream_t)stream);
     const uint32_t cmax = std::min(b->n, c->chunk);
     if ((r = ensure_groups(c, cmax, true))) return r;
     std::set<const void *> seen;
@@ -1995,7 +2059,6 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream, true);
     }
-    mark_stream(c, (hipStream_t)stream);
     return 0;
 }
 

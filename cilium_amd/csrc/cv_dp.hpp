@@ -92,8 +92,15 @@ struct Admit {
     uint32_t *tsum;                    // per map and scan tile: the (sum, prefix minimum) of D - A
     uint32_t *hi;                      // [0] the first unsure packet (the window's end), [1] the first
                                        // packet whose intent changed from the previous pass, [2] the first
-                                       // packet whose intent rests on an earlier member's budget
+                                       // packet whose intent rests on an earlier member's budget, [3] error
+                                       // bits (ADMIT_ERR_*: the host fails the batch with -EPROTO)
+    uint32_t inject;                   // test hook (CV_ADMIT_INJECT): this packet's ib byte is corrupted
+                                       // after the intents (~0u: none)
 };
+// a packet's CT map is not one of the launch's (k_ct_intent), an ib byte names a map
+// index past nmaps (k_adm_apply): a stale or corrupt intent, failed loudly instead of
+// indexing past Admit's arrays
+enum : uint32_t { ADMIT_ERR_MAP = 1, ADMIT_ERR_IB = 2 };
 
 struct BatchDev {
     const uint8_t *frames;

@@ -1484,10 +1484,14 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
         const uint32_t *map = nullptr;
         bool used = false;
         const uint32_t v = ct_intent<V6>(p, b, g, x, cg, a.budget, map, used);
-        uint32_t mi = 0;
+        uint32_t mi = ~0u;
 #pragma unroll
         for (int k = 0; k < ADMIT_MAPS; ++k)
             if ((uint32_t)k < a.nmaps && a.maps[k] == map) mi = k;
+        if (mi == ~0u) {                                          // (no conntrack stage: map 0, no intent)
+            if (v) atomicOr(a.hi + 3, ADMIT_ERR_MAP);
+            mi = 0;
+        }
         const uint32_t nv = v | mi << 3 | (used ? IB_USED : 0u), old = a.ib[x];
         a.ib[x] = (uint8_t)nv;
         if (v & IB_UNSURE) atomicMin(a.hi, x);
@@ -1525,7 +1529,13 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
 
 __global__ void k_admit_init(Admit a, uint32_t n)
 {
-    if (threadIdx.x < 3 && blockIdx.x == 0) a.hi[threadIdx.x] = n;
+    if (threadIdx.x < 4 && blockIdx.x == 0) a.hi[threadIdx.x] = threadIdx.x < 3 ? n : 0u;
+}
+
+// test hook: a packet's intent byte names map 3 with one create (past nmaps when fewer)
+__global__ void k_admit_inject(Admit a)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0) a.ib[a.inject] = (uint8_t)(1u | 3u << 3);
 }
 
 // The reflected walk's two scans as one, over the monoid of (sum, prefix minimum) pairs:
@@ -1638,6 +1648,11 @@ __global__ void __launch_bounds__(1024) k_adm_apply(Admit a, uint32_t n, uint32_
     const uint32_t w = adm_ib4(a, L, j);
     const SumMin *agg = reinterpret_cast<const SumMin *>(a.tsum);
     uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {                                 // a map index past the launch's maps
+        const uint32_t v = w >> (8 * k) & 0xFFu;
+        if ((v & 7u) && ((v >> 3) & 3u) >= a.nmaps) atomicOr(a.hi + 3, ADMIT_ERR_IB);
+    }
     for (uint32_t m = 0; m < a.nmaps; ++m) {
         SumMin t{0, SM_INF};
 #pragma unroll
@@ -1674,6 +1689,7 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     g6.single = g.single6;
     g6.work = g.work6;
     hipLaunchKernelGGL(k_ct_intent<true>, grid, blk, 0, s, p, b, g6, a);
+    if (a.inject >= a.lo && a.inject < b.n) hipLaunchKernelGGL(k_admit_inject, dim3(1), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
     hipLaunchKernelGGL(k_adm_top, dim3(1), dim3(1024), 0, s, a, tiles);
     hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise one `tools/gpu_session.sh <tag> <workload> <k> pmc` run (gpurun_out/<tag>/) into committed profiles:
+"""Summarise one `tools/session.sh <tag> pmc=<workload> cal` run (gpurun_out/<tag>/) into committed profiles:
 
   profiles/<tag>/<workload>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
   profiles/<tag>/bench_<workload>.json         the bench line of that run

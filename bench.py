@@ -66,7 +66,7 @@ def lib_sha():
     return build.kernel_sha()
 
 
-def make_workload(name, n, rank, world):
+def make_workload(name, n, rank, world, flows=1 << 24):
     from cilium_amd import synth
     if name == "config2":
         return synth.config2(n)
@@ -77,7 +77,7 @@ def make_workload(name, n, rank, world):
         # whose address pair it owns, and packets of its own pairs (pre-steered by the
         # producer): conntrack sharded by address pair, config 4 of BASELINE.json
         seed = 0xC1A00003 if name == "config3" else 0xC1A00004
-        return synth.config3(n, n_flows=1 << 24, seed=seed, shard=(rank, world) if world > 1 else None)
+        return synth.config3(n, n_flows=flows, seed=seed, shard=(rank, world) if world > 1 else None)
     if name == "config5":
         return synth.config5(n)
     raise SystemExit(f"unknown workload {name}")
@@ -271,8 +271,24 @@ def main():
     ap.add_argument("--ct-room", type=int, default=None,
                     help="configs 3/4: max_entries = the preloaded entries + this many (0: a full table, every "
                          "create fails; the exact-admission regime) instead of room for every create of the run")
+    ap.add_argument("--ct-max-log2", type=int, default=None,
+                    help="configs 3/4: max_entries = 2^N (the device table: 2^N entries at 60%% slot load) instead "
+                         "of room for every create of the run; with --gc-step the run stays within it")
+    ap.add_argument("--gc-step", type=int, default=0,
+                    help="steady state: every step is this many seconds after the previous one and ctmap.GC "
+                         "(cv_ct_gc, GCFilterByTime at the step's now) runs before it, inside the timed region")
+    ap.add_argument("--flows", type=int, default=1 << 24, help="configs 3/4: conntrack flows per GPU")
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend at N > 1 (nccl = RCCL)")
+    ap.add_argument("--dump", default=None,
+                    help="test hook: every rank writes <dir>/rank<r>.npz (its packets' address-pair keys, its "
+                         "cilium_metrics before and after the all_reduce)")
     args = ap.parse_args()
 
+    # the JSON line is the only thing on stdout: everything else (libraries that print
+    # to fd 1, e.g. gloo's connection messages) goes to stderr
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -282,7 +298,7 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
     device = f"cuda:{local}"
     torch.cuda.set_device(local)
 
@@ -295,11 +311,13 @@ def main():
     stateful = name in STATEFUL
     passes = args.warmup + args.steps + 1                          # + the accounting step after the timed ones
     t0 = time.time()
-    w = make_workload(name, args.packets, rank, world)
+    w = make_workload(name, args.packets, rank, world, args.flows)
     if stateful:
         size_conntrack(name, w, passes)
         if args.ct_room is not None and name in ("config3", "config4"):
             w.maps["ct4"].max_entries = len(np.unique(w.maps["ct4"].keys, axis=0)) + args.ct_room
+        if args.ct_max_log2 is not None and name in ("config3", "config4"):
+            w.maps["ct4"].max_entries = 1 << args.ct_max_log2
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
     ctx, maps = H.product_ctx(w, device=local)
     log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")
@@ -350,7 +368,16 @@ def main():
             batches[v] = fv
         log(f"[rank {rank}] {passes} step batches built on the device ({time.time() - t0:.1f}s)")
 
+    gc_maps = [maps[k] for k in ("ct4", "ct6") if k in maps] if stateful else []
+    gc_deleted = [0]
+
+    def now_of(v):
+        return w.now + (v * args.gc_step if args.gc_step else v)
+
     def step(o, v):
+        if args.gc_step:                                           # the agent's ctmap.GC before the batch
+            for m in gc_maps:
+                gc_deleted[0] += m.ct_gc(now_of(v))
         if name == "config1":
             ctx.xdp_prefilter(frames, length, o)
         elif name == "config2":
@@ -359,10 +386,10 @@ def main():
             for k, (part, off) in enumerate(zip(dev_parts, offs)):
                 rows = len(part["length"])
                 sub = {kk: t[off:off + rows] for kk, t in o.items()}
-                ctx.lxc_egress(batches[v][k], part["length"], sub, w.now + v, src_ep=part["src_ep"],
+                ctx.lxc_egress(batches[v][k], part["length"], sub, now_of(v), src_ep=part["src_ep"],
                                flow_hash=part["flow_hash"])
         else:
-            ctx.netdev_ingress(batches[v], length, o, w.now + v, mark=mark)
+            ctx.netdev_ingress(batches[v], length, o, now_of(v), mark=mark)
 
     v = 1
     for _ in range(args.warmup):
@@ -371,6 +398,17 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] warmup done ({time.time() - t0:.1f}s)")
 
+    def slot_load():
+        """live entries / slots of every device CT map (cv_ct_slots; syncs, untimed)"""
+        r = {}
+        for k in ("ct4", "ct6"):
+            if k in maps and stateful:
+                e, d, l = maps[k].ct_slots()
+                r[k] = round(l / max(e + d + l, 1), 4)
+        return r
+
+    load_first = slot_load()
+    gc_deleted[0] = 0
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -388,6 +426,8 @@ def main():
     elapsed = time.perf_counter() - t_start
     step_ms = [a.elapsed_time(b) for a, b in ev]
     kern_ms = float(np.mean(step_ms))
+    load_last = slot_load()
+    gc_timed = gc_deleted[0]
 
     # accounting step (untimed, after the timed region, in the same regime): L(p), U(p)
     acct = dict(out)
@@ -405,12 +445,21 @@ def main():
     del acct
     log(f"[rank {rank}] accounting step done ({time.time() - t0:.1f}s)")
 
+    local_metrics = metrics_t.cpu().numpy().copy() if args.dump else None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.all_reduce(metrics_t)           # cilium_metrics: the one RCCL reduction
     torch.cuda.synchronize()
+    if args.dump:
+        from cilium_amd import shard
+        os.makedirs(args.dump, exist_ok=True)
+        fr = w.frames
+        sa = fr[:, 26:30].copy().view("<u4").ravel()
+        da = fr[:, 30:34].copy().view("<u4").ravel()
+        np.savez(os.path.join(args.dump, f"rank{rank}.npz"), pair_keys=np.unique(shard.pair_key4(sa, da)),
+                 metrics_local=local_metrics, metrics_reduced=metrics_t.cpu().numpy(), elapsed=elapsed)
 
     total_pkts = n * args.steps * world
     value = total_pkts / elapsed / 1e6
@@ -448,7 +497,7 @@ def main():
                 "packets_per_step_per_gpu": n,
                 "header_bytes": "64 (v4) / 128 (v6)" if name == "config5" else int(w.frames.shape[1]),
                 "parallelism": f"replicated tables, {world} GPU(s), batch per GPU"
-                               + (", conntrack sharded by address pair (16M flows per GPU of one node-wide set)"
+                               + (f", conntrack sharded by address pair ({args.flows} flows per GPU of one node-wide set)"
                                   if name in ("config3", "config4") and world > 1 else "")
                                + (", independent CT per rank (N separate nodes: replicas, DESIGN.md §7)"
                                   if name == "config5" and world > 1 else ""),
@@ -476,7 +525,15 @@ def main():
         }
         if stateful:
             line["config"]["ct_max_entries"] = {k: int(w.maps[k].max_entries) for k in ("ct4", "ct6") if k in w.maps}
-        print(json.dumps(line), flush=True)
+            # live entries / device slots at the first and the last timed step (a table is sized
+            # for max_entries at 60 % slot load, so the load tells how far probes walk)
+            line["config"]["ct_slot_load"] = {k: [load_first.get(k), load_last.get(k)] for k in load_first}
+            if args.gc_step:
+                line["config"]["steady_state"] = {
+                    "gc_step_s": args.gc_step, "gc_deleted_in_timed_steps": gc_timed,
+                    "how": "now advances gc_step seconds per step; ctmap.GC(GCFilterByTime, now) runs before "
+                           "every step inside the timed region"}
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
     if dist:
         dist.destroy_process_group()
     ctx.close()

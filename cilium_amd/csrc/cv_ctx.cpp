@@ -1019,6 +1019,7 @@ int sync_body(cv_ctx *c, hipStream_t stream)
     }
     if (eps_changed) {
         if ((r = rebuild())) return r;
+        if (injected_failure(CV_NUM_ROLES)) return -EIO;    // (the endpoint table)
         std::vector<EpDev> ev;
         std::vector<EpHot> hot;
         std::vector<uint16_t> of(65536, 0);

@@ -277,3 +277,46 @@ def test_config5_replicas_gloo_hip():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _c5_check(_c5_run(2, use_gpu=True), 2)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo(tmp_path):
+    """bench.py's N > 1 path, executed before any 8-GPU node runs it: two spawned ranks
+    (WORLD_SIZE=2, both on GPU 0, gloo instead of RCCL) through the init, the per-rank
+    shard draw, the barriers, the MAX-reduce of the elapsed time and the cilium_metrics
+    all_reduce.  One JSON line (rank 0) with n_gpus 2; the ranks' packets lie on
+    disjoint address pairs (config 4: conntrack sharded by pair); the reduced metrics
+    equal the sum of the two ranks' own."""
+    import json
+    import subprocess
+    import sys
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "config3",
+             "--packets", "65536", "--flows", "65536", "--steps", "2", "--warmup", "1", "--no-cpu",
+             "--dist-backend", "gloo", "--dump", str(tmp_path)],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [l for l in outs[0][0].splitlines() if l.strip()]
+    assert len(lines) == 1 and not outs[1][0].strip()
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["config"]["ct_slot_load"]["ct4"][0] > 0
+    d = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
+    assert len(np.intersect1d(d[0]["pair_keys"], d[1]["pair_keys"])) == 0
+    for r in range(2):                                              # every packet on a pair its rank owns
+        assert (d[r]["pair_keys"] % np.uint64(2) == r).all()
+    total = d[0]["metrics_local"] + d[1]["metrics_local"]
+    assert total.sum() > 0
+    assert (d[0]["metrics_reduced"] == total).all() and (d[1]["metrics_reduced"] == total).all()
+    assert d[0]["elapsed"] == d[1]["elapsed"]                       # the MAX over ranks

@@ -216,7 +216,7 @@ struct cv_ctx {
     cv_node_cfg node{};
     std::vector<Endpoint> eps;
     bool eps_dirty = true;
-    DevBuf eps_dev, ephot_dev, ep_of_lxc;
+    DevBuf eps_dev, ephot_dev, ephot6_dev, ep_of_lxc;
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
@@ -1021,7 +1021,7 @@ int sync_body(cv_ctx *c, hipStream_t stream)
         if ((r = rebuild())) return r;
         if (injected_failure(CV_NUM_ROLES)) return -EIO;    // (the endpoint table)
         std::vector<EpDev> ev;
-        std::vector<EpHot> hot;
+        std::vector<EpHot> hot, hot6;
         std::vector<uint16_t> of(65536, 0);
         for (size_t i = 0; i < c->eps.size(); ++i) {
             const Endpoint &e = c->eps[i];
@@ -1038,17 +1038,23 @@ int sync_body(cv_ctx *c, hipStream_t stream)
             for (int j = 0; j < 4; ++j) d.ipv6[j] = e.ipv6[j];
             for (int j = 0; j < 2; ++j) { d.mac[j] = e.mac[j]; d.node_mac[j] = e.node_mac[j]; }
             ev.push_back(d);
+            const uint32_t v4 = (d.ct_id & EPH_CT_ID) | (d.ipv4 ? EPH_V4 : 0u);
             EpHot h{d.policy.buckets, d.policy.vals, d.policy.aux, d.ct4.buckets, d.ct4.vals, d.ct4.live,
-                    (uint32_t)d.policy.mask, (uint32_t)d.ct4.mask, d.ipv4, d.ct_id};
+                    (uint32_t)d.policy.mask, (uint32_t)d.ct4.mask, d.seclabel, v4};
+            EpHot h6{d.policy.buckets, d.policy.vals, d.policy.aux, d.ct6.buckets, d.ct6.vals, d.ct6.live,
+                     (uint32_t)d.policy.mask, (uint32_t)d.ct6.mask, d.seclabel, v4};
             if ((d.policy.buckets && d.policy.vstride != 32) || (d.ct4.buckets && d.ct4.vstride != CT_COLD) ||
-                d.policy.mask > 0xFFFFFFFFull || d.ct4.mask > 0xFFFFFFFFull)
+                (d.ct6.buckets && d.ct6.vstride != CT_COLD) || d.policy.mask > 0xFFFFFFFFull ||
+                d.ct4.mask > 0xFFFFFFFFull || d.ct6.mask > 0xFFFFFFFFull)
                 return -EINVAL;                                   // (EpHot's fixed strides and 32-bit masks)
             hot.push_back(h);
+            hot6.push_back(h6);
             of[e.lxc_id] = (uint16_t)(i + 1);
         }
-        if (ev.empty()) { ev.push_back(EpDev{}); hot.push_back(EpHot{}); }
+        if (ev.empty()) { ev.push_back(EpDev{}); hot.push_back(EpHot{}); hot6.push_back(EpHot{}); }
         r = c->eps_dev.upload(ev.data(), ev.size() * sizeof(EpDev));
         if (!r) r = c->ephot_dev.upload(hot.data(), hot.size() * sizeof(EpHot));
+        if (!r) r = c->ephot6_dev.upload(hot6.data(), hot6.size() * sizeof(EpHot));
         if (!r) r = c->ep_of_lxc.upload(of.data(), of.size() * 2);
         if (r) return r;
         c->eps_dirty = false;
@@ -1074,6 +1080,7 @@ DpParams params(cv_ctx *c)
     p.ipc6 = c->role[CV_ROLE_IPCACHE] >= 0 ? c->ipc6.view : Lpm6{};
     p.eps = c->eps_dev.as<EpDev>();
     p.ephot = c->ephot_dev.as<EpHot>();
+    p.ephot6 = c->ephot6_dev.as<EpHot>();
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
     p.lb4 = c->role[CV_ROLE_LB4_SERVICES] >= 0 ? c->lb4.view : HashTable{};
@@ -1454,6 +1461,27 @@ uint32_t ct_plan(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t want, ui
         m->gen++;
     }
     return (uint32_t)n;
+}
+
+// How many of the next n packets (each creating at most W entries per map) surely fit
+// every map's room (no reservation); the exact live counts are read (after every batch
+// already submitted) when the running upper bound says the n may not fit.
+constexpr uint32_t SPLIT_MIN = 1u << 20;
+uint32_t ct_fit_count(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t n, uint32_t W)
+{
+    auto room = [&]() {
+        uint64_t r = ~0ull;
+        for (MapObj *m : maps) r = std::min(r, m->cap > m->live_upper ? m->cap - m->live_upper : 0);
+        return r;
+    };
+    if (room() < (uint64_t)W * n) {
+        drain(c);
+        for (MapObj *m : maps) {
+            uint64_t v = 0;
+            if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
+        }
+    }
+    return (uint32_t)std::min<uint64_t>(n, room() / W);
 }
 
 // Whether a launch of n packets (each creating at most W entries per map) surely
@@ -2005,6 +2033,12 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         // at full width; one that may reach a CT map's max_entries runs admitted
         // (run_admitted), or, with more CT maps than Admit holds, in one-packet guarded launches
         n = std::min(c->chunk, b->n - off);
+        // short of room for 2 n creates: a launch of room / 2 packets (>= 2^20, so it still
+        // fills the device) surely fits and runs at full width without the admission passes
+        // -- a right-sized table (max_entries near twice the live entries) is always short of
+        // 2 n for a 2^24-packet batch, though its real creates are a fraction of that
+        uint32_t fit_n = ct_fit_count(c, cts, n, 2);
+        if (fit_n < n && fit_n >= std::min<uint32_t>(n, SPLIT_MIN)) n = fit_n;
         const bool fits = ct_fits(c, cts, n, 2);
         if (!fits && cts.size() > (size_t)ADMIT_MAPS)
             n = ct_plan(c, cts, n, 2, (hipStream_t)stream, &p.ct_guard);

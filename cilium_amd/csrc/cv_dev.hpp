@@ -707,6 +707,58 @@ __device__ __forceinline__ int policy_egress(const HashTable &pol, uint32_t flag
     return r >= 0 ? r : DROP_POLICY;
 }
 
+// ------------------------------------------------------------------ convergent probes
+// The position stages (k_egress_ct, k_egress_deliver) run one packet per lane with every
+// lane of a wave at the same call sites (a lane without a packet, or past its drop,
+// passes want = false), so their 64-B-bucket lookups are quad probes (cv_hash.hpp): a
+// bucket read costs the texture path one line access per lane instead of four.  Q =
+// false: the same lookups lane by lane (the continuation list, whose lanes diverge).
+template <bool Q, class S>
+__device__ __forceinline__ int64_t find_q(const HashTable &t, const uint32_t *key, bool want, uint4 *st, uint32_t *ival)
+{
+    if constexpr (Q) return quad_find<S>(t, key, want, st, ival);
+    else return want ? dev_find<S>(t, key, ival) : -1;
+}
+
+// ipcache_lookup4 at /32 of a raw address (0 = no entry); counts the lookup when `want`
+template <bool Q>
+__device__ __forceinline__ uint32_t ipcache4_at(const DpParams &p, uint32_t addr_raw, bool want, Acct &a, uint4 *st)
+{
+    if (!p.ipc4.l1) return 0;
+    if (want) a.nl++;
+    if constexpr (Q) return lpm4_lookup_q(p.ipc4, bswap32(addr_raw), want, st);
+    else return want ? lpm4_lookup(p.ipc4, bswap32(addr_raw)) : 0u;
+}
+
+// policy_can_egress / policy_can_access_ingress with the convergent probes (`want` as
+// in quad_find; the result of a lane without a lookup is meaningless)
+template <bool Q>
+__device__ __forceinline__ int policy_egress_at(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t identity,
+                                                uint32_t dport_raw, uint32_t proto, Acct &a, bool want, uint4 *st)
+{
+    if constexpr (!Q) {
+        if (!want) return DROP_POLICY;
+        return policy_egress<true>(pol, flags, len, identity, dport_raw, proto, a);
+    } else {
+        if (!(flags & F_POLICY_EGRESS)) return (flags & F_DROP_ALL) ? DROP_POLICY : TC_ACT_OK;
+        if (flags & F_DROP_ALL) return DROP_POLICY;
+        const int r = policy_access_q(pol, flags, len, identity, dport_raw, proto, CT_EGRESS, a, nullptr, want, st);
+        return r >= 0 ? r : DROP_POLICY;
+    }
+}
+
+template <bool Q>
+__device__ __forceinline__ int policy_ingress_at(const HashTable &pol, uint32_t flags, uint32_t len, uint32_t src,
+                                                 uint32_t dport_raw, uint32_t proto, Acct &a, bool want, uint4 *st)
+{
+    if constexpr (!Q) {
+        if (!want) return DROP_POLICY;
+        return policy_ingress<false>(pol, flags, len, src, dport_raw, proto, a);
+    } else {
+        return policy_ingress_q(pol, flags, len, src, dport_raw, proto, a, nullptr, want, st);
+    }
+}
+
 __device__ __forceinline__ void store_out(const OutDev &o, uint32_t i, const Acct &a)
 {
     if (o.nl) o.nl[i] = (uint8_t)a.nl;
@@ -829,25 +881,66 @@ __device__ __forceinline__ CV_G uint32_t *ct_cold(const HashTable &t, int64_t sl
     return reinterpret_cast<CV_G uint32_t *>(G(t.vals) + (size_t)slot * CT_COLD);
 }
 
-// hot words <-> CtE (the hot run is 8-B aligned: KEY0, KW and KS are even)
+// hot words <-> CtE, the 40-B hot run h0..h9 = {w8 w9 w10 w11 w12 w13 w0 w2 w4 w6} moved
+// with three vector accesses (two 16-B, one 8-B) instead of five 8-B ones: the texture
+// path spends its cycles per instruction, so every access saved counts for a stage
+// bound by line accesses.  A CT6 slot's run starts 16-B aligned (bytes 48 / 128 / 208 of
+// its 256-B bucket); a CT4 slot's at byte 24 (slot 0) or 80 (slot 1) of its 128-B bucket:
+// the same three instructions for both slots, at per-lane addresses (16-B pair at A,
+// 8-B word at B) and a per-lane word order -- no branch, so lanes on either slot issue
+// the same instructions.
+template <class S>
+struct HotAt {
+    CV_G uint4 *a;             // 16-B pair start
+    CV_G uint2 *b;             // the 8-B part
+    bool lo;                   // the 8-B part holds h0, h1 (CT4 slot 0), else h8, h9
+};
+
+template <class S>
+__device__ __forceinline__ HotAt<S> hot_at(const HashTable &t, int64_t slot)
+{
+    CV_G uint32_t *h = ct_hot<S>(t, slot);
+    static_assert(S::KW == 4 || S::KW == 10, "CT4 / CT6 slots");
+    if constexpr (S::KW == 10) {                                  // CT6: 16-B aligned run
+        return HotAt<S>{reinterpret_cast<CV_G uint4 *>(h), reinterpret_cast<CV_G uint2 *>(h + 8), false};
+    } else {
+        const bool s0 = ((uint64_t)slot % S::SPB) == 0;           // run at byte 24: h0 h1 | h2-h5 | h6-h9
+        return HotAt<S>{reinterpret_cast<CV_G uint4 *>(s0 ? h + 2 : h), reinterpret_cast<CV_G uint2 *>(s0 ? h : h + 8),
+                        s0};
+    }
+}
+
 template <class S>
 __device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, CtE &e)
 {
-    const CV_G uint2 *h = reinterpret_cast<const CV_G uint2 *>(ct_hot<S>(t, slot));
-    const uint2 a = h[0], b = h[1], c = h[2], d = h[3], f = h[4];
-    e.w[8] = a.x; e.w[9] = a.y; e.w[10] = b.x; e.w[11] = b.y; e.w[12] = c.x; e.w[13] = c.y;
-    e.w[0] = d.x; e.w[2] = d.y; e.w[4] = f.x; e.w[6] = f.y;
+    const HotAt<S> q = hot_at<S>(t, slot);
+    const uint4 u = q.a[0], v = q.a[1];
+    const uint2 w = *q.b;
+    uint32_t h[10];
+    if (q.lo) {
+        h[0] = w.x; h[1] = w.y; h[2] = u.x; h[3] = u.y; h[4] = u.z; h[5] = u.w; h[6] = v.x; h[7] = v.y; h[8] = v.z; h[9] = v.w;
+    } else {
+        h[0] = u.x; h[1] = u.y; h[2] = u.z; h[3] = u.w; h[4] = v.x; h[5] = v.y; h[6] = v.z; h[7] = v.w; h[8] = w.x; h[9] = w.y;
+    }
+    e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
+    e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
 }
 
 template <class S>
 __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, const CtE &e)
 {
-    CV_G uint2 *h = reinterpret_cast<CV_G uint2 *>(ct_hot<S>(t, slot));
-    h[0] = make_uint2(e.w[8], e.w[9]);
-    h[1] = make_uint2(e.w[10], e.w[11]);
-    h[2] = make_uint2(e.w[12], e.w[13]);
-    h[3] = make_uint2(e.w[0], e.w[2]);
-    h[4] = make_uint2(e.w[4], e.w[6]);
+    const HotAt<S> q = hot_at<S>(t, slot);
+    const uint32_t h[10] = {e.w[8], e.w[9], e.w[10], e.w[11], e.w[12], e.w[13], e.w[0], e.w[2], e.w[4], e.w[6]};
+    uint4 u, v;
+    uint2 w;
+    if (q.lo) {
+        w = make_uint2(h[0], h[1]); u = make_uint4(h[2], h[3], h[4], h[5]); v = make_uint4(h[6], h[7], h[8], h[9]);
+    } else {
+        u = make_uint4(h[0], h[1], h[2], h[3]); v = make_uint4(h[4], h[5], h[6], h[7]); w = make_uint2(h[8], h[9]);
+    }
+    q.a[0] = u;
+    q.a[1] = v;
+    *q.b = w;
 }
 
 template <class S>
@@ -1673,8 +1766,24 @@ __device__ __forceinline__ EpDev ep_stage4(const DpParams &p, uint32_t idx)
     e.ct4 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, (uint32_t)CT_COLD, (uint32_t)Ct4Spec::SPB, nullptr, h.ct_live,
                       0};
     if (p.ct_guard) e.ct4.cap = G(p.eps)[idx].ct4.cap;
-    e.ipv4 = h.ipv4;
-    e.ct_id = h.ct_id;
+    e.ipv4 = (h.ct_v4 & EPH_V4) ? 1u : 0u;                        // (the stages test LXC_IPV4 for nonzero only)
+    e.ct_id = h.ct_v4 & EPH_CT_ID;
+    e.seclabel = h.seclabel;
+    return e;
+}
+
+// the same for the IPv6 stages: policy and CT6 tables, SECLABEL
+template <bool FULL>
+__device__ __forceinline__ EpDev ep_stage6(const DpParams &p, uint32_t idx)
+{
+    if constexpr (FULL) return G(p.eps)[idx];
+    const EpHot h = G(p.ephot6)[idx];
+    EpDev e{};
+    e.policy = HashTable{h.pol_buckets, h.pol_vals, h.pol_mask, 32u, (uint32_t)PolicySpec::SPB, h.pol_aux, nullptr, 0};
+    e.ct6 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, (uint32_t)CT_COLD, (uint32_t)Ct6Spec::SPB, nullptr, h.ct_live,
+                      0};
+    if (p.ct_guard) e.ct6.cap = G(p.eps)[idx].ct6.cap;
+    e.seclabel = h.seclabel;
     return e;
 }
 
@@ -1685,69 +1794,88 @@ __device__ __forceinline__ void l1_inv() { __builtin_amdgcn_fence(__ATOMIC_ACQUI
 
 // ipv4_policy (bpf_lxc.c:865-979) + tail_ipv4_policy (:981-993), LXC_NAT46 off.
 // Returns the final verdict (TC_ACT_*, drops accounted as METRIC_INGRESS) or E_TRUNC.
-template <class M, bool FRESH = true>
+// Q: every lane of the wave calls it (live = false: no packet; returns TC_ACT_OK with no
+// effect), and the policy lookup is a quad probe at a convergent call site.
+template <class M, bool FRESH = true, bool Q = false>
 __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                            uint16_t &proxy, int32_t &reason, Acct &a, M &m,
-                                           RevNatOut *rn = nullptr, bool *defer = nullptr)
+                                           RevNatOut *rn = nullptr, bool *defer = nullptr, bool live = true,
+                                           uint4 *sq = nullptr)
 {
-    int ret;
-    int verdict;
-    Tuple4 t;
+    int ret = 0;
+    Tuple4 t{};
     const bool may_defer = defer && *defer;
     if (defer) *defer = false;
     CtState st{0, 0, 0, 0, 0, 0};
-    int64_t slot;
-    bool mon = false;
-    if (s.len < 34) { ret = DROP_INVALID; goto drop; }          // revalidate_data
-    t.nexthdr = s.nexthdr;
-    t.daddr = s.daddr;
-    t.saddr = s.saddr;
-    t.dport = t.sport = 0;
-    ret = ct_lookup<false, FRESH>(ep.ct4, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a, &mon);
-    if (ret < 0) goto drop;
-    ct_out = (uint8_t)ret;
-    if (ret == CT_REPLY && st.rev_nat && !st.loopback) {         // lb4_rev_nat(REV_NAT_F_TUPLE_SADDR)
-        uint32_t na, np;
-        if (revnat4(p, st.rev_nat, na, np, a)) {
-            const int r2 = rev_map_port(s.h, t.nexthdr, np);
-            if (r2) { ret = r2; goto drop; }
-            const int r3 = l4_csum_err(s, t.nexthdr);             // __lb4_rev_nat checksum updates
-            if (r3) { ret = r3; goto drop; }
-            t.saddr = na;
-            if (rn) *rn = RevNatOut{true, false, na, np};
-        }
-    }
-    verdict = policy_ingress<false>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
-    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) {
-            ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);       // ct_delete4
-            if (!FRESH) l1_inv();
-        }
-        ret = DROP_POLICY;
-        goto drop;
-    }
-    if (skip_proxy) verdict = 0;
-    if (ret == CT_NEW) {
-        if (may_defer) {                                           // k_ct_commit writes it
-            a.nu += 2;
-            *defer = true;
+    int64_t slot = -1;
+    bool mon = false, go = live, dropped = false;
+    if (go && s.len < 34) { ret = DROP_INVALID; go = false; dropped = true; }   // revalidate_data
+    if (go) {
+        t.nexthdr = s.nexthdr;
+        t.daddr = s.daddr;
+        t.saddr = s.saddr;
+        t.dport = t.sport = 0;
+        ret = ct_lookup<false, FRESH>(ep.ct4, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a, &mon);
+        if (ret < 0) {
+            go = false;
+            dropped = true;
         } else {
-            CtState sn{0, 0, 0, 0, 0, src_label};
-            const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);
-            if (!FRESH) l1_inv();
-            if (is_err(c)) { ret = c; goto drop; }
+            ct_out = (uint8_t)ret;
+            if (ret == CT_REPLY && st.rev_nat && !st.loopback) {  // lb4_rev_nat(REV_NAT_F_TUPLE_SADDR)
+                uint32_t na, np;
+                if (revnat4(p, st.rev_nat, na, np, a)) {
+                    const int r2 = rev_map_port(s.h, t.nexthdr, np);
+                    const int r3 = r2 ? 0 : l4_csum_err(s, t.nexthdr);   // __lb4_rev_nat checksum updates
+                    if (r2 || r3) {
+                        ret = r2 ? r2 : r3;
+                        go = false;
+                        dropped = true;
+                    } else {
+                        t.saddr = na;
+                        if (rn) *rn = RevNatOut{true, false, na, np};
+                    }
+                }
+            }
         }
     }
-    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
-        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, (uint32_t)ret, mon);
-        proxy = (uint16_t)verdict;                                 // ipv4_redirect_to_host_port
-        return TC_ACT_REDIRECT;                                    // redirect(HOST_IFINDEX)
+    int verdict = policy_ingress_at<Q>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a, go, sq);
+    if (go) {
+        if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+            if (ret == CT_ESTABLISHED) {
+                ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);   // ct_delete4
+                if (!FRESH) l1_inv();
+            }
+            ret = DROP_POLICY;
+            dropped = true;
+        } else {
+            if (skip_proxy) verdict = 0;
+            if (ret == CT_NEW) {
+                if (may_defer) {                                   // k_ct_commit writes it
+                    a.nu += 2;
+                    *defer = true;
+                } else {
+                    CtState sn{0, 0, 0, 0, 0, src_label};
+                    const int c = ct_create<false>(ep.ct4, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);
+                    if (!FRESH) l1_inv();
+                    if (is_err(c)) { ret = c; dropped = true; }
+                }
+            }
+            if (!dropped) {
+                if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+                    notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX,
+                                 (uint32_t)ret, mon);
+                    proxy = (uint16_t)verdict;                     // ipv4_redirect_to_host_port
+                    return TC_ACT_REDIRECT;                        // redirect(HOST_IFINDEX)
+                }
+                m.fwd(s.len, METRIC_INGRESS);                      // send_trace_notify(TRACE_TO_LXC)
+                notify_trace(p, m, TRACE_TO_LXC, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex,
+                             (uint32_t)ret, mon);
+                return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+            }
+        }
     }
-    m.fwd(s.len, METRIC_INGRESS);                                  // send_trace_notify(TRACE_TO_LXC)
-    notify_trace(p, m, TRACE_TO_LXC, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex, (uint32_t)ret, mon);
-    return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
-drop:
+    if (!dropped) return TC_ACT_OK;                                // (no packet)
     if (ret == E_TRUNC) return ret;
     m.drop(ret, s.len, METRIC_INGRESS);                            // tail_ipv{4,6}_policy: send_drop_notify
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
@@ -1760,75 +1888,96 @@ __device__ __forceinline__ bool eq4(const uint32_t *a, const uint32_t *b)
     return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
 }
 
-// ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862)
-template <class M, bool FRESH = true>
+// ipv6_policy (bpf_lxc.c:721-849) + tail_ipv6_policy (:851-862); Q / live as ipv4_policy
+template <class M, bool FRESH = true, bool Q = false>
 __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                            bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                            uint16_t &proxy, int32_t &reason, Acct &a, M &m,
-                                           RevNat6Out *rn = nullptr, bool *defer = nullptr)
+                                           RevNat6Out *rn = nullptr, bool *defer = nullptr, bool live = true,
+                                           uint4 *sq = nullptr)
 {
-    int ret;
-    int verdict;
-    Tuple6 t;
+    int ret = 0;
+    Tuple6 t{};
     const bool may_defer = defer && *defer;
     if (defer) *defer = false;
     CtState st{0, 0, 0, 0, 0, 0};
     CtState sn{0, 0, 0, 0, 0, src_label};
-    int64_t slot;
-    bool mon = false;
-    if (s.len < 54) { ret = DROP_INVALID; goto drop; }
-    if (s.l4off < 0) { ret = s.l4off; goto drop; }              // ipv6_hdrlen error
+    int64_t slot = -1;
+    bool mon = false, go = live, dropped = false;
+    if (go && s.len < 54) { ret = DROP_INVALID; go = false; dropped = true; }
+    if (go && s.l4off < 0) { ret = s.l4off; go = false; dropped = true; }   // ipv6_hdrlen error
+    if (go) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
-    t.nexthdr = s.nexthdr;
-    t.dport = t.sport = 0;
-    sn.rev_nat = s.daddr[3] & 0xFFFFu;                           // derive reverse NAT index (:750-766)
-    if (sn.rev_nat && l4_coff6(t.nexthdr)) {                     // zeroed in the packet: L4 checksum
-        const int c = l4_csum_err6(s);
-        if (c) { ret = c; goto drop; }
-    }
-    ret = ct_lookup<true, FRESH>(ep.ct6, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a, &mon);
-    if (ret < 0) goto drop;
-    ct_out = (uint8_t)ret;
-    if (st.rev_nat) {                                            // lb6_rev_nat(.., 0)
-        uint32_t na[4], np;
-        if (revnat6(p, st.rev_nat, na, np, a)) {
-            const int r2 = rev_map_port(s.h, t.nexthdr, np);
-            if (r2) { ret = r2; goto drop; }
-            const int r3 = l4_csum_err6(s);                       // __lb6_rev_nat checksum update
-            if (r3) { ret = r3; goto drop; }
-            if (rn) { rn->valid = true; rn->np = np; for (int j = 0; j < 4; ++j) rn->na[j] = na[j]; }
+        for (int j = 0; j < 4; ++j) { t.daddr[j] = s.daddr[j]; t.saddr[j] = s.saddr[j]; }
+        t.nexthdr = s.nexthdr;
+        t.dport = t.sport = 0;
+        sn.rev_nat = s.daddr[3] & 0xFFFFu;                       // derive reverse NAT index (:750-766)
+        if (sn.rev_nat && l4_coff6(t.nexthdr)) {                 // zeroed in the packet: L4 checksum
+            const int c = l4_csum_err6(s);
+            if (c) { ret = c; go = false; dropped = true; }
         }
     }
-    verdict = policy_ingress<false>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
-    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) {
-            ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);       // ct_delete6
-            if (!FRESH) l1_inv();
-        }
-        ret = DROP_POLICY;
-        goto drop;
-    }
-    if (skip_proxy) verdict = 0;
-    if (ret == CT_NEW) {
-        if (may_defer) {
-            a.nu += 2;
-            *defer = true;
+    if (go) {
+        ret = ct_lookup<true, FRESH>(ep.ct6, t, s.h, CT_INGRESS, s.len, now, p.flags, slot, &st, a, &mon);
+        if (ret < 0) {
+            go = false;
+            dropped = true;
         } else {
-            const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);
-            if (!FRESH) l1_inv();
-            if (is_err(c)) { ret = c; goto drop; }
+            ct_out = (uint8_t)ret;
+            if (st.rev_nat) {                                    // lb6_rev_nat(.., 0)
+                uint32_t na[4], np;
+                if (revnat6(p, st.rev_nat, na, np, a)) {
+                    const int r2 = rev_map_port(s.h, t.nexthdr, np);
+                    const int r3 = r2 ? 0 : l4_csum_err6(s);      // __lb6_rev_nat checksum update
+                    if (r2 || r3) {
+                        ret = r2 ? r2 : r3;
+                        go = false;
+                        dropped = true;
+                    } else if (rn) {
+                        rn->valid = true;
+                        rn->np = np;
+                        for (int j = 0; j < 4; ++j) rn->na[j] = na[j];
+                    }
+                }
+            }
         }
     }
-    if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
-        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, (uint32_t)ret, mon);
-        proxy = (uint16_t)verdict;
-        return TC_ACT_REDIRECT;
+    int verdict = policy_ingress_at<Q>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a, go, sq);
+    if (go) {
+        if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+            if (ret == CT_ESTABLISHED) {
+                ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);   // ct_delete6
+                if (!FRESH) l1_inv();
+            }
+            ret = DROP_POLICY;
+            dropped = true;
+        } else {
+            if (skip_proxy) verdict = 0;
+            if (ret == CT_NEW) {
+                if (may_defer) {
+                    a.nu += 2;
+                    *defer = true;
+                } else {
+                    const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);
+                    if (!FRESH) l1_inv();
+                    if (is_err(c)) { ret = c; dropped = true; }
+                }
+            }
+            if (!dropped) {
+                if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+                    notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX,
+                                 (uint32_t)ret, mon);
+                    proxy = (uint16_t)verdict;
+                    return TC_ACT_REDIRECT;
+                }
+                m.fwd(s.len, METRIC_INGRESS);
+                notify_trace(p, m, TRACE_TO_LXC, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex,
+                             (uint32_t)ret, mon);
+                return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+            }
+        }
     }
-    m.fwd(s.len, METRIC_INGRESS);
-    notify_trace(p, m, TRACE_TO_LXC, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex, (uint32_t)ret, mon);
-    return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
-drop:
+    if (!dropped) return TC_ACT_OK;                                // (no packet)
     if (ret == E_TRUNC) return ret;
     m.drop(ret, s.len, METRIC_INGRESS);                            // tail_ipv{4,6}_policy: send_drop_notify
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
@@ -1837,39 +1986,43 @@ drop:
 }
 
 // handle_policy (bpf_lxc.c:1003-1038) for an IPv4 / IPv6 packet: DROP_ALL drops
-// before any conntrack work; IPv4 needs the endpoint's LXC_IPV4 program.
-template <class M, bool FRESH = true>
+// before any conntrack work; IPv4 needs the endpoint's LXC_IPV4 program.  Q / live as
+// ipv4_policy (the policy program's call is convergent: flags are uniform).
+template <class M, bool FRESH = true, bool Q = false>
 __device__ __forceinline__ int handle_policy4(const DpParams &p, const EpDev &ep, Skb4 &s, uint32_t src_label,
                                               bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                               uint16_t &proxy, int32_t &reason, Acct &a, M &m,
-                                              RevNatOut *rn = nullptr, bool *defer = nullptr)
+                                              RevNatOut *rn = nullptr, bool *defer = nullptr, bool live = true,
+                                              uint4 *sq = nullptr)
 {
-    int ret;
     if (defer && ((p.flags & F_DROP_ALL) || !ep.ipv4)) *defer = false;
-    if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ipv4)
-        return ipv4_policy<M, FRESH>(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn,
-                                     defer);
-    else ret = DROP_UNKNOWN_L3;
+    const bool run = live && !(p.flags & F_DROP_ALL) && ep.ipv4;
+    int r = TC_ACT_OK;
+    if (!(p.flags & F_DROP_ALL))
+        r = ipv4_policy<M, FRESH, Q>(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn,
+                                     defer, run, sq);
+    if (run || !live) return r;
+    const int ret = (p.flags & F_DROP_ALL) ? DROP_POLICY : DROP_UNKNOWN_L3;
     m.drop(ret, s.len, METRIC_INGRESS);                            // bpf_lxc.c:1032-1035
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
     reason = ret;
     return TC_ACT_SHOT;
 }
 
-template <class M, bool FRESH = true>
+template <class M, bool FRESH = true, bool Q = false>
 __device__ __forceinline__ int handle_policy6(const DpParams &p, const EpDev &ep, Skb6 &s, uint32_t src_label,
                                               bool skip_proxy, uint32_t ifindex, uint32_t now, uint8_t &ct_out,
                                               uint16_t &proxy, int32_t &reason, Acct &a, M &m, RevNat6Out *rn = nullptr,
-                                              bool *defer = nullptr)
+                                              bool *defer = nullptr, bool live = true, uint4 *sq = nullptr)
 {
-    int ret;
     if (defer && ((p.flags & F_DROP_ALL) || !ep.ct6.buckets)) *defer = false;
-    if (p.flags & F_DROP_ALL) ret = DROP_POLICY;
-    else if (ep.ct6.buckets)
-        return ipv6_policy<M, FRESH>(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn,
-                                     defer);
-    else ret = DROP_MISSED_TAIL_CALL;
+    const bool run = live && !(p.flags & F_DROP_ALL) && ep.ct6.buckets;
+    int r = TC_ACT_OK;
+    if (!(p.flags & F_DROP_ALL))
+        r = ipv6_policy<M, FRESH, Q>(p, ep, s, src_label, skip_proxy, ifindex, now, ct_out, proxy, reason, a, m, rn,
+                                     defer, run, sq);
+    if (run || !live) return r;
+    const int ret = (p.flags & F_DROP_ALL) ? DROP_POLICY : DROP_MISSED_TAIL_CALL;
     m.drop(ret, s.len, METRIC_INGRESS);
     notify_drop(p, m, ret, s.len, ep.lxc_id, src_label, ep.seclabel, ep.lxc_id, ifindex);
     reason = ret;

@@ -25,9 +25,10 @@ struct EpDev {                 // one endpoint program (bpf_lxc.c), its maps and
     uint32_t node_mac[2];      // NODE_MAC
 };
 
-// The fields the IPv4 conntrack stages read per packet, in one 64-B line per endpoint
-// (policy and CT4 tables; value strides are fixed: 32-B policy_entry slots, 32-B
-// ct_entry side slots), so a lane reads one line instead of three table structs' fields.
+// The fields the conntrack stages read per packet, in one 64-B line per endpoint (policy
+// and CT tables; value strides are fixed: 32-B policy_entry slots, 32-B ct_entry side
+// slots), so a lane reads one line instead of the table structs' fields scattered over
+// EpDev.  Two arrays: the CT4 map's (IPv4 stages) and the CT6 map's (IPv6 stages).
 struct EpHot {
     uint32_t *pol_buckets;
     uint8_t *pol_vals;
@@ -36,9 +37,11 @@ struct EpHot {
     uint8_t *ct_vals;
     unsigned long long *ct_live;
     uint32_t pol_mask, ct_mask;    // bucket counts - 1 (< 2^32)
-    uint32_t ipv4, ct_id;
+    uint32_t seclabel;             // SECLABEL
+    uint32_t ct_v4;                // ct_id & EPH_CT_ID (the CT4 map's group-key salt) | EPH_V4 (LXC_IPV4 set)
 };
 static_assert(sizeof(EpHot) == 64, "one line per endpoint");
+constexpr uint32_t EPH_CT_ID = 0x3FFFFFFFu, EPH_V4 = 0x80000000u;
 
 struct DpParams {              // by value as the kernel argument
     uint32_t flags;
@@ -47,7 +50,8 @@ struct DpParams {              // by value as the kernel argument
     Lpm4 cidr4_dyn, ipc4;
     Lpm6 cidr6_dyn, ipc6;
     const EpDev *eps;
-    const EpHot *ephot;        // per endpoint, same index as eps
+    const EpHot *ephot;        // per endpoint, same index as eps (CT4 map)
+    const EpHot *ephot6;       // the same with the endpoint's CT6 map
     const uint16_t *ep_of_lxc; // lxc_id -> endpoint index + 1 (0 = no program)
     unsigned long long *metrics;   // [256][4][2]
     // load balancer (lb.h): services and dense reverse-NAT tables indexed by the raw u16 key

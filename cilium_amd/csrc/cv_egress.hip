@@ -938,135 +938,148 @@ __device__ __noinline__ void eg4_frame(const DpParams &p, const BatchDev &b, con
     frame4_emit(f, in, o.frames + (size_t)i * b.stride, b.stride, r.len);
 }
 
-template <class M>
+template <bool Q, class M>
 __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                             const GroupScratch &g, uint32_t i, M &m);
-template <class M>
+                                             const GroupScratch &g, uint32_t i, bool live, M &m, uint4 *sq);
+template <bool Q, class M>
 __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                             const GroupScratch &g, uint32_t i, M &m);
+                                             const GroupScratch &g, uint32_t i, bool live, M &m, uint4 *sq);
 
 // handle_ipv4_from_lxc (bpf_lxc.c:464-649) from skip_service_lookup on.  INL: the local
 // delivery runs inline (the continuation list, whose lanes run several members of a
-// group in one launch), else it is handed to k_egress_deliver.
-template <bool INL, class M>
+// group in one launch), else it is handed to k_egress_deliver.  Q: every lane of the
+// wave calls (live = false: no packet), so the ipcache, policy and endpoint lookups are
+// quad probes at convergent call sites; `state` replaces the early exits: 0 going on,
+// 1 final (outputs written), 2 dropped with `ret`.
+template <bool INL, bool Q, class M>
 __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                            const GroupScratch &g, uint32_t i, M &m)
+                                            const GroupScratch &g, uint32_t i, bool live, M &m, uint4 *sq)
 {
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    Eg4 x;
-    uint32_t epi, fl;
-    eg4_unpack(g.est + (size_t)i * 4, b.stride, x, epi, fl);
-    // the source endpoint's tables from its EpHot line (table constants folded: fewer
-    // live registers); the full EpDev where the event records need its constants
-    const EpDev ep = eg_src4<M::EV>(p, epi);
-    m.pkt = b.base + i;
-    m.hash = b.hash ? b.hash[i] : 0u;
-    m.src_id = ep.lxc_id;
-    m.src_label = ep.seclabel;
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    Eg4 x{};
+    uint32_t epi = 0, fl = 0;
+    EpDev ep{};
+    Acct a{0, 0, m.pc};
+    if (live) {
+        eg4_unpack(g.est + (size_t)i * 4, b.stride, x, epi, fl);
+        // the source endpoint's tables and SECLABEL from its EpHot line; the full EpDev
+        // where the event records need its constants
+        ep = ep_stage4<M::EV>(p, epi);
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+        m.src_id = ep.lxc_id;
+        m.src_label = ep.seclabel;
+        a.nl = o.nl ? o.nl[i] : 0u;
+        a.nu = o.nu ? o.nu[i] : 0u;
+    }
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Skb4 &s = x.s;
     Tuple4 &t = x.t;
     CtState st{0, 0, 0, 0, 0, 0};
-    int64_t slot;
+    int64_t slot = -1;
     const uint32_t orig_dip = t.daddr;
-    // the ipcache lookup of orig_dip issued ahead of the conntrack probes (independent
-    // reads of a read-only table); the endpoint lookup of daddr waits for its use (issued
-    // early, its 64-B bucket stayed in registers across the probes: no faster, and it
-    // spilled)
-    Lpm4Pending ipq;
-    if (p.ipc4.l1) ipq = lpm4_begin(p.ipc4, bswap32(orig_dip));
     bool mon = false;
-    int ret = ct_lookup<false, EGF>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
-    int verdict;
-    uint32_t iv;
-    bool lxc_hit = false;
-    int64_t lxc_slot = -1;
-    RevNatOut rn1{false, false, 0, 0}, rn2{false, false, 0, 0};                 // reverse NATs applied (output frames)
-    if (ret < 0) goto drop;
-    res.ct = (uint8_t)ret;
-    {                                                             // destination category (:482-494)
-        uint32_t lab = 0;
-        if (p.ipc4.l1) { a.nl++; lab = lpm4_end(ipq, p.ipc4); }
+    int ret = live ? ct_lookup<false, EGF>(ep.ct4, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon) : 0;
+    int state = !live ? 1 : ret < 0 ? 2 : 0;
+    RevNatOut rn1{false, false, 0, 0}, rn2{false, false, 0, 0};   // reverse NATs applied (output frames)
+    // destination category (:482-494): the ipcache identity of the original daddr
+    const uint32_t lab = ipcache4_at<Q>(p, orig_dip, state == 0, a, sq);
+    if (state == 0) {
+        res.ct = (uint8_t)ret;
         res.dst = lab ? lab : ((orig_dip & p.v4_cluster_mask) == p.v4_cluster_range ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = policy_egress(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
-    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) {
-            ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);       // ct_delete4
+    const int verdict = policy_egress_at<Q>(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a, state == 0, sq);
+    if (state == 0) {
+        if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+            if (ret == CT_ESTABLISHED) {
+                ct_kill<Ct4Spec>(ep.ct4, slot, a, p.ct_guard);   // ct_delete4
+                eg_changed();
+            }
+            ret = verdict;
+            state = 2;
+        } else if (ret == CT_NEW) {
+            x.stn.src_sec_id = ep.seclabel;
+            const bool defer = g.ifx[i] & BIT_NAT_DEFER;
+            const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer, true);
             eg_changed();
+            if (defer && c != DROP_CT_CREATE_FAILED) g.ifx[i] |= BIT_NAT_DONE;
+            if (is_err(c)) { ret = c; state = 2; }
+        } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
+            uint32_t na, np;
+            if (revnat4(p, st.rev_nat, na, np, a)) {
+                const int r2 = rev_map_port(s.h, t.nexthdr, np);
+                const int r3 = r2 ? 0 : l4_csum_err(s, t.nexthdr);   // __lb4_rev_nat checksum updates
+                if (r2 || r3) {
+                    ret = r2 ? r2 : r3;
+                    state = 2;
+                } else {
+                    rn1 = RevNatOut{true, st.loopback != 0, na, np};
+                    const uint32_t old_sip = s.saddr;
+                    if (st.loopback) s.daddr = old_sip;
+                    s.saddr = na;
+                }
+            }
         }
-        ret = verdict;
-        goto drop;
-    }
-    if (ret == CT_NEW) {
-        x.stn.src_sec_id = ep.seclabel;
-        const bool defer = g.ifx[i] & BIT_NAT_DEFER;
-        const int c = ct_create<false>(ep.ct4, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, defer, true);
-        eg_changed();
-        if (defer && c != DROP_CT_CREATE_FAILED) g.ifx[i] |= BIT_NAT_DONE;
-        if (is_err(c)) { ret = c; goto drop; }
-    } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb4_rev_nat(.., 0)
-        uint32_t na, np;
-        if (revnat4(p, st.rev_nat, na, np, a)) {
-            const int r2 = rev_map_port(s.h, t.nexthdr, np);
-            if (r2) { ret = r2; goto drop; }
-            const int r3 = l4_csum_err(s, t.nexthdr);             // __lb4_rev_nat checksum updates
-            if (r3) { ret = r3; goto drop; }
-            rn1 = RevNatOut{true, st.loopback != 0, na, np};
-            const uint32_t old_sip = s.saddr;
-            if (st.loopback) s.daddr = old_sip;
-            s.saddr = na;
+        if (state == 0 && verdict > 0) {                          // ipv4_redirect_to_host_port + ipv4_l3
+            notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
+            res.proxy = (uint16_t)verdict;
+            if (s.ttl <= 1) {
+                ret = DROP_INVALID;
+                state = 2;
+            } else {
+                res.ret = TC_ACT_REDIRECT;
+                eg_final(o, i, res, a);
+                state = 1;
+            }
         }
     }
-    if (verdict > 0) {                                            // ipv4_redirect_to_host_port + ipv4_l3
-        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
-        res.proxy = (uint16_t)verdict;
-        if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }
-        res.ret = TC_ACT_REDIRECT;
-        eg_final(o, i, res, a);
-        return;
-    }
+    uint32_t iv = 0;                                              // lookup_ip4_endpoint(ip4)
+    int64_t lxc_slot = -1;
     if (p.lxc4.buckets) {
-        a.nl++;                                                   // lookup_ip4_endpoint(ip4)
-        lxc_slot = dev_find<LxcV4Spec>(p.lxc4, &s.daddr, &iv);
-        lxc_hit = lxc_slot >= 0;
+        if (state == 0) a.nl++;
+        lxc_slot = find_q<Q, LxcV4Spec>(p.lxc4, &s.daddr, state == 0, sq, &iv);
     }
-    if (lxc_hit) {
-        if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }        // ipv4_l3 -> ipv4_dec_ttl
-        m.fwd(s.len, METRIC_EGRESS);                              // TRACE_TO_HOST / ipv4_local_delivery
-        if (iv & (1u << 16)) {                                    // to_host
-            res.ret = TC_ACT_REDIRECT;
-            notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
-            if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+    if (state == 0) {
+        if (s.ttl <= 1) {                                         // ipv4_l3 -> ipv4_dec_ttl
+            ret = DROP_INVALID;
+            state = 2;
+        } else if (lxc_slot >= 0) {
+            m.fwd(s.len, METRIC_EGRESS);                          // TRACE_TO_HOST / ipv4_local_delivery
+            const uint32_t e2 = (iv & (1u << 16)) ? 0u : p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
+            if (iv & (1u << 16)) {                                // to_host
+                res.ret = TC_ACT_REDIRECT;
+                notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
+                if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+                eg_final(o, i, res, a);
+            } else if (!e2) {
+                ret = DROP_MISSED_TAIL_CALL;
+                state = 2;
+            } else {
+                // ipv4_local_delivery -> the destination's handle_policy: k_egress_deliver
+                uint32_t w4, chk;
+                uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+                d[0] = skb4_pack(s, w4, chk);
+                d[1] = make_uint4(w4, chk | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24,
+                                  (e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u) |
+                                      (rn1.loopback ? 1u << 26 : 0u),
+                                  ep.seclabel);
+                d[2] = make_uint4(ifindex_of(m, p.lxc4, lxc_slot, iv), res.dst, (uint32_t)lxc_slot, rn1.na);
+                if (M::EV) d[3] = make_uint4(rn1.np, 0, 0, 0);
+                if constexpr (INL) deliver4_one<false>(p, b, now, o, g, i, true, m, sq);
+                else del_list(g, false, i);
+            }
+        } else {                                                  // pass_to_stack: ipv4_l3
+            m.fwd(s.len, METRIC_EGRESS);                          // TRACE_TO_STACK
+            notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
+            res.ret = TC_ACT_OK;
+            if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
             eg_final(o, i, res, a);
-            return;
         }
-        const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
-        if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
-        // ipv4_local_delivery -> the destination's handle_policy: k_egress_deliver
-        uint32_t w4, chk;
-        uint4 *d = g.del + (size_t)i * DEL_SLOTS;
-        d[0] = skb4_pack(s, w4, chk);
-        d[1] = make_uint4(w4, chk | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24,
-                          (e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u) | (rn1.loopback ? 1u << 26 : 0u),
-                          ep.seclabel);
-        d[2] = make_uint4(ifindex_of(m, p.lxc4, lxc_slot, iv), res.dst, (uint32_t)lxc_slot, rn1.na);
-        if (M::EV) d[3] = make_uint4(rn1.np, 0, 0, 0);
-        if constexpr (INL) deliver4_one(p, b, now, o, g, i, m);
-        else del_list(g, false, i);
-        return;
     }
-    if (s.ttl <= 1) { ret = DROP_INVALID; goto drop; }            // pass_to_stack: ipv4_l3
-    m.fwd(s.len, METRIC_EGRESS);                                  // TRACE_TO_STACK
-    notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
-    res.ret = TC_ACT_OK;
-    if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
-    eg_final(o, i, res, a);
-    return;
-drop:
-    eg_drop(p, res, ret, s.len, m);
-    eg_final(o, i, res, a);
+    if (state == 2) {
+        eg_drop(p, res, ret, s.len, m);
+        eg_final(o, i, res, a);
+    }
 }
 
 // The forwarded IPv6 frame of ipv6_l3_from_lxc: lb6_xlate (the LB stage's target and
@@ -1102,123 +1115,140 @@ __device__ __noinline__ void eg6_frame(const DpParams &p, const BatchDev &b, con
     frame6_emit(f, in, o.frames + (size_t)i * b.stride, b.stride);
 }
 
-// ipv6_l3_from_lxc (bpf_lxc.c:133-352) from skip_service_lookup on
-template <bool INL, class M>
+// ipv6_l3_from_lxc (bpf_lxc.c:133-352) from skip_service_lookup on; Q / live / state as
+// egress4_one (here the policy lookup is the quad probe: the IPv6 endpoint and ipcache
+// tables have 128-B buckets, probed tag-first per lane)
+template <bool INL, bool Q, class M>
 __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                            const GroupScratch &g, uint32_t i, M &m)
+                                            const GroupScratch &g, uint32_t i, bool live, M &m, uint4 *sq)
 {
     const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    Eg6 x;
-    uint32_t epi;
-    eg6_unpack(g.est + (size_t)i * 4, b.stride, x, epi);
-    const EpDev ep = G(p.eps)[epi];
-    m.pkt = b.base + i;
-    m.hash = b.hash ? b.hash[i] : 0u;
-    m.src_id = ep.lxc_id;
-    m.src_label = ep.seclabel;
-    Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    Eg6 x{};
+    uint32_t epi = 0;
+    EpDev ep{};
+    Acct a{0, 0, m.pc};
+    if (live) {
+        eg6_unpack(g.est + (size_t)i * 4, b.stride, x, epi);
+        ep = ep_stage6<M::EV>(p, epi);
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+        m.src_id = ep.lxc_id;
+        m.src_label = ep.seclabel;
+        a.nl = o.nl ? o.nl[i] : 0u;
+        a.nu = o.nu ? o.nu[i] : 0u;
+    }
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Skb6 &s = x.s;
     Tuple6 &t = x.t;
     CtState st{0, 0, 0, 0, 0, 0};
-    int64_t slot;
+    int64_t slot = -1;
     const uint32_t orig_dip[4] = {t.daddr[0], t.daddr[1], t.daddr[2], t.daddr[3]};
     bool mon = false;
-    int ret = ct_lookup<true, EGF, true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon);
-    int verdict;
-    uint32_t iv;
-    bool lxc_hit = false;
-    int64_t lxc_slot = -1;
+    int ret = live ? ct_lookup<true, EGF, true>(ep.ct6, t, s.h, CT_EGRESS, s.len, now, p.flags, slot, &st, a, &mon) : 0;
+    int state = !live ? 1 : ret < 0 ? 2 : 0;
     RevNat6Out rn1, rn2;                                          // reverse NATs applied (output frames)
     rn1.valid = rn2.valid = false;
-    if (ret < 0) goto drop;
-    res.ct = (uint8_t)ret;
-    {
+    if (state == 0) {
+        res.ct = (uint8_t)ret;
         const uint32_t lab = ipcache6(p, orig_dip, a);
         res.dst = lab ? lab
                       : ((s.daddr[0] == p.router6[0] && s.daddr[1] == p.router6[1]) ? CLUSTER_ID : WORLD_ID);
     }
-    verdict = policy_egress<false>(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a);
-    if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
-        if (ret == CT_ESTABLISHED) {
-            ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);       // ct_delete6
+    const int verdict = policy_egress_at<Q>(ep.policy, p.flags, s.len, res.dst, t.dport, t.nexthdr, a, state == 0, sq);
+    if (state == 0) {
+        if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+            if (ret == CT_ESTABLISHED) {
+                ct_kill<Ct6Spec>(ep.ct6, slot, a, p.ct_guard);   // ct_delete6
+                eg_changed();
+            }
+            ret = verdict;
+            state = 2;
+        } else if (ret == CT_NEW) {
+            x.stn.src_sec_id = ep.seclabel;
+            const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, false, true);
             eg_changed();
-        }
-        ret = verdict;
-        goto drop;
-    }
-    if (ret == CT_NEW) {
-        x.stn.src_sec_id = ep.seclabel;
-        const int c = ct_create<true>(ep.ct6, t, s.len, CT_EGRESS, x.stn, now, a, p.ct_guard, false, true);
-        eg_changed();
-        if (is_err(c)) { ret = c; goto drop; }
-    } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
-        uint32_t na[4], np;
-        if (revnat6(p, st.rev_nat, na, np, a)) {
-            const int r2 = rev_map_port(s.h, t.nexthdr, np);
-            if (r2) { ret = r2; goto drop; }
-            const int r3 = l4_csum_err6(s);                       // __lb6_rev_nat checksum update
-            if (r3) { ret = r3; goto drop; }
-            rn1.valid = true;
-            rn1.np = np;
+            if (is_err(c)) { ret = c; state = 2; }
+        } else if ((ret == CT_REPLY || ret == CT_RELATED) && st.rev_nat) {   // lb6_rev_nat(.., 0)
+            uint32_t na[4], np;
+            if (revnat6(p, st.rev_nat, na, np, a)) {
+                const int r2 = rev_map_port(s.h, t.nexthdr, np);
+                const int r3 = r2 ? 0 : l4_csum_err6(s);          // __lb6_rev_nat checksum update
+                if (r2 || r3) {
+                    ret = r2 ? r2 : r3;
+                    state = 2;
+                } else {
+                    rn1.valid = true;
+                    rn1.np = np;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { s.saddr[j] = na[j]; rn1.na[j] = na[j]; }
+                    for (int j = 0; j < 4; ++j) { s.saddr[j] = na[j]; rn1.na[j] = na[j]; }
+                }
+            }
+        }
+        if (state == 0 && verdict > 0) {                          // ipv6_redirect_to_host_port + ipv6_l3
+            notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
+            res.proxy = (uint16_t)verdict;
+            if (s.hoplimit <= 1) {
+                ret = E_PUNT;
+                state = 2;
+            } else {
+                res.ret = TC_ACT_REDIRECT;
+                eg_final(o, i, res, a);
+                state = 1;
+            }
         }
     }
-    if (verdict > 0) {                                            // ipv6_redirect_to_host_port + ipv6_l3
-        notify_trace(p, m, TRACE_TO_PROXY, s.len, ep.lxc_id, ep.seclabel, 0, 0, HOST_IFINDEX, res.ct, mon);
-        res.proxy = (uint16_t)verdict;
-        if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
-        res.ret = TC_ACT_REDIRECT;
-        eg_final(o, i, res, a);
-        return;
-    }
-    if (p.lxc6.buckets) {                                         // lookup_ip6_endpoint (the daddr is unchanged)
-        a.nl++;
-        lxc_slot = dev_find<LxcV6Spec>(p.lxc6, s.daddr, &iv);
-        lxc_hit = lxc_slot >= 0;
-    }
-    if (lxc_hit) {
-        if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }         // icmp6_send_time_exceeded
-        m.fwd(s.len, METRIC_EGRESS);
-        if (iv & (1u << 16)) {                                    // to_host
-            res.ret = TC_ACT_REDIRECT;
-            notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
-            if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+    if (state == 0) {
+        uint32_t iv = 0;
+        int64_t lxc_slot = -1;
+        if (p.lxc6.buckets) {                                     // lookup_ip6_endpoint (the daddr is unchanged)
+            a.nl++;
+            lxc_slot = dev_find<LxcV6Spec>(p.lxc6, s.daddr, &iv);
+        }
+        if (s.hoplimit <= 1) {                                    // icmp6_send_time_exceeded / ipv6_l3
+            ret = E_PUNT;
+            state = 2;
+        } else if (lxc_slot >= 0) {
+            m.fwd(s.len, METRIC_EGRESS);
+            const uint32_t e2 = (iv & (1u << 16)) ? 0u : p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
+            if (iv & (1u << 16)) {                                // to_host
+                res.ret = TC_ACT_REDIRECT;
+                notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
+                if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
+                eg_final(o, i, res, a);
+            } else if (!e2) {
+                ret = DROP_MISSED_TAIL_CALL;
+                state = 2;
+            } else {
+                // ipv6_local_delivery -> the destination's handle_policy: k_egress_deliver
+                uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+                d[0] = make_uint4(s.saddr[0], s.saddr[1], s.saddr[2], s.saddr[3]);
+                d[1] = make_uint4(s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3]);
+                d[2] = make_uint4(s.len, (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 |
+                                             ((uint32_t)s.l4off & 0xFFu) << 24,
+                                  (s.h.p0 & 0xFFFFu) | s.h.p2 << 16,
+                                  chk2(s.h.c1) | chk2(s.h.c14) << 2 | chk2(s.h.c4) << 4 | chk2(s.h.c2a) << 6 |
+                                      chk2(s.h.c2b) << 8 | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24);
+                d[3] = make_uint4((e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u), ep.seclabel,
+                                  ifindex_of(m, p.lxc6, lxc_slot, iv), res.dst);
+                if (M::EV) {
+                    d[4] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
+                    d[5] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
+                }
+                if constexpr (INL) deliver6_one<false>(p, b, now, o, g, i, true, m, sq);
+                else del_list(g, true, i);
+            }
+        } else {
+            m.fwd(s.len, METRIC_EGRESS);
+            notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
+            res.ret = TC_ACT_OK;
+            if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
             eg_final(o, i, res, a);
-            return;
         }
-        const uint32_t e2 = p.ep_of_lxc ? p.ep_of_lxc[iv & 0xFFFFu] : 0u;
-        if (!e2) { ret = DROP_MISSED_TAIL_CALL; goto drop; }
-        // ipv6_local_delivery -> the destination's handle_policy: k_egress_deliver
-        uint4 *d = g.del + (size_t)i * DEL_SLOTS;
-        d[0] = make_uint4(s.saddr[0], s.saddr[1], s.saddr[2], s.saddr[3]);
-        d[1] = make_uint4(s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3]);
-        d[2] = make_uint4(s.len, (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 |
-                                     ((uint32_t)s.l4off & 0xFFu) << 24,
-                          (s.h.p0 & 0xFFFFu) | s.h.p2 << 16,
-                          chk2(s.h.c1) | chk2(s.h.c14) << 2 | chk2(s.h.c4) << 4 | chk2(s.h.c2a) << 6 | chk2(s.h.c2b) << 8 |
-                              (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24);
-        d[3] = make_uint4((e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u), ep.seclabel,
-                          ifindex_of(m, p.lxc6, lxc_slot, iv), res.dst);
-        if (M::EV) {
-            d[4] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
-            d[5] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
-        }
-        if constexpr (INL) deliver6_one(p, b, now, o, g, i, m);
-        else del_list(g, true, i);
-        return;
     }
-    if (s.hoplimit <= 1) { ret = E_PUNT; goto drop; }
-    m.fwd(s.len, METRIC_EGRESS);
-    notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
-    res.ret = TC_ACT_OK;
-    if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
-    eg_final(o, i, res, a);
-    return;
-drop:
-    eg_drop(p, res, ret, s.len, m);
-    eg_final(o, i, res, a);
+    if (state == 2) {
+        eg_drop(p, res, ret, s.len, m);
+        eg_final(o, i, res, a);
+    }
 }
 
 // ================================================================== local delivery
@@ -1231,35 +1261,47 @@ drop:
 // each packet whole; the next position's launch follows both.  The split keeps the
 // delivery path out of the egress kernel's registers (it spilled over a hundred VGPRs
 // to scratch) and runs the deliveries with every lane on the same path.
-template <class M>
+template <bool Q, class M>
 __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                             const GroupScratch &g, uint32_t i, M &m)
+                                             const GroupScratch &g, uint32_t i, bool live, M &m, uint4 *sq)
 {
-    const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
-    const uint4 d0 = d[0], d1 = d[1], d2 = d[2];
+    uint4 d0{}, d1{}, d2{};
+    if (live) {
+        const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+        d0 = d[0]; d1 = d[1]; d2 = d[2];
+    }
     Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
     Acct a{(d1.y >> 16) & 0xFFu, d1.y >> 24, m.pc};
     EgOut res{TC_ACT_OK, 0, d2.y, (uint8_t)(d1.z >> 16), 0};
-    m.pkt = b.base + i;
-    m.hash = b.hash ? b.hash[i] : 0u;
+    if (live) {
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+    }
     RevNatOut rn2{false, false, 0, 0};
     uint8_t ct2 = CT_NONE;
-    res.ret = handle_policy4<M, EGF>(p, G(p.eps)[d1.z & 0xFFFFu], s, d1.w, false, d2.x, now, ct2, res.proxy,
-                                     res.reason, a, m, &rn2);
+    // the destination's tables from its EpHot line (the full EpDev for the event records)
+    const EpDev ep = live ? ep_stage4<M::EV>(p, d1.z & 0xFFFFu) : EpDev{};
+    res.ret = handle_policy4<M, EGF, Q>(p, ep, s, d1.w, false, d2.x, now, ct2, res.proxy, res.reason, a, m, &rn2,
+                                        nullptr, live, sq);
+    if (!live) return;
     if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy) {
         const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-        const RevNatOut rn1{(d1.z >> 25) & 1u ? true : false, (d1.z >> 26) & 1u ? true : false, d2.w, d[3].x};
+        const RevNatOut rn1{(d1.z >> 25) & 1u ? true : false, (d1.z >> 26) & 1u ? true : false, d2.w,
+                            g.del[(size_t)i * DEL_SLOTS + 3].x};
         eg4_frame(p, b, o, eg, i, G(p.eps)[eg[1] & 0xFFFFu], rn1, 2, (int64_t)d2.z, rn2);   // ipv4_local_delivery
     }
     eg_final(o, i, res, a);
 }
 
-template <class M>
+template <bool Q, class M>
 __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
-                                             const GroupScratch &g, uint32_t i, M &m)
+                                             const GroupScratch &g, uint32_t i, bool live, M &m, uint4 *sq)
 {
-    const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
-    const uint4 d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+    uint4 d0{}, d1{}, d2{}, d3{};
+    if (live) {
+        const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+        d0 = d[0]; d1 = d[1]; d2 = d[2]; d3 = d[3];
+    }
     Skb6 s;
     s.saddr[0] = d0.x; s.saddr[1] = d0.y; s.saddr[2] = d0.z; s.saddr[3] = d0.w;
     s.daddr[0] = d1.x; s.daddr[1] = d1.y; s.daddr[2] = d1.z; s.daddr[3] = d1.w;
@@ -1279,14 +1321,19 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     s.h.c2b = unchk2((d2.w >> 8) & 3u);
     Acct a{(d2.w >> 16) & 0xFFu, d2.w >> 24, m.pc};
     EgOut res{TC_ACT_OK, 0, d3.w, (uint8_t)(d3.x >> 16), 0};
-    m.pkt = b.base + i;
-    m.hash = b.hash ? b.hash[i] : 0u;
+    if (live) {
+        m.pkt = b.base + i;
+        m.hash = b.hash ? b.hash[i] : 0u;
+    }
     RevNat6Out rn2;
     rn2.valid = false;
     uint8_t ct2 = CT_NONE;
-    res.ret = handle_policy6<M, EGF>(p, G(p.eps)[d3.x & 0xFFFFu], s, d3.y, false, d3.z, now, ct2, res.proxy,
-                                     res.reason, a, m, &rn2);
+    const EpDev ep = live ? ep_stage6<M::EV>(p, d3.x & 0xFFFFu) : EpDev{};
+    res.ret = handle_policy6<M, EGF, Q>(p, ep, s, d3.y, false, d3.z, now, ct2, res.proxy, res.reason, a, m, &rn2,
+                                        nullptr, live, sq);
+    if (!live) return;
     if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy) {
+        const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
         const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         const uint4 d4 = d[4], d5 = d[5];
         RevNat6Out rn1;
@@ -1298,22 +1345,37 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     eg_final(o, i, res, a);
 }
 
+// the wave-uniform loop over the list of the deliveries a position handed over: every
+// lane of a wave calls fn the same number of times (live = false past the end)
+template <class F>
+__device__ __forceinline__ void for_each_wave(uint32_t total, F &&fn)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t j0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); j0 < total; j0 += stride) {
+        const uint32_t j = j0 + lane;
+        fn(j, j < total);
+    }
+}
+
 template <bool V6, bool EV>
 __global__ void __launch_bounds__(BLOCK) k_egress_deliver(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
+    __shared__ uint4 stage[BLOCK / 64][256];                      // quad probes
+    uint4 *sq = stage[threadIdx.x >> 6];
     using M = MetT<EV>;
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
     const uint32_t total = g.cursor[del_ctr(V6, g.pos)];
-    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < total; j += gridDim.x * BLOCK) {
-        const uint32_t i = g.single[j];
-        if constexpr (V6) deliver6_one(p, b, now, o, g, i, m);
-        else deliver4_one(p, b, now, o, g, i, m);
-    }
+    for_each_wave(total, [&](uint32_t j, bool live) {
+        const uint32_t i = live ? g.single[j] : 0u;
+        if constexpr (V6) deliver6_one<true>(p, b, now, o, g, i, live, m, sq);
+        else deliver4_one<true>(p, b, now, o, g, i, live, m, sq);
+    });
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
 }
@@ -1333,16 +1395,32 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
+    __shared__ uint4 stage[BLOCK / 64][256];                      // quad probes
+    uint4 *sq = stage[threadIdx.x >> 6];
     using M = MetT<EV>;
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    // member `pos` of every group, in packet order (one launch per position)
-    for_each_at(g, V6 ? Q_CT6 : Q_CT4, pos, [&](uint32_t x) {
-        if constexpr (V6) egress6_one<INL>(p, b, now, o, g, x, m);
-        else egress4_one<INL>(p, b, now, o, g, x, m);
-    });
+    const int q = V6 ? Q_CT6 : Q_CT4;
+    if constexpr (INL) {
+        // the continuation list: a lane runs the members of its group from `pos` on, lane
+        // by lane (per-lane probes)
+        for_each_at(g, q, pos, [&](uint32_t x) {
+            if constexpr (V6) egress6_one<true, false>(p, b, now, o, g, x, true, m, sq);
+            else egress4_one<true, false>(p, b, now, o, g, x, true, m, sq);
+        });
+    } else {
+        // member `pos` of every group, in packet order (one launch per position); every
+        // lane of a wave at the same call sites (quad probes)
+        uint32_t base = 0;
+        for (uint32_t l = 0; l < pos; ++l) base += g.cursor[qcls(q, l)];
+        for_each_wave(g.cursor[qcls(q, pos)], [&](uint32_t j, bool live) {
+            const uint32_t x = live ? g.work[base + j] : 0u;
+            if constexpr (V6) egress6_one<false, true>(p, b, now, o, g, x, live, m, sq);
+            else egress4_one<false, true>(p, b, now, o, g, x, live, m, sq);
+        });
+    }
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
 }

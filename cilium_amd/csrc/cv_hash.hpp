@@ -403,6 +403,7 @@ __device__ __forceinline__ int64_t quad_find(const HashTable &t, const uint32_t 
     const uint64_t h = home_hash<S>(key, tag);
     const uint64_t b = h & t.mask;
     const uint32_t *bw = (want && t.buckets) ? t.buckets + b * S::BW : nullptr;
+    if (!__ballot(bw != nullptr)) return -1;                      // (wave-uniform: no lane looks up)
     uint32_t w[16];
     quad_load64(bw, st, w);
     if (!bw) return -1;

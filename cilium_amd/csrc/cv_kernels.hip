@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, 
         // groups by it
         unsigned long long gkey = 0;
         if (staged) {
-            const uint32_t ct_id = G(p.ephot)[smeta & 0xFFFFu].ct_id;
+            const uint32_t ct_id = G(p.ephot)[smeta & 0xFFFFu].ct_v4 & EPH_CT_ID;
             gkey = (pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ct_id << 17) & ~3ull) | 2ull;
         } else if (v6stage) {
             const EpDev ep = G(p.eps)[smeta & 0xFFFFu];

@@ -3,7 +3,7 @@
 # and the session stops at the first failure (no retries).
 #   usage: bash tools/session.sh <tag> <step>...
 # steps (outputs under gpurun_out/<tag>/):
-#   tests[=<pytest -k expr>]      the -m gpu tests                       pytest.log
+#   tests[=<pytest -k expr>]      the -m gpu tests (commas for spaces)   pytest.log
 #   bench=<workload>[,<args>]     one bench line (args: comma-separated)  bench_<workload>.json
 #   stats=<workload>              rocprofv3 kernel trace + stats          <workload>_kernel_stats.csv
 #   pmc=<workload>                FETCH / WRITE / TCC hit-miss passes     pmc<k>_<workload>/
@@ -37,7 +37,7 @@ for st in "$@"; do
   IFS=, read -r -a A <<< "$arg"
   case $name in
   tests)
-    K=(); [ -n "$arg" ] && K=(-k "$arg")
+    K=(); [ -n "$arg" ] && K=(-k "${arg//,/ }")   # (commas stand for spaces)
     run 900 "$OUT/pytest.log" python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${K[@]}"
     grep -cE "PASSED" "$OUT/pytest.log" >&2 ;;
   bench)

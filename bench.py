@@ -66,7 +66,7 @@ def lib_sha():
     return build.kernel_sha()
 
 
-def make_workload(name, n, rank, world, flows=1 << 24):
+def make_workload(name, n, rank, world, flows=1 << 24, zipf=None):
     from cilium_amd import synth
     if name == "config2":
         return synth.config2(n)
@@ -77,7 +77,7 @@ def make_workload(name, n, rank, world, flows=1 << 24):
         # whose address pair it owns, and packets of its own pairs (pre-steered by the
         # producer): conntrack sharded by address pair, config 4 of BASELINE.json
         seed = 0xC1A00003 if name == "config3" else 0xC1A00004
-        return synth.config3(n, n_flows=flows, seed=seed, shard=(rank, world) if world > 1 else None)
+        return synth.config3(n, n_flows=flows, seed=seed, shard=(rank, world) if world > 1 else None, zipf=zipf)
     if name == "config5":
         return synth.config5(n)
     raise SystemExit(f"unknown workload {name}")
@@ -278,6 +278,8 @@ def main():
                     help="steady state: every step is this many seconds after the previous one and ctmap.GC "
                          "(cv_ct_gc, GCFilterByTime at the step's now) runs before it, inside the timed region")
     ap.add_argument("--flows", type=int, default=1 << 24, help="configs 3/4: conntrack flows per GPU")
+    ap.add_argument("--zipf", type=float, default=None,
+                    help="configs 3/4: Zipf(a) flow popularity for the existing flows' packets (elephant flows)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend at N > 1 (nccl = RCCL)")
     ap.add_argument("--dump", default=None,
                     help="test hook: every rank writes <dir>/rank<r>.npz (its packets' address-pair keys, its "
@@ -311,7 +313,7 @@ def main():
     stateful = name in STATEFUL
     passes = args.warmup + args.steps + 1                          # + the accounting step after the timed ones
     t0 = time.time()
-    w = make_workload(name, args.packets, rank, world, args.flows)
+    w = make_workload(name, args.packets, rank, world, args.flows, args.zipf)
     if stateful:
         size_conntrack(name, w, passes)
         if args.ct_room is not None and name in ("config3", "config4"):
@@ -528,6 +530,14 @@ def main():
             # live entries / device slots at the first and the last timed step (a table is sized
             # for max_entries at 60 % slot load, so the load tells how far probes walk)
             line["config"]["ct_slot_load"] = {k: [load_first.get(k), load_last.get(k)] for k in load_first}
+            if args.zipf:
+                from cilium_amd import shard
+                fl = w.frames
+                pk = shard.pair_key4(fl[:, 26:30].copy().view("<u4").ravel(), fl[:, 30:34].copy().view("<u4").ravel()) \
+                    if name in ("config3", "config4") else None
+                _, cnt = np.unique(pk, return_counts=True)
+                line["config"]["zipf"] = {"a": args.zipf, "largest_pair_packets": int(cnt.max()),
+                                          "pairs_over_1000_packets": int((cnt > 1000).sum())}
             if args.gc_step:
                 line["config"]["steady_state"] = {
                     "gc_step_s": args.gc_step, "gc_deleted_in_timed_steps": gc_timed,

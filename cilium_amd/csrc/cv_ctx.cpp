@@ -222,6 +222,7 @@ struct cv_ctx {
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
     DevBuf gdel, gest;            // egress: local-delivery records (DEL_SLOTS x 16 B per packet),
                                   // the conntrack stage's input states (64 B per packet)
+    DevBuf gres, gdel_ev;         // egress: packed outputs (16 B), delivery records' event part (32 B)
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
     uint64_t gcap = 0, gn = 0;
@@ -1172,7 +1173,8 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     (void)hipMemset(c->gtable.p, 0, cap * 16);
     if (egress || c->g_egress) {
         if (c->gparent.alloc(cap * 8) || c->geg.alloc((size_t)cmax * EG_WORDS * 4) ||
-            c->gdel.alloc((size_t)cmax * DEL_SLOTS * 16) || c->gest.alloc((size_t)cmax * 64))
+            c->gdel.alloc((size_t)cmax * DEL_SLOTS * 16) || c->gest.alloc((size_t)cmax * 64) ||
+            c->gres.alloc((size_t)cmax * 16) || c->gdel_ev.alloc((size_t)cmax * 32))
             return -ENOMEM;
         (void)hipMemset(c->gparent.p, 0, cap * 8);
         c->g_egress = true;
@@ -1215,6 +1217,8 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
                     c->gwork6.as<uint32_t>(), c->ghword.as<uint32_t>(), c->ghcnt.as<uint32_t>(), (uint32_t)Q_NETDEV,
                     0};
     gs.del = c->gdel.as<uint4>();
+    gs.res = c->gres.as<uint4>();
+    gs.del_ev = c->gdel_ev.as<uint4>();
     gs.est = c->gest.as<uint4>();
     gs.q6 = (uint32_t)Q_NETDEV6;
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);

@@ -166,6 +166,9 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
                                // group, list NPOS - 1 the runs of groups past NPOS - 1 members, in
                                // packet order (k_gbin_group -> k_heads_place)
     uint32_t pos;              // egress: the member position of the current launch pair
+    uint4 *res;                // egress: per packet the packed final outputs of the scattered stages
+                               // (eg_done), written out in packet order by k_out_unpack
+    uint4 *del_ev;             // egress: per packet 2 x 16 B, the event-only part of a delivery record
     uint4 *del;                // egress: per packet DEL_SLOTS x 16 B, the local-delivery record
                                // k_egress_ct hands to k_egress_deliver (listed in `single`)
     uint4 *est;                // egress: per packet 64 B, the conntrack stage's packed input state
@@ -199,7 +202,7 @@ constexpr int EG_WORDS = 16;
 // position lists of the egress conntrack stage: one launch per member position, the last
 // one continuing the few groups past NPOS - 1 members (<= 16: the lists are k_heads' 16)
 constexpr uint32_t NPOS = 8;
-constexpr uint32_t DEL_SLOTS = 6;
+constexpr uint32_t DEL_SLOTS = 4;                 // (64 B: one aligned half line per record)
 // the local-delivery list counter of a position (the netdev queue's sub-queue counters,
 // which the egress path does not use)
 __host__ __device__ constexpr int del_ctr(bool v6, uint32_t pos) { return 32 + (int)((v6 ? 8u : 0u) + pos) * 32; }

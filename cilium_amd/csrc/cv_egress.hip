@@ -84,6 +84,36 @@ __device__ __forceinline__ void eg_final(const OutDev &o, uint32_t i, const EgOu
     store_out(o, i, a);
 }
 
+// The final outputs of a packet a scattered stage (service, conntrack, delivery: lanes
+// take packets in group order) finishes, as ONE 16-B store into its g.res slot instead
+// of a store per output array -- each a random line of HBM -- written out in packet
+// order by k_out_unpack: {identity, ret | -reason << 8 | ct << 16 | RES_DONE,
+// proxy | nl << 16 | nu << 24, 0} (ret is one of the small TC_ACT_* / E_* codes, reason
+// a DROP_* code or 0)
+constexpr uint32_t RES_DONE = 1u << 24;
+__device__ __forceinline__ void eg_done(const GroupScratch &g, uint32_t i, const EgOut &r, const Acct &a)
+{
+    g.res[i] = make_uint4(r.dst, ((uint32_t)r.ret & 0xFFu) | ((uint32_t)(-r.reason) & 0xFFu) << 8 |
+                                     (uint32_t)r.ct << 16 | RES_DONE,
+                          (uint32_t)r.proxy | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24, 0u);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_out_unpack(OutDev o, GroupScratch g, uint32_t n)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint4 r = g.res[i];
+        if (!(r.y & RES_DONE)) continue;                          // (finished in the front)
+        if (o.ret) o.ret[i] = (int32_t)(int8_t)(r.y & 0xFFu);
+        if (o.reason) o.reason[i] = -(int32_t)((r.y >> 8) & 0xFFu);
+        if (o.identity) o.identity[i] = r.x;
+        if (o.ct) o.ct[i] = (uint8_t)(r.y >> 16);
+        if (o.proxy) o.proxy[i] = (uint16_t)r.z;
+        if (o.xdp) o.xdp[i] = 0;
+        if (o.nl) o.nl[i] = (uint8_t)(r.z >> 16);
+        if (o.nu) o.nu[i] = (uint8_t)(r.z >> 24);
+    }
+}
+
 template <bool FULL>
 __device__ __forceinline__ EpDev eg_src4(const DpParams &p, uint32_t idx)
 {
@@ -363,6 +393,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
             }
         }
         g.pkey[i] = gk;
+        g.res[i] = make_uint4(0u, 0u, 0u, 0u);                   // (RES_DONE clear: finished here or later)
         if (!full && stage == STAGE_LB) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) g.est[(size_t)i * 4 + k] = es[k];
@@ -476,7 +507,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
 fin:
     eg[0] = STAGE_DONE;
     eg_drop(p, res, ret, sk.len, m);
-    eg_final(o, i, res, a);
+    eg_done(g, i, res, a);
 }
 
 // lb6_local (lb.h:426-483) + lb6_xlate (:386-424)
@@ -569,7 +600,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
 fin:
     eg[0] = STAGE_DONE;
     eg_drop(p, res, ret, s.len, m);
-    eg_final(o, i, res, a);
+    eg_done(g, i, res, a);
 }
 
 // the service groups by member position, as the conntrack stage (position lists of the
@@ -1028,7 +1059,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
                 state = 2;
             } else {
                 res.ret = TC_ACT_REDIRECT;
-                eg_final(o, i, res, a);
+                eg_done(g, i, res, a);
                 state = 1;
             }
         }
@@ -1050,7 +1081,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
                 res.ret = TC_ACT_REDIRECT;
                 notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
                 if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
-                eg_final(o, i, res, a);
+                eg_done(g, i, res, a);
             } else if (!e2) {
                 ret = DROP_MISSED_TAIL_CALL;
                 state = 2;
@@ -1064,7 +1095,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
                                       (rn1.loopback ? 1u << 26 : 0u),
                                   ep.seclabel);
                 d[2] = make_uint4(ifindex_of(m, p.lxc4, lxc_slot, iv), res.dst, (uint32_t)lxc_slot, rn1.na);
-                if (M::EV) d[3] = make_uint4(rn1.np, 0, 0, 0);
+                if (M::EV) g.del_ev[2 * (size_t)i] = make_uint4(rn1.np, 0, 0, 0);
                 if constexpr (INL) deliver4_one<false>(p, b, now, o, g, i, true, m, sq);
                 else del_list(g, false, i);
             }
@@ -1073,12 +1104,12 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
             notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
             res.ret = TC_ACT_OK;
             if (M::EV && o.frames) eg4_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
-            eg_final(o, i, res, a);
+            eg_done(g, i, res, a);
         }
     }
     if (state == 2) {
         eg_drop(p, res, ret, s.len, m);
-        eg_final(o, i, res, a);
+        eg_done(g, i, res, a);
     }
 }
 
@@ -1192,7 +1223,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
                 state = 2;
             } else {
                 res.ret = TC_ACT_REDIRECT;
-                eg_final(o, i, res, a);
+                eg_done(g, i, res, a);
                 state = 1;
             }
         }
@@ -1214,7 +1245,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
                 res.ret = TC_ACT_REDIRECT;
                 notify_trace(p, m, TRACE_TO_HOST, s.len, ep.lxc_id, ep.seclabel, HOST_ID, 0, HOST_IFINDEX, res.ct, mon);
                 if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 1, -1, rn2);
-                eg_final(o, i, res, a);
+                eg_done(g, i, res, a);
             } else if (!e2) {
                 ret = DROP_MISSED_TAIL_CALL;
                 state = 2;
@@ -1231,8 +1262,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
                 d[3] = make_uint4((e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u), ep.seclabel,
                                   ifindex_of(m, p.lxc6, lxc_slot, iv), res.dst);
                 if (M::EV) {
-                    d[4] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
-                    d[5] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
+                    g.del_ev[2 * (size_t)i] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
+                    g.del_ev[2 * (size_t)i + 1] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
                 }
                 if constexpr (INL) deliver6_one<false>(p, b, now, o, g, i, true, m, sq);
                 else del_list(g, true, i);
@@ -1242,12 +1273,12 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
             notify_trace(p, m, TRACE_TO_STACK, s.len, ep.lxc_id, ep.seclabel, res.dst, 0, 0, res.ct, mon);
             res.ret = TC_ACT_OK;
             if (M::EV && o.frames) eg6_frame(p, b, o, eg, i, ep, rn1, 0, -1, rn2);
-            eg_final(o, i, res, a);
+            eg_done(g, i, res, a);
         }
     }
     if (state == 2) {
         eg_drop(p, res, ret, s.len, m);
-        eg_final(o, i, res, a);
+        eg_done(g, i, res, a);
     }
 }
 
@@ -1287,10 +1318,10 @@ __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &
     if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy) {
         const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         const RevNatOut rn1{(d1.z >> 25) & 1u ? true : false, (d1.z >> 26) & 1u ? true : false, d2.w,
-                            g.del[(size_t)i * DEL_SLOTS + 3].x};
+                            g.del_ev[2 * (size_t)i].x};
         eg4_frame(p, b, o, eg, i, G(p.eps)[eg[1] & 0xFFFFu], rn1, 2, (int64_t)d2.z, rn2);   // ipv4_local_delivery
     }
-    eg_final(o, i, res, a);
+    eg_done(g, i, res, a);
 }
 
 template <bool Q, class M>
@@ -1333,16 +1364,15 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
                                         nullptr, live, sq);
     if (!live) return;
     if (M::EV && o.frames && (res.ret == TC_ACT_OK || res.ret == TC_ACT_REDIRECT) && !res.proxy) {
-        const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
         const uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-        const uint4 d4 = d[4], d5 = d[5];
+        const uint4 d4 = g.del_ev[2 * (size_t)i], d5 = g.del_ev[2 * (size_t)i + 1];
         RevNat6Out rn1;
         rn1.valid = (d3.x >> 25) & 1u;
         rn1.np = d4.y;
         rn1.na[0] = d5.x; rn1.na[1] = d5.y; rn1.na[2] = d5.z; rn1.na[3] = d5.w;
         eg6_frame(p, b, o, eg, i, G(p.eps)[eg[1] & 0xFFFFu], rn1, 2, (int64_t)d4.x, rn2);   // ipv6_local_delivery
     }
-    eg_final(o, i, res, a);
+    eg_done(g, i, res, a);
 }
 
 // the wave-uniform loop over the list of the deliveries a position handed over: every
@@ -1563,6 +1593,7 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
     g.epoch += 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);
+    hipLaunchKernelGGL(k_out_unpack, grid, blk, 0, s, o, g, b.n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -166,11 +166,39 @@ __device__ __forceinline__ bool key_eq(const CV_G uint32_t *kw, const uint32_t *
             const uint2 v = *reinterpret_cast<const CV_G uint2 *>(kw + j);
             eq &= (v.x == key[j]) & (v.y == key[j + 1]);
         }
+    } else if constexpr (S::KW % 2 == 0 && S::KEY0 % 2 == 0 && S::KS % 2 == 0) {
+        // 8-B aligned key words (buckets are 64-B aligned): half the load instructions
+#pragma unroll
+        for (int j = 0; j < S::KW; j += 2) {
+            const uint2 v = *reinterpret_cast<const CV_G uint2 *>(kw + j);
+            eq &= (v.x == key[j]) & (v.y == key[j + 1]);
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < S::KW; ++j) eq &= (kw[j] == key[j]);
     }
     return eq;
+}
+
+// the inline value words of slot sl of a bucket (wide loads where the words are 8-B
+// aligned, a 12-B load for the lb4_service triple)
+template <class S>
+__device__ __forceinline__ void ival_load(const CV_G uint32_t *bw, int sl, uint32_t *ival)
+{
+    const CV_G uint32_t *iv = bw + S::IVAL0 + sl * S::IVW;
+    if constexpr (S::IVW == 3) {
+        const uint3 v = *reinterpret_cast<const CV_G uint3 *>(iv);
+        ival[0] = v.x; ival[1] = v.y; ival[2] = v.z;
+    } else if constexpr (S::IVW % 2 == 0 && S::IVAL0 % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < S::IVW; j += 2) {
+            const uint2 v = *reinterpret_cast<const CV_G uint2 *>(iv + j);
+            ival[j] = v.x; ival[j + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < S::IVW; ++j) ival[j] = iv[j];
+    }
 }
 template <class S>
 __device__ __forceinline__ void load_bucket(const uint32_t *__restrict__ buckets, uint64_t b, uint32_t (&w)[S::BW])
@@ -217,8 +245,7 @@ __device__ __forceinline__ int64_t dev_find_tf(const HashTable &t, const uint32_
             const CV_G uint32_t *kw = bw + S::KEY0 + sl * S::KS;
             const bool eq = key_eq<S, FRESH>(kw, key);
             if (eq) {
-#pragma unroll
-                for (int j = 0; j < S::IVW; ++j) ival[j] = bw[S::IVAL0 + sl * S::IVW + j];
+                ival_load<S>(bw, sl, ival);
                 if (S::IVH) ival[0] = half_at<S>(bw, S::HVAL0 + sl);
                 return (int64_t)(b * S::SPB + sl);
             }
@@ -473,8 +500,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
             const CV_G uint32_t *kw = pr.bw + S::KEY0 + sl * S::KS;
             const bool eq = key_eq<S, FRESH>(kw, key);
             if (eq) {
-#pragma unroll
-                for (int j = 0; j < S::IVW; ++j) ival[j] = pr.bw[S::IVAL0 + sl * S::IVW + j];
+                ival_load<S>(pr.bw, sl, ival);
                 return (int64_t)(b * S::SPB + sl);
             }
         }
@@ -509,8 +535,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
                 const CV_G uint32_t *kw = nx.bw + S::KEY0 + sl * S::KS;
                 const bool eq = key_eq<S, FRESH>(kw, key);
                 if (eq) {
-#pragma unroll
-                    for (int j = 0; j < S::IVW; ++j) ival[j] = nx.bw[S::IVAL0 + sl * S::IVW + j];
+                    ival_load<S>(nx.bw, sl, ival);
                     return (int64_t)(b * S::SPB + sl);
                 }
             }

@@ -389,10 +389,27 @@ def ct_entries(n, now, ingress, tcp, src_sec_id, seen_non_syn=False, length=64) 
     return v
 
 
+def zipf_ranks(s: "Stream", n: int, N: int, a: float) -> np.ndarray:
+    """n draws from a Zipf(a) popularity over N items (P(rank k) ~ (k + 1)^-a, the
+    continuous inverse CDF), mapped through a fixed bijection of [0, N) so the popular
+    items are scattered over the table rather than its first rows."""
+    u = s.frac(n)
+    if abs(a - 1.0) < 1e-9:
+        x = np.exp(u * np.log(N + 1.0))
+    else:
+        x = ((np.power(N + 1.0, 1.0 - a) - 1.0) * u + 1.0) ** (1.0 / (1.0 - a))
+    r = np.clip(np.floor(x).astype(np.int64) - 1, 0, N - 1)
+    mult = 0x9E3779B1
+    while np.gcd(mult, N) != 1:
+        mult += 2
+    return ((r.astype(np.uint64) * np.uint64(mult) + np.uint64(12345)) % np.uint64(N)).astype(np.int64)
+
+
 def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A00003, now0: int = 1_000_000,
             n_cidrs: int = 102400, n_ids: int = 10000, n_ep: int = 4096, ct_max: Optional[int] = None,
             ttl_low: float = 0.0005, v6_frac: float = 0.0, stride: Optional[int] = None,
-            n_flows6: Optional[int] = None, shard: Optional[Tuple[int, int]] = None) -> Workload:
+            n_flows6: Optional[int] = None, shard: Optional[Tuple[int, int]] = None,
+            zipf: Optional[float] = None) -> Workload:
     """Ingress through from_netdev into the endpoints' policy programs with conntrack.
     v6_frac > 0 makes a dual-stack batch: that fraction of the packets becomes IPv6
     (handle_ipv6 -> ipv6_policy with a global CT6 map, v6 endpoints in cilium_lxc, v6
@@ -402,7 +419,10 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     draws the same candidate (remote, endpoint) pairs from the same seed and keeps
     those whose address pair (cilium_amd.shard.pair_key4) it owns, n_flows of them; its
     packets (existing and new flows) are its own pairs too, as a producer steering by
-    address pair would hand them over.  The ranks' CT shards are disjoint."""
+    address pair would hand them over.  The ranks' CT shards are disjoint.
+    zipf = a: the existing flows' packets (forward and reply) follow a Zipf(a) popularity
+    instead of a uniform one (elephant flows: a few address pairs carry many packets of
+    the batch); drawn from a stream of their own, the rest of the batch is unchanged."""
     s = Stream(seed)
     c1 = config1(16, n_ep=n_ep)
     c2 = config2(16, n_cidrs=n_cidrs, n_ids=n_ids)
@@ -460,6 +480,10 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     egr_idx = np.nonzero(~ingress_init)[0]
     fi = ing_idx[s.choice(n_pkts, len(ing_idx))]
     fe = egr_idx[s.choice(n_pkts, max(len(egr_idx), 1))] if len(egr_idx) else fi
+    if zipf:
+        zs = Stream(seed ^ 0x5A1F5A1F)
+        fi = ing_idx[zipf_ranks(zs, n_pkts, len(ing_idx), zipf)]
+        fe = egr_idx[zipf_ranks(zs, n_pkts, len(egr_idx), zipf)] if len(egr_idx) else fi
     kind = np.where(r < 0.6, 0, np.where(r < 0.8, 1, 2))
     f = np.where(kind == 0, fi, fe)
     saddr = remote[f].copy()

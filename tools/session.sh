@@ -7,7 +7,7 @@
 #   bench=<workload>[,<args>]     one bench line (args: comma-separated)  bench_<workload>.json
 #   stats=<workload>              rocprofv3 kernel trace + stats          <workload>_kernel_stats.csv
 #   pmc=<workload>                FETCH / WRITE / TCC hit-miss passes     pmc<k>_<workload>/
-#   deep=<workload>[,<packets>]   SQ / TA / TCP counter passes            deep_<workload>/
+#   deep=<workload>[,<packets>[,<v>]]  SQ / TA / TCP counter passes (v: an _ab/ library)  deep_<workload>[_<v>]/
 #   cal                           the random-line FETCH_SIZE calibration  pmc_cal/
 #   ab=<workload>,<v>[,<v>...]    timing-only A/B of library variants (v = main or a
 #                                 directory under _ab/ holding libcilium_hip.so)  ab_<v>/
@@ -60,16 +60,18 @@ for st in "$@"; do
         -- python3 bench.py --workload "$W" --steps 3 --warmup 1 --no-cpu
     done ;;
   deep)
-    W=${A[0]}; P=${A[1]:-4194304}; i=0
+    W=${A[0]}; P=${A[1]:-4194304}; V=${A[2]:-}; i=0
+    if [ -n "$V" ]; then export CV_LIB=$PWD/_ab/$V/libcilium_hip.so; D=deep_${W}_$V; else unset CV_LIB; D=deep_$W; fi
     for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH SQ_IFETCH SQ_INSTS_LDS SQ_INST_LEVEL_VMEM SQ_WAIT_ANY" \
                 "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum"; do
       i=$((i+1))
-      mkdir -p "$OUT/deep_$W"
-      run 150 "$OUT/deep_$W/p$i.log" rocprofv3 --pmc $CTRS -d "$OUT/deep_$W/p$i" -o run --output-format csv \
+      mkdir -p "$OUT/$D"
+      run 150 "$OUT/$D/p$i.log" rocprofv3 --pmc $CTRS -d "$OUT/$D/p$i" -o run --output-format csv \
         -- python3 bench.py --workload "$W" --packets "$P" --steps 1 --warmup 1 --no-cpu
     done
-    python3 tools/pmc_table.py "$OUT/deep_$W" > "$OUT/deep_$W.txt" 2>&1; cat "$OUT/deep_$W.txt" >&2 ;;
+    unset CV_LIB
+    python3 tools/pmc_table.py "$OUT/$D" > "$OUT/$D.txt" 2>&1 ;;
   cal)
     run 120 "$OUT/pmc_cal.log" rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_cal" -o run --output-format csv \
       -- python3 tools/pmc_calibrate.py ;;

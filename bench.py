@@ -269,11 +269,14 @@ def main():
     ap.add_argument("--packets", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg and the random-access probe (profiling runs)")
     ap.add_argument("--ct-room", type=int, default=None,
-                    help="configs 3/4: max_entries = the preloaded entries + this many (0: a full table, every "
+                    help="max_entries = the preloaded entries + this many (0: a full table, every "
                          "create fails; the exact-admission regime) instead of room for every create of the run")
     ap.add_argument("--ct-max-log2", type=int, default=None,
-                    help="configs 3/4: max_entries = 2^N (the device table: 2^N entries at 60%% slot load) instead "
+                    help="max_entries = 2^N (the device table: 2^N entries at 60%% slot load) instead "
                          "of room for every create of the run; with --gc-step the run stays within it")
+    ap.add_argument("--ct-max", type=int, default=None,
+                    help="max_entries of every CT map (config 5: CT4 and CT6; a run that creates more fills them "
+                         "and then runs next to the limit: the exact-admission regime)")
     ap.add_argument("--gc-step", type=int, default=0,
                     help="steady state: every step is this many seconds after the previous one and ctmap.GC "
                          "(cv_ct_gc, GCFilterByTime at the step's now) runs before it, inside the timed region")
@@ -316,10 +319,14 @@ def main():
     w = make_workload(name, args.packets, rank, world, args.flows, args.zipf)
     if stateful:
         size_conntrack(name, w, passes)
-        if args.ct_room is not None and name in ("config3", "config4"):
-            w.maps["ct4"].max_entries = len(np.unique(w.maps["ct4"].keys, axis=0)) + args.ct_room
-        if args.ct_max_log2 is not None and name in ("config3", "config4"):
-            w.maps["ct4"].max_entries = 1 << args.ct_max_log2
+        cts = [k for k in ("ct4", "ct6") if k in w.maps and (name != "config3" or k == "ct4")]
+        for k in cts:
+            if args.ct_room is not None:
+                w.maps[k].max_entries = len(np.unique(w.maps[k].keys, axis=0)) + args.ct_room
+            if args.ct_max_log2 is not None:
+                w.maps[k].max_entries = 1 << args.ct_max_log2
+            if args.ct_max is not None:
+                w.maps[k].max_entries = args.ct_max
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
     ctx, maps = H.product_ctx(w, device=local)
     log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")

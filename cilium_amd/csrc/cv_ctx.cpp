@@ -225,6 +225,7 @@ struct cv_ctx {
     DevBuf gres, gdel_ev;         // egress: packed outputs (16 B), delivery records' event part (32 B)
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
+    DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -1599,6 +1600,118 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     return 0;
 }
 
+// An egress launch next to max_entries, exact (cv_kernels.hip "egress admission"): the
+// whole pipeline runs with per-packet budgets of CT creates, and the budget scan then
+// tells whether every packet got the creates the sequential run gives it.  If not, the
+// device state the pass wrote (the CT maps, the policy counters, the metrics, the event
+// rings' counts) goes back to the copy taken before the first pass and the pipeline runs
+// again with the scan's budgets.  The first pass gives every packet 7 (none if a map is
+// full): a launch that crosses max_entries settles in two passes, one that starts full in
+// one.  One host read per pass (one word).  Needs one CT4 and at most one CT6 map.
+bool egress_admissible(const std::vector<MapObj *> &cts)
+{
+    int n4 = 0, n6 = 0;
+    for (MapObj *m : cts) (m->kind == MK_CT4 ? n4 : n6)++;
+    return n4 <= 1 && n6 <= 1;
+}
+
+int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_t *src_ep, uint32_t ep0,
+                 const uint32_t *flow_hash, uint32_t now, const OutDev &oc, const std::vector<MapObj *> &cts,
+                 hipStream_t s)
+{
+    constexpr int MAX_PASSES = 8;
+    const uint32_t n = bc.n;
+    // the state a pass writes, and where its copy goes
+    struct Region { void *src; size_t bytes, off; };
+    std::vector<Region> regs;
+    size_t total = 0;
+    auto add = [&](void *src, size_t bytes) {
+        if (!src || !bytes) return;
+        regs.push_back(Region{src, bytes, total});
+        total += (bytes + 255) & ~(size_t)255;
+    };
+    MapObj *map_of[2] = {nullptr, nullptr};
+    for (MapObj *m : cts) map_of[m->kind == MK_CT4 ? 0 : 1] = m;
+    size_t live_off[2] = {0, 0};
+    add(c->metrics, METRICS_WORDS * 8);
+    for (int k = 0; k < 2; ++k)
+        if (MapObj *m = map_of[k]) {
+            live_off[k] = total;
+            add(m->live.p, 8);
+            add(m->ct.buckets.p, m->ct.buckets.n);
+            add(m->ct.vals.p, m->ct.vals.n);
+            add(m->ct.aux.p, m->ct.aux.n);
+        }
+    std::set<const void *> seen;
+    for (auto &e : c->eps) {
+        MapObj *m = get(c, e.policy);
+        if (m && seen.insert(m->pol.vals.p).second) {
+            add(m->pol.vals.p, m->pol.vals.n);
+            add(m->pol.aux.p, m->pol.aux.n);
+        }
+    }
+    add(c->notify_count, 4);
+    add(c->trace_count, 4);
+    if ((c->eadm_save.n < total && c->eadm_save.alloc(total)) ||
+        (c->eadm_buf.n < (size_t)n * 4 + 2 * 4096 * 8 + 256 && c->eadm_buf.alloc((size_t)n * 4 + 2 * 4096 * 8 + 256)))
+        return -ENOMEM;
+    uint8_t *save = c->eadm_save.as<uint8_t>();
+    for (const Region &g : regs)
+        if (hipMemcpyAsync(save + g.off, g.src, g.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return -EIO;
+    uint8_t *buf = c->eadm_buf.as<uint8_t>();
+    EAdmit a{};
+    a.n = n;
+    a.intent = buf;
+    uint8_t *bud[2] = {buf + n, buf + 2 * (size_t)n};
+    uint8_t *left = buf + 3 * (size_t)n;
+    a.tsum = reinterpret_cast<uint32_t *>(buf + ((4 * (size_t)n + 255) & ~(size_t)255));
+    a.flag = a.tsum + 2 * 4096 * 2;
+    bool full = true;                                             // (the live counts: exact, read by ct_fits)
+    for (int k = 0; k < 2; ++k) {
+        a.live0[k] = reinterpret_cast<const unsigned long long *>(save + live_off[k]);   // (absent: cap 0, no room)
+        a.cap[k] = map_of[k] ? map_of[k]->cap : 0;
+        if (map_of[k] && map_of[k]->live_upper < map_of[k]->cap) full = false;
+    }
+    // the first pass: 7 creates per packet, or none when every map is full
+    if (hipMemsetAsync(bud[0], full ? 0 : 7, n, s) != hipSuccess) return -EIO;
+    const bool stats = getenv("CV_ADMIT_STATS") != nullptr;
+    int cur = 0, pass = 0;
+    for (;; ++pass) {
+        DpParams pp = p;
+        pp.budget = bud[cur];
+        pp.eg_left = left;
+        pp.eg_intent = const_cast<uint8_t *>(a.intent);
+        GroupScratch gs = next_groups(c, 3, s);
+        gs.gbits = gbin_bits(n);
+        int r = launch_lxc_egress(pp, bc, src_ep, ep0, flow_hash, now, oc, gs, s);
+        if (r) return r;
+        a.used = bud[cur];
+        a.next = bud[cur ^ 1];
+        if ((r = launch_egress_admission(a, s))) return r;
+        uint32_t flag = 0;
+        hipError_t e = hipMemcpyAsync(&flag, a.flag, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[cv] egress admission pass %d: %s\n", pass, hipGetErrorString(e));
+            return -EIO;
+        }
+        if (!flag) break;                                         // the sequential run
+        for (const Region &g : regs)                              // back to the state before the window
+            if (hipMemcpyAsync(g.src, save + g.off, g.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return -EIO;
+        if (pass + 1 == MAX_PASSES) {
+            fprintf(stderr, "[cv] egress admission: no fixed point after %d passes (%u packets)\n", MAX_PASSES, n);
+            return -EAGAIN;
+        }
+        cur ^= 1;
+    }
+    for (MapObj *m : cts) {
+        m->live_upper = m->cap;                                   // (re-read when the next launch plans)
+        m->gen++;
+    }
+    if (stats) fprintf(stderr, "[cv admit] egress: %u packets, %d passes\n", n, pass + 1);
+    return 0;
+}
+
 // live policy counters of one key from HBM (device-authoritative)
 void policy_counters(MapObj *mo, const uint8_t *key, uint8_t *val)
 {
@@ -2084,16 +2197,30 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
     }
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
+    const bool admissible = egress_admissible(cts) && !getenv("CV_EGRESS_GUARDED");
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
-        n = ct_plan(c, cts, std::min(c->chunk, b->n - off), 7, (hipStream_t)stream, &p.ct_guard);
-        GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
-        gs.gbits = gbin_bits(n);                                  // (the binned grouping of the components)
+        // a launch whose creates (at most 7 per packet) fit runs at full width; one that may
+        // reach max_entries runs admitted (lxc_admitted), or, with more CT maps than that
+        // handles, in one-packet guarded launches.  Short of room for 7 n creates, a launch
+        // of room / 7 packets (>= 2^20) surely fits and runs without the admission passes.
+        n = std::min(c->chunk, b->n - off);
+        const uint32_t fit_n = ct_fit_count(c, cts, n, 7);
+        if (fit_n < n && fit_n >= std::min<uint32_t>(n, SPLIT_MIN)) n = fit_n;
+        const bool fits = ct_fits(c, cts, n, 7);
+        if (!fits && !admissible) n = ct_plan(c, cts, n, 7, (hipStream_t)stream, &p.ct_guard);
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
-        if ((r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0,
-                                   flow_hash ? flow_hash + off : nullptr, now, chunk(o, off, b->stride), gs,
-                                   (hipStream_t)stream)))
-            return r;
+        if (!fits && admissible) {
+            r = lxc_admitted(c, p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
+                             now, chunk(o, off, b->stride), cts, (hipStream_t)stream);
+        } else {
+            GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
+            gs.gbits = gbin_bits(n);                              // (the binned grouping of the components)
+            r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
+                                  now, chunk(o, off, b->stride), gs, (hipStream_t)stream);
+        }
+        p.ct_guard = 0;
+        if (r) return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream, true);

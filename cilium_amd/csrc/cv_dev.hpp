@@ -443,6 +443,8 @@ struct Acct {
     uint32_t nl, nu;
     LdsPolicy *pc = nullptr;   // policy counter cache of the workgroup, if any
     uint32_t budget = ~0u;     // admission windows: creates of new CT entries that may still succeed
+    uint32_t tried = 0;        // admission: creates of new entries tried (a failing one included)
+    uint32_t killed = 0;       // admission: entries deleted
 };
 
 // lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
@@ -1080,6 +1082,12 @@ __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, in
 // *mon: the `monitor` output of __ct_lookup (report requested), left as is when the
 // reference leaves it (a dead entry on a plain lookup).  Reads and writes the hot
 // words only (the bucket line the lookup just read).
+// the update of a hit entry's words e (ct_hit without its load and store; the hot-run
+// fold of k_ct_hot applies it to an entry it holds for a whole chunk); *mon as ct_hit
+template <class S>
+__device__ __forceinline__ void ct_hit_apply(const HashTable &ct, int64_t slot, CtE &e, int action, int dir, bool tcp,
+                                             uint32_t seen, uint32_t len, uint32_t now, uint32_t flags, bool *mon);
+
 template <class S>
 __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
                                        uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a, bool *mon)
@@ -1087,13 +1095,21 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
     a.nu++;
     CtE e;
     ct_load_hot<S>(ct, slot, e);
-    bool m = mon ? *mon : false;
-    if (ct_alive(e)) m = ct_timeout(e, tcp, dir, seen, now);
     if (st) {
         st->rev_nat = e.w[9] >> 16;
         st->loopback = (e.bits() & CTB_LB_LOOPBACK) ? 1u : 0u;
         st->slave = e.w[10] & 0xFFFFu;
     }
+    ct_hit_apply<S>(ct, slot, e, action, dir, tcp, seen, len, now, flags, mon);
+    ct_store_hot<S>(ct, slot, e);
+}
+
+template <class S>
+__device__ __forceinline__ void ct_hit_apply(const HashTable &ct, int64_t slot, CtE &e, int action, int dir, bool tcp,
+                                             uint32_t seen, uint32_t len, uint32_t now, uint32_t flags, bool *mon)
+{
+    bool m = mon ? *mon : false;
+    if (ct_alive(e)) m = ct_timeout(e, tcp, dir, seen, now);
     if (flags & F_CT_ACCOUNTING) {
         if (dir == CT_INGRESS) { ct_count<S>(ct, slot, e, 0, 1u); ct_count<S>(ct, slot, e, 2, len); }
         else                   { ct_count<S>(ct, slot, e, 4, 1u); ct_count<S>(ct, slot, e, 6, len); }
@@ -1109,7 +1125,6 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         if (!ct_alive(e)) ct_timeout_raw(e, CT_CLOSE_TIMEOUT, dir, seen, now);
     }
     if (mon) *mon = m;
-    ct_store_hot<S>(ct, slot, e);
 }
 
 __device__ __forceinline__ uint8_t dir_flags(int dir)
@@ -1215,6 +1230,56 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     return CT_ESTABLISHED;
 }
 
+// A hit whose entry update is deferred (k_ct_hot's fold applies it in member order)
+struct HitRec {
+    int64_t slot;              // -1: no hit
+    uint32_t action, dir, tcp, seen, len;
+};
+
+// ct_lookup4 (conntrack.h:442-562) for the hot-run path: the lookups and the result
+// only -- what the entry's hit fields give ct_state (rev_nat_index, loopback, slave)
+// -- with the hit's update returned in hr instead of written; accounting as ct_lookup
+template <class T>
+__device__ __forceinline__ int ct_lookup_pre(const HashTable &ct, T &t, const L4Hdr &h, int dir, uint32_t len,
+                                             int64_t &slot, CtState *st, Acct &a, HitRec &hr)
+{
+    using S = typename T::Spec;
+    static_assert(S::SYM != 0, "conntrack");
+    uint32_t seen;
+    hr.slot = -1;
+    slot = -1;
+    const int action = ct_l4<T::KW == 10>(t, h, dir, seen);
+    if (action < 0) return action;
+    T t2 = t;
+    t2.reverse();
+    uint32_t k1[T::KW], k2[T::KW];
+    t.key(k1);
+    t2.key(k2);
+    int ret;
+    a.nl++;
+    slot = dev_find<S, false>(ct, k1, nullptr);
+    if (slot >= 0) {
+        ret = (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+    } else {
+        if (dir == CT_SERVICE) return CT_NEW;
+        t = t2;
+        a.nl++;
+        slot = dev_find<S, false>(ct, k2, nullptr);
+        if (slot < 0) return CT_NEW;
+        ret = CT_ESTABLISHED;
+    }
+    a.nu++;
+    const CV_G uint32_t *hw = ct_hot<S>(ct, slot);                 // hot words h1 = w9, h2 = w10
+    const uint32_t w9 = hw[1], w10 = hw[2];
+    if (st) {
+        st->rev_nat = w9 >> 16;
+        st->loopback = (w9 & CTB_LB_LOOPBACK) ? 1u : 0u;
+        st->slave = w10 & 0xFFFFu;
+    }
+    hr = HitRec{slot, (uint32_t)action, (uint32_t)dir, t.nexthdr == 6 ? 1u : 0u, seen, len};
+    return ret;
+}
+
 // The live-entry count of a CT map (its max_entries check).  A launch either has room
 // for every create it can make (the host plans launch chunks by the worst case per
 // packet, cv_ctx.cpp ct_plan): creates then only count, summed per workgroup in the
@@ -1239,6 +1304,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
         __hip_atomic_load(G(ct.live), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ct.cap)
         return false;                                             // full: -E2BIG
     if (a.budget != ~0u && (absent || dev_find<typename T::Spec>(ct, k, nullptr) < 0)) {
+        ++a.tried;
         if (!a.budget) return false;                              // admission: the map is full here (-E2BIG)
         --a.budget;
     }
@@ -1257,6 +1323,7 @@ __device__ __forceinline__ void ct_kill(const HashTable &ct, int64_t slot, Acct 
     dev_kill<S>(ct, slot);
     ct_live_add(ct, a, guard, -1);
     a.nu++;
+    a.killed++;
 }
 
 // the entry ct_create4 / ct_create6 write for `t` (conntrack.h:668-690 / 593-612)
@@ -2171,7 +2238,7 @@ __device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint
 // order and members in packet order, then every singleton group (listed densely in
 // `single`); the next member's index is loaded while fn runs.
 template <class F>
-__device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool first_only, F &&fn)
+__device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool first_only, F &&fn, uint32_t skip = 0)
 {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     auto run = [&](uint32_t off) {
@@ -2187,7 +2254,7 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
     uint32_t multi = 0;                                           // listed runs: classes >= 1
 #pragma unroll
     for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
-    for (uint32_t j = tid; j < multi; j += stride) run(g.work[j]);
+    for (uint32_t j = skip + tid; j < multi; j += stride) run(g.work[j]);   // (skip: the hot runs, k_ct_hot)
     const uint32_t singles = g.cursor[SINGLE_WORD0 + q];
     for (uint32_t j = tid; j < singles; j += stride) fn(g.single[j], 1u);
 }

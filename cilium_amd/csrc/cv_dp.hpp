@@ -77,6 +77,10 @@ struct DpParams {              // by value as the kernel argument
     uint32_t win_lo, win_span; // the conntrack stages run the packets in [win_lo, win_lo + win_span) (admission
                                // windows; 0, ~0 otherwise)
     const uint8_t *budget;     // admission: per packet the creates of new CT entries that succeed, or null
+    // egress admission (cv_ctx.cpp lxc_admitted): per packet the budget left for its next
+    // stage, and its intent {creates tried (3 bits), deletes << 3, CT map (0 CT4, 1 CT6) << 4}
+    uint8_t *eg_left;
+    uint8_t *eg_intent;
 };
 
 // Exact conntrack admission next to max_entries (cv_kernels.hip "conntrack
@@ -105,6 +109,19 @@ struct Admit {
 // index past nmaps (k_adm_apply): a stale or corrupt intent, failed loudly instead of
 // indexing past Admit's arrays
 enum : uint32_t { ADMIT_ERR_MAP = 1, ADMIT_ERR_IB = 2 };
+
+// Exact egress admission (cv_kernels.hip "egress admission", cv_ctx.cpp lxc_admitted):
+// whether a pass was the sequential run, and the next pass's budgets (one CT4, one CT6 map)
+struct EAdmit {
+    const uint8_t *intent;             // per packet (DpParams::eg_intent)
+    const uint8_t *used;               // the budgets the pass ran with
+    uint8_t *next;                     // the next pass's budgets
+    uint32_t *tsum;                    // per map and scan tile: (sum, prefix minimum)
+    const unsigned long long *live0[2];  // the maps' live counts as the window started
+    unsigned long long cap[2];         // max_entries (CT4, CT6)
+    uint32_t *flag;                    // set when a packet's creates differ from the sequential run's
+    uint32_t n;
+};
 
 struct BatchDev {
     const uint8_t *frames;
@@ -224,6 +241,7 @@ int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, con
 // admission, per window from packet a.lo (after launch_netdev_front): every later
 // packet's creates and deletes, the window's end (*a.hi) and the budgets
 int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s);
+int launch_egress_admission(const EAdmit &a, hipStream_t s);
 // config 5: from-container of the packets' source endpoints (src_ep[i], or ep0)
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s);

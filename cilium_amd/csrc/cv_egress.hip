@@ -73,6 +73,35 @@ struct EgOut {                  // per-packet results on the way to the outputs
     uint16_t proxy;
 };
 
+// Egress admission (cv_ctx.cpp lxc_admitted): a packet's creates of new conntrack
+// entries draw on ONE budget across its service, conntrack and delivery stages, in that
+// order (the order of its map_update_elem calls in the reference).  A stage takes the
+// budget left from p.eg_left, hands back what it did not use, and adds to the packet's
+// intent byte the creates it tried (a failing one included: the reference's failing
+// map_update_elem ends the packet) and the deletes it made.  `flush` hands over before
+// an inline delivery of the same packet.
+struct EgAdm {
+    const DpParams &p;
+    uint32_t i;
+    Acct &a;
+    bool on;
+    __device__ EgAdm(const DpParams &pp, uint32_t ii, Acct &aa, bool live) : p(pp), i(ii), a(aa), on(live && pp.eg_left)
+    {
+        if (on) {
+            a.budget = p.eg_left[i];
+            a.tried = a.killed = 0;
+        }
+    }
+    __device__ void flush()
+    {
+        if (!on) return;
+        p.eg_left[i] = (uint8_t)a.budget;
+        p.eg_intent[i] = (uint8_t)(p.eg_intent[i] + a.tried + (a.killed << 3));
+        on = false;
+    }
+    __device__ ~EgAdm() { flush(); }
+};
+
 __device__ __forceinline__ void eg_final(const OutDev &o, uint32_t i, const EgOut &r, const Acct &a)
 {
     if (o.ret) o.ret[i] = r.ret;
@@ -394,6 +423,10 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         }
         g.pkey[i] = gk;
         g.res[i] = make_uint4(0u, 0u, 0u, 0u);                   // (RES_DONE clear: finished here or later)
+        if (p.eg_left) {                                          // admission: this pass's budget, the intent's map
+            p.eg_left[i] = stage == STAGE_DONE ? 0u : p.budget[i];
+            p.eg_intent[i] = stage == STAGE_DONE ? 0u : (egl[0] & EG_V6) ? 16u : 0u;
+        }
         if (!full && stage == STAGE_LB) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) g.est[(size_t)i * 4 + k] = es[k];
@@ -420,6 +453,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    EgAdm adm(p, i, a, true);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
     uint32_t key_dport = d3.x >> 16;
@@ -526,6 +560,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    EgAdm adm(p, i, a, true);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
     uint32_t key_dport = d3.x >> 16;
@@ -908,7 +943,18 @@ __global__ void __launch_bounds__(BLOCK) k_egress_nat(DpParams p, BatchDev b, Gr
         if (p.ct_guard) continue;                                 // one-packet launch: written inline, in order
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         uint32_t nn;
-        if (eg[0] & EG_LOOPBACK) {                                // (client, IPV4_LOOPBACK): by pair
+        if (p.eg_left) {
+            // admission: every writer joins the group of its NAT key's readers (a node
+            // made if none reads it), so the writes run inline, in packet order, and
+            // each draws on its packet's budget as the reference's create does
+            if (eg[0] & EG_LOOPBACK) {
+                nn = group_node(g, pair_hash4(eg[4], eg[5], SALT_CT4));
+            } else {
+                nn = group_node(g, self_hash(eg[4], eg[9], eg[10]));
+                const uint32_t any = group_find(g, self_hash(eg[4], 0, 0x100));
+                if (any != NONE) uf_union(g, g.gslot[i], any);
+            }
+        } else if (eg[0] & EG_LOOPBACK) {                         // (client, IPV4_LOOPBACK): by pair
             nn = group_find(g, pair_hash4(eg[4], eg[5], SALT_CT4));
         } else {                                                  // (backend, backend, ports, proto)
             nn = group_find(g, self_hash(eg[4], eg[9], eg[10]));
@@ -1003,6 +1049,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         a.nl = o.nl ? o.nl[i] : 0u;
         a.nu = o.nu ? o.nu[i] : 0u;
     }
+    EgAdm adm(p, i, a, live);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Skb4 &s = x.s;
     Tuple4 &t = x.t;
@@ -1096,6 +1143,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
                                   ep.seclabel);
                 d[2] = make_uint4(ifindex_of(m, p.lxc4, lxc_slot, iv), res.dst, (uint32_t)lxc_slot, rn1.na);
                 if (M::EV) g.del_ev[2 * (size_t)i] = make_uint4(rn1.np, 0, 0, 0);
+                adm.flush();                                      // (the delivery draws on what is left)
                 if constexpr (INL) deliver4_one<false>(p, b, now, o, g, i, true, m, sq);
                 else del_list(g, false, i);
             }
@@ -1168,6 +1216,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         a.nl = o.nl ? o.nl[i] : 0u;
         a.nu = o.nu ? o.nu[i] : 0u;
     }
+    EgAdm adm(p, i, a, live);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Skb6 &s = x.s;
     Tuple6 &t = x.t;
@@ -1265,6 +1314,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
                     g.del_ev[2 * (size_t)i] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
                     g.del_ev[2 * (size_t)i + 1] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
                 }
+                adm.flush();
                 if constexpr (INL) deliver6_one<false>(p, b, now, o, g, i, true, m, sq);
                 else del_list(g, true, i);
             }
@@ -1303,6 +1353,7 @@ __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &
     }
     Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
     Acct a{(d1.y >> 16) & 0xFFu, d1.y >> 24, m.pc};
+    EgAdm adm(p, i, a, live);
     EgOut res{TC_ACT_OK, 0, d2.y, (uint8_t)(d1.z >> 16), 0};
     if (live) {
         m.pkt = b.base + i;
@@ -1351,6 +1402,7 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     s.h.c2a = unchk2((d2.w >> 6) & 3u);
     s.h.c2b = unchk2((d2.w >> 8) & 3u);
     Acct a{(d2.w >> 16) & 0xFFu, d2.w >> 24, m.pc};
+    EgAdm adm(p, i, a, live);
     EgOut res{TC_ACT_OK, 0, d3.w, (uint8_t)(d3.x >> 16), 0};
     if (live) {
         m.pkt = b.base + i;

@@ -433,9 +433,224 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     store_out(o, i, a);
 }
 
-// stage 2: conntrack + policy, each address-pair group by one lane in packet order
+// ------------------------------------------------------------------ hot runs
+// A group of many packets (an elephant flow: one address pair carrying thousands of
+// the batch's packets) walked by one lane costs a chain of dependent memory round trips
+// per member.  Runs of size class >= HOT_CLASS (more than 32 members) go to k_ct_hot,
+// a wave per run, 64 members at a time:
+//  1. every lane looks its member up against the table as the chunk starts (read only:
+//     ct_lookup_pre, policy_ingress_denies) and tells whether its ipv4_policy would
+//     change which keys exist -- a create (CT_NEW, allowed) or a delete (CT_ESTABLISHED,
+//     denied);
+//  2. the members before the first such one (c) change no key, so each sees exactly
+//     what the sequential run shows it: they finish in parallel (verdicts, policy
+//     counters, metrics), their hits' entry updates deferred;
+//  3. one lane applies those updates in member order (ct_hit_apply) to the entries held
+//     in LDS for the chunk and writes each entry back once;
+//  4. member c runs whole (its create or delete), then the next chunk starts after it.
+// An elephant flow's established packets all take step 2: 64 members cost one round of
+// lookups instead of 64 dependent ones.  Only the plain instance (no event records,
+// whose trace decisions need the per-packet entry state) and launches without admission
+// budgets or guards use it; the others keep one lane per run.
+constexpr int HOT_CLASS = 12;                                     // size_class: runs of more than 32 members
+constexpr int HOT_CACHE = 8;                                      // entries one chunk's fold holds
+
+__device__ __forceinline__ uint32_t hot_runs(const GroupScratch &g, int q)
+{
+    uint32_t n = 0;
+#pragma unroll
+    for (int c = HOT_CLASS; c < NCLASS; ++c) n += g.cursor[qcls(q, c)];
+    return n;
+}
+
+struct HotWave {                                                  // per wave, LDS
+    unsigned long long hslot[64];                                 // the members' deferred hits (slot, ~0: none)
+    uint32_t hpar[64];                                            // action | dir << 2 | tcp << 4 | seen << 8
+    uint32_t hlen[64];
+    unsigned long long cslot[HOT_CACHE];                          // the fold's entries
+    uint32_t cw[HOT_CACHE][CT_HOTW];
+};
+
+// ipv4_policy (bpf_lxc.c:865-979) of a member that creates and deletes nothing: its
+// lookup (ct_lookup_pre) hit -- the entry update deferred to the fold -- or missed with
+// a denying policy
+template <class M>
+__device__ __forceinline__ int hot_finish(const DpParams &p, const EpDev &ep, Skb4 &s, Tuple4 &t, int ret,
+                                          const CtState &st, uint32_t src_label, bool skip_proxy, uint32_t ifindex,
+                                          uint8_t &ct_out, uint16_t &proxy, int32_t &reason, Acct &a, M &m)
+{
+    if (ret >= 0) {
+        ct_out = (uint8_t)ret;
+        if (ret == CT_REPLY && st.rev_nat && !st.loopback) {     // lb4_rev_nat(REV_NAT_F_TUPLE_SADDR)
+            uint32_t na, np;
+            if (revnat4(p, st.rev_nat, na, np, a)) {
+                const int r2 = rev_map_port(s.h, t.nexthdr, np);
+                const int r3 = r2 ? 0 : l4_csum_err(s, t.nexthdr);
+                if (r2 || r3) ret = r2 ? r2 : r3;
+                else t.saddr = na;
+            }
+        }
+    }
+    if (ret >= 0) {
+        int verdict = policy_ingress<false>(ep.policy, p.flags, s.len, src_label, t.dport, t.nexthdr, a);
+        if (ret != CT_REPLY && ret != CT_RELATED && verdict < 0) {
+            ret = DROP_POLICY;                                    // (a miss: an established one would delete)
+        } else {
+            if (skip_proxy) verdict = 0;
+            if (verdict > 0 && (ret == CT_NEW || ret == CT_ESTABLISHED)) {
+                proxy = (uint16_t)verdict;                        // ipv4_redirect_to_host_port
+                return TC_ACT_REDIRECT;
+            }
+            m.fwd(s.len, METRIC_INGRESS);                         // send_trace_notify(TRACE_TO_LXC)
+            return ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+        }
+    }
+    if (ret == E_TRUNC) return ret;
+    m.drop(ret, s.len, METRIC_INGRESS);                           // tail_ipv4_policy: send_drop_notify
+    reason = ret;
+    return TC_ACT_SHOT;
+}
+
+__device__ __forceinline__ void hot_cache_flush(const HashTable &ct, HotWave &w, int n)
+{
+    for (int u = 0; u < n; ++u) {
+        CtE e;
+        const uint32_t *h = w.cw[u];
+        e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
+        e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
+        ct_store_hot<Ct4Spec>(ct, (int64_t)w.cslot[u], e);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_ct_hot(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+{
+    __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
+    __shared__ HotWave hws[BLOCK / 64];
+    using M = MetT<false>;
+    M m;
+    pol_cache_init(pc);
+    met_init(m, lm);
+    m.pc = &pc;
+    HotWave &w = hws[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nhot = hot_runs(g, Q_NETDEV);
+    const uint32_t nw = (gridDim.x * BLOCK) >> 6;
+    for (uint32_t r = (blockIdx.x * BLOCK + threadIdx.x) >> 6; r < nhot; r += nw) {   // a wave per run
+        const uint32_t off = g.work[r], cnt = g.order[off];
+        for (uint32_t k0 = 0; k0 < cnt;) {                        // (wave-uniform)
+            const uint32_t k = k0 + lane;
+            const bool live = k < cnt;
+            const uint32_t x = live ? g.order[off + 1 + k] : 0u;
+            uint4 s0{}, s1{};
+            if (live) { s0 = g.srec[2 * x]; s1 = g.srec[2 * x + 1]; }
+            const uint32_t meta = s1.z;
+            const EpDev ep = ep_stage4<false>(p, meta & 0xFFFFu);
+            Skb4 s = skb4_unpack(s0, s1.x, s1.y & 0x3FFu, b.stride);
+            const bool skip_proxy = (meta >> 16) & 1u;
+            const uint32_t ifx = (meta >> 17) & 1u;               // ifindex != 0 (the plain instance's view)
+            // 1. the lookups against the chunk's starting table, read only
+            const bool simple = live && !(p.flags & F_DROP_ALL) && ep.ipv4 && s.len >= 34;
+            Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
+            Tuple4 t{};
+            t.nexthdr = s.nexthdr; t.daddr = s.daddr; t.saddr = s.saddr;
+            CtState st{0, 0, 0, 0, 0, 0};
+            HitRec hr{-1, 0, 0, 0, 0, 0};
+            int64_t slot = -1;
+            const int ret = simple ? ct_lookup_pre(ep.ct4, t, s.h, CT_INGRESS, s.len, slot, &st, a, hr) : 0;
+            const bool deny = simple && ret >= 0 && policy_ingress_denies(ep.policy, p.flags, s1.w, t.dport, t.nexthdr);
+            const bool change = simple && ((ret == CT_ESTABLISHED && deny) || (ret == CT_NEW && !deny));
+            const unsigned long long chg = __ballot(change);
+            const uint32_t c = chg ? (uint32_t)(__ffsll((long long)chg) - 1) : 64u;
+            // 2. the members before c, in parallel
+            if (live && lane < c) {
+                uint8_t ct = CT_NONE;
+                uint16_t proxy = 0;
+                int32_t reason = 0;
+                int rv;
+                if (simple) {
+                    rv = hot_finish(p, ep, s, t, ret, st, s1.w, skip_proxy, ifx, ct, proxy, reason, a, m);
+                } else {                                          // drops before any conntrack work
+                    Acct a0{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
+                    a = a0;
+                    rv = handle_policy4<M, false>(p, ep, s, s1.w, skip_proxy, ifx, now, ct, proxy, reason, a, m);
+                }
+                if (o.ret) o.ret[x] = rv;
+                if (o.reason) o.reason[x] = reason;
+                if (o.ct) o.ct[x] = ct;
+                if (o.proxy) o.proxy[x] = proxy;
+                store_out(o, x, a);
+            }
+            // 3. their hits' entry updates in member order, each entry written once
+            w.hslot[lane] = (live && lane < c && hr.slot >= 0) ? (unsigned long long)hr.slot : ~0ull;
+            w.hpar[lane] = hr.action | hr.dir << 2 | hr.tcp << 4 | hr.seen << 8;
+            w.hlen[lane] = hr.len;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const HashTable ct = ep_stage4<false>(p, __shfl(meta, 0, 64) & 0xFFFFu).ct4;   // (the run's CT map)
+            if (lane == 0) {
+                int n = 0;
+                const uint32_t upto = c < cnt - k0 ? c : cnt - k0;
+                for (uint32_t j = 0; j < upto; ++j) {
+                    const unsigned long long sl = w.hslot[j];
+                    if (sl == ~0ull) continue;
+                    int q = -1;
+                    for (int u = 0; u < n; ++u)
+                        if (w.cslot[u] == sl) q = u;
+                    if (q < 0) {
+                        if (n == HOT_CACHE) { hot_cache_flush(ct, w, n); n = 0; }
+                        q = n++;
+                        w.cslot[q] = sl;
+                        CtE e;
+                        ct_load_hot<Ct4Spec>(ct, (int64_t)sl, e);
+                        uint32_t *h = w.cw[q];
+                        h[0] = e.w[8]; h[1] = e.w[9]; h[2] = e.w[10]; h[3] = e.w[11]; h[4] = e.w[12]; h[5] = e.w[13];
+                        h[6] = e.w[0]; h[7] = e.w[2]; h[8] = e.w[4]; h[9] = e.w[6];
+                    }
+                    uint32_t *h = w.cw[q];
+                    CtE e;
+                    e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
+                    e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
+                    const uint32_t pr = w.hpar[j];
+                    ct_hit_apply<Ct4Spec>(ct, (int64_t)sl, e, (int)(pr & 3u), (int)((pr >> 2) & 3u), (pr >> 4) & 1u,
+                                          pr >> 8, w.hlen[j], now, p.flags, nullptr);
+                    h[0] = e.w[8]; h[1] = e.w[9]; h[2] = e.w[10]; h[3] = e.w[11]; h[4] = e.w[12]; h[5] = e.w[13];
+                    h[6] = e.w[0]; h[7] = e.w[2]; h[8] = e.w[4]; h[9] = e.w[6];
+                }
+                hot_cache_flush(ct, w, n);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (the entries written before any re-read)
+            l1_inv();
+            __builtin_amdgcn_wave_barrier();
+            // 4. member c whole: its create or delete, against the table the fold left
+            if (chg && lane == c) {
+                Acct a1{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
+                uint8_t ct = CT_NONE;
+                uint16_t proxy = 0;
+                int32_t reason = 0;
+                const int rv = handle_policy4<M, false>(p, ep, s, s1.w, skip_proxy, ifx, now, ct, proxy, reason, a1, m);
+                if (o.ret) o.ret[x] = rv;
+                if (o.reason) o.reason[x] = reason;
+                if (o.ct) o.ct[x] = ct;
+                if (o.proxy) o.proxy[x] = proxy;
+                store_out(o, x, a1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            l1_inv();
+            __builtin_amdgcn_wave_barrier();
+            k0 += chg ? c + 1 : 64u;
+        }
+    }
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
+}
+
+// stage 2: conntrack + policy, each address-pair group by one lane in packet order (the
+// hot runs by k_ct_hot when `hot`)
 template <bool EV>
-__global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+__global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now,
+                                                    int hot)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
@@ -445,7 +660,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutD
     m.pc = &pc;
     for_each_run(g, Q_NETDEV, false, [&](uint32_t x, uint32_t n) {
         if (x - p.win_lo < p.win_span) stage2_one(p, b, o, g, x, now, m, n == 1);     // (admission windows)
-    });
+    }, hot ? hot_runs(g, Q_NETDEV) : 0u);
     met_flush(m, p.metrics);                                      // (ends with a barrier)
     pol_cache_flush(pc);
 }
@@ -1276,8 +1491,11 @@ int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, con
     if (!b.n) return 0;
     const bool ev = o.frames || p.notify || p.trace;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
-    if (ev) hipLaunchKernelGGL(k_ct_stage<true>, grid, blk, 0, s, p, b, o, g, now);
-    else hipLaunchKernelGGL(k_ct_stage<false>, grid, blk, 0, s, p, b, o, g, now);
+    // the hot runs by whole waves (plain instance, no admission budgets or guards)
+    const int hot = !ev && !p.ct_guard && !p.budget && !getenv("CV_NO_HOT_RUNS");
+    if (hot) hipLaunchKernelGGL(k_ct_hot, dim3(1024), blk, 0, s, p, b, o, g, now);
+    if (ev) hipLaunchKernelGGL(k_ct_stage<true>, grid, blk, 0, s, p, b, o, g, now, 0);
+    else hipLaunchKernelGGL(k_ct_stage<false>, grid, blk, 0, s, p, b, o, g, now, hot);
     GroupScratch g6 = g;
     g6.single = g.single6;
     g6.work = g.work6;
@@ -1693,6 +1911,119 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
     hipLaunchKernelGGL(k_adm_top, dim3(1), dim3(1024), 0, s, a, tiles);
     hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
+    return launch_status(__func__);
+}
+
+// ------------------------------------------------------------------ egress admission
+// The budgets of an egress window (cv_ctx.cpp lxc_admitted) from what a pass recorded
+// (EgAdm in cv_egress.hip): per packet the creates it tried, t (a failing one included:
+// it ends the packet), and its deletes, d.  A packet's creates come before its delete
+// (its service, conntrack and delivery stages; the delete is the delivery's), so per CT
+// map its element of the (sum, prefix minimum) walk is (d - t, t ? -t : d), and the room
+// before it is R = r0 + S - min(0, r0 + M).  The pass was the sequential run exactly when
+// every packet got min(t, R) creates -- min(t, b) with b the budget it ran with: then the
+// walk subtracted what the pass consumed, and a create failed exactly where the map was
+// full.  The next pass's budgets are min(7, R) (generous: a packet that now creates more
+// than it did finds room if the map has it).
+__device__ __forceinline__ SumMin eadm_elem(uint32_t v, uint32_t m)
+{
+    const int32_t A = (int32_t)(v & 7u), D = (int32_t)((v >> 3) & 1u);
+    if (((v >> 4) & 1u) != m || (!A && !D)) return SumMin{0, SM_INF};
+    return SumMin{D - A, A ? -A : D};
+}
+
+__device__ __forceinline__ uint32_t eadm_v4(const EAdmit &a, uint32_t j)
+{
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (j + k < a.n) w |= (uint32_t)a.intent[j + k] << (8 * k);
+    return w;
+}
+
+__global__ void __launch_bounds__(1024) k_eadm_tiles(EAdmit a, uint32_t tiles)
+{
+    __shared__ SumMin lds[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    const uint32_t w = eadm_v4(a, j);
+    SumMin *agg = reinterpret_cast<SumMin *>(a.tsum);
+    for (uint32_t m = 0; m < 2; ++m) {
+        SumMin t{0, SM_INF};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (j + k < a.n) t = sm_comb(t, eadm_elem(w >> (8 * k) & 0xFFu, m));
+        SumMin tot;
+        block_excl_summin(t, lds, &tot);
+        if (threadIdx.x == 0) agg[m * tiles + blockIdx.x] = tot;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_eadm_top(EAdmit a, uint32_t tiles)
+{
+    __shared__ SumMin lds[17];
+    SumMin *agg = reinterpret_cast<SumMin *>(a.tsum);
+    for (uint32_t m = 0; m < 2; ++m) {
+        SumMin v[4], t{0, SM_INF};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = threadIdx.x * 4 + k;
+            v[k] = q < tiles ? agg[m * tiles + q] : SumMin{0, SM_INF};
+            t = sm_comb(t, v[k]);
+        }
+        SumMin e = block_excl_summin(t, lds, nullptr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = threadIdx.x * 4 + k;
+            if (q < tiles) agg[m * tiles + q] = e;
+            e = sm_comb(e, v[k]);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_eadm_apply(EAdmit a, uint32_t tiles)
+{
+    __shared__ SumMin lds[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    const uint32_t w = eadm_v4(a, j);
+    const SumMin *agg = reinterpret_cast<const SumMin *>(a.tsum);
+    uint32_t out = 0;
+    bool bad = false;
+    for (uint32_t m = 0; m < 2; ++m) {
+        SumMin t{0, SM_INF};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (j + k < a.n) t = sm_comb(t, eadm_elem(w >> (8 * k) & 0xFFu, m));
+        SumMin P = sm_comb(agg[m * tiles + blockIdx.x], block_excl_summin(t, lds, nullptr));
+        const unsigned long long live = *a.live0[m];
+        const long long r0 = live < a.cap[m] ? (long long)(a.cap[m] - live) : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t v = w >> (8 * k) & 0xFFu, t = v & 7u;
+            if (((v >> 4) & 1u) == m && j + k < a.n) {
+                const long long lowest = r0 + P.m < 0 ? r0 + P.m : 0;
+                const long long R = r0 + P.s - lowest;
+                const uint32_t b = a.used[j + k];
+                bad |= (uint32_t)(R < (long long)t ? R : (long long)t) != (t < b ? t : b);
+                out |= (uint32_t)(R < 7 ? R : 7) << (8 * k);
+            }
+            P = sm_comb(P, eadm_elem(v, m));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (j + k < a.n) a.next[j + k] = (uint8_t)(out >> (8 * k));
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(a.flag, 1u);
+}
+
+int launch_egress_admission(const EAdmit &a, hipStream_t s)
+{
+    if (!a.n) return 0;
+    const uint32_t tiles = (a.n + SCAN_TILE - 1) / SCAN_TILE;
+    if (tiles > 4096) return -EINVAL;
+    (void)hipMemsetAsync(a.flag, 0, 4, s);
+    hipLaunchKernelGGL(k_eadm_tiles, dim3(tiles), dim3(1024), 0, s, a, tiles);
+    hipLaunchKernelGGL(k_eadm_top, dim3(1), dim3(1024), 0, s, a, tiles);
+    hipLaunchKernelGGL(k_eadm_apply, dim3(tiles), dim3(1024), 0, s, a, tiles);
     return launch_status(__func__);
 }
 

@@ -295,3 +295,35 @@ def test_ct_capacity_egress(dev):
     w = synth.config5(1 << 12, n_svc=2000, n_ep=256, n_remote=512, ct_max=1500)
     dp = check_egress(w, dev, batches=2, rounds=1)
     assert dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0       # DROP_CT_CREATE_FAILED happened
+
+
+def test_ct_capacity_egress_admitted(dev, monkeypatch):
+    """A 2^20-packet config-5 batch whose creates cross max_entries in CT4 (about 2/3 in)
+    and CT6 (about 3/4 in), at full width (cv_ctx.cpp lxc_admitted: the pipeline runs with
+    per-packet create budgets until the budget scan says every packet got the sequential
+    run's creates); then a batch into the full maps after the agent removed a third of the
+    ingress L4 policy entries, so denied established flows are deleted and later packets'
+    creates take the room, in packet order.  Verdicts, tables, counters, metrics exact."""
+    monkeypatch.setenv("CV_ADMIT_STATS", "1")
+    w = synth.config5(1 << 20, n_svc=20000, n_ep=1024, n_remote=4096, seed=81, ct_max=300_000)
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    for rnd in (0, 1):
+        if rnd == 1:
+            keys = w.maps["policy"].keys
+            for k in keys[(keys[:, 6] != 0) & (keys[:, 7] == 0)][::3]:           # ingress, L4
+                assert pm["policy"].delete(k.tobytes()) == 0 == om["policy"].delete(k.tobytes())
+        now = w.now + 3 * rnd
+        o = run_egress(ctx, w, dev, 0, w.n, now, events=False)
+        ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=now)
+        for k in FIELDS:
+            bad = np.nonzero(o[k] != getattr(ref, k))[0]
+            assert len(bad) == 0, (rnd, k, len(bad), bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+        assert (ctx.metrics() == dp.metrics()).all(), rnd
+        for name in ("ct4", "ct6", "policy"):
+            same_table(pm, om, name)
+        assert len(pm["ct4"]) == len(om["ct4"]) and len(pm["ct6"]) == len(om["ct6"])
+    m = dp.metrics()
+    assert m[155, 2, 0] + m[155, 1, 0] > 100_000                           # DROP_CT_CREATE_FAILED
+    assert len(om["ct4"]) == len(om["ct6"]) == 300_000
+    ctx.close()

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from cilium_amd import synth
+from cilium_amd import shard, synth
 from tests import harness as H
 
 pytestmark = pytest.mark.gpu
@@ -298,9 +298,45 @@ def test_config3_plain_instances(dev):
 
 
 def test_config3_hot_groups(dev):
-    # few flows -> groups far larger than the in-register limit, FIN/RST/SYN mixes
+    # few flows -> groups far larger than the in-register limit, FIN/RST/SYN mixes; the
+    # plain instance takes the wave-per-run path (k_ct_hot) for them
     w = synth.config3(1 << 15, 64, n_ep=16, n_cidrs=512, n_ids=50, seed=11)
     check_ingress(w, dev, batches=3)
+    check_ingress(w, dev, batches=3, events=False)
+
+
+def test_config3_zipf_hot_runs(dev):
+    """Elephant flows (Zipf 1.1 flow popularity: the largest address pairs carry
+    thousands of the batch's packets) through k_ct_hot, a wave per run: every output,
+    the counters and the CT table against the oracle over fresh batches, one after the
+    agent removed a third of the L4 policy entries -- established members of hot runs
+    are then denied and deleted, and later members of the same run create again --
+    so the chunks end at creates and deletes as well as running whole."""
+    w = synth.config3(1 << 18, 1 << 13, n_ep=64, n_cidrs=1024, n_ids=100, seed=61, zipf=1.1)
+    pk = shard.pair_key4(w.frames[:, 26:30].copy().view("<u4").ravel(), w.frames[:, 30:34].copy().view("<u4").ravel())
+    assert np.unique(pk, return_counts=True)[1].max() > 5000
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    for v in (0, 1, 2):
+        if v == 2:
+            keys = w.maps["policy"].keys
+            for k in keys[(keys[:, 6] != 0)][::3]:
+                assert pm["policy"].delete(k.tobytes()) == 0 == om["policy"].delete(k.tobytes())
+        f = H.apply_variant(w.frames, *synth.port_variant(w, v)) if v else w.frames
+        wv = synth.Workload(w.name, w.maps, f, w.length, w.mark, w.endpoints, now=w.now + v, extra=w.extra)
+        o = run_ingress(ctx, wv, dev, 0, w.n, events=False)
+        ref = dp.netdev_ingress(f, w.length, w.mark, now=w.now + v)
+        for k in ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason"):
+            bad = np.nonzero(o[k] != getattr(ref, k))[0]
+            assert len(bad) == 0, (v, k, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+        assert (ctx.metrics() == dp.metrics()).all(), v
+        ck, cv = pm["ct4"].dump()
+        ok, ov = om["ct4"].dump()
+        assert len(ck) == len(ok), v
+        assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), v
+        check_policy_maps(pm["policy"], om["policy"])
+    assert dp.metrics()[133, 1, 0] > 0                             # DROP_POLICY (the denied hot flows)
+    ctx.close()
 
 
 def test_config3_icmp_and_options(dev):

@@ -928,7 +928,15 @@ __device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, Ct
     e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
 }
 
-template <class S>
+// NT: the lookup-hit update (ct_hit), written with non-temporal stores -- an entry a
+// batch touches once leaves the L2 to the policy tables and endpoint descriptors
+#ifndef CV_NT_HIT
+#define CV_NT_HIT 0
+#endif
+typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t nt_u2 __attribute__((ext_vector_type(2)));
+
+template <class S, bool NT = false>
 __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, const CtE &e)
 {
     const HotAt<S> q = hot_at<S>(t, slot);
@@ -940,9 +948,15 @@ __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, c
     } else {
         u = make_uint4(h[0], h[1], h[2], h[3]); v = make_uint4(h[4], h[5], h[6], h[7]); w = make_uint2(h[8], h[9]);
     }
-    q.a[0] = u;
-    q.a[1] = v;
-    *q.b = w;
+    if constexpr (NT) {
+        __builtin_nontemporal_store(nt_u4{u.x, u.y, u.z, u.w}, reinterpret_cast<CV_G nt_u4 *>(q.a));
+        __builtin_nontemporal_store(nt_u4{v.x, v.y, v.z, v.w}, reinterpret_cast<CV_G nt_u4 *>(q.a + 1));
+        __builtin_nontemporal_store(nt_u2{w.x, w.y}, reinterpret_cast<CV_G nt_u2 *>(q.b));
+    } else {
+        q.a[0] = u;
+        q.a[1] = v;
+        *q.b = w;
+    }
 }
 
 template <class S>
@@ -1101,7 +1115,7 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         st->slave = e.w[10] & 0xFFFFu;
     }
     ct_hit_apply<S>(ct, slot, e, action, dir, tcp, seen, len, now, flags, mon);
-    ct_store_hot<S>(ct, slot, e);
+    ct_store_hot<S, CV_NT_HIT != 0>(ct, slot, e);
 }
 
 template <class S>

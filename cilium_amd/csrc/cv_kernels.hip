@@ -436,24 +436,28 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 // ------------------------------------------------------------------ hot runs
 // A group of many packets (an elephant flow: one address pair carrying thousands of
 // the batch's packets) walked by one lane costs a chain of dependent memory round trips
-// per member.  Runs of size class >= HOT_CLASS (more than 32 members) go to k_ct_hot,
-// a wave per run, 64 members at a time:
-//  1. every lane looks its member up against the table as the chunk starts (read only:
-//     ct_lookup_pre, policy_ingress_denies) and tells whether its ipv4_policy would
-//     change which keys exist -- a create (CT_NEW, allowed) or a delete (CT_ESTABLISHED,
-//     denied);
+// per member.  Runs of size class >= HOT_CLASS (more than 32 members) go to k_ct_hot, a
+// workgroup of HOTB threads per run, HOTB members at a time:
+//  1. every thread looks its member up against the table as the chunk starts (read
+//     only: ct_lookup_pre, policy_ingress_denies) and tells whether its ipv4_policy
+//     would change which keys exist -- a create (CT_NEW, allowed) or a delete
+//     (CT_ESTABLISHED, denied);
 //  2. the members before the first such one (c) change no key, so each sees exactly
 //     what the sequential run shows it: they finish in parallel (verdicts, policy
 //     counters, metrics), their hits' entry updates deferred;
-//  3. one lane applies those updates in member order (ct_hit_apply) to the entries held
-//     in LDS for the chunk and writes each entry back once;
+//  3. the deferred updates of one entry are folded in parallel (hot_fold): what an update
+//     does next depends on the entry only through three bits (RX / TX closing, seen
+//     non-SYN), so every member's update is an 8-state transition table, a block scan of
+//     their compositions gives each member the bits it meets, and the rest of the entry
+//     is a reduction -- the lifetime of the last update that set one, the OR of the
+//     flags seen per direction, the report stamps, the counter sums;
 //  4. member c runs whole (its create or delete), then the next chunk starts after it.
-// An elephant flow's established packets all take step 2: 64 members cost one round of
-// lookups instead of 64 dependent ones.  Only the plain instance (no event records,
+// An elephant flow's established packets all take step 2 and 3: a chunk of HOTB members
+// costs one round of lookups and a scan.  Only the plain instance (no event records,
 // whose trace decisions need the per-packet entry state) and launches without admission
 // budgets or guards use it; the others keep one lane per run.
 constexpr int HOT_CLASS = 12;                                     // size_class: runs of more than 32 members
-constexpr int HOT_CACHE = 8;                                      // entries one chunk's fold holds
+constexpr uint32_t HOTB = 1024;                                   // threads (members) per chunk
 
 __device__ __forceinline__ uint32_t hot_runs(const GroupScratch &g, int q)
 {
@@ -463,13 +467,158 @@ __device__ __forceinline__ uint32_t hot_runs(const GroupScratch &g, int q)
     return n;
 }
 
-struct HotWave {                                                  // per wave, LDS
-    unsigned long long hslot[64];                                 // the members' deferred hits (slot, ~0: none)
-    uint32_t hpar[64];                                            // action | dir << 2 | tcp << 4 | seen << 8
-    uint32_t hlen[64];
-    unsigned long long cslot[HOT_CACHE];                          // the fold's entries
-    uint32_t cw[HOT_CACHE][CT_HOTW];
+// The hit update ct_hit_apply (conntrack.h:213-258) as a function of the three bits it
+// reads, x = RX_CLOSING | TX_CLOSING << 1 | SEEN_NON_SYN << 2: the bits it leaves, whether
+// it ran __ct_update_timeout at all (every run uses the member's direction and flags) and
+// the lifetime of its last run.
+struct HitFx {
+    uint32_t x, any, life;
 };
+
+__device__ __forceinline__ HitFx hit_fx(uint32_t x, uint32_t action, uint32_t dir, uint32_t tcp, uint32_t seen)
+{
+    HitFx f{x, 0u, 0u};
+    auto alive = [&]() { return (f.x & 3u) != 3u; };
+    auto timeout = [&]() {                                        // ct_update_timeout (conntrack.h:169-186)
+        if (tcp && !(seen & TCPF_SYN)) f.x |= 4u;
+        f.life = tcp ? ((f.x & 4u) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT) : CT_LIFETIME_NONTCP;
+        f.any = 1u;
+    };
+    if (alive()) timeout();
+    if (action == ACTION_CREATE) {
+        if (f.x & 3u) { f.x &= ~3u; timeout(); }
+    } else if (action == ACTION_CLOSE) {
+        f.x |= dir == CT_INGRESS ? 1u : 2u;
+        if (!alive()) { f.life = CT_CLOSE_TIMEOUT; f.any = 1u; }  // __ct_update_timeout(CT_CLOSE_TIMEOUT)
+    }
+    return f;
+}
+
+constexpr uint32_t FX_IDENT = 0u | 1u << 3 | 2u << 6 | 3u << 9 | 4u << 12 | 5u << 15 | 6u << 18 | 7u << 21;
+__device__ __forceinline__ uint32_t fx_at(uint32_t T, uint32_t x) { return (T >> (3 * x)) & 7u; }
+__device__ __forceinline__ uint32_t fx_then(uint32_t A, uint32_t B)   // A, then B
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < 8; ++x) r |= fx_at(B, fx_at(A, x)) << (3 * x);
+    return r;
+}
+__device__ __forceinline__ uint32_t bits_x(uint32_t b)
+{
+    return (b & CTB_RX_CLOSING ? 1u : 0u) | (b & CTB_TX_CLOSING ? 2u : 0u) | (b & CTB_SEEN_NON_SYN ? 4u : 0u);
+}
+
+struct HotLds {
+    uint32_t c, lead, wscan[HOTB / 64], fxtot, fxlast, seen[2], any[2];
+    unsigned long long slot;
+    uint32_t pk[2], by[2];                                        // (a chunk's sums fit 32 bits)
+    uint32_t e[CT_HOTW];                                          // the folded entry's hot run (h0..h9)
+};
+
+// the block's exclusive scan of transition tables in thread order (its total in *tot)
+__device__ __forceinline__ uint32_t fx_scan(uint32_t T, HotLds &L, uint32_t *tot)
+{
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = T;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
+        if (lane >= (uint32_t)d) incl = fx_then(t, incl);
+    }
+    if (lane == 63) L.wscan[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = FX_IDENT;
+        for (uint32_t w = 0; w < nw; ++w) { const uint32_t t = L.wscan[w]; L.wscan[w] = acc; acc = fx_then(acc, t); }
+        L.fxtot = acc;
+    }
+    __syncthreads();
+    uint32_t ex = (uint32_t)__shfl_up((int)incl, 1, 64);
+    if (lane == 0) ex = FX_IDENT;
+    const uint32_t r = fx_then(L.wscan[wv], ex);
+    *tot = L.fxtot;
+    __syncthreads();
+    return r;
+}
+
+// step 3 for the entry at L.slot: the deferred hits of the participating threads (in
+// thread = member order) applied as the sequential run applies them one by one
+template <class S>
+__device__ __forceinline__ void hot_fold(const HashTable &ct, HotLds &L, bool part, const HitRec &hr, uint32_t now,
+                                         uint32_t flags)
+{
+    const int64_t slot = (int64_t)L.slot;
+    if (threadIdx.x == 0) {
+        CtE e;
+        ct_load_hot<S>(ct, slot, e);
+        L.e[0] = e.w[8]; L.e[1] = e.w[9]; L.e[2] = e.w[10]; L.e[3] = e.w[11]; L.e[4] = e.w[12]; L.e[5] = e.w[13];
+        L.e[6] = e.w[0]; L.e[7] = e.w[2]; L.e[8] = e.w[4]; L.e[9] = e.w[6];
+        L.fxlast = 0; L.seen[0] = L.seen[1] = 0; L.any[0] = L.any[1] = 0;
+        L.pk[0] = L.pk[1] = L.by[0] = L.by[1] = 0;
+    }
+    __syncthreads();
+    uint32_t T = FX_IDENT;
+    if (part) {
+        T = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < 8; ++x) T |= hit_fx(x, hr.action, hr.dir, hr.tcp, hr.seen).x << (3 * x);
+    }
+    uint32_t tot;
+    const uint32_t pre = fx_scan(T, L, &tot);                    // (ends with a barrier)
+    const uint32_t x0 = bits_x(L.e[1] & 0xFFFFu);
+    const bool rx = hr.dir == CT_INGRESS;
+    if (part) {
+        const HitFx f = hit_fx(fx_at(pre, x0), hr.action, hr.dir, hr.tcp, hr.seen);
+        if (f.any) {
+            atomicMax(&L.fxlast, (threadIdx.x + 1) << 8 | (f.life == CT_LIFETIME_TCP ? 1u : f.life == CT_CLOSE_TIMEOUT ? 2u
+                                                                                      : 0u));
+            atomicOr(&L.seen[rx ? 1 : 0], hr.seen & 0xFFu);
+            atomicOr(&L.any[rx ? 1 : 0], 1u);
+        }
+        if (flags & F_CT_ACCOUNTING) {
+            atomicAdd(&L.pk[rx ? 1 : 0], 1u);
+            atomicAdd(&L.by[rx ? 1 : 0], hr.len);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t *h = L.e;                                        // h0 = w8 (lifetime), h1 = w9 (bits), h2 = w10 (flags seen)
+        const uint32_t x1 = fx_at(tot, x0);
+        uint32_t b = h[1] & ~(uint32_t)(CTB_RX_CLOSING | CTB_TX_CLOSING | CTB_SEEN_NON_SYN);
+        b |= (x1 & 1u ? CTB_RX_CLOSING : 0u) | (x1 & 2u ? CTB_TX_CLOSING : 0u) | (x1 & 4u ? CTB_SEEN_NON_SYN : 0u);
+        h[1] = b;
+        if (L.fxlast) {
+            const uint32_t lc = L.fxlast & 0xFFu;                  // (NONTCP and SYN_TIMEOUT are both 60 s)
+            h[0] = now + (lc == 1u ? CT_LIFETIME_TCP : lc == 2u ? CT_CLOSE_TIMEOUT : CT_LIFETIME_NONTCP);
+        }
+        for (int d = 0; d < 2; ++d) {                             // __ct_update_timeout's reports (0 tx, 1 rx)
+            if (!L.any[d]) continue;
+            const int fsh = d ? 24 : 16, li = d ? 5 : 4;           // rx_flags_seen / tx_flags_seen; last_rx / tx_report
+            const uint32_t acc = (h[2] >> fsh) & 0xFFu, nacc = acc | L.seen[d];
+            if (h[li] + CT_REPORT_INTERVAL < now || nacc != acc) {
+                h[li] = now;
+                h[2] = (h[2] & ~(0xFFu << fsh)) | (nacc << fsh);
+            }
+        }
+        CtE e;
+        e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
+        e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
+        if (flags & F_CT_ACCOUNTING) {                            // ct_count: low words in place, carries to the side slot
+            for (int d = 0; d < 2; ++d) {
+                const int k0 = d ? 0 : 4;                          // rx_packets / rx_bytes @0 / 2, tx @4 / 6
+                const unsigned long long sp = (unsigned long long)e.w[k0] + L.pk[d];
+                const unsigned long long sb = (unsigned long long)e.w[k0 + 2] + L.by[d];
+                e.w[k0] = (uint32_t)sp;
+                e.w[k0 + 2] = (uint32_t)sb;
+                CV_G uint32_t *cold = ct_cold<S>(ct, slot);
+                if (sp >> 32) cold[k0 >> 1] += (uint32_t)(sp >> 32);
+                if (sb >> 32) cold[(k0 + 2) >> 1] += (uint32_t)(sb >> 32);
+            }
+        }
+        ct_store_hot<S>(ct, slot, e);
+    }
+    __syncthreads();
+}
 
 // ipv4_policy (bpf_lxc.c:865-979) of a member that creates and deletes nothing: its
 // lookup (ct_lookup_pre) hit -- the entry update deferred to the fold -- or missed with
@@ -511,35 +660,21 @@ __device__ __forceinline__ int hot_finish(const DpParams &p, const EpDev &ep, Sk
     return TC_ACT_SHOT;
 }
 
-__device__ __forceinline__ void hot_cache_flush(const HashTable &ct, HotWave &w, int n)
-{
-    for (int u = 0; u < n; ++u) {
-        CtE e;
-        const uint32_t *h = w.cw[u];
-        e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
-        e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
-        ct_store_hot<Ct4Spec>(ct, (int64_t)w.cslot[u], e);
-    }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_ct_hot(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+__global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
-    __shared__ HotWave hws[BLOCK / 64];
+    __shared__ HotLds L;
     using M = MetT<false>;
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
     m.pc = &pc;
-    HotWave &w = hws[threadIdx.x >> 6];
-    const uint32_t lane = threadIdx.x & 63;
     const uint32_t nhot = hot_runs(g, Q_NETDEV);
-    const uint32_t nw = (gridDim.x * BLOCK) >> 6;
-    for (uint32_t r = (blockIdx.x * BLOCK + threadIdx.x) >> 6; r < nhot; r += nw) {   // a wave per run
+    for (uint32_t r = blockIdx.x; r < nhot; r += gridDim.x) {     // a workgroup per run
         const uint32_t off = g.work[r], cnt = g.order[off];
-        for (uint32_t k0 = 0; k0 < cnt;) {                        // (wave-uniform)
-            const uint32_t k = k0 + lane;
+        for (uint32_t k0 = 0; k0 < cnt;) {                        // (block-uniform)
+            const uint32_t k = k0 + threadIdx.x;
             const bool live = k < cnt;
             const uint32_t x = live ? g.order[off + 1 + k] : 0u;
             uint4 s0{}, s1{};
@@ -560,10 +695,13 @@ __global__ void __launch_bounds__(BLOCK) k_ct_hot(DpParams p, BatchDev b, OutDev
             const int ret = simple ? ct_lookup_pre(ep.ct4, t, s.h, CT_INGRESS, s.len, slot, &st, a, hr) : 0;
             const bool deny = simple && ret >= 0 && policy_ingress_denies(ep.policy, p.flags, s1.w, t.dport, t.nexthdr);
             const bool change = simple && ((ret == CT_ESTABLISHED && deny) || (ret == CT_NEW && !deny));
-            const unsigned long long chg = __ballot(change);
-            const uint32_t c = chg ? (uint32_t)(__ffsll((long long)chg) - 1) : 64u;
+            if (threadIdx.x == 0) L.c = HOTB;
+            __syncthreads();
+            if (change) atomicMin(&L.c, threadIdx.x);
+            __syncthreads();
+            const uint32_t c = L.c;
             // 2. the members before c, in parallel
-            if (live && lane < c) {
+            if (live && threadIdx.x < c) {
                 uint8_t ct = CT_NONE;
                 uint16_t proxy = 0;
                 int32_t reason = 0;
@@ -581,65 +719,40 @@ __global__ void __launch_bounds__(BLOCK) k_ct_hot(DpParams p, BatchDev b, OutDev
                 if (o.proxy) o.proxy[x] = proxy;
                 store_out(o, x, a);
             }
-            // 3. their hits' entry updates in member order, each entry written once
-            w.hslot[lane] = (live && lane < c && hr.slot >= 0) ? (unsigned long long)hr.slot : ~0ull;
-            w.hpar[lane] = hr.action | hr.dir << 2 | hr.tcp << 4 | hr.seen << 8;
-            w.hlen[lane] = hr.len;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const HashTable ct = ep_stage4<false>(p, __shfl(meta, 0, 64) & 0xFFFFu).ct4;   // (the run's CT map)
-            if (lane == 0) {
-                int n = 0;
-                const uint32_t upto = c < cnt - k0 ? c : cnt - k0;
-                for (uint32_t j = 0; j < upto; ++j) {
-                    const unsigned long long sl = w.hslot[j];
-                    if (sl == ~0ull) continue;
-                    int q = -1;
-                    for (int u = 0; u < n; ++u)
-                        if (w.cslot[u] == sl) q = u;
-                    if (q < 0) {
-                        if (n == HOT_CACHE) { hot_cache_flush(ct, w, n); n = 0; }
-                        q = n++;
-                        w.cslot[q] = sl;
-                        CtE e;
-                        ct_load_hot<Ct4Spec>(ct, (int64_t)sl, e);
-                        uint32_t *h = w.cw[q];
-                        h[0] = e.w[8]; h[1] = e.w[9]; h[2] = e.w[10]; h[3] = e.w[11]; h[4] = e.w[12]; h[5] = e.w[13];
-                        h[6] = e.w[0]; h[7] = e.w[2]; h[8] = e.w[4]; h[9] = e.w[6];
-                    }
-                    uint32_t *h = w.cw[q];
-                    CtE e;
-                    e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
-                    e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
-                    const uint32_t pr = w.hpar[j];
-                    ct_hit_apply<Ct4Spec>(ct, (int64_t)sl, e, (int)(pr & 3u), (int)((pr >> 2) & 3u), (pr >> 4) & 1u,
-                                          pr >> 8, w.hlen[j], now, p.flags, nullptr);
-                    h[0] = e.w[8]; h[1] = e.w[9]; h[2] = e.w[10]; h[3] = e.w[11]; h[4] = e.w[12]; h[5] = e.w[13];
-                    h[6] = e.w[0]; h[7] = e.w[2]; h[8] = e.w[4]; h[9] = e.w[6];
-                }
-                hot_cache_flush(ct, w, n);
+            // 3. their hits' entry updates, entry by entry, in member order
+            const HashTable ct = ep_stage4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;   // (the run's map)
+            bool pend = live && threadIdx.x < c && hr.slot >= 0;
+            while (__syncthreads_or(pend)) {
+                if (threadIdx.x == 0) L.lead = HOTB;
+                __syncthreads();
+                if (pend) atomicMin(&L.lead, threadIdx.x);
+                __syncthreads();
+                if (threadIdx.x == L.lead) L.slot = (unsigned long long)hr.slot;
+                __syncthreads();
+                const bool part = pend && (unsigned long long)hr.slot == L.slot;
+                hot_fold<Ct4Spec>(ct, L, part, hr, now, p.flags);
+                pend &= !part;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (the entries written before any re-read)
             l1_inv();
-            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
             // 4. member c whole: its create or delete, against the table the fold left
-            if (chg && lane == c) {
+            if (c < HOTB && threadIdx.x == c) {
                 Acct a1{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
-                uint8_t ct = CT_NONE;
+                uint8_t ct1 = CT_NONE;
                 uint16_t proxy = 0;
                 int32_t reason = 0;
-                const int rv = handle_policy4<M, false>(p, ep, s, s1.w, skip_proxy, ifx, now, ct, proxy, reason, a1, m);
+                const int rv = handle_policy4<M, false>(p, ep, s, s1.w, skip_proxy, ifx, now, ct1, proxy, reason, a1, m);
                 if (o.ret) o.ret[x] = rv;
                 if (o.reason) o.reason[x] = reason;
-                if (o.ct) o.ct[x] = ct;
+                if (o.ct) o.ct[x] = ct1;
                 if (o.proxy) o.proxy[x] = proxy;
                 store_out(o, x, a1);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             l1_inv();
-            __builtin_amdgcn_wave_barrier();
-            k0 += chg ? c + 1 : 64u;
+            __syncthreads();
+            k0 += c < HOTB ? c + 1 : HOTB;
         }
     }
     met_flush(m, p.metrics);                                      // (ends with a barrier)
@@ -844,9 +957,9 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Out
 // k_gkey_hist counts the keys per (bin = the key's top gbits bits, binning block) in
 // LDS; three small kernels scan the counts into offsets; k_gkey_scatter writes every
 // staged packet as {packet, key low word} into its bin's slice; k_gbin_group sorts each
-// bin by (key low word, packet) -- in LDS, or for a bin past LCAP entries (a hot
-// address pair) in global memory -- so a group's members end up contiguous and in packet
-// order, and writes the runs {size, members} into `order`; k_heads_count / k_heads_place
+// bin by (key low word, packet) in LDS -- a bin past LCAP entries by sub-bins, and a
+// hot address pair's members by packet through a bitmap (gbin_split_key) -- so a group's
+// members end up contiguous and in packet order, and writes the runs {size, members} into `order`; k_heads_count / k_heads_place
 // list the groups' first packets in packet order, size class by size class (the
 // `work` and `single` lists for_each_run reads).  Keys that share the bin bits and the
 // low word merge into one group (about 2^-32 per pair of groups in a bin): a coarser
@@ -1008,117 +1121,319 @@ __device__ __forceinline__ void bitonic_sort(P v, uint32_t p)
 constexpr uint32_t SUBMAX = 48;                                  // largest sub-bin sorted by insertion
 __device__ __forceinline__ uint32_t sub_of(unsigned long long composite) { return (uint32_t)(composite >> 34) & 255u; }
 
-__global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g)
+// base[idx] += 1 for the active lanes, returning each its old value, with one LDS atomic
+// for all the lanes that share the first active lane's counter: a bin or tile of a hot
+// address pair sends nearly every lane to one counter, which plain LDS atomics serialise
+__device__ __forceinline__ uint32_t lds_inc(uint32_t *base, uint32_t idx, bool active)
 {
-    __shared__ unsigned long long lv[LCAP];
-    __shared__ uint16_t perm[LCAP];
-    __shared__ uint32_t sub_cnt[256], sub_off[256], sub_max, wsum[17], fill, big[2];
-    const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
-    const uint32_t start = g.gcnt[b * GBLK], end = b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m];
-    const uint32_t nb = end - start;
-    if (!nb) return;                                              // (block-uniform)
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long act = __ballot(active);
+    if (!act) return 0;
+    const int l = __ffsll((long long)act) - 1;
+    const uint32_t li = (uint32_t)__shfl((int)idx, l, 64);
+    const unsigned long long same = __ballot(active && idx == li);
+    uint32_t b = 0;
+    if (lane == (uint32_t)l) b = atomicAdd(&base[li], (uint32_t)__popcll(same));
+    b = (uint32_t)__shfl((int)b, l, 64);
+    if ((same >> lane) & 1ull) return b + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+    return active ? atomicAdd(&base[idx], 1u) : 0u;
+}
+
+struct GbinLds {                                                  // k_gbin_group's LDS
+    unsigned long long lv[LCAP];                                  // (a split key's tile bitmap when not sorting)
+    uint16_t perm[LCAP];
+    uint32_t sub_cnt[256], sub_off[256], sub_max, wsum[17], fill, big[2];
+    uint32_t bcnt[256], boff[256], bfill[256];                    // a bin past LCAP: its sub-bins
+    uint32_t pcnt[256], poff[256];                                // a split key: its members per scatter tile
+    uint32_t rest, mcount, key, head[NPOS];
+};
+
+// v[0, nb) (nb <= LCAP) sorted by composite in LDS: a counting sort by 8 more key bits
+// (sub-bins of a few entries), then every entry ranked within its sub-bin by its own
+// thread (a rank sort: m compares per entry, all entries at once; one insertion sort per
+// sub-bin and thread spent m^2 steps on its largest sub-bin); a sub-bin past SUBMAX takes
+// the bitonic sort instead
+__device__ void gbin_lds_sort(GbinLds &L, uint32_t nb)
+{
+    unsigned long long *lv = L.lv;
     uint32_t p = 64;
     while (p < nb) p <<= 1;
-    if (threadIdx.x == 0) fill = 0;
-    if (threadIdx.x < 2) big[threadIdx.x] = 0;
-    // composite {key low word, packet}: sorted, a group's members are contiguous and ascending
-    unsigned long long *gv = g.gbig + 2 * (size_t)start;          // (a bin past LCAP: 2 words per entry)
-    const bool in_lds = nb <= LCAP;
-    for (uint32_t j = threadIdx.x; j < p; j += blockDim.x) {
-        unsigned long long x = ~0ull;
-        if (j < nb) { const uint2 e = g.gent[start + j]; x = (unsigned long long)e.y << 32 | e.x; }
-        if (in_lds) lv[j] = x; else gv[j] = x;
+    for (uint32_t j = nb + threadIdx.x; j < p; j += blockDim.x) lv[j] = ~0ull;
+    uint32_t *cnt = L.sub_cnt, *off = L.sub_off;
+    cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) L.sub_max = 0;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) atomicAdd(&cnt[sub_of(lv[j])], 1u);
+    __syncthreads();
+    uint32_t total;
+    const uint32_t mine = cnt[threadIdx.x];
+    off[threadIdx.x] = block_excl_scan(mine, L.wsum, total);
+    atomicMax(&L.sub_max, mine);
+    cnt[threadIdx.x] = 0;                                         // (reused as the fill counters)
+    __syncthreads();
+    if (L.sub_max > SUBMAX) {
+        bitonic_sort(lv, p);
+        return;
+    }
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        const uint32_t sb = sub_of(lv[j]);
+        L.perm[off[sb] + atomicAdd(&cnt[sb], 1u)] = (uint16_t)j;
     }
     __syncthreads();
-    if (in_lds) {
-        // counting sort by 8 more key bits (sub-bins of a few entries), then every entry
-        // ranked within its sub-bin by its own thread (a rank sort: m compares per entry,
-        // all entries at once; one insertion sort per sub-bin and thread spent m^2 steps
-        // on its largest sub-bin); a bin with a sub-bin past SUBMAX (a hot address pair)
-        // takes the bitonic sort instead
-        uint32_t *cnt = sub_cnt, *off = sub_off;
-        cnt[threadIdx.x] = 0;
-        if (threadIdx.x == 0) sub_max = 0;
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) atomicAdd(&cnt[sub_of(lv[j])], 1u);
-        __syncthreads();
-        uint32_t total;
-        const uint32_t mine = cnt[threadIdx.x];
-        off[threadIdx.x] = block_excl_scan(mine, wsum, total);
-        atomicMax(&sub_max, mine);
-        cnt[threadIdx.x] = 0;                                     // (reused as the fill counters)
-        __syncthreads();
-        if (sub_max > SUBMAX) {
-            bitonic_sort(lv, p);
-        } else {
-            for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
-                const uint32_t sb = sub_of(lv[j]);
-                perm[off[sb] + atomicAdd(&cnt[sb], 1u)] = (uint16_t)j;
-            }
-            __syncthreads();
-            uint32_t dst[LCAP / 256];
-            unsigned long long val[LCAP / 256];
+    uint32_t dst[LCAP / 256];
+    unsigned long long val[LCAP / 256];
 #pragma unroll
-            for (uint32_t k = 0; k < LCAP / 256; ++k) {
-                const uint32_t j = threadIdx.x + k * 256;
-                if (j < nb) {
-                    const unsigned long long xv = lv[j];
-                    const uint32_t sb = sub_of(xv), o = off[sb], c = cnt[sb];
-                    uint32_t rank = 0;
-                    for (uint32_t q = o; q < o + c; ++q) rank += lv[perm[q]] < xv ? 1u : 0u;   // (composites differ)
-                    dst[k] = o + rank;
-                    val[k] = xv;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t k = 0; k < LCAP / 256; ++k) {
-                const uint32_t j = threadIdx.x + k * 256;
-                if (j < nb) lv[dst[k]] = val[k];
-            }
-            __syncthreads();
+    for (uint32_t k = 0; k < LCAP / 256; ++k) {
+        const uint32_t j = threadIdx.x + k * 256;
+        if (j < nb) {
+            const unsigned long long xv = lv[j];
+            const uint32_t sb = sub_of(xv), o = off[sb], c = cnt[sb];
+            uint32_t rank = 0;
+            for (uint32_t q = o; q < o + c; ++q) rank += lv[L.perm[q]] < xv ? 1u : 0u;   // (composites differ)
+            dst[k] = o + rank;
+            val[k] = xv;
         }
-    } else {
-        bitonic_sort(gv, p);
     }
-    const unsigned long long *v = in_lds ? lv : gv;
-    // one pass: the runs into the bin's own region of `order` (2 words per entry: a run
-    // of c members takes c + 1 <= 2c; no allocation atomics), and every group's first
-    // packet marked with its list and run (k_heads_place lists them in packet order)
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < LCAP / 256; ++k) {
+        const uint32_t j = threadIdx.x + k * 256;
+        if (j < nb) lv[dst[k]] = val[k];
+    }
+    __syncthreads();
+}
+
+// the first packets of a group of c members: its `hword` marks (and, from NPOS members
+// on for position lists, or from 2 members on for runs, its run at `off` in `order`)
+__device__ __forceinline__ void gbin_mark(const GroupScratch &g, uint32_t key, uint32_t c, uint32_t off,
+                                          const uint32_t *first, uint32_t *big)
+{
+    const uint32_t q6 = key & 1u;
+    if (c > 8) atomicMax(&big[q6], c);
+    if (g.flat) {
+        const uint32_t m = c < NPOS ? c : NPOS;
+        for (uint32_t t = 0; t < m; ++t)
+            g.hword[first[t]] = (1u + q6 * 16 + t) << 26 | (t + 1 == NPOS ? off : 0u);
+        return;
+    }
+    const uint32_t list = c > 1 ? 15 - (uint32_t)size_class(c) : 15u;   // 15: singletons (bit 25: a singleton)
+    g.hword[first[0]] = (1u + q6 * 16 + list) << 26 | (c > 1 ? off : 1u << 25);
+}
+
+// one pass over the sorted v[0, nb): the runs into the bin's own region of `order` (2
+// words per entry: a run of c members takes c + 1 <= 2c; no allocation atomics), and
+// every group's first packet marked with its list and run (k_heads_place lists them in
+// packet order)
+__device__ void gbin_emit(const GroupScratch &g, GbinLds &L, const unsigned long long *v, uint32_t nb, uint32_t start)
+{
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
         const uint32_t key = (uint32_t)(v[j] >> 32);
         if (j && (uint32_t)(v[j - 1] >> 32) == key) continue;     // not a group's first member
         uint32_t c = 1;
         while (j + c < nb && (uint32_t)(v[j + c] >> 32) == key) ++c;
-        const uint32_t q6 = key & 1u, x = (uint32_t)v[j];
-        if (g.flat) {                                             // position lists (egress)
-            uint32_t off = 0;
-            if (c >= NPOS) {                                      // the continuation list needs the run
-                off = 2 * start + atomicAdd(&fill, c + 1);
-                uint32_t *o = g.order + off;
-                o[0] = c;
-                for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
-            }
-            if (c > 8) atomicMax(&big[q6], c);
-            const uint32_t m = c < NPOS ? c : NPOS;
-            for (uint32_t t = 0; t < m; ++t)
-                g.hword[(uint32_t)v[j + t]] = (1u + q6 * 16 + t) << 26 | (t + 1 == NPOS ? off : 0u);
-            continue;
-        }
-        uint32_t list = 15u, off = 1u << 25;                      // 15: singletons (bit 25: a singleton)
-        if (c > 1) {
-            off = 2 * start + atomicAdd(&fill, c + 1);
+        uint32_t off = 0, first[NPOS];
+        if (c >= (g.flat ? NPOS : 2u)) {                          // (position lists: the continuation list)
+            off = 2 * start + atomicAdd(&L.fill, c + 1);
             uint32_t *o = g.order + off;
             o[0] = c;
             for (uint32_t t = 0; t < c; ++t) o[1 + t] = (uint32_t)v[j + t];
-            list = 15 - (uint32_t)size_class(c);                  // largest class first
-            if (c > 8) atomicMax(&big[q6], c);
         }
-        g.hword[x] = (1u + q6 * 16 + list) << 26 | off;
+        for (uint32_t t = 0; t < NPOS && t < c; ++t) first[t] = (uint32_t)v[j + t];
+        gbin_mark(g, key, c, off, first, L.big);
+    }
+}
+
+// A sub-bin past LCAP entries (an elephant: one address pair carrying thousands of the
+// launch's packets) at r[0, cnt): the key most of 64 samples hold is taken out, its members
+// ordered by packet with a bitmap in LDS per scatter tile -- k_gkey_scatter writes a tile's
+// entries in any order, but the tiles in packet order -- and written as one run; the
+// rest stays at r[0, L.rest) for the next key.  Members past the bitmap go through m.
+__device__ void gbin_split_key(const GroupScratch &g, GbinLds &L, unsigned long long *r, uint32_t cnt,
+                               uint32_t *m, uint32_t start, uint32_t tile)
+{
+    __syncthreads();                                              // (every thread has read the last call's rest)
+    // the key: the most frequent of 64 evenly spaced samples (wave 0)
+    if (threadIdx.x < 64) {
+        const uint32_t sk = (uint32_t)(r[(unsigned long long)threadIdx.x * cnt / 64] >> 32);
+        uint32_t same = 0;
+        for (int l = 0; l < 64; ++l) same += __shfl(sk, l, 64) == sk ? 1u : 0u;
+        uint32_t best = same << 6 | (63u - threadIdx.x);          // (ties: the lowest lane)
+        for (int d = 32; d; d >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, d, 64));
+        if (threadIdx.x == 63u - (best & 63u)) L.key = sk;
+    }
+    L.pcnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) { L.rest = 0; L.mcount = 0; }
+    __syncthreads();
+    const uint32_t key = L.key;
+    for (uint32_t j0 = 0; j0 < cnt; j0 += GUNROLL * blockDim.x) { // its members per scatter tile
+        unsigned long long xs[GUNROLL];                           // (GUNROLL loads in flight: one block
+#pragma unroll                                                    //  streams the whole hot bin)
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
+            xs[u] = j < cnt ? r[j] : ~0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            const bool mine = (uint32_t)(xs[u] >> 32) == key && xs[u] != ~0ull;
+            lds_inc(L.pcnt, mine ? (uint32_t)xs[u] / tile : 0u, mine);
+        }
     }
     __syncthreads();
-    if (threadIdx.x < 2 && big[threadIdx.x])                      // (diagnostics: the largest group)
-        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? g.q6 : g.q4)], big[threadIdx.x]);
+    uint32_t total;
+    L.poff[threadIdx.x] = block_excl_scan(L.pcnt[threadIdx.x], L.wsum, total);
+    L.bfill[threadIdx.x] = 0;
+    __syncthreads();
+    // members to m by tile; the others packed to the front of r (a chunk is read whole
+    // before any of it is overwritten: the write position never passes the read one)
+    for (uint32_t j0 = 0; j0 < cnt; j0 += GUNROLL * blockDim.x) {
+        unsigned long long xs[GUNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
+            xs[u] = j < cnt ? r[j] : ~0ull;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < GUNROLL; ++u) {
+            const unsigned long long x = xs[u];
+            const bool live = x != ~0ull, mine = live && (uint32_t)(x >> 32) == key, other = live && !mine;
+            const uint32_t t = mine ? (uint32_t)x / tile : 0u;
+            const uint32_t at = lds_inc(L.bfill, t, mine);
+            if (mine) m[L.poff[t] + at] = (uint32_t)x;
+            const uint32_t ro = lds_inc(&L.rest, 0u, other);
+            if (other) r[ro] = x;
+        }
+    }
+    __syncthreads();
+    // the run: tile by tile, the members' bits set in LDS, then read back in order
+    const uint32_t c = total;
+    const bool listed = c >= (g.flat ? NPOS : 2u);                // (a run in `order`; its offset may be 0)
+    if (threadIdx.x == 0) L.mcount = listed ? 2 * start + atomicAdd(&L.fill, c + 1) : 0u;
+    __syncthreads();
+    const uint32_t off = L.mcount;
+    uint32_t *o = g.order + off;
+    if (threadIdx.x == 0 && listed) o[0] = c;
+    uint32_t *bm = reinterpret_cast<uint32_t *>(L.lv);            // tile bits (tile <= 2^16: 8 KiB)
+    constexpr uint32_t BMW = 2048;
+    for (uint32_t t = 0; t < GBLK; ++t) {
+        const uint32_t pc = L.pcnt[t], po = L.poff[t];            // (block-uniform)
+        if (!pc) continue;
+        for (uint32_t w = threadIdx.x; w < BMW; w += blockDim.x) bm[w] = 0;
+        __syncthreads();
+        const uint32_t base = t * tile;
+        for (uint32_t q = threadIdx.x; q < pc; q += blockDim.x) {
+            const uint32_t d = m[po + q] - base;
+            atomicOr(&bm[d >> 5], 1u << (d & 31));
+        }
+        __syncthreads();
+        constexpr uint32_t PER = BMW / 256;                       // words per thread, in order
+        uint32_t wv[PER], n1 = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) { wv[k] = bm[threadIdx.x * PER + k]; n1 += __popc(wv[k]); }
+        uint32_t tot;
+        uint32_t rank = po + block_excl_scan(n1, L.wsum, tot);
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k)
+            for (uint32_t w = wv[k]; w; w &= w - 1) {
+                const uint32_t x = base + (threadIdx.x * PER + k) * 32 + (uint32_t)__ffs((int)w) - 1;
+                if (listed) o[1 + rank] = x;
+                if (rank < NPOS) L.head[rank] = x;
+                ++rank;
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gbin_mark(g, key, c, off, L.head, L.big);
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g, uint32_t n)
+{
+    __shared__ GbinLds L;
+    const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
+    const uint32_t start = g.gcnt[b * GBLK], end = b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m];
+    const uint32_t nb = end - start;
+    if (!nb) return;                                              // (block-uniform)
+    if (threadIdx.x == 0) L.fill = 0;
+    if (threadIdx.x < 2) L.big[threadIdx.x] = 0;
+    // composite {key low word, packet}: sorted, a group's members are contiguous and ascending
+    if (nb <= LCAP) {
+        for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+            const uint2 e = g.gent[start + j];
+            L.lv[j] = (unsigned long long)e.y << 32 | e.x;
+        }
+        __syncthreads();
+        gbin_lds_sort(L, nb);
+        gbin_emit(g, L, L.lv, nb, start);
+    } else {
+        // a bin past LCAP: its entries by 8 more key bits into sub-bins (gbig: 2 words per
+        // entry, the second half the split keys' member lists), sub-bins of up to LCAP
+        // sorted in LDS a batch at a time, a larger one split key by key
+        unsigned long long *gv = g.gbig + 2 * (size_t)start;
+        uint32_t *mem = reinterpret_cast<uint32_t *>(gv + nb);
+        const uint32_t tile = (n + GBLK - 1) / GBLK;
+        L.bcnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < nb; j0 += GUNROLL * blockDim.x) {
+            uint2 es[GUNROLL];
+#pragma unroll
+            for (uint32_t u = 0; u < GUNROLL; ++u) {
+                const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
+                es[u] = j < nb ? g.gent[start + j] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < GUNROLL; ++u)
+                lds_inc(L.bcnt, sub_of((unsigned long long)es[u].y << 32 | es[u].x),
+                        j0 + u * blockDim.x + threadIdx.x < nb);
+        }
+        __syncthreads();
+        uint32_t total;
+        L.boff[threadIdx.x] = block_excl_scan(L.bcnt[threadIdx.x], L.wsum, total);
+        L.bfill[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < nb; j0 += GUNROLL * blockDim.x) {
+            uint2 es[GUNROLL];
+#pragma unroll
+            for (uint32_t u = 0; u < GUNROLL; ++u) {
+                const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
+                es[u] = j < nb ? g.gent[start + j] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < GUNROLL; ++u) {
+                const bool live = j0 + u * blockDim.x + threadIdx.x < nb;
+                const unsigned long long x = (unsigned long long)es[u].y << 32 | es[u].x;
+                const uint32_t sb = sub_of(x);
+                const uint32_t at = lds_inc(L.bfill, sb, live);
+                if (live) gv[L.boff[sb] + at] = x;
+            }
+        }
+        __syncthreads();
+        for (uint32_t sb = 0; sb < 256;) {                        // (block-uniform)
+            uint32_t cnt = L.bcnt[sb];
+            if (cnt > LCAP) {
+                unsigned long long *r = gv + L.boff[sb];
+                while (cnt > LCAP) {
+                    gbin_split_key(g, L, r, cnt, mem, start, tile);
+                    cnt = L.rest;
+                }
+                for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) L.lv[j] = r[j];
+                ++sb;
+            } else {
+                const uint32_t lo = L.boff[sb];
+                cnt = 0;
+                while (sb < 256 && cnt + L.bcnt[sb] <= LCAP) cnt += L.bcnt[sb++];
+                for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) L.lv[j] = gv[lo + j];
+            }
+            __syncthreads();
+            if (cnt) {
+                gbin_lds_sort(L, cnt);
+                gbin_emit(g, L, L.lv, cnt, start);
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 && L.big[threadIdx.x])                    // (diagnostics: the largest group)
+        atomicMax(&g.cursor[GMAX_WORD0 + (threadIdx.x ? g.q6 : g.q4)], L.big[threadIdx.x]);
 }
 
 // The groups' first packets listed in packet order, list by list (IPv4 runs class
@@ -1175,7 +1490,7 @@ void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
     hipLaunchKernelGGL(k_gkey_hist, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
     launch_scan(g.gcnt, m, g.gcnt + m + 1, g.gcnt + m, false, s);
     hipLaunchKernelGGL(k_gkey_scatter, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
-    hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g, n);
     const uint32_t tiles = (n + HTILE - 1) / HTILE;
     hipLaunchKernelGGL(k_heads_count, dim3(tiles), dim3(1024), 0, s, g, n, tiles);
     launch_scan(g.hcnt, 32 * tiles, g.hcnt + 32 * tiles + 1, g.hcnt + 32 * tiles, false, s);
@@ -1493,7 +1808,7 @@ int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, con
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     // the hot runs by whole waves (plain instance, no admission budgets or guards)
     const int hot = !ev && !p.ct_guard && !p.budget && !getenv("CV_NO_HOT_RUNS");
-    if (hot) hipLaunchKernelGGL(k_ct_hot, dim3(1024), blk, 0, s, p, b, o, g, now);
+    if (hot) hipLaunchKernelGGL(k_ct_hot, dim3(512), dim3(HOTB), 0, s, p, b, o, g, now);
     if (ev) hipLaunchKernelGGL(k_ct_stage<true>, grid, blk, 0, s, p, b, o, g, now, 0);
     else hipLaunchKernelGGL(k_ct_stage<false>, grid, blk, 0, s, p, b, o, g, now, hot);
     GroupScratch g6 = g;

@@ -105,6 +105,17 @@ def sorted_rows(keys, vals):
     return rows[order]
 
 
+def rows_diff(a, b):
+    """where two sorted_rows tables differ: the row count, or the differing byte columns
+    and the first differing row of each (for assertion messages)"""
+    if a.shape != b.shape:
+        return f"shapes {a.shape} vs {b.shape}"
+    bad = np.nonzero((a != b).any(axis=0))[0]
+    r = np.nonzero((a != b).any(axis=1))[0]
+    return f"{len(r)} rows differ in byte columns {bad.tolist()}; first: {a[r[0]].tolist()} vs {b[r[0]].tolist()}" \
+        if len(r) else "equal"
+
+
 def apply_variant(frames, rows, offs, ports):
     """frames with the 2-byte big-endian ports of synth.port_variant written in"""
     out = frames.copy()

@@ -327,3 +327,11 @@ def test_ct_capacity_egress_admitted(dev, monkeypatch):
     assert m[155, 2, 0] + m[155, 1, 0] > 100_000                           # DROP_CT_CREATE_FAILED
     assert len(om["ct4"]) == len(om["ct6"]) == 300_000
     ctx.close()
+
+
+def test_config5_elephant_flows(dev):
+    """Four flows carry a 2^16-packet batch: groups of thousands of members, past the
+    grouping's LDS sort (k_gbin_group: the bin split by sub-bins and the elephant's
+    members ordered by packet through the tile bitmaps), in position lists."""
+    w = synth.config5(1 << 16, n_svc=40, n_ep=8, n_remote=16, n_flows=4, seed=59)
+    check_egress(w, dev, batches=1, rounds=2)

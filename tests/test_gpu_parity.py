@@ -282,7 +282,8 @@ def check_ingress(w, dev, batches, with_prefilter=True, trace_agg=0, events=True
         ck, cv = pm[name].dump()
         ok, ov = om[name].dump()
         assert len(ck) == len(ok), name
-        assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), name
+        ra, rb = H.sorted_rows(ck, cv), H.sorted_rows(ok, ov)
+        assert (ra == rb).all(), (name, H.rows_diff(ra, rb))
     return dp
 
 
@@ -333,7 +334,8 @@ def test_config3_zipf_hot_runs(dev):
         ck, cv = pm["ct4"].dump()
         ok, ov = om["ct4"].dump()
         assert len(ck) == len(ok), v
-        assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), v
+        ra, rb = H.sorted_rows(ck, cv), H.sorted_rows(ok, ov)
+        assert (ra == rb).all(), (v, H.rows_diff(ra, rb))
         check_policy_maps(pm["policy"], om["policy"])
     assert dp.metrics()[133, 1, 0] > 0                             # DROP_POLICY (the denied hot flows)
     ctx.close()
@@ -678,7 +680,8 @@ def test_ipcache6_churn_dual_stack(dev, monkeypatch, incremental):
     for name in ("ct4", "ct6"):
         ck, cv = pm[name].dump()
         ok, ov = om[name].dump()
-        assert (H.sorted_rows(ck, cv) == H.sorted_rows(ok, ov)).all(), name
+        ra, rb = H.sorted_rows(ck, cv), H.sorted_rows(ok, ov)
+        assert (ra == rb).all(), (name, H.rows_diff(ra, rb))
     pubs, rebuilds = ctx.publish_stats()
     if incremental:
         assert pubs - base[0] >= 5 and rebuilds == base[1], (base, pubs, rebuilds)

@@ -5,7 +5,7 @@
 # steps (outputs under gpurun_out/<tag>/):
 #   tests[=<pytest -k expr>]      the -m gpu tests (commas for spaces)   pytest.log
 #   bench=<workload>[,<args>]     one bench line (args: comma-separated)  bench_<workload>.json
-#   stats=<workload>              rocprofv3 kernel trace + stats          <workload>_kernel_stats.csv
+#   stats=<workload>[,<args>]     rocprofv3 kernel trace + stats          <workload>[args]_kernel_stats.csv
 #   pmc=<workload>                FETCH / WRITE / TCC hit-miss passes     pmc<k>_<workload>/
 #   deep=<workload>[,<packets>[,<v>]]  SQ / TA / TCP counter passes (v: an _ab/ library)  deep_<workload>[_<v>]/
 #   cal                           the random-line FETCH_SIZE calibration  pmc_cal/
@@ -47,11 +47,11 @@ for st in "$@"; do
       || { rc=$?; echo "[session] bench rc=$rc" >&2; tail -20 "$OUT/bench_$W.err" >&2; exit $rc; }
     cat "$OUT/bench_$W.json" ;;
   stats)
-    W=${A[0]}
-    run 600 "$OUT/stats_$W.log" rocprofv3 --kernel-trace --stats -d "$OUT/stats_$W" -o run --output-format csv \
-      -- python3 bench.py --workload "$W" --steps 10 --warmup 2 --no-cpu
-    cp "$OUT/stats_$W/run_kernel_stats.csv" "$OUT/${W}_kernel_stats.csv"
-    kstats "$OUT/${W}_kernel_stats.csv" >&2 ;;
+    W=${A[0]}; T=$W; [ ${#A[@]} -gt 1 ] && T=${W}$(printf '%s' "${A[@]:1}" | tr -c 'a-zA-Z0-9.' '_')
+    run 600 "$OUT/stats_$T.log" rocprofv3 --kernel-trace --stats -d "$OUT/stats_$T" -o run --output-format csv \
+      -- python3 bench.py --workload "$W" --steps 10 --warmup 2 --no-cpu "${A[@]:1}"
+    cp "$OUT/stats_$T/run_kernel_stats.csv" "$OUT/${T}_kernel_stats.csv"
+    echo "== $T" >&2; kstats "$OUT/${T}_kernel_stats.csv" >&2 ;;
   pmc)
     W=${A[0]}; i=0
     for CTRS in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do

@@ -1624,6 +1624,12 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;
         *final = 1;                                                 /* handle_policy -> tail_ipv4_policy */
+        if (dp->split) {                                            /* (or_lxc_egress_split) */
+            dp->pend_ep = (int32_t)(prog - dp->ep);
+            dp->pend_ifindex = dep->ifindex;
+            dp->pend_label = ep->seclabel;
+            return OR_E_DEFER;
+        }
         uint8_t ct_egress = ps->ct;                                 /* out.ct reports the egress CT result */
         r = handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
         ps->ct = ct_egress;
@@ -2085,6 +2091,12 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         or_endpoint_prog *prog = find_ep(dp, dep->lxc_id);
         if (!prog) return OR_DROP_MISSED_TAIL_CALL;
         *final = 1;
+        if (dp->split) {                                            /* (or_lxc_egress_split) */
+            dp->pend_ep = (int32_t)(prog - dp->ep);
+            dp->pend_ifindex = dep->ifindex;
+            dp->pend_label = ep->seclabel;
+            return OR_E_DEFER;
+        }
         uint8_t ct_egress = ps->ct;
         r = handle_policy(dp, prog, skb, dep->ifindex, ep->seclabel, 0, now, ps, reason);
         ps->ct = ct_egress;
@@ -2130,15 +2142,17 @@ static int from_container(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t
     return ret;
 }
 
-void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
-                   const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
-                   uint32_t now, or_out *out)
+static void lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                       const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
+                       uint32_t now, or_out *out, int32_t *dl_ep, uint32_t *dl_ifindex, uint32_t *dl_label)
 {
     or_skb skb;
+    dp->split = dl_ep != NULL;
     for (uint32_t i = 0; i < n; i++) {
         skb_init(&skb, frames + (size_t)i * stride, stride, len[i]);
         pkt_state ps = { OR_CT_NONE, 0, 0, 0 };
         dp->cur_pkt = i;
+        dp->pend_ep = -1;
         dp->cur_hash = flow_hash ? flow_hash[i] : 0;   /* get_hash_recalc(skb) */
         uint32_t e = src_ep ? src_ep[i] : ep0, dst = 0;
         int32_t reason = 0, ret;
@@ -2153,6 +2167,47 @@ void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint
         if (out->reason) out->reason[i] = reason;
         if (out->xdp) out->xdp[i] = 0;
         emit_frame(out, i, frames + (size_t)i * stride, stride, &skb, ret, ps.proxy);
+        if (dl_ep) {
+            dl_ep[i] = ret == OR_E_DEFER ? dp->pend_ep : -1;
+            dl_ifindex[i] = dp->pend_ifindex;
+            dl_label[i] = dp->pend_label;
+            if (ret == OR_E_DEFER && out->frames_out) memcpy(out->frames_out + (size_t)i * stride, skb.b, skb.avail);
+        }
+    }
+    dp->split = 0;
+}
+
+void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                   const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
+                   uint32_t now, or_out *out)
+{
+    lxc_egress(dp, frames, stride, len, src_ep, ep0, flow_hash, n, now, out, NULL, NULL, NULL);
+}
+
+void or_lxc_egress_split(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                         const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
+                         uint32_t now, or_out *out, int32_t *dl_ep, uint32_t *dl_ifindex, uint32_t *dl_label)
+{
+    lxc_egress(dp, frames, stride, len, src_ep, ep0, flow_hash, n, now, out, dl_ep, dl_ifindex, dl_label);
+}
+
+void or_lxc_deliver(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len, const int32_t *dl_ep,
+                    const uint32_t *dl_ifindex, const uint32_t *dl_label, const uint32_t *pkt, uint32_t n,
+                    uint32_t now, or_out *out)
+{
+    or_skb skb;
+    for (uint32_t j = 0; j < n; j++) {
+        skb_init(&skb, frames + (size_t)j * stride, stride, len[j]);
+        pkt_state ps = { OR_CT_NONE, 0, out->nl ? out->nl[j] : 0, out->nu ? out->nu[j] : 0 };
+        dp->cur_pkt = pkt ? pkt[j] : j;
+        int32_t reason = 0;
+        const int ret = handle_policy(dp, &dp->ep[dl_ep[j]], &skb, dl_ifindex[j], dl_label[j], 0, now, &ps, &reason);
+        if (out->ret) out->ret[j] = ret;
+        if (out->proxy) out->proxy[j] = ps.proxy;
+        if (out->nl) out->nl[j] = ps.nl;
+        if (out->nu) out->nu[j] = ps.nu;
+        if (out->reason) out->reason[j] = reason;
+        emit_frame(out, j, frames + (size_t)j * stride, stride, &skb, ret, ps.proxy);
     }
 }
 

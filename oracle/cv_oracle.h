@@ -204,6 +204,10 @@ typedef struct or_dp {
     uint32_t trace_agg;               /* MONITOR_AGGREGATION (pkg/option/monitor.go levels 0-3) */
     uint32_t ingress_ifindex;         /* skb->ingress_ifindex of from_netdev */
     uint32_t cur_pkt, cur_hash;       /* the packet being processed and its skb hash */
+    /* or_lxc_egress_split: stop a packet at its local delivery, recording where it goes */
+    int32_t  split;
+    int32_t  pend_ep;                 /* the destination endpoint's index (-1: none) */
+    uint32_t pend_ifindex, pend_label;
 } or_dp;
 
 or_dp *or_dp_create(uint32_t flags);
@@ -265,6 +269,21 @@ void or_netdev_ingress(or_dp *dp, const uint8_t *frames, uint32_t stride, const 
 void or_lxc_egress(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
                    const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
                    uint32_t now, or_out *out);
+
+/* Config 5 split at the local delivery, for the endpoint-owned CT prototype
+ * (tests/ep_shard.py): as or_lxc_egress, but a packet whose program reaches a local
+ * endpoint's policy program (ipv{4,6}_local_delivery -> tail call) stops there:
+ * ret = OR_E_DEFER, dl_ep[i] = the destination endpoint's index (else -1), dl_ifindex /
+ * dl_label = its ifindex and the source's seclabel, frames_out[i] the frame as the
+ * source's program left it.  or_lxc_deliver then runs the destination programs of such
+ * packets (pkt[j]: the batch index for notifications; nl / nu add to what out holds). */
+#define OR_E_DEFER (-3)
+void or_lxc_egress_split(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len,
+                         const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash, uint32_t n,
+                         uint32_t now, or_out *out, int32_t *dl_ep, uint32_t *dl_ifindex, uint32_t *dl_label);
+void or_lxc_deliver(or_dp *dp, const uint8_t *frames, uint32_t stride, const uint32_t *len, const int32_t *dl_ep,
+                    const uint32_t *dl_ifindex, const uint32_t *dl_label, const uint32_t *pkt, uint32_t n,
+                    uint32_t now, or_out *out);
 
 /* ct_create4 on a given tuple (conntrack.h:663-744), for building preloaded tables. */
 int or_ct_create4(or_map *ct, or_ipv4_ct_tuple *tuple, uint32_t skb_len, int dir,

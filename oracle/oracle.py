@@ -64,6 +64,8 @@ def lib():
         L.or_dp_node_config.argtypes = [vp, u32, u32, u32, vp, vp, vp]
         L.or_csum_apply.argtypes = [vp, u32, u32, u32, u32, u32, u32, vp]
         L.or_lxc_egress.argtypes = [vp, vp, u32, vp, vp, u32, vp, u32, u32, vp]
+        L.or_lxc_egress_split.argtypes = [vp, vp, u32, vp, vp, u32, vp, u32, u32, vp, vp, vp, vp]
+        L.or_lxc_deliver.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, u32, u32, vp]
         L.or_dp_notify_attach.argtypes = [vp, vp, u32]
         L.or_dp_notify_count.restype = u32
         L.or_dp_notify_count.argtypes = [vp]
@@ -249,6 +251,40 @@ class ODp:
         s = out.struct()
         lib().or_lxc_egress(self.h, _p(frames), frames.shape[1], _p(length), _p(src_ep), ep0, _p(flow_hash), n,
                             now, C.byref(s))
+        return out
+
+    def lxc_egress_split(self, frames, length, src_ep, flow_hash, now=0):
+        """lxc_egress stopped at local deliveries (ret OR_E_DEFER = -3): returns the outputs
+        (frames_out holds the frames as the source programs left them) and, per packet,
+        the destination endpoint index (-1: none), its ifindex and the source seclabel."""
+        n = len(length)
+        out = Out(n)
+        frames = np.ascontiguousarray(frames, np.uint8)
+        out.frames_out = np.zeros(frames.shape, np.uint8)
+        length = np.ascontiguousarray(length, np.uint32)
+        src_ep = np.ascontiguousarray(src_ep, np.uint16)
+        flow_hash = np.ascontiguousarray(flow_hash, np.uint32)
+        dl = np.full(n, -1, np.int32)
+        ifx = np.zeros(n, np.uint32)
+        lab = np.zeros(n, np.uint32)
+        s = out.struct()
+        lib().or_lxc_egress_split(self.h, _p(frames), frames.shape[1], _p(length), _p(src_ep), 0, _p(flow_hash), n,
+                                  now, C.byref(s), _p(dl), _p(ifx), _p(lab))
+        return out, dl, ifx, lab
+
+    def lxc_deliver(self, frames, length, dl_ep, dl_ifindex, dl_label, nl, nu, now=0):
+        """the destination programs of deferred packets (nl / nu: the source programs' counts)"""
+        n = len(length)
+        out = Out(n)
+        out.nl[:] = nl
+        out.nu[:] = nu
+        frames = np.ascontiguousarray(frames, np.uint8)
+        length = np.ascontiguousarray(length, np.uint32)
+        args = [np.ascontiguousarray(a, t) for a, t in ((dl_ep, np.int32), (dl_ifindex, np.uint32),
+                                                         (dl_label, np.uint32))]
+        s = out.struct()
+        lib().or_lxc_deliver(self.h, _p(frames), frames.shape[1], _p(length), *[_p(a) for a in args], None, n, now,
+                             C.byref(s))
         return out
 
     def xdp_prefilter(self, frames, length):

@@ -1,0 +1,126 @@
+"""Config 5 as one node across ranks with endpoint-owned CT maps (tests/ep_shard.py):
+the prototype's merged result against one sequential run of the same per-endpoint-map
+datapath -- every packet's verdict, drop reason, identity, CT result, proxy port and
+lookup counts, every endpoint's CT4 and CT6 table, the policy counters, cilium_metrics.
+CPU only (the oracle is every rank's datapath); the gloo variant exchanges the delivery
+records between two processes."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from cilium_amd import synth
+from tests import ep_shard as E
+from tests import harness as H
+
+CT_REPLY = 1
+
+
+def _workload(n=1 << 12, seed=0xE5):
+    # few endpoints: most flows stay on the node, services with local backends, replies
+    return synth.config5(n, n_svc=120, n_ep=24, n_remote=32, seed=seed, vip_frac=0.5)
+
+
+def _sequential(w):
+    dp, maps = E.per_endpoint_dp(w)
+    ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    return ref, dp, maps
+
+
+def _check(w, results, world):
+    ref, dp, maps = _sequential(w)
+    out, ct, metrics, (pk, pv) = E.merge(w, results)
+    for k in E.RankState.FIELDS:
+        bad = np.nonzero(out[k] != getattr(ref, k).astype(np.int64))[0]
+        assert len(bad) == 0, (k, len(bad), bad[:5], out[k][bad[:5]], getattr(ref, k)[bad[:5]])
+    for e in range(len(w.endpoints)):
+        for fam, (keys, vals) in zip(("ct4", "ct6"), ct[e]):
+            ok, ov = maps[fam][e].dump()
+            a, b = H.sorted_rows(keys, vals), H.sorted_rows(ok, ov)
+            assert a.shape == b.shape and (a == b).all(), (e, fam, H.rows_diff(a, b))
+    assert (metrics == dp.metrics()).all()
+    ok, ov = maps["policy"].dump()
+    assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all()
+    # the dependency DESIGN.md §7 names: replies whose source program finds the entry
+    # an earlier packet's delivery created on the replier's map, with the two endpoints
+    # on different ranks
+    src = w.extra["src_ep"].astype(int)
+    deliv = ref.ret != -3
+    cross_reply = (ref.ct == CT_REPLY) & deliv
+    n_cross = 0
+    for i in np.nonzero(cross_reply)[0]:
+        dst = [d for d in E.candidates(w)[i]]
+        n_cross += any(d % world != src[i] % world for d in dst)
+    assert n_cross > 0
+    assert sum(r["cross"] for r in results) > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_endpoint_owned_ct_simulated(world):
+    w = _workload()
+    results, rounds = E.simulate(w, world, w.now)
+    print(f"world {world}: {w.n} packets in {rounds} exchange rounds")
+    _check(w, results, world)
+    assert rounds < w.n // 32                                      # rounds follow reply chains, not packets
+
+
+def test_candidates_cover_every_delivery():
+    w = _workload(seed=0xE6)
+    dp, _ = E.per_endpoint_dp(w)
+    o, dl, _, _ = dp.lxc_egress_split(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    cand = E.candidates(w)
+    deferred = np.nonzero(o.ret == E.DEFER)[0]
+    assert len(deferred) > 0
+    assert all(int(dl[i]) in cand[i] for i in deferred)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = _workload()
+        st = E.RankState(w, rank, world, w.now)
+        rounds = 0
+        while True:
+            box = st.progress()
+            rounds += 1
+            boxes = [None] * world
+            dist.all_gather_object(boxes, box)                     # the exchange: delivery records
+            for b in boxes:
+                st.receive(b.get(rank, []))
+            flags = [None] * world
+            dist.all_gather_object(flags, st.done())
+            if all(flags):
+                break
+        res = [None] * world
+        dist.all_gather_object(res, st.result())
+        if rank == 0:
+            q.put((res, rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_endpoint_owned_ct_two_ranks_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results, rounds = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    w = _workload()
+    _check(w, results, 2)

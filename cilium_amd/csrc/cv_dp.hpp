@@ -218,7 +218,10 @@ constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q 
 constexpr int EG_WORDS = 16;
 // position lists of the egress conntrack stage: one launch per member position, the last
 // one continuing the few groups past NPOS - 1 members (<= 16: the lists are k_heads' 16)
-constexpr uint32_t NPOS = 8;
+#ifndef CV_NPOS
+#define CV_NPOS 3
+#endif
+constexpr uint32_t NPOS = CV_NPOS;
 constexpr uint32_t DEL_SLOTS = 4;                 // (64 B: one aligned half line per record)
 // the local-delivery list counter of a position (the netdev queue's sub-queue counters,
 // which the egress path does not use)

@@ -122,6 +122,20 @@ def algorithmic_bytes(name, nl, nu, record=64):
     return n * (R + V) + 64 * (int(nl.astype(np.int64).sum()) + int(nu.astype(np.int64).sum()))
 
 
+def hbm_resident_bytes(ct, ret, record=64, V=9):
+    """config 3: the algorithmic bytes of the HBM-resident part -- the record stream, the
+    outputs and the conntrack lines (a 2^27..2^28-entry table) -- from each packet's CT
+    result as ct_lookup4 (conntrack.h:442-562) reaches it: REPLY / RELATED one probe,
+    ESTABLISHED / NEW two (the tuple, then its reverse); a hit writes its line back; an
+    allowed NEW writes the tuple and its ICMP twin.  The rest of B(p) (policy, ipcache,
+    endpoint and prefilter lines) stays in L2 / Infinity Cache."""
+    ct = ct.astype(np.int64)
+    lines = np.where((ct == 2) | (ct == 3), 1, np.where((ct == 0) | (ct == 1), 2, 0))
+    lines += np.where((ct >= 1) & (ct <= 3), 1, 0)
+    lines += np.where((ct == 0) & ((ret == 0) | (ret == 7)), 2, 0)       # TC_ACT_OK / TC_ACT_REDIRECT
+    return len(ct) * (record + V) + 64 * int(lines.sum())
+
+
 def host_info():
     model = platform.processor() or ""
     try:
@@ -446,6 +460,8 @@ def main():
     torch.cuda.synchronize()
     nl, nu = acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy()
     created = int((acct["ct"].cpu().numpy() == 0).sum()) if stateful else 0
+    hbm_res = hbm_resident_bytes(acct["ct"].cpu().numpy(), acct["ret"].cpu().numpy()) \
+        if name in ("config3", "config4") else None
     if name == "config5":
         k4 = offs[1]
         alg_bytes = algorithmic_bytes(name, nl[:k4], nu[:k4], 64) + algorithmic_bytes(name, nl[k4:], nu[k4:], 128)
@@ -529,6 +545,15 @@ def main():
                 "random_access": None if ra_peak is None else {
                     "peak": ra_peak, "unit": "GB/s", "frac": round(achieved / ra_peak, 4),
                     "probe": "random 64-B line reads from a 4 GiB HBM table, measured in this run"},
+                # the HBM-resident part of the algorithmic bytes (record stream, outputs,
+                # conntrack lines) against the same random-line peak; the rest is
+                # cache-resident (policy, ipcache, endpoint, prefilter lines)
+                "hbm_resident": None if hbm_res is None else {
+                    "bytes_per_step": hbm_res, "cache_resident_bytes_per_step": alg_bytes - hbm_res,
+                    "achieved": round(hbm_res / (kern_ms * 1e-3) / 1e9, 1), "unit": "GB/s",
+                    "frac_random_access": None if ra_peak is None else
+                    round(hbm_res / (kern_ms * 1e-3) / 1e9 / ra_peak, 4),
+                    "how": "bench.hbm_resident_bytes: CT probes / writes per packet from its CT result"},
             },
             "cpu_baseline": cpu,
         }

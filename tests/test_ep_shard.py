@@ -14,7 +14,7 @@ from cilium_amd import synth
 from tests import ep_shard as E
 from tests import harness as H
 
-CT_REPLY = 1
+CT_REPLY = 2
 
 
 def _workload(n=1 << 12, seed=0xE5):

@@ -225,11 +225,22 @@ __device__ __forceinline__ int netdev_ipv6(const DpParams &p, const RecT<NW> &r,
 
 constexpr uint64_t SALT_NETDEV6 = 0x4E45543600000000ULL;
 
+// Occupancy of the netdev front and conntrack stage (waves per SIMD the compiler must
+// allow; 0: its own choice, 4 at 107-110 VGPRs)
+#ifndef CV_NS_WAVES
+#define CV_NS_WAVES 0
+#endif
+#if CV_NS_WAVES
+#define CV_NS_OCC __attribute__((amdgpu_waves_per_eu(CV_NS_WAVES, 8)))
+#else
+#define CV_NS_OCC
+#endif
+
 // stage 1: XDP prefilter + from_netdev -> handle_ipv4 / handle_ipv6 up to the tail call
 // into the endpoint's policy program; packets reaching it join their address-pair
 // group (IPv4 in Q_NETDEV, IPv6 in Q_NETDEV6).
 template <bool EV>
-__global__ void __launch_bounds__(BLOCK) k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
+__global__ void __launch_bounds__(BLOCK) CV_NS_OCC k_netdev_front(DpParams p, BatchDev b, OutDev o, GroupScratch g,
                                                         int with_prefilter)
 {
     __shared__ LdsMetrics lm;
@@ -762,7 +773,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
 // stage 2: conntrack + policy, each address-pair group by one lane in packet order (the
 // hot runs by k_ct_hot when `hot`)
 template <bool EV>
-__global__ void __launch_bounds__(BLOCK) k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now,
+__global__ void __launch_bounds__(BLOCK) CV_NS_OCC k_ct_stage(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now,
                                                     int hot)
 {
     __shared__ LdsMetrics lm;

@@ -43,7 +43,7 @@ def main():
     shutil.copy(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv"), os.path.join(dst, f"{w}_kernel_stats.csv"))
     shutil.copy(os.path.join(src, f"bench_{w}.json"), os.path.join(dst, f"bench_{w}.json"))
     kname = DOMINANT[w]
-    setup = ("k_ct_load", "k_ct_scan", "k_ct_op", "k_ct_gc")      # table loads / map API, not the step
+    setup = ("k_ct_load", "k_ct_scan", "k_ct_op", "k_ct_gc", "k_ct_tags")   # table loads, map API, slot-load probe
     ctr, step = {}, defaultdict(float)
     nsteps = 0
     for i in (1, 2, 3):

@@ -1644,53 +1644,90 @@ __global__ void k_ct_scan(HashTable t, int v6, uint64_t nslots, uint64_t *slots,
 // check reads b+1 while its own lane may change it; those changes only delete keys or
 // add empty slots, which keeps the conclusion true (a key read half-deleted looks
 // displaced: the bucket then just keeps its tombstones this pass).
+// n words at word offset o of a 128-B-aligned bucket set to zero, 16 B at a time where
+// aligned (o and n are compile-time constants here: the branches fold away)
+__device__ __forceinline__ void zero_words(uint32_t *bw, int o, int n)
+{
+    if ((o & 3) && n >= 2 && !(o & 1)) { *reinterpret_cast<uint2 *>(bw + o) = make_uint2(0u, 0u); o += 2; n -= 2; }
+    for (; n >= 4 && !(o & 3); o += 4, n -= 4) *reinterpret_cast<uint4 *>(bw + o) = make_uint4(0u, 0u, 0u, 0u);
+    for (; n >= 2 && !(o & 1); o += 2, n -= 2) *reinterpret_cast<uint2 *>(bw + o) = make_uint2(0u, 0u);
+    for (; n > 0; ++o, --n) bw[o] = 0u;
+}
+
 template <class S>
 __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted, uint32_t *freed)
 {
     uint32_t mine = 0, cleared = 0;
-    for (uint64_t b = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BLOCK) {
-        uint32_t *bw = t.buckets + b * S::BW;
-        const uint2 tg = *reinterpret_cast<const uint2 *>(bw);
-        uint64_t tags = (uint64_t)tg.x | ((uint64_t)tg.y << 32), out = tags;
-        bool dead = false;
+    // GC_U buckets per thread and iteration: their tag words, then the live slots'
+    // lifetimes, are loaded before any is used (a scan bound by load latency at one
+    // bucket per step)
+    constexpr int GC_U = 4;
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t b0 = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; b0 < nb; b0 += GC_U * stride) {
+        uint64_t tgs[GC_U];
+        uint32_t lifes[GC_U][S::SPB];
 #pragma unroll
-        for (int sl = 0; sl < S::SPB; ++sl) {
-            const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
-            if (tag == TAG_DEAD) dead = true;
-            if (tag < 3) continue;
-            const uint32_t life = *ct_hot<S>(t, (int64_t)(b * S::SPB + sl));   // lifetime: hot word 0
-            if (life < time) {
-                out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
-#pragma unroll
-                for (int j = 0; j < S::KS; ++j) bw[S::KEY0 + sl * S::KS + j] = 0;   // free slots hold zero keys,
-                uint4 *c = reinterpret_cast<uint4 *>(t.vals + (b * S::SPB + sl) * CT_COLD);   // hot and side words
-                c[0] = c[1] = make_uint4(0, 0, 0, 0);
-                ++mine;
-                dead = true;
+        for (int u = 0; u < GC_U; ++u) {
+            const uint64_t b = b0 + u * stride;
+            tgs[u] = 0;
+            if (b < nb) {
+                const uint2 tg = *reinterpret_cast<const uint2 *>(t.buckets + b * S::BW);
+                tgs[u] = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
             }
         }
-        if (dead) {
-            const uint64_t nx = (b + 1) & t.mask;
-            const volatile uint32_t *nw = t.buckets + nx * S::BW;
-            const uint64_t ntags = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
-            bool has_empty = false, displaced = false;
+#pragma unroll
+        for (int u = 0; u < GC_U; ++u)
 #pragma unroll
             for (int sl = 0; sl < S::SPB; ++sl) {
-                const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
-                has_empty |= tag == TAG_EMPTY;
+                const uint64_t b = b0 + u * stride;
+                lifes[u][sl] = (b < nb && ((uint32_t)(tgs[u] >> (8 * sl)) & 0xFFu) >= 3)
+                                   ? *ct_hot<S>(t, (int64_t)(b * S::SPB + sl)) : 0u;   // lifetime: hot word 0
+            }
+#pragma unroll
+        for (int u = 0; u < GC_U; ++u) {
+            const uint64_t b = b0 + u * stride;
+            if (b >= nb) break;
+            uint32_t *bw = t.buckets + b * S::BW;
+            uint64_t tags = tgs[u], out = tags;
+            bool dead = false;
+#pragma unroll
+            for (int sl = 0; sl < S::SPB; ++sl) {
+                const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
+                if (tag == TAG_DEAD) dead = true;
                 if (tag < 3) continue;
-                uint32_t key[S::KW], tg2;
-#pragma unroll
-                for (int j = 0; j < S::KW; ++j) key[j] = nw[S::KEY0 + sl * S::KS + j];
-                displaced |= (home_hash<S>(key, tg2) & t.mask) != nx;
+                const uint32_t life = lifes[u][sl];
+                if (life < time) {
+                    out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
+                    zero_words(bw, S::KEY0 + sl * S::KS, S::KS);   // free slots hold zero keys,
+                    uint4 *c = reinterpret_cast<uint4 *>(t.vals + (b * S::SPB + sl) * CT_COLD);   // hot and side words
+                    c[0] = c[1] = make_uint4(0, 0, 0, 0);
+                    ++mine;
+                    dead = true;
+                }
             }
-            if (has_empty && !displaced) {
+            if (dead) {
+                const uint64_t nx = (b + 1) & t.mask;
+                const uint32_t *nw = t.buckets + nx * S::BW;        // (any version of it will do, above)
+                const uint64_t ntags = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
+                bool has_empty = false, displaced = false;
 #pragma unroll
-                for (int sl = 0; sl < S::SPB; ++sl)
-                    if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) { out &= ~(0xFFull << (8 * sl)); ++cleared; }
+                for (int sl = 0; sl < S::SPB; ++sl) {
+                    const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
+                    has_empty |= tag == TAG_EMPTY;
+                    if (tag < 3) continue;
+                    uint32_t key[S::KW], tg2;
+#pragma unroll
+                    for (int j = 0; j < S::KW; ++j) key[j] = nw[S::KEY0 + sl * S::KS + j];
+                    displaced |= (home_hash<S>(key, tg2) & t.mask) != nx;
+                }
+                if (has_empty && !displaced) {
+#pragma unroll
+                    for (int sl = 0; sl < S::SPB; ++sl)
+                        if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) { out &= ~(0xFFull << (8 * sl)); ++cleared; }
+                }
             }
+            if (out != tags) *reinterpret_cast<uint2 *>(bw) = make_uint2((uint32_t)out, (uint32_t)(out >> 32));
         }
-        if (out != tags) *reinterpret_cast<uint2 *>(bw) = make_uint2((uint32_t)out, (uint32_t)(out >> 32));
     }
     const unsigned long long fr = wave_sum(cleared);
     if ((threadIdx.x & 63) == 0 && fr && freed) atomicAdd(freed, (uint32_t)fr);

@@ -555,15 +555,23 @@ __device__ __forceinline__ uint32_t fx_scan(uint32_t T, HotLds &L, uint32_t *tot
 // step 3 for the entry at L.slot: the deferred hits of the participating threads (in
 // thread = member order) applied as the sequential run applies them one by one
 template <class S>
+__device__ __forceinline__ void hot_load(const HashTable &ct, HotLds &L, int64_t slot)
+{
+    CtE e;
+    ct_load_hot<S>(ct, slot, e);
+    L.e[0] = e.w[8]; L.e[1] = e.w[9]; L.e[2] = e.w[10]; L.e[3] = e.w[11]; L.e[4] = e.w[12]; L.e[5] = e.w[13];
+    L.e[6] = e.w[0]; L.e[7] = e.w[2]; L.e[8] = e.w[4]; L.e[9] = e.w[6];
+}
+
+// (loaded: L.e already holds the entry's hot run -- the chunk's first entry, loaded by its
+// first member's thread while the others finish their packets)
+template <class S>
 __device__ __forceinline__ void hot_fold(const HashTable &ct, HotLds &L, bool part, const HitRec &hr, uint32_t now,
-                                         uint32_t flags)
+                                         uint32_t flags, bool loaded)
 {
     const int64_t slot = (int64_t)L.slot;
     if (threadIdx.x == 0) {
-        CtE e;
-        ct_load_hot<S>(ct, slot, e);
-        L.e[0] = e.w[8]; L.e[1] = e.w[9]; L.e[2] = e.w[10]; L.e[3] = e.w[11]; L.e[4] = e.w[12]; L.e[5] = e.w[13];
-        L.e[6] = e.w[0]; L.e[7] = e.w[2]; L.e[8] = e.w[4]; L.e[9] = e.w[6];
+        if (!loaded) hot_load<S>(ct, L, slot);
         L.fxlast = 0; L.seen[0] = L.seen[1] = 0; L.any[0] = L.any[1] = 0;
         L.pk[0] = L.pk[1] = L.by[0] = L.by[1] = 0;
     }
@@ -684,6 +692,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
     const uint32_t nhot = hot_runs(g, Q_NETDEV);
     for (uint32_t r = blockIdx.x; r < nhot; r += gridDim.x) {     // a workgroup per run
         const uint32_t off = g.work[r], cnt = g.order[off];
+        const HashTable ct = ep_stage4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;   // (the run's map)
         for (uint32_t k0 = 0; k0 < cnt;) {                        // (block-uniform)
             const uint32_t k = k0 + threadIdx.x;
             const bool live = k < cnt;
@@ -706,11 +715,17 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             const int ret = simple ? ct_lookup_pre(ep.ct4, t, s.h, CT_INGRESS, s.len, slot, &st, a, hr) : 0;
             const bool deny = simple && ret >= 0 && policy_ingress_denies(ep.policy, p.flags, s1.w, t.dport, t.nexthdr);
             const bool change = simple && ((ret == CT_ESTABLISHED && deny) || (ret == CT_NEW && !deny));
-            if (threadIdx.x == 0) L.c = HOTB;
+            if (threadIdx.x == 0) { L.c = HOTB; L.lead = HOTB; }
             __syncthreads();
             if (change) atomicMin(&L.c, threadIdx.x);
+            if (hr.slot >= 0) atomicMin(&L.lead, threadIdx.x);    // the first hit
             __syncthreads();
             const uint32_t c = L.c;
+            uint32_t lead = L.lead;
+            if (lead < c && threadIdx.x == lead) {                // its entry, while the others finish
+                L.slot = (unsigned long long)hr.slot;
+                hot_load<Ct4Spec>(ct, L, hr.slot);
+            }
             // 2. the members before c, in parallel
             if (live && threadIdx.x < c) {
                 uint8_t ct = CT_NONE;
@@ -731,24 +746,28 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
                 store_out(o, x, a);
             }
             // 3. their hits' entry updates, entry by entry, in member order
-            const HashTable ct = ep_stage4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;   // (the run's map)
             bool pend = live && threadIdx.x < c && hr.slot >= 0;
-            while (__syncthreads_or(pend)) {
+            for (bool first = true; lead < c; first = false) {    // (block-uniform)
+                __syncthreads();
+                const bool part = pend && (unsigned long long)hr.slot == L.slot;
+                hot_fold<Ct4Spec>(ct, L, part, hr, now, p.flags, first);   // (ends with a barrier)
+                pend &= !part;
                 if (threadIdx.x == 0) L.lead = HOTB;
                 __syncthreads();
                 if (pend) atomicMin(&L.lead, threadIdx.x);
                 __syncthreads();
-                if (threadIdx.x == L.lead) L.slot = (unsigned long long)hr.slot;
-                __syncthreads();
-                const bool part = pend && (unsigned long long)hr.slot == L.slot;
-                hot_fold<Ct4Spec>(ct, L, part, hr, now, p.flags);
-                pend &= !part;
+                lead = L.lead;
+                if (lead < c && threadIdx.x == lead) L.slot = (unsigned long long)hr.slot;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (the entries written before any re-read)
             l1_inv();
             __syncthreads();
+            if (c >= HOTB) {                                      // (block-uniform) no member changes a key
+                k0 += HOTB;
+                continue;
+            }
             // 4. member c whole: its create or delete, against the table the fold left
-            if (c < HOTB && threadIdx.x == c) {
+            if (threadIdx.x == c) {
                 Acct a1{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
                 uint8_t ct1 = CT_NONE;
                 uint16_t proxy = 0;
@@ -763,7 +782,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             l1_inv();
             __syncthreads();
-            k0 += c < HOTB ? c + 1 : HOTB;
+            k0 += c + 1;
         }
     }
     met_flush(m, p.metrics);                                      // (ends with a barrier)

@@ -988,9 +988,10 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Out
 // LDS; three small kernels scan the counts into offsets; k_gkey_scatter writes every
 // staged packet as {packet, key low word} into its bin's slice; k_gbin_group sorts each
 // bin by (key low word, packet) in LDS -- a bin past LCAP entries by sub-bins, and a
-// hot address pair's members by packet through a bitmap (gbin_split_key) -- so a group's
-// members end up contiguous and in packet order, and writes the runs {size, members} into `order`; k_heads_count / k_heads_place
-// list the groups' first packets in packet order, size class by size class (the
+// hot address pair's members by packet through a bitmap (gbin_split_key) -- so a
+// group's members end up contiguous and in packet order, and writes the runs {size,
+// members} into `order`; k_heads_count / k_heads_place list the groups' first
+// packets in packet order, size class by size class (the
 // `work` and `single` lists for_each_run reads).  Keys that share the bin bits and the
 // low word merge into one group (about 2^-32 per pair of groups in a bin): a coarser
 // grouping, equally exact.

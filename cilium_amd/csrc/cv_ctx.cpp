@@ -1619,7 +1619,8 @@ int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_
                  const uint32_t *flow_hash, uint32_t now, const OutDev &oc, const std::vector<MapObj *> &cts,
                  hipStream_t s)
 {
-    constexpr int MAX_PASSES = 8;
+    const char *mp = getenv("CV_EADM_MAX_PASSES");             // (tests of the fallback)
+    const int MAX_PASSES = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
     const uint32_t n = bc.n;
     // the state a pass writes, and where its copy goes
     struct Region { void *src; size_t bytes, off; };
@@ -2213,6 +2214,23 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
         if (!fits && admissible) {
             r = lxc_admitted(c, p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
                              now, chunk(o, off, b->stride), cts, (hipStream_t)stream);
+            // no fixed point (the state is back as before the chunk): the chunk again in
+            // planned launches, one guarded packet at a time next to the limit
+            for (uint32_t o2 = off, m; r == -EAGAIN && o2 < off + n; o2 += m) {
+                m = ct_plan(c, cts, off + n - o2, 7, (hipStream_t)stream, &p.ct_guard);
+                BatchDev bm = chunk(b, o2, m);
+                bm.hash = flow_hash ? flow_hash + o2 : nullptr;
+                GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
+                gs.gbits = gbin_bits(m);
+                int r2 = launch_lxc_egress(p, bm, src_ep ? src_ep + o2 : nullptr, ep0,
+                                           flow_hash ? flow_hash + o2 : nullptr, now, chunk(o, o2, b->stride), gs,
+                                           (hipStream_t)stream);
+                p.ct_guard = 0;
+                for (const HashTable &t : pols)
+                    if (!r2) r2 = launch_policy_fold(t, (hipStream_t)stream);
+                if (r2) return r2;
+                if (o2 + m == off + n) r = 0;
+            }
         } else {
             GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
             gs.gbits = gbin_bits(n);                              // (the binned grouping of the components)

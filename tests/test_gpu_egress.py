@@ -335,3 +335,14 @@ def test_config5_elephant_flows(dev):
     members ordered by packet through the tile bitmaps), in position lists."""
     w = synth.config5(1 << 16, n_svc=40, n_ep=8, n_remote=16, n_flows=4, seed=59)
     check_egress(w, dev, batches=1, rounds=2)
+
+
+def test_ct_capacity_egress_admission_fallback(dev, monkeypatch):
+    """An egress launch whose admission finds no fixed point within its pass limit
+    (forced here: one pass, which a batch crossing max_entries cannot settle in) puts the
+    maps back as they were and runs the chunk again in planned launches, guarded next to
+    the limit: still the sequential run's answer."""
+    monkeypatch.setenv("CV_EADM_MAX_PASSES", "1")
+    w = synth.config5(1 << 12, n_svc=2000, n_ep=256, n_remote=512, ct_max=1500, seed=83)
+    dp = check_egress(w, dev, batches=2, rounds=1)
+    assert dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0       # DROP_CT_CREATE_FAILED happened

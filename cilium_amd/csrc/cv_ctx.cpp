@@ -217,6 +217,8 @@ struct cv_ctx {
     std::vector<Endpoint> eps;
     bool eps_dirty = true;
     DevBuf eps_dev, ephot_dev, ephot6_dev, ep_of_lxc;
+    bool uni4_on = false;      // every endpoint on one policy + CT4 map, LXC_IPV4 set (DpParams::uni4)
+    EpHot uni4{};
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
@@ -1053,6 +1055,13 @@ int sync_body(cv_ctx *c, hipStream_t stream)
             hot6.push_back(h6);
             of[e.lxc_id] = (uint16_t)(i + 1);
         }
+        // one policy and CT4 map for every endpoint, each with LXC_IPV4: the netdev stages'
+        // common line (DpParams::uni4)
+        c->uni4_on = !hot.empty();
+        for (size_t i = 0; i < hot.size() && c->uni4_on; ++i)
+            c->uni4_on = hot[i].pol_buckets == hot[0].pol_buckets && hot[i].ct_buckets == hot[0].ct_buckets &&
+                         hot[i].ct_v4 == hot[0].ct_v4 && (hot[i].ct_v4 & EPH_V4);
+        if (c->uni4_on) c->uni4 = hot[0];
         if (ev.empty()) { ev.push_back(EpDev{}); hot.push_back(EpHot{}); hot6.push_back(EpHot{}); }
         r = c->eps_dev.upload(ev.data(), ev.size() * sizeof(EpDev));
         if (!r) r = c->ephot_dev.upload(hot.data(), hot.size() * sizeof(EpHot));
@@ -1083,6 +1092,8 @@ DpParams params(cv_ctx *c)
     p.eps = c->eps_dev.as<EpDev>();
     p.ephot = c->ephot_dev.as<EpHot>();
     p.ephot6 = c->ephot6_dev.as<EpHot>();
+    p.uni4_on = c->uni4_on && !getenv("CV_NO_UNI4") ? 1u : 0u;
+    p.uni4 = c->uni4;
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
     p.lb4 = c->role[CV_ROLE_LB4_SERVICES] >= 0 ? c->lb4.view : HashTable{};

@@ -1837,11 +1837,8 @@ __device__ __forceinline__ void frame6_emit(const Frame6 &f, const uint8_t *in, 
 // The endpoint program's tables for the IPv4 conntrack stages from its EpHot line
 // (one 64-B read); the full EpDev where the event records need its constants or a
 // guarded launch needs the CT map's max_entries.
-template <bool FULL>
-__device__ __forceinline__ EpDev ep_stage4(const DpParams &p, uint32_t idx)
+__device__ __forceinline__ EpDev ep_hot4(const DpParams &p, const EpHot &h, uint32_t idx)
 {
-    if constexpr (FULL) return G(p.eps)[idx];
-    const EpHot h = G(p.ephot)[idx];
     EpDev e{};
     e.policy = HashTable{h.pol_buckets, h.pol_vals, h.pol_mask, 32u, (uint32_t)PolicySpec::SPB, h.pol_aux, nullptr, 0};
     e.ct4 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, (uint32_t)CT_COLD, (uint32_t)Ct4Spec::SPB, nullptr, h.ct_live,
@@ -1851,6 +1848,24 @@ __device__ __forceinline__ EpDev ep_stage4(const DpParams &p, uint32_t idx)
     e.ct_id = h.ct_v4 & EPH_CT_ID;
     e.seclabel = h.seclabel;
     return e;
+}
+
+template <bool FULL>
+__device__ __forceinline__ EpDev ep_stage4(const DpParams &p, uint32_t idx)
+{
+    if constexpr (FULL) return G(p.eps)[idx];
+    return ep_hot4(p, G(p.ephot)[idx], idx);
+}
+
+// The netdev conntrack stages' view of an endpoint: with one policy and CT4 map for every
+// endpoint (p.uni4_on) no per-packet read at all.  Its SECLABEL is then not the
+// endpoint's, which only the event records read (those instances take the full entry).
+template <bool FULL>
+__device__ __forceinline__ EpDev ep_netdev4(const DpParams &p, uint32_t idx)
+{
+    if constexpr (!FULL)
+        if (p.uni4_on && !p.ct_guard) return ep_hot4(p, p.uni4, idx);
+    return ep_stage4<FULL>(p, idx);
 }
 
 // the same for the IPv6 stages: policy and CT6 tables, SECLABEL

@@ -81,6 +81,10 @@ struct DpParams {              // by value as the kernel argument
     // stage, and its intent {creates tried (3 bits), deletes << 3, CT map (0 CT4, 1 CT6) << 4}
     uint8_t *eg_left;
     uint8_t *eg_intent;
+    // every endpoint on one policy map and one CT4 map with LXC_IPV4 set (cv_ctx.cpp): the
+    // netdev stages take that line from here instead of a per-packet EpHot read
+    uint32_t uni4_on;
+    EpHot uni4;
 };
 
 // Exact conntrack admission next to max_entries (cv_kernels.hip "conntrack

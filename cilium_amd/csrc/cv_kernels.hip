@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(BLOCK) CV_NS_OCC k_netdev_front(DpParams p, Ba
         // groups by it
         unsigned long long gkey = 0;
         if (staged) {
-            const uint32_t ct_id = G(p.ephot)[smeta & 0xFFFFu].ct_v4 & EPH_CT_ID;
+            const uint32_t ct_id = (p.uni4_on ? p.uni4.ct_v4 : G(p.ephot)[smeta & 0xFFFFu].ct_v4) & EPH_CT_ID;
             gkey = (pair_hash4(rec_raw32c<26>(r), daddr, (uint64_t)ct_id << 17) & ~3ull) | 2ull;
         } else if (v6stage) {
             const EpDev ep = G(p.eps)[smeta & 0xFFFFu];
@@ -401,7 +401,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 {
     const uint4 s0 = g.srec[2 * i], s1 = g.srec[2 * i + 1];
     const uint32_t meta = s1.z;
-    const EpDev ep = ep_stage4<M::EV>(p, meta & 0xFFFFu);
+    const EpDev ep = ep_netdev4<M::EV>(p, meta & 0xFFFFu);
     Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
     const uint32_t nhot = hot_runs(g, Q_NETDEV);
     for (uint32_t r = blockIdx.x; r < nhot; r += gridDim.x) {     // a workgroup per run
         const uint32_t off = g.work[r], cnt = g.order[off];
-        const HashTable ct = ep_stage4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;   // (the run's map)
+        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;   // (the run's map)
         for (uint32_t k0 = 0; k0 < cnt;) {                        // (block-uniform)
             const uint32_t k = k0 + threadIdx.x;
             const bool live = k < cnt;
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             uint4 s0{}, s1{};
             if (live) { s0 = g.srec[2 * x]; s1 = g.srec[2 * x + 1]; }
             const uint32_t meta = s1.z;
-            const EpDev ep = ep_stage4<false>(p, meta & 0xFFFFu);
+            const EpDev ep = ep_netdev4<false>(p, meta & 0xFFFFu);
             Skb4 s = skb4_unpack(s0, s1.x, s1.y & 0x3FFu, b.stride);
             const bool skip_proxy = (meta >> 16) & 1u;
             const uint32_t ifx = (meta >> 17) & 1u;               // ifindex != 0 (the plain instance's view)
@@ -899,7 +899,7 @@ __device__ __forceinline__ int commit_one(const DpParams &p, const BatchDev &b, 
     const uint4 s1 = g.srec[2 * i + 1];
     uint32_t seen;
     if (!v6) {
-        const EpDev ep = ep_stage4<false>(p, s1.z & 0xFFFFu);
+        const EpDev ep = ep_netdev4<false>(p, s1.z & 0xFFFFu);
         const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
         Tuple4 t;
         t.nexthdr = s.nexthdr;
@@ -1949,7 +1949,7 @@ __device__ __forceinline__ bool intent_tuple(const DpParams &p, const BatchDev &
     uint32_t seen;
     src = s1.w;
     if constexpr (!V6) {
-        ep = ep_stage4<false>(p, meta & 0xFFFFu);
+        ep = ep_netdev4<false>(p, meta & 0xFFFFu);
         if ((p.flags & F_DROP_ALL) || !ep.ipv4) return false;
         const Skb4 s = skb4_unpack(g.srec[2 * i], s1.x, s1.y & 0x3FFu, b.stride);
         if (s.len < 34) return false;

@@ -218,7 +218,8 @@ struct cv_ctx {
     bool eps_dirty = true;
     DevBuf eps_dev, ephot_dev, ephot6_dev, ep_of_lxc;
     bool uni4_on = false;      // every endpoint on one policy + CT4 map, LXC_IPV4 set (DpParams::uni4)
-    EpHot uni4{};
+    bool uni6_on = false;      // every endpoint on one policy + CT6 map (DpParams::uni6)
+    EpHot uni4{}, uni6{};
     DevBuf metrics_own;
     unsigned long long *metrics = nullptr;
     DevBuf gtable, gsingle, gslot, gnext, gsrec, gparent, geg, gorder, gcursor, gqueue, gwork, gifx;
@@ -1062,6 +1063,10 @@ int sync_body(cv_ctx *c, hipStream_t stream)
             c->uni4_on = hot[i].pol_buckets == hot[0].pol_buckets && hot[i].ct_buckets == hot[0].ct_buckets &&
                          hot[i].ct_v4 == hot[0].ct_v4 && (hot[i].ct_v4 & EPH_V4);
         if (c->uni4_on) c->uni4 = hot[0];
+        c->uni6_on = !hot6.empty();
+        for (size_t i = 0; i < hot6.size() && c->uni6_on; ++i)
+            c->uni6_on = hot6[i].pol_buckets == hot6[0].pol_buckets && hot6[i].ct_buckets == hot6[0].ct_buckets;
+        if (c->uni6_on) c->uni6 = hot6[0];
         if (ev.empty()) { ev.push_back(EpDev{}); hot.push_back(EpHot{}); hot6.push_back(EpHot{}); }
         r = c->eps_dev.upload(ev.data(), ev.size() * sizeof(EpDev));
         if (!r) r = c->ephot_dev.upload(hot.data(), hot.size() * sizeof(EpHot));
@@ -1094,6 +1099,8 @@ DpParams params(cv_ctx *c)
     p.ephot6 = c->ephot6_dev.as<EpHot>();
     p.uni4_on = c->uni4_on && !getenv("CV_NO_UNI4") ? 1u : 0u;
     p.uni4 = c->uni4;
+    p.uni6_on = c->uni6_on && !getenv("CV_NO_UNI4") ? 1u : 0u;
+    p.uni6 = c->uni6;
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
     p.lb4 = c->role[CV_ROLE_LB4_SERVICES] >= 0 ? c->lb4.view : HashTable{};

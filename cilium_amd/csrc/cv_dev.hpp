@@ -1869,11 +1869,26 @@ __device__ __forceinline__ EpDev ep_netdev4(const DpParams &p, uint32_t idx)
 }
 
 // the same for the IPv6 stages: policy and CT6 tables, SECLABEL
+__device__ __forceinline__ EpDev ep_hot6(const DpParams &p, const EpHot &h, uint32_t idx);
+
 template <bool FULL>
 __device__ __forceinline__ EpDev ep_stage6(const DpParams &p, uint32_t idx)
 {
     if constexpr (FULL) return G(p.eps)[idx];
-    const EpHot h = G(p.ephot6)[idx];
+    return ep_hot6(p, G(p.ephot6)[idx], idx);
+}
+
+// ep_netdev4's IPv6 counterpart (one policy and CT6 map for every endpoint: p.uni6_on)
+template <bool FULL>
+__device__ __forceinline__ EpDev ep_uni6(const DpParams &p, uint32_t idx)
+{
+    if constexpr (!FULL)
+        if (p.uni6_on && !p.ct_guard) return ep_hot6(p, p.uni6, idx);
+    return ep_stage6<FULL>(p, idx);
+}
+
+__device__ __forceinline__ EpDev ep_hot6(const DpParams &p, const EpHot &h, uint32_t idx)
+{
     EpDev e{};
     e.policy = HashTable{h.pol_buckets, h.pol_vals, h.pol_mask, 32u, (uint32_t)PolicySpec::SPB, h.pol_aux, nullptr, 0};
     e.ct6 = HashTable{h.ct_buckets, h.ct_vals, h.ct_mask, (uint32_t)CT_COLD, (uint32_t)Ct6Spec::SPB, nullptr, h.ct_live,

@@ -83,8 +83,8 @@ struct DpParams {              // by value as the kernel argument
     uint8_t *eg_intent;
     // every endpoint on one policy map and one CT4 map with LXC_IPV4 set (cv_ctx.cpp): the
     // netdev stages take that line from here instead of a per-packet EpHot read
-    uint32_t uni4_on;
-    EpHot uni4;
+    uint32_t uni4_on, uni6_on;
+    EpHot uni4, uni6;          // (uni6: one policy and CT6 map for every endpoint)
 };
 
 // Exact conntrack admission next to max_entries (cv_kernels.hip "conntrack

@@ -147,9 +147,7 @@ template <bool FULL>
 __device__ __forceinline__ EpDev eg_src4(const DpParams &p, uint32_t idx)
 {
     if constexpr (FULL) return G(p.eps)[idx];
-    EpDev e = ep_stage4<false>(p, idx);
-    e.seclabel = G(p.eps)[idx].seclabel;
-    return e;
+    return ep_netdev4<false>(p, idx);                             // (the plain LB stage reads the CT map only)
 }
 
 // The service stage's input state of a packet (the front parsed it anyway), in the
@@ -554,7 +552,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     Skb6 s;
     skb6_unpack(d[0], d[1], d[2], b.stride, s);
     uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
-    const EpDev ep = G(p.eps)[d3.x & 0xFFFFu];
+    const EpDev ep = ep_uni6<M::EV>(p, d3.x & 0xFFFFu);          // (the plain instance reads the CT6 map only)
     m.pkt = b.base + i;
     m.hash = b.hash ? b.hash[i] : 0u;
     m.src_id = ep.lxc_id;
@@ -823,6 +821,7 @@ __device__ __forceinline__ void pairs_one(const DpParams &p, const BatchDev &b, 
             Eg4 x;
             eg4_state(r, eg, x);
             eg4_pack(x, eg[1], es);
+            es[2].w = ep.seclabel;                                // (the stage's SECLABEL with uniform tables)
             const uint32_t S = x.t.saddr;
             const uint32_t P = group_node(g, pair_hash4(S, x.t.daddr, SALT_CT4));
             g.gslot[i] = P;
@@ -880,6 +879,7 @@ __device__ __forceinline__ void pairs_one(const DpParams &p, const BatchDev &b, 
             Eg6 x;
             eg6_state(r, eg, x);
             eg6_pack(x, eg[1], (eg[0] & EG_SVC) ? eg[3] : 0u, es);
+            es[3].z = ep.seclabel;
             const uint32_t P = group_node(g, pair_hash6(x.t.saddr, x.t.daddr, SALT_CT6));
             g.gslot[i] = P;
             uint32_t xs[4] = {x.s.saddr[0], x.s.saddr[1], x.s.saddr[2], x.s.saddr[3]};
@@ -1039,9 +1039,11 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     Acct a{0, 0, m.pc};
     if (live) {
         eg4_unpack(g.est + (size_t)i * 4, b.stride, x, epi, fl);
-        // the source endpoint's tables and SECLABEL from its EpHot line; the full EpDev
-        // where the event records need its constants
-        ep = ep_stage4<M::EV>(p, epi);
+        // the source endpoint's tables and SECLABEL from its EpHot line (with one policy
+        // and CT4 map for every endpoint: the common line, SECLABEL from the state); the
+        // full EpDev where the event records need its constants
+        ep = ep_netdev4<M::EV>(p, epi);
+        if (!M::EV) ep.seclabel = g.est[(size_t)i * 4 + 2].w;
         m.pkt = b.base + i;
         m.hash = b.hash ? b.hash[i] : 0u;
         m.src_id = ep.lxc_id;
@@ -1208,7 +1210,8 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     Acct a{0, 0, m.pc};
     if (live) {
         eg6_unpack(g.est + (size_t)i * 4, b.stride, x, epi);
-        ep = ep_stage6<M::EV>(p, epi);
+        ep = ep_uni6<M::EV>(p, epi);
+        if (!M::EV) ep.seclabel = g.est[(size_t)i * 4 + 3].z;
         m.pkt = b.base + i;
         m.hash = b.hash ? b.hash[i] : 0u;
         m.src_id = ep.lxc_id;
@@ -1362,7 +1365,7 @@ __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &
     RevNatOut rn2{false, false, 0, 0};
     uint8_t ct2 = CT_NONE;
     // the destination's tables from its EpHot line (the full EpDev for the event records)
-    const EpDev ep = live ? ep_stage4<M::EV>(p, d1.z & 0xFFFFu) : EpDev{};
+    const EpDev ep = live ? ep_netdev4<M::EV>(p, d1.z & 0xFFFFu) : EpDev{};
     res.ret = handle_policy4<M, EGF, Q>(p, ep, s, d1.w, false, d2.x, now, ct2, res.proxy, res.reason, a, m, &rn2,
                                         nullptr, live, sq);
     if (!live) return;
@@ -1411,7 +1414,7 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     RevNat6Out rn2;
     rn2.valid = false;
     uint8_t ct2 = CT_NONE;
-    const EpDev ep = live ? ep_stage6<M::EV>(p, d3.x & 0xFFFFu) : EpDev{};
+    const EpDev ep = live ? ep_uni6<M::EV>(p, d3.x & 0xFFFFu) : EpDev{};
     res.ret = handle_policy6<M, EGF, Q>(p, ep, s, d3.y, false, d3.z, now, ct2, res.proxy, res.reason, a, m, &rn2,
                                         nullptr, live, sq);
     if (!live) return;

@@ -1,0 +1,160 @@
+"""Endpoints that do not share their maps: the launch parameters then carry no common
+endpoint line (DpParams.uni4 / uni6) and every stage reads the packet's
+own endpoint line.  Endpoints in G groups, each group with its own CT4 and CT6 maps
+(per-endpoint conntrack, bpf_lxc.c's CT_MAP_TCP4 / CT_MAP_TCP6 when the endpoint's CT is
+local: bpf/lib/conntrack_map.h) and every other group with its own copy of the policy
+map (the per-endpoint POLICY_MAP, bpf/lib/maps.h); plus the shared-map workloads with the
+common line switched off (CV_NO_UNI4).  Config 3 (netdev -> lxc ingress) and config 5
+(from-container egress with local delivery): every output, every map of every group,
+the metrics, against the oracle, bit-exact."""
+import numpy as np
+import pytest
+
+from cilium_amd import synth
+from tests import harness as H
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+ING = ("xdp", "ret", "identity", "ct", "proxy", "nl", "nu", "reason")
+EGR = ("ret", "reason", "identity", "ct", "proxy", "nl", "nu")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return "cuda:0"
+
+
+def _grouped(w, groups, make_ctx):
+    """(datapath, maps) with endpoint i on group i % groups: group 0 keeps the workload's
+    CT maps (their preloaded flows), the other groups start empty; odd groups use their
+    own copy of the policy map."""
+    from oracle import oracle as O
+    from cilium_amd import lib
+    if make_ctx:
+        dp = lib.Ctx(0, lib.F_DEFAULT)
+        spec_map = dp.map_from_spec
+        empty = dp.map_create
+        add, cfg = dp.endpoint_add, dp.endpoint_config
+    else:
+        dp = O.ODp(O.F_DEFAULT)
+        spec_map = O.OMap.from_spec
+        empty = O.OMap
+        add, cfg = dp.add_endpoint, dp.endpoint_config
+    maps = {}
+    for name, spec in w.maps.items():
+        if name in ("ct4", "ct6"):
+            continue
+        maps[name] = spec_map(spec)
+        if name in H.ROLE_NAMES:
+            dp.bind(name, maps[name])
+    per = {"ct4": [], "ct6": [], "policy": [maps["policy"]]}
+    for g in range(groups):
+        for name in ("ct4", "ct6"):
+            s = w.maps.get(name)
+            per[name].append(None if s is None else
+                             spec_map(s) if g == 0 else empty(s.type, s.key_size, s.val_size, s.max_entries))
+        if g % 2 == 1:
+            per["policy"].append(spec_map(w.maps["policy"]))
+    for i, e in enumerate(w.endpoints):
+        g = i % groups
+        pol = per["policy"][(g + 1) // 2 if g % 2 == 1 else 0]
+        k = add(e["lxc_id"], e["seclabel"], pol, per["ct4"][g])
+        cfg(k, ct6=per["ct6"][g], **H._ep_cfg(e))
+    if w.extra and "node" in w.extra:
+        dp.node_config(**w.extra["node"])
+    if make_ctx:
+        dp.sync()
+    else:
+        dp.keep += list(maps.values()) + [m for v in per.values() for m in v if m is not None]
+    return dp, per
+
+
+def _same_maps(pm, om):
+    for name in ("ct4", "ct6", "policy"):
+        for g, (a, b) in enumerate(zip(pm[name], om[name])):
+            if a is None:
+                continue
+            ak, av = a.dump()
+            bk, bv = b.dump()
+            assert len(ak) == len(bk), (name, g, len(ak), len(bk))
+            ra, rb = H.sorted_rows(ak, av), H.sorted_rows(bk, bv)
+            assert (ra == rb).all(), (name, g, H.rows_diff(ra, rb))
+
+
+def _check_fields(o, ref, fields, tag):
+    for k in fields:
+        bad = np.nonzero(o[k] != getattr(ref, k))[0]
+        assert len(bad) == 0, (tag, k, bad[:5], o[k][bad[:5]], getattr(ref, k)[bad[:5]])
+
+
+def _ingress_grouped(w, dev, groups, rounds):
+    from tests.test_gpu_parity import run_ingress
+    dp, om = _grouped(w, groups, False)
+    ctx, pm = _grouped(w, groups, True)
+    for r in range(rounds):
+        wr = synth.Workload(w.name, w.maps, w.frames, w.length, w.mark, w.endpoints, now=w.now + r, extra=w.extra)
+        o = run_ingress(ctx, wr, dev, 0, w.n, events=False)
+        ref = dp.netdev_ingress(w.frames, w.length, w.mark, now=w.now + r)
+        _check_fields(o, ref, ING, r)
+        assert (ctx.metrics() == dp.metrics()).all(), r
+    _same_maps(pm, om)
+    assert sum(len(m) for m in pm["ct4"][1:]) > 0                  # the empty groups created flows
+    ctx.close()
+
+
+def _egress_grouped(w, dev, groups, rounds):
+    from tests.test_gpu_egress import run_egress
+    dp, om = _grouped(w, groups, False)
+    ctx, pm = _grouped(w, groups, True)
+    for r in range(rounds):
+        o = run_egress(ctx, w, dev, 0, w.n, w.now + 3 * r, events=False)
+        ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now + 3 * r)
+        _check_fields(o, ref, EGR, r)
+        assert (ctx.metrics() == dp.metrics()).all(), r
+    _same_maps(pm, om)
+    assert sum(len(m) for m in pm["ct4"][1:]) > 0 and sum(len(m) for m in pm["ct6"][1:]) > 0
+    ctx.close()
+
+
+@pytest.mark.parametrize("groups", [2, 5])
+def test_config3_endpoint_groups(dev, groups):
+    w = synth.config3(1 << 16, 1 << 13, n_ep=128, n_cidrs=2048, n_ids=300, seed=71 + groups)
+    _ingress_grouped(w, dev, groups, rounds=2)
+
+
+def test_config3_endpoint_groups_dual_stack(dev):
+    w = synth.config3(1 << 15, 1 << 12, n_ep=96, n_cidrs=2048, n_ids=300, seed=77, v6_frac=0.4)
+    _ingress_grouped(w, dev, 3, rounds=2)
+
+
+def test_config3_endpoint_groups_hot_runs(dev):
+    """few address pairs: runs far over the in-register limit go through k_ct_hot with
+    endpoints on different CT maps"""
+    w = synth.config3(1 << 15, 64, n_ep=16, n_cidrs=512, n_ids=50, seed=78)
+    _ingress_grouped(w, dev, 3, rounds=2)
+
+
+@pytest.mark.parametrize("groups", [2, 5])
+def test_config5_endpoint_groups(dev, groups):
+    w = synth.config5(1 << 15, n_svc=1000, n_ep=128, n_remote=512, seed=81 + groups)
+    _egress_grouped(w, dev, groups, rounds=2)
+
+
+def test_config5_endpoint_groups_hot_flows(dev):
+    w = synth.config5(1 << 14, n_svc=40, n_ep=8, n_remote=16, n_flows=64, seed=88, odd_frac=5.0)
+    _egress_grouped(w, dev, 3, rounds=3)
+
+
+def test_shared_maps_without_common_line(dev, monkeypatch):
+    """The workloads whose endpoints do share their maps, with the common line off: the
+    per-packet endpoint reads the line replaced, on the same inputs."""
+    from tests.test_gpu_egress import check_egress
+    from tests.test_gpu_parity import check_ingress
+    monkeypatch.setenv("CV_NO_UNI4", "1")
+    check_ingress(synth.config3(1 << 15, 1 << 12, n_ep=128, n_cidrs=2048, n_ids=300, seed=91, v6_frac=0.3),
+                  dev, batches=2, events=False)
+    check_egress(synth.config5(1 << 14, n_svc=500, n_ep=64, n_remote=256, seed=92), dev, batches=2,
+                 events=False)

@@ -912,9 +912,27 @@ __device__ __forceinline__ HotAt<S> hot_at(const HashTable &t, int64_t slot)
     }
 }
 
+// CV_HOT_CONTIG: the run read and written in its memory order (h0-h3, h4-h7, h8-h9) at
+// the run's own start -- 8-B aligned for a CT4 slot, so the 16-B accesses there are
+// dword-aligned, not 16-B aligned (the global path serves both at one request each) --
+// and a hit writes back only the parts whose words changed (ct_store_hot_diff)
+#ifndef CV_HOT_CONTIG
+#define CV_HOT_CONTIG 1
+#endif
+
 template <class S>
 __device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, CtE &e)
 {
+#if CV_HOT_CONTIG
+    {
+        const CV_G uint32_t *h = ct_hot<S>(t, slot);
+        const uint4 u = *reinterpret_cast<const CV_G uint4 *>(h), v = *reinterpret_cast<const CV_G uint4 *>(h + 4);
+        const uint2 w = *reinterpret_cast<const CV_G uint2 *>(h + 8);
+        e.w[8] = u.x; e.w[9] = u.y; e.w[10] = u.z; e.w[11] = u.w; e.w[12] = v.x; e.w[13] = v.y;
+        e.w[0] = v.z; e.w[2] = v.w; e.w[4] = w.x; e.w[6] = w.y;
+        return;
+    }
+#endif
     const HotAt<S> q = hot_at<S>(t, slot);
     const uint4 u = q.a[0], v = q.a[1];
     const uint2 w = *q.b;
@@ -939,6 +957,15 @@ typedef uint32_t nt_u2 __attribute__((ext_vector_type(2)));
 template <class S, bool NT = false>
 __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, const CtE &e)
 {
+#if CV_HOT_CONTIG
+    if constexpr (!NT) {
+        CV_G uint32_t *h = ct_hot<S>(t, slot);
+        *reinterpret_cast<CV_G uint4 *>(h) = make_uint4(e.w[8], e.w[9], e.w[10], e.w[11]);
+        *reinterpret_cast<CV_G uint4 *>(h + 4) = make_uint4(e.w[12], e.w[13], e.w[0], e.w[2]);
+        *reinterpret_cast<CV_G uint2 *>(h + 8) = make_uint2(e.w[4], e.w[6]);
+        return;
+    }
+#endif
     const HotAt<S> q = hot_at<S>(t, slot);
     const uint32_t h[10] = {e.w[8], e.w[9], e.w[10], e.w[11], e.w[12], e.w[13], e.w[0], e.w[2], e.w[4], e.w[6]};
     uint4 u, v;
@@ -957,6 +984,26 @@ __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, c
         q.a[1] = v;
         *q.b = w;
     }
+}
+
+// a hit's write-back: the parts of the run whose words differ from what was loaded (o)
+// -- an ingress hit leaves the tx counters alone, an egress hit the rx ones, and the
+// report stamps change once per CT_REPORT_INTERVAL
+template <class S>
+__device__ __forceinline__ void ct_store_hot_diff(const HashTable &t, int64_t slot, const CtE &e, const CtE &o)
+{
+#if CV_HOT_CONTIG
+    CV_G uint32_t *h = ct_hot<S>(t, slot);
+    if ((e.w[8] ^ o.w[8]) | (e.w[9] ^ o.w[9]) | (e.w[10] ^ o.w[10]) | (e.w[11] ^ o.w[11]))
+        *reinterpret_cast<CV_G uint4 *>(h) = make_uint4(e.w[8], e.w[9], e.w[10], e.w[11]);
+    if ((e.w[12] ^ o.w[12]) | (e.w[13] ^ o.w[13]) | (e.w[0] ^ o.w[0]) | (e.w[2] ^ o.w[2]))
+        *reinterpret_cast<CV_G uint4 *>(h + 4) = make_uint4(e.w[12], e.w[13], e.w[0], e.w[2]);
+    if ((e.w[4] ^ o.w[4]) | (e.w[6] ^ o.w[6]))
+        *reinterpret_cast<CV_G uint2 *>(h + 8) = make_uint2(e.w[4], e.w[6]);
+#else
+    (void)o;
+    ct_store_hot<S, CV_NT_HIT != 0>(t, slot, e);
+#endif
 }
 
 template <class S>
@@ -1114,8 +1161,9 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
         st->loopback = (e.bits() & CTB_LB_LOOPBACK) ? 1u : 0u;
         st->slave = e.w[10] & 0xFFFFu;
     }
+    const CtE e0 = e;
     ct_hit_apply<S>(ct, slot, e, action, dir, tcp, seen, len, now, flags, mon);
-    ct_store_hot<S, CV_NT_HIT != 0>(ct, slot, e);
+    ct_store_hot_diff<S>(ct, slot, e, e0);
 }
 
 template <class S>

@@ -498,8 +498,9 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         if (s2 >= 0) {
             CtE e;
             ct_load_hot<Ct4Spec>(ep.ct4, s2, e);                  // (w10: a hot word)
+            const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
-            ct_store_hot<Ct4Spec>(ep.ct4, s2, e);
+            ct_store_hot_diff<Ct4Spec>(ep.ct4, s2, e, e0);
             a.nu++;
         }
     }
@@ -604,8 +605,9 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         if (s2 >= 0) {
             CtE e;
             ct_load_hot<Ct6Spec>(ep.ct6, s2, e);
+            const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
-            ct_store_hot<Ct6Spec>(ep.ct6, s2, e);
+            ct_store_hot_diff<Ct6Spec>(ep.ct6, s2, e, e0);
             a.nu++;
         }
     }

@@ -28,6 +28,23 @@ __global__ void __launch_bounds__(256) k_gather64(const uint4 *t, uint64_t nline
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// k_gather64 with the lines in ascending order: read i goes to line i * step + a random
+// jitter below step (what sorting a batch's random lookups by address gives: the same
+// lines, the same count, nearby addresses per wave)
+__global__ void __launch_bounds__(256) k_gather64_sorted(const uint4 *t, uint64_t nlines, uint64_t n, uint32_t seed,
+                                                         uint32_t *sink)
+{
+    const uint64_t step = nlines / n > 0 ? nlines / n : 1;
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t l = (i * step + mix(i ^ ((uint64_t)seed << 40)) % step) % nlines;
+        const uint4 *p = t + l * 4;
+        uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+        acc += a.x ^ b.y ^ c.z ^ d.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 __global__ void __launch_bounds__(256) k_gather4(const uint32_t *t, uint64_t nwords, uint64_t n, uint32_t seed,
                                                  uint32_t *sink)
 {
@@ -54,7 +71,7 @@ __global__ void __launch_bounds__(256) k_stream(const uint4 *t, uint64_t nvec, u
 }
 
 extern "C" {
-// kind: 0 gather64, 1 gather4, 2 atomic8, 3 stream; returns kernel ms (median of reps)
+// kind: 0 gather64, 1 gather4, 2 atomic8, 3 stream, 4 gather64 sorted; returns kernel ms (median of reps)
 float probe_run(int kind, uint64_t table_bytes, uint64_t n, int grid, int reps)
 {
     void *t = nullptr, *sink = nullptr;
@@ -75,6 +92,9 @@ float probe_run(int kind, uint64_t table_bytes, uint64_t n, int grid, int reps)
                                (uint32_t *)sink);
         else if (kind == 2)
             hipLaunchKernelGGL(k_atomic8, dim3(grid), dim3(256), 0, 0, (unsigned long long *)t, table_bytes / 8, n, r);
+        else if (kind == 4)
+            hipLaunchKernelGGL(k_gather64_sorted, dim3(grid), dim3(256), 0, 0, (const uint4 *)t, table_bytes / 64, n, r,
+                               (uint32_t *)sink);
         else
             hipLaunchKernelGGL(k_stream, dim3(grid), dim3(256), 0, 0, (const uint4 *)t, table_bytes / 16,
                                (uint32_t *)sink);

@@ -4,13 +4,14 @@
 #   usage: bash tools/session.sh <tag> <step>...
 # steps (outputs under gpurun_out/<tag>/):
 #   tests[=<pytest -k expr>]      the -m gpu tests (commas for spaces)   pytest.log
-#   bench=<workload>[,<args>]     one bench line (args: comma-separated)  bench_<workload>.json
+#   bench=<workload>[,<args>]     one bench line (args: comma-separated)  bench_<workload>[args].json
+#   smoke                         __graft_entry__.smoke()                  smoke.log
 #   stats=<workload>[,<args>]     rocprofv3 kernel trace + stats          <workload>[args]_kernel_stats.csv
 #   pmc=<workload>                FETCH / WRITE / TCC hit-miss passes     pmc<k>_<workload>/
 #   deep=<workload>[,<packets>[,<v>]]  SQ / TA / TCP counter passes (v: an _ab/ library)  deep_<workload>[_<v>]/
 #   cal                           the random-line FETCH_SIZE calibration  pmc_cal/
 #   ab=<workload>,<v>[,<v>...]    timing-only A/B of library variants (v = main or a
-#                                 directory under _ab/ holding libcilium_hip.so)  ab_<v>/
+#                                 directory under _ab/ holding libcilium_hip.so)  ab_<workload>_<v>/
 #   env=<workload>,<ENV=V ...>    kernel trace of a short bench run under the settings
 set -u
 TAG=$1; shift
@@ -41,11 +42,14 @@ for st in "$@"; do
     run 900 "$OUT/pytest.log" python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${K[@]}"
     grep -cE "PASSED" "$OUT/pytest.log" >&2 ;;
   bench)
-    W=${A[0]}
+    W=${A[0]}; T=$W; [ ${#A[@]} -gt 1 ] && T=${W}$(printf '%s' "${A[@]:1}" | tr -c 'a-zA-Z0-9.' '_')
     echo "[$(date +%T)] bench $W ${A[*]:1}" >&2
-    timeout -k 10 600 python3 -u bench.py --workload "$W" "${A[@]:1}" > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err" \
-      || { rc=$?; echo "[session] bench rc=$rc" >&2; tail -20 "$OUT/bench_$W.err" >&2; exit $rc; }
-    cat "$OUT/bench_$W.json" ;;
+    timeout -k 10 600 python3 -u bench.py --workload "$W" "${A[@]:1}" > "$OUT/bench_$T.json" 2> "$OUT/bench_$T.err" \
+      || { rc=$?; echo "[session] bench rc=$rc" >&2; tail -20 "$OUT/bench_$T.err" >&2; exit $rc; }
+    cat "$OUT/bench_$T.json" ;;
+  smoke)
+    run 300 "$OUT/smoke.log" python3 -c "import __graft_entry__ as g; g.smoke()"
+    tail -1 "$OUT/smoke.log" >&2 ;;
   stats)
     W=${A[0]}; T=$W; [ ${#A[@]} -gt 1 ] && T=${W}$(printf '%s' "${A[@]:1}" | tr -c 'a-zA-Z0-9.' '_')
     run 600 "$OUT/stats_$T.log" rocprofv3 --kernel-trace --stats -d "$OUT/stats_$T" -o run --output-format csv \
@@ -79,9 +83,10 @@ for st in "$@"; do
     W=${A[0]}
     for v in "${A[@]:1}"; do
       if [ "$v" = main ]; then L=$PWD/cilium_amd/_lib/libcilium_hip.so; else L=$PWD/_ab/$v/libcilium_hip.so; fi
-      CV_LIB=$L run 300 "$OUT/ab_$v.log" rocprofv3 --kernel-trace --stats -d "$OUT/ab_$v" -o run --output-format csv \
+      k=$(ls -d "$OUT/ab_${W}_$v"* 2>/dev/null | wc -l); D=$OUT/ab_${W}_$v$([ "$k" -gt 0 ] && echo ".$k")
+      CV_LIB=$L run 300 "$D.log" rocprofv3 --kernel-trace --stats -d "$D" -o run --output-format csv \
         -- python3 bench.py --workload "$W" --steps 5 --warmup 1 --no-cpu
-      echo "== $v" >&2; kstats "$OUT/ab_$v/run_kernel_stats.csv" >&2
+      echo "== $v" >&2; kstats "$D/run_kernel_stats.csv" >&2
     done ;;
   env)
     W=${A[0]}

@@ -586,17 +586,37 @@ __device__ __forceinline__ void hot_fold(const HashTable &ct, HotLds &L, bool pa
     const uint32_t pre = fx_scan(T, L, &tot);                    // (ends with a barrier)
     const uint32_t x0 = bits_x(L.e[1] & 0xFFFFu);
     const bool rx = hr.dir == CT_INGRESS;
+    // the reductions per wave first (shuffles), then one LDS atomic per wave and word: the
+    // members of a hot run all update one entry, so per-lane atomics would serialise on
+    // the same LDS words
+    uint32_t last = 0, sn[2] = {0u, 0u}, an[2] = {0u, 0u}, pk[2] = {0u, 0u}, by[2] = {0u, 0u};
     if (part) {
         const HitFx f = hit_fx(fx_at(pre, x0), hr.action, hr.dir, hr.tcp, hr.seen);
+        const int d = rx ? 1 : 0;
         if (f.any) {
-            atomicMax(&L.fxlast, (threadIdx.x + 1) << 8 | (f.life == CT_LIFETIME_TCP ? 1u : f.life == CT_CLOSE_TIMEOUT ? 2u
-                                                                                      : 0u));
-            atomicOr(&L.seen[rx ? 1 : 0], hr.seen & 0xFFu);
-            atomicOr(&L.any[rx ? 1 : 0], 1u);
+            last = (threadIdx.x + 1) << 8 | (f.life == CT_LIFETIME_TCP ? 1u : f.life == CT_CLOSE_TIMEOUT ? 2u : 0u);
+            sn[d] = hr.seen & 0xFFu;
+            an[d] = 1u;
         }
-        if (flags & F_CT_ACCOUNTING) {
-            atomicAdd(&L.pk[rx ? 1 : 0], 1u);
-            atomicAdd(&L.by[rx ? 1 : 0], hr.len);
+        if (flags & F_CT_ACCOUNTING) { pk[d] = 1u; by[d] = hr.len; }
+    }
+#pragma unroll
+    for (int k = 32; k; k >>= 1) {
+        last = max(last, (uint32_t)__shfl_xor((int)last, k, 64));
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            sn[d] |= (uint32_t)__shfl_xor((int)sn[d], k, 64);
+            an[d] |= (uint32_t)__shfl_xor((int)an[d], k, 64);
+            pk[d] += (uint32_t)__shfl_xor((int)pk[d], k, 64);
+            by[d] += (uint32_t)__shfl_xor((int)by[d], k, 64);
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (last) atomicMax(&L.fxlast, last);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            if (an[d]) { atomicOr(&L.seen[d], sn[d]); atomicOr(&L.any[d], 1u); }
+            if (pk[d]) { atomicAdd(&L.pk[d], pk[d]); atomicAdd(&L.by[d], by[d]); }
         }
     }
     __syncthreads();

@@ -883,7 +883,7 @@ __device__ __forceinline__ CV_G uint32_t *ct_cold(const HashTable &t, int64_t sl
     return reinterpret_cast<CV_G uint32_t *>(G(t.vals) + (size_t)slot * CT_COLD);
 }
 
-// hot words <-> CtE, the 40-B hot run h0..h9 = {w8 w9 w10 w11 w12 w13 w0 w2 w4 w6} moved
+// hot words <-> CtE, the 40-B hot run h0..h9 = {w8 w9 w0 w2 w10 w11 w12 w13 w4 w6} moved
 // with three vector accesses (two 16-B, one 8-B) instead of five 8-B ones: the texture
 // path spends its cycles per instruction, so every access saved counts for a stage
 // bound by line accesses.  A CT6 slot's run starts 16-B aligned (bytes 48 / 128 / 208 of
@@ -928,8 +928,8 @@ __device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, Ct
         const CV_G uint32_t *h = ct_hot<S>(t, slot);
         const uint4 u = *reinterpret_cast<const CV_G uint4 *>(h), v = *reinterpret_cast<const CV_G uint4 *>(h + 4);
         const uint2 w = *reinterpret_cast<const CV_G uint2 *>(h + 8);
-        e.w[8] = u.x; e.w[9] = u.y; e.w[10] = u.z; e.w[11] = u.w; e.w[12] = v.x; e.w[13] = v.y;
-        e.w[0] = v.z; e.w[2] = v.w; e.w[4] = w.x; e.w[6] = w.y;
+        e.w[8] = u.x; e.w[9] = u.y; e.w[0] = u.z; e.w[2] = u.w; e.w[10] = v.x; e.w[11] = v.y;
+        e.w[12] = v.z; e.w[13] = v.w; e.w[4] = w.x; e.w[6] = w.y;
         return;
     }
 #endif
@@ -942,8 +942,8 @@ __device__ __forceinline__ void ct_load_hot(const HashTable &t, int64_t slot, Ct
     } else {
         h[0] = u.x; h[1] = u.y; h[2] = u.z; h[3] = u.w; h[4] = v.x; h[5] = v.y; h[6] = v.z; h[7] = v.w; h[8] = w.x; h[9] = w.y;
     }
-    e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
-    e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
+    e.w[8] = h[0]; e.w[9] = h[1]; e.w[0] = h[2]; e.w[2] = h[3]; e.w[10] = h[4]; e.w[11] = h[5];
+    e.w[12] = h[6]; e.w[13] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
 }
 
 // NT: the lookup-hit update (ct_hit), written with non-temporal stores -- an entry a
@@ -960,14 +960,14 @@ __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, c
 #if CV_HOT_CONTIG
     if constexpr (!NT) {
         CV_G uint32_t *h = ct_hot<S>(t, slot);
-        *reinterpret_cast<CV_G uint4 *>(h) = make_uint4(e.w[8], e.w[9], e.w[10], e.w[11]);
-        *reinterpret_cast<CV_G uint4 *>(h + 4) = make_uint4(e.w[12], e.w[13], e.w[0], e.w[2]);
+        *reinterpret_cast<CV_G uint4 *>(h) = make_uint4(e.w[8], e.w[9], e.w[0], e.w[2]);
+        *reinterpret_cast<CV_G uint4 *>(h + 4) = make_uint4(e.w[10], e.w[11], e.w[12], e.w[13]);
         *reinterpret_cast<CV_G uint2 *>(h + 8) = make_uint2(e.w[4], e.w[6]);
         return;
     }
 #endif
     const HotAt<S> q = hot_at<S>(t, slot);
-    const uint32_t h[10] = {e.w[8], e.w[9], e.w[10], e.w[11], e.w[12], e.w[13], e.w[0], e.w[2], e.w[4], e.w[6]};
+    const uint32_t h[10] = {e.w[8], e.w[9], e.w[0], e.w[2], e.w[10], e.w[11], e.w[12], e.w[13], e.w[4], e.w[6]};
     uint4 u, v;
     uint2 w;
     if (q.lo) {
@@ -987,17 +987,18 @@ __device__ __forceinline__ void ct_store_hot(const HashTable &t, int64_t slot, c
 }
 
 // a hit's write-back: the parts of the run whose words differ from what was loaded (o)
-// -- an ingress hit leaves the tx counters alone, an egress hit the rx ones, and the
-// report stamps change once per CT_REPORT_INTERVAL
+// -- an ingress hit changes h0-h3 alone (lifetime, bits, the rx counters), an egress hit
+// h0-h3 and the tx counters, and the flags-seen word and report stamps (h4-h7) change
+// once per CT_REPORT_INTERVAL
 template <class S>
 __device__ __forceinline__ void ct_store_hot_diff(const HashTable &t, int64_t slot, const CtE &e, const CtE &o)
 {
 #if CV_HOT_CONTIG
     CV_G uint32_t *h = ct_hot<S>(t, slot);
-    if ((e.w[8] ^ o.w[8]) | (e.w[9] ^ o.w[9]) | (e.w[10] ^ o.w[10]) | (e.w[11] ^ o.w[11]))
-        *reinterpret_cast<CV_G uint4 *>(h) = make_uint4(e.w[8], e.w[9], e.w[10], e.w[11]);
-    if ((e.w[12] ^ o.w[12]) | (e.w[13] ^ o.w[13]) | (e.w[0] ^ o.w[0]) | (e.w[2] ^ o.w[2]))
-        *reinterpret_cast<CV_G uint4 *>(h + 4) = make_uint4(e.w[12], e.w[13], e.w[0], e.w[2]);
+    if ((e.w[8] ^ o.w[8]) | (e.w[9] ^ o.w[9]) | (e.w[0] ^ o.w[0]) | (e.w[2] ^ o.w[2]))
+        *reinterpret_cast<CV_G uint4 *>(h) = make_uint4(e.w[8], e.w[9], e.w[0], e.w[2]);
+    if ((e.w[10] ^ o.w[10]) | (e.w[11] ^ o.w[11]) | (e.w[12] ^ o.w[12]) | (e.w[13] ^ o.w[13]))
+        *reinterpret_cast<CV_G uint4 *>(h + 4) = make_uint4(e.w[10], e.w[11], e.w[12], e.w[13]);
     if ((e.w[4] ^ o.w[4]) | (e.w[6] ^ o.w[6]))
         *reinterpret_cast<CV_G uint2 *>(h + 8) = make_uint2(e.w[4], e.w[6]);
 #else
@@ -1331,8 +1332,8 @@ __device__ __forceinline__ int ct_lookup_pre(const HashTable &ct, T &t, const L4
         ret = CT_ESTABLISHED;
     }
     a.nu++;
-    const CV_G uint32_t *hw = ct_hot<S>(ct, slot);                 // hot words h1 = w9, h2 = w10
-    const uint32_t w9 = hw[1], w10 = hw[2];
+    const CV_G uint32_t *hw = ct_hot<S>(ct, slot);                 // hot words h1 = w9, h4 = w10
+    const uint32_t w9 = hw[1], w10 = hw[4];
     if (st) {
         st->rev_nat = w9 >> 16;
         st->loopback = (w9 & CTB_LB_LOOPBACK) ? 1u : 0u;

@@ -114,6 +114,43 @@ def split_families(w):
     return parts, where
 
 
+def to_device(a, device):
+    """a host array on the device (u16 / u32 as the int16 / int32 views torch holds)"""
+    import torch
+    if a.dtype == np.uint16:
+        a = a.view(np.int16)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def step_batch(name, w, v, base, where, device):
+    """Step v's batch, built on the device from the resident base batch: the workload with
+    fresh client ports on its new flows (synth.port_variant).  Config 5: the two family
+    parts (base = their device frames, where = split_families' row map); else one frame
+    array."""
+    import torch
+    from cilium_amd import synth
+    rows, boff, ports = synth.port_variant(w, v)
+    hi = torch.from_numpy((ports >> 8).astype(np.uint8)).to(device)
+    lo = torch.from_numpy((ports & 0xFF).astype(np.uint8)).to(device)
+    if name == "config5":
+        fv = [p.clone() for p in base]
+        for k in (0, 1):
+            sel = where[rows, 0] == k
+            r = torch.from_numpy(where[rows[sel], 1]).to(device)
+            o = torch.from_numpy(boff[sel]).to(device)
+            s = torch.from_numpy(sel).to(device)
+            fv[k][r, o] = hi[s]
+            fv[k][r, o + 1] = lo[s]
+        return fv
+    fv = base.clone()
+    r, o = torch.from_numpy(rows).to(device), torch.from_numpy(boff).to(device)
+    fv[r, o] = hi
+    fv[r, o + 1] = lo
+    return fv
+
+
 def algorithmic_bytes(name, nl, nu, record=64):
     """B(p) = R + V + 64*L(p) + 64*U(p), summed over the batch."""
     R = record
@@ -354,41 +391,19 @@ def main():
     if stateful:
         out["ct"] = torch.empty(n, dtype=torch.uint8, device=device)
 
-    def to_dev(a):
-        if a.dtype == np.uint16:
-            a = a.view(np.int16)
-        elif a.dtype == np.uint32 and a is not None:
-            a = a.view(np.int32)
-        return torch.from_numpy(np.ascontiguousarray(a)).to(device)
-
     # the batch of every pass, resident in HBM before anything is timed
+    where = None
     if name == "config5":
         parts, where = split_families(w)
-        dev_parts = [{k: to_dev(v) for k, v in p.items()} for p in parts]
+        dev_parts = [{k: to_device(v, device) for k, v in p.items()} for p in parts]
         offs = [0, len(parts[0]["length"])]
     else:
         frames, length, mark = H.to_dev(w, device)
     batches = [None] * (passes + 1)
     if stateful:
-        base = dev_parts if name == "config5" else frames
+        base = [p["frames"] for p in dev_parts] if name == "config5" else frames
         for v in range(1, passes + 1):
-            rows, boff, ports = synth.port_variant(w, v)
-            hi = torch.from_numpy((ports >> 8).astype(np.uint8)).to(device)
-            lo = torch.from_numpy((ports & 0xFF).astype(np.uint8)).to(device)
-            if name == "config5":
-                fv = [p["frames"].clone() for p in base]
-                for k in (0, 1):
-                    sel = where[rows, 0] == k
-                    r = torch.from_numpy(where[rows[sel], 1]).to(device)
-                    o = torch.from_numpy(boff[sel]).to(device)
-                    fv[k][r, o] = hi[torch.from_numpy(sel).to(device)]
-                    fv[k][r, o + 1] = lo[torch.from_numpy(sel).to(device)]
-            else:
-                fv = base.clone()
-                r, o = torch.from_numpy(rows).to(device), torch.from_numpy(boff).to(device)
-                fv[r, o] = hi
-                fv[r, o + 1] = lo
-            batches[v] = fv
+            batches[v] = step_batch(name, w, v, base, where, device)
         log(f"[rank {rank}] {passes} step batches built on the device ({time.time() - t0:.1f}s)")
 
     gc_maps = [maps[k] for k in ("ct4", "ct6") if k in maps] if stateful else []

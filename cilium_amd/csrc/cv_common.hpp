@@ -43,6 +43,10 @@ constexpr uint32_t HOST_ID = 1, WORLD_ID = 2, CLUSTER_ID = 3, HEALTH_ID = 4, HOS
 // datapath option bits (include/cilium_hip.h CV_F_*)
 constexpr uint32_t F_FROM_HOST = 0x1, F_HAVE_L4_POLICY = 0x2, F_DROP_ALL = 0x4, F_CT_ACCOUNTING = 0x8,
                    F_POLICY_INGRESS = 0x10, F_POLICY_EGRESS = 0x20;
+// test hook (CV_COARSE_GROUPS, cv_ctx.cpp params): the netdev front keeps 8 bits of every
+// group key, so groups of different address pairs and CT maps merge into long runs (a
+// coarser grouping is equally exact: DESIGN.md §4)
+constexpr uint32_t F_TEST_COARSE_GROUPS = 0x80000000u;
 
 // conntrack.h:31-66
 constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,

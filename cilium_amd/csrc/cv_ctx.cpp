@@ -252,6 +252,9 @@ struct cv_ctx {
     bool have_last = false;
     bool force_full = false;                   // a publication was lost: compile ipcache / policies in full
     uint64_t publications = 0, full_compiles = 0;
+    // the walkers' error word (GroupScratch::err): host-mapped, so a corrupt list a kernel
+    // met fails the context's next call with -EPROTO without a device wait
+    uint32_t *gerr_host = nullptr, *gerr_dev = nullptr;
 };
 
 namespace {
@@ -944,8 +947,20 @@ int sync_body(cv_ctx *c, hipStream_t stream);
 // the batches already submitted.  All or nothing per table: a table whose compile fails
 // keeps its old version (the next boundary retries it), and the patches already queued
 // for other tables are published against the buffers they were made for.
+// a kernel of an earlier batch met a list word past its launch (GroupScratch::err): the
+// device state of that batch is unknown, every later call fails
+int walker_error(cv_ctx *c)
+{
+    if (c->gerr_host && __atomic_load_n(c->gerr_host, __ATOMIC_ACQUIRE)) {
+        fprintf(stderr, "[cv] a conntrack stage read a list word past its launch (error %#x)\n", *c->gerr_host);
+        return -EPROTO;
+    }
+    return 0;
+}
+
 int sync_locked(cv_ctx *c, hipStream_t stream = nullptr)
 {
+    if (const int e = walker_error(c)) return e;
     const int r = sync_body(c, stream);
     if (r) (void)flush_patches(c, stream);
     return r;
@@ -1083,6 +1098,7 @@ DpParams params(cv_ctx *c)
 {
     DpParams p{};
     p.flags = c->flags;
+    if (getenv("CV_COARSE_GROUPS")) p.flags |= F_TEST_COARSE_GROUPS;
     p.win_lo = 0;
     p.win_span = ~0u;
     p.n_eps = (uint32_t)c->eps.size();
@@ -1240,6 +1256,7 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
     gs.del_ev = c->gdel_ev.as<uint4>();
     gs.est = c->gest.as<uint4>();
     gs.q6 = (uint32_t)Q_NETDEV6;
+    gs.err = c->gerr_dev;
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;
@@ -1771,6 +1788,15 @@ int cv_open(int hip_device, cv_ctx **out)
     if (c->metrics_own.alloc(METRICS_WORDS * 8)) { delete c; return -ENOMEM; }
     (void)hipMemset(c->metrics_own.p, 0, METRICS_WORDS * 8);
     c->metrics = c->metrics_own.as<unsigned long long>();
+    void *eh = nullptr;
+    if (hipHostMalloc(&eh, 64, hipHostMallocMapped) != hipSuccess) { delete c; return -ENOMEM; }
+    c->gerr_host = static_cast<uint32_t *>(eh);
+    *c->gerr_host = 0;
+    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->gerr_dev), eh, 0) != hipSuccess) {
+        (void)hipHostFree(eh);
+        delete c;
+        return -ENOMEM;
+    }
     if (const char *e = getenv("CV_MAX_CHUNK")) {
         const unsigned long v = strtoul(e, nullptr, 0);
         if (v >= 1 && v <= MAX_CHUNK) c->chunk = (uint32_t)v;
@@ -1791,6 +1817,7 @@ void cv_close(cv_ctx *c)
             (void)hipEventDestroy(x.done);
         }
         if (c->last_ev) (void)hipEventDestroy(c->last_ev);
+        if (c->gerr_host) (void)hipHostFree(c->gerr_host);
     }
     delete c;
 }
@@ -2111,7 +2138,7 @@ int cv_sync(cv_ctx *c)
 {
     if (!c) return -EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    return sync_locked(c, nullptr);
+    return sync_locked(c, nullptr);         // (fails with -EPROTO after a walker error: walker_error)
 }
 
 int cv_xdp_prefilter(cv_ctx *c, const cv_batch *b, cv_out *o, void *stream)

@@ -2327,6 +2327,29 @@ __device__ __forceinline__ void uf_union(const GroupScratch &g, uint32_t a, uint
     }
 }
 
+// The walkers trust no list word: a packet index past the launch, or a run {size, members}
+// reaching past `order`'s 2 * lim words (a stale or corrupt list), is stored in g.err --
+// host-mapped, so the context fails its next call with -EPROTO without a device wait --
+// and skipped, never dereferenced.
+__device__ __noinline__ void group_err(const GroupScratch &g, uint32_t code)
+{
+    if (g.err) __hip_atomic_store(g.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool pkt_ok(const GroupScratch &g, uint32_t x)
+{
+    if (x < g.lim) return true;
+    group_err(g, GERR_INDEX);
+    return false;
+}
+// the run at `off` with `cnt` members fits `order` (1 + cnt words from off)
+__device__ __forceinline__ bool run_ok(const GroupScratch &g, uint32_t off, uint32_t cnt)
+{
+    const uint32_t words = 2u * g.lim;
+    if (off < words && cnt >= 1u && cnt < words - off) return true;
+    group_err(g, GERR_INDEX);
+    return false;
+}
+
 // fn(i, run size) for every member of every listed run of queue q, runs in `work`
 // order and members in packet order, then every singleton group (listed densely in
 // `single`); the next member's index is loaded while fn runs.
@@ -2335,12 +2358,14 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
 {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     auto run = [&](uint32_t off) {
+        if (off >= 2u * g.lim) { group_err(g, GERR_INDEX); return; }
         const uint32_t cnt = first_only ? 1u : g.order[off];
+        if (!run_ok(g, off, cnt)) return;
         uint32_t v = g.order[off + 1];
 #pragma unroll 1
         for (uint32_t k = 0; k < cnt; ++k) {
             const uint32_t vn = k + 1 < cnt ? g.order[off + 2 + k] : NONE;
-            fn(v, cnt);
+            if (pkt_ok(g, v)) fn(v, cnt);
             v = vn;
         }
     };
@@ -2349,7 +2374,10 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
     for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
     for (uint32_t j = skip + tid; j < multi; j += stride) run(g.work[j]);   // (skip: the hot runs, k_ct_hot)
     const uint32_t singles = g.cursor[SINGLE_WORD0 + q];
-    for (uint32_t j = tid; j < singles; j += stride) fn(g.single[j], 1u);
+    for (uint32_t j = tid; j < singles; j += stride) {
+        const uint32_t x = g.single[j];
+        if (pkt_ok(g, x)) fn(x, 1u);
+    }
 }
 
 // fn(i) for member `pos` of every group of queue q (position lists, g.flat), in packet
@@ -2365,9 +2393,17 @@ __device__ __forceinline__ void for_each_at(const GroupScratch &g, int q, uint32
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t j = tid; j < total; j += stride) {
         const uint32_t e = g.work[base + j];
-        const uint32_t k1 = runs ? g.order[e] : pos + 1;
+        uint32_t k1 = pos + 1;
+        if (runs) {
+            if (e >= 2u * g.lim) { group_err(g, GERR_INDEX); continue; }
+            k1 = g.order[e];
+            if (!run_ok(g, e, k1)) continue;
+        }
 #pragma unroll 1
-        for (uint32_t k = pos; k < k1; ++k) fn(runs ? g.order[e + 1 + k] : e);
+        for (uint32_t k = pos; k < k1; ++k) {
+            const uint32_t x = runs ? g.order[e + 1 + k] : e;
+            if (pkt_ok(g, x)) fn(x);
+        }
     }
 }
 

@@ -195,7 +195,13 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint4 *est;                // egress: per packet 64 B, the conntrack stage's packed input state
                                // (k_egress_pairs -> k_egress_ct)
     uint32_t q6;               // the IPv6 queue the binned grouping fills (Q_NETDEV6, or Q_LB6 / Q_CT6)
+    uint32_t lim;              // packets of this launch (set by the launchers): every list word the
+                               // walkers read is a packet < lim or an `order` offset < 2 * lim
+    uint32_t *err;             // host-mapped error word of the context: a walker that reads a list
+                               // word past the launch stores GERR_* here and skips it (the host fails
+                               // its next call with -EPROTO), or null
 };
+enum : uint32_t { GERR_INDEX = 1 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
 // the most bins (2^gbits) a launch uses
 constexpr uint32_t GBLK = 256, GBIN_MAX = 1u << 14;

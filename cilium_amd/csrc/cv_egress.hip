@@ -1459,7 +1459,8 @@ __global__ void __launch_bounds__(BLOCK) k_egress_deliver(DpParams p, BatchDev b
     m.pc = &pc;
     const uint32_t total = g.cursor[del_ctr(V6, g.pos)];
     for_each_wave(total, [&](uint32_t j, bool live) {
-        const uint32_t i = live ? g.single[j] : 0u;
+        uint32_t i = live ? g.single[j] : 0u;
+        if (live && !pkt_ok(g, i)) { live = false; i = 0u; }
         if constexpr (V6) deliver6_one<true>(p, b, now, o, g, i, live, m, sq);
         else deliver4_one<true>(p, b, now, o, g, i, live, m, sq);
     });
@@ -1503,7 +1504,8 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
         uint32_t base = 0;
         for (uint32_t l = 0; l < pos; ++l) base += g.cursor[qcls(q, l)];
         for_each_wave(g.cursor[qcls(q, pos)], [&](uint32_t j, bool live) {
-            const uint32_t x = live ? g.work[base + j] : 0u;
+            uint32_t x = live ? g.work[base + j] : 0u;
+            if (live && !pkt_ok(g, x)) { live = false; x = 0u; }
             if constexpr (V6) egress6_one<false, true>(p, b, now, o, g, x, live, m, sq);
             else egress4_one<false, true>(p, b, now, o, g, x, live, m, sq);
         });
@@ -1568,6 +1570,7 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s)
 {
+    g.lim = b.n;
     if (!b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs

@@ -365,6 +365,7 @@ __global__ void __launch_bounds__(BLOCK) CV_NS_OCC k_netdev_front(DpParams p, Ba
             const uint32_t da[4] = {rec_raw32c<38>(r), rec_raw32c<42>(r), rec_raw32c<46>(r), rec_raw32c<50>(r)};
             gkey = (pair_hash6(sa, da, SALT_NETDEV6 ^ (uint64_t)(uintptr_t)ep.ct6.buckets) & ~3ull) | 3ull;
         }
+        if (p.flags & F_TEST_COARSE_GROUPS) gkey &= 0xFF00000000000003ull;
         if (!live) continue;
         g.pkey[i] = gkey;
         g.hword[i] = 0;
@@ -711,12 +712,16 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
     m.pc = &pc;
     const uint32_t nhot = hot_runs(g, Q_NETDEV);
     for (uint32_t r = blockIdx.x; r < nhot; r += gridDim.x) {     // a workgroup per run
-        const uint32_t off = g.work[r], cnt = g.order[off];
-        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;   // (the run's map)
+        const uint32_t off = g.work[r];
+        if (off >= 2u * g.lim) { if (threadIdx.x == 0) group_err(g, GERR_INDEX); continue; }   // (block-uniform)
+        const uint32_t cnt = g.order[off], x0 = g.order[off + 1];
+        if (!run_ok(g, off, cnt) || !pkt_ok(g, x0)) continue;
+        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;   // (the run's map)
         for (uint32_t k0 = 0; k0 < cnt;) {                        // (block-uniform)
             const uint32_t k = k0 + threadIdx.x;
-            const bool live = k < cnt;
-            const uint32_t x = live ? g.order[off + 1 + k] : 0u;
+            uint32_t x = k < cnt ? g.order[off + 1 + k] : 0u;
+            const bool live = k < cnt && pkt_ok(g, x);
+            if (!live) x = 0u;
             uint4 s0{}, s1{};
             if (live) { s0 = g.srec[2 * x]; s1 = g.srec[2 * x + 1]; }
             const uint32_t meta = s1.z;
@@ -734,7 +739,11 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             int64_t slot = -1;
             const int ret = simple ? ct_lookup_pre(ep.ct4, t, s.h, CT_INGRESS, s.len, slot, &st, a, hr) : 0;
             const bool deny = simple && ret >= 0 && policy_ingress_denies(ep.policy, p.flags, s1.w, t.dport, t.nexthdr);
-            const bool change = simple && ((ret == CT_ESTABLISHED && deny) || (ret == CT_NEW && !deny));
+            // a member on another CT map than the run's first (two groups merged by a key
+            // collision: endpoints with their own maps) runs whole, like a key change: the
+            // fold writes the run's map only
+            const bool other_map = simple && ep.ct4.buckets != ct.buckets;
+            const bool change = simple && (other_map || (ret == CT_ESTABLISHED && deny) || (ret == CT_NEW && !deny));
             if (threadIdx.x == 0) { L.c = HOTB; L.lead = HOTB; }
             __syncthreads();
             if (change) atomicMin(&L.c, threadIdx.x);
@@ -1873,9 +1882,22 @@ int launch_policy_ingress(const DpParams &p, int ep, const BatchDev &b, const Ou
     return launch_status(__func__);
 }
 
-int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter, const OutDev &o,
-                        const GroupScratch &g, hipStream_t s)
+// test hook (CV_LIST_INJECT): the first singleton and the first listed run of the IPv4
+// queue name a packet / an `order` offset past the launch, as a stale or corrupt list would
+__global__ void k_list_inject(GroupScratch g)
 {
+    if (threadIdx.x) return;
+    if (g.cursor[SINGLE_WORD0 + Q_NETDEV]) g.single[0] = 0xFFFFFFF0u;
+    uint32_t multi = 0;
+    for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(Q_NETDEV, c)];
+    if (multi) g.work[0] = 0xFFFFFFF0u;
+}
+
+int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter, const OutDev &o,
+                        const GroupScratch &g0, hipStream_t s)
+{
+    GroupScratch g = g0;
+    g.lim = b.n;
     if (!b.n) return 0;
     const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
@@ -1883,14 +1905,17 @@ int launch_netdev_front(const DpParams &p, const BatchDev &b, int with_prefilter
     else hipLaunchKernelGGL(k_netdev_front<false>, grid, blk, 0, s, p, b, o, g, with_prefilter);
     if (const int r = launch_status(__func__)) return r;
     launch_gbin_groups(g, b.n, s);                                // both families' runs and singletons, listed
+    if (getenv("CV_LIST_INJECT")) hipLaunchKernelGGL(k_list_inject, dim3(1), dim3(64), 0, s, g);
     return launch_status(__func__);
 }
 
 // the IPv4 runs, then the IPv6 runs (the two families' conntrack state is disjoint, so
 // the order between them is free), then the deferred creates
-int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, const GroupScratch &g,
+int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, const GroupScratch &g0,
                          hipStream_t s)
 {
+    GroupScratch g = g0;
+    g.lim = b.n;
     if (!b.n) return 0;
     const bool ev = o.frames || p.notify || p.trace;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
@@ -2123,12 +2148,15 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
 #pragma unroll
     for (int c = 1; c < NCLASS; ++c) multi += g.cursor[qcls(q, c)];
     for (uint32_t j = tid; j < multi; j += stride) {
-        const uint32_t off = g.work[j], cnt = g.order[off];
+        const uint32_t off = g.work[j];
+        if (off >= 2u * g.lim) { group_err(g, GERR_INDEX); continue; }
+        const uint32_t cnt = g.order[off];
+        if (!run_ok(g, off, cnt)) continue;
         if (a.pass) {
             bool redo = false;
             for (uint32_t k = 0; k < cnt && !redo; ++k) {
                 const uint32_t x = g.order[off + 1 + k];
-                redo = x >= a.lo && (a.ib[x] & (IB_USED | IB_UNSURE));
+                redo = pkt_ok(g, x) && x >= a.lo && (a.ib[x] & (IB_USED | IB_UNSURE));
             }
             if (!redo) continue;
         }
@@ -2136,7 +2164,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
 #pragma unroll 1
         for (uint32_t k = 0; k < cnt; ++k) {
             const uint32_t x = g.order[off + 1 + k];
-            if (x >= a.lo) one(x);                                // (below: run by an earlier window)
+            if (pkt_ok(g, x) && x >= a.lo) one(x);                // (below: run by an earlier window)
         }
     }
     if (a.pass) return;
@@ -2144,7 +2172,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
     for (uint32_t j = tid; j < singles; j += stride) {
         const uint32_t x = g.single[j];
         cg.reset();
-        if (x >= a.lo) one(x);
+        if (pkt_ok(g, x) && x >= a.lo) one(x);
     }
 }
 
@@ -2298,8 +2326,10 @@ __global__ void __launch_bounds__(1024) k_adm_apply(Admit a, uint32_t n, uint32_
         if (j + k < L) a.budget[a.lo + j + k] = (uint8_t)(out >> (8 * k));
 }
 
-int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s)
+int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g0, const Admit &a, hipStream_t s)
 {
+    GroupScratch g = g0;
+    g.lim = b.n;
     if (!b.n || a.lo >= b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     const uint32_t L = b.n - a.lo, tiles = (L + SCAN_TILE - 1) / SCAN_TILE;

@@ -123,11 +123,14 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
  * behaves like a kernel HASH map: a create past max_entries fails (-E2BIG, the
  * datapath's DROP_CT_CREATE_FAILED), identically in the oracle.  Size max_entries for
  * the flows the node keeps (HBM: ~137 B per entry at the 60 % bucket load) and run
- * cv_ct_gc.  A from-netdev batch next to the limit runs at full width with exact
- * admission: every packet's creates and deletes are resolved against the map's room
- * in packet order first (DESIGN.md §2 "Admission"); other entry points (egress, or
- * more CT maps in one launch than admission tracks) fall back to launches of as many
- * packets as surely fit, and one-packet launches at the limit. */
+ * cv_ct_gc.  A batch next to the limit runs at full width with exact admission:
+ * from-netdev, every packet's creates and deletes are resolved against its map's room
+ * in packet order first; from-container (egress), the pipeline runs with per-packet
+ * create budgets and a scan checks them against the sequential run, re-running the
+ * launch from a saved state until they agree.  Layouts beyond what
+ * admission tracks (more CT maps in one launch than ADMIT_MAPS from-netdev, more than
+ * one CT4 / CT6 map from-container) fall back to launches of as many packets as surely
+ * fit, and one-packet launches at the limit. */
 int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
 /* Slot occupancy of a device CT map (diagnostics, no reference counterpart): out[0]
  * empty slots, out[1] tombstones (deleted entries not yet reclaimed by cv_ct_gc),
@@ -171,7 +174,10 @@ int cv_node_config(cv_ctx *ctx, const cv_node_cfg *cfg);
  * and v6 prefixes and policy entries without waiting for the device.  A write the
  * incremental path cannot apply (other maps, endpoint changes, /0, a table past 80 %
  * load) rebuilds the table after the submitted batches finish.  A context's batches
- * are ordered across streams on the device (no host wait). */
+ * are ordered across streams on the device (no host wait).  -EPROTO (here and from
+ * every later call): a conntrack stage of an earlier batch read a group-list word past
+ * its launch (a corrupt list; the word is skipped, never dereferenced) -- the device
+ * state is suspect, close the context. */
 int cv_sync(cv_ctx *ctx);
 /* publications of incremental writes so far, and rebuilds (boundaries that waited) */
 int cv_publish_stats(cv_ctx *ctx, uint64_t *publications, uint64_t *rebuilds);

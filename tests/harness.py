@@ -199,6 +199,44 @@ class ShardedOracle:
         return base
 
 
+class FamilyOracle:
+    """Config 5's oracle the way bench.py runs the GPU: the IPv4 packets and the IPv6
+    packets as two batches (64-B and 128-B records).  Their conntrack, service and
+    reverse-NAT state is disjoint (CT4 / lb4 vs CT6 / lb6; LXC_NAT46 off); they share only
+    additive state -- the policy counters and cilium_metrics -- so one datapath per family
+    on its own host thread, counters summed, equals one sequential run."""
+
+    def __init__(self, w):
+        from concurrent.futures import ThreadPoolExecutor
+        self.w = w
+        with ThreadPoolExecutor(2) as ex:
+            self.dps = list(ex.map(lambda _: oracle_dp(w), range(2)))
+
+    def lxc_egress(self, parts, frames, now):
+        """per family: the oracle's outputs for its part of the step's frames"""
+        from concurrent.futures import ThreadPoolExecutor
+        run = lambda k: self.dps[k][0].lxc_egress(frames[k], parts[k]["length"], parts[k]["src_ep"],
+                                                  parts[k]["flow_hash"], now=now)
+        with ThreadPoolExecutor(2) as ex:
+            return list(ex.map(run, range(2)))
+
+    def metrics(self):
+        return sum(dp.metrics() for dp, _ in self.dps)
+
+    def policy_rows(self):
+        rows = [sorted_rows(*maps["policy"].dump()) for _, maps in self.dps]
+        assert (rows[0][:, :16] == rows[1][:, :16]).all()
+        init = sorted_rows(self.w.maps["policy"].keys, self.w.maps["policy"].vals)[:, 16:32].copy().view("<u8")
+        c = [r[:, 16:32].copy().view("<u8") for r in rows]
+        out = rows[0].copy()
+        with np.errstate(over="ignore"):
+            out[:, 16:32] = (c[0] + c[1] - init).view(np.uint8)
+        return out
+
+    def digest(self, name):
+        return self.dps[0 if name == "ct4" else 1][1][name].digest()
+
+
 def _dg_mix(z):
     with np.errstate(over="ignore"):
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)

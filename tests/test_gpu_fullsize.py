@@ -176,3 +176,56 @@ def test_config5_full_services(dev):
         ck, cv = pm[name].dump()
         assert H.table_digest(ck, cv) == om[name].digest(), name
     ctx.close()
+
+
+def test_config5_bench_regime(dev, say):
+    """The config-5 regime bench.py times (verdict r04 item 1): the 2^24-packet dual-stack
+    egress batch (50k services, 4096 endpoints) with the CT maps sized by
+    bench.size_conntrack for a default run, split into its IPv4 (64-B) and IPv6 (128-B)
+    launches, two consecutive fresh steps built on the device by bench.step_batch: every
+    per-packet output, cilium_metrics, the policy counters and the CT4 / CT6 digests after
+    each step, bit-exact against the oracle.  At this size the position lists, the
+    continuation lanes and the binned groupings run at the bench's occupancy."""
+    import bench
+    w = bench.make_workload("config5", 1 << 24, 0, 1)
+    bench.size_conntrack("config5", w, passes=3 + 20 + 1)
+    parts, where = bench.split_families(w)
+    say(f"workload: {w.n} packets ({len(parts[0]['length'])} v4, {len(parts[1]['length'])} v6), "
+        f"CT max_entries {w.maps['ct4'].max_entries} / {w.maps['ct6'].max_entries}")
+    fo = H.FamilyOracle(w)
+    say("oracle: one datapath per family loaded")
+    ctx, pm = H.product_ctx(w)
+    dev_parts = [{k: bench.to_device(v, dev) for k, v in p.items()} for p in parts]
+    base = [p["frames"] for p in dev_parts]
+    say("device tables compiled")
+    for v in (1, 2):
+        fv = bench.step_batch("config5", w, v, base, where, dev)
+        got = []
+        for k, p in enumerate(dev_parts):
+            out = H.dev_out(len(parts[k]["length"]), dev)
+            del out["xdp"]
+            ctx.lxc_egress(fv[k], p["length"], out, w.now + v, src_ep=p["src_ep"], flow_hash=p["flow_hash"])
+            got.append(H.host_out(out))
+        del fv
+        rows, boff, ports = synth.port_variant(w, v)
+        fr = H.apply_variant(w.frames, rows, boff, ports)
+        host = [np.ascontiguousarray(fr[np.nonzero(where[:, 0] == k)[0], :s]) for k, s in ((0, 64), (1, 128))]
+        del fr
+        t0 = __import__("time").time()
+        refs = fo.lxc_egress(parts, host, w.now + v)
+        say(f"step {v}: device done, oracle {__import__('time').time() - t0:.1f}s")
+        for k in (0, 1):
+            for f in ("ret", "reason", "identity", "ct", "proxy", "nl", "nu"):
+                bad = np.nonzero(got[k][f] != getattr(refs[k], f))[0]
+                assert len(bad) == 0, (v, k, f, bad[:5], got[k][f][bad[:5]], getattr(refs[k], f)[bad[:5]])
+        assert (ctx.metrics() == fo.metrics()).all(), v
+        pk, pv = pm["policy"].dump()
+        assert (H.sorted_rows(pk, pv) == fo.policy_rows()).all(), v
+        for name in ("ct4", "ct6"):
+            ck, cv = pm[name].dump()
+            assert H.table_digest(ck, cv) == fo.digest(name), (v, name)
+            del ck, cv
+        news = sum(int((g["ct"] == 0).sum()) for g in got)
+        say(f"step {v}: outputs, metrics, policy counters, CT4 {fo.digest('ct4')[0]} / CT6 {fo.digest('ct6')[0]} "
+            f"entries bit-exact ({news} CT_NEW)")
+    ctx.close()

@@ -526,6 +526,37 @@ def test_ct_admission_corrupt_intent_fails_loudly(dev, monkeypatch):
     ctx.close()
 
 
+def test_corrupt_group_list_fails_loudly(dev, monkeypatch):
+    """A group list naming a packet / a run past the launch (CV_LIST_INJECT: the first
+    singleton and the first run of a config-3 batch, written after the grouping) is
+    skipped by the conntrack stages -- no access through it, no fault -- and fails the
+    context's next call with -EPROTO (the host-mapped error word); a fresh context then
+    runs the same batch bit-exact."""
+    w = synth.config3(1 << 16, 1 << 12, n_ep=64, n_cidrs=1024, n_ids=100, seed=59)
+    ctx, pm = H.product_ctx(w)
+    f, l, m = H.to_dev(w, dev)
+    out = H.dev_out(w.n, dev)
+    monkeypatch.setenv("CV_LIST_INJECT", "1")
+    ctx.netdev_ingress(f, l, out, now=w.now, mark=m)           # (asynchronous: the error shows next)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("CV_LIST_INJECT")
+    with pytest.raises(OSError) as ei:
+        ctx.sync()
+    assert ei.value.errno == errno.EPROTO
+    with pytest.raises(OSError) as ei:
+        ctx.netdev_ingress(f, l, out, now=w.now, mark=m)
+    assert ei.value.errno == errno.EPROTO
+    ctx.close()
+    dp, om = H.oracle_dp(w)
+    ctx, pm = H.product_ctx(w)
+    o = run_ingress(ctx, w, dev, 0, w.n, events=False)
+    ref = dp.netdev_ingress(w.frames, w.length, w.mark, now=w.now)
+    for k in ("ret", "identity", "ct", "reason"):
+        assert (o[k] == getattr(ref, k)).all(), k
+    ctx.sync()
+    ctx.close()
+
+
 def test_ct_churn_fill_gc_refill(dev):
     """Conntrack churn at about 50 % slot load: every round a fresh batch creates ~26k
     entries (lifetime now + 60), then ctmap.GC at the next `now` deletes the previous

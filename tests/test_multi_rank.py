@@ -320,3 +320,29 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert total.sum() > 0
     assert (d[0]["metrics_reduced"] == total).all() and (d[1]["metrics_reduced"] == total).all()
     assert d[0]["elapsed"] == d[1]["elapsed"]                       # the MAX over ranks
+
+
+def test_family_oracle_equals_sequential():
+    """test_config5_bench_regime's oracle: config 5's IPv4 and IPv6 packets as two batches
+    on two datapaths (tests/harness.FamilyOracle, the split bench.py runs on the GPU) give
+    one sequential run's outputs, CT4 / CT6 tables, summed policy counters and metrics,
+    over two fresh steps."""
+    import bench
+    w = synth.config5(1 << 13, n_svc=400, n_ep=64, n_remote=256, seed=97)
+    parts, where = bench.split_families(w)
+    dp, om = H.oracle_dp(w)
+    fo = H.FamilyOracle(w)
+    for v in (1, 2):
+        f = H.apply_variant(w.frames, *synth.port_variant(w, v))
+        ref = dp.lxc_egress(f, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now + v)
+        host = [np.ascontiguousarray(f[np.nonzero(where[:, 0] == k)[0], :s]) for k, s in ((0, 64), (1, 128))]
+        got = fo.lxc_egress(parts, host, w.now + v)
+        for k in (0, 1):
+            idx = np.nonzero(where[:, 0] == k)[0]
+            for f_ in ("ret", "reason", "identity", "ct", "proxy", "nl", "nu"):
+                assert (getattr(got[k], f_) == getattr(ref, f_)[idx]).all(), (v, k, f_)
+        assert (fo.metrics() == dp.metrics()).all()
+        assert (fo.policy_rows() == H.sorted_rows(*om["policy"].dump())).all()
+        for name in ("ct4", "ct6"):
+            assert fo.digest(name) == om[name].digest(), name
+    assert sum(int((getattr(g, "ct") == 0).sum()) for g in got) > 0

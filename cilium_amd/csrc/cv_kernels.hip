@@ -1787,16 +1787,140 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
     }
 }
 
+// The same pass as a stream (round 5): a wave reads 1 KiB of the bucket array per
+// instruction (16 B per lane: PARTS lanes per bucket, 8 CT4 / 4 CT6 buckets), GC_W such
+// instructions in flight per lane, and the lanes of a bucket exchange its tag word and
+// the slots' lifetimes by shuffles -- a thread per bucket issued three scattered 8-B /
+// 4-B accesses per bucket, each wave-instruction touching 64 lines.  A deleted slot's
+// words (key + hot run) are zeroed by the lanes holding them, each writing its 16-B part
+// back only when it changed; the part-0 lane writes the tag word, checks the next bucket
+// for the tombstones' reclaim, and zeroes the slot's side words.
+template <class S>
+__device__ void ct_gc_stream(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted, uint32_t *freed)
+{
+    constexpr int PARTS = S::BW / 4, BPC = 64 / PARTS;            // 16-B parts per bucket, buckets per chunk
+    constexpr int GC_W = 8;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    static_assert(64 % PARTS == 0, "whole buckets per wave chunk");
+    const uint32_t lane = threadIdx.x & 63, part = lane % PARTS, lead = lane - part;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t nchunks = (nb + BPC - 1) / BPC;
+    uint4 *B = reinterpret_cast<uint4 *>(t.buckets);
+    uint32_t mine = 0, cleared = 0;
+    for (uint64_t c0 = wave; c0 < nchunks; c0 += GC_W * waves) {
+        uint4 v[GC_W];
+#pragma unroll
+        for (int u = 0; u < GC_W; ++u) {
+            const uint64_t b = (c0 + u * waves) * BPC + lane / PARTS;
+            v[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (b < nb) {
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(B + b * PARTS + part));
+                v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < GC_W; ++u) {
+            if (c0 + u * waves >= nchunks) break;                    // (wave-uniform)
+            const uint64_t b = (c0 + u * waves) * BPC + lane / PARTS;
+            const bool in = b < nb;
+            const uint64_t tags = (uint64_t)(uint32_t)__shfl((int)v[u].x, lead, 64) |
+                                  (uint64_t)(uint32_t)__shfl((int)v[u].y, lead, 64) << 32;
+            uint64_t out = tags;
+            uint32_t del = 0;
+            bool dead = false;
+#pragma unroll
+            for (int sl = 0; sl < S::SPB; ++sl) {
+                constexpr int L0 = S::KEY0 + S::KW;                  // hot word 0 (lifetime) of slot 0
+                const int L = L0 + sl * S::KS;
+                const uint32_t w = (L & 3) == 0 ? v[u].x : (L & 3) == 1 ? v[u].y : (L & 3) == 2 ? v[u].z : v[u].w;
+                const uint32_t life = (uint32_t)__shfl((int)w, lead + (L >> 2), 64);
+                const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
+                if (tag == TAG_DEAD) dead = true;
+                if (tag >= 3 && life < time) {
+                    out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
+                    del |= 1u << sl;
+                    dead = true;
+                }
+            }
+            uint32_t clr = 0;
+            if (in && dead && part == 0) {                           // tombstones back to empty slots
+                const uint64_t nx = (b + 1) & t.mask;
+                const uint32_t *nw = t.buckets + nx * S::BW;         // (any version of it will do, as in ct_gc)
+                const uint64_t ntags = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
+                bool has_empty = false, displaced = false;
+#pragma unroll
+                for (int sl = 0; sl < S::SPB; ++sl) {
+                    const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
+                    has_empty |= tag == TAG_EMPTY;
+                    if (tag < 3) continue;
+                    uint32_t key[S::KW], tg2;
+#pragma unroll
+                    for (int j = 0; j < S::KW; ++j) key[j] = nw[S::KEY0 + sl * S::KS + j];
+                    displaced |= (home_hash<S>(key, tg2) & t.mask) != nx;
+                }
+                if (has_empty && !displaced)
+#pragma unroll
+                    for (int sl = 0; sl < S::SPB; ++sl)
+                        if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) clr |= 1u << sl;
+            }
+            clr = (uint32_t)__shfl((int)clr, lead, 64);
+            if (!in) continue;
+#pragma unroll
+            for (int sl = 0; sl < S::SPB; ++sl)
+                if (clr >> sl & 1u) out &= ~(0xFFull << (8 * sl));
+            if (part == 0) { mine += __popc(del); cleared += __popc(clr); }
+            // this lane's 16-B part as the pass leaves it
+            uint32_t nwd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int W = (int)part * 4 + k;
+                if (W == 0) nwd[k] = (uint32_t)out;
+                if (W == 1) nwd[k] = (uint32_t)(out >> 32);
+#pragma unroll
+                for (int sl = 0; sl < S::SPB; ++sl)
+                    if ((del >> sl & 1u) && W >= S::KEY0 + sl * S::KS && W < S::KEY0 + (sl + 1) * S::KS) nwd[k] = 0u;
+            }
+            if (nwd[0] != v[u].x || nwd[1] != v[u].y || nwd[2] != v[u].z || nwd[3] != v[u].w)
+                B[b * PARTS + part] = make_uint4(nwd[0], nwd[1], nwd[2], nwd[3]);
+            if (part < (uint32_t)S::SPB && (del >> part & 1u)) {     // the slot's side words
+                uint4 *c = reinterpret_cast<uint4 *>(t.vals + (b * S::SPB + part) * CT_COLD);
+                c[0] = c[1] = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+    }
+    const unsigned long long fr = wave_sum(cleared);
+    if (lane == 0 && fr && freed) atomicAdd(freed, (uint32_t)fr);
+    const unsigned long long tot = wave_sum(mine);
+    if (lane == 0 && tot) {
+        atomicAdd(deleted, (uint32_t)tot);
+        if (t.live) atomicAdd(t.live, 0ull - tot);
+    }
+}
+
+#ifndef CV_GC_LANE
+#define CV_GC_LANE 0
+#endif
 __global__ void __launch_bounds__(BLOCK) k_ct_gc(HashTable t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted)
 {
+#if CV_GC_LANE
     if (v6) ct_gc<Ct6Spec>(t, nb, time, deleted, deleted + 1);
     else ct_gc<Ct4Spec>(t, nb, time, deleted, deleted + 1);
+#else
+    if (v6) ct_gc_stream<Ct6Spec>(t, nb, time, deleted, deleted + 1);
+    else ct_gc_stream<Ct4Spec>(t, nb, time, deleted, deleted + 1);
+#endif
 }
 
 // deleted[0]: entries the pass deleted, deleted[1]: tombstones it turned back into empty slots
 int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s)
 {
+#if CV_GC_LANE
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
+#else
+    const uint64_t per_wave = 64 / (v6 ? Ct6Spec::BW / 4 : Ct4Spec::BW / 4);   // buckets per wave chunk
+    uint64_t g = (nb + per_wave * (BLOCK / 64) - 1) / (per_wave * (BLOCK / 64));
+#endif
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_gc, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, time, deleted);
     return launch_status(__func__);

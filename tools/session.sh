@@ -13,6 +13,7 @@
 #   ab=<workload>,<v>[,<v>...]    timing-only A/B of library variants (v = main or a
 #                                 directory under _ab/ holding libcilium_hip.so)  ab_<workload>_<v>/
 #   env=<workload>,<ENV=V ...>    kernel trace of a short bench run under the settings
+#   abx=<v>,<workload>[,<args>]   kernel trace of a short bench run (args) with library variant v
 set -u
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -88,6 +89,14 @@ for st in "$@"; do
         -- python3 bench.py --workload "$W" --steps 5 --warmup 1 --no-cpu
       echo "== $v" >&2; kstats "$D/run_kernel_stats.csv" >&2
     done ;;
+  abx)                                  # abx=<v>,<workload>[,<args>]: kernel trace of a bench run with a library variant
+    v=${A[0]}; W=${A[1]}
+    if [ "$v" = main ]; then L=$PWD/cilium_amd/_lib/libcilium_hip.so; else L=$PWD/_ab/$v/libcilium_hip.so; fi
+    T=${W}$(printf '%s' "${A[@]:2}" | tr -c 'a-zA-Z0-9.' '_')
+    k=$(ls -d "$OUT/abx_${v}_$T"* 2>/dev/null | wc -l); D=$OUT/abx_${v}_$T$([ "$k" -gt 0 ] && echo ".$k")
+    CV_LIB=$L run 400 "$D.log" rocprofv3 --kernel-trace --stats -d "$D" -o run --output-format csv \
+      -- python3 bench.py --workload "$W" --steps 5 --warmup 1 --no-cpu "${A[@]:2}"
+    echo "== $v $T: $(grep -o '"value": [0-9.]*' "$D.log" | head -1)" >&2; kstats "$D/run_kernel_stats.csv" >&2 ;;
   env)
     W=${A[0]}
     k=$(ls -d "$OUT"/env* 2>/dev/null | wc -l)

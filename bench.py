@@ -66,7 +66,7 @@ def lib_sha():
     return build.kernel_sha()
 
 
-def make_workload(name, n, rank, world, flows=1 << 24, zipf=None):
+def make_workload(name, n, rank, world, flows=1 << 24, zipf=None, ep_zipf=None):
     from cilium_amd import synth
     if name == "config2":
         return synth.config2(n)
@@ -77,7 +77,8 @@ def make_workload(name, n, rank, world, flows=1 << 24, zipf=None):
         # whose address pair it owns, and packets of its own pairs (pre-steered by the
         # producer): conntrack sharded by address pair, config 4 of BASELINE.json
         seed = 0xC1A00003 if name == "config3" else 0xC1A00004
-        return synth.config3(n, n_flows=flows, seed=seed, shard=(rank, world) if world > 1 else None, zipf=zipf)
+        return synth.config3(n, n_flows=flows, seed=seed, shard=(rank, world) if world > 1 else None, zipf=zipf,
+                             ep_zipf=ep_zipf)
     if name == "config5":
         return synth.config5(n)
     raise SystemExit(f"unknown workload {name}")
@@ -334,6 +335,12 @@ def main():
     ap.add_argument("--flows", type=int, default=1 << 24, help="configs 3/4: conntrack flows per GPU")
     ap.add_argument("--zipf", type=float, default=None,
                     help="configs 3/4: Zipf(a) flow popularity for the existing flows' packets (elephant flows)")
+    ap.add_argument("--ct-local", type=int, default=None,
+                    help="configs 3/4: ConntrackLocal -- every endpoint its own CT4 map of this max_entries "
+                         "(ctmap.go:54: 64000) holding its flows' preloaded entries (synth.per_endpoint_ct)")
+    ap.add_argument("--ep-zipf", type=float, default=None,
+                    help="configs 3/4: Zipf(a) popularity of the endpoints the preloaded flows belong to (with "
+                         "--ct-local: the busiest endpoints' maps are full)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend at N > 1 (nccl = RCCL)")
     ap.add_argument("--dump", default=None,
                     help="test hook: every rank writes <dir>/rank<r>.npz (its packets' address-pair keys, its "
@@ -367,8 +374,13 @@ def main():
     stateful = name in STATEFUL
     passes = args.warmup + args.steps + 1                          # + the accounting step after the timed ones
     t0 = time.time()
-    w = make_workload(name, args.packets, rank, world, args.flows, args.zipf)
-    if stateful:
+    w = make_workload(name, args.packets, rank, world, args.flows, args.zipf, args.ep_zipf)
+    per_ep = None
+    if args.ct_local:
+        if name not in ("config3", "config4"):
+            raise SystemExit("--ct-local: configs 3 / 4")
+        per_ep = synth.per_endpoint_ct(w, args.ct_local)
+    if stateful and per_ep is None:
         size_conntrack(name, w, passes)
         cts = [k for k in ("ct4", "ct6") if k in w.maps and (name != "config3" or k == "ct4")]
         for k in cts:
@@ -379,7 +391,7 @@ def main():
             if args.ct_max is not None:
                 w.maps[k].max_entries = args.ct_max
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
-    ctx, maps = H.product_ctx(w, device=local)
+    ctx, maps = H.product_ctx(w, device=local, ct_per_ep=per_ep)
     log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")
     metrics_t = torch.zeros(2048, dtype=torch.int64, device=device)
     ctx.metrics_attach(metrics_t)
@@ -406,7 +418,8 @@ def main():
             batches[v] = step_batch(name, w, v, base, where, device)
         log(f"[rank {rank}] {passes} step batches built on the device ({time.time() - t0:.1f}s)")
 
-    gc_maps = [maps[k] for k in ("ct4", "ct6") if k in maps] if stateful else []
+    gc_maps = ([maps[k] for k in ("ct4", "ct6") if k in maps] if per_ep is None else list(maps["ct4_ep"])) \
+        if stateful else []
     gc_deleted = [0]
 
     def now_of(v):
@@ -436,9 +449,15 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] warmup done ({time.time() - t0:.1f}s)")
 
+    def full_maps():
+        """--ct-local: how many endpoint maps hold max_entries entries (syncs, untimed)"""
+        return sum(len(m) >= args.ct_local for m in maps["ct4_ep"])
+
     def slot_load():
         """live entries / slots of every device CT map (cv_ct_slots; syncs, untimed)"""
         r = {}
+        if per_ep is not None:
+            return r
         for k in ("ct4", "ct6"):
             if k in maps and stateful:
                 e, d, l = maps[k].ct_slots()
@@ -446,6 +465,7 @@ def main():
         return r
 
     load_first = slot_load()
+    full_first = full_maps() if per_ep is not None else None
     gc_deleted[0] = 0
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -465,6 +485,7 @@ def main():
     step_ms = [a.elapsed_time(b) for a, b in ev]
     kern_ms = float(np.mean(step_ms))
     load_last = slot_load()
+    full_last = full_maps() if per_ep is not None else None
     gc_timed = gc_deleted[0]
 
     # accounting step (untimed, after the timed region, in the same regime): L(p), U(p)
@@ -572,7 +593,14 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        if stateful:
+        if stateful and per_ep is not None:
+            line["config"]["ct_local"] = {
+                "maps": len(per_ep), "max_entries_per_map": args.ct_local, "ep_zipf": args.ep_zipf,
+                "preloaded_entries": int(sum(len(s) for s in per_ep)),
+                "full_maps_first_last_timed_step": [full_first, full_last],
+                "how": "ConntrackLocal: every endpoint its own CT4 map (synth.per_endpoint_ct); launches next to a "
+                       "map's max_entries run admitted (one sorted segmented scan over all maps' walks)"}
+        elif stateful:
             line["config"]["ct_max_entries"] = {k: int(w.maps[k].max_entries) for k in ("ct4", "ct6") if k in w.maps}
             # live entries / device slots at the first and the last timed step (a table is sized
             # for max_entries at 60 % slot load, so the load tells how far probes walk)

@@ -10,11 +10,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libcilium_hip.so")
-SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip", "cv_agent.cpp"]
+SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip", "cv_sort.hip", "cv_agent.cpp"]
 ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 
 
-DEVICE_SOURCES = ["cv_kernels.hip", "cv_egress.hip", "cv_dev.hpp", "cv_dp.hpp", "cv_hash.hpp", "cv_lpm.hpp",
+DEVICE_SOURCES = ["cv_kernels.hip", "cv_egress.hip", "cv_sort.hip", "cv_dev.hpp", "cv_dp.hpp", "cv_hash.hpp", "cv_lpm.hpp",
                   "cv_common.hpp"]
 
 

@@ -18,6 +18,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/cilium_hip.h"
@@ -228,6 +229,11 @@ struct cv_ctx {
     DevBuf gres, gdel_ev;         // egress: packed outputs (16 B), delivery records' event part (32 B)
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
+    DevBuf adm_mi, adm_keys, adm_sort; // (per packet: map index; walk keys, sorted; radix-sort scratch)
+    // the launch's CT maps as admission and the live-count reads see them (map_table)
+    std::vector<MapObj *> mt_maps;
+    size_t mt_eps = ~(size_t)0;
+    DevBuf mt_live, mt_cap, mt_epmi4, mt_epmi6, mt_out;
     DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
@@ -1455,12 +1461,66 @@ int ct_next_key(cv_ctx *c, MapObj *mo, const uint8_t *key, uint8_t *next)
 std::vector<MapObj *> batch_ct_maps(cv_ctx *c)
 {
     std::vector<MapObj *> v;
+    std::unordered_set<MapObj *> seen;
     for (auto &e : c->eps)
         for (int h : {e.ct4, e.ct6}) {
             MapObj *m = get(c, h);
-            if (m && m->kind != MK_PLAIN && std::find(v.begin(), v.end(), m) == v.end()) v.push_back(m);
+            if (m && m->kind != MK_PLAIN && seen.insert(m).second) v.push_back(m);
         }
     return v;
+}
+
+// The device view of the launch's CT maps (rebuilt when the map list or the endpoints
+// change): per map its live-count pointer and max_entries, per endpoint the index of its
+// CT4 / CT6 map (ADMIT_NO_MAP: none) -- what the admission walks of any number of maps
+// (per-endpoint maps: ConntrackLocal) and the batched live-count reads use.
+int map_table(cv_ctx *c, const std::vector<MapObj *> &maps)
+{
+    if (maps == c->mt_maps && c->mt_eps == c->eps.size()) return 0;
+    if (maps.size() >= ADMIT_NO_MAP) return -E2BIG;
+    std::unordered_map<const MapObj *, uint16_t> idx;
+    std::vector<unsigned long long *> live(maps.size());
+    std::vector<unsigned long long> cap(maps.size());
+    for (size_t k = 0; k < maps.size(); ++k) {
+        idx[maps[k]] = (uint16_t)k;
+        live[k] = maps[k]->live.as<unsigned long long>();
+        cap[k] = maps[k]->cap;
+    }
+    std::vector<uint16_t> mi4(c->eps.size() + 1, (uint16_t)ADMIT_NO_MAP), mi6(c->eps.size() + 1, (uint16_t)ADMIT_NO_MAP);
+    for (size_t e = 0; e < c->eps.size(); ++e) {
+        auto a = idx.find(get(c, c->eps[e].ct4)), b = idx.find(get(c, c->eps[e].ct6));
+        if (a != idx.end()) mi4[e] = a->second;
+        if (b != idx.end()) mi6[e] = b->second;
+    }
+    int r = 0;
+    if ((r = c->mt_live.upload(live.data(), std::max<size_t>(1, live.size()) * 8)) ||
+        (r = c->mt_cap.upload(cap.data(), std::max<size_t>(1, cap.size()) * 8)) ||
+        (r = c->mt_epmi4.upload(mi4.data(), mi4.size() * 2)) || (r = c->mt_epmi6.upload(mi6.data(), mi6.size() * 2)) ||
+        (r = c->mt_out.alloc(std::max<size_t>(1, maps.size()) * 8)))
+        return r;
+    c->mt_maps = maps;
+    c->mt_eps = c->eps.size();
+    return 0;
+}
+
+// every map's exact live count into live_upper (after every batch already submitted, on
+// any stream): one gather kernel and one read for many maps
+void refresh_live(cv_ctx *c, const std::vector<MapObj *> &maps)
+{
+    drain(c);
+    if (maps.size() > 4 && !map_table(c, maps)) {
+        std::vector<unsigned long long> v(maps.size());
+        if (!launch_gather_u64(c->mt_live.as<unsigned long long *const>(), c->mt_out.as<unsigned long long>(),
+                               (uint32_t)maps.size(), nullptr) &&
+            hipMemcpy(v.data(), c->mt_out.p, v.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            for (size_t k = 0; k < maps.size(); ++k) maps[k]->live_upper = v[k];
+            return;
+        }
+    }
+    for (MapObj *m : maps) {
+        uint64_t v = 0;
+        if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
+    }
 }
 
 // Launch-chunk planning against max_entries (ct_live_add, cv_dev.hpp).  A packet
@@ -1484,11 +1544,7 @@ uint32_t ct_plan(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t want, ui
         // every batch already submitted, on any stream, has finished (a batch on another
         // stream against the same CT maps holds a reservation this read would drop)
         (void)s;
-        drain(c);
-        for (MapObj *m : maps) {
-            uint64_t v = 0;
-            if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
-        }
+        refresh_live(c, maps);
         r = room();
     }
     uint64_t n = std::min<uint64_t>(want, r / W);
@@ -1514,13 +1570,7 @@ uint32_t ct_fit_count(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t n, 
         for (MapObj *m : maps) r = std::min(r, m->cap > m->live_upper ? m->cap - m->live_upper : 0);
         return r;
     };
-    if (room() < (uint64_t)W * n) {
-        drain(c);
-        for (MapObj *m : maps) {
-            uint64_t v = 0;
-            if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
-        }
-    }
+    if (room() < (uint64_t)W * n) refresh_live(c, maps);
     return (uint32_t)std::min<uint64_t>(n, room() / W);
 }
 
@@ -1536,11 +1586,7 @@ bool ct_fits(cv_ctx *c, const std::vector<MapObj *> &maps, uint32_t n, uint32_t 
         return r;
     };
     if (room() < (uint64_t)W * n) {
-        drain(c);
-        for (MapObj *m : maps) {
-            uint64_t v = 0;
-            if (hipMemcpy(&v, m->live.p, 8, hipMemcpyDeviceToHost) == hipSuccess) m->live_upper = v;
-        }
+        refresh_live(c, maps);
         if (room() < (uint64_t)W * n) return false;
     }
     for (MapObj *m : maps) {
@@ -1563,23 +1609,34 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
 {
     constexpr int MAX_PASSES = 12;
     const uint32_t n = bc.n;
+    int r = map_table(c, cts);
+    if (r) return r;
     Admit a{};
     a.nmaps = (uint32_t)cts.size();
-    for (size_t k = 0; k < cts.size(); ++k) {
-        a.maps[k] = cts[k]->ct.view.buckets;
-        a.live[k] = cts[k]->live.as<unsigned long long>();
-        a.cap[k] = cts[k]->cap;
-    }
+    a.live = c->mt_live.as<unsigned long long *const>();
+    a.cap = c->mt_cap.as<const unsigned long long>();
+    a.ep_mi4 = c->mt_epmi4.as<const uint16_t>();
+    a.ep_mi6 = c->mt_epmi6.as<const uint16_t>();
+    size_t sort_bytes = 0;
+    if (sort_keys64(nullptr, &sort_bytes, nullptr, nullptr, n, 48, nullptr)) return -EIO;
     if ((c->adm_ib.n < (size_t)n * 2 && c->adm_ib.alloc((size_t)n * 2)) ||
-        (!c->adm_tsum.p && c->adm_tsum.alloc((size_t)ADMIT_MAPS * 4096 * 8)) || (!c->adm_win.p && c->adm_win.alloc(16)))
+        (c->adm_mi.n < (size_t)n * 2 && c->adm_mi.alloc((size_t)n * 2)) ||
+        (c->adm_keys.n < (size_t)n * 16 && c->adm_keys.alloc((size_t)n * 16)) ||
+        (c->adm_sort.n < sort_bytes && c->adm_sort.alloc(sort_bytes)) ||
+        (!c->adm_tsum.p && c->adm_tsum.alloc((size_t)4096 * 12)) || (!c->adm_win.p && c->adm_win.alloc(16)))
         return -ENOMEM;
     a.ib = c->adm_ib.as<uint8_t>();
     a.budget = a.ib + n;
+    a.mi = c->adm_mi.as<uint16_t>();
+    a.keys = c->adm_keys.as<unsigned long long>();
+    a.keys_sorted = a.keys + n;
+    a.sort_tmp = c->adm_sort.p;
+    a.sort_bytes = c->adm_sort.n;
     a.tsum = c->adm_tsum.as<uint32_t>();
     a.hi = c->adm_win.as<uint32_t>();
     const char *inj = getenv("CV_ADMIT_INJECT");
     a.inject = inj ? (uint32_t)strtoul(inj, nullptr, 0) : ~0u;
-    int r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
+    r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
     if (r) return r;
     // packets that reach no conntrack stage keep 0 (no creates, no deletes, map 0);
     // k_ct_intent rewrites the others every pass.  The first pass assumes that earlier
@@ -1688,6 +1745,10 @@ int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_
     }
     add(c->notify_count, 4);
     add(c->trace_count, 4);
+    if (c->eadm_save.n < total) {                                 // a copy that would crowd the device out:
+        size_t fr = 0, all = 0;                                   // the caller's planned launches instead
+        if (hipMemGetInfo(&fr, &all) != hipSuccess || total > fr / 2) return -ENOMEM;
+    }
     if ((c->eadm_save.n < total && c->eadm_save.alloc(total)) ||
         (c->eadm_buf.n < (size_t)n * 4 + 2 * 4096 * 8 + 256 && c->eadm_buf.alloc((size_t)n * 4 + 2 * 4096 * 8 + 256)))
         return -ENOMEM;
@@ -2194,7 +2255,7 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         // a launch whose creates (at most the tuple and its ICMP twin per packet) fit runs
         // at full width; one that may reach a CT map's max_entries runs admitted
-        // (run_admitted), or, with more CT maps than Admit holds, in one-packet guarded launches
+        // (run_admitted: any number of CT maps, each map's walk a segment of one scan)
         n = std::min(c->chunk, b->n - off);
         // short of room for 2 n creates: a launch of room / 2 packets (>= 2^20, so it still
         // fills the device) surely fits and runs at full width without the admission passes
@@ -2203,11 +2264,9 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         uint32_t fit_n = ct_fit_count(c, cts, n, 2);
         if (fit_n < n && fit_n >= std::min<uint32_t>(n, SPLIT_MIN)) n = fit_n;
         const bool fits = ct_fits(c, cts, n, 2);
-        if (!fits && cts.size() > (size_t)ADMIT_MAPS)
-            n = ct_plan(c, cts, n, 2, (hipStream_t)stream, &p.ct_guard);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
         gs.gbits = gbin_bits(n);
-        if (!fits && cts.size() <= (size_t)ADMIT_MAPS) {
+        if (!fits) {
             r = run_admitted(c, p, chunk(b, off, n), chunk(o, off, b->stride), now, with_prefilter, gs, cts,
                              (hipStream_t)stream);
         } else {
@@ -2259,9 +2318,11 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
         if (!fits && admissible) {
             r = lxc_admitted(c, p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
                              now, chunk(o, off, b->stride), cts, (hipStream_t)stream);
-            // no fixed point (the state is back as before the chunk): the chunk again in
-            // planned launches, one guarded packet at a time next to the limit
-            for (uint32_t o2 = off, m; r == -EAGAIN && o2 < off + n; o2 += m) {
+            // no fixed point (the state is back as before the chunk), or no room for the
+            // state's copy (nothing ran): the chunk again in planned launches, one guarded
+            // packet at a time next to the limit
+            const bool again = r == -EAGAIN || r == -ENOMEM;
+            for (uint32_t o2 = off, m; again && o2 < off + n; o2 += m) {
                 m = ct_plan(c, cts, off + n - o2, 7, (hipStream_t)stream, &p.ct_guard);
                 BatchDev bm = chunk(b, o2, m);
                 bm.hash = flow_hash ? flow_hash + o2 : nullptr;

@@ -88,31 +88,44 @@ struct DpParams {              // by value as the kernel argument
 };
 
 // Exact conntrack admission next to max_entries (cv_kernels.hip "conntrack
-// admission", cv_ctx.cpp run_admitted).
-constexpr int ADMIT_MAPS = 4;
+// admission", cv_ctx.cpp run_admitted), for any number of CT maps: every endpoint's
+// CT4 / CT6 map has an index in the launch's map list (per-endpoint maps:
+// ConntrackLocal), and each map's walk is one segment of a scan over the packets with
+// creates or deletes sorted by (map, packet).
+constexpr uint32_t ADMIT_NO_MAP = 0xFFFFu;  // (an endpoint without a CT map of that family)
 struct Admit {
-    const uint32_t *maps[ADMIT_MAPS];  // bucket arrays of the launch's CT maps (map index = position)
-    unsigned long long *live[ADMIT_MAPS];
-    unsigned long long cap[ADMIT_MAPS];
+    const uint16_t *ep_mi4, *ep_mi6;   // per endpoint: its CT4 / CT6 map's index in the map list
+    unsigned long long *const *live;   // per map: its live-entry count
+    const unsigned long long *cap;     // per map: max_entries
     uint32_t nmaps;
     uint32_t lo;                       // the first packet not yet run
     uint32_t pass;                     // the pass over this window (0: every packet from lo)
-    uint8_t *ib;                       // per packet: creates A | deletes D << 2 | map << 3 | read a
-                                       // budget << 5 | unsure << 6 (bit 7: too many changed keys in its run)
+    uint8_t *ib;                       // per packet: creates A | deletes D << 2 | read a budget << 5 |
+                                       // unsure << 6 (bit 7: too many changed keys in its run)
+    uint16_t *mi;                      // per packet: its CT map's index (k_ct_intent)
     uint8_t *budget;                   // per packet: how many of its creates of new entries succeed (the
                                        // previous pass's: what k_ct_intent assumes of earlier creates)
-    uint32_t *tsum;                    // per map and scan tile: the (sum, prefix minimum) of D - A
+    unsigned long long *keys;          // per packet from lo: map << 32 | packet for a packet with creates or
+                                       // deletes, else ~0 (sorted into keys_sorted, the walks' elements)
+    unsigned long long *keys_sorted;
+    uint32_t *tsum;                    // per scan tile of keys_sorted: the segmented (sum, prefix minimum)
     uint32_t *hi;                      // [0] the first unsure packet (the window's end), [1] the first
                                        // packet whose intent changed from the previous pass, [2] the first
                                        // packet whose intent rests on an earlier member's budget, [3] error
                                        // bits (ADMIT_ERR_*: the host fails the batch with -EPROTO)
-    uint32_t inject;                   // test hook (CV_ADMIT_INJECT): this packet's ib byte is corrupted
+    uint32_t inject;                   // test hook (CV_ADMIT_INJECT): this packet's map index is corrupted
                                        // after the intents (~0u: none)
+    void *sort_tmp;                    // radix-sort scratch
+    size_t sort_bytes;
 };
-// a packet's CT map is not one of the launch's (k_ct_intent), an ib byte names a map
-// index past nmaps (k_adm_apply): a stale or corrupt intent, failed loudly instead of
-// indexing past Admit's arrays
+// a packet's endpoint has no CT map in the list (k_ct_intent), a packet's map index is
+// past nmaps (k_adm_keys): a stale or corrupt intent, failed loudly instead of indexing
+// past the map arrays
 enum : uint32_t { ADMIT_ERR_MAP = 1, ADMIT_ERR_IB = 2 };
+// the 64-bit key sort of the admission walks (cv_sort.hip, rocPRIM radix sort over the
+// low end_bit bits); tmp = null: *bytes = the scratch size n keys need
+int sort_keys64(void *tmp, size_t *bytes, const unsigned long long *in, unsigned long long *out, uint32_t n,
+                int end_bit, hipStream_t s);
 
 // Exact egress admission (cv_kernels.hip "egress admission", cv_ctx.cpp lxc_admitted):
 // whether a pass was the sequential run, and the next pass's budgets (one CT4, one CT6 map)
@@ -272,6 +285,8 @@ int launch_ct_op(const HashTable &t, int v6, int op, uint64_t flags, uint32_t *i
 // ctmap.GC (GCFilterByTime): mark entries with lifetime < time dead; adds the count
 int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s);
 int launch_ct_tags(const HashTable &t, int v6, uint64_t nb, unsigned long long *out, hipStream_t s);
+// out[k] = *ptrs[k] (the CT maps' live counts in one read)
+int launch_gather_u64(unsigned long long *const *ptrs, unsigned long long *out, uint32_t n, hipStream_t s);
 // every live entry: slot index (may be null), key words, 16 value words
 int launch_ct_scan(const HashTable &t, int v6, uint64_t nb, uint64_t *out_slots, uint32_t *out_keys, uint32_t *out_vals,
                    uint32_t *count, uint32_t max, hipStream_t s);

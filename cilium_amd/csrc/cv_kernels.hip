@@ -1787,14 +1787,16 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
     }
 }
 
-// The same pass as a stream (round 5): a wave reads 1 KiB of the bucket array per
-// instruction (16 B per lane: PARTS lanes per bucket, 8 CT4 / 4 CT6 buckets), GC_W such
-// instructions in flight per lane, and the lanes of a bucket exchange its tag word and
-// the slots' lifetimes by shuffles -- a thread per bucket issued three scattered 8-B /
-// 4-B accesses per bucket, each wave-instruction touching 64 lines.  A deleted slot's
-// words (key + hot run) are zeroed by the lanes holding them, each writing its 16-B part
-// back only when it changed; the part-0 lane writes the tag word, checks the next bucket
-// for the tombstones' reclaim, and zeroes the slot's side words.
+// The same pass as a stream (round 5): a wave owns GC_W consecutive 1-KiB chunks of the
+// bucket array per iteration (16 B per lane: PARTS lanes per bucket, 8 CT4 / 4 CT6
+// buckets per chunk), all loaded before any is used, plus the bucket after them; the
+// lanes of a bucket exchange its tag word and the slots' lifetimes by shuffles, and the
+// tombstone reclaim reads the next bucket's tags and keys from the registers of the lanes
+// holding it (a thread per bucket issued three scattered 8-B / 4-B accesses per bucket,
+// each wave-instruction touching 64 lines, and its reclaim check two dependent loads).
+// A deleted slot's words (key + hot run) are zeroed by the lanes holding them, each
+// writing its 16-B part back only when it changed; the part-0 lane writes the tag word
+// and a slot's lane zeroes its side words.
 template <class S>
 __device__ void ct_gc_stream(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted, uint32_t *freed)
 {
@@ -1802,27 +1804,30 @@ __device__ void ct_gc_stream(HashTable t, uint64_t nb, uint32_t time, uint32_t *
     constexpr int GC_W = 8;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     static_assert(64 % PARTS == 0, "whole buckets per wave chunk");
-    const uint32_t lane = threadIdx.x & 63, part = lane % PARTS, lead = lane - part;
+    const uint32_t lane = threadIdx.x & 63, part = lane % PARTS, grp = lane / PARTS, lead = lane - part;
     const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
     const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t nchunks = (nb + BPC - 1) / BPC;
     uint4 *B = reinterpret_cast<uint4 *>(t.buckets);
+    auto load = [&](uint64_t b) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (b < nb) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(B + b * PARTS + part));
+            v = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+        return v;
+    };
+    auto comp = [](const uint4 &v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; };
     uint32_t mine = 0, cleared = 0;
-    for (uint64_t c0 = wave; c0 < nchunks; c0 += GC_W * waves) {
+    for (uint64_t c0 = wave * GC_W; c0 < nchunks; c0 += waves * GC_W) {
         uint4 v[GC_W];
 #pragma unroll
-        for (int u = 0; u < GC_W; ++u) {
-            const uint64_t b = (c0 + u * waves) * BPC + lane / PARTS;
-            v[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (b < nb) {
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(B + b * PARTS + part));
-                v[u] = make_uint4(x[0], x[1], x[2], x[3]);
-            }
-        }
+        for (int u = 0; u < GC_W; ++u) v[u] = load((c0 + u) * BPC + grp);
+        const uint4 vn = grp == 0 ? load((c0 + GC_W) * BPC) : make_uint4(0u, 0u, 0u, 0u);   // the bucket after
 #pragma unroll
         for (int u = 0; u < GC_W; ++u) {
-            if (c0 + u * waves >= nchunks) break;                    // (wave-uniform)
-            const uint64_t b = (c0 + u * waves) * BPC + lane / PARTS;
+            if (c0 + u >= nchunks) break;                            // (wave-uniform)
+            const uint64_t b = (c0 + u) * BPC + grp;
             const bool in = b < nb;
             const uint64_t tags = (uint64_t)(uint32_t)__shfl((int)v[u].x, lead, 64) |
                                   (uint64_t)(uint32_t)__shfl((int)v[u].y, lead, 64) << 32;
@@ -1831,10 +1836,8 @@ __device__ void ct_gc_stream(HashTable t, uint64_t nb, uint32_t time, uint32_t *
             bool dead = false;
 #pragma unroll
             for (int sl = 0; sl < S::SPB; ++sl) {
-                constexpr int L0 = S::KEY0 + S::KW;                  // hot word 0 (lifetime) of slot 0
-                const int L = L0 + sl * S::KS;
-                const uint32_t w = (L & 3) == 0 ? v[u].x : (L & 3) == 1 ? v[u].y : (L & 3) == 2 ? v[u].z : v[u].w;
-                const uint32_t life = (uint32_t)__shfl((int)w, lead + (L >> 2), 64);
+                const int L = S::KEY0 + S::KW + sl * S::KS;           // hot word 0 (lifetime) of the slot
+                const uint32_t life = (uint32_t)__shfl((int)comp(v[u], L & 3), lead + (L >> 2), 64);
                 const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
                 if (tag == TAG_DEAD) dead = true;
                 if (tag >= 3 && life < time) {
@@ -1843,28 +1846,38 @@ __device__ void ct_gc_stream(HashTable t, uint64_t nb, uint32_t time, uint32_t *
                     dead = true;
                 }
             }
+            // the next bucket's tags and keys (as loaded: any version of it will do, as in
+            // ct_gc): lanes of group g + 1, and for the chunk's last bucket group 0 of the
+            // next chunk -- source lanes of group 0 hand over that one
             uint32_t clr = 0;
-            if (in && dead && part == 0) {                           // tombstones back to empty slots
-                const uint64_t nx = (b + 1) & t.mask;
-                const uint32_t *nw = t.buckets + nx * S::BW;         // (any version of it will do, as in ct_gc)
-                const uint64_t ntags = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
-                bool has_empty = false, displaced = false;
+            if (__any(in && dead)) {
+                const uint4 src = grp == 0 ? (u + 1 < GC_W ? v[u + 1] : vn) : v[u];
+                const uint32_t nlead = ((grp + 1) % BPC) * PARTS;
+                auto nword = [&](int W) { return (uint32_t)__shfl((int)comp(src, W & 3), nlead + (W >> 2), 64); };
+                const uint64_t ntags = (uint64_t)nword(0) | (uint64_t)nword(1) << 32;
+                uint32_t nkey[S::SPB][S::KW];
 #pragma unroll
-                for (int sl = 0; sl < S::SPB; ++sl) {
-                    const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
-                    has_empty |= tag == TAG_EMPTY;
-                    if (tag < 3) continue;
-                    uint32_t key[S::KW], tg2;
+                for (int sl = 0; sl < S::SPB; ++sl)
 #pragma unroll
-                    for (int j = 0; j < S::KW; ++j) key[j] = nw[S::KEY0 + sl * S::KS + j];
-                    displaced |= (home_hash<S>(key, tg2) & t.mask) != nx;
+                    for (int j = 0; j < S::KW; ++j) nkey[sl][j] = nword(S::KEY0 + sl * S::KS + j);
+                if (in && dead && part == 0) {
+                    const uint64_t nx = (b + 1) & t.mask;
+                    bool has_empty = false, displaced = false;
+#pragma unroll
+                    for (int sl = 0; sl < S::SPB; ++sl) {
+                        const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
+                        has_empty |= tag == TAG_EMPTY;
+                        uint32_t tg2;
+                        if (tag >= 3) displaced |= (home_hash<S>(nkey[sl], tg2) & t.mask) != nx;
+                    }
+                    if (nx == 0) has_empty = false;                  // (the wrap: not in registers)
+                    if (has_empty && !displaced)
+#pragma unroll
+                        for (int sl = 0; sl < S::SPB; ++sl)
+                            if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) clr |= 1u << sl;
                 }
-                if (has_empty && !displaced)
-#pragma unroll
-                    for (int sl = 0; sl < S::SPB; ++sl)
-                        if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) clr |= 1u << sl;
+                clr = (uint32_t)__shfl((int)clr, lead, 64);
             }
-            clr = (uint32_t)__shfl((int)clr, lead, 64);
             if (!in) continue;
 #pragma unroll
             for (int sl = 0; sl < S::SPB; ++sl)
@@ -1918,8 +1931,9 @@ int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_
 #if CV_GC_LANE
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
 #else
-    const uint64_t per_wave = 64 / (v6 ? Ct6Spec::BW / 4 : Ct4Spec::BW / 4);   // buckets per wave chunk
+    const uint64_t per_wave = 8 * 64 / (v6 ? Ct6Spec::BW / 4 : Ct4Spec::BW / 4);   // buckets per wave iteration
     uint64_t g = (nb + per_wave * (BLOCK / 64) - 1) / (per_wave * (BLOCK / 64));
+    if (g > 2048) g = 2048;
 #endif
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_gc, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, time, deleted);
@@ -1957,6 +1971,21 @@ int launch_ct_tags(const HashTable &t, int v6, uint64_t nb, unsigned long long *
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_tags, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, out);
+    return launch_status(__func__);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_gather_u64(unsigned long long *const *ptrs, unsigned long long *out,
+                                                      uint32_t n)
+{
+    for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < n; k += gridDim.x * BLOCK)
+        out[k] = __hip_atomic_load(ptrs[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int launch_gather_u64(unsigned long long *const *ptrs, unsigned long long *out, uint32_t n, hipStream_t s)
+{
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_gather_u64, dim3((n + BLOCK - 1) / BLOCK < 1024 ? (n + BLOCK - 1) / BLOCK : 1024), dim3(BLOCK),
+                       0, s, ptrs, out, n);
     return launch_status(__func__);
 }
 
@@ -2202,13 +2231,12 @@ __device__ __forceinline__ void changed_state(const DpParams &p, const BatchDev 
 // reason: too many changed keys in its run for Changed to hold)
 template <bool V6, class T>
 __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev &b, const GroupScratch &g, uint32_t i,
-                                              Changed<T> &cg, const uint8_t *budget, const uint32_t *&map, bool &used)
+                                              Changed<T> &cg, const uint8_t *budget, bool &used)
 {
     T t;
     EpDev ep;
     uint32_t src;
     const bool any = intent_tuple<V6>(p, b, g, i, t, ep, src);
-    map = V6 ? ep.ct6.buckets : ep.ct4.buckets;
     if (!any) return 0;
     if (cg.overflow()) return 64u | 128u;
     const HashTable &ct = V6 ? ep.ct6 : ep.ct4;
@@ -2251,19 +2279,17 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     Changed<T> cg;
     auto one = [&](uint32_t x) {
-        const uint32_t *map = nullptr;
         bool used = false;
-        const uint32_t v = ct_intent<V6>(p, b, g, x, cg, a.budget, map, used);
-        uint32_t mi = ~0u;
-#pragma unroll
-        for (int k = 0; k < ADMIT_MAPS; ++k)
-            if ((uint32_t)k < a.nmaps && a.maps[k] == map) mi = k;
-        if (mi == ~0u) {                                          // (no conntrack stage: map 0, no intent)
+        const uint32_t v = ct_intent<V6>(p, b, g, x, cg, a.budget, used);
+        const uint32_t e = g.srec[2 * x + 1].z & 0xFFFFu;        // the destination endpoint
+        uint32_t mi = e < p.n_eps ? (V6 ? a.ep_mi6 : a.ep_mi4)[e] : ADMIT_NO_MAP;
+        if (mi >= a.nmaps) {                                      // (no conntrack stage: no intent)
             if (v) atomicOr(a.hi + 3, ADMIT_ERR_MAP);
             mi = 0;
         }
-        const uint32_t nv = v | mi << 3 | (used ? IB_USED : 0u), old = a.ib[x];
+        const uint32_t nv = v | (used ? IB_USED : 0u), old = a.ib[x];
         a.ib[x] = (uint8_t)nv;
+        if (v & 7u) a.mi[x] = (uint16_t)mi;
         if (v & IB_UNSURE) atomicMin(a.hi, x);
         if ((nv ^ old) & ~IB_USED) atomicMin(a.hi + 1, x);
         if (used) atomicMin(a.hi + 2, x);
@@ -2305,17 +2331,22 @@ __global__ void k_admit_init(Admit a, uint32_t n)
     if (threadIdx.x < 4 && blockIdx.x == 0) a.hi[threadIdx.x] = threadIdx.x < 3 ? n : 0u;
 }
 
-// test hook: a packet's intent byte names map 3 with one create (past nmaps when fewer)
+// test hook: a packet with one create whose map index is past the launch's maps
 __global__ void k_admit_inject(Admit a)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) a.ib[a.inject] = (uint8_t)(1u | 3u << 3);
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        a.ib[a.inject] = (uint8_t)((a.ib[a.inject] & ~7u) | 1u);
+        a.mi[a.inject] = (uint16_t)a.nmaps;
+    }
 }
 
 // The reflected walk's two scans as one, over the monoid of (sum, prefix minimum) pairs:
-// (s1, m1) then (s2, m2) = (s1 + s2, min(m1, s1 + m2)); a packet of map m contributes
-// (D - A, D - A) to m's walk and the identity (0, +inf) to the others.  Three kernels
-// for all maps: tile aggregates, their exclusive scan, and a pass that rescans each tile
-// and writes the budgets directly (no per-packet sums in HBM).
+// (s1, m1) then (s2, m2) = (s1 + s2, min(m1, s1 + m2)); a packet contributes (D - A, D - A)
+// to its map's walk.  Every map's walk at once: the packets with creates or deletes,
+// keyed map << 32 | packet and sorted (cv_sort.hip), are one sequence whose maps are
+// segments; a head flag restarts the pair at a segment's first element, (f1, p1) then
+// (f2, p2) = (f1 | f2, f2 ? p2 : p1 then p2).  Three kernels: tile aggregates, their
+// exclusive scan, and a pass that rescans each tile and writes the budgets directly.
 struct SumMin {
     int32_t s, m;
 };
@@ -2355,99 +2386,149 @@ __device__ __forceinline__ SumMin block_excl_summin(SumMin v, SumMin *lds, SumMi
     return r;
 }
 
-// this thread's 4 packets (lo + tile * SCAN_TILE + 4 * thread ..): their ib bytes
-__device__ __forceinline__ uint32_t adm_ib4(const Admit &a, uint32_t L, uint32_t j)
+// the segmented form: (f, s, m), f = a segment starts inside
+struct SegSM {
+    int32_t f, s, m;
+};
+__device__ __forceinline__ SegSM seg_comb(SegSM l, SegSM r)
 {
-    uint32_t w = 0;
+    return r.f ? r : SegSM{l.f, l.s + r.s, min(l.m, l.s + r.m)};
+}
+__device__ __forceinline__ SegSM seg_shfl_up(SegSM v, int d)
+{
+    return {__shfl_up(v.f, d, 64), __shfl_up(v.s, d, 64), __shfl_up(v.m, d, 64)};
+}
+constexpr SegSM SEG_ID{0, 0, SM_INF};
+
+__device__ __forceinline__ SegSM block_excl_seg(SegSM v, SegSM *lds, SegSM *total)
+{
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    SegSM incl = v;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (j + k < L) w |= (uint32_t)a.ib[a.lo + j + k] << (8 * k);
-    return w;
+    for (int d = 1; d < 64; d <<= 1) {
+        const SegSM t = seg_shfl_up(incl, d);
+        if (lane >= (uint32_t)d) incl = seg_comb(t, incl);
+    }
+    if (lane == 63) lds[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SegSM acc = SEG_ID;
+        for (uint32_t w = 0; w < nw; ++w) { const SegSM t = lds[w]; lds[w] = acc; acc = seg_comb(acc, t); }
+        lds[16] = acc;
+    }
+    __syncthreads();
+    SegSM ex = seg_shfl_up(incl, 1);
+    if (!lane) ex = SEG_ID;
+    const SegSM r = seg_comb(lds[wv], ex);
+    if (total) *total = lds[16];
+    __syncthreads();
+    return r;
 }
 
-__device__ __forceinline__ SumMin adm_elem(uint32_t v, uint32_t m)
+// the walks' keys: map << 32 | packet for the packets from lo with creates or deletes
+__global__ void __launch_bounds__(BLOCK) k_adm_keys(Admit a, uint32_t n)
 {
-    if (((v >> 3) & 3u) != m) return SumMin{0, SM_INF};
-    const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
-    return SumMin{d, d};
-}
-
-__global__ void __launch_bounds__(1024) k_adm_tiles(Admit a, uint32_t n, uint32_t tiles)
-{
-    __shared__ SumMin lds[17];
-    const uint32_t L = n - a.lo, j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-    const uint32_t w = adm_ib4(a, L, j);
-    SumMin *agg = reinterpret_cast<SumMin *>(a.tsum);
-    for (uint32_t m = 0; m < a.nmaps; ++m) {
-        SumMin t{0, SM_INF};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (j + k < L) t = sm_comb(t, adm_elem(w >> (8 * k) & 0xFFu, m));
-        SumMin tot;
-        block_excl_summin(t, lds, &tot);
-        if (threadIdx.x == 0) agg[m * tiles + blockIdx.x] = tot;
+    for (uint32_t j = a.lo + blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
+        const uint32_t v = a.ib[j];
+        unsigned long long k = ~0ull;
+        if (v & 7u) {
+            const uint32_t mi = a.mi[j];
+            if (mi >= a.nmaps) atomicOr(a.hi + 3, ADMIT_ERR_IB);   // (a corrupt or stale map index)
+            else k = (unsigned long long)mi << 32 | j;
+        }
+        a.keys[j - a.lo] = k;
     }
 }
 
-// one block: each map's tile aggregates -> exclusive prefixes, in place
+constexpr uint32_t KEY_NONE = 0xFFFFu;                            // (the map field of ~0 keys sorted on 48 bits)
+__device__ __forceinline__ uint32_t key_map(unsigned long long k) { return (uint32_t)(k >> 32) & 0xFFFFu; }
+
+// element q of the sorted sequence (L of them): its map, packet, walk step and head flag
+__device__ __forceinline__ SegSM adm_elem(const Admit &a, uint32_t L, uint32_t q, uint32_t &map, uint32_t &pkt)
+{
+    map = KEY_NONE;
+    pkt = 0;
+    if (q >= L) return SEG_ID;
+    const unsigned long long k = a.keys_sorted[q];
+    map = key_map(k);
+    if (map == KEY_NONE) return SEG_ID;
+    pkt = (uint32_t)k;
+    const uint32_t v = a.ib[pkt];
+    const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
+    const int32_t f = q == 0 || key_map(a.keys_sorted[q - 1]) != map;
+    return SegSM{f, d, d};
+}
+
+__global__ void __launch_bounds__(1024) k_adm_tiles(Admit a, uint32_t L)
+{
+    __shared__ SegSM lds[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    SegSM t = SEG_ID;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t m, x;
+        t = seg_comb(t, adm_elem(a, L, j + k, m, x));
+    }
+    SegSM tot;
+    block_excl_seg(t, lds, &tot);
+    if (threadIdx.x == 0) reinterpret_cast<SegSM *>(a.tsum)[blockIdx.x] = tot;
+}
+
+// one block: the tile aggregates -> exclusive prefixes, in place
 __global__ void __launch_bounds__(1024) k_adm_top(Admit a, uint32_t tiles)
 {
-    __shared__ SumMin lds[17];
-    SumMin *agg = reinterpret_cast<SumMin *>(a.tsum);
-    for (uint32_t m = 0; m < a.nmaps; ++m) {
-        SumMin v[4], t{0, SM_INF};
+    __shared__ SegSM lds[17];
+    SegSM *agg = reinterpret_cast<SegSM *>(a.tsum);
+    SegSM v[4], t = SEG_ID;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t q = threadIdx.x * 4 + k;
-            v[k] = q < tiles ? agg[m * tiles + q] : SumMin{0, SM_INF};
-            t = sm_comb(t, v[k]);
-        }
-        SumMin e = block_excl_summin(t, lds, nullptr);
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t q = threadIdx.x * 4 + k;
+        v[k] = q < tiles ? agg[q] : SEG_ID;
+        t = seg_comb(t, v[k]);
+    }
+    SegSM e = block_excl_seg(t, lds, nullptr);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t q = threadIdx.x * 4 + k;
-            if (q < tiles) agg[m * tiles + q] = e;
-            e = sm_comb(e, v[k]);
-        }
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t q = threadIdx.x * 4 + k;
+        if (q < tiles) agg[q] = e;
+        e = seg_comb(e, v[k]);
     }
 }
 
 // the budgets: the room before packet j is r0 + S - min(0, r0 + M) with (S, M) the
-// walk's (sum, prefix minimum) over lo .. j - 1 of j's map (r0 before lo)
-__global__ void __launch_bounds__(1024) k_adm_apply(Admit a, uint32_t n, uint32_t tiles)
+// walk's (sum, prefix minimum) over the earlier elements of j's map (r0 before lo)
+__global__ void __launch_bounds__(1024) k_adm_apply(Admit a, uint32_t L)
 {
-    __shared__ SumMin lds[17];
-    const uint32_t L = n - a.lo, j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-    const uint32_t w = adm_ib4(a, L, j);
-    const SumMin *agg = reinterpret_cast<const SumMin *>(a.tsum);
-    uint32_t out = 0;
+    __shared__ SegSM lds[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    uint32_t map[4], pkt[4];
+    SegSM e[4], t = SEG_ID;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {                                 // a map index past the launch's maps
-        const uint32_t v = w >> (8 * k) & 0xFFu;
-        if ((v & 7u) && ((v >> 3) & 3u) >= a.nmaps) atomicOr(a.hi + 3, ADMIT_ERR_IB);
+    for (int k = 0; k < 4; ++k) {
+        e[k] = adm_elem(a, L, j + k, map[k], pkt[k]);
+        t = seg_comb(t, e[k]);
     }
-    for (uint32_t m = 0; m < a.nmaps; ++m) {
-        SumMin t{0, SM_INF};
+    SegSM P = seg_comb(reinterpret_cast<const SegSM *>(a.tsum)[blockIdx.x], block_excl_seg(t, lds, nullptr));
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (j + k < L) t = sm_comb(t, adm_elem(w >> (8 * k) & 0xFFu, m));
-        SumMin P = sm_comb(agg[m * tiles + blockIdx.x], block_excl_summin(t, lds, nullptr));
-        const unsigned long long live = __hip_atomic_load(a.live[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const long long r0 = live < a.cap[m] ? (long long)(a.cap[m] - live) : 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t v = w >> (8 * k) & 0xFFu, A = v & 3u;
-            if (((v >> 3) & 3u) == m && A) {
-                const long long lowest = r0 + P.m < 0 ? r0 + P.m : 0;
-                const long long r = r0 + P.s - lowest;
-                out |= (uint32_t)(r < (long long)A ? r : (long long)A) << (8 * k);
-            }
-            P = sm_comb(P, adm_elem(v, m));
+    for (int k = 0; k < 4; ++k) {
+        if (map[k] == KEY_NONE) continue;
+        if (e[k].f) P = SEG_ID;                                   // (the map's first element)
+        const uint32_t A = a.ib[pkt[k]] & 3u;
+        if (A) {
+            const unsigned long long live = __hip_atomic_load(a.live[map[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long r0 = live < a.cap[map[k]] ? (long long)(a.cap[map[k]] - live) : 0;
+            const long long lowest = r0 + P.m < 0 ? r0 + P.m : 0;
+            const long long r = r0 + P.s - lowest;
+            a.budget[pkt[k]] = (uint8_t)(r < (long long)A ? r : (long long)A);
         }
+        P = seg_comb(P, SegSM{0, e[k].s, e[k].m});
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (j + k < L) a.budget[a.lo + j + k] = (uint8_t)(out >> (8 * k));
+}
+
+// every packet from lo: budget 0 until the walks give it one
+__global__ void __launch_bounds__(BLOCK) k_adm_zero(Admit a, uint32_t n)
+{
+    for (uint32_t j = a.lo + blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) a.budget[j] = 0;
 }
 
 int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g0, const Admit &a, hipStream_t s)
@@ -2457,7 +2538,7 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     if (!b.n || a.lo >= b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     const uint32_t L = b.n - a.lo, tiles = (L + SCAN_TILE - 1) / SCAN_TILE;
-    if (tiles > 4096 || a.nmaps > ADMIT_MAPS) return -EINVAL;
+    if (tiles > 4096 || a.nmaps >= KEY_NONE) return -EINVAL;
     hipLaunchKernelGGL(k_admit_init, dim3(1), dim3(64), 0, s, a, b.n);
     hipLaunchKernelGGL(k_ct_intent<false>, grid, blk, 0, s, p, b, g, a);
     GroupScratch g6 = g;
@@ -2465,9 +2546,13 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     g6.work = g.work6;
     hipLaunchKernelGGL(k_ct_intent<true>, grid, blk, 0, s, p, b, g6, a);
     if (a.inject >= a.lo && a.inject < b.n) hipLaunchKernelGGL(k_admit_inject, dim3(1), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
+    hipLaunchKernelGGL(k_adm_keys, grid, blk, 0, s, a, b.n);
+    size_t bytes = a.sort_bytes;
+    if (int r = sort_keys64(a.sort_tmp, &bytes, a.keys, a.keys_sorted, L, 48, s)) return r;
+    hipLaunchKernelGGL(k_adm_zero, grid, blk, 0, s, a, b.n);
+    hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, L);
     hipLaunchKernelGGL(k_adm_top, dim3(1), dim3(1024), 0, s, a, tiles);
-    hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, b.n, tiles);
+    hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, L);
     return launch_status(__func__);
 }
 

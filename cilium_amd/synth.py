@@ -409,7 +409,7 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
             n_cidrs: int = 102400, n_ids: int = 10000, n_ep: int = 4096, ct_max: Optional[int] = None,
             ttl_low: float = 0.0005, v6_frac: float = 0.0, stride: Optional[int] = None,
             n_flows6: Optional[int] = None, shard: Optional[Tuple[int, int]] = None,
-            zipf: Optional[float] = None) -> Workload:
+            zipf: Optional[float] = None, ep_zipf: Optional[float] = None) -> Workload:
     """Ingress through from_netdev into the endpoints' policy programs with conntrack.
     v6_frac > 0 makes a dual-stack batch: that fraction of the packets becomes IPv6
     (handle_ipv6 -> ipv6_policy with a global CT6 map, v6 endpoints in cilium_lxc, v6
@@ -422,7 +422,10 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
     address pair would hand them over.  The ranks' CT shards are disjoint.
     zipf = a: the existing flows' packets (forward and reply) follow a Zipf(a) popularity
     instead of a uniform one (elephant flows: a few address pairs carry many packets of
-    the batch); drawn from a stream of their own, the rest of the batch is unchanged."""
+    the batch); drawn from a stream of their own, the rest of the batch is unchanged.
+    ep_zipf = a: the existing flows' local endpoints follow Zipf(a) instead of a uniform
+    draw (a few endpoints hold most connections: with per-endpoint CT maps,
+    per_endpoint_ct, their maps are the ones at max_entries)."""
     s = Stream(seed)
     c1 = config1(16, n_ep=n_ep)
     c2 = config2(16, n_cidrs=n_cidrs, n_ids=n_ids)
@@ -439,6 +442,8 @@ def config3(n_pkts: int = 1 << 24, n_flows: int = 1 << 24, seed: int = 0xC1A0000
         pick = s.choice(n_flows, len(cidr_addr))
         remote = _rand_addrs_in(s, cidr_addr[pick], cidr_plen[pick])
         epi = s.choice(n_flows, n_ep)
+        if ep_zipf:
+            epi = zipf_ranks(Stream(seed ^ 0xE9E9E9E9), n_flows, n_ep, ep_zipf)
     else:
         pick, remote, epi = _owned_pairs(s, n_flows, shard, cidr_addr, cidr_plen, lxc_ip)
     local = lxc_ip[epi]
@@ -845,6 +850,36 @@ def flow_hash32(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
         z = (z ^ (z >> np.uint64(31))) * np.uint64(0xBF58476D1CE4E5B9)
         z = z ^ (z >> np.uint64(29))
     return (z >> np.uint64(16)).astype(np.uint32)
+
+
+def per_endpoint_ct(w: Workload, max_entries: int, family: str = "ct4") -> List[MapSpec]:
+    """ConntrackLocal (pkg/endpoint/bpf.go:182-187, bpf_lxc.c:53-75): every endpoint its own
+    CT map of `max_entries` (ctmap.go:54: 64000 per endpoint) holding the preloaded entries
+    of its own flows -- the global map's entries whose address is the endpoint's, the first
+    max_entries of them in insertion order (an agent never holds more)."""
+    spec = w.maps[family]
+    alen = 4 if family == "ct4" else 16
+    if alen == 4:
+        ips = np.array([e["ip"] for e in w.endpoints], np.uint32)
+        da = spec.keys[:, 0:4].copy().view(">u4").reshape(-1).astype(np.uint32)
+        sa = spec.keys[:, 4:8].copy().view(">u4").reshape(-1).astype(np.uint32)
+        order = np.argsort(ips)
+        def owner(a):
+            pos = np.clip(np.searchsorted(ips[order], a), 0, len(ips) - 1)
+            return np.where(ips[order][pos] == a, order[pos], -1)
+        ep = owner(da)
+        ep = np.where(ep >= 0, ep, owner(sa))
+    else:
+        where = {bytes(e["ip6"]): i for i, e in enumerate(w.endpoints)}
+        ep = np.array([where.get(bytes(k[0:16]), where.get(bytes(k[16:32]), -1)) for k in spec.keys], np.int64)
+    out = []
+    order = np.argsort(ep, kind="stable")                          # (insertion order within an endpoint)
+    bounds = np.searchsorted(ep[order], np.arange(len(w.endpoints) + 1))
+    for i in range(len(w.endpoints)):
+        idx = order[bounds[i]:bounds[i + 1]][:max_entries]
+        out.append(MapSpec(f"cilium_{family}_{w.endpoints[i]['lxc_id']:05d}", spec.type, spec.key_size, spec.val_size,
+                           max_entries, spec.keys[idx], spec.vals[idx]))
+    return out
 
 
 def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n_ep: int = 4096,

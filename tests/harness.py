@@ -17,40 +17,50 @@ def _ep_cfg(e):
                 node_mac=e.get("node_mac", NODE_MAC))
 
 
-def oracle_dp(w: synth.Workload, flags=None, with_ct=True):
+def oracle_dp(w: synth.Workload, flags=None, with_ct=True, ct_per_ep=None):
+    """ct_per_ep: a CT4 MapSpec per endpoint (synth.per_endpoint_ct, ConntrackLocal) instead
+    of the global map; maps["ct4_ep"] holds them"""
     from oracle import oracle as O
     dp = O.ODp(O.F_DEFAULT if flags is None else flags)
     maps = {}
     for name, spec in w.maps.items():
+        if ct_per_ep is not None and name == "ct4":
+            continue
         maps[name] = O.OMap.from_spec(spec)
         if name in ROLE_NAMES:
             dp.bind(name, maps[name])
     pol = maps.get("policy")
     ct = maps.get("ct4") if with_ct else None
     ct6 = maps.get("ct6") if with_ct else None
+    if ct_per_ep is not None:
+        maps["ct4_ep"] = [O.OMap.from_spec(s) for s in ct_per_ep]
     if w.endpoints:
-        for e in w.endpoints:
-            i = dp.add_endpoint(e["lxc_id"], e["seclabel"], pol, ct)
+        for k, e in enumerate(w.endpoints):
+            i = dp.add_endpoint(e["lxc_id"], e["seclabel"], pol, ct if ct_per_ep is None else maps["ct4_ep"][k])
             dp.endpoint_config(i, ct6=ct6, **_ep_cfg(e))
     if w.extra and "node" in w.extra:
         dp.node_config(**w.extra["node"])
-    dp.keep += list(maps.values())
+    dp.keep += [m for k, m in maps.items() if k != "ct4_ep"] + maps.get("ct4_ep", [])
     return dp, maps
 
 
-def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True):
+def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True, ct_per_ep=None):
     from cilium_amd import lib
     ctx = lib.Ctx(device, lib.F_DEFAULT if flags is None else flags)
     maps = {}
     for name, spec in w.maps.items():
+        if ct_per_ep is not None and name == "ct4":
+            continue
         maps[name] = ctx.map_from_spec(spec)
         if name in ROLE_NAMES:
             ctx.bind(name, maps[name])
     pol = maps.get("policy")
     ct = maps.get("ct4") if with_ct else None
     ct6 = maps.get("ct6") if with_ct else None
-    for e in w.endpoints:
-        i = ctx.endpoint_add(e["lxc_id"], e["seclabel"], pol, ct)
+    if ct_per_ep is not None:
+        maps["ct4_ep"] = [ctx.map_from_spec(s) for s in ct_per_ep]
+    for k, e in enumerate(w.endpoints):
+        i = ctx.endpoint_add(e["lxc_id"], e["seclabel"], pol, ct if ct_per_ep is None else maps["ct4_ep"][k])
         ctx.endpoint_config(i, ct6=ct6, **_ep_cfg(e))
     if w.extra and "node" in w.extra:
         ctx.node_config(**w.extra["node"])

@@ -168,3 +168,58 @@ def test_shared_maps_without_common_line(dev, monkeypatch):
                   dev, batches=2, events=False)
     check_egress(synth.config5(1 << 14, n_svc=500, n_ep=64, n_remote=256, seed=92), dev, batches=2,
                  events=False)
+
+
+def test_config3_per_endpoint_ct_admission(dev, capfd):
+    """ConntrackLocal next to max_entries (verdict r04 item 3): 256 endpoints, each its
+    own CT4 map (synth.per_endpoint_ct), connections concentrated on a few endpoints
+    (ep_zipf) so dozens of maps start full while the others have room.  Each batch runs
+    admitted at full width -- every map's walk one segment of the sorted scan -- with no
+    one-packet launches; every output, every endpoint's map, metrics and policy counters
+    against the oracle, over two batches (deletes after a policy change make room)."""
+    import re
+    w = synth.config3(1 << 18, 1 << 16, n_ep=256, n_cidrs=2048, n_ids=300, seed=83, ep_zipf=1.1)
+    per = synth.per_endpoint_ct(w, 1 << 20)
+    counts = np.array(sorted(len(s) for s in per))
+    cap = int(counts[-40])                                       # the 40 busiest maps start full
+    per = synth.per_endpoint_ct(w, cap)
+    full0 = sum(len(s) >= cap for s in per)
+    assert full0 >= 40
+    dp, om = H.oracle_dp(w, ct_per_ep=per)
+    ctx, pm = H.product_ctx(w, ct_per_ep=per)
+    capfd.readouterr()
+    import os
+    os.environ["CV_ADMIT_STATS"] = "1"
+    try:
+        for r in range(2):
+            if r == 1:                                           # the agent removes a third of the L4 rules
+                pk, _ = om["policy"].dump()
+                for k in pk[::3]:
+                    if k[6]:
+                        assert om["policy"].delete(k.tobytes()) == 0
+                        assert pm["policy"].delete(k.tobytes()) == 0
+            wr = synth.Workload(w.name, w.maps, w.frames, w.length, w.mark, w.endpoints, now=w.now + r, extra=w.extra)
+            from tests.test_gpu_parity import run_ingress
+            o = run_ingress(ctx, wr, dev, 0, w.n, events=False)
+            ref = dp.netdev_ingress(w.frames, w.length, w.mark, now=w.now + r)
+            _check_fields(o, ref, ING, r)
+            assert (ctx.metrics() == dp.metrics()).all(), r
+    finally:
+        del os.environ["CV_ADMIT_STATS"]
+    err = capfd.readouterr().err
+    stats = re.findall(r"\[cv admit\] (\d+) packets in (\d+) windows, (\d+) passes", err)
+    assert stats and all(int(p) == w.n for p, _, _ in stats), err[-2000:]    # whole-batch launches
+    full = 0
+    for a, b in zip(pm["ct4_ep"], om["ct4_ep"]):
+        ak, av = a.dump()
+        bk, bv = b.dump()
+        assert len(ak) == len(bk)
+        assert (H.sorted_rows(ak, av) == H.sorted_rows(bk, bv)).all()
+        full += len(bk) == cap
+    assert full >= 40
+    ok, ov = om["policy"].dump()
+    pk, pv = pm["policy"].dump()
+    assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all()
+    m = dp.metrics()
+    assert m[155, 1, 0] > 1000                                     # DROP_CT_CREATE_FAILED in the full maps
+    ctx.close()

@@ -32,7 +32,8 @@ enum : int32_t {
 // more of the frame); E_PUNT: the packet left the path through a tail call into a
 // responder program (ARP, ICMPv6 NS / echo-to-router / hop limit); E_FAULT: the
 // -EFAULT of a failed skb_load_bytes(), which the reference treats as a drop code.
-enum : int32_t { TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7, E_TRUNC = -1, E_PUNT = -2, E_FAULT = -14 };
+enum : int32_t { TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7, E_TRUNC = -1, E_PUNT = -2, E_DEFER = -3,
+                 E_FAULT = -14 };
 enum : uint8_t { XDP_DROP = 1, XDP_PASS = 2 };
 enum : uint8_t { CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3, CT_NONE = 0xff };
 enum : int { CT_EGRESS = 0, CT_INGRESS = 1, CT_SERVICE = 2 };

@@ -1623,7 +1623,7 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
         (c->adm_mi.n < (size_t)n * 2 && c->adm_mi.alloc((size_t)n * 2)) ||
         (c->adm_keys.n < (size_t)n * 16 && c->adm_keys.alloc((size_t)n * 16)) ||
         (c->adm_sort.n < sort_bytes && c->adm_sort.alloc(sort_bytes)) ||
-        (!c->adm_tsum.p && c->adm_tsum.alloc((size_t)4096 * 12)) || (!c->adm_win.p && c->adm_win.alloc(16)))
+        (!c->adm_tsum.p && c->adm_tsum.alloc((size_t)4096 * 12)) || (!c->adm_win.p && c->adm_win.alloc(32)))
         return -ENOMEM;
     a.ib = c->adm_ib.as<uint8_t>();
     a.budget = a.ib + n;
@@ -1646,12 +1646,12 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     uint32_t windows = 0, passes = 0;
     for (uint32_t lo = 0; lo < n; ++windows) {
         a.lo = lo;
-        uint32_t end = lo, w[4] = {n, n, n, 0};
+        uint32_t end = lo, w[5] = {n, n, n, 0, 0};
         for (int pass = 0;; ++pass) {
             a.pass = (uint32_t)pass;
             if ((r = launch_admission(p, bc, gs, a, s))) return r;
             ++passes;
-            hipError_t e = hipMemcpyAsync(w, a.hi, 16, hipMemcpyDeviceToHost, s);
+            hipError_t e = hipMemcpyAsync(w, a.hi, 20, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) {
                 fprintf(stderr, "[cv] admission pass at %u: %s\n", lo, hipGetErrorString(e));
@@ -1661,6 +1661,7 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
                 fprintf(stderr, "[cv] admission pass at %u: intent error %#x\n", lo, w[3]);
                 return -EPROTO;
             }
+            if ((r = launch_admission_walks(bc, a, w[4], s))) return r;   // (the budgets, in stream order)
             const uint32_t hi = w[0], chg = w[1], used = w[2];
             if (hi <= lo || hi > n || (pass && chg <= lo) || used <= lo) {   // (the window's first packet is exact)
                 fprintf(stderr, "[cv] admission window at %u: %u %u %u of %u\n", lo, hi, chg, used, n);
@@ -2282,10 +2283,21 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
     return 0;
 }
 
-int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash,
-                  uint32_t now, cv_out *o, void *stream)
+}  // extern "C"
+
+namespace {
+
+// cv_lxc_egress, and with `deliver` its split form (cv_lxc_egress_split)
+int lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash,
+               uint32_t now, cv_out *o, uint8_t *deliver, void *stream)
 {
     if (!c) return -EINVAL;
+    if (deliver && (reinterpret_cast<uintptr_t>(deliver) & 15)) return -EINVAL;
+    auto oc = [&](uint32_t off) {
+        OutDev d = chunk(o, off, b->stride);
+        if (deliver) d.deliver = reinterpret_cast<uint4 *>(deliver) + (size_t)off * DEL_SLOTS;
+        return d;
+    };
     int r = check_batch(b);
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
@@ -2317,7 +2329,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
         if (!fits && admissible) {
             r = lxc_admitted(c, p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
-                             now, chunk(o, off, b->stride), cts, (hipStream_t)stream);
+                             now, oc(off), cts, (hipStream_t)stream);
             // no fixed point (the state is back as before the chunk), or no room for the
             // state's copy (nothing ran): the chunk again in planned launches, one guarded
             // packet at a time next to the limit
@@ -2329,7 +2341,7 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
                 GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
                 gs.gbits = gbin_bits(m);
                 int r2 = launch_lxc_egress(p, bm, src_ep ? src_ep + o2 : nullptr, ep0,
-                                           flow_hash ? flow_hash + o2 : nullptr, now, chunk(o, o2, b->stride), gs,
+                                           flow_hash ? flow_hash + o2 : nullptr, now, oc(o2), gs,
                                            (hipStream_t)stream);
                 p.ct_guard = 0;
                 for (const HashTable &t : pols)
@@ -2341,13 +2353,67 @@ int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t
             GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
             gs.gbits = gbin_bits(n);                              // (the binned grouping of the components)
             r = launch_lxc_egress(p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
-                                  now, chunk(o, off, b->stride), gs, (hipStream_t)stream);
+                                  now, oc(off), gs, (hipStream_t)stream);
         }
         p.ct_guard = 0;
         if (r) return r;
         for (const HashTable &t : pols)
             if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
         if (getenv("CV_GROUP_STATS")) group_stats(c, "egress", (hipStream_t)stream, true);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cv_lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash,
+                  uint32_t now, cv_out *o, void *stream)
+{
+    return lxc_egress(c, b, src_ep, ep0, flow_hash, now, o, nullptr, stream);
+}
+
+int cv_lxc_egress_split(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0, const uint32_t *flow_hash,
+                        uint32_t now, cv_out *o, uint8_t *deliver, void *stream)
+{
+    if (!deliver) return -EINVAL;
+    return lxc_egress(c, b, src_ep, ep0, flow_hash, now, o, deliver, stream);
+}
+
+int cv_lxc_deliver(cv_ctx *c, const uint8_t *records, uint32_t n, int v6, uint32_t now, cv_out *o, void *stream)
+{
+    if (!c || (n && !records) || (reinterpret_cast<uintptr_t>(records) & 15)) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    for (auto &e : c->eps) if (e.ct4 < 0 || e.policy < 0) return -EINVAL;
+    int r;
+    if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
+    StreamScope scope(c, (hipStream_t)stream);
+    const uint32_t cmax = std::min(n, c->chunk);
+    if ((r = ensure_groups(c, std::max<uint32_t>(cmax, 1), false))) return r;
+    std::set<const void *> seen;
+    std::vector<HashTable> pols;
+    for (auto &e : c->eps) {
+        const HashTable &t = get(c, e.policy)->pol.view;
+        if (seen.insert(t.vals).second) pols.push_back(t);
+    }
+    DpParams p = params(c);
+    const std::vector<MapObj *> cts = batch_ct_maps(c);
+    for (uint32_t off = 0, m; off < n; off += m) {
+        // a record creates at most the tuple and its ICMP twin in its destination's map: a
+        // launch that surely fits runs whole, else planned launches (one guarded record at
+        // a time next to the limit)
+        m = std::min(c->chunk, n - off);
+        if (!ct_fits(c, cts, m, 2)) m = ct_plan(c, cts, m, 2, (hipStream_t)stream, &p.ct_guard);
+        GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
+        gs.gbits = gbin_bits(m);
+        gs.del = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(records)) + (size_t)off * DEL_SLOTS;
+        const BatchDev bd{nullptr, v6 ? 128u : 64u, m, nullptr, nullptr, off, nullptr};
+        r = launch_lxc_deliver(p, bd, now, chunk(o, off), gs, v6, (hipStream_t)stream);
+        p.ct_guard = 0;
+        if (r) return r;
+        for (const HashTable &t : pols)
+            if ((r = launch_policy_fold(t, (hipStream_t)stream))) return r;
     }
     return 0;
 }

@@ -91,7 +91,7 @@ struct DpParams {              // by value as the kernel argument
 // admission", cv_ctx.cpp run_admitted), for any number of CT maps: every endpoint's
 // CT4 / CT6 map has an index in the launch's map list (per-endpoint maps:
 // ConntrackLocal), and each map's walk is one segment of a scan over the packets with
-// creates or deletes sorted by (map, packet).
+// creates or deletes sorted by (map, packet).  (Launch chunks hold <= MAX_CHUNK = 2^24 packets.)
 constexpr uint32_t ADMIT_NO_MAP = 0xFFFFu;  // (an endpoint without a CT map of that family)
 struct Admit {
     const uint16_t *ep_mi4, *ep_mi6;   // per endpoint: its CT4 / CT6 map's index in the map list
@@ -105,14 +105,15 @@ struct Admit {
     uint16_t *mi;                      // per packet: its CT map's index (k_ct_intent)
     uint8_t *budget;                   // per packet: how many of its creates of new entries succeed (the
                                        // previous pass's: what k_ct_intent assumes of earlier creates)
-    unsigned long long *keys;          // per packet from lo: map << 32 | packet for a packet with creates or
-                                       // deletes, else ~0 (sorted into keys_sorted, the walks' elements)
+    unsigned long long *keys;          // map << 24 | packet of every packet from lo with creates or deletes
+                                       // (hi[4] of them, sorted into keys_sorted: the walks' elements)
     unsigned long long *keys_sorted;
     uint32_t *tsum;                    // per scan tile of keys_sorted: the segmented (sum, prefix minimum)
     uint32_t *hi;                      // [0] the first unsure packet (the window's end), [1] the first
                                        // packet whose intent changed from the previous pass, [2] the first
                                        // packet whose intent rests on an earlier member's budget, [3] error
-                                       // bits (ADMIT_ERR_*: the host fails the batch with -EPROTO)
+                                       // bits (ADMIT_ERR_*: the host fails the batch with -EPROTO), [4] the
+                                       // walks' elements (k_adm_keys)
     uint32_t inject;                   // test hook (CV_ADMIT_INJECT): this packet's map index is corrupted
                                        // after the intents (~0u: none)
     void *sort_tmp;                    // radix-sort scratch
@@ -158,6 +159,9 @@ struct OutDev {
     uint8_t *nl, *nu;          // optional accounting of map lookups / entry writes
     int32_t *reason;           // DROP_* behind a TC_ACT_SHOT, else 0
     uint8_t *frames;           // optional output records (the batch's stride), see cv_out.frames_out
+    uint4 *deliver;            // egress split (cv_lxc_egress_split): a packet delivered to a local endpoint
+                               // leaves its 64-B delivery record here (DEL_SLOTS x 16 B) with ret E_DEFER
+                               // instead of running the destination's program, or null
 };
 
 struct GroupScratch {          // address-pair grouping for conntrack (config 3)
@@ -267,7 +271,13 @@ int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, con
 // admission, per window from packet a.lo (after launch_netdev_front): every later
 // packet's creates and deletes, the window's end (*a.hi) and the budgets
 int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g, const Admit &a, hipStream_t s);
+// then, with K = a.hi[4] (the packets with creates or deletes), the per-map walks: budgets
+int launch_admission_walks(const BatchDev &b, const Admit &a, uint32_t K, hipStream_t s);
 int launch_egress_admission(const EAdmit &a, hipStream_t s);
+// the destination's policy program of delivery records (cv_lxc_deliver): records in
+// g.del, grouped by (destination CT map, address pair), each group in record order
+int launch_lxc_deliver(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, GroupScratch g,
+                       int v6, hipStream_t s);
 // config 5: from-container of the packets' source endpoints (src_ep[i], or ep0)
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s);

@@ -1137,9 +1137,10 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
                 ret = DROP_MISSED_TAIL_CALL;
                 state = 2;
             } else {
-                // ipv4_local_delivery -> the destination's handle_policy: k_egress_deliver
+                // ipv4_local_delivery -> the destination's handle_policy: k_egress_deliver,
+                // or (split) the record handed over to the destination's rank
                 uint32_t w4, chk;
-                uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+                uint4 *d = (o.deliver ? o.deliver : g.del) + (size_t)i * DEL_SLOTS;
                 d[0] = skb4_pack(s, w4, chk);
                 d[1] = make_uint4(w4, chk | (a.nl & 0xFFu) << 16 | (a.nu & 0xFFu) << 24,
                                   (e2 - 1) | (uint32_t)res.ct << 16 | (rn1.valid ? 1u << 25 : 0u) |
@@ -1147,9 +1148,15 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
                                   ep.seclabel);
                 d[2] = make_uint4(ifindex_of(m, p.lxc4, lxc_slot, iv), res.dst, (uint32_t)lxc_slot, rn1.na);
                 if (M::EV) g.del_ev[2 * (size_t)i] = make_uint4(rn1.np, 0, 0, 0);
-                adm.flush();                                      // (the delivery draws on what is left)
-                if constexpr (INL) deliver4_one<false>(p, b, now, o, g, i, true, m, sq);
-                else del_list(g, false, i);
+                if (o.deliver) {
+                    d[3] = make_uint4(0u, 0u, 0u, 0u);
+                    res.ret = E_DEFER;
+                    eg_done(g, i, res, a);
+                } else {
+                    adm.flush();                                  // (the delivery draws on what is left)
+                    if constexpr (INL) deliver4_one<false>(p, b, now, o, g, i, true, m, sq);
+                    else del_list(g, false, i);
+                }
             }
         } else {                                                  // pass_to_stack: ipv4_l3
             m.fwd(s.len, METRIC_EGRESS);                          // TRACE_TO_STACK
@@ -1304,8 +1311,9 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
                 ret = DROP_MISSED_TAIL_CALL;
                 state = 2;
             } else {
-                // ipv6_local_delivery -> the destination's handle_policy: k_egress_deliver
-                uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+                // ipv6_local_delivery -> the destination's handle_policy: k_egress_deliver,
+                // or (split) the record handed over to the destination's rank
+                uint4 *d = (o.deliver ? o.deliver : g.del) + (size_t)i * DEL_SLOTS;
                 d[0] = make_uint4(s.saddr[0], s.saddr[1], s.saddr[2], s.saddr[3]);
                 d[1] = make_uint4(s.daddr[0], s.daddr[1], s.daddr[2], s.daddr[3]);
                 d[2] = make_uint4(s.len, (s.nexthdr & 0xFFu) | (s.h.type & 0xFFu) << 8 | (s.h.tflags & 0xFFu) << 16 |
@@ -1319,9 +1327,14 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
                     g.del_ev[2 * (size_t)i] = make_uint4((uint32_t)lxc_slot, rn1.np, 0, 0);
                     g.del_ev[2 * (size_t)i + 1] = make_uint4(rn1.na[0], rn1.na[1], rn1.na[2], rn1.na[3]);
                 }
-                adm.flush();
-                if constexpr (INL) deliver6_one<false>(p, b, now, o, g, i, true, m, sq);
-                else del_list(g, true, i);
+                if (o.deliver) {
+                    res.ret = E_DEFER;
+                    eg_done(g, i, res, a);
+                } else {
+                    adm.flush();
+                    if constexpr (INL) deliver6_one<false>(p, b, now, o, g, i, true, m, sq);
+                    else del_list(g, true, i);
+                }
             }
         } else {
             m.fwd(s.len, METRIC_EGRESS);
@@ -1563,6 +1576,75 @@ __global__ void __launch_bounds__(BLOCK) k_nat_apply(DpParams p, BatchDev b, uin
     });
     __syncthreads();
     pol_cache_flush(pc);
+}
+
+// ================================================================== delivery records
+// cv_lxc_deliver: the destination's policy program (handle_policy -> ipv4_policy /
+// ipv6_policy) of delivery records a source program left on another rank (endpoint-owned
+// conntrack across GPUs).  Every entry the program reads or writes carries
+// the record's address pair in the destination's CT map, so the records are grouped by
+// (map, pair) with the binned grouping, each group in record order on one lane.
+constexpr uint64_t SALT_DELIVER6 = 0x44454C3600000000ULL;
+template <bool V6>
+__global__ void __launch_bounds__(BLOCK) k_deliver_keys(DpParams p, BatchDev b, GroupScratch g)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        const uint4 *d = g.del + (size_t)i * DEL_SLOTS;
+        uint64_t gh = 0;
+        uint32_t e;
+        if constexpr (V6) {
+            const uint4 d0 = d[0], d1 = d[1];
+            e = d[3].x & 0xFFFFu;
+            const uint32_t sa[4] = {d0.x, d0.y, d0.z, d0.w}, da[4] = {d1.x, d1.y, d1.z, d1.w};
+            if (e < p.n_eps) gh = pair_hash6(sa, da, SALT_DELIVER6 ^ (uint64_t)(uintptr_t)G(p.eps)[e].ct6.buckets);
+        } else {
+            const uint4 d0 = d[0], d1 = d[1];
+            e = d1.z & 0xFFFFu;
+            const Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
+            if (e < p.n_eps) gh = pair_hash4(s.saddr, s.daddr, (uint64_t)(G(p.ephot)[e].ct_v4 & EPH_CT_ID) << 17);
+        }
+        if (e >= p.n_eps) group_err(g, GERR_INDEX);               // (a corrupt record: no program)
+        g.pkey[i] = e < p.n_eps ? ((gh & ~3ull) | 2ull | (V6 ? 1ull : 0ull)) : 0ull;
+        g.hword[i] = 0;
+        g.gslot[i] = NONE;
+        g.res[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+template <bool V6>
+__global__ void __launch_bounds__(BLOCK) k_deliver_runs(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
+{
+    __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
+    using M = MetT<false>;
+    M m;
+    pol_cache_init(pc);
+    met_init(m, lm);
+    m.pc = &pc;
+    for_each_run(g, V6 ? Q_NETDEV6 : Q_NETDEV, false, [&](uint32_t x, uint32_t) {
+        if constexpr (V6) deliver6_one<false>(p, b, now, o, g, x, true, m, nullptr);
+        else deliver4_one<false>(p, b, now, o, g, x, true, m, nullptr);
+    });
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
+}
+
+int launch_lxc_deliver(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o, GroupScratch g, int v6,
+                       hipStream_t s)
+{
+    g.lim = b.n;
+    if (!b.n) return 0;
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
+    if (v6) hipLaunchKernelGGL(k_deliver_keys<true>, grid, blk, 0, s, p, b, g);
+    else hipLaunchKernelGGL(k_deliver_keys<false>, grid, blk, 0, s, p, b, g);
+    launch_gbin_groups(g, b.n, s);
+    GroupScratch g6 = g;
+    g6.single = g.single6;
+    g6.work = g.work6;
+    if (v6) hipLaunchKernelGGL(k_deliver_runs<true>, grid, blk, 0, s, p, b, now, o, g6);
+    else hipLaunchKernelGGL(k_deliver_runs<false>, grid, blk, 0, s, p, b, now, o, g);
+    hipLaunchKernelGGL(k_out_unpack, grid, blk, 0, s, o, g, b.n);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 // ================================================================== launcher

@@ -1787,154 +1787,16 @@ __device__ void ct_gc(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted
     }
 }
 
-// The same pass as a stream (round 5): a wave owns GC_W consecutive 1-KiB chunks of the
-// bucket array per iteration (16 B per lane: PARTS lanes per bucket, 8 CT4 / 4 CT6
-// buckets per chunk), all loaded before any is used, plus the bucket after them; the
-// lanes of a bucket exchange its tag word and the slots' lifetimes by shuffles, and the
-// tombstone reclaim reads the next bucket's tags and keys from the registers of the lanes
-// holding it (a thread per bucket issued three scattered 8-B / 4-B accesses per bucket,
-// each wave-instruction touching 64 lines, and its reclaim check two dependent loads).
-// A deleted slot's words (key + hot run) are zeroed by the lanes holding them, each
-// writing its 16-B part back only when it changed; the part-0 lane writes the tag word
-// and a slot's lane zeroes its side words.
-template <class S>
-__device__ void ct_gc_stream(HashTable t, uint64_t nb, uint32_t time, uint32_t *deleted, uint32_t *freed)
-{
-    constexpr int PARTS = S::BW / 4, BPC = 64 / PARTS;            // 16-B parts per bucket, buckets per chunk
-    constexpr int GC_W = 8;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    static_assert(64 % PARTS == 0, "whole buckets per wave chunk");
-    const uint32_t lane = threadIdx.x & 63, part = lane % PARTS, grp = lane / PARTS, lead = lane - part;
-    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
-    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const uint64_t nchunks = (nb + BPC - 1) / BPC;
-    uint4 *B = reinterpret_cast<uint4 *>(t.buckets);
-    auto load = [&](uint64_t b) {
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (b < nb) {
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(B + b * PARTS + part));
-            v = make_uint4(x[0], x[1], x[2], x[3]);
-        }
-        return v;
-    };
-    auto comp = [](const uint4 &v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; };
-    uint32_t mine = 0, cleared = 0;
-    for (uint64_t c0 = wave * GC_W; c0 < nchunks; c0 += waves * GC_W) {
-        uint4 v[GC_W];
-#pragma unroll
-        for (int u = 0; u < GC_W; ++u) v[u] = load((c0 + u) * BPC + grp);
-        const uint4 vn = grp == 0 ? load((c0 + GC_W) * BPC) : make_uint4(0u, 0u, 0u, 0u);   // the bucket after
-#pragma unroll
-        for (int u = 0; u < GC_W; ++u) {
-            if (c0 + u >= nchunks) break;                            // (wave-uniform)
-            const uint64_t b = (c0 + u) * BPC + grp;
-            const bool in = b < nb;
-            const uint64_t tags = (uint64_t)(uint32_t)__shfl((int)v[u].x, lead, 64) |
-                                  (uint64_t)(uint32_t)__shfl((int)v[u].y, lead, 64) << 32;
-            uint64_t out = tags;
-            uint32_t del = 0;
-            bool dead = false;
-#pragma unroll
-            for (int sl = 0; sl < S::SPB; ++sl) {
-                const int L = S::KEY0 + S::KW + sl * S::KS;           // hot word 0 (lifetime) of the slot
-                const uint32_t life = (uint32_t)__shfl((int)comp(v[u], L & 3), lead + (L >> 2), 64);
-                const uint32_t tag = (uint32_t)(tags >> (8 * sl)) & 0xFFu;
-                if (tag == TAG_DEAD) dead = true;
-                if (tag >= 3 && life < time) {
-                    out = (out & ~(0xFFull << (8 * sl))) | ((uint64_t)TAG_DEAD << (8 * sl));
-                    del |= 1u << sl;
-                    dead = true;
-                }
-            }
-            // the next bucket's tags and keys (as loaded: any version of it will do, as in
-            // ct_gc): lanes of group g + 1, and for the chunk's last bucket group 0 of the
-            // next chunk -- source lanes of group 0 hand over that one
-            uint32_t clr = 0;
-            if (__any(in && dead)) {
-                const uint4 src = grp == 0 ? (u + 1 < GC_W ? v[u + 1] : vn) : v[u];
-                const uint32_t nlead = ((grp + 1) % BPC) * PARTS;
-                auto nword = [&](int W) { return (uint32_t)__shfl((int)comp(src, W & 3), nlead + (W >> 2), 64); };
-                const uint64_t ntags = (uint64_t)nword(0) | (uint64_t)nword(1) << 32;
-                uint32_t nkey[S::SPB][S::KW];
-#pragma unroll
-                for (int sl = 0; sl < S::SPB; ++sl)
-#pragma unroll
-                    for (int j = 0; j < S::KW; ++j) nkey[sl][j] = nword(S::KEY0 + sl * S::KS + j);
-                if (in && dead && part == 0) {
-                    const uint64_t nx = (b + 1) & t.mask;
-                    bool has_empty = false, displaced = false;
-#pragma unroll
-                    for (int sl = 0; sl < S::SPB; ++sl) {
-                        const uint32_t tag = (uint32_t)(ntags >> (8 * sl)) & 0xFFu;
-                        has_empty |= tag == TAG_EMPTY;
-                        uint32_t tg2;
-                        if (tag >= 3) displaced |= (home_hash<S>(nkey[sl], tg2) & t.mask) != nx;
-                    }
-                    if (nx == 0) has_empty = false;                  // (the wrap: not in registers)
-                    if (has_empty && !displaced)
-#pragma unroll
-                        for (int sl = 0; sl < S::SPB; ++sl)
-                            if (((out >> (8 * sl)) & 0xFFu) == TAG_DEAD) clr |= 1u << sl;
-                }
-                clr = (uint32_t)__shfl((int)clr, lead, 64);
-            }
-            if (!in) continue;
-#pragma unroll
-            for (int sl = 0; sl < S::SPB; ++sl)
-                if (clr >> sl & 1u) out &= ~(0xFFull << (8 * sl));
-            if (part == 0) { mine += __popc(del); cleared += __popc(clr); }
-            // this lane's 16-B part as the pass leaves it
-            uint32_t nwd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int W = (int)part * 4 + k;
-                if (W == 0) nwd[k] = (uint32_t)out;
-                if (W == 1) nwd[k] = (uint32_t)(out >> 32);
-#pragma unroll
-                for (int sl = 0; sl < S::SPB; ++sl)
-                    if ((del >> sl & 1u) && W >= S::KEY0 + sl * S::KS && W < S::KEY0 + (sl + 1) * S::KS) nwd[k] = 0u;
-            }
-            if (nwd[0] != v[u].x || nwd[1] != v[u].y || nwd[2] != v[u].z || nwd[3] != v[u].w)
-                B[b * PARTS + part] = make_uint4(nwd[0], nwd[1], nwd[2], nwd[3]);
-            if (part < (uint32_t)S::SPB && (del >> part & 1u)) {     // the slot's side words
-                uint4 *c = reinterpret_cast<uint4 *>(t.vals + (b * S::SPB + part) * CT_COLD);
-                c[0] = c[1] = make_uint4(0u, 0u, 0u, 0u);
-            }
-        }
-    }
-    const unsigned long long fr = wave_sum(cleared);
-    if (lane == 0 && fr && freed) atomicAdd(freed, (uint32_t)fr);
-    const unsigned long long tot = wave_sum(mine);
-    if (lane == 0 && tot) {
-        atomicAdd(deleted, (uint32_t)tot);
-        if (t.live) atomicAdd(t.live, 0ull - tot);
-    }
-}
-
-#ifndef CV_GC_LANE
-#define CV_GC_LANE 0
-#endif
 __global__ void __launch_bounds__(BLOCK) k_ct_gc(HashTable t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted)
 {
-#if CV_GC_LANE
     if (v6) ct_gc<Ct6Spec>(t, nb, time, deleted, deleted + 1);
     else ct_gc<Ct4Spec>(t, nb, time, deleted, deleted + 1);
-#else
-    if (v6) ct_gc_stream<Ct6Spec>(t, nb, time, deleted, deleted + 1);
-    else ct_gc_stream<Ct4Spec>(t, nb, time, deleted, deleted + 1);
-#endif
 }
 
 // deleted[0]: entries the pass deleted, deleted[1]: tombstones it turned back into empty slots
 int launch_ct_gc(const HashTable &t, int v6, uint64_t nb, uint32_t time, uint32_t *deleted, hipStream_t s)
 {
-#if CV_GC_LANE
     uint64_t g = (nb + BLOCK - 1) / BLOCK;
-#else
-    const uint64_t per_wave = 8 * 64 / (v6 ? Ct6Spec::BW / 4 : Ct4Spec::BW / 4);   // buckets per wave iteration
-    uint64_t g = (nb + per_wave * (BLOCK / 64) - 1) / (per_wave * (BLOCK / 64));
-    if (g > 2048) g = 2048;
-#endif
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_ct_gc, dim3((uint32_t)(g ? g : 1)), dim3(BLOCK), 0, s, t, v6, nb, time, deleted);
     return launch_status(__func__);
@@ -2328,7 +2190,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
 
 __global__ void k_admit_init(Admit a, uint32_t n)
 {
-    if (threadIdx.x < 4 && blockIdx.x == 0) a.hi[threadIdx.x] = threadIdx.x < 3 ? n : 0u;
+    if (threadIdx.x < 5 && blockIdx.x == 0) a.hi[threadIdx.x] = threadIdx.x < 3 ? n : 0u;
 }
 
 // test hook: a packet with one create whose map index is past the launch's maps
@@ -2425,23 +2287,32 @@ __device__ __forceinline__ SegSM block_excl_seg(SegSM v, SegSM *lds, SegSM *tota
     return r;
 }
 
-// the walks' keys: map << 32 | packet for the packets from lo with creates or deletes
+// the walks' elements: map << 24 | packet for the packets from lo with creates or
+// deletes, appended in any order (the sort orders them); hi[4] counts them
 __global__ void __launch_bounds__(BLOCK) k_adm_keys(Admit a, uint32_t n)
 {
-    for (uint32_t j = a.lo + blockIdx.x * BLOCK + threadIdx.x; j < n; j += gridDim.x * BLOCK) {
-        const uint32_t v = a.ib[j];
-        unsigned long long k = ~0ull;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t j0 = a.lo + blockIdx.x * BLOCK + (threadIdx.x & ~63u); j0 < n; j0 += gridDim.x * BLOCK) {
+        const uint32_t j = j0 + lane;
+        const uint32_t v = j < n ? a.ib[j] : 0u;
+        bool el = false;
+        unsigned long long k = 0;
         if (v & 7u) {
             const uint32_t mi = a.mi[j];
             if (mi >= a.nmaps) atomicOr(a.hi + 3, ADMIT_ERR_IB);   // (a corrupt or stale map index)
-            else k = (unsigned long long)mi << 32 | j;
+            else { k = (unsigned long long)mi << 24 | j; el = true; }   // (j < MAX_CHUNK = 2^24)
         }
-        a.keys[j - a.lo] = k;
+        const unsigned long long bal = __ballot(el);
+        if (!bal) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.hi + 4, (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        if (el) a.keys[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = k;
     }
 }
 
-constexpr uint32_t KEY_NONE = 0xFFFFu;                            // (the map field of ~0 keys sorted on 48 bits)
-__device__ __forceinline__ uint32_t key_map(unsigned long long k) { return (uint32_t)(k >> 32) & 0xFFFFu; }
+constexpr uint32_t KEY_NONE = 0xFFFFu;                            // (no element)
+__device__ __forceinline__ uint32_t key_map(unsigned long long k) { return (uint32_t)(k >> 24) & 0xFFFFu; }
 
 // element q of the sorted sequence (L of them): its map, packet, walk step and head flag
 __device__ __forceinline__ SegSM adm_elem(const Admit &a, uint32_t L, uint32_t q, uint32_t &map, uint32_t &pkt)
@@ -2451,8 +2322,7 @@ __device__ __forceinline__ SegSM adm_elem(const Admit &a, uint32_t L, uint32_t q
     if (q >= L) return SEG_ID;
     const unsigned long long k = a.keys_sorted[q];
     map = key_map(k);
-    if (map == KEY_NONE) return SEG_ID;
-    pkt = (uint32_t)k;
+    pkt = (uint32_t)k & 0xFFFFFFu;
     const uint32_t v = a.ib[pkt];
     const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
     const int32_t f = q == 0 || key_map(a.keys_sorted[q - 1]) != map;
@@ -2537,8 +2407,7 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     g.lim = b.n;
     if (!b.n || a.lo >= b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
-    const uint32_t L = b.n - a.lo, tiles = (L + SCAN_TILE - 1) / SCAN_TILE;
-    if (tiles > 4096 || a.nmaps >= KEY_NONE) return -EINVAL;
+    if (a.nmaps >= KEY_NONE) return -EINVAL;
     hipLaunchKernelGGL(k_admit_init, dim3(1), dim3(64), 0, s, a, b.n);
     hipLaunchKernelGGL(k_ct_intent<false>, grid, blk, 0, s, p, b, g, a);
     GroupScratch g6 = g;
@@ -2547,12 +2416,26 @@ int launch_admission(const DpParams &p, const BatchDev &b, const GroupScratch &g
     hipLaunchKernelGGL(k_ct_intent<true>, grid, blk, 0, s, p, b, g6, a);
     if (a.inject >= a.lo && a.inject < b.n) hipLaunchKernelGGL(k_admit_inject, dim3(1), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_adm_keys, grid, blk, 0, s, a, b.n);
-    size_t bytes = a.sort_bytes;
-    if (int r = sort_keys64(a.sort_tmp, &bytes, a.keys, a.keys_sorted, L, 48, s)) return r;
+    return launch_status(__func__);
+}
+
+// the walks over the K elements k_adm_keys listed (a.hi[4], read by the host): sort,
+// tile aggregates, their scan, the budgets
+int launch_admission_walks(const BatchDev &b, const Admit &a, uint32_t K, hipStream_t s)
+{
+    if (!b.n || a.lo >= b.n) return 0;
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
+    const uint32_t tiles = (K + SCAN_TILE - 1) / SCAN_TILE;
+    if (tiles > 4096 || K > b.n - a.lo) return -EINVAL;
     hipLaunchKernelGGL(k_adm_zero, grid, blk, 0, s, a, b.n);
-    hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, L);
+    if (!K) return launch_status(__func__);
+    int bits = 24;                                                // packet bits, then the map index's
+    while ((1u << (bits - 24)) < a.nmaps) ++bits;
+    size_t bytes = a.sort_bytes;
+    if (int r = sort_keys64(a.sort_tmp, &bytes, a.keys, a.keys_sorted, K, bits, s)) return r;
+    hipLaunchKernelGGL(k_adm_tiles, dim3(tiles), dim3(1024), 0, s, a, K);
     hipLaunchKernelGGL(k_adm_top, dim3(1), dim3(1024), 0, s, a, tiles);
-    hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, L);
+    hipLaunchKernelGGL(k_adm_apply, dim3(tiles), dim3(1024), 0, s, a, K);
     return launch_status(__func__);
 }
 

@@ -106,6 +106,8 @@ def load():
         "cv_policy_ingress": (i32, [vp, i32, C.POINTER(Batch), C.POINTER(Out), vp]),
         "cv_netdev_ingress": (i32, [vp, C.POINTER(Batch), u32, i32, C.POINTER(Out), vp]),
         "cv_lxc_egress": (i32, [vp, C.POINTER(Batch), vp, u32, vp, u32, C.POINTER(Out), vp]),
+        "cv_lxc_egress_split": (i32, [vp, C.POINTER(Batch), vp, u32, vp, u32, C.POINTER(Out), vp, vp]),
+        "cv_lxc_deliver": (i32, [vp, vp, u32, i32, u32, C.POINTER(Out), vp]),
         "cv_endpoint_config": (i32, [vp, i32, C.POINTER(EndpointCfg)]),
         "cv_node_config": (i32, [vp, C.POINTER(NodeCfg)]),
         "cv_metrics_read": (i32, [vp, vp]),
@@ -321,6 +323,19 @@ class Ctx:
         b, o = self._batch(frames, length), self._out(out)
         _check(load().cv_lxc_egress(self.h, C.byref(b), _ptr(src_ep), ep0, _ptr(flow_hash), now, C.byref(o),
                                     _stream()), "cv_lxc_egress")
+
+    def lxc_egress_split(self, frames, length, out, now, deliver, src_ep=None, flow_hash=None, ep0=0):
+        """cv_lxc_egress_split: local deliveries end with ret E_DEFER (-3) and their 64-B
+        record in deliver (a uint8 device tensor of n x 64)"""
+        b, o = self._batch(frames, length), self._out(out)
+        _check(load().cv_lxc_egress_split(self.h, C.byref(b), _ptr(src_ep), ep0, _ptr(flow_hash), now, C.byref(o),
+                                          _ptr(deliver), _stream()), "cv_lxc_egress_split")
+
+    def lxc_deliver(self, records, n, v6, out, now):
+        """cv_lxc_deliver: the destination programs of n delivery records (device, n x 64 B)"""
+        o = self._out(out)
+        _check(load().cv_lxc_deliver(self.h, _ptr(records), n, 1 if v6 else 0, now, C.byref(o), _stream()),
+               "cv_lxc_deliver")
 
     def metrics(self):
         m = np.zeros((256, 4, 2), np.uint64)

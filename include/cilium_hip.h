@@ -228,6 +228,25 @@ int cv_netdev_ingress(cv_ctx *ctx, const cv_batch *b, uint32_t now, int with_pre
 int cv_lxc_egress(cv_ctx *ctx, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0,
                   const uint32_t *flow_hash, uint32_t now, cv_out *o, void *stream);
 
+/* Config 5 as ONE node across GPUs with endpoint-owned conntrack (per-endpoint CT maps,
+ * bpf_lxc.c:53-75 CT_MAP4 / CT_MAP6 per program): a packet's source program
+ * runs on its source endpoint's GPU and its local delivery -- the destination's
+ * ipv4_policy / ipv6_policy on the destination's map -- on the destination's GPU.
+ * cv_lxc_egress_split = cv_lxc_egress without running local deliveries: such a packet
+ * ends with ret CV_E_DEFER and its 64-byte delivery record in deliver[i] (n x 64 B,
+ * 16-B aligned device buffer; byte 24 (IPv4) / 48 (IPv6) holds the destination endpoint
+ * index as a u16), identity / ct as for cv_lxc_egress.
+ * cv_lxc_deliver runs the destination programs of n such records (all IPv4, or all IPv6
+ * with v6 = 1) in record order per (destination map, address pair): ret, reason, proxy,
+ * nl, nu are the packet's final outputs, identity / ct the source program's.  The
+ * caller exchanges the records between GPUs (RCCL all_to_all) and orders the calls so
+ * every map sees its operations in packet order (cilium_amd/epnode.py). */
+#define CV_E_DEFER (-3)
+int cv_lxc_egress_split(cv_ctx *ctx, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0,
+                        const uint32_t *flow_hash, uint32_t now, cv_out *o, uint8_t *deliver, void *stream);
+int cv_lxc_deliver(cv_ctx *ctx, const uint8_t *records, uint32_t n, int v6, uint32_t now, cv_out *o,
+                   void *stream);
+
 /* ---- cilium_metrics (metrics.h:43-58): dense [256 reasons][4 dirs]{count, bytes} u64,
  * device resident.  Read sums it to host; the device pointer lets a caller reduce it
  * across GPUs (RCCL) without a copy; an external buffer may replace it. */

@@ -59,76 +59,25 @@ def per_endpoint_dp(w: synth.Workload):
     return dp, maps
 
 
-def _addr_tables(w: synth.Workload):
-    """address -> local endpoints; VIP -> backend addresses; backend address -> VIPs"""
-    import struct
-    where, backends, vips = {}, {}, {}
-    for idx, e in enumerate(w.endpoints):
-        where.setdefault(struct.pack(">I", e["ip"]), set()).add(idx)
-        where.setdefault(bytes(e["ip6"]), set()).add(idx)
-    for name, alen in (("lb4_services", 4), ("lb6_services", 16)):
-        spec = w.maps.get(name)
-        if spec is None:
-            continue
-        slave = spec.keys[:, alen + 2] | (spec.keys[:, alen + 3].astype(np.int64) << 8)
-        for k, v in zip(spec.keys[slave > 0], spec.vals[slave > 0]):
-            vip, be = bytes(k[:alen]), bytes(v[:alen])
-            backends.setdefault(vip, set()).add(be)
-            vips.setdefault(be, set()).add(vip)
-    return where, backends, vips
-
-
-def _addrs(f):
-    """(saddr, daddr) bytes of a frame, or None"""
-    if f[12] == 0x08 and f[13] == 0x00:
-        return bytes(f[26:30]), bytes(f[30:34])
-    if f[12] == 0x86 and f[13] == 0xDD:
-        return bytes(f[22:38]), bytes(f[38:54])
-    return None
+def _tables(w: synth.Workload):
+    from cilium_amd import epnode
+    return epnode.node_tables(w.endpoints, {k: (w.maps[k].keys, w.maps[k].vals) for k in ("lb4_services", "lb6_services")
+                                            if k in w.maps})
 
 
 def candidates(w: synth.Workload):
-    """per packet, the endpoints its source program may deliver it to (a superset): the
-    destination address's endpoint, or the local backends of the VIP it is"""
-    where, backends, _ = _addr_tables(w)
-    out = []
-    for f in w.frames:
-        a = _addrs(f)
-        c = set()
-        if a is not None:
-            c |= where.get(a[1], set())
-            for be in backends.get(a[1], ()):
-                c |= where.get(be, set())
-        out.append(frozenset(c))
-    return out
+    """per packet, the endpoints its source program may deliver it to (a superset:
+    cilium_amd.epnode.candidates, shared with the HIP form)"""
+    from cilium_amd import epnode
+    return epnode.candidates(w.frames, _tables(w))
 
 
 def peers(w: synth.Workload):
-    """per packet, the peer addresses of the CT entries its source program (on the
-    source's map) and its delivery (on the destination's map) may touch -- supersets.
-    An entry of an endpoint's map is keyed by a tuple of the endpoint's address and a
-    peer: the source program's peer is the destination address, or a VIP's backends (its
-    service entry, the translated connection, the NAT tuple) and, when the client backs
-    the VIP itself, the loopback address; the delivery's is the source address as the
-    source program left it: the original, a VIP (reverse NAT of a backend's reply) or the
-    loopback address."""
-    import struct
-    where, backends, vips = _addr_tables(w)
+    """per packet, the peer addresses its source program and its delivery may touch
+    (supersets: cilium_amd.epnode.peers, shared with the HIP form)"""
+    from cilium_amd import epnode
     lo = w.extra.get("node", {}).get("loopback", 0) if w.extra else 0
-    lob = struct.pack(">I", lo) if lo else b""
-    src_p, dst_p = [], []
-    for f in w.frames:
-        a = _addrs(f)
-        if a is None:
-            src_p.append(frozenset())
-            dst_p.append(frozenset())
-            continue
-        loop = lob and a[0] in backends.get(a[1], ())                # a VIP the client itself backs
-        sp = {a[1]} | backends.get(a[1], set()) | ({lob} if loop else set())
-        dp = {a[0]} | vips.get(a[0], set()) | ({lob} if loop else set())
-        src_p.append(frozenset(sp))
-        dst_p.append(frozenset(dp))
-    return src_p, dst_p
+    return epnode.peers(w.frames, _tables(w), lo)
 
 
 class RankState:

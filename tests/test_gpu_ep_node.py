@@ -1,0 +1,168 @@
+"""Config 5 as ONE node across GPUs with endpoint-owned conntrack, on the HIP datapath
+(cilium_amd/epnode.py): every endpoint its own CT4 and CT6 map (ConntrackLocal,
+bpf_lxc.c:53-75), a packet's source program on its source's rank (cv_lxc_egress_split),
+its local delivery on the destination's rank (cv_lxc_deliver) from the record exchanged
+between them.  The ranks' merged result against one sequential run of the same
+per-endpoint-map datapath on the oracle (tests/ep_shard.per_endpoint_dp): every packet's
+verdict, drop reason, identity, CT result, proxy port and lookup counts, every endpoint's
+CT4 and CT6 table, cilium_metrics and the policy counters.  One rank (every operation on
+one GPU, in rounds) and two ranks as two processes on one GPU exchanging over gloo."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from cilium_amd import synth
+from tests import ep_shard as E
+from tests import harness as H
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return "cuda:0"
+
+
+def _workload(n=1 << 12, seed=0xE5):
+    # few endpoints: most flows stay on the node, services with local backends, replies
+    return synth.config5(n, n_svc=120, n_ep=24, n_remote=32, seed=seed, vip_frac=0.5)
+
+
+def per_endpoint_ctx(w, device=0):
+    """the product context of w whose endpoints each own a fresh CT4 and CT6 map"""
+    from cilium_amd import lib
+    ctx = lib.Ctx(device, lib.F_DEFAULT)
+    maps = {}
+    for name, spec in w.maps.items():
+        if name in ("ct4", "ct6"):
+            continue
+        maps[name] = ctx.map_from_spec(spec)
+        if name in H.ROLE_NAMES:
+            ctx.bind(name, maps[name])
+    c4, c6 = w.maps["ct4"], w.maps["ct6"]
+    maps["ct4"], maps["ct6"] = [], []
+    for e in w.endpoints:
+        m4 = ctx.map_create(c4.type, c4.key_size, c4.val_size, c4.max_entries)
+        m6 = ctx.map_create(c6.type, c6.key_size, c6.val_size, c6.max_entries)
+        i = ctx.endpoint_add(e["lxc_id"], e["seclabel"], maps["policy"], m4)
+        ctx.endpoint_config(i, ct6=m6, **H._ep_cfg(e))
+        maps["ct4"].append(m4)
+        maps["ct6"].append(m6)
+    if w.extra and "node" in w.extra:
+        ctx.node_config(**w.extra["node"])
+    ctx.sync()
+    return ctx, maps
+
+
+def _rank_run(w, rank, world, device, exchange=None, all_sum=None):
+    from cilium_amd import epnode
+    ctx, maps = per_endpoint_ctx(w, int(device.split(":")[1]))
+    cand, (sp, dp) = E.candidates(w), E.peers(w)
+    node = epnode.EpNode(ctx, rank, world, w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], cand, sp, dp,
+                         device=device, exchange=exchange, all_sum=all_sum)
+    rounds = node.run(w.now)
+    owned = [e for e in range(len(w.endpoints)) if e % world == rank]
+    res = {"out": {k: v[node.mine] for k, v in node.out.items()}, "idx": np.nonzero(node.mine)[0],
+           "ct": {e: (maps["ct4"][e].dump(), maps["ct6"][e].dump()) for e in owned},
+           "metrics": ctx.metrics(), "policy": maps["policy"].dump(), "cross": node.cross, "rounds": rounds,
+           "launches": node.launches}
+    ctx.close()
+    return res
+
+
+def _check(w, results):
+    dp, maps = E.per_endpoint_dp(w)
+    ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    out = {k: np.zeros(w.n, np.int64) for k in E.RankState.FIELDS}
+    seen = np.zeros(w.n, int)
+    ct = {}
+    metrics = np.zeros((256, 4, 2), np.uint64)
+    for r in results:
+        for k in E.RankState.FIELDS:
+            out[k][r["idx"]] = r["out"][k]
+        seen[r["idx"]] += 1
+        ct.update(r["ct"])
+        metrics += r["metrics"]
+    assert (seen == 1).all(), "every packet finishes on exactly one rank"
+    for k in E.RankState.FIELDS:
+        want = getattr(ref, k).astype(np.int64)
+        if k == "identity":
+            want &= 0xFFFFFFFF
+        bad = np.nonzero(out[k] != want)[0]
+        assert len(bad) == 0, (k, len(bad), bad[:5], out[k][bad[:5]], want[bad[:5]])
+    for e in range(len(w.endpoints)):
+        for fam, (keys, vals) in zip(("ct4", "ct6"), ct[e]):
+            ok, ov = maps[fam][e].dump()
+            a, b = H.sorted_rows(keys, vals), H.sorted_rows(ok, ov)
+            assert a.shape == b.shape and (a == b).all(), (e, fam, H.rows_diff(a, b))
+    assert (metrics == dp.metrics()).all()
+    # policy counters: every rank adds its deltas to the shared initial values
+    init = H.sorted_rows(w.maps["policy"].keys, w.maps["policy"].vals)
+    tot = init[:, 16:32].copy().view("<u8").reshape(-1, 2).copy()
+    for r in results:
+        rows = H.sorted_rows(*r["policy"])
+        with np.errstate(over="ignore"):
+            tot += rows[:, 16:32].copy().view("<u8").reshape(-1, 2) - init[:, 16:32].copy().view("<u8").reshape(-1, 2)
+    got = init.copy()
+    got[:, 16:32] = tot.view(np.uint8).reshape(-1, 16)
+    ok, ov = maps["policy"].dump()
+    assert (got == H.sorted_rows(ok, ov)).all()
+    return ref
+
+
+def test_endpoint_owned_one_rank(dev, capsys):
+    """every operation on one GPU in rounds: the split source launches and the delivery
+    launches reproduce one sequential run of the per-endpoint-map datapath"""
+    w = _workload()
+    res = _rank_run(w, 0, 1, dev)
+    ref = _check(w, [res])
+    assert (ref.ret == E.DEFER).sum() == 0 and res["rounds"] >= 2
+    with capsys.disabled():
+        print(f"\n  1 rank: {w.n} packets in {res['rounds']} rounds, {res['launches']} launches")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    import torch.distributed as dist
+    from cilium_amd import epnode
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ex, s = epnode.dist_exchange(world, device=None)
+        q.put((rank, _rank_run(_workload(), rank, world, "cuda:0", exchange=ex, all_sum=s)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_endpoint_owned_two_ranks_gloo(dev, capsys):
+    """two ranks (two processes on one GPU, records exchanged over gloo): the merged
+    result equals one sequential run, with cross-rank deliveries among them"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    w = _workload()
+    _check(w, [results[0], results[1]])
+    assert sum(r["cross"] for r in results.values()) > 0
+    with capsys.disabled():
+        print(f"\n  2 ranks: {w.n} packets in {results[0]['rounds']} rounds, "
+              f"{sum(r['cross'] for r in results.values())} cross-rank deliveries")

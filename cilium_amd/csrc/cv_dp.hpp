@@ -212,6 +212,12 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint4 *est;                // egress: per packet 64 B, the conntrack stage's packed input state
                                // (k_egress_pairs -> k_egress_ct)
     uint32_t q6;               // the IPv6 queue the binned grouping fills (Q_NETDEV6, or Q_LB6 / Q_CT6)
+    uint32_t *sjob;            // the binned grouping's split keys (elephant address pairs): SJOB_WORDS per
+                               // job, ordered tile by tile in parallel by k_gbin_tiles; cursor[SJOB_WORD]
+                               // counts them
+    uint32_t sjob_cap;         // jobs sjob holds
+    uint32_t *hot;             // elephants in parallel (cv_kernels.hip k_hpar_*): per hot run and chunk
+    uint32_t hot_chunks;       // chunks it holds
     uint32_t lim;              // packets of this launch (set by the launchers): every list word the
                                // walkers read is a packet < lim or an `order` offset < 2 * lim
     uint32_t *err;             // host-mapped error word of the context: a walker that reads a list
@@ -242,6 +248,10 @@ __host__ __device__ constexpr int qcls(int q, int c) { return CLS0 + (q * NCLASS
 constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (diagnostics)
 constexpr uint32_t SINGLE_RUN = 0x80000000u; // a list word naming a singleton's packet (diagnostics)
 constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
+constexpr int SJOB_WORD = 24;    // cursor[24]: split-key jobs of the binned grouping (GroupScratch::sjob)
+// a split-key job: {key, members c, order offset, listed, member base in gbig (u32 words), q6, pad[2],
+// head[NPOS <= 8], per tile its member count [GBLK] and offset [GBLK]}
+constexpr uint32_t SJOB_HEAD = 8, SJOB_PCNT = 16, SJOB_WORDS = 16 + 2 * 256;
 constexpr int EG_WORDS = 16;
 // position lists of the egress conntrack stage: one launch per member position, the last
 // one continuing the few groups past NPOS - 1 members (<= 16: the lists are k_heads' 16)

@@ -553,6 +553,45 @@ __device__ __forceinline__ uint32_t fx_scan(uint32_t T, HotLds &L, uint32_t *tot
     return r;
 }
 
+// the folded hot run written back: the three state bits the updates leave (x1), the
+// lifetime of the last update that set one (lc: 1 TCP, 2 close, 0 otherwise; valid), the
+// report stamps and flags seen per direction, the counter sums (carries to the side slot)
+__device__ __forceinline__ void hot_store(const HashTable &ct, int64_t slot, uint32_t *h, uint32_t x1, bool lvalid,
+                                          uint32_t lc, const uint32_t *seen, const uint32_t *any,
+                                          const unsigned long long *pk, const unsigned long long *by, uint32_t now,
+                                          uint32_t flags)
+{
+    uint32_t b = h[1] & ~(uint32_t)(CTB_RX_CLOSING | CTB_TX_CLOSING | CTB_SEEN_NON_SYN);
+    b |= (x1 & 1u ? CTB_RX_CLOSING : 0u) | (x1 & 2u ? CTB_TX_CLOSING : 0u) | (x1 & 4u ? CTB_SEEN_NON_SYN : 0u);
+    h[1] = b;
+    if (lvalid) h[0] = now + (lc == 1u ? CT_LIFETIME_TCP : lc == 2u ? CT_CLOSE_TIMEOUT : CT_LIFETIME_NONTCP);
+    for (int d = 0; d < 2; ++d) {                                 // __ct_update_timeout's reports (0 tx, 1 rx)
+        if (!any[d]) continue;
+        const int fsh = d ? 24 : 16, li = d ? 5 : 4;               // rx_flags_seen / tx_flags_seen; last_rx / tx_report
+        const uint32_t acc = (h[2] >> fsh) & 0xFFu, nacc = acc | seen[d];
+        if (h[li] + CT_REPORT_INTERVAL < now || nacc != acc) {
+            h[li] = now;
+            h[2] = (h[2] & ~(0xFFu << fsh)) | (nacc << fsh);
+        }
+    }
+    CtE e;
+    e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
+    e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
+    if (flags & F_CT_ACCOUNTING) {                                // ct_count: low words in place, carries to the side slot
+        for (int d = 0; d < 2; ++d) {
+            const int k0 = d ? 0 : 4;                              // rx_packets / rx_bytes @0 / 2, tx @4 / 6
+            const unsigned long long sp = (unsigned long long)e.w[k0] + pk[d];
+            const unsigned long long sb = (unsigned long long)e.w[k0 + 2] + by[d];
+            e.w[k0] = (uint32_t)sp;
+            e.w[k0 + 2] = (uint32_t)sb;
+            CV_G uint32_t *cold = ct_cold<Ct4Spec>(ct, slot);
+            if (sp >> 32) cold[k0 >> 1] += (uint32_t)(sp >> 32);
+            if (sb >> 32) cold[(k0 + 2) >> 1] += (uint32_t)(sb >> 32);
+        }
+    }
+    ct_store_hot<Ct4Spec>(ct, slot, e);
+}
+
 // step 3 for the entry at L.slot: the deferred hits of the participating threads (in
 // thread = member order) applied as the sequential run applies them one by one
 template <class S>
@@ -622,40 +661,8 @@ __device__ __forceinline__ void hot_fold(const HashTable &ct, HotLds &L, bool pa
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t *h = L.e;                                        // h0 = w8 (lifetime), h1 = w9 (bits), h2 = w10 (flags seen)
-        const uint32_t x1 = fx_at(tot, x0);
-        uint32_t b = h[1] & ~(uint32_t)(CTB_RX_CLOSING | CTB_TX_CLOSING | CTB_SEEN_NON_SYN);
-        b |= (x1 & 1u ? CTB_RX_CLOSING : 0u) | (x1 & 2u ? CTB_TX_CLOSING : 0u) | (x1 & 4u ? CTB_SEEN_NON_SYN : 0u);
-        h[1] = b;
-        if (L.fxlast) {
-            const uint32_t lc = L.fxlast & 0xFFu;                  // (NONTCP and SYN_TIMEOUT are both 60 s)
-            h[0] = now + (lc == 1u ? CT_LIFETIME_TCP : lc == 2u ? CT_CLOSE_TIMEOUT : CT_LIFETIME_NONTCP);
-        }
-        for (int d = 0; d < 2; ++d) {                             // __ct_update_timeout's reports (0 tx, 1 rx)
-            if (!L.any[d]) continue;
-            const int fsh = d ? 24 : 16, li = d ? 5 : 4;           // rx_flags_seen / tx_flags_seen; last_rx / tx_report
-            const uint32_t acc = (h[2] >> fsh) & 0xFFu, nacc = acc | L.seen[d];
-            if (h[li] + CT_REPORT_INTERVAL < now || nacc != acc) {
-                h[li] = now;
-                h[2] = (h[2] & ~(0xFFu << fsh)) | (nacc << fsh);
-            }
-        }
-        CtE e;
-        e.w[8] = h[0]; e.w[9] = h[1]; e.w[10] = h[2]; e.w[11] = h[3]; e.w[12] = h[4]; e.w[13] = h[5];
-        e.w[0] = h[6]; e.w[2] = h[7]; e.w[4] = h[8]; e.w[6] = h[9];
-        if (flags & F_CT_ACCOUNTING) {                            // ct_count: low words in place, carries to the side slot
-            for (int d = 0; d < 2; ++d) {
-                const int k0 = d ? 0 : 4;                          // rx_packets / rx_bytes @0 / 2, tx @4 / 6
-                const unsigned long long sp = (unsigned long long)e.w[k0] + L.pk[d];
-                const unsigned long long sb = (unsigned long long)e.w[k0 + 2] + L.by[d];
-                e.w[k0] = (uint32_t)sp;
-                e.w[k0 + 2] = (uint32_t)sb;
-                CV_G uint32_t *cold = ct_cold<S>(ct, slot);
-                if (sp >> 32) cold[k0 >> 1] += (uint32_t)(sp >> 32);
-                if (sb >> 32) cold[(k0 + 2) >> 1] += (uint32_t)(sb >> 32);
-            }
-        }
-        ct_store_hot<S>(ct, slot, e);
+        const unsigned long long pk[2] = {L.pk[0], L.pk[1]}, by[2] = {L.by[0], L.by[1]};
+        hot_store(ct, slot, L.e, fx_at(tot, x0), L.fxlast != 0, L.fxlast & 0xFFu, L.seen, L.any, pk, by, now, flags);
     }
     __syncthreads();
 }
@@ -700,6 +707,329 @@ __device__ __forceinline__ int hot_finish(const DpParams &p, const EpDev &ep, Sk
     return TC_ACT_SHOT;
 }
 
+// One member of a hot run: its stage record and its lookups against the table as the
+// chunk starts (read only: ct_lookup_pre, policy_ingress_denies), and whether its
+// ipv4_policy would change which keys exist -- a create (CT_NEW, allowed) or a delete
+// (CT_ESTABLISHED, denied) -- or it is on another CT map than the run's first member
+// (two groups merged by a key collision: endpoints with their own maps): such a member
+// runs whole.
+struct HotMember {
+    uint32_t x;
+    bool live, simple, change;
+    uint4 s1;
+    EpDev ep;
+    Skb4 s;
+    Tuple4 t;
+    CtState st;
+    HitRec hr;
+    int ret;
+};
+
+__device__ __forceinline__ void hot_lookup(const DpParams &p, const BatchDev &b, const GroupScratch &g,
+                                           const HashTable &ct, uint32_t off, uint32_t cnt, uint32_t k, HotMember &h,
+                                           Acct &a)
+{
+    h.x = k < cnt ? g.order[off + 1 + k] : 0u;
+    h.live = k < cnt && pkt_ok(g, h.x);
+    if (!h.live) h.x = 0u;
+    uint4 s0{};
+    h.s1 = uint4{};
+    if (h.live) { s0 = g.srec[2 * h.x]; h.s1 = g.srec[2 * h.x + 1]; }
+    const uint32_t meta = h.s1.z;
+    h.ep = ep_netdev4<false>(p, meta & 0xFFFFu);
+    h.s = skb4_unpack(s0, h.s1.x, h.s1.y & 0x3FFu, b.stride);
+    h.simple = h.live && !(p.flags & F_DROP_ALL) && h.ep.ipv4 && h.s.len >= 34;
+    a = Acct{(h.s1.y >> 16) & 0xFFu, h.s1.y >> 24, a.pc};
+    h.t = Tuple4{};
+    h.t.nexthdr = h.s.nexthdr; h.t.daddr = h.s.daddr; h.t.saddr = h.s.saddr;
+    h.st = CtState{0, 0, 0, 0, 0, 0};
+    h.hr = HitRec{-1, 0, 0, 0, 0, 0};
+    int64_t slot = -1;
+    h.ret = h.simple ? ct_lookup_pre(h.ep.ct4, h.t, h.s.h, CT_INGRESS, h.s.len, slot, &h.st, a, h.hr) : 0;
+    const bool deny = h.simple && h.ret >= 0 &&
+                      policy_ingress_denies(h.ep.policy, p.flags, h.s1.w, h.t.dport, h.t.nexthdr);
+    const bool other_map = h.simple && h.ep.ct4.buckets != ct.buckets;
+    h.change = h.simple && (other_map || (h.ret == CT_ESTABLISHED && deny) || (h.ret == CT_NEW && !deny));
+}
+
+// a member before the chunk's first change, whole: its lookup hit (the entry update
+// deferred to the fold) or missed with a denying policy, or it drops before any
+// conntrack work
+template <class M>
+__device__ __forceinline__ void hot_member_finish(const DpParams &p, const OutDev &o, HotMember &h, Acct &a, M &m,
+                                                  uint32_t now)
+{
+    uint8_t ct = CT_NONE;
+    uint16_t proxy = 0;
+    int32_t reason = 0;
+    const bool skip_proxy = (h.s1.z >> 16) & 1u;
+    const uint32_t ifx = (h.s1.z >> 17) & 1u;                     // ifindex != 0 (the plain instance's view)
+    int rv;
+    if (h.simple) {
+        rv = hot_finish(p, h.ep, h.s, h.t, h.ret, h.st, h.s1.w, skip_proxy, ifx, ct, proxy, reason, a, m);
+    } else {
+        a = Acct{(h.s1.y >> 16) & 0xFFu, h.s1.y >> 24, a.pc};
+        rv = handle_policy4<M, false>(p, h.ep, h.s, h.s1.w, skip_proxy, ifx, now, ct, proxy, reason, a, m);
+    }
+    if (o.ret) o.ret[h.x] = rv;
+    if (o.reason) o.reason[h.x] = reason;
+    if (o.ct) o.ct[h.x] = ct;
+    if (o.proxy) o.proxy[h.x] = proxy;
+    store_out(o, h.x, a);
+}
+
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, uint32_t &total);
+
+// ------------------------------------------------------------------ elephants in parallel
+// A run of at least HPAR_MIN members (an elephant flow's address pair) is walked by
+// k_ct_hot a chunk of HOTB members at a time, and its chunks are sequential.  But up to
+// the run's first member that changes a key (or hits a second entry), every member sees
+// the table as the launch found it, so the chunks before it need not wait for each other:
+//  k_hpar_look  the elephants among the first HPAR_RUNS hot runs, their chunks numbered;
+//               per chunk (a workgroup each, all at once): the lookups, the first change,
+//               the first hit and its entry, the first hit on another entry;
+//  k_hpar_fin   per chunk: the elephant's entry e (its first hit's) and its cut -- the
+//               first change or hit on another entry -- from every chunk's record; the
+//               members before the cut finish (verdicts, policy counters, metrics) and
+//               their updates of e are summarised as a function of the three bits e has
+//               when the chunk starts (the 8-state transition table of hot_fold, and per
+//               starting state the reductions: the lifetime class of the last update that
+//               set one, the flags seen and whether any ran, per direction), with the
+//               counter sums;
+//  k_ct_hot     per elephant: the chunk summaries composed in order -- (T1, R1) then
+//               (T2, R2) = (T2 . T1, R1 then R2 evaluated at T1(x)) -- applied to e once,
+//               then the walk resumes at the cut, serially as before.
+// An elephant of established packets is one round of parallel lookups instead of a chain
+// of ~24-us chunks.
+constexpr uint32_t HPAR_RUNS = 256, HPAR_MIN = 8 * HOTB;
+// g.hot layout: per run r < HPAR_RUNS: HP_RUN + 4r {off, cnt, first chunk, chunks} (chunks
+// 0: not in parallel), HP_CUT + 4r {cut, e lo, e hi, -}; HP_TOTAL the chunks; per chunk q:
+// HP_CHUNK + 8q {run, first change, first hit, hit on another entry, e lo, e hi, -, -} and
+// hp_sum + 16q its summary {T, R[8], pk[2], by[2], -}, R[x] = valid | class << 1 |
+// any tx << 3 | any rx << 4 | seen tx << 8 | seen rx << 16
+constexpr uint32_t HP_RUN = 0, HP_CUT = 4 * HPAR_RUNS, HP_TOTAL = 8 * HPAR_RUNS, HP_CHUNK = 8 * HPAR_RUNS + 64;
+__host__ __device__ constexpr uint32_t hp_sum(uint32_t chunks_cap) { return HP_CHUNK + 8 * chunks_cap; }
+__host__ __device__ constexpr uint32_t hp_words(uint32_t chunks_cap) { return hp_sum(chunks_cap) + 16 * chunks_cap; }
+
+__global__ void __launch_bounds__(HOTB) k_hpar_look(DpParams p, BatchDev b, GroupScratch g)
+{
+    __shared__ unsigned long long fs;
+    __shared__ uint32_t fl[4], wsum[17], tot_s;
+    // the plan (every workgroup; the first writes it for k_hpar_fin and k_ct_hot)
+    {
+        const uint32_t nhot = hot_runs(g, Q_NETDEV), r = threadIdx.x;
+        uint32_t off = 0, cnt = 0, nch = 0;
+        if (r < HPAR_RUNS && r < nhot) {
+            off = g.work[r];
+            if (off < 2u * g.lim) {
+                cnt = g.order[off];
+                if (!run_ok(g, off, cnt)) cnt = 0;
+            }
+            if (cnt >= HPAR_MIN) nch = (cnt + HOTB - 1) / HOTB;
+        }
+        uint32_t total;
+        const uint32_t first = block_excl_scan(nch, wsum, total);
+        if (threadIdx.x == 0) tot_s = total <= g.hot_chunks ? total : 0u;   // (past the scratch: all serial)
+        __syncthreads();
+        if (!tot_s) nch = 0;
+        if (blockIdx.x == 0 && r < HPAR_RUNS) {
+            uint32_t *run = g.hot + HP_RUN + 4 * r;
+            run[0] = off; run[1] = cnt; run[2] = first; run[3] = nch;
+            if (r == 0) g.hot[HP_TOTAL] = tot_s;
+        }
+        __syncthreads();
+    }
+    const uint32_t total = tot_s;
+    for (uint32_t q = blockIdx.x; q < total; q += gridDim.x) {    // (block-uniform) a workgroup per chunk
+        // (the plan: recomputed here; block 0's copy is read by the later kernels)
+        uint32_t r = 0, off = 0, cnt = 0, first = 0;
+        {
+            const uint32_t nhot = hot_runs(g, Q_NETDEV);
+            uint32_t acc = 0;
+            for (uint32_t x = 0; x < HPAR_RUNS && x < nhot; ++x) {   // (uniform; HPAR_RUNS reads, cached)
+                const uint32_t o2 = g.work[x];
+                if (o2 >= 2u * g.lim) continue;
+                const uint32_t c2 = g.order[o2];
+                if (c2 < HPAR_MIN || c2 >= 2u * g.lim - o2) continue;
+                const uint32_t n2 = (c2 + HOTB - 1) / HOTB;
+                if (q < acc + n2) { r = x; off = o2; cnt = c2; first = acc; break; }
+                acc += n2;
+            }
+        }
+        (void)r;
+        const uint32_t k = (q - first) * HOTB + threadIdx.x;
+        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;
+        HotMember h;
+        Acct a{0, 0, nullptr};
+        hot_lookup(p, b, g, ct, off, cnt, k, h, a);
+        if (threadIdx.x < 3) fl[threadIdx.x] = cnt;
+        __syncthreads();
+        if (h.change) atomicMin(&fl[0], k);
+        if (h.hr.slot >= 0) atomicMin(&fl[1], k);
+        __syncthreads();
+        if (h.hr.slot >= 0 && k == fl[1]) fs = (unsigned long long)h.hr.slot;
+        __syncthreads();
+        if (h.hr.slot >= 0 && (unsigned long long)h.hr.slot != fs) atomicMin(&fl[2], k);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t *rec = g.hot + HP_CHUNK + 8 * q;
+            rec[0] = r; rec[1] = fl[0]; rec[2] = fl[1]; rec[3] = fl[2];
+            rec[4] = fl[1] < cnt ? (uint32_t)fs : 0u; rec[5] = fl[1] < cnt ? (uint32_t)(fs >> 32) : 0u;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(HOTB) k_hpar_fin(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
+{
+    __shared__ LdsMetrics lm;
+    __shared__ LdsPolicy pc;
+    __shared__ HotLds L;
+    __shared__ uint32_t R[8], last[8], sums[4], cq[2];
+    __shared__ unsigned long long es;
+    using M = MetT<false>;
+    M m;
+    pol_cache_init(pc);
+    met_init(m, lm);
+    m.pc = &pc;
+    const uint32_t total = g.hot[HP_TOTAL];
+    for (uint32_t q = blockIdx.x; q < total; q += gridDim.x) {    // (block-uniform) a workgroup per chunk
+        const uint32_t r = g.hot[HP_CHUNK + 8 * q];
+        const uint32_t off = g.hot[HP_RUN + 4 * r], cnt = g.hot[HP_RUN + 4 * r + 1];
+        const uint32_t first = g.hot[HP_RUN + 4 * r + 2], nch = g.hot[HP_RUN + 4 * r + 3];
+        // the run's entry (the first chunk with a hit: its first hit's) and its cut
+        if (threadIdx.x == 0) { cq[0] = ~0u; cq[1] = cnt; }
+        __syncthreads();
+        for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x)
+            if (g.hot[HP_CHUNK + 8 * (first + c) + 2] < cnt) atomicMin(&cq[0], c);
+        __syncthreads();
+        if (threadIdx.x == 0)
+            es = cq[0] == ~0u ? ~0ull : (unsigned long long)g.hot[HP_CHUNK + 8 * (first + cq[0]) + 5] << 32 |
+                                            g.hot[HP_CHUNK + 8 * (first + cq[0]) + 4];
+        __syncthreads();
+        const unsigned long long e = es;
+        for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
+            const uint32_t *rec = g.hot + HP_CHUNK + 8 * (first + c);
+            uint32_t cut = min(rec[1], rec[3]);
+            if (rec[2] < cnt && ((unsigned long long)rec[5] << 32 | rec[4]) != e) cut = min(cut, rec[2]);
+            if (cut < cnt) atomicMin(&cq[1], cut);
+        }
+        __syncthreads();
+        const uint32_t cut = cq[1], k0 = (q - first) * HOTB;
+        if (q == first && threadIdx.x == 0) {
+            uint32_t *c = g.hot + HP_CUT + 4 * r;
+            c[0] = cut; c[1] = (uint32_t)e; c[2] = (uint32_t)(e >> 32);
+        }
+        uint32_t *sum = g.hot + hp_sum(g.hot_chunks) + 16 * q;
+        if (k0 >= cut) {                                          // (block-uniform) past the cut: no summary
+            if (threadIdx.x < 16) sum[threadIdx.x] = threadIdx.x == 0 ? FX_IDENT : 0u;
+            __syncthreads();
+            continue;
+        }
+        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;
+        HotMember h;
+        Acct a{0, 0, m.pc};
+        const uint32_t k = k0 + threadIdx.x;
+        hot_lookup(p, b, g, ct, off, cnt, k, h, a);
+        const bool fin = h.live && k < cut;
+        if (fin) hot_member_finish(p, o, h, a, m, now);
+        // the summary of the chunk's updates of e, per starting state x
+        const bool part = fin && h.hr.slot >= 0 && (unsigned long long)h.hr.slot == e;
+        uint32_t T = FX_IDENT;
+        if (part) {
+            T = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < 8; ++x) T |= hit_fx(x, h.hr.action, h.hr.dir, h.hr.tcp, h.hr.seen).x << (3 * x);
+        }
+        if (threadIdx.x < 8) { R[threadIdx.x] = 0; last[threadIdx.x] = 0; }
+        if (threadIdx.x < 4) sums[threadIdx.x] = 0;
+        uint32_t tot;
+        const uint32_t pre = fx_scan(T, L, &tot);                // (ends with a barrier)
+        const int d = h.hr.dir == CT_INGRESS ? 1 : 0;
+#pragma unroll 1
+        for (uint32_t x = 0; x < 8; ++x) {
+            uint32_t lst = 0, bits = 0;
+            if (part) {
+                const HitFx f = hit_fx(fx_at(pre, x), h.hr.action, h.hr.dir, h.hr.tcp, h.hr.seen);
+                if (f.any) {
+                    lst = (threadIdx.x + 1) << 8 | (f.life == CT_LIFETIME_TCP ? 1u : f.life == CT_CLOSE_TIMEOUT ? 2u : 0u);
+                    bits = (1u << (3 + d)) | (h.hr.seen & 0xFFu) << (d ? 16 : 8);
+                }
+            }
+#pragma unroll
+            for (int s2 = 32; s2; s2 >>= 1) {
+                lst = max(lst, (uint32_t)__shfl_xor((int)lst, s2, 64));
+                bits |= (uint32_t)__shfl_xor((int)bits, s2, 64);
+            }
+            if ((threadIdx.x & 63) == 0) {
+                if (lst) atomicMax(&last[x], lst);
+                if (bits) atomicOr(&R[x], bits);
+            }
+        }
+        uint32_t pk[2] = {0u, 0u}, by[2] = {0u, 0u};
+        if (part && (p.flags & F_CT_ACCOUNTING)) { pk[d] = 1u; by[d] = h.hr.len; }
+#pragma unroll
+        for (int s2 = 32; s2; s2 >>= 1)
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd) {
+                pk[dd] += (uint32_t)__shfl_xor((int)pk[dd], s2, 64);
+                by[dd] += (uint32_t)__shfl_xor((int)by[dd], s2, 64);
+            }
+        if ((threadIdx.x & 63) == 0)
+#pragma unroll
+            for (int dd = 0; dd < 2; ++dd) {
+                if (pk[dd]) atomicAdd(&sums[dd], pk[dd]);
+                if (by[dd]) atomicAdd(&sums[2 + dd], by[dd]);
+            }
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            uint32_t v = 0;
+            if (threadIdx.x == 0) v = tot;
+            else if (threadIdx.x <= 8) {
+                const uint32_t x = threadIdx.x - 1;
+                v = R[x] | (last[x] ? 1u | (last[x] & 3u) << 1 : 0u);
+            } else if (threadIdx.x <= 12) v = sums[threadIdx.x - 9];
+            sum[threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    met_flush(m, p.metrics);                                      // (ends with a barrier)
+    pol_cache_flush(pc);
+}
+
+// the elephant r's chunk summaries composed in order and applied to its entry (one
+// thread); returns where k_ct_hot resumes
+__device__ uint32_t hpar_fold(const DpParams &p, const GroupScratch &g, const HashTable &ct, uint32_t r, uint32_t now)
+{
+    const uint32_t first = g.hot[HP_RUN + 4 * r + 2], nch = g.hot[HP_RUN + 4 * r + 3];
+    if (!nch) return 0;
+    const uint32_t cut = g.hot[HP_CUT + 4 * r];
+    const unsigned long long e = (unsigned long long)g.hot[HP_CUT + 4 * r + 2] << 32 | g.hot[HP_CUT + 4 * r + 1];
+    if (e == ~0ull || !cut) return cut;                           // (no hit before the cut)
+    uint32_t T = FX_IDENT, A[8];                                  // per starting state: what the updates so far did
+    unsigned long long pk[2] = {0, 0}, by[2] = {0, 0};
+    for (int x = 0; x < 8; ++x) A[x] = 0;
+    for (uint32_t q = first; q < first + nch && (q - first) * HOTB < cut; ++q) {
+        const uint32_t *sm = g.hot + hp_sum(g.hot_chunks) + 16 * q;
+        for (uint32_t x = 0; x < 8; ++x) {
+            const uint32_t bx = sm[1 + fx_at(T, x)];
+            if (bx & 1u) A[x] = (A[x] & ~7u) | (bx & 7u);         // (the later update's lifetime class)
+            A[x] |= bx & 0xFFFF18u;                               // (any / seen accumulate)
+        }
+        T = fx_then(T, sm[0]);
+        for (int d = 0; d < 2; ++d) { pk[d] += sm[9 + d]; by[d] += sm[11 + d]; }
+    }
+    const int64_t slot = (int64_t)e;
+    CtE en;
+    ct_load_hot<Ct4Spec>(ct, slot, en);
+    uint32_t h[CT_HOTW] = {en.w[8], en.w[9], en.w[10], en.w[11], en.w[12], en.w[13], en.w[0], en.w[2], en.w[4], en.w[6]};
+    const uint32_t x0 = bits_x(h[1] & 0xFFFFu), a = A[x0];
+    const uint32_t seen[2] = {(a >> 8) & 0xFFu, (a >> 16) & 0xFFu}, any[2] = {(a >> 3) & 1u, (a >> 4) & 1u};
+    hot_store(ct, slot, h, fx_at(T, x0), a & 1u, (a >> 1) & 3u, seen, any, pk, by, now, p.flags);
+    return cut;
+}
+
 __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev o, GroupScratch g, uint32_t now)
 {
     __shared__ LdsMetrics lm;
@@ -717,76 +1047,45 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
         const uint32_t cnt = g.order[off], x0 = g.order[off + 1];
         if (!run_ok(g, off, cnt) || !pkt_ok(g, x0)) continue;
         const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;   // (the run's map)
-        for (uint32_t k0 = 0; k0 < cnt;) {                        // (block-uniform)
-            const uint32_t k = k0 + threadIdx.x;
-            uint32_t x = k < cnt ? g.order[off + 1 + k] : 0u;
-            const bool live = k < cnt && pkt_ok(g, x);
-            if (!live) x = 0u;
-            uint4 s0{}, s1{};
-            if (live) { s0 = g.srec[2 * x]; s1 = g.srec[2 * x + 1]; }
-            const uint32_t meta = s1.z;
-            const EpDev ep = ep_netdev4<false>(p, meta & 0xFFFFu);
-            Skb4 s = skb4_unpack(s0, s1.x, s1.y & 0x3FFu, b.stride);
-            const bool skip_proxy = (meta >> 16) & 1u;
-            const uint32_t ifx = (meta >> 17) & 1u;               // ifindex != 0 (the plain instance's view)
+        // an elephant's members before its cut ran in parallel (k_hpar_*): their updates of
+        // its entry folded here, then the walk resumes at the cut
+        if (threadIdx.x == 0) L.c = r < HPAR_RUNS ? hpar_fold(p, g, ct, r, now) : 0u;
+        __syncthreads();
+        const uint32_t start = L.c;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        l1_inv();
+        __syncthreads();
+        for (uint32_t k0 = start; k0 < cnt;) {                    // (block-uniform)
             // 1. the lookups against the chunk's starting table, read only
-            const bool simple = live && !(p.flags & F_DROP_ALL) && ep.ipv4 && s.len >= 34;
-            Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
-            Tuple4 t{};
-            t.nexthdr = s.nexthdr; t.daddr = s.daddr; t.saddr = s.saddr;
-            CtState st{0, 0, 0, 0, 0, 0};
-            HitRec hr{-1, 0, 0, 0, 0, 0};
-            int64_t slot = -1;
-            const int ret = simple ? ct_lookup_pre(ep.ct4, t, s.h, CT_INGRESS, s.len, slot, &st, a, hr) : 0;
-            const bool deny = simple && ret >= 0 && policy_ingress_denies(ep.policy, p.flags, s1.w, t.dport, t.nexthdr);
-            // a member on another CT map than the run's first (two groups merged by a key
-            // collision: endpoints with their own maps) runs whole, like a key change: the
-            // fold writes the run's map only
-            const bool other_map = simple && ep.ct4.buckets != ct.buckets;
-            const bool change = simple && (other_map || (ret == CT_ESTABLISHED && deny) || (ret == CT_NEW && !deny));
+            HotMember h;
+            Acct a{0, 0, m.pc};
+            hot_lookup(p, b, g, ct, off, cnt, k0 + threadIdx.x, h, a);
             if (threadIdx.x == 0) { L.c = HOTB; L.lead = HOTB; }
             __syncthreads();
-            if (change) atomicMin(&L.c, threadIdx.x);
-            if (hr.slot >= 0) atomicMin(&L.lead, threadIdx.x);    // the first hit
+            if (h.change) atomicMin(&L.c, threadIdx.x);
+            if (h.hr.slot >= 0) atomicMin(&L.lead, threadIdx.x);  // the first hit
             __syncthreads();
             const uint32_t c = L.c;
             uint32_t lead = L.lead;
             if (lead < c && threadIdx.x == lead) {                // its entry, while the others finish
-                L.slot = (unsigned long long)hr.slot;
-                hot_load<Ct4Spec>(ct, L, hr.slot);
+                L.slot = (unsigned long long)h.hr.slot;
+                hot_load<Ct4Spec>(ct, L, h.hr.slot);
             }
             // 2. the members before c, in parallel
-            if (live && threadIdx.x < c) {
-                uint8_t ct = CT_NONE;
-                uint16_t proxy = 0;
-                int32_t reason = 0;
-                int rv;
-                if (simple) {
-                    rv = hot_finish(p, ep, s, t, ret, st, s1.w, skip_proxy, ifx, ct, proxy, reason, a, m);
-                } else {                                          // drops before any conntrack work
-                    Acct a0{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
-                    a = a0;
-                    rv = handle_policy4<M, false>(p, ep, s, s1.w, skip_proxy, ifx, now, ct, proxy, reason, a, m);
-                }
-                if (o.ret) o.ret[x] = rv;
-                if (o.reason) o.reason[x] = reason;
-                if (o.ct) o.ct[x] = ct;
-                if (o.proxy) o.proxy[x] = proxy;
-                store_out(o, x, a);
-            }
+            if (h.live && threadIdx.x < c) hot_member_finish(p, o, h, a, m, now);
             // 3. their hits' entry updates, entry by entry, in member order
-            bool pend = live && threadIdx.x < c && hr.slot >= 0;
+            bool pend = h.live && threadIdx.x < c && h.hr.slot >= 0;
             for (bool first = true; lead < c; first = false) {    // (block-uniform)
                 __syncthreads();
-                const bool part = pend && (unsigned long long)hr.slot == L.slot;
-                hot_fold<Ct4Spec>(ct, L, part, hr, now, p.flags, first);   // (ends with a barrier)
+                const bool part = pend && (unsigned long long)h.hr.slot == L.slot;
+                hot_fold<Ct4Spec>(ct, L, part, h.hr, now, p.flags, first);   // (ends with a barrier)
                 pend &= !part;
                 if (threadIdx.x == 0) L.lead = HOTB;
                 __syncthreads();
                 if (pend) atomicMin(&L.lead, threadIdx.x);
                 __syncthreads();
                 lead = L.lead;
-                if (lead < c && threadIdx.x == lead) L.slot = (unsigned long long)hr.slot;
+                if (lead < c && threadIdx.x == lead) L.slot = (unsigned long long)h.hr.slot;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (the entries written before any re-read)
             l1_inv();
@@ -797,16 +1096,17 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             }
             // 4. member c whole: its create or delete, against the table the fold left
             if (threadIdx.x == c) {
-                Acct a1{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
+                Acct a1{(h.s1.y >> 16) & 0xFFu, h.s1.y >> 24, m.pc};
                 uint8_t ct1 = CT_NONE;
                 uint16_t proxy = 0;
                 int32_t reason = 0;
-                const int rv = handle_policy4<M, false>(p, ep, s, s1.w, skip_proxy, ifx, now, ct1, proxy, reason, a1, m);
-                if (o.ret) o.ret[x] = rv;
-                if (o.reason) o.reason[x] = reason;
-                if (o.ct) o.ct[x] = ct1;
-                if (o.proxy) o.proxy[x] = proxy;
-                store_out(o, x, a1);
+                const int rv = handle_policy4<M, false>(p, h.ep, h.s, h.s1.w, (h.s1.z >> 16) & 1u, (h.s1.z >> 17) & 1u,
+                                                        now, ct1, proxy, reason, a1, m);
+                if (o.ret) o.ret[h.x] = rv;
+                if (o.reason) o.reason[h.x] = reason;
+                if (o.ct) o.ct[h.x] = ct1;
+                if (o.proxy) o.proxy[h.x] = proxy;
+                store_out(o, h.x, a1);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             l1_inv();
@@ -1179,6 +1479,7 @@ __device__ __forceinline__ void bitonic_sort(P v, uint32_t p)
 }
 
 constexpr uint32_t SUBMAX = 48;                                  // largest sub-bin sorted by insertion
+constexpr uint32_t SPLIT_PAR = 4096;                              // split keys ordered by k_gbin_tiles from here
 __device__ __forceinline__ uint32_t sub_of(unsigned long long composite) { return (uint32_t)(composite >> 34) & 255u; }
 
 // base[idx] += 1 for the active lanes, returning each its old value, with one LDS atomic
@@ -1205,7 +1506,7 @@ struct GbinLds {                                                  // k_gbin_grou
     uint32_t sub_cnt[256], sub_off[256], sub_max, wsum[17], fill, big[2];
     uint32_t bcnt[256], boff[256], bfill[256];                    // a bin past LCAP: its sub-bins
     uint32_t pcnt[256], poff[256];                                // a split key: its members per scatter tile
-    uint32_t rest, mcount, key, head[NPOS];
+    uint32_t rest, mcount, key, head[NPOS], mused;
 };
 
 // v[0, nb) (nb <= LCAP) sorted by composite in LDS: a counting sort by 8 more key bits
@@ -1325,6 +1626,7 @@ __device__ void gbin_split_key(const GroupScratch &g, GbinLds &L, unsigned long 
     if (threadIdx.x == 0) { L.rest = 0; L.mcount = 0; }
     __syncthreads();
     const uint32_t key = L.key;
+    m += L.mused;                                                 // (past the bin's earlier split keys)
     for (uint32_t j0 = 0; j0 < cnt; j0 += GUNROLL * blockDim.x) { // its members per scatter tile
         unsigned long long xs[GUNROLL];                           // (GUNROLL loads in flight: one block
 #pragma unroll                                                    //  streams the whole hot bin)
@@ -1365,11 +1667,35 @@ __device__ void gbin_split_key(const GroupScratch &g, GbinLds &L, unsigned long 
         }
     }
     __syncthreads();
-    // the run: tile by tile, the members' bits set in LDS, then read back in order
+    // the run: a large one is ordered tile by tile in parallel by k_gbin_tiles (a job: the
+    // key, its members per tile in m, where the run goes; the next key's members go past
+    // these in m), a smaller one here -- per tile the members' bits set in LDS, then read
+    // back in order
     const uint32_t c = total;
     const bool listed = c >= (g.flat ? NPOS : 2u);                // (a run in `order`; its offset may be 0)
-    if (threadIdx.x == 0) L.mcount = listed ? 2 * start + atomicAdd(&L.fill, c + 1) : 0u;
+    if (threadIdx.x == 0) {
+        L.mcount = listed ? 2 * start + atomicAdd(&L.fill, c + 1) : 0u;
+        const uint32_t jx = c >= SPLIT_PAR ? atomicAdd(&g.cursor[SJOB_WORD], 1u) : ~0u;
+        L.head[0] = jx < g.sjob_cap ? jx : ~0u;                   // (the job's index; full: ordered here)
+    }
     __syncthreads();
+    if (L.head[0] != ~0u) {                                       // (block-uniform)
+        uint32_t *job = g.sjob + (size_t)L.head[0] * SJOB_WORDS;
+        if (threadIdx.x == 0) {
+            job[0] = key;
+            job[1] = c;
+            job[2] = L.mcount;
+            job[3] = listed ? 1u : 0u;
+            job[4] = (uint32_t)(m - reinterpret_cast<uint32_t *>(g.gbig));
+            job[5] = (uint32_t)tile;
+        }
+        job[SJOB_PCNT + threadIdx.x] = L.pcnt[threadIdx.x];
+        job[SJOB_PCNT + 256 + threadIdx.x] = L.poff[threadIdx.x];
+        __syncthreads();
+        if (threadIdx.x == 0) L.mused += c;
+        __syncthreads();
+        return;
+    }
     const uint32_t off = L.mcount;
     uint32_t *o = g.order + off;
     if (threadIdx.x == 0 && listed) o[0] = c;
@@ -1402,8 +1728,67 @@ __device__ void gbin_split_key(const GroupScratch &g, GbinLds &L, unsigned long 
             }
         __syncthreads();
     }
-    if (threadIdx.x == 0) gbin_mark(g, key, c, off, L.head, L.big);
+    if (threadIdx.x == 0) {
+        gbin_mark(g, key, c, off, L.head, L.big);
+        L.mused += c;
+    }
     __syncthreads();
+}
+
+
+// k_gbin_group's split keys, ordered: a workgroup per (job, scatter tile) -- the tile's
+// members' bits set in an LDS bitmap (a tile is a contiguous packet range of at most 2^16),
+// read back in order into the run at their rank (the tile's offset + the rank within it);
+// the members of rank < NPOS are the group's first packets (k_gbin_marks)
+__global__ void __launch_bounds__(256) k_gbin_tiles(GroupScratch g)
+{
+    __shared__ uint32_t bm[2048], wsum[17];
+    const uint32_t jobs = min(g.cursor[SJOB_WORD], g.sjob_cap);
+    for (uint32_t w = blockIdx.x; w < jobs * GBLK; w += gridDim.x) {   // (block-uniform)
+        const uint32_t *job = g.sjob + (size_t)(w / GBLK) * SJOB_WORDS;
+        const uint32_t t = w % GBLK, pc = job[SJOB_PCNT + t], po = job[SJOB_PCNT + 256 + t];
+        if (!pc) continue;
+        const uint32_t *m = reinterpret_cast<const uint32_t *>(g.gbig) + job[4];
+        const uint32_t tile = job[5], base = t * tile;
+        uint32_t *o = g.order + job[2];
+        const bool listed = job[3] != 0;
+        for (uint32_t k = threadIdx.x; k < 2048; k += blockDim.x) bm[k] = 0;
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < pc; q += blockDim.x) {
+            const uint32_t d = m[po + q] - base;
+            if (d < 65536u) atomicOr(&bm[d >> 5], 1u << (d & 31));
+        }
+        __syncthreads();
+        constexpr uint32_t PER = 2048 / 256;                      // words per thread, in order
+        uint32_t wv[PER], n1 = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) { wv[k] = bm[threadIdx.x * PER + k]; n1 += __popc(wv[k]); }
+        uint32_t tot;
+        uint32_t rank = po + block_excl_scan(n1, wsum, tot);
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k)
+            for (uint32_t v = wv[k]; v; v &= v - 1) {
+                const uint32_t x = base + (threadIdx.x * PER + k) * 32 + (uint32_t)__ffs((int)v) - 1;
+                if (listed) o[1 + rank] = x;
+                if (rank < NPOS) const_cast<uint32_t *>(job)[SJOB_HEAD + rank] = x;
+                ++rank;
+            }
+        __syncthreads();
+    }
+}
+
+// every split key's group marks (its first packets, from k_gbin_tiles), one thread per job
+__global__ void __launch_bounds__(256) k_gbin_marks(GroupScratch g)
+{
+    const uint32_t jobs = min(g.cursor[SJOB_WORD], g.sjob_cap);
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < jobs; w += gridDim.x * blockDim.x) {
+        const uint32_t *job = g.sjob + (size_t)w * SJOB_WORDS;
+        const uint32_t key = job[0], c = job[1];
+        if (job[3]) g.order[job[2]] = c;
+        uint32_t big[2] = {0u, 0u};
+        gbin_mark(g, key, c, job[2], job + SJOB_HEAD, big);
+        if (big[key & 1u]) atomicMax(&g.cursor[GMAX_WORD0 + ((key & 1u) ? g.q6 : g.q4)], big[key & 1u]);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g, uint32_t n)
@@ -1432,6 +1817,7 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g, uint32_t n)
         uint32_t *mem = reinterpret_cast<uint32_t *>(gv + nb);
         const uint32_t tile = (n + GBLK - 1) / GBLK;
         L.bcnt[threadIdx.x] = 0;
+        if (threadIdx.x == 0) L.mused = 0;
         __syncthreads();
         for (uint32_t j0 = 0; j0 < nb; j0 += GUNROLL * blockDim.x) {
             uint2 es[GUNROLL];
@@ -1551,6 +1937,8 @@ void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
     launch_scan(g.gcnt, m, g.gcnt + m + 1, g.gcnt + m, false, s);
     hipLaunchKernelGGL(k_gkey_scatter, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
     hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g, n);
+    hipLaunchKernelGGL(k_gbin_tiles, dim3(1024), dim3(256), 0, s, g);   // (split keys: elephant pairs)
+    hipLaunchKernelGGL(k_gbin_marks, dim3(8), dim3(256), 0, s, g);
     const uint32_t tiles = (n + HTILE - 1) / HTILE;
     hipLaunchKernelGGL(k_heads_count, dim3(tiles), dim3(1024), 0, s, g, n, tiles);
     launch_scan(g.hcnt, 32 * tiles, g.hcnt + 32 * tiles + 1, g.hcnt + 32 * tiles, false, s);
@@ -1936,7 +2324,11 @@ int launch_netdev_stages(const DpParams &p, const BatchDev &b, uint32_t now, con
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
     // the hot runs by whole waves (plain instance, no admission budgets or guards)
     const int hot = !ev && !p.ct_guard && !p.budget && !getenv("CV_NO_HOT_RUNS");
-    if (hot) hipLaunchKernelGGL(k_ct_hot, dim3(512), dim3(HOTB), 0, s, p, b, o, g, now);
+    if (hot) {                                                    // elephants: their chunks in parallel first
+        hipLaunchKernelGGL(k_hpar_look, dim3(1024), dim3(HOTB), 0, s, p, b, g);
+        hipLaunchKernelGGL(k_hpar_fin, dim3(1024), dim3(HOTB), 0, s, p, b, o, g, now);
+        hipLaunchKernelGGL(k_ct_hot, dim3(512), dim3(HOTB), 0, s, p, b, o, g, now);
+    }
     if (ev) hipLaunchKernelGGL(k_ct_stage<true>, grid, blk, 0, s, p, b, o, g, now, 0);
     else hipLaunchKernelGGL(k_ct_stage<false>, grid, blk, 0, s, p, b, o, g, now, hot);
     GroupScratch g6 = g;

@@ -137,13 +137,17 @@ def test_config3_endpoint_groups_hot_runs(dev):
     _ingress_grouped(w, dev, 3, rounds=2)
 
 
-def test_config3_merged_runs_across_maps(dev, monkeypatch):
+@pytest.mark.parametrize("n", [1 << 15, 1 << 18])
+def test_config3_merged_runs_across_maps(dev, monkeypatch, n):
     """Runs that hold members of different CT maps (advisor r04: two groups merged by a
     key collision): CV_COARSE_GROUPS keeps 8 bits of every group key, so each run of
     k_ct_hot mixes address pairs of endpoints on 5 CT maps; a member on another map than
-    the run's first runs whole instead of folding into the run's map"""
+    the run's first runs whole instead of folding into the run's map.  At 2^18 packets the
+    runs pass HPAR_MIN members (the parallel elephant kernels cut them at their first
+    member on another map or entry) and their bins pass LCAP (split keys ordered by
+    k_gbin_tiles)."""
     monkeypatch.setenv("CV_COARSE_GROUPS", "1")
-    w = synth.config3(1 << 15, 1 << 11, n_ep=40, n_cidrs=512, n_ids=60, seed=79)
+    w = synth.config3(n, 1 << 11, n_ep=40, n_cidrs=512, n_ids=60, seed=79)
     _ingress_grouped(w, dev, 5, rounds=2)
 
 

@@ -859,7 +859,9 @@ __global__ void __launch_bounds__(HOTB) k_hpar_look(DpParams p, BatchDev b, Grou
         }
         (void)r;
         const uint32_t k = (q - first) * HOTB + threadIdx.x;
-        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;
+        const uint32_t x0 = g.order[off + 1];
+        if (!pkt_ok(g, x0)) continue;                             // (block-uniform; reported)
+        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;
         HotMember h;
         Acct a{0, 0, nullptr};
         hot_lookup(p, b, g, ct, off, cnt, k, h, a);
@@ -927,7 +929,9 @@ __global__ void __launch_bounds__(HOTB) k_hpar_fin(DpParams p, BatchDev b, OutDe
             __syncthreads();
             continue;
         }
-        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * g.order[off + 1] + 1].z & 0xFFFFu).ct4;
+        const uint32_t x0 = g.order[off + 1];
+        if (!pkt_ok(g, x0)) continue;                             // (block-uniform; reported)
+        const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;
         HotMember h;
         Acct a{0, 0, m.pc};
         const uint32_t k = k0 + threadIdx.x;
@@ -1363,6 +1367,8 @@ __global__ void __launch_bounds__(1024) k_gkey_hist(GroupScratch g, uint32_t n)
 {
     extern __shared__ uint32_t hist[];                           // one counter per bin
     const uint32_t nb = 1u << g.gbits;
+    if (blockIdx.x == 0 && threadIdx.x == 0) g.cursor[SJOB_WORD] = 0;   // (this grouping's split keys: none yet;
+                                                                        //  a launch may run two groupings)
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[j] = 0;
     __syncthreads();
     const uint32_t tile = (n + GBLK - 1) / GBLK, lo = blockIdx.x * tile, hi = min(n, lo + tile);
@@ -1769,6 +1775,7 @@ __global__ void __launch_bounds__(256) k_gbin_tiles(GroupScratch g)
         for (uint32_t k = 0; k < PER; ++k)
             for (uint32_t v = wv[k]; v; v &= v - 1) {
                 const uint32_t x = base + (threadIdx.x * PER + k) * 32 + (uint32_t)__ffs((int)v) - 1;
+                if (!pkt_ok(g, x) || rank >= job[1]) { ++rank; continue; }   // (a corrupt job)
                 if (listed) o[1 + rank] = x;
                 if (rank < NPOS) const_cast<uint32_t *>(job)[SJOB_HEAD + rank] = x;
                 ++rank;
@@ -1784,6 +1791,9 @@ __global__ void __launch_bounds__(256) k_gbin_marks(GroupScratch g)
     for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < jobs; w += gridDim.x * blockDim.x) {
         const uint32_t *job = g.sjob + (size_t)w * SJOB_WORDS;
         const uint32_t key = job[0], c = job[1];
+        bool ok = run_ok(g, job[2], c);
+        for (uint32_t t = 0; t < NPOS && t < c; ++t) ok = ok && pkt_ok(g, job[SJOB_HEAD + t]);
+        if (!ok) continue;                                        // (a corrupt job: reported, skipped)
         if (job[3]) g.order[job[2]] = c;
         uint32_t big[2] = {0u, 0u};
         gbin_mark(g, key, c, job[2], job + SJOB_HEAD, big);

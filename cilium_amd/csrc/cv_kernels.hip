@@ -470,6 +470,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 // budgets or guards use it; the others keep one lane per run.
 constexpr int HOT_CLASS = 12;                                     // size_class: runs of more than 32 members
 constexpr uint32_t HOTB = 1024;                                   // threads (members) per chunk
+constexpr uint32_t HOT_ENTRIES = 16;                              // entries one chunk may fold
 
 __device__ __forceinline__ uint32_t hot_runs(const GroupScratch &g, int q)
 {
@@ -1002,35 +1003,63 @@ __global__ void __launch_bounds__(HOTB) k_hpar_fin(DpParams p, BatchDev b, OutDe
     pol_cache_flush(pc);
 }
 
-// the elephant r's chunk summaries composed in order and applied to its entry (one
-// thread); returns where k_ct_hot resumes
-__device__ uint32_t hpar_fold(const DpParams &p, const GroupScratch &g, const HashTable &ct, uint32_t r, uint32_t now)
+// the elephant r's chunk summaries composed in order and applied to its entry: the whole
+// workgroup stages HPF_BATCH summaries at a time in LDS (one round of loads each), thread
+// 0 composes them; returns where k_ct_hot resumes (every thread)
+constexpr uint32_t HPF_BATCH = 256;
+struct HparLds {
+    uint32_t sm[HPF_BATCH * 16];
+    uint32_t T, A[8], cut;
+    unsigned long long pk[2], by[2];
+};
+
+__device__ uint32_t hpar_fold(const DpParams &p, const GroupScratch &g, const HashTable &ct, uint32_t r, uint32_t now,
+                              HparLds &F)
 {
     const uint32_t first = g.hot[HP_RUN + 4 * r + 2], nch = g.hot[HP_RUN + 4 * r + 3];
-    if (!nch) return 0;
+    if (!nch) return 0;                                           // (block-uniform)
     const uint32_t cut = g.hot[HP_CUT + 4 * r];
     const unsigned long long e = (unsigned long long)g.hot[HP_CUT + 4 * r + 2] << 32 | g.hot[HP_CUT + 4 * r + 1];
     if (e == ~0ull || !cut) return cut;                           // (no hit before the cut)
-    uint32_t T = FX_IDENT, A[8];                                  // per starting state: what the updates so far did
-    unsigned long long pk[2] = {0, 0}, by[2] = {0, 0};
-    for (int x = 0; x < 8; ++x) A[x] = 0;
-    for (uint32_t q = first; q < first + nch && (q - first) * HOTB < cut; ++q) {
-        const uint32_t *sm = g.hot + hp_sum(g.hot_chunks) + 16 * q;
-        for (uint32_t x = 0; x < 8; ++x) {
-            const uint32_t bx = sm[1 + fx_at(T, x)];
-            if (bx & 1u) A[x] = (A[x] & ~7u) | (bx & 7u);         // (the later update's lifetime class)
-            A[x] |= bx & 0xFFFF18u;                               // (any / seen accumulate)
-        }
-        T = fx_then(T, sm[0]);
-        for (int d = 0; d < 2; ++d) { pk[d] += sm[9 + d]; by[d] += sm[11 + d]; }
+    const uint32_t used = min(nch, (cut + HOTB - 1) / HOTB);      // chunks with members before the cut
+    if (threadIdx.x == 0) {                                       // per starting state: what the updates so far did
+        F.T = FX_IDENT;
+        for (int x = 0; x < 8; ++x) F.A[x] = 0;
+        F.pk[0] = F.pk[1] = F.by[0] = F.by[1] = 0;
     }
-    const int64_t slot = (int64_t)e;
-    CtE en;
-    ct_load_hot<Ct4Spec>(ct, slot, en);
-    uint32_t h[CT_HOTW] = {en.w[8], en.w[9], en.w[10], en.w[11], en.w[12], en.w[13], en.w[0], en.w[2], en.w[4], en.w[6]};
-    const uint32_t x0 = bits_x(h[1] & 0xFFFFu), a = A[x0];
-    const uint32_t seen[2] = {(a >> 8) & 0xFFu, (a >> 16) & 0xFFu}, any[2] = {(a >> 3) & 1u, (a >> 4) & 1u};
-    hot_store(ct, slot, h, fx_at(T, x0), a & 1u, (a >> 1) & 3u, seen, any, pk, by, now, p.flags);
+    for (uint32_t q0 = 0; q0 < used; q0 += HPF_BATCH) {           // (block-uniform)
+        const uint32_t nb = min(HPF_BATCH, used - q0);
+        const uint32_t *src = g.hot + hp_sum(g.hot_chunks) + 16 * (first + q0);
+        __syncthreads();
+        for (uint32_t w = threadIdx.x; w < nb * 16; w += blockDim.x) F.sm[w] = src[w];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t T = F.T, A[8];
+            for (int x = 0; x < 8; ++x) A[x] = F.A[x];
+            for (uint32_t q = 0; q < nb; ++q) {
+                const uint32_t *sm = F.sm + 16 * q;
+                for (uint32_t x = 0; x < 8; ++x) {
+                    const uint32_t bx = sm[1 + fx_at(T, x)];
+                    if (bx & 1u) A[x] = (A[x] & ~7u) | (bx & 7u);     // (the later update's lifetime class)
+                    A[x] |= bx & 0xFFFF18u;                           // (any / seen accumulate)
+                }
+                T = fx_then(T, sm[0]);
+                for (int d = 0; d < 2; ++d) { F.pk[d] += sm[9 + d]; F.by[d] += sm[11 + d]; }
+            }
+            F.T = T;
+            for (int x = 0; x < 8; ++x) F.A[x] = A[x];
+        }
+    }
+    if (threadIdx.x == 0) {
+        const int64_t slot = (int64_t)e;
+        CtE en;
+        ct_load_hot<Ct4Spec>(ct, slot, en);
+        uint32_t h[CT_HOTW] = {en.w[8], en.w[9], en.w[10], en.w[11], en.w[12], en.w[13], en.w[0], en.w[2], en.w[4],
+                               en.w[6]};
+        const uint32_t x0 = bits_x(h[1] & 0xFFFFu), a = F.A[x0];
+        const uint32_t seen[2] = {(a >> 8) & 0xFFu, (a >> 16) & 0xFFu}, any[2] = {(a >> 3) & 1u, (a >> 4) & 1u};
+        hot_store(ct, slot, h, fx_at(F.T, x0), a & 1u, (a >> 1) & 3u, seen, any, F.pk, F.by, now, p.flags);
+    }
     return cut;
 }
 
@@ -1039,6 +1068,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
     __shared__ HotLds L;
+    __shared__ HparLds F;
     using M = MetT<false>;
     M m;
     pol_cache_init(pc);
@@ -1053,9 +1083,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
         const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;   // (the run's map)
         // an elephant's members before its cut ran in parallel (k_hpar_*): their updates of
         // its entry folded here, then the walk resumes at the cut
-        if (threadIdx.x == 0) L.c = r < HPAR_RUNS ? hpar_fold(p, g, ct, r, now) : 0u;
-        __syncthreads();
-        const uint32_t start = L.c;
+        const uint32_t start = r < HPAR_RUNS ? hpar_fold(p, g, ct, r, now, F) : 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         l1_inv();
         __syncthreads();
@@ -1067,6 +1095,29 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             if (threadIdx.x == 0) { L.c = HOTB; L.lead = HOTB; }
             __syncthreads();
             if (h.change) atomicMin(&L.c, threadIdx.x);
+            __syncthreads();
+            // at most HOT_ENTRIES entries per chunk (the fold runs a pass per entry): the
+            // chunk ends at the first hit on a further one -- a hot pair carrying many port
+            // flows takes several chunks instead of a pass per flow (advisor r04)
+            bool seen_e = !(h.hr.slot >= 0 && threadIdx.x < L.c);
+            for (uint32_t ne = 0;; ++ne) {                        // (block-uniform)
+                if (threadIdx.x == 0) L.lead = HOTB;
+                __syncthreads();
+                if (!seen_e) atomicMin(&L.lead, threadIdx.x);
+                __syncthreads();
+                const uint32_t ld = L.lead;
+                if (ld >= HOTB) break;
+                if (ne == HOT_ENTRIES) {                          // ld: the first hit on one entry too many
+                    if (threadIdx.x == 0) L.c = ld;
+                    __syncthreads();
+                    break;
+                }
+                if (threadIdx.x == ld) L.slot = (unsigned long long)h.hr.slot;
+                __syncthreads();
+                if (!seen_e && (unsigned long long)h.hr.slot == L.slot) seen_e = true;
+            }
+            if (threadIdx.x == 0) L.lead = HOTB;
+            __syncthreads();
             if (h.hr.slot >= 0) atomicMin(&L.lead, threadIdx.x);  // the first hit
             __syncthreads();
             const uint32_t c = L.c;

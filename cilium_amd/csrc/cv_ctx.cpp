@@ -232,6 +232,8 @@ struct cv_ctx {
     DevBuf ghot;                  // elephants in parallel (k_hpar_*)
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
     DevBuf adm_mi, adm_keys, adm_sort; // (per packet: map index; walk keys, sorted; radix-sort scratch)
+    DevBuf adm_evt;                    // (k_ct_intent's spill tables)
+    uint32_t adm_stamp = 0;
     // the launch's CT maps as admission and the live-count reads see them (map_table)
     std::vector<MapObj *> mt_maps;
     size_t mt_eps = ~(size_t)0;
@@ -1631,6 +1633,8 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
         (c->adm_mi.n < (size_t)n * 2 && c->adm_mi.alloc((size_t)n * 2)) ||
         (c->adm_keys.n < (size_t)n * 16 && c->adm_keys.alloc((size_t)n * 16)) ||
         (c->adm_sort.n < sort_bytes && c->adm_sort.alloc(sort_bytes)) ||
+        (c->adm_evt.n < (size_t)n * 128 &&
+         (c->adm_evt.alloc((size_t)n * 128) || hipMemset(c->adm_evt.p, 0, c->adm_evt.n) != hipSuccess)) ||
         (!c->adm_tsum.p && c->adm_tsum.alloc((size_t)4096 * 12)) || (!c->adm_win.p && c->adm_win.alloc(32)))
         return -ENOMEM;
     a.ib = c->adm_ib.as<uint8_t>();
@@ -1642,6 +1646,7 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
     a.sort_bytes = c->adm_sort.n;
     a.tsum = c->adm_tsum.as<uint32_t>();
     a.hi = c->adm_win.as<uint32_t>();
+    a.evt = c->adm_evt.as<unsigned long long>();
     const char *inj = getenv("CV_ADMIT_INJECT");
     a.inject = inj ? (uint32_t)strtoul(inj, nullptr, 0) : ~0u;
     r = launch_netdev_front(p, bc, with_prefilter, oc, gs, s);
@@ -1657,6 +1662,11 @@ int run_admitted(cv_ctx *c, DpParams p, const BatchDev &bc, const OutDev &oc, ui
         uint32_t end = lo, w[5] = {n, n, n, 0, 0};
         for (int pass = 0;; ++pass) {
             a.pass = (uint32_t)pass;
+            if (++c->adm_stamp == 0) {                            // (2^32 passes: stale stamps cleared)
+                (void)hipMemsetAsync(c->adm_evt.p, 0, c->adm_evt.n, s);
+                c->adm_stamp = 1;
+            }
+            a.stamp = c->adm_stamp;
             if ((r = launch_admission(p, bc, gs, a, s))) return r;
             ++passes;
             hipError_t e = hipMemcpyAsync(w, a.hi, 20, hipMemcpyDeviceToHost, s);

@@ -118,6 +118,8 @@ struct Admit {
                                        // after the intents (~0u: none)
     void *sort_tmp;                    // radix-sort scratch
     size_t sort_bytes;
+    unsigned long long *evt;           // k_ct_intent's spill tables: 4 slots of 16 B per `order` word
+    uint32_t stamp;                    // this pass's (spill-table slots of other passes are free)
 };
 // a packet's endpoint has no CT map in the list (k_ct_intent), a packet's map index is
 // past nmaps (k_adm_keys): a stale or corrupt intent, failed loudly instead of indexing

@@ -2432,22 +2432,57 @@ int launch_netdev_ingress(const DpParams &p, const BatchDev &b, uint32_t now, in
 // (by hash; a hit is confirmed against the member's key re-derived from its record),
 // the member, and its kind: 0 a delete (certain), 1 / 2 a create that went in iff the
 // member's budget reaches 1 (its tuple) / 2 (its ICMP twin, tried second).
+// Past N events a run's events move to its spill table (a region of Admit::evt
+// addressed by the run's place in `order`, 4 slots per member at most half full, slots
+// stamped with the pass), which keeps the latest event per key hash -- a run of many
+// creates (a busy endpoint's map next to its limit) no longer ends the window.
 template <class T>
 struct Changed {
     static constexpr int N = 6;
     uint64_t h[N];
     uint32_t ev[N];                                               // member | kind << 30
     int n = 0;
-    __device__ void reset() { n = 0; }
-    __device__ bool overflow() const { return n > N; }
+    unsigned long long *tab = nullptr;                            // {hash, stamp << 32 | event} per slot
+    uint32_t cap = 0, stamp = 0;
+    bool spill = false;
+    __device__ void reset() { n = 0; spill = false; tab = nullptr; }
+    __device__ bool overflow() const { return n > N && !spill; }
+    __device__ void put(uint64_t hk, uint32_t e)
+    {
+        uint32_t sl = (uint32_t)(hk % cap);
+        for (uint32_t k = 0; k < cap; ++k, sl = sl + 1 == cap ? 0u : sl + 1) {
+            const unsigned long long w1 = tab[2 * (size_t)sl + 1];
+            if ((uint32_t)(w1 >> 32) != stamp || tab[2 * (size_t)sl] == hk) {
+                tab[2 * (size_t)sl] = hk;
+                tab[2 * (size_t)sl + 1] = (unsigned long long)stamp << 32 | e;
+                return;
+            }
+        }
+    }
+    __device__ uint32_t find(uint64_t hk) const                   // the latest event on hk, or ~0u
+    {
+        uint32_t sl = (uint32_t)(hk % cap);
+        for (uint32_t k = 0; k < cap; ++k, sl = sl + 1 == cap ? 0u : sl + 1) {
+            const unsigned long long w1 = tab[2 * (size_t)sl + 1];
+            if ((uint32_t)(w1 >> 32) != stamp) return ~0u;
+            if (tab[2 * (size_t)sl] == hk) return (uint32_t)w1;
+        }
+        return ~0u;
+    }
     __device__ void add(const T &t, uint32_t member, uint32_t kind)
     {
         uint32_t k[T::KW];
         t.key(k);
         const uint64_t hk = key_hash<typename T::Spec>(k);
+        const uint32_t e = member | kind << 30;
+        if (!spill && n == N && tab) {                            // (to the run's table)
+            spill = true;
+            for (int j = 0; j < N; ++j) put(h[j], ev[j]);
+        }
+        if (spill) { put(hk, e); return; }
 #pragma unroll
         for (int j = 0; j < N; ++j)
-            if (j == n) { h[j] = hk; ev[j] = member | kind << 30; }
+            if (j == n) { h[j] = hk; ev[j] = e; }
         ++n;
     }
 };
@@ -2500,10 +2535,34 @@ __device__ __forceinline__ T twin_of(const T &t2)
 // counts: a delete leaves it absent, a create present iff the member's budget covered
 // it (a failed create leaves it absent, as it was).  *used: a state came from a budget.
 template <bool V6, class T>
-__device__ __forceinline__ void changed_state(const DpParams &p, const BatchDev &b, const GroupScratch &g,
+__device__ __forceinline__ bool changed_state(const DpParams &p, const BatchDev &b, const GroupScratch &g,
                                               const Changed<T> &cg, const uint32_t (&ks)[3][T::KW],
                                               const uint8_t *budget, uint32_t (&st)[3], bool &used)
 {
+    if (cg.spill) {                                               // the run's table: the latest event per key
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            st[q] = 2;
+            const uint32_t e = cg.find(key_hash<typename T::Spec>(ks[q]));
+            if (e == ~0u) continue;
+            const uint32_t m = e & 0x3FFFFFFFu, kind = e >> 30;
+            T te;
+            EpDev ep;
+            uint32_t src;
+            if (!intent_tuple<V6>(p, b, g, m, te, ep, src)) return false;
+            te.reverse();
+            if (kind == 2) te = twin_of<V6>(te);
+            uint32_t km[T::KW];
+            te.key(km);
+            bool eq = true;
+#pragma unroll
+            for (int w = 0; w < T::KW; ++w) eq &= km[w] == ks[q][w];
+            if (!eq) return false;                                // (a hash collision: unsure)
+            if (kind) used = true;
+            st[q] = kind ? (budget[m] >= kind ? 1u : 0u) : 0u;
+        }
+        return true;
+    }
     uint32_t hit[3], all = 0;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -2540,6 +2599,7 @@ __device__ __forceinline__ void changed_state(const DpParams &p, const BatchDev 
             st[q] = kind ? (budget[m] >= kind ? 1u : 0u) : 0u;
         }
     }
+    return true;
 }
 
 // one packet's creates (bits 0-1), delete (bit 2) and unsure flag (bit 6, bit 7 the
@@ -2562,7 +2622,7 @@ __device__ __forceinline__ uint32_t ct_intent(const DpParams &p, const BatchDev 
     t.key(ks[0]);
     t2.key(ks[1]);
     tw.key(ks[2]);
-    changed_state<V6>(p, b, g, cg, ks, budget, st, used);
+    if (!changed_state<V6>(p, b, g, cg, ks, budget, st, used)) return 64u | 128u;
     auto present = [&](int q) { return st[q] == 2 ? dev_find<typename T::Spec>(ct, ks[q], nullptr) >= 0 : st[q] == 1; };
     if (present(0)) return 0;                                     // CT_REPLY / CT_RELATED
     const bool est = present(1);
@@ -2626,6 +2686,11 @@ __global__ void __launch_bounds__(BLOCK) k_ct_intent(DpParams p, BatchDev b, Gro
             if (!redo) continue;
         }
         cg.reset();
+        if (cnt > 2 && a.evt) {                                   // (a spill table, should the run need one)
+            cg.tab = a.evt + 2 * 4 * (size_t)off;
+            cg.cap = 4 * (cnt + 1);
+            cg.stamp = a.stamp;
+        }
 #pragma unroll 1
         for (uint32_t k = 0; k < cnt; ++k) {
             const uint32_t x = g.order[off + 1 + k];
@@ -2741,26 +2806,41 @@ __device__ __forceinline__ SegSM block_excl_seg(SegSM v, SegSM *lds, SegSM *tota
 }
 
 // the walks' elements: map << 24 | packet for the packets from lo with creates or
-// deletes, appended in any order (the sort orders them); hi[4] counts them
+// deletes, appended in any order (the sort orders them); hi[4] counts them.  A block
+// takes ADM_KPT packets per thread, contiguous, and allocates once per block (one
+// returning atomic per lane-wave on one word serialised at the device's atomic rate:
+// 2.9 ms per 2^24 packets)
+constexpr uint32_t ADM_KPT = 16;
 __global__ void __launch_bounds__(BLOCK) k_adm_keys(Admit a, uint32_t n)
 {
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t j0 = a.lo + blockIdx.x * BLOCK + (threadIdx.x & ~63u); j0 < n; j0 += gridDim.x * BLOCK) {
-        const uint32_t j = j0 + lane;
-        const uint32_t v = j < n ? a.ib[j] : 0u;
-        bool el = false;
-        unsigned long long k = 0;
-        if (v & 7u) {
-            const uint32_t mi = a.mi[j];
-            if (mi >= a.nmaps) atomicOr(a.hi + 3, ADMIT_ERR_IB);   // (a corrupt or stale map index)
-            else { k = (unsigned long long)mi << 24 | j; el = true; }   // (j < MAX_CHUNK = 2^24)
+    __shared__ uint32_t wsum[17], base_s;
+    const uint32_t per = BLOCK * ADM_KPT;
+    for (uint32_t b0 = a.lo + blockIdx.x * per; b0 < n; b0 += gridDim.x * per) {   // (block-uniform)
+        const uint32_t j0 = b0 + threadIdx.x * ADM_KPT;
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < ADM_KPT; ++u) {
+            const uint32_t j = j0 + u;
+            if (j < n && (a.ib[j] & 7u)) ++mine;
         }
-        const unsigned long long bal = __ballot(el);
-        if (!bal) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.hi + 4, (uint32_t)__popcll(bal));
-        base = (uint32_t)__shfl((int)base, 0, 64);
-        if (el) a.keys[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = k;
+        uint32_t total;
+        uint32_t at = block_excl_scan(mine, wsum, total);
+        if (threadIdx.x == 0) base_s = total ? atomicAdd(a.hi + 4, total) : 0u;
+        __syncthreads();
+        at += base_s;
+#pragma unroll
+        for (uint32_t u = 0; u < ADM_KPT; ++u) {
+            const uint32_t j = j0 + u;
+            if (j >= n || !(a.ib[j] & 7u)) continue;
+            const uint32_t mi = a.mi[j];
+            unsigned long long k = (unsigned long long)mi << 24 | j;   // (j < MAX_CHUNK = 2^24)
+            if (mi >= a.nmaps) {                                  // (a corrupt or stale map index)
+                atomicOr(a.hi + 3, ADMIT_ERR_IB);
+                k = (unsigned long long)(a.nmaps) << 24 | j;      // (sorted past every map, never applied)
+            }
+            a.keys[at++] = k;
+        }
+        __syncthreads();
     }
 }
 
@@ -2776,6 +2856,10 @@ __device__ __forceinline__ SegSM adm_elem(const Admit &a, uint32_t L, uint32_t q
     const unsigned long long k = a.keys_sorted[q];
     map = key_map(k);
     pkt = (uint32_t)k & 0xFFFFFFu;
+    if (map >= a.nmaps) {                                         // (a corrupt element: never applied)
+        map = KEY_NONE;
+        return SEG_ID;
+    }
     const uint32_t v = a.ib[pkt];
     const int32_t d = (int32_t)((v >> 2) & 1u) - (int32_t)(v & 3u);
     const int32_t f = q == 0 || key_map(a.keys_sorted[q - 1]) != map;

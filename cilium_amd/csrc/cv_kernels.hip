@@ -468,7 +468,10 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 // costs one round of lookups and a scan.  Only the plain instance (no event records,
 // whose trace decisions need the per-packet entry state) and launches without admission
 // budgets or guards use it; the others keep one lane per run.
-constexpr int HOT_CLASS = 12;                                     // size_class: runs of more than 32 members
+#ifndef CV_HOT_CLASS
+#define CV_HOT_CLASS 12
+#endif
+constexpr int HOT_CLASS = CV_HOT_CLASS;                           // size_class: runs of more than 32 members
 constexpr uint32_t HOTB = 1024;                                   // threads (members) per chunk
 constexpr uint32_t HOT_ENTRIES = 16;                              // entries one chunk may fold
 
@@ -803,7 +806,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, 
 //               then the walk resumes at the cut, serially as before.
 // An elephant of established packets is one round of parallel lookups instead of a chain
 // of ~24-us chunks.
-constexpr uint32_t HPAR_RUNS = 256, HPAR_MIN = 8 * HOTB;
+#ifndef CV_HPAR_MIN
+#define CV_HPAR_MIN (8 * 1024)
+#endif
+constexpr uint32_t HPAR_RUNS = 256, HPAR_MIN = CV_HPAR_MIN;
 // g.hot layout: per run r < HPAR_RUNS: HP_RUN + 4r {off, cnt, first chunk, chunks} (chunks
 // 0: not in parallel), HP_CUT + 4r {cut, e lo, e hi, -}; HP_TOTAL the chunks; per chunk q:
 // HP_CHUNK + 8q {run, first change, first hit, hit on another entry, e lo, e hi, -, -} and

@@ -229,6 +229,7 @@ struct cv_ctx {
     DevBuf gres, gdel_ev;         // egress: packed outputs (16 B), delivery records' event part (32 B)
     DevBuf gpkey, gent, gbig, gcnt, gwork6, ghword, ghcnt;   // the netdev path's binned grouping
     DevBuf gsjob;                 // (its split-key jobs)
+    DevBuf gbx;                   // (its big-bin records)
     DevBuf ghot;                  // elephants in parallel (k_hpar_*)
     DevBuf adm_ib, adm_tsum, adm_win;  // conntrack admission next to max_entries
     DevBuf adm_mi, adm_keys, adm_sort; // (per packet: map index; walk keys, sorted; radix-sort scratch)
@@ -1207,6 +1208,7 @@ int ensure_groups(cv_ctx *c, uint32_t cmax, bool egress)
     if (c->gtable.alloc(cap * 16) || c->gsingle.alloc((size_t)cmax * 4) ||
         c->gpkey.alloc((size_t)cmax * 8) || c->gent.alloc((size_t)cmax * 8) || c->gbig.alloc((size_t)cmax * 16) ||
         c->gsjob.alloc(((size_t)cmax / 4096 + 16) * SJOB_WORDS * 4) ||
+        c->gbx.alloc(((size_t)GBIN_MAX + ((size_t)cmax / BIG_MIN + 2) * BIGW) * 4) ||
         c->ghot.alloc(((size_t)(cmax / 1024 + 256) * 24 + 4096) * 4) ||
         c->gcnt.alloc(((size_t)GBIN_MAX * GBLK + 1 + 1024) * 4) || c->gwork6.alloc((size_t)cmax * 4) ||
         c->ghword.alloc((size_t)cmax * 4) ||
@@ -1273,6 +1275,8 @@ GroupScratch next_groups(cv_ctx *c, uint32_t epochs, hipStream_t stream)
     gs.sjob_cap = (uint32_t)(c->gn / 4096 + 16);
     gs.hot = c->ghot.as<uint32_t>();
     gs.hot_chunks = (uint32_t)(c->gn / 1024 + 256);
+    gs.gbx = c->gbx.as<uint32_t>();
+    gs.gbx_cap = (uint32_t)(c->gn / BIG_MIN + 2);
     (void)hipMemsetAsync(c->gcursor.p, 0, CURSOR_WORDS * 4, stream);
     c->epoch += epochs;
     return gs;

@@ -225,6 +225,9 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *err;             // host-mapped error word of the context: a walker that reads a list
                                // word past the launch stores GERR_* here and skips it (the host fails
                                // its next call with -EPROTO), or null
+    uint32_t *gbx;             // the binned grouping's big bins (k_gbig_*): per bin its record + 1 (0:
+                               // none), then BIGW words per record (BIG_*)
+    uint32_t gbx_cap;          // records gbx holds
 };
 enum : uint32_t { GERR_INDEX = 1 };
 // binning blocks of k_gkey_hist / k_gkey_scatter (each a contiguous packet range), and
@@ -251,7 +254,12 @@ constexpr int GMAX_WORD0 = 8;   // cursor[8 + q]: the largest group of queue q (
 constexpr uint32_t SINGLE_RUN = 0x80000000u; // a list word naming a singleton's packet (diagnostics)
 constexpr int SINGLE_WORD0 = 16; // cursor[16 + q]: singleton groups of queue q listed in `single`
 constexpr int SJOB_WORD = 24;    // cursor[24]: split-key jobs of the binned grouping (GroupScratch::sjob)
-// a split-key job: {key, members c, order offset, listed, member base in gbig (u32 words), q6, pad[2],
+constexpr int BIG_WORD = 25;     // cursor[25]: big-bin records of the binned grouping (GroupScratch::gbx)
+// a big bin (>= BIG_MIN entries): a record of BIGW words {bin, key, start, entries, the key's
+// members, the other entries, its job (~0: not taken out), the others' fill, per scatter
+// tile the key's members [GBLK] (then the tile's fill cursor [GBLK])}
+constexpr uint32_t BIG_MIN = 8192, BIG_PCNT = 8, BIG_FILL = 8 + 256, BIGW = 8 + 512;
+// a split-key job: {key, members c, order offset, listed, member base in gbig (u32 words), tile, pad[2],
 // head[NPOS <= 8], per tile its member count [GBLK] and offset [GBLK]}
 constexpr uint32_t SJOB_HEAD = 8, SJOB_PCNT = 16, SJOB_WORDS = 16 + 2 * 256;
 constexpr int EG_WORDS = 16;

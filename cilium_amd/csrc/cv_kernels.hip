@@ -469,9 +469,10 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
 // whose trace decisions need the per-packet entry state) and launches without admission
 // budgets or guards use it; the others keep one lane per run.
 #ifndef CV_HOT_CLASS
-#define CV_HOT_CLASS 12
+#define CV_HOT_CLASS 14
 #endif
-constexpr int HOT_CLASS = CV_HOT_CLASS;                           // size_class: runs of more than 32 members
+constexpr int HOT_CLASS = CV_HOT_CLASS;                           // size_class: runs of more than 128 members
+                                                                  // (12 / 13: 32 / 64 measured 13 % / 2 % slower on Zipf 1.1)
 constexpr uint32_t HOTB = 1024;                                   // threads (members) per chunk
 constexpr uint32_t HOT_ENTRIES = 16;                              // entries one chunk may fold
 
@@ -1424,8 +1425,10 @@ __global__ void __launch_bounds__(1024) k_gkey_hist(GroupScratch g, uint32_t n)
 {
     extern __shared__ uint32_t hist[];                           // one counter per bin
     const uint32_t nb = 1u << g.gbits;
-    if (blockIdx.x == 0 && threadIdx.x == 0) g.cursor[SJOB_WORD] = 0;   // (this grouping's split keys: none yet;
-                                                                        //  a launch may run two groupings)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                   // (this grouping's split keys and big bins:
+        g.cursor[SJOB_WORD] = 0;                                  //  none yet; a launch may run two groupings)
+        g.cursor[BIG_WORD] = 0;
+    }
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) hist[j] = 0;
     __syncthreads();
     const uint32_t tile = (n + GBLK - 1) / GBLK, lo = blockIdx.x * tile, hi = min(n, lo + tile);
@@ -1858,40 +1861,220 @@ __global__ void __launch_bounds__(256) k_gbin_marks(GroupScratch g)
     }
 }
 
+// Big bins in parallel.  A bin of BIG_MIN entries or more is an elephant's (one address
+// pair carrying a large share of the launch) next to a few ordinary keys: one workgroup
+// streaming it (the sub-bin scatter, then gbin_split_key's two passes) took 5 ms for
+// 837 000 entries.  Four launches take its dominant key out across the device first:
+// k_gbig_list picks the key (the most frequent of 64 evenly spaced samples, as
+// gbin_split_key does) and opens a record; k_gbig_count counts the key's members per
+// scatter tile and the other entries, a workgroup per chunk of the bin; k_gbig_plan
+// turns a key with at least half of its bin into a split-key job (its run first in the
+// bin's region of `order`, its members per tile at the tile offsets); k_gbig_place writes
+// the members by tile and packs the other entries to the front of the bin's gbig region.
+// k_gbin_group then groups only those others, and k_gbin_tiles orders the job's members.
+constexpr uint32_t BIG_CHUNK = 2048;                              // bin entries per workgroup step (256 x 8)
+
+__device__ __forceinline__ void gbin_range(const GroupScratch &g, uint32_t b, uint32_t &start, uint32_t &nb)
+{
+    const uint32_t nbins = 1u << g.gbits, m = nbins * GBLK;
+    start = g.gcnt[b * GBLK];
+    nb = (b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m]) - start;
+}
+
+// a wave per bin: its record, or 0
+__global__ void __launch_bounds__(256) k_gbig_list(GroupScratch g)
+{
+    const uint32_t lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= (1u << g.gbits) || !g.gbx) return;                 // (wave-uniform)
+    uint32_t start, nb;
+    gbin_range(g, b, start, nb);
+    uint32_t *bx = g.gbx;
+    if (nb < BIG_MIN) {
+        if (!lane) bx[b] = 0;
+        return;
+    }
+    const uint32_t sk = g.gent[start + (uint32_t)((unsigned long long)lane * nb / 64)].y;
+    uint32_t same = 0;
+    for (int l = 0; l < 64; ++l) same += __shfl(sk, l, 64) == sk ? 1u : 0u;
+    uint32_t best = same << 6 | (63u - lane);                     // (ties: the lowest lane)
+    for (int d = 32; d; d >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, d, 64));
+    const uint32_t key = __shfl(sk, 63 - (int)(best & 63u), 64);
+    uint32_t r = 0;
+    if (!lane) r = atomicAdd(&g.cursor[BIG_WORD], 1u);
+    r = (uint32_t)__shfl((int)r, 0, 64);
+    if (r >= g.gbx_cap) {                                         // (full: the bin stays whole)
+        if (!lane) bx[b] = 0;
+        return;
+    }
+    uint32_t *rec = bx + GBIN_MAX + (size_t)r * BIGW;
+    if (!lane) {
+        rec[0] = b; rec[1] = key; rec[2] = start; rec[3] = nb;
+        rec[4] = 0; rec[5] = 0; rec[6] = ~0u; rec[7] = 0;
+        bx[b] = r + 1;
+    }
+    for (uint32_t t = lane; t < 2 * GBLK; t += 64) rec[BIG_PCNT + t] = 0;
+}
+
+// the records' chunks over the grid: record k's chunk u goes to workgroup (u + 97 k) mod grid
+template <class F>
+__device__ __forceinline__ void for_each_big_chunk(const GroupScratch &g, F &&fn)
+{
+    const uint32_t nrec = g.gbx ? min(g.cursor[BIG_WORD], g.gbx_cap) : 0u;
+    for (uint32_t k = 0; k < nrec; ++k) {                         // (block-uniform)
+        uint32_t *rec = g.gbx + GBIN_MAX + (size_t)k * BIGW;
+        const uint32_t nb = rec[3], chunks = (nb + BIG_CHUNK - 1) / BIG_CHUNK;
+        const uint32_t u0 = (blockIdx.x + gridDim.x - (97u * k) % gridDim.x) % gridDim.x;
+        for (uint32_t u = u0; u < chunks; u += gridDim.x) fn(rec, u);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gbig_count(GroupScratch g, uint32_t n)
+{
+    __shared__ uint32_t cnt[GBLK], other;
+    const uint32_t tile = (n + GBLK - 1) / GBLK;
+    for_each_big_chunk(g, [&](uint32_t *rec, uint32_t u) {
+        const uint32_t key = rec[1], start = rec[2], nb = rec[3];
+        cnt[threadIdx.x] = 0;
+        if (!threadIdx.x) other = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t v = 0; v < BIG_CHUNK / 256; ++v) {
+            const uint32_t j = u * BIG_CHUNK + v * 256 + threadIdx.x;
+            const bool live = j < nb;
+            const uint2 e = live ? g.gent[start + j] : make_uint2(0u, 0u);
+            const bool mine = live && e.y == key;
+            lds_inc(cnt, mine ? min(e.x / tile, GBLK - 1) : 0u, mine);
+            lds_inc(&other, 0u, live && !mine);
+        }
+        __syncthreads();
+        if (cnt[threadIdx.x]) atomicAdd(&rec[BIG_PCNT + threadIdx.x], cnt[threadIdx.x]);
+        if (!threadIdx.x && other) atomicAdd(&rec[5], other);
+        __syncthreads();
+    });
+}
+
+// a workgroup per record: a key with half of its bin or more becomes a split-key job
+__global__ void __launch_bounds__(256) k_gbig_plan(GroupScratch g, uint32_t n)
+{
+    __shared__ uint32_t wsum[17], jx;
+    const uint32_t nrec = g.gbx ? min(g.cursor[BIG_WORD], g.gbx_cap) : 0u;
+    if (blockIdx.x >= nrec) return;
+    uint32_t *rec = g.gbx + GBIN_MAX + (size_t)blockIdx.x * BIGW;
+    const uint32_t pc = rec[BIG_PCNT + threadIdx.x];
+    uint32_t c;
+    const uint32_t po = block_excl_scan(pc, wsum, c);
+    const uint32_t start = rec[2], nb = rec[3];
+    if (!threadIdx.x) {
+        jx = ~0u;
+        if (2 * c >= nb && c + rec[5] == nb) {                    // (the others fit before the sub-bins)
+            const uint32_t j = atomicAdd(&g.cursor[SJOB_WORD], 1u);
+            if (j < g.sjob_cap) jx = j;
+        }
+        rec[4] = c;
+        rec[6] = jx;
+        if (jx == ~0u) g.gbx[rec[0]] = 0;                         // (the bin stays whole)
+    }
+    __syncthreads();
+    if (jx == ~0u) return;
+    uint32_t *job = g.sjob + (size_t)jx * SJOB_WORDS;
+    rec[BIG_FILL + threadIdx.x] = po;
+    job[SJOB_PCNT + threadIdx.x] = pc;
+    job[SJOB_PCNT + 256 + threadIdx.x] = po;
+    if (!threadIdx.x) {
+        job[0] = rec[1];
+        job[1] = c;
+        job[2] = 2 * start;                                       // (the bin's region of `order`: the run first)
+        job[3] = c >= (g.flat ? NPOS : 2u) ? 1u : 0u;
+        job[4] = 4 * start + 2 * nb;                              // (the members: gbin's `mem` of the bin)
+        job[5] = (n + GBLK - 1) / GBLK;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gbig_place(GroupScratch g, uint32_t n)
+{
+    __shared__ uint32_t cnt[GBLK], base[GBLK], other, obase;
+    const uint32_t tile = (n + GBLK - 1) / GBLK;
+    for_each_big_chunk(g, [&](uint32_t *rec, uint32_t u) {
+        if (rec[6] == ~0u) return;                                // (block-uniform: not taken out)
+        const uint32_t key = rec[1], start = rec[2], nb = rec[3];
+        uint32_t *mem = reinterpret_cast<uint32_t *>(g.gbig + 2 * (size_t)start + nb);
+        uint2 *rest = reinterpret_cast<uint2 *>(g.gbig + 2 * (size_t)start);
+        uint2 es[BIG_CHUNK / 256];
+        cnt[threadIdx.x] = 0;
+        if (!threadIdx.x) other = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t v = 0; v < BIG_CHUNK / 256; ++v) {
+            const uint32_t j = u * BIG_CHUNK + v * 256 + threadIdx.x;
+            const bool live = j < nb;
+            es[v] = live ? g.gent[start + j] : make_uint2(0u, 0u);
+            const bool mine = live && es[v].y == key;
+            lds_inc(cnt, mine ? min(es[v].x / tile, GBLK - 1) : 0u, mine);
+            lds_inc(&other, 0u, live && !mine);
+        }
+        __syncthreads();
+        base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&rec[BIG_FILL + threadIdx.x], cnt[threadIdx.x]) : 0u;
+        cnt[threadIdx.x] = 0;
+        if (!threadIdx.x) {
+            obase = other ? atomicAdd(&rec[7], other) : 0u;
+            other = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t v = 0; v < BIG_CHUNK / 256; ++v) {
+            const uint32_t j = u * BIG_CHUNK + v * 256 + threadIdx.x;
+            const bool live = j < nb, mine = live && es[v].y == key;
+            const uint32_t t = mine ? min(es[v].x / tile, GBLK - 1) : 0u;
+            const uint32_t at = lds_inc(cnt, t, mine);
+            const uint32_t ro = lds_inc(&other, 0u, live && !mine);
+            if (mine) mem[base[t] + at] = es[v].x;
+            else if (live) rest[obase + ro] = es[v];
+        }
+        __syncthreads();
+    });
+}
+
 __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g, uint32_t n)
 {
     __shared__ GbinLds L;
-    const uint32_t nbins = 1u << g.gbits, b = blockIdx.x, m = nbins * GBLK;
-    const uint32_t start = g.gcnt[b * GBLK], end = b + 1 < nbins ? g.gcnt[(b + 1) * GBLK] : g.gcnt[m];
-    const uint32_t nb = end - start;
-    if (!nb) return;                                              // (block-uniform)
-    if (threadIdx.x == 0) L.fill = 0;
+    const uint32_t b = blockIdx.x;
+    uint32_t start, nb0;
+    gbin_range(g, b, start, nb0);
+    if (!nb0) return;                                             // (block-uniform)
+    // a big bin whose dominant key k_gbig_* took out: its other entries, packed at the front
+    // of its gbig region, after the key's run in `order` and its members in `mem`
+    const uint32_t bx = g.gbx ? g.gbx[b] : 0u;
+    const uint32_t *rec = bx ? g.gbx + GBIN_MAX + (size_t)(bx - 1) * BIGW : nullptr;
+    const uint32_t taken = rec ? rec[4] : 0u, nb = rec ? rec[5] : nb0;
+    const uint2 *src = rec ? reinterpret_cast<const uint2 *>(g.gbig + 2 * (size_t)start) : g.gent + start;
+    if (threadIdx.x == 0) { L.fill = rec ? taken + 1 : 0u; L.mused = taken; }
     if (threadIdx.x < 2) L.big[threadIdx.x] = 0;
     // composite {key low word, packet}: sorted, a group's members are contiguous and ascending
     if (nb <= LCAP) {
         for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
-            const uint2 e = g.gent[start + j];
+            const uint2 e = src[j];
             L.lv[j] = (unsigned long long)e.y << 32 | e.x;
         }
         __syncthreads();
-        gbin_lds_sort(L, nb);
-        gbin_emit(g, L, L.lv, nb, start);
+        if (nb) {
+            gbin_lds_sort(L, nb);
+            gbin_emit(g, L, L.lv, nb, start);
+        }
     } else {
         // a bin past LCAP: its entries by 8 more key bits into sub-bins (gbig: 2 words per
         // entry, the second half the split keys' member lists), sub-bins of up to LCAP
         // sorted in LDS a batch at a time, a larger one split key by key
-        unsigned long long *gv = g.gbig + 2 * (size_t)start;
-        uint32_t *mem = reinterpret_cast<uint32_t *>(gv + nb);
+        unsigned long long *gv = g.gbig + 2 * (size_t)start + (rec ? nb : 0u);   // (past the packed others)
+        uint32_t *mem = reinterpret_cast<uint32_t *>(g.gbig + 2 * (size_t)start + nb0);
         const uint32_t tile = (n + GBLK - 1) / GBLK;
         L.bcnt[threadIdx.x] = 0;
-        if (threadIdx.x == 0) L.mused = 0;
         __syncthreads();
         for (uint32_t j0 = 0; j0 < nb; j0 += GUNROLL * blockDim.x) {
             uint2 es[GUNROLL];
 #pragma unroll
             for (uint32_t u = 0; u < GUNROLL; ++u) {
                 const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
-                es[u] = j < nb ? g.gent[start + j] : make_uint2(0u, 0u);
+                es[u] = j < nb ? src[j] : make_uint2(0u, 0u);
             }
 #pragma unroll
             for (uint32_t u = 0; u < GUNROLL; ++u)
@@ -1908,7 +2091,7 @@ __global__ void __launch_bounds__(256) k_gbin_group(GroupScratch g, uint32_t n)
 #pragma unroll
             for (uint32_t u = 0; u < GUNROLL; ++u) {
                 const uint32_t j = j0 + u * blockDim.x + threadIdx.x;
-                es[u] = j < nb ? g.gent[start + j] : make_uint2(0u, 0u);
+                es[u] = j < nb ? src[j] : make_uint2(0u, 0u);
             }
 #pragma unroll
             for (uint32_t u = 0; u < GUNROLL; ++u) {
@@ -2003,6 +2186,10 @@ void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
     hipLaunchKernelGGL(k_gkey_hist, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
     launch_scan(g.gcnt, m, g.gcnt + m + 1, g.gcnt + m, false, s);
     hipLaunchKernelGGL(k_gkey_scatter, dim3(GBLK), dim3(1024), nb * 4, s, g, n);
+    hipLaunchKernelGGL(k_gbig_list, dim3((nb + 3) / 4), dim3(256), 0, s, g);   // (big bins: dominant keys out)
+    hipLaunchKernelGGL(k_gbig_count, dim3(512), dim3(256), 0, s, g, n);
+    hipLaunchKernelGGL(k_gbig_plan, dim3(g.gbx_cap), dim3(256), 0, s, g, n);
+    hipLaunchKernelGGL(k_gbig_place, dim3(512), dim3(256), 0, s, g, n);
     hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g, n);
     hipLaunchKernelGGL(k_gbin_tiles, dim3(1024), dim3(256), 0, s, g);   // (split keys: elephant pairs)
     hipLaunchKernelGGL(k_gbin_marks, dim3(8), dim3(256), 0, s, g);

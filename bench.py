@@ -80,7 +80,7 @@ def make_workload(name, n, rank, world, flows=1 << 24, zipf=None, ep_zipf=None):
         return synth.config3(n, n_flows=flows, seed=seed, shard=(rank, world) if world > 1 else None, zipf=zipf,
                              ep_zipf=ep_zipf)
     if name == "config5":
-        return synth.config5(n)
+        return synth.config5(n, ep_zipf=ep_zipf)
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -336,11 +336,12 @@ def main():
     ap.add_argument("--zipf", type=float, default=None,
                     help="configs 3/4: Zipf(a) flow popularity for the existing flows' packets (elephant flows)")
     ap.add_argument("--ct-local", type=int, default=None,
-                    help="configs 3/4: ConntrackLocal -- every endpoint its own CT4 map of this max_entries "
-                         "(ctmap.go:54: 64000) holding its flows' preloaded entries (synth.per_endpoint_ct)")
+                    help="configs 3/4/5: ConntrackLocal -- every endpoint its own CT4 map (config 5: CT4 and CT6) "
+                         "of this max_entries (ctmap.go:54: 64000) holding its flows' preloaded entries "
+                         "(synth.per_endpoint_ct)")
     ap.add_argument("--ep-zipf", type=float, default=None,
-                    help="configs 3/4: Zipf(a) popularity of the endpoints the preloaded flows belong to (with "
-                         "--ct-local: the busiest endpoints' maps are full)")
+                    help="configs 3/4: Zipf(a) popularity of the endpoints the preloaded flows belong to; config 5: "
+                         "of the flows' client endpoints (with --ct-local: the busiest endpoints' maps are full)")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend at N > 1 (nccl = RCCL)")
     ap.add_argument("--dump", default=None,
                     help="test hook: every rank writes <dir>/rank<r>.npz (its packets' address-pair keys, its "
@@ -375,11 +376,13 @@ def main():
     passes = args.warmup + args.steps + 1                          # + the accounting step after the timed ones
     t0 = time.time()
     w = make_workload(name, args.packets, rank, world, args.flows, args.zipf, args.ep_zipf)
-    per_ep = None
+    per_ep = per_ep6 = None
     if args.ct_local:
-        if name not in ("config3", "config4"):
-            raise SystemExit("--ct-local: configs 3 / 4")
+        if name not in ("config3", "config4", "config5"):
+            raise SystemExit("--ct-local: configs 3 / 4 / 5")
         per_ep = synth.per_endpoint_ct(w, args.ct_local)
+        if name == "config5":                                     # (CT4 and CT6 per endpoint, empty)
+            per_ep6 = synth.per_endpoint_ct(w, args.ct_local, "ct6")
     if stateful and per_ep is None:
         size_conntrack(name, w, passes)
         cts = [k for k in ("ct4", "ct6") if k in w.maps and (name != "config3" or k == "ct4")]
@@ -391,7 +394,7 @@ def main():
             if args.ct_max is not None:
                 w.maps[k].max_entries = args.ct_max
     log(f"[rank {rank}] generated {name}: {w.n} packets in {time.time() - t0:.1f}s")
-    ctx, maps = H.product_ctx(w, device=local, ct_per_ep=per_ep)
+    ctx, maps = H.product_ctx(w, device=local, ct_per_ep=per_ep, ct6_per_ep=per_ep6)
     log(f"[rank {rank}] tables compiled ({time.time() - t0:.1f}s)")
     metrics_t = torch.zeros(2048, dtype=torch.int64, device=device)
     ctx.metrics_attach(metrics_t)
@@ -418,8 +421,8 @@ def main():
             batches[v] = step_batch(name, w, v, base, where, device)
         log(f"[rank {rank}] {passes} step batches built on the device ({time.time() - t0:.1f}s)")
 
-    gc_maps = ([maps[k] for k in ("ct4", "ct6") if k in maps] if per_ep is None else list(maps["ct4_ep"])) \
-        if stateful else []
+    gc_maps = ([maps[k] for k in ("ct4", "ct6") if k in maps] if per_ep is None
+               else list(maps["ct4_ep"]) + list(maps.get("ct6_ep", []))) if stateful else []
     gc_deleted = [0]
 
     def now_of(v):
@@ -451,7 +454,7 @@ def main():
 
     def full_maps():
         """--ct-local: how many endpoint maps hold max_entries entries (syncs, untimed)"""
-        return sum(len(m) >= args.ct_local for m in maps["ct4_ep"])
+        return sum(len(m) >= args.ct_local for m in list(maps["ct4_ep"]) + list(maps.get("ct6_ep", [])))
 
     def slot_load():
         """live entries / slots of every device CT map (cv_ct_slots; syncs, untimed)"""
@@ -595,11 +598,13 @@ def main():
         }
         if stateful and per_ep is not None:
             line["config"]["ct_local"] = {
-                "maps": len(per_ep), "max_entries_per_map": args.ct_local, "ep_zipf": args.ep_zipf,
+                "maps": len(per_ep) + len(per_ep6 or []), "max_entries_per_map": args.ct_local,
+                "ep_zipf": args.ep_zipf,
                 "preloaded_entries": int(sum(len(s) for s in per_ep)),
                 "full_maps_first_last_timed_step": [full_first, full_last],
-                "how": "ConntrackLocal: every endpoint its own CT4 map (synth.per_endpoint_ct); launches next to a "
-                       "map's max_entries run admitted (one sorted segmented scan over all maps' walks)"}
+                "how": "ConntrackLocal: every endpoint its own CT4 map (config 5: and CT6 map; "
+                       "synth.per_endpoint_ct); launches next to a map's max_entries run admitted (one sorted "
+                       "segmented scan over all maps' walks)"}
         elif stateful:
             line["config"]["ct_max_entries"] = {k: int(w.maps[k].max_entries) for k in ("ct4", "ct6") if k in w.maps}
             # live entries / device slots at the first and the last timed step (a table is sized

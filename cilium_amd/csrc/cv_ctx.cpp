@@ -240,6 +240,8 @@ struct cv_ctx {
     size_t mt_eps = ~(size_t)0;
     DevBuf mt_live, mt_cap, mt_epmi4, mt_epmi6, mt_out;
     DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
+    DevBuf eam_buf, eam_keys, eam_snap;  // (many CT maps: per-slot intents + budgets, walk keys, the slot set)
+    Snap eam_snap_host{};
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -1832,6 +1834,168 @@ int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_
     return 0;
 }
 
+// Egress next to max_entries with any number of CT maps (ConntrackLocal: every endpoint
+// its own CT4 / CT6 map), exact.  As lxc_admitted, a pass runs the whole pipeline with
+// budgets and the budget scan tells whether it was the sequential run; here a packet has
+// two budgets -- its source program's creates go to its source endpoint's map, its local
+// delivery's to the destination's -- and every map's walk is one segment of a scan over
+// the (map, packet, slot) elements, sorted (launch_eam_*).  A pass that was not the
+// sequential run is undone without a copy of the maps: each CT slot the pass wrote was
+// saved before its first write (Snap: copy-on-first-write into a set sized for 8 written
+// slots per packet, cv_dev.hpp snap_slot), the live counts, the metrics, the policy values
+// and the event rings' counts were copied before the first pass.  Launches of at most
+// EAM_WINDOW packets; -EAGAIN (no fixed point, state restored) and -ENOMEM (no room for the
+// set, nothing ran) send the caller to planned launches.
+constexpr uint32_t EAM_WINDOW = 1u << 22;
+int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_t *src_ep, uint32_t ep0,
+                      const uint32_t *flow_hash, uint32_t now, const OutDev &oc, const std::vector<MapObj *> &cts,
+                      hipStream_t s)
+{
+    const char *mp = getenv("CV_EADM_MAX_PASSES");
+    const int MAX_PASSES = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
+    const uint32_t n = bc.n;
+    if (n > EAM_WINDOW) return -EINVAL;
+    int r = map_table(c, cts);
+    if (r) return r;
+    const uint32_t nm = (uint32_t)cts.size();
+    // the state besides the CT slots, copied once
+    struct Region { void *src; size_t bytes, off; };
+    std::vector<Region> regs;
+    size_t total = 0;
+    auto add = [&](void *src, size_t bytes) {
+        if (!src || !bytes) return;
+        regs.push_back(Region{src, bytes, total});
+        total += (bytes + 255) & ~(size_t)255;
+    };
+    add(c->metrics, METRICS_WORDS * 8);
+    std::set<const void *> seen;
+    for (auto &e : c->eps) {
+        MapObj *m = get(c, e.policy);
+        if (m && seen.insert(m->pol.vals.p).second) {
+            add(m->pol.vals.p, m->pol.vals.n);
+            add(m->pol.aux.p, m->pol.aux.n);
+        }
+    }
+    add(c->notify_count, 4);
+    add(c->trace_count, 4);
+    uint64_t scap = 1024;
+    while (scap < (uint64_t)n * 10) scap <<= 1;                   // (<= 8 written slots per packet, load <= 0.8)
+    size_t sort_bytes = 0;
+    if (sort_keys64(nullptr, &sort_bytes, nullptr, nullptr, 2 * n, 48, nullptr)) return -EIO;
+    const size_t nb = (size_t)n, live_off = ((10 * nb + 255) & ~(size_t)255);
+    const size_t buf_bytes = live_off + (size_t)nm * 8 + 4096 * 12 + 256;
+    const size_t snap_bytes = scap * 8 + scap * SNAP_U4 * 16;
+    if (c->eam_snap.n < snap_bytes || c->eadm_save.n < total) {
+        size_t fr = 0, all = 0;                                   // (a set that would crowd the device out:
+        if (hipMemGetInfo(&fr, &all) != hipSuccess || snap_bytes + total > fr / 2) return -ENOMEM;   // planned)
+    }
+    if ((c->eadm_save.n < total && c->eadm_save.alloc(total)) ||
+        (c->eam_buf.n < buf_bytes && c->eam_buf.alloc(buf_bytes)) ||
+        (c->eam_keys.n < (size_t)n * 32 + sort_bytes && c->eam_keys.alloc((size_t)n * 32 + sort_bytes)) ||
+        (c->eam_snap.n < snap_bytes && c->eam_snap.alloc(snap_bytes)) ||
+        (c->eadm_buf.n < 128 && c->eadm_buf.alloc(128)))
+        return -ENOMEM;
+    uint8_t *save = c->eadm_save.as<uint8_t>();
+    for (const Region &g : regs)
+        if (hipMemcpyAsync(save + g.off, g.src, g.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return -EIO;
+    uint8_t *buf = c->eam_buf.as<uint8_t>();
+    uint8_t *intent = buf, *intent2 = buf + nb, *left = buf + 2 * nb, *left2 = buf + 3 * nb;
+    uint8_t *bud[2] = {buf + 4 * nb, buf + 6 * nb};               // (2n each: slot 0, then slot 1)
+    uint16_t *dst = reinterpret_cast<uint16_t *>(buf + 8 * nb);  // (per packet the delivery's endpoint)
+    unsigned long long *live0 = reinterpret_cast<unsigned long long *>(buf + live_off);
+    EAdmitM a{};
+    a.n = n;
+    a.nmaps = nm;
+    a.intent = intent;
+    a.intent2 = intent2;
+    a.src_ep = src_ep;
+    a.ep0 = ep0;
+    a.ep_mi4 = c->mt_epmi4.as<const uint16_t>();
+    a.ep_mi6 = c->mt_epmi6.as<const uint16_t>();
+    a.n_eps = (uint32_t)c->eps.size();
+    a.live0 = live0;
+    a.cap = c->mt_cap.as<const unsigned long long>();
+    a.keys = c->eam_keys.as<unsigned long long>();
+    a.keys_sorted = a.keys + 2 * nb;
+    a.sort_tmp = a.keys + 4 * nb;
+    a.sort_bytes = sort_bytes;
+    a.tsum = reinterpret_cast<uint32_t *>(buf + live_off + (size_t)nm * 8);
+    a.cnt = c->eadm_buf.as<uint32_t>();
+    a.dst_ep = dst;
+    Snap sn{};
+    sn.keys = c->eam_snap.as<unsigned long long>();
+    sn.data = reinterpret_cast<uint4 *>(sn.keys + scap);
+    sn.mask = (uint32_t)(scap - 1);
+    sn.err = a.cnt + 4;
+    c->eam_snap_host = sn;                                        // (the async copy's source outlives the call)
+    if (hipMemcpyAsync(a.cnt + 8, &c->eam_snap_host, sizeof(Snap), hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+    if ((r = launch_gather_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s))) return r;
+    a.next = bud[0];
+    a.next2 = bud[0] + nb;
+    if ((r = launch_eam_first(a, s))) return r;
+    const bool stats = getenv("CV_ADMIT_STATS") != nullptr;
+    int cur = 0, pass = 0;
+    for (;; ++pass) {
+        if (hipMemsetAsync(sn.keys, 0, scap * 8, s) != hipSuccess || hipMemsetAsync(a.cnt, 0, 32, s) != hipSuccess)
+            return -EIO;
+        DpParams pp = p;
+        pp.budget = bud[cur];
+        pp.eg_left = left;
+        pp.eg_intent = intent;
+        pp.eg_left2 = left2;
+        pp.eg_intent2 = intent2;
+        pp.eg_dst = dst;
+        pp.snap = reinterpret_cast<const Snap *>(a.cnt + 8);
+        GroupScratch gs = next_groups(c, 3, s);
+        gs.gbits = gbin_bits(n);
+        if ((r = launch_lxc_egress(pp, bc, src_ep, ep0, flow_hash, now, oc, gs, s))) return r;
+        a.used = bud[cur];
+        a.used2 = bud[cur] + nb;
+        a.next = bud[cur ^ 1];
+        a.next2 = bud[cur ^ 1] + nb;
+        if (hipMemcpyAsync(a.next, a.used, 2 * nb, hipMemcpyDeviceToDevice, s) != hipSuccess) return -EIO;
+        if ((r = launch_eam_keys(a, s))) return r;
+        uint32_t w[8] = {};
+        hipError_t e = hipMemcpyAsync(w, a.cnt, 32, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[cv] egress admission pass %d: %s\n", pass, hipGetErrorString(e));
+            return -EIO;
+        }
+        if (w[2]) {
+            fprintf(stderr, "[cv] egress admission pass %d: a create in a CT map outside the launch's\n", pass);
+            return -EPROTO;
+        }
+        if ((r = launch_eam_walks(a, w[0], s))) return r;
+        e = hipMemcpyAsync(w, a.cnt, 32, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return -EIO;
+        if (!w[1]) break;                                         // the sequential run
+        if (w[4]) {                                               // (cannot be undone: never with <= 8 slots per packet)
+            fprintf(stderr, "[cv] egress admission pass %d: slot set full (%llu entries)\n", pass,
+                    (unsigned long long)scap);
+            return -EIO;
+        }
+        if ((r = launch_snap_restore(sn, s)) ||                   // back to the state before the window
+            (r = launch_scatter_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s)))
+            return r;
+        for (const Region &g : regs)
+            if (hipMemcpyAsync(g.src, save + g.off, g.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return -EIO;
+        if (pass + 1 == MAX_PASSES) {
+            fprintf(stderr, "[cv] egress admission: no fixed point after %d passes (%u packets, %u maps)\n",
+                    MAX_PASSES, n, nm);
+            return -EAGAIN;
+        }
+        cur ^= 1;
+    }
+    for (MapObj *m : cts) {
+        m->live_upper = m->cap;                                   // (re-read when the next launch plans)
+        m->gen++;
+    }
+    if (stats) fprintf(stderr, "[cv admit] egress: %u packets, %d passes, %u maps\n", n, pass + 1, nm);
+    return 0;
+}
+
 // live policy counters of one key from HBM (device-authoritative)
 void policy_counters(MapObj *mo, const uint8_t *key, uint8_t *val)
 {
@@ -2336,22 +2500,29 @@ int lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep
     }
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
-    const bool admissible = egress_admissible(cts) && !getenv("CV_EGRESS_GUARDED");
+    const bool guarded = getenv("CV_EGRESS_GUARDED") != nullptr;   // (tests: the planned launches)
+    const bool one_map = egress_admissible(cts);
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         // a launch whose creates (at most 7 per packet) fit runs at full width; one that may
-        // reach max_entries runs admitted (lxc_admitted), or, with more CT maps than that
-        // handles, in one-packet guarded launches.  Short of room for 7 n creates, a launch
-        // of room / 7 packets (>= 2^20) surely fits and runs without the admission passes.
+        // reach max_entries runs admitted: lxc_admitted with one CT map per family,
+        // lxc_admitted_maps (windows of EAM_WINDOW packets) with more.  Short of room for
+        // 7 n creates, a launch of room / 7 packets (>= 2^20) surely fits and runs without
+        // the admission passes.
         n = std::min(c->chunk, b->n - off);
         const uint32_t fit_n = ct_fit_count(c, cts, n, 7);
         if (fit_n < n && fit_n >= std::min<uint32_t>(n, SPLIT_MIN)) n = fit_n;
-        const bool fits = ct_fits(c, cts, n, 7);
-        if (!fits && !admissible) n = ct_plan(c, cts, n, 7, (hipStream_t)stream, &p.ct_guard);
+        bool fits = ct_fits(c, cts, n, 7);
+        if (!fits && !one_map && n > EAM_WINDOW) {
+            n = EAM_WINDOW;
+            fits = ct_fits(c, cts, n, 7);
+        }
+        if (!fits && guarded) n = ct_plan(c, cts, n, 7, (hipStream_t)stream, &p.ct_guard);
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
-        if (!fits && admissible) {
-            r = lxc_admitted(c, p, bc, src_ep ? src_ep + off : nullptr, ep0, flow_hash ? flow_hash + off : nullptr,
-                             now, oc(off), cts, (hipStream_t)stream);
+        if (!fits && !guarded) {
+            r = (one_map ? lxc_admitted : lxc_admitted_maps)(c, p, bc, src_ep ? src_ep + off : nullptr, ep0,
+                                                             flow_hash ? flow_hash + off : nullptr, now, oc(off), cts,
+                                                             (hipStream_t)stream);
             // no fixed point (the state is back as before the chunk), or no room for the
             // state's copy (nothing ran): the chunk again in planned launches, one guarded
             // packet at a time next to the limit

@@ -445,6 +445,7 @@ struct Acct {
     uint32_t budget = ~0u;     // admission windows: creates of new CT entries that may still succeed
     uint32_t tried = 0;        // admission: creates of new entries tried (a failing one included)
     uint32_t killed = 0;       // admission: entries deleted
+    const Snap *snap = nullptr;  // egress admission with many CT maps: slots saved before their first write
 };
 
 // lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
@@ -1042,6 +1043,46 @@ __device__ __forceinline__ void ct_count(const HashTable &t, int64_t slot, CtE &
     e.w[k] = lo;
 }
 
+// The slot as it was before this pass's first write to it (Snap, cv_dp.hpp): `fresh` = the
+// slot was just claimed for a new key (it held nothing: restored as a dead slot, which
+// every probe chain passes).  One CAS on the set; a slot already in it keeps its first
+// copy (a slot deleted and claimed again within the pass goes back to the entry it held).
+template <class S>
+__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh)
+{
+    const uint64_t b = (uint64_t)slot / S::SPB;
+    const uint32_t s = (uint32_t)((uint64_t)slot % S::SPB);
+    const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
+    const CV_G uint32_t *cold = ct_cold<S>(t, slot);
+    const unsigned long long id = (unsigned long long)(uintptr_t)cold;
+    uint32_t h = (uint32_t)(mix64(id) >> 20) & sn.mask;
+#pragma unroll 1
+    for (uint32_t k = 0; k <= sn.mask; ++k, h = (h + 1) & sn.mask) {
+        const unsigned long long cur = atomicCAS(sn.keys + h, 0ull, id);
+        if (cur == id) return;                                    // (saved before)
+        if (cur) continue;
+        uint32_t *d = reinterpret_cast<uint32_t *>(sn.data + (size_t)h * SNAP_U4);
+        const uint32_t tag = fresh ? TAG_DEAD : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+        const unsigned long long ba = (unsigned long long)(uintptr_t)bw;
+        d[0] = (uint32_t)ba;
+        d[1] = (uint32_t)(ba >> 32);
+        d[2] = s | tag << 8 | (uint32_t)S::KS << 16;
+        const CV_G uint32_t *kw = bw + S::KEY0 + s * S::KS;
+#pragma unroll 1
+        for (int j = 0; j < S::KS; ++j) d[4 + j] = fresh ? 0u : kw[j];
+#pragma unroll 1
+        for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : cold[j];
+        return;
+    }
+    atomicOr(sn.err, 1u);
+}
+
+template <class S>
+__device__ __forceinline__ void snap_before(const Acct &a, const HashTable &t, int64_t slot, bool fresh = false)
+{
+    if (a.snap) snap_slot<S>(*a.snap, t, slot, fresh);
+}
+
 // __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)
 __device__ __forceinline__ bool ct_timeout_raw(CtE &e, uint32_t lifetime, int dir, uint32_t seen, uint32_t now)
 {
@@ -1155,6 +1196,7 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
                                        uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a, bool *mon)
 {
     a.nu++;
+    snap_before<S>(a, ct, slot);
     CtE e;
     ct_load_hot<S>(ct, slot, e);
     if (st) {
@@ -1374,6 +1416,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
     bool created;
     const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent);
     if (s < 0) return false;
+    snap_before<typename T::Spec>(a, ct, s, created);
     if (created) ct_live_add(ct, a, guard, 1);
     ct_store<typename T::Spec>(ct, s, e, created);
     return true;
@@ -1383,6 +1426,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
 template <class S>
 __device__ __forceinline__ void ct_kill(const HashTable &ct, int64_t slot, Acct &a, bool guard)
 {
+    snap_before<S>(a, ct, slot);
     dev_kill<S>(ct, slot);
     ct_live_add(ct, a, guard, -1);
     a.nu++;

@@ -43,6 +43,20 @@ struct EpHot {
 static_assert(sizeof(EpHot) == 64, "one line per endpoint");
 constexpr uint32_t EPH_CT_ID = 0x3FFFFFFFu, EPH_V4 = 0x80000000u;
 
+// Copy-on-first-write of conntrack slots (egress admission with many CT maps, cv_ctx.cpp
+// lxc_admitted_maps): before a pass's first write to a CT slot, the slot as it was -- its
+// tag byte, key and hot words, side slot -- goes into an open-addressing set keyed by the
+// side slot's address; a pass that was not the sequential run is undone from the set
+// (k_snap_restore) instead of from a copy of every map.
+struct Snap {
+    unsigned long long *keys;  // per entry: the slot's side-slot address, 0 = free
+    uint4 *data;               // per entry SNAP_U4 x 16 B: {bucket address, s | tag << 8 | KS << 16, 0,
+                               // the slot's KS bucket words from KEY0, the side slot's 8 words at 24}
+    uint32_t mask;             // entries - 1
+    uint32_t *err;             // set when the set is full (the pass cannot be undone: loud failure)
+};
+constexpr uint32_t SNAP_U4 = 8;
+
 struct DpParams {              // by value as the kernel argument
     uint32_t flags;
     uint32_t n_eps;
@@ -81,6 +95,14 @@ struct DpParams {              // by value as the kernel argument
     // stage, and its intent {creates tried (3 bits), deletes << 3, CT map (0 CT4, 1 CT6) << 4}
     uint8_t *eg_left;
     uint8_t *eg_intent;
+    // many CT maps (lxc_admitted_maps): the local delivery's creates and delete go to the
+    // destination's map, with a budget and an intent of their own ({tried, deletes << 3}),
+    // and its endpoint; null with one map per family (one budget per packet)
+    uint8_t *eg_left2;
+    uint8_t *eg_intent2;
+    uint16_t *eg_dst;
+    const Snap *snap;          // in device memory (not the kernel argument: its address would copy the
+                               // parameters to scratch); null: off
     // every endpoint on one policy map and one CT4 map with LXC_IPV4 set (cv_ctx.cpp): the
     // netdev stages take that line from here instead of a per-packet EpHot read
     uint32_t uni4_on, uni6_on;
@@ -142,6 +164,35 @@ struct EAdmit {
     uint32_t *flag;                    // set when a packet's creates differ from the sequential run's
     uint32_t n;
 };
+
+// Exact egress admission with any number of CT maps (lxc_admitted_maps): a packet's
+// elements are its source program's creates and deletes (slot 0, the source endpoint's
+// map) and its local delivery's (slot 1, the destination's map), keyed map << 25 |
+// packet << 1 | slot and sorted, each map's walk one segment of the (sum, prefix
+// minimum) scan; the check and the next budgets per element as EAdmit's per packet
+struct EAdmitM {
+    const uint8_t *intent, *intent2;   // per packet (DpParams::eg_intent / eg_intent2)
+    const uint8_t *used, *used2;       // the budgets the pass ran with
+    uint8_t *next, *next2;             // the next pass's budgets
+    const uint16_t *src_ep;            // per packet the source endpoint, or null: ep0
+    uint32_t ep0;
+    const uint16_t *dst_ep;            // per packet the delivery's endpoint (DpParams::eg_dst)
+    const uint16_t *ep_mi4, *ep_mi6;   // per endpoint its CT4 / CT6 map's index (ADMIT_NO_MAP: none)
+    uint32_t n_eps;
+    const unsigned long long *live0;   // per map its live count as the window started
+    const unsigned long long *cap;     // per map max_entries
+    unsigned long long *keys, *keys_sorted;
+    void *sort_tmp;
+    size_t sort_bytes;
+    uint32_t *tsum;
+    uint32_t *cnt;                     // [0] elements, [1] not the sequential run, [2] a bad map index
+    uint32_t n, nmaps;
+};
+int launch_eam_first(const EAdmitM &a, hipStream_t s);     // first-pass budgets: 0 in a full source map, else 7
+int launch_eam_keys(const EAdmitM &a, hipStream_t s);      // the elements -> keys, cnt[0] their number
+int launch_eam_walks(const EAdmitM &a, uint32_t K, hipStream_t s);   // sort + scan: cnt[1], next budgets
+int launch_snap_restore(const Snap &sn, hipStream_t s);
+int launch_scatter_u64(unsigned long long *const *ptrs, const unsigned long long *in, uint32_t n, hipStream_t s);
 
 struct BatchDev {
     const uint8_t *frames;

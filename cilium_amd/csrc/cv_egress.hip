@@ -79,24 +79,34 @@ struct EgOut {                  // per-packet results on the way to the outputs
 // budget left from p.eg_left, hands back what it did not use, and adds to the packet's
 // intent byte the creates it tried (a failing one included: the reference's failing
 // map_update_elem ends the packet) and the deletes it made.  `flush` hands over before
-// an inline delivery of the same packet.
+// an inline delivery of the same packet.  With many CT maps (p.eg_left2) the local
+// delivery (slot 1) draws on a budget of its own -- its creates and delete go to the
+// destination's map -- and records the destination endpoint (dep); every stage saves a
+// CT slot before its first write in the pass (p.snap).
 struct EgAdm {
     const DpParams &p;
     uint32_t i;
     Acct &a;
     bool on;
-    __device__ EgAdm(const DpParams &pp, uint32_t ii, Acct &aa, bool live) : p(pp), i(ii), a(aa), on(live && pp.eg_left)
+    uint8_t *left, *intent;
+    __device__ EgAdm(const DpParams &pp, uint32_t ii, Acct &aa, bool live, int slot = 0, uint32_t dep = 0)
+        : p(pp), i(ii), a(aa), on(live && pp.eg_left)
     {
+        const bool two = slot && pp.eg_left2;
+        left = two ? pp.eg_left2 : pp.eg_left;
+        intent = two ? pp.eg_intent2 : pp.eg_intent;
         if (on) {
-            a.budget = p.eg_left[i];
+            a.budget = left[i];
             a.tried = a.killed = 0;
+            a.snap = p.snap;
+            if (two) p.eg_dst[i] = (uint16_t)dep;
         }
     }
     __device__ void flush()
     {
         if (!on) return;
-        p.eg_left[i] = (uint8_t)a.budget;
-        p.eg_intent[i] = (uint8_t)(p.eg_intent[i] + a.tried + (a.killed << 3));
+        left[i] = (uint8_t)a.budget;
+        intent[i] = (uint8_t)(intent[i] + a.tried + (a.killed << 3));
         on = false;
     }
     __device__ ~EgAdm() { flush(); }
@@ -424,6 +434,11 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         if (p.eg_left) {                                          // admission: this pass's budget, the intent's map
             p.eg_left[i] = stage == STAGE_DONE ? 0u : p.budget[i];
             p.eg_intent[i] = stage == STAGE_DONE ? 0u : (egl[0] & EG_V6) ? 16u : 0u;
+            if (p.eg_left2) {                                     // (the delivery's: budgets after the first pass's)
+                p.eg_left2[i] = stage == STAGE_DONE ? 0u : p.budget[b.n + i];
+                p.eg_intent2[i] = 0;
+                p.eg_dst[i] = 0xFFFFu;
+            }
         }
         if (!full && stage == STAGE_LB) {
 #pragma unroll
@@ -497,6 +512,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         const int64_t s2 = dev_find<Ct4Spec, EGF>(ep.ct4, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
+            snap_before<Ct4Spec>(a, ep.ct4, s2);
             ct_load_hot<Ct4Spec>(ep.ct4, s2, e);                  // (w10: a hot word)
             const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
@@ -604,6 +620,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         const int64_t s2 = dev_find<Ct6Spec, EGF>(ep.ct6, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
+            snap_before<Ct6Spec>(a, ep.ct6, s2);
             ct_load_hot<Ct6Spec>(ep.ct6, s2, e);
             const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
@@ -1371,7 +1388,7 @@ __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &
     }
     Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
     Acct a{(d1.y >> 16) & 0xFFu, d1.y >> 24, m.pc};
-    EgAdm adm(p, i, a, live);
+    EgAdm adm(p, i, a, live, 1, d1.z & 0xFFFFu);
     EgOut res{TC_ACT_OK, 0, d2.y, (uint8_t)(d1.z >> 16), 0};
     if (live) {
         m.pkt = b.base + i;
@@ -1420,7 +1437,7 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     s.h.c2a = unchk2((d2.w >> 6) & 3u);
     s.h.c2b = unchk2((d2.w >> 8) & 3u);
     Acct a{(d2.w >> 16) & 0xFFu, d2.w >> 24, m.pc};
-    EgAdm adm(p, i, a, live);
+    EgAdm adm(p, i, a, live, 1, d3.x & 0xFFFFu);
     EgOut res{TC_ACT_OK, 0, d3.w, (uint8_t)(d3.x >> 16), 0};
     if (live) {
         m.pkt = b.base + i;
@@ -1458,8 +1475,18 @@ __device__ __forceinline__ void for_each_wave(uint32_t total, F &&fn)
     }
 }
 
+// Occupancy of the egress conntrack stage: left alone the compiler spends 177 VGPRs
+// (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
+// capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
+// 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
+#ifndef CV_EG_WAVES
+#define CV_EG_WAVES 4
+#endif
+#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WAVES, 8)))
+
 template <bool V6, bool EV>
-__global__ void __launch_bounds__(BLOCK) k_egress_deliver(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
+__global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_deliver(DpParams p, BatchDev b, uint32_t now, OutDev o,
+                                                                     GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
@@ -1481,14 +1508,6 @@ __global__ void __launch_bounds__(BLOCK) k_egress_deliver(DpParams p, BatchDev b
     pol_cache_flush(pc);
 }
 
-// Occupancy of the egress conntrack stage: left alone the compiler spends 177 VGPRs
-// (2 waves/SIMD) on a lane whose time goes to ~15-20 dependent memory round trips;
-// capping it at 4 waves/SIMD (<= 128 VGPRs) hides more of that latency: config 5
-// 880 -> 971 Mpps (A/B on the box: 3 waves 958, 5 waves 809)
-#ifndef CV_EG_WAVES
-#define CV_EG_WAVES 4
-#endif
-#define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WAVES, 8)))
 
 template <bool V6, bool EV, bool INL>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g,

@@ -3282,6 +3282,254 @@ int launch_egress_admission(const EAdmit &a, hipStream_t s)
     return launch_status(__func__);
 }
 
+// ------------------------------------------------------------------ egress admission, many CT maps
+// (cv_ctx.cpp lxc_admitted_maps; EAdmitM in cv_dp.hpp).  A packet's slot-0 element is its
+// source program's creates and delete in its source endpoint's map, its slot-1 element
+// its local delivery's in the destination's map; per map the elements in packet order
+// (slot 0 before slot 1 of one packet) are a walk of (d - t, t ? -t : d) steps, as one CT
+// map's packets are in the one-budget form above.
+__device__ __forceinline__ uint32_t eam_map(const EAdmitM &a, uint32_t j, uint32_t slot)
+{
+    const uint32_t f = (a.intent[j] >> 4) & 1u;
+    const uint32_t e = slot ? a.dst_ep[j] : a.src_ep ? a.src_ep[j] : a.ep0;
+    return e < a.n_eps ? (f ? a.ep_mi6 : a.ep_mi4)[e] : ADMIT_NO_MAP;
+}
+
+// first pass: 7 creates per element, none in a source map that is full
+__global__ void __launch_bounds__(BLOCK) k_eam_first(EAdmitM a)
+{
+    for (uint32_t j = blockIdx.x * BLOCK + threadIdx.x; j < a.n; j += gridDim.x * BLOCK) {
+        const uint32_t e = a.src_ep ? a.src_ep[j] : a.ep0;
+        uint32_t mi4 = e < a.n_eps ? a.ep_mi4[e] : ADMIT_NO_MAP, mi6 = e < a.n_eps ? a.ep_mi6[e] : ADMIT_NO_MAP;
+        const bool room4 = mi4 < a.nmaps && a.live0[mi4] < a.cap[mi4];
+        const bool room6 = mi6 < a.nmaps && a.live0[mi6] < a.cap[mi6];
+        // (the family is not known before the front: room in either map gives 7, the
+        // check corrects a guess that was too generous)
+        a.next[j] = room4 || room6 ? 7u : 0u;
+        a.next2[j] = 7u;
+    }
+}
+
+// the elements from their intents: map << 25 | packet << 1 | slot, appended in any order
+// (block-aggregated allocation, as k_adm_keys)
+__global__ void __launch_bounds__(BLOCK) k_eam_keys(EAdmitM a)
+{
+    __shared__ uint32_t wsum[17], base_s;
+    const uint32_t per = BLOCK * ADM_KPT;
+    for (uint32_t b0 = blockIdx.x * per; b0 < a.n; b0 += gridDim.x * per) {   // (block-uniform)
+        const uint32_t j0 = b0 + threadIdx.x * ADM_KPT;
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < ADM_KPT; ++u) {
+            const uint32_t j = j0 + u;
+            if (j < a.n) mine += ((a.intent[j] & 15u) ? 1u : 0u) + ((a.intent2[j] & 15u) ? 1u : 0u);
+        }
+        uint32_t total;
+        uint32_t at = block_excl_scan(mine, wsum, total);
+        if (threadIdx.x == 0) base_s = total ? atomicAdd(a.cnt, total) : 0u;
+        __syncthreads();
+        at += base_s;
+#pragma unroll
+        for (uint32_t u = 0; u < ADM_KPT; ++u) {
+            const uint32_t j = j0 + u;
+            if (j >= a.n) continue;
+            for (uint32_t sl = 0; sl < 2; ++sl) {
+                if (!((sl ? a.intent2 : a.intent)[j] & 15u)) continue;
+                uint32_t mi = eam_map(a, j, sl);
+                if (mi >= a.nmaps) {                              // (a create in a map not in the list)
+                    atomicOr(a.cnt + 2, 1u);
+                    mi = a.nmaps;                                 // (sorted past every map, never applied)
+                }
+                a.keys[at++] = (unsigned long long)mi << 25 | (unsigned long long)j << 1 | sl;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint32_t eam_key_map(unsigned long long k) { return (uint32_t)(k >> 25) & 0xFFFFu; }
+
+__device__ __forceinline__ SegSM eam_elem(const EAdmitM &a, uint32_t L, uint32_t q, uint32_t &map, uint32_t &pkt,
+                                          uint32_t &slot)
+{
+    map = KEY_NONE;
+    pkt = slot = 0;
+    if (q >= L) return SEG_ID;
+    const unsigned long long k = a.keys_sorted[q];
+    map = eam_key_map(k);
+    pkt = (uint32_t)(k >> 1) & 0xFFFFFFu;
+    slot = (uint32_t)k & 1u;
+    if (map >= a.nmaps || pkt >= a.n) {
+        map = KEY_NONE;
+        return SEG_ID;
+    }
+    const uint32_t v = (slot ? a.intent2 : a.intent)[pkt];
+    const int32_t A = (int32_t)(v & 7u), D = (int32_t)((v >> 3) & 1u);
+    const int32_t f = q == 0 || eam_key_map(a.keys_sorted[q - 1]) != map;
+    return SegSM{f, D - A, A ? -A : D};
+}
+
+__global__ void __launch_bounds__(1024) k_eam_tiles(EAdmitM a, uint32_t L)
+{
+    __shared__ SegSM lds[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    SegSM t = SEG_ID;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t m, x, sl;
+        t = seg_comb(t, eam_elem(a, L, j + k, m, x, sl));
+    }
+    SegSM tot;
+    block_excl_seg(t, lds, &tot);
+    if (threadIdx.x == 0) reinterpret_cast<SegSM *>(a.tsum)[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(1024) k_eam_top(EAdmitM a, uint32_t tiles)
+{
+    __shared__ SegSM lds[17];
+    SegSM *agg = reinterpret_cast<SegSM *>(a.tsum);
+    SegSM v[4], t = SEG_ID;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t q = threadIdx.x * 4 + k;
+        v[k] = q < tiles ? agg[q] : SEG_ID;
+        t = seg_comb(t, v[k]);
+    }
+    SegSM e = block_excl_seg(t, lds, nullptr);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t q = threadIdx.x * 4 + k;
+        if (q < tiles) agg[q] = e;
+        e = seg_comb(e, v[k]);
+    }
+}
+
+// per element the room before it, R = r0 + S - min(0, r0 + M): the pass was the sequential
+// run iff min(t, b) = min(t, R) for every element (t its creates, b its budget); the next
+// budget min(7, R)
+__global__ void __launch_bounds__(1024) k_eam_apply(EAdmitM a, uint32_t L)
+{
+    __shared__ SegSM lds[17];
+    const uint32_t j = blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+    uint32_t map[4], pkt[4], slot[4];
+    SegSM e[4], t = SEG_ID;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        e[k] = eam_elem(a, L, j + k, map[k], pkt[k], slot[k]);
+        t = seg_comb(t, e[k]);
+    }
+    SegSM P = seg_comb(reinterpret_cast<const SegSM *>(a.tsum)[blockIdx.x], block_excl_seg(t, lds, nullptr));
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (map[k] == KEY_NONE) continue;
+        if (e[k].f) P = SEG_ID;                                   // (the map's first element)
+        const uint32_t v = (slot[k] ? a.intent2 : a.intent)[pkt[k]], A = v & 7u;
+        const unsigned long long live = a.live0[map[k]];
+        const long long r0 = live < a.cap[map[k]] ? (long long)(a.cap[map[k]] - live) : 0;
+        const long long lowest = r0 + P.m < 0 ? r0 + P.m : 0;
+        const long long R = r0 + P.s - lowest;
+        const uint32_t b = (slot[k] ? a.used2 : a.used)[pkt[k]];
+        bad |= (uint32_t)(R < (long long)A ? R : (long long)A) != (A < b ? A : b);
+        (slot[k] ? a.next2 : a.next)[pkt[k]] = (uint8_t)(R < 7 ? R : 7);
+        P = seg_comb(P, SegSM{0, e[k].s, e[k].m});
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(a.cnt + 1, 1u);
+}
+
+int launch_eam_first(const EAdmitM &a, hipStream_t s)
+{
+    if (!a.n) return 0;
+    const uint32_t g = (a.n + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(k_eam_first, dim3(g < 2048 ? g : 2048), dim3(BLOCK), 0, s, a);
+    return launch_status(__func__);
+}
+
+int launch_eam_keys(const EAdmitM &a, hipStream_t s)
+{
+    if (a.nmaps >= KEY_NONE || a.n > MAX_CHUNK) return -EINVAL;
+    (void)hipMemsetAsync(a.cnt, 0, 12, s);
+    if (!a.n) return 0;
+    const uint32_t per = BLOCK * ADM_KPT, g = (a.n + per - 1) / per;
+    hipLaunchKernelGGL(k_eam_keys, dim3(g < 2048 ? g : 2048), dim3(BLOCK), 0, s, a);
+    return launch_status(__func__);
+}
+
+// K elements (cnt[0], read by the host): sort, tile aggregates, their scan, the check and
+// the next budgets (an element-less slot keeps the budget it ran with: the caller copies
+// used -> next first)
+int launch_eam_walks(const EAdmitM &a, uint32_t K, hipStream_t s)
+{
+    const uint32_t tiles = (K + SCAN_TILE - 1) / SCAN_TILE;
+    if (tiles > 4096 || K > 2 * a.n) return -EINVAL;
+    if (!K) return 0;
+    int bits = 25;                                                // packet and slot bits, then the map index's
+    while ((1u << (bits - 25)) <= a.nmaps) ++bits;                // (nmaps itself: the corrupt elements)
+    size_t bytes = a.sort_bytes;
+    if (int r = sort_keys64(a.sort_tmp, &bytes, a.keys, a.keys_sorted, K, bits, s)) return r;
+    hipLaunchKernelGGL(k_eam_tiles, dim3(tiles), dim3(1024), 0, s, a, K);
+    hipLaunchKernelGGL(k_eam_top, dim3(1), dim3(1024), 0, s, a, tiles);
+    hipLaunchKernelGGL(k_eam_apply, dim3(tiles), dim3(1024), 0, s, a, K);
+    return launch_status(__func__);
+}
+
+// A pass undone (Snap, cv_dp.hpp): every saved slot back as it was -- its bucket words,
+// side slot and tag byte (a CAS on the tag word, which other slots of the bucket share)
+__global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
+{
+    for (uint32_t h = blockIdx.x * BLOCK + threadIdx.x; h <= sn.mask; h += gridDim.x * BLOCK) {
+        const unsigned long long id = sn.keys[h];
+        if (!id) continue;
+        const uint4 *d = sn.data + (size_t)h * SNAP_U4;
+        const uint4 h0 = d[0];
+        uint32_t *bw = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)h0.y << 32 | h0.x));
+        const uint32_t s = h0.z & 0xFFu, tag = (h0.z >> 8) & 0xFFu, ks = (h0.z >> 16) & 0xFFu;
+        if (ks > 20) continue;                                    // (not a CT slot record)
+        uint32_t w[20];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint4 u = d[1 + q];
+            w[4 * q] = u.x; w[4 * q + 1] = u.y; w[4 * q + 2] = u.z; w[4 * q + 3] = u.w;
+        }
+        uint32_t *kw = bw + 2 + s * ks;                           // (KEY0 = 2 for both CT specs)
+        for (uint32_t j = 0; j < ks; ++j) kw[j] = w[j];
+        uint4 *cold = reinterpret_cast<uint4 *>((uintptr_t)id);
+        cold[0] = d[6];
+        cold[1] = d[7];
+        uint32_t *tw = bw + (s >> 2);
+        const uint32_t sh = 8 * (s & 3);
+        uint32_t c = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            const uint32_t nw = (c & ~(0xFFu << sh)) | (tag << sh);
+            if (__hip_atomic_compare_exchange_strong(tw, &c, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                break;
+        }
+    }
+}
+
+int launch_snap_restore(const Snap &sn, hipStream_t s)
+{
+    const uint32_t g = (sn.mask / BLOCK) + 1;
+    hipLaunchKernelGGL(k_snap_restore, dim3(g < 4096 ? g : 4096), dim3(BLOCK), 0, s, sn);
+    return launch_status(__func__);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_scatter_u64(unsigned long long *const *ptrs, const unsigned long long *in,
+                                                       uint32_t n)
+{
+    for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < n; k += gridDim.x * BLOCK)
+        __hip_atomic_store(ptrs[k], in[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int launch_scatter_u64(unsigned long long *const *ptrs, const unsigned long long *in, uint32_t n, hipStream_t s)
+{
+    if (!n) return 0;
+    const uint32_t g = (n + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(k_scatter_u64, dim3(g < 1024 ? g : 1024), dim3(BLOCK), 0, s, ptrs, in, n);
+    return launch_status(__func__);
+}
+
 // the agent's staged table writes (cv_ctx.cpp PatchQueue): a block per run of words
 __global__ void __launch_bounds__(BLOCK) k_patch(const PatchRec *recs, uint32_t n, const uint32_t *words)
 {

@@ -885,7 +885,7 @@ def per_endpoint_ct(w: Workload, max_entries: int, family: str = "ct4") -> List[
 def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n_ep: int = 4096,
             n_remote: int = 16384, v6_frac: float = 0.5, vip_frac: float = 0.70, reply_frac: float = 0.20,
             n_flows: Optional[int] = None, ct_max: Optional[int] = None, stride: Optional[int] = None,
-            family: Optional[int] = None, odd_frac: float = 1.0) -> Workload:
+            family: Optional[int] = None, odd_frac: float = 1.0, ep_zipf: Optional[float] = None) -> Workload:
     """Egress from local pods through lb4/lb6 services, dual stack.
 
     Tables: 4096 local endpoints (v4 10.0.x.y + v6 fd00::a:x, each its own MAC),
@@ -994,6 +994,8 @@ def config5(n_pkts: int = 1 << 20, seed: int = 0xC1A00005, n_svc: int = 50000, n
     F = n_flows
     fam6 = (s.frac(F) < v6_frac) if family is None else np.full(F, family == 6)
     cli = s.choice(F, n_ep)
+    if ep_zipf:                                                    # (the busiest clients: Zipf(a) over endpoints)
+        cli = zipf_ranks(Stream(seed ^ 0xE9E9E9E9), F, n_ep, ep_zipf)
     r = s.frac(F)
     kind = np.where(r < vip_frac, 0, np.where(r < vip_frac + 0.15, 1, np.where(r < vip_frac + 0.25, 2, 3)))
     # 0 service, 1 local pod, 2 remote pod, 3 world

@@ -17,14 +17,14 @@ def _ep_cfg(e):
                 node_mac=e.get("node_mac", NODE_MAC))
 
 
-def oracle_dp(w: synth.Workload, flags=None, with_ct=True, ct_per_ep=None):
+def oracle_dp(w: synth.Workload, flags=None, with_ct=True, ct_per_ep=None, ct6_per_ep=None):
     """ct_per_ep: a CT4 MapSpec per endpoint (synth.per_endpoint_ct, ConntrackLocal) instead
-    of the global map; maps["ct4_ep"] holds them"""
+    of the global map; maps["ct4_ep"] holds them (ct6_per_ep, maps["ct6_ep"]: the same for CT6)"""
     from oracle import oracle as O
     dp = O.ODp(O.F_DEFAULT if flags is None else flags)
     maps = {}
     for name, spec in w.maps.items():
-        if ct_per_ep is not None and name == "ct4":
+        if (ct_per_ep is not None and name == "ct4") or (ct6_per_ep is not None and name == "ct6"):
             continue
         maps[name] = O.OMap.from_spec(spec)
         if name in ROLE_NAMES:
@@ -34,22 +34,25 @@ def oracle_dp(w: synth.Workload, flags=None, with_ct=True, ct_per_ep=None):
     ct6 = maps.get("ct6") if with_ct else None
     if ct_per_ep is not None:
         maps["ct4_ep"] = [O.OMap.from_spec(s) for s in ct_per_ep]
+    if ct6_per_ep is not None:
+        maps["ct6_ep"] = [O.OMap.from_spec(s) for s in ct6_per_ep]
     if w.endpoints:
         for k, e in enumerate(w.endpoints):
             i = dp.add_endpoint(e["lxc_id"], e["seclabel"], pol, ct if ct_per_ep is None else maps["ct4_ep"][k])
-            dp.endpoint_config(i, ct6=ct6, **_ep_cfg(e))
+            dp.endpoint_config(i, ct6=ct6 if ct6_per_ep is None else maps["ct6_ep"][k], **_ep_cfg(e))
     if w.extra and "node" in w.extra:
         dp.node_config(**w.extra["node"])
-    dp.keep += [m for k, m in maps.items() if k != "ct4_ep"] + maps.get("ct4_ep", [])
+    dp.keep += [m for k, m in maps.items() if k not in ("ct4_ep", "ct6_ep")] + maps.get("ct4_ep", []) + \
+        maps.get("ct6_ep", [])
     return dp, maps
 
 
-def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True, ct_per_ep=None):
+def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True, ct_per_ep=None, ct6_per_ep=None):
     from cilium_amd import lib
     ctx = lib.Ctx(device, lib.F_DEFAULT if flags is None else flags)
     maps = {}
     for name, spec in w.maps.items():
-        if ct_per_ep is not None and name == "ct4":
+        if (ct_per_ep is not None and name == "ct4") or (ct6_per_ep is not None and name == "ct6"):
             continue
         maps[name] = ctx.map_from_spec(spec)
         if name in ROLE_NAMES:
@@ -59,9 +62,11 @@ def product_ctx(w: synth.Workload, device=0, flags=None, with_ct=True, ct_per_ep
     ct6 = maps.get("ct6") if with_ct else None
     if ct_per_ep is not None:
         maps["ct4_ep"] = [ctx.map_from_spec(s) for s in ct_per_ep]
+    if ct6_per_ep is not None:
+        maps["ct6_ep"] = [ctx.map_from_spec(s) for s in ct6_per_ep]
     for k, e in enumerate(w.endpoints):
         i = ctx.endpoint_add(e["lxc_id"], e["seclabel"], pol, ct if ct_per_ep is None else maps["ct4_ep"][k])
-        ctx.endpoint_config(i, ct6=ct6, **_ep_cfg(e))
+        ctx.endpoint_config(i, ct6=ct6 if ct6_per_ep is None else maps["ct6_ep"][k], **_ep_cfg(e))
     if w.extra and "node" in w.extra:
         ctx.node_config(**w.extra["node"])
     ctx.sync()

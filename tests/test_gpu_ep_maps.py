@@ -227,3 +227,59 @@ def test_config3_per_endpoint_ct_admission(dev, capfd):
     m = dp.metrics()
     assert m[155, 1, 0] > 1000                                     # DROP_CT_CREATE_FAILED in the full maps
     ctx.close()
+
+
+def test_config5_per_endpoint_ct_admission(dev, monkeypatch, capfd):
+    """ConntrackLocal on egress next to max_entries (verdict r04 item 3): every endpoint
+    its own CT4 and CT6 map, sized so that about a third of them fill within the batch.
+    A packet's source program creates in its source endpoint's map and its local delivery
+    in the destination's: each launch runs admitted at full width (cv_ctx.cpp
+    lxc_admitted_maps -- two budgets per packet, every map's walk a segment of the sorted
+    scan, a pass that was not the sequential run undone from the copy-on-first-write slot
+    set), with no one-packet launches.  Every output, every endpoint's two maps, metrics
+    and policy counters against the oracle, over two batches (the second after the agent
+    removed a third of the ingress L4 rules: denied established deliveries delete)."""
+    import re
+    from tests import ep_shard as E
+    from tests.test_gpu_egress import run_egress
+    from tests.test_gpu_ep_node import per_endpoint_ctx
+    kw = dict(n_svc=4000, n_ep=192, n_remote=768, seed=87)
+    n = 1 << 17
+    w = synth.config5(n, ct_max=1 << 20, **kw)                   # the creates per map with room for all
+    dp0, m0 = E.per_endpoint_dp(w)
+    dp0.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    cap = int(sizes[len(sizes) * 2 // 3])
+    w = synth.config5(n, ct_max=cap, **kw)
+    dp, om = E.per_endpoint_dp(w)
+    ctx, pm = per_endpoint_ctx(w)
+    monkeypatch.setenv("CV_ADMIT_STATS", "1")
+    capfd.readouterr()
+    for rnd in (0, 1):
+        if rnd == 1:
+            keys = w.maps["policy"].keys
+            for k in keys[(keys[:, 6] != 0) & (keys[:, 7] == 0)][::3]:           # ingress, L4
+                assert pm["policy"].delete(k.tobytes()) == 0 == om["policy"].delete(k.tobytes())
+        now = w.now + 3 * rnd
+        o = run_egress(ctx, w, dev, 0, w.n, now, events=False)
+        ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=now)
+        _check_fields(o, ref, EGR, rnd)
+        assert (ctx.metrics() == dp.metrics()).all(), rnd
+    err = capfd.readouterr().err
+    stats = re.findall(r"\[cv admit\] egress: (\d+) packets, (\d+) passes, (\d+) maps", err)
+    assert stats and all(int(p) == w.n for p, _, _ in stats), err[-2000:]    # whole-batch launches
+    full = 0
+    for fam in ("ct4", "ct6"):
+        for e, (a, b) in enumerate(zip(pm[fam], om[fam])):
+            ak, av = a.dump()
+            bk, bv = b.dump()
+            assert len(ak) == len(bk), (fam, e, len(ak), len(bk))
+            assert (H.sorted_rows(ak, av) == H.sorted_rows(bk, bv)).all(), (fam, e)
+            full += len(bk) == cap
+    assert full >= 40, full
+    ok, ov = om["policy"].dump()
+    pk, pv = pm["policy"].dump()
+    assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all()
+    m = dp.metrics()
+    assert m[155, 2, 0] + m[155, 1, 0] > 500                      # DROP_CT_CREATE_FAILED in the full maps
+    ctx.close()

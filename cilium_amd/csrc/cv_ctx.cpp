@@ -1967,9 +1967,12 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
             return -EPROTO;
         }
         if ((r = launch_eam_walks(a, w[0], s))) return r;
+        const uint32_t K = w[0];
         e = hipMemcpyAsync(w, a.cnt, 32, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return -EIO;
+        if (stats) fprintf(stderr, "[cv admit] egress pass %d: %u elements, %u not sequential (first packet %d)\n",
+                           pass, K, w[1], w[1] ? (int)w[3] : -1);
         if (!w[1]) break;                                         // the sequential run
         if (w[4]) {                                               // (cannot be undone: never with <= 8 slots per packet)
             fprintf(stderr, "[cv] egress admission pass %d: slot set full (%llu entries)\n", pass,

@@ -185,7 +185,8 @@ struct EAdmitM {
     void *sort_tmp;
     size_t sort_bytes;
     uint32_t *tsum;
-    uint32_t *cnt;                     // [0] elements, [1] not the sequential run, [2] a bad map index
+    uint32_t *cnt;                     // [0] elements, [1] elements not as in the sequential run, [2] a bad
+                                       // map index, [3] the first packet of such an element
     uint32_t n, nmaps;
 };
 int launch_eam_first(const EAdmitM &a, hipStream_t s);     // first-pass budgets: 0 in a full source map, else 7

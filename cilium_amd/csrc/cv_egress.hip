@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
         g.res[i] = make_uint4(0u, 0u, 0u, 0u);                   // (RES_DONE clear: finished here or later)
         if (p.eg_left) {                                          // admission: this pass's budget, the intent's map
             p.eg_left[i] = stage == STAGE_DONE ? 0u : p.budget[i];
-            p.eg_intent[i] = stage == STAGE_DONE ? 0u : (egl[0] & EG_V6) ? 16u : 0u;
+            p.eg_intent[i] = stage == STAGE_DONE ? 0u : ((egl[0] & EG_V6) ? 16u : 0u) | 32u;   // (32: runs on)
             if (p.eg_left2) {                                     // (the delivery's: budgets after the first pass's)
                 p.eg_left2[i] = stage == STAGE_DONE ? 0u : p.budget[b.n + i];
                 p.eg_intent2[i] = 0;

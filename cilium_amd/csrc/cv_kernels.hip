@@ -3295,6 +3295,17 @@ __device__ __forceinline__ uint32_t eam_map(const EAdmitM &a, uint32_t j, uint32
     return e < a.n_eps ? (f ? a.ep_mi6 : a.ep_mi4)[e] : ADMIT_NO_MAP;
 }
 
+// A slot is an element when it ran in the pass -- the source program of a packet past the
+// front (intent bit 32), a delivery that reached its destination (dst_ep set) -- with or
+// without creates: then the next pass gives it the room at its place in its map's walk
+// (a packet that created nothing here may try to in the next pass, once an earlier create
+// it hit fails; a stale budget would let it succeed where the map is full, one more pass
+// per such packet of a flow)
+__device__ __forceinline__ bool eam_has(const EAdmitM &a, uint32_t j, uint32_t slot)
+{
+    return slot ? (a.dst_ep[j] != 0xFFFFu || (a.intent2[j] & 15u)) : (a.intent[j] & 47u) != 0;
+}
+
 // first pass: 7 creates per element, none in a source map that is full
 __global__ void __launch_bounds__(BLOCK) k_eam_first(EAdmitM a)
 {
@@ -3322,7 +3333,7 @@ __global__ void __launch_bounds__(BLOCK) k_eam_keys(EAdmitM a)
 #pragma unroll
         for (uint32_t u = 0; u < ADM_KPT; ++u) {
             const uint32_t j = j0 + u;
-            if (j < a.n) mine += ((a.intent[j] & 15u) ? 1u : 0u) + ((a.intent2[j] & 15u) ? 1u : 0u);
+            if (j < a.n) mine += (eam_has(a, j, 0) ? 1u : 0u) + (eam_has(a, j, 1) ? 1u : 0u);
         }
         uint32_t total;
         uint32_t at = block_excl_scan(mine, wsum, total);
@@ -3334,7 +3345,7 @@ __global__ void __launch_bounds__(BLOCK) k_eam_keys(EAdmitM a)
             const uint32_t j = j0 + u;
             if (j >= a.n) continue;
             for (uint32_t sl = 0; sl < 2; ++sl) {
-                if (!((sl ? a.intent2 : a.intent)[j] & 15u)) continue;
+                if (!eam_has(a, j, sl)) continue;
                 uint32_t mi = eam_map(a, j, sl);
                 if (mi >= a.nmaps) {                              // (a create in a map not in the list)
                     atomicOr(a.cnt + 2, 1u);
@@ -3419,7 +3430,7 @@ __global__ void __launch_bounds__(1024) k_eam_apply(EAdmitM a, uint32_t L)
         t = seg_comb(t, e[k]);
     }
     SegSM P = seg_comb(reinterpret_cast<const SegSM *>(a.tsum)[blockIdx.x], block_excl_seg(t, lds, nullptr));
-    bool bad = false;
+    uint32_t bad = 0, first = ~0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (map[k] == KEY_NONE) continue;
@@ -3430,11 +3441,21 @@ __global__ void __launch_bounds__(1024) k_eam_apply(EAdmitM a, uint32_t L)
         const long long lowest = r0 + P.m < 0 ? r0 + P.m : 0;
         const long long R = r0 + P.s - lowest;
         const uint32_t b = (slot[k] ? a.used2 : a.used)[pkt[k]];
-        bad |= (uint32_t)(R < (long long)A ? R : (long long)A) != (A < b ? A : b);
+        if ((uint32_t)(R < (long long)A ? R : (long long)A) != (A < b ? A : b)) {
+            ++bad;
+            first = min(first, pkt[k]);
+        }
         (slot[k] ? a.next2 : a.next)[pkt[k]] = (uint8_t)(R < 7 ? R : 7);
         P = seg_comb(P, SegSM{0, e[k].s, e[k].m});
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(a.cnt + 1, 1u);
+    for (int d = 32; d; d >>= 1) {                                // (per wave: the count, the first packet)
+        bad += (uint32_t)__shfl_xor((int)bad, d, 64);
+        first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
+    }
+    if (bad && (threadIdx.x & 63) == 0) {
+        atomicAdd(a.cnt + 1, bad);
+        atomicMin(a.cnt + 3, first);
+    }
 }
 
 int launch_eam_first(const EAdmitM &a, hipStream_t s)
@@ -3449,6 +3470,7 @@ int launch_eam_keys(const EAdmitM &a, hipStream_t s)
 {
     if (a.nmaps >= KEY_NONE || a.n > MAX_CHUNK) return -EINVAL;
     (void)hipMemsetAsync(a.cnt, 0, 12, s);
+    (void)hipMemsetAsync(a.cnt + 3, 0xFF, 4, s);
     if (!a.n) return 0;
     const uint32_t per = BLOCK * ADM_KPT, g = (a.n + per - 1) / per;
     hipLaunchKernelGGL(k_eam_keys, dim3(g < 2048 ? g : 2048), dim3(BLOCK), 0, s, a);

@@ -241,7 +241,8 @@ struct cv_ctx {
     DevBuf mt_live, mt_cap, mt_epmi4, mt_epmi6, mt_out;
     DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
     DevBuf eam_buf, eam_keys, eam_snap;  // (many CT maps: per-slot intents + budgets, walk keys, the slot set)
-    Snap eam_snap_host{};
+    Snap eam_snap_host[2]{};
+    uint32_t snap_stamp = 0;
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -1878,13 +1879,12 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     }
     add(c->notify_count, 4);
     add(c->trace_count, 4);
-    uint64_t scap = 1024;
-    while (scap < (uint64_t)n * 10) scap <<= 1;                   // (<= 8 written slots per packet, load <= 0.8)
+    const uint64_t scap = (uint64_t)n * 8 + 1024;                 // (a packet writes <= 6 slots)
     size_t sort_bytes = 0;
     if (sort_keys64(nullptr, &sort_bytes, nullptr, nullptr, 2 * n, 48, nullptr)) return -EIO;
     const size_t nb = (size_t)n, live_off = ((10 * nb + 255) & ~(size_t)255);
     const size_t buf_bytes = live_off + (size_t)nm * 8 + 4096 * 12 + 256;
-    const size_t snap_bytes = scap * 8 + scap * SNAP_U4 * 16;
+    const size_t snap_bytes = scap * SNAP_U4 * 16;
     if (c->eam_snap.n < snap_bytes || c->eadm_save.n < total) {
         size_t fr = 0, all = 0;                                   // (a set that would crowd the device out:
         if (hipMemGetInfo(&fr, &all) != hipSuccess || snap_bytes + total > fr / 2) return -ENOMEM;   // planned)
@@ -1923,12 +1923,10 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     a.cnt = c->eadm_buf.as<uint32_t>();
     a.dst_ep = dst;
     Snap sn{};
-    sn.keys = c->eam_snap.as<unsigned long long>();
-    sn.data = reinterpret_cast<uint4 *>(sn.keys + scap);
-    sn.mask = (uint32_t)(scap - 1);
+    sn.log = c->eam_snap.as<uint4>();
+    sn.count = a.cnt + 5;
+    sn.cap = (uint32_t)scap;
     sn.err = a.cnt + 4;
-    c->eam_snap_host = sn;                                        // (the async copy's source outlives the call)
-    if (hipMemcpyAsync(a.cnt + 8, &c->eam_snap_host, sizeof(Snap), hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
     if ((r = launch_gather_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s))) return r;
     a.next = bud[0];
     a.next2 = bud[0] + nb;
@@ -1936,7 +1934,11 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     const bool stats = getenv("CV_ADMIT_STATS") != nullptr;
     int cur = 0, pass = 0;
     for (;; ++pass) {
-        if (hipMemsetAsync(sn.keys, 0, scap * 8, s) != hipSuccess || hipMemsetAsync(a.cnt, 0, 32, s) != hipSuccess)
+        if (++c->snap_stamp == 0) c->snap_stamp = 1;              // (a stamp per pass, never 0)
+        sn.stamp = c->snap_stamp;
+        c->eam_snap_host[pass & 1] = sn;                          // (the async copy's source outlives the call)
+        if (hipMemsetAsync(a.cnt, 0, 32, s) != hipSuccess ||
+            hipMemcpyAsync(a.cnt + 8, &c->eam_snap_host[pass & 1], sizeof(Snap), hipMemcpyHostToDevice, s) != hipSuccess)
             return -EIO;
         DpParams pp = p;
         pp.budget = bud[cur];

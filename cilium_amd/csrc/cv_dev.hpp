@@ -307,9 +307,11 @@ __device__ __forceinline__ void pol_cache_flush(const LdsPolicy &pc)
 
 // EVENTS: the kernel instance that emits the optional outputs (drop / trace records,
 // rewritten frames); the plain instance compiles them out (launchers pick one per call)
-template <bool EVENTS>
+// SNAP: the egress admission instance with many CT maps (CT slots saved before their first
+// write in a pass, Snap); the other instances compile the saving out
+template <bool EVENTS, bool SNAP = false>
 struct MetT {
-    static constexpr bool EV = EVENTS;
+    static constexpr bool EV = EVENTS, SN = SNAP;
     LdsMetrics *lm;
     Fwd f;
     LdsPolicy *pc;             // optional policy counter cache (conntrack stages)
@@ -1045,36 +1047,44 @@ __device__ __forceinline__ void ct_count(const HashTable &t, int64_t slot, CtE &
 
 // The slot as it was before this pass's first write to it (Snap, cv_dp.hpp): `fresh` = the
 // slot was just claimed for a new key (it held nothing: restored as a dead slot, which
-// every probe chain passes).  One CAS on the set; a slot already in it keeps its first
-// copy (a slot deleted and claimed again within the pass goes back to the entry it held).
+// every probe chain passes).  The stamp exchange in the side slot tells the first writer;
+// the log entries of one wave's first writers are allocated with one atomic.  A slot
+// deleted (its side slot cleared) and claimed again within the pass is logged twice: the
+// restore takes the earlier entry, the entry it held.
 template <class S>
 __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh)
 {
     const uint64_t b = (uint64_t)slot / S::SPB;
     const uint32_t s = (uint32_t)((uint64_t)slot % S::SPB);
     const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
-    const CV_G uint32_t *cold = ct_cold<S>(t, slot);
-    const unsigned long long id = (unsigned long long)(uintptr_t)cold;
-    uint32_t h = (uint32_t)(mix64(id) >> 20) & sn.mask;
-#pragma unroll 1
-    for (uint32_t k = 0; k <= sn.mask; ++k, h = (h + 1) & sn.mask) {
-        const unsigned long long cur = atomicCAS(sn.keys + h, 0ull, id);
-        if (cur == id) return;                                    // (saved before)
-        if (cur) continue;
-        uint32_t *d = reinterpret_cast<uint32_t *>(sn.data + (size_t)h * SNAP_U4);
-        const uint32_t tag = fresh ? TAG_DEAD : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
-        const unsigned long long ba = (unsigned long long)(uintptr_t)bw;
-        d[0] = (uint32_t)ba;
-        d[1] = (uint32_t)(ba >> 32);
-        d[2] = s | tag << 8 | (uint32_t)S::KS << 16;
-        const CV_G uint32_t *kw = bw + S::KEY0 + s * S::KS;
-#pragma unroll 1
-        for (int j = 0; j < S::KS; ++j) d[4 + j] = fresh ? 0u : kw[j];
-#pragma unroll 1
-        for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : cold[j];
+    CV_G uint32_t *cold = ct_cold<S>(t, slot);
+    const uint32_t prev = __hip_atomic_exchange(cold + SNAP_STAMP_WORD, sn.stamp, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const bool first = prev != sn.stamp;
+    const unsigned long long m = __ballot(first);
+    if (!first) return;
+    const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(sn.count, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)lead, 64);
+    const uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (at >= sn.cap) {
+        atomicOr(sn.err, 1u);
         return;
     }
-    atomicOr(sn.err, 1u);
+    uint32_t *d = reinterpret_cast<uint32_t *>(sn.log + (size_t)at * SNAP_U4);
+    const uint32_t tag = fresh ? TAG_DEAD : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+    const unsigned long long ba = (unsigned long long)(uintptr_t)bw, ca = (unsigned long long)(uintptr_t)cold;
+    d[0] = (uint32_t)ba;
+    d[1] = (uint32_t)(ba >> 32);
+    d[2] = s | tag << 8 | (uint32_t)S::KS << 16;
+    const CV_G uint32_t *kw = bw + S::KEY0 + s * S::KS;
+#pragma unroll 1
+    for (int j = 0; j < S::KS; ++j) d[4 + j] = fresh ? 0u : kw[j];
+#pragma unroll 1
+    for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : j == (int)SNAP_STAMP_WORD ? prev : cold[j];
+    d[32] = (uint32_t)ca;
+    d[33] = (uint32_t)(ca >> 32);
 }
 
 template <class S>

@@ -45,17 +45,22 @@ constexpr uint32_t EPH_CT_ID = 0x3FFFFFFFu, EPH_V4 = 0x80000000u;
 
 // Copy-on-first-write of conntrack slots (egress admission with many CT maps, cv_ctx.cpp
 // lxc_admitted_maps): before a pass's first write to a CT slot, the slot as it was -- its
-// tag byte, key and hot words, side slot -- goes into an open-addressing set keyed by the
-// side slot's address; a pass that was not the sequential run is undone from the set
-// (k_snap_restore) instead of from a copy of every map.
+// tag byte, key and hot words, side slot -- goes to a log; a pass that was not the
+// sequential run is undone from the log (k_snap_*) instead of from a copy of every map.
+// "First" is the pass's stamp in word 6 of the slot's side slot (padding of the 56-B
+// ct_entry layout): one atomic exchange, no table of saved slots.  A whole-entry store
+// (ct_store) clears the word, so a slot created and then hit within the pass is logged
+// again; the restore takes each slot's first entry.
 struct Snap {
-    unsigned long long *keys;  // per entry: the slot's side-slot address, 0 = free
-    uint4 *data;               // per entry SNAP_U4 x 16 B: {bucket address, s | tag << 8 | KS << 16, 0,
-                               // the slot's KS bucket words from KEY0, the side slot's 8 words at 24}
-    uint32_t mask;             // entries - 1
-    uint32_t *err;             // set when the set is full (the pass cannot be undone: loud failure)
+    uint4 *log;                // per entry SNAP_U4 x 16 B: {bucket address, s | tag << 8 | KS << 16, -,
+                               // the slot's KS bucket words from KEY0 at word 4, the side slot's 8 words
+                               // at word 24, the side slot's address at word 32}
+    uint32_t *count;           // entries written (a full log sets *err and logs no more)
+    uint32_t cap;              // entries the log holds
+    uint32_t stamp;            // this pass's (never 0)
+    uint32_t *err;             // set when the log is full (the pass cannot be undone: loud failure)
 };
-constexpr uint32_t SNAP_U4 = 8;
+constexpr uint32_t SNAP_U4 = 9, SNAP_STAMP_WORD = 6;
 
 struct DpParams {              // by value as the kernel argument
     uint32_t flags;

@@ -87,25 +87,23 @@ struct EgAdm {
     const DpParams &p;
     uint32_t i;
     Acct &a;
-    bool on;
-    uint8_t *left, *intent;
-    __device__ EgAdm(const DpParams &pp, uint32_t ii, Acct &aa, bool live, int slot = 0, uint32_t dep = 0)
-        : p(pp), i(ii), a(aa), on(live && pp.eg_left)
+    bool on, two;
+    // sn: the kernel instance saves CT slots (MetT::SN; the others compile it out)
+    __device__ EgAdm(const DpParams &pp, uint32_t ii, Acct &aa, bool live, bool sn, int slot = 0, uint32_t dep = 0)
+        : p(pp), i(ii), a(aa), on(live && pp.eg_left), two(sn && slot && pp.eg_left2)   // (many maps: SN only)
     {
-        const bool two = slot && pp.eg_left2;
-        left = two ? pp.eg_left2 : pp.eg_left;
-        intent = two ? pp.eg_intent2 : pp.eg_intent;
         if (on) {
-            a.budget = left[i];
+            a.budget = (two ? p.eg_left2 : p.eg_left)[i];
             a.tried = a.killed = 0;
-            a.snap = p.snap;
+            if (sn) a.snap = p.snap;
             if (two) p.eg_dst[i] = (uint16_t)dep;
         }
     }
     __device__ void flush()
     {
         if (!on) return;
-        left[i] = (uint8_t)a.budget;
+        uint8_t *intent = two ? p.eg_intent2 : p.eg_intent;
+        (two ? p.eg_left2 : p.eg_left)[i] = (uint8_t)a.budget;
         intent[i] = (uint8_t)(intent[i] + a.tried + (a.killed << 3));
         on = false;
     }
@@ -466,7 +464,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
-    EgAdm adm(p, i, a, true);
+    EgAdm adm(p, i, a, true, M::SN);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
     uint32_t key_dport = d3.x >> 16;
@@ -575,7 +573,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
-    EgAdm adm(p, i, a, true);
+    EgAdm adm(p, i, a, true, M::SN);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
     uint32_t key_dport = d3.x >> 16;
@@ -657,13 +655,13 @@ fin:
 
 // the service groups by member position, as the conntrack stage (position lists of the
 // binned grouping; one launch per position)
-template <bool V6, bool EV>
+template <bool V6, bool EV, bool SN = false>
 __global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
                                                     OutDev o, GroupScratch g, uint32_t pos)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;                                      // (here: the CT maps' live counts)
-    using M = MetT<EV>;
+    using M = MetT<EV, SN>;
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
@@ -1070,7 +1068,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
         a.nl = o.nl ? o.nl[i] : 0u;
         a.nu = o.nu ? o.nu[i] : 0u;
     }
-    EgAdm adm(p, i, a, live);
+    EgAdm adm(p, i, a, live, M::SN);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Skb4 &s = x.s;
     Tuple4 &t = x.t;
@@ -1245,7 +1243,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
         a.nl = o.nl ? o.nl[i] : 0u;
         a.nu = o.nu ? o.nu[i] : 0u;
     }
-    EgAdm adm(p, i, a, live);
+    EgAdm adm(p, i, a, live, M::SN);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     Skb6 &s = x.s;
     Tuple6 &t = x.t;
@@ -1388,7 +1386,7 @@ __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &
     }
     Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
     Acct a{(d1.y >> 16) & 0xFFu, d1.y >> 24, m.pc};
-    EgAdm adm(p, i, a, live, 1, d1.z & 0xFFFFu);
+    EgAdm adm(p, i, a, live, M::SN, 1, d1.z & 0xFFFFu);
     EgOut res{TC_ACT_OK, 0, d2.y, (uint8_t)(d1.z >> 16), 0};
     if (live) {
         m.pkt = b.base + i;
@@ -1437,7 +1435,7 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     s.h.c2a = unchk2((d2.w >> 6) & 3u);
     s.h.c2b = unchk2((d2.w >> 8) & 3u);
     Acct a{(d2.w >> 16) & 0xFFu, d2.w >> 24, m.pc};
-    EgAdm adm(p, i, a, live, 1, d3.x & 0xFFFFu);
+    EgAdm adm(p, i, a, live, M::SN, 1, d3.x & 0xFFFFu);
     EgOut res{TC_ACT_OK, 0, d3.w, (uint8_t)(d3.x >> 16), 0};
     if (live) {
         m.pkt = b.base + i;
@@ -1484,7 +1482,7 @@ __device__ __forceinline__ void for_each_wave(uint32_t total, F &&fn)
 #endif
 #define CV_EG_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_WAVES, 8)))
 
-template <bool V6, bool EV>
+template <bool V6, bool EV, bool SN = false>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_deliver(DpParams p, BatchDev b, uint32_t now, OutDev o,
                                                                      GroupScratch g)
 {
@@ -1492,7 +1490,7 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_deliver(DpParams p, 
     __shared__ LdsPolicy pc;
     __shared__ uint4 stage[BLOCK / 64][256];                      // quad probes
     uint4 *sq = stage[threadIdx.x >> 6];
-    using M = MetT<EV>;
+    using M = MetT<EV, SN>;
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
@@ -1509,7 +1507,7 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_deliver(DpParams p, 
 }
 
 
-template <bool V6, bool EV, bool INL>
+template <bool V6, bool EV, bool INL, bool SN = false>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g,
                                                                 uint32_t pos)
 {
@@ -1517,7 +1515,7 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, Batch
     __shared__ LdsPolicy pc;
     __shared__ uint4 stage[BLOCK / 64][256];                      // quad probes
     uint4 *sq = stage[threadIdx.x >> 6];
-    using M = MetT<EV>;
+    using M = MetT<EV, SN>;
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
@@ -1666,22 +1664,15 @@ int launch_lxc_deliver(const DpParams &p, const BatchDev &b, uint32_t now, const
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// ================================================================== launcher
-// g.epoch .. g.epoch + 2 are used (service groups, conntrack groups, NAT writers).
-int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
-                      const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s)
+// the stages after the front (service groups and LB positions, pairs, NAT links, the
+// components and their CT / delivery positions) of one instance: EV the optional outputs,
+// SN the saving of CT slots (egress admission with many CT maps).  Uses g.epoch and
+// g.epoch + 1.
+template <bool EV, bool SN>
+void eg_stages(const DpParams &p, const BatchDev &b, const uint32_t *flow_hash, uint32_t now, const OutDev &o,
+               GroupScratch g, hipStream_t s)
 {
-    g.lim = b.n;
-    if (!b.n) return 0;
     const dim3 grid(grid_for(b.n)), blk(BLOCK);
-    const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
-    if (b.stride >= 128) {
-        if (ev) hipLaunchKernelGGL((k_egress_front<32, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-        else hipLaunchKernelGGL((k_egress_front<32, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-    } else {
-        if (ev) hipLaunchKernelGGL((k_egress_front<16, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-        else hipLaunchKernelGGL((k_egress_front<16, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
-    }
     // the service groups (source, VIP) by binning, then one LB launch per member position
     {
         GroupScratch gl = g;
@@ -1693,12 +1684,9 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
         gl6.work = g.work6;
         for (uint32_t k = 0; k < NPOS; ++k) {
             const dim3 gk(grid_for(b.n / (k + 1)));
-            if (ev) hipLaunchKernelGGL((k_lb_stage<false, true>), gk, blk, 0, s, p, b, flow_hash, now, o, gl, k);
-            else hipLaunchKernelGGL((k_lb_stage<false, false>), gk, blk, 0, s, p, b, flow_hash, now, o, gl, k);
-            if (b.stride >= 128) {
-                if (ev) hipLaunchKernelGGL((k_lb_stage<true, true>), gk, blk, 0, s, p, b, flow_hash, now, o, gl6, k);
-                else hipLaunchKernelGGL((k_lb_stage<true, false>), gk, blk, 0, s, p, b, flow_hash, now, o, gl6, k);
-            }
+            hipLaunchKernelGGL((k_lb_stage<false, EV, SN>), gk, blk, 0, s, p, b, flow_hash, now, o, gl, k);
+            if (b.stride >= 128)
+                hipLaunchKernelGGL((k_lb_stage<true, EV, SN>), gk, blk, 0, s, p, b, flow_hash, now, o, gl6, k);
         }
     }
     g.epoch += 1;
@@ -1723,35 +1711,48 @@ int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_
         for (int v6 = 0; v6 < (b.stride >= 128 ? 2 : 1); ++v6) {
             const GroupScratch &gv = v6 ? g6 : gp;
             if (last) {
-                if (v6) {
-                    if (ev) hipLaunchKernelGGL((k_egress_ct<true, true, true>), gk, blk, 0, s, p, b, now, o, gv, k);
-                    else hipLaunchKernelGGL((k_egress_ct<true, false, true>), gk, blk, 0, s, p, b, now, o, gv, k);
-                } else {
-                    if (ev) hipLaunchKernelGGL((k_egress_ct<false, true, true>), gk, blk, 0, s, p, b, now, o, gv, k);
-                    else hipLaunchKernelGGL((k_egress_ct<false, false, true>), gk, blk, 0, s, p, b, now, o, gv, k);
-                }
+                if (v6) hipLaunchKernelGGL((k_egress_ct<true, EV, true, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
+                else hipLaunchKernelGGL((k_egress_ct<false, EV, true, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
                 continue;
             }
             if (v6) {
-                if (ev) {
-                    hipLaunchKernelGGL((k_egress_ct<true, true, false>), gk, blk, 0, s, p, b, now, o, gv, k);
-                    hipLaunchKernelGGL((k_egress_deliver<true, true>), gk, blk, 0, s, p, b, now, o, gv);
-                } else {
-                    hipLaunchKernelGGL((k_egress_ct<true, false, false>), gk, blk, 0, s, p, b, now, o, gv, k);
-                    hipLaunchKernelGGL((k_egress_deliver<true, false>), gk, blk, 0, s, p, b, now, o, gv);
-                }
+                hipLaunchKernelGGL((k_egress_ct<true, EV, false, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
+                hipLaunchKernelGGL((k_egress_deliver<true, EV, SN>), gk, blk, 0, s, p, b, now, o, gv);
             } else {
-                if (ev) {
-                    hipLaunchKernelGGL((k_egress_ct<false, true, false>), gk, blk, 0, s, p, b, now, o, gv, k);
-                    hipLaunchKernelGGL((k_egress_deliver<false, true>), gk, blk, 0, s, p, b, now, o, gv);
-                } else {
-                    hipLaunchKernelGGL((k_egress_ct<false, false, false>), gk, blk, 0, s, p, b, now, o, gv, k);
-                    hipLaunchKernelGGL((k_egress_deliver<false, false>), gk, blk, 0, s, p, b, now, o, gv);
-                }
+                hipLaunchKernelGGL((k_egress_ct<false, EV, false, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
+                hipLaunchKernelGGL((k_egress_deliver<false, EV, SN>), gk, blk, 0, s, p, b, now, o, gv);
             }
         }
     }
-    g.epoch += 1;
+}
+
+// ================================================================== launcher
+// g.epoch .. g.epoch + 2 are used (service groups, conntrack groups, NAT writers).
+int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
+                      const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s)
+{
+    g.lim = b.n;
+    if (!b.n) return 0;
+    const dim3 grid(grid_for(b.n)), blk(BLOCK);
+    const bool ev = o.frames || p.notify || p.trace;              // the instance with the optional outputs
+    if (b.stride >= 128) {
+        if (ev) hipLaunchKernelGGL((k_egress_front<32, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+        else hipLaunchKernelGGL((k_egress_front<32, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+    } else {
+        if (ev) hipLaunchKernelGGL((k_egress_front<16, true>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+        else hipLaunchKernelGGL((k_egress_front<16, false>), grid, blk, 0, s, p, b, src_ep, ep0, o, g);
+    }
+    if (ev) {
+        if (p.snap) eg_stages<true, true>(p, b, flow_hash, now, o, g, s);
+        else eg_stages<true, false>(p, b, flow_hash, now, o, g, s);
+    } else {
+        if (p.snap) eg_stages<false, true>(p, b, flow_hash, now, o, g, s);
+        else eg_stages<false, false>(p, b, flow_hash, now, o, g, s);
+    }
+    g.epoch += 2;                                                 // (as eg_stages left its copy)
+    g.q4 = Q_CT4;
+    g.q6 = Q_CT6;
+    g.flat = 1;
     hipLaunchKernelGGL(k_nat_group, grid, blk, 0, s, b, g);
     hipLaunchKernelGGL(k_nat_apply, grid, blk, 0, s, p, b, now, g);
     hipLaunchKernelGGL(k_out_unpack, grid, blk, 0, s, o, g, b.n);

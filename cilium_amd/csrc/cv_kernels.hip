@@ -3495,29 +3495,42 @@ int launch_eam_walks(const EAdmitM &a, uint32_t K, hipStream_t s)
     return launch_status(__func__);
 }
 
-// A pass undone (Snap, cv_dp.hpp): every saved slot back as it was -- its bucket words,
-// side slot and tag byte (a CAS on the tag word, which other slots of the bucket share)
+// A pass undone (Snap, cv_dp.hpp): every logged slot back as it was -- its bucket words,
+// side slot and tag byte (a CAS on the tag word, which other slots of the bucket share).
+// A slot logged twice (deleted and claimed again within the pass) takes its first entry:
+// the stamp word of its side slot is set to ~0, then to the least entry index naming it,
+// and only that entry writes.
+__device__ __forceinline__ uint32_t *snap_cold(const uint4 *d)
+{
+    const uint4 q = d[8];
+    return reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)q.y << 32 | q.x));
+}
+
+__global__ void __launch_bounds__(BLOCK) k_snap_mark(Snap sn, uint32_t phase)
+{
+    const uint32_t n = min(*sn.count, sn.cap);
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        uint32_t *w = snap_cold(sn.log + (size_t)i * SNAP_U4) + SNAP_STAMP_WORD;
+        if (phase == 0) *w = ~0u;
+        else atomicMin(w, i);
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
 {
-    for (uint32_t h = blockIdx.x * BLOCK + threadIdx.x; h <= sn.mask; h += gridDim.x * BLOCK) {
-        const unsigned long long id = sn.keys[h];
-        if (!id) continue;
-        const uint4 *d = sn.data + (size_t)h * SNAP_U4;
+    const uint32_t n = min(*sn.count, sn.cap);
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const uint4 *d = sn.log + (size_t)i * SNAP_U4;
+        uint32_t *cold = snap_cold(d);
+        if (cold[SNAP_STAMP_WORD] != i) continue;                 // (a later entry of the slot)
         const uint4 h0 = d[0];
         uint32_t *bw = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)h0.y << 32 | h0.x));
         const uint32_t s = h0.z & 0xFFu, tag = (h0.z >> 8) & 0xFFu, ks = (h0.z >> 16) & 0xFFu;
         if (ks > 20) continue;                                    // (not a CT slot record)
-        uint32_t w[20];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const uint4 u = d[1 + q];
-            w[4 * q] = u.x; w[4 * q + 1] = u.y; w[4 * q + 2] = u.z; w[4 * q + 3] = u.w;
-        }
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(d);
         uint32_t *kw = bw + 2 + s * ks;                           // (KEY0 = 2 for both CT specs)
-        for (uint32_t j = 0; j < ks; ++j) kw[j] = w[j];
-        uint4 *cold = reinterpret_cast<uint4 *>((uintptr_t)id);
-        cold[0] = d[6];
-        cold[1] = d[7];
+        for (uint32_t j = 0; j < ks; ++j) kw[j] = w[4 + j];
+        for (uint32_t j = 0; j < 8; ++j) cold[j] = w[24 + j];
         uint32_t *tw = bw + (s >> 2);
         const uint32_t sh = 8 * (s & 3);
         uint32_t c = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3532,8 +3545,11 @@ __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
 
 int launch_snap_restore(const Snap &sn, hipStream_t s)
 {
-    const uint32_t g = (sn.mask / BLOCK) + 1;
-    hipLaunchKernelGGL(k_snap_restore, dim3(g < 4096 ? g : 4096), dim3(BLOCK), 0, s, sn);
+    const uint32_t g = (sn.cap / BLOCK) + 1;
+    const dim3 grid(g < 4096 ? g : 4096), blk(BLOCK);
+    hipLaunchKernelGGL(k_snap_mark, grid, blk, 0, s, sn, 0u);
+    hipLaunchKernelGGL(k_snap_mark, grid, blk, 0, s, sn, 1u);
+    hipLaunchKernelGGL(k_snap_restore, grid, blk, 0, s, sn);
     return launch_status(__func__);
 }
 

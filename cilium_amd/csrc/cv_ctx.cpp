@@ -1879,12 +1879,12 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     }
     add(c->notify_count, 4);
     add(c->trace_count, 4);
-    const uint64_t scap = (uint64_t)n * 8 + 1024;                 // (a packet writes <= 6 slots)
+    const uint64_t scap = (uint64_t)n * SNAP_PER;                 // (a packet writes <= 6 slots)
     size_t sort_bytes = 0;
     if (sort_keys64(nullptr, &sort_bytes, nullptr, nullptr, 2 * n, 48, nullptr)) return -EIO;
     const size_t nb = (size_t)n, live_off = ((10 * nb + 255) & ~(size_t)255);
     const size_t buf_bytes = live_off + (size_t)nm * 8 + 4096 * 12 + 256;
-    const size_t snap_bytes = scap * SNAP_U4 * 16;
+    const size_t snap_bytes = scap * SNAP_U4 * 16 + nb;           // (+ the per-packet entry counts)
     if (c->eam_snap.n < snap_bytes || c->eadm_save.n < total) {
         size_t fr = 0, all = 0;                                   // (a set that would crowd the device out:
         if (hipMemGetInfo(&fr, &all) != hipSuccess || snap_bytes + total > fr / 2) return -ENOMEM;   // planned)
@@ -1924,8 +1924,8 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     a.dst_ep = dst;
     Snap sn{};
     sn.log = c->eam_snap.as<uint4>();
-    sn.count = a.cnt + 5;
-    sn.cap = (uint32_t)scap;
+    sn.cnt = reinterpret_cast<uint8_t *>(sn.log + scap * SNAP_U4);
+    sn.n = n;
     sn.err = a.cnt + 4;
     if ((r = launch_gather_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s))) return r;
     a.next = bud[0];
@@ -1937,7 +1937,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
         if (++c->snap_stamp == 0) c->snap_stamp = 1;              // (a stamp per pass, never 0)
         sn.stamp = c->snap_stamp;
         c->eam_snap_host[pass & 1] = sn;                          // (the async copy's source outlives the call)
-        if (hipMemsetAsync(a.cnt, 0, 32, s) != hipSuccess ||
+        if (hipMemsetAsync(a.cnt, 0, 32, s) != hipSuccess || hipMemsetAsync(sn.cnt, 0, nb, s) != hipSuccess ||
             hipMemcpyAsync(a.cnt + 8, &c->eam_snap_host[pass & 1], sizeof(Snap), hipMemcpyHostToDevice, s) != hipSuccess)
             return -EIO;
         DpParams pp = p;

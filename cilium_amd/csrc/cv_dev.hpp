@@ -448,6 +448,7 @@ struct Acct {
     uint32_t tried = 0;        // admission: creates of new entries tried (a failing one included)
     uint32_t killed = 0;       // admission: entries deleted
     const Snap *snap = nullptr;  // egress admission with many CT maps: slots saved before their first write
+    uint32_t spkt = 0, scnt = 0;   // (the packet and its log entries so far)
 };
 
 // lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
@@ -1045,14 +1046,11 @@ __device__ __forceinline__ void ct_count(const HashTable &t, int64_t slot, CtE &
     e.w[k] = lo;
 }
 
-// The slot as it was before this pass's first write to it (Snap, cv_dp.hpp): `fresh` = the
-// slot was just claimed for a new key (it held nothing: restored as a dead slot, which
-// every probe chain passes).  The stamp exchange in the side slot tells the first writer;
-// the log entries of one wave's first writers are allocated with one atomic.  A slot
-// deleted (its side slot cleared) and claimed again within the pass is logged twice: the
-// restore takes the earlier entry, the entry it held.
+// The slot as it was before this pass's first write to it (Snap, cv_dp.hpp), into the
+// packet's next log entry: `fresh` = the slot was just claimed for a new key (it held
+// nothing: restored as a dead slot, which every probe chain passes).
 template <class S>
-__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh)
+__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh, Acct &a)
 {
     const uint64_t b = (uint64_t)slot / S::SPB;
     const uint32_t s = (uint32_t)((uint64_t)slot % S::SPB);
@@ -1060,19 +1058,12 @@ __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, in
     CV_G uint32_t *cold = ct_cold<S>(t, slot);
     const uint32_t prev = __hip_atomic_exchange(cold + SNAP_STAMP_WORD, sn.stamp, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-    const bool first = prev != sn.stamp;
-    const unsigned long long m = __ballot(first);
-    if (!first) return;
-    const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == lead) base = atomicAdd(sn.count, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, (int)lead, 64);
-    const uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (at >= sn.cap) {
+    if (prev == sn.stamp) return;                                 // (saved before in this pass)
+    if (a.scnt >= SNAP_PER || a.spkt >= sn.n) {
         atomicOr(sn.err, 1u);
         return;
     }
-    uint32_t *d = reinterpret_cast<uint32_t *>(sn.log + (size_t)at * SNAP_U4);
+    uint32_t *d = reinterpret_cast<uint32_t *>(sn.log + ((size_t)a.spkt * SNAP_PER + a.scnt++) * SNAP_U4);
     const uint32_t tag = fresh ? TAG_DEAD : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
     const unsigned long long ba = (unsigned long long)(uintptr_t)bw, ca = (unsigned long long)(uintptr_t)cold;
     d[0] = (uint32_t)ba;
@@ -1088,9 +1079,9 @@ __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, in
 }
 
 template <class S>
-__device__ __forceinline__ void snap_before(const Acct &a, const HashTable &t, int64_t slot, bool fresh = false)
+__device__ __forceinline__ void snap_before(Acct &a, const HashTable &t, int64_t slot, bool fresh = false)
 {
-    if (a.snap) snap_slot<S>(*a.snap, t, slot, fresh);
+    if (a.snap) snap_slot<S>(*a.snap, t, slot, fresh, a);
 }
 
 // __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)

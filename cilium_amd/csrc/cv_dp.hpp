@@ -48,19 +48,24 @@ constexpr uint32_t EPH_CT_ID = 0x3FFFFFFFu, EPH_V4 = 0x80000000u;
 // tag byte, key and hot words, side slot -- goes to a log; a pass that was not the
 // sequential run is undone from the log (k_snap_*) instead of from a copy of every map.
 // "First" is the pass's stamp in word 6 of the slot's side slot (padding of the 56-B
-// ct_entry layout): one atomic exchange, no table of saved slots.  A whole-entry store
-// (ct_store) clears the word, so a slot created and then hit within the pass is logged
-// again; the restore takes each slot's first entry.
+// ct_entry layout): one atomic exchange, no table of saved slots.  The log has SNAP_PER
+// entries per packet, written by the packet's own stages in order (no allocation
+// atomics).  A whole-entry store (ct_store) clears the stamp, so a slot created and then
+// hit by later packets of its group is logged again -- by a later packet, as a group runs
+// in packet order; a delete keeps it (dev_kill), so a slot deleted and claimed again by
+// another group is not.  The restore takes each slot's entry of least index: its state
+// before the pass.
 struct Snap {
     uint4 *log;                // per entry SNAP_U4 x 16 B: {bucket address, s | tag << 8 | KS << 16, -,
                                // the slot's KS bucket words from KEY0 at word 4, the side slot's 8 words
                                // at word 24, the side slot's address at word 32}
-    uint32_t *count;           // entries written (a full log sets *err and logs no more)
-    uint32_t cap;              // entries the log holds
+    uint8_t *cnt;              // per packet the entries written
+    uint32_t n;                // packets
     uint32_t stamp;            // this pass's (never 0)
-    uint32_t *err;             // set when the log is full (the pass cannot be undone: loud failure)
+    uint32_t *err;             // set when a packet has more entries than SNAP_PER (the pass cannot be undone:
+                               // loud failure)
 };
-constexpr uint32_t SNAP_U4 = 9, SNAP_STAMP_WORD = 6;
+constexpr uint32_t SNAP_U4 = 9, SNAP_STAMP_WORD = 6, SNAP_PER = 8;
 
 struct DpParams {              // by value as the kernel argument
     uint32_t flags;

@@ -95,13 +95,18 @@ struct EgAdm {
         if (on) {
             a.budget = (two ? p.eg_left2 : p.eg_left)[i];
             a.tried = a.killed = 0;
-            if (sn) a.snap = p.snap;
+            if (sn) {
+                a.snap = p.snap;
+                a.spkt = i;
+                a.scnt = p.snap->cnt[i];
+            }
             if (two) p.eg_dst[i] = (uint16_t)dep;
         }
     }
     __device__ void flush()
     {
         if (!on) return;
+        if (a.snap) a.snap->cnt[i] = (uint8_t)a.scnt;
         uint8_t *intent = two ? p.eg_intent2 : p.eg_intent;
         (two ? p.eg_left2 : p.eg_left)[i] = (uint8_t)a.budget;
         intent[i] = (uint8_t)(intent[i] + a.tried + (a.killed << 3));

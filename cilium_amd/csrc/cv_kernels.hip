@@ -3497,32 +3497,36 @@ int launch_eam_walks(const EAdmitM &a, uint32_t K, hipStream_t s)
 
 // A pass undone (Snap, cv_dp.hpp): every logged slot back as it was -- its bucket words,
 // side slot and tag byte (a CAS on the tag word, which other slots of the bucket share).
-// A slot logged twice (deleted and claimed again within the pass) takes its first entry:
-// the stamp word of its side slot is set to ~0, then to the least entry index naming it,
-// and only that entry writes.
+// A slot logged twice takes its entry of least index: the stamp word of its side slot is
+// set to ~0, then to the least entry index naming it, and only that entry writes.
 __device__ __forceinline__ uint32_t *snap_cold(const uint4 *d)
 {
     const uint4 q = d[8];
     return reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)q.y << 32 | q.x));
 }
 
+__device__ __forceinline__ bool snap_used(const Snap &sn, uint32_t e)
+{
+    return e % SNAP_PER < sn.cnt[e / SNAP_PER];
+}
+
 __global__ void __launch_bounds__(BLOCK) k_snap_mark(Snap sn, uint32_t phase)
 {
-    const uint32_t n = min(*sn.count, sn.cap);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        uint32_t *w = snap_cold(sn.log + (size_t)i * SNAP_U4) + SNAP_STAMP_WORD;
+    for (uint32_t e = blockIdx.x * BLOCK + threadIdx.x; e < sn.n * SNAP_PER; e += gridDim.x * BLOCK) {
+        if (!snap_used(sn, e)) continue;
+        uint32_t *w = snap_cold(sn.log + (size_t)e * SNAP_U4) + SNAP_STAMP_WORD;
         if (phase == 0) *w = ~0u;
-        else atomicMin(w, i);
+        else atomicMin(w, e);
     }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
 {
-    const uint32_t n = min(*sn.count, sn.cap);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        const uint4 *d = sn.log + (size_t)i * SNAP_U4;
+    for (uint32_t e = blockIdx.x * BLOCK + threadIdx.x; e < sn.n * SNAP_PER; e += gridDim.x * BLOCK) {
+        if (!snap_used(sn, e)) continue;
+        const uint4 *d = sn.log + (size_t)e * SNAP_U4;
         uint32_t *cold = snap_cold(d);
-        if (cold[SNAP_STAMP_WORD] != i) continue;                 // (a later entry of the slot)
+        if (cold[SNAP_STAMP_WORD] != e) continue;                 // (a later entry of the slot)
         const uint4 h0 = d[0];
         uint32_t *bw = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)h0.y << 32 | h0.x));
         const uint32_t s = h0.z & 0xFFu, tag = (h0.z >> 8) & 0xFFu, ks = (h0.z >> 16) & 0xFFu;
@@ -3545,7 +3549,7 @@ __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
 
 int launch_snap_restore(const Snap &sn, hipStream_t s)
 {
-    const uint32_t g = (sn.cap / BLOCK) + 1;
+    const uint32_t g = (sn.n * SNAP_PER / BLOCK) + 1;
     const dim3 grid(g < 4096 ? g : 4096), blk(BLOCK);
     hipLaunchKernelGGL(k_snap_mark, grid, blk, 0, s, sn, 0u);
     hipLaunchKernelGGL(k_snap_mark, grid, blk, 0, s, sn, 1u);

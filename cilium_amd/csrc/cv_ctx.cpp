@@ -2506,7 +2506,7 @@ int lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
     const bool guarded = getenv("CV_EGRESS_GUARDED") != nullptr;   // (tests: the planned launches)
-    const bool one_map = egress_admissible(cts);
+    const bool one_map = egress_admissible(cts) && !getenv("CV_EAM_FORCE");   // (measurements: the many-map form)
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         // a launch whose creates (at most 7 per packet) fit runs at full width; one that may
         // reach max_entries runs admitted: lxc_admitted with one CT map per family,

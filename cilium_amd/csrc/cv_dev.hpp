@@ -1047,10 +1047,12 @@ __device__ __forceinline__ void ct_count(const HashTable &t, int64_t slot, CtE &
 }
 
 // The slot as it was before this pass's first write to it (Snap, cv_dp.hpp), into the
-// packet's next log entry: `fresh` = the slot was just claimed for a new key (it held
-// nothing: restored as a dead slot, which every probe chain passes).
+// packet's next log entry: `fresh` = the slot was just claimed for a new key, `was` its tag
+// before the claim (empty or dead; restored exactly: a pass undone as tombstones would
+// lengthen every later miss's probe chain, and undone passes repeat).
 template <class S>
-__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh, Acct &a)
+__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh, uint32_t was,
+                                          Acct &a)
 {
     const uint64_t b = (uint64_t)slot / S::SPB;
     const uint32_t s = (uint32_t)((uint64_t)slot % S::SPB);
@@ -1064,7 +1066,7 @@ __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, in
         return;
     }
     uint32_t *d = reinterpret_cast<uint32_t *>(sn.log + ((size_t)a.spkt * SNAP_PER + a.scnt++) * SNAP_U4);
-    const uint32_t tag = fresh ? TAG_DEAD : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+    const uint32_t tag = fresh ? was : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
     const unsigned long long ba = (unsigned long long)(uintptr_t)bw, ca = (unsigned long long)(uintptr_t)cold;
     d[0] = (uint32_t)ba;
     d[1] = (uint32_t)(ba >> 32);
@@ -1079,9 +1081,10 @@ __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, in
 }
 
 template <class S>
-__device__ __forceinline__ void snap_before(Acct &a, const HashTable &t, int64_t slot, bool fresh = false)
+__device__ __forceinline__ void snap_before(Acct &a, const HashTable &t, int64_t slot, bool fresh = false,
+                                            uint32_t was = TAG_DEAD)
 {
-    if (a.snap) snap_slot<S>(*a.snap, t, slot, fresh, a);
+    if (a.snap) snap_slot<S>(*a.snap, t, slot, fresh, was, a);
 }
 
 // __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)
@@ -1415,9 +1418,10 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
         --a.budget;
     }
     bool created;
-    const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent);
+    uint32_t was = TAG_DEAD;
+    const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent, &was);
     if (s < 0) return false;
-    snap_before<typename T::Spec>(a, ct, s, created);
+    snap_before<typename T::Spec>(a, ct, s, created, was);
     if (created) ct_live_add(ct, a, guard, 1);
     ct_store<typename T::Spec>(ct, s, e, created);
     return true;

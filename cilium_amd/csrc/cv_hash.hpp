@@ -577,7 +577,7 @@ __device__ __forceinline__ int64_t probe_end(const Probe<S> &pr, const HashTable
 // slot holds (dev_kill and the GC clear a key before its slot turns dead), neither of
 // which is its own key.  The kernel boundary publishes the entry to later launches.
 __device__ __forceinline__ bool claim_in_word(CV_G uint32_t *tw, uint32_t cur, int first, int nslots, uint32_t tag,
-                                              int &got)
+                                              int &got, uint32_t &was)
 {
     for (;;) {
         int k = -1;
@@ -586,9 +586,11 @@ __device__ __forceinline__ bool claim_in_word(CV_G uint32_t *tw, uint32_t cur, i
             if (q < nslots && ((cur >> (8 * q)) & 0xFFu) < TAG_BUSY) k = q;
         if (k < 0) return false;
         const uint32_t nw = (cur & ~(0xFFu << (8 * k))) | (tag << (8 * k));
+        const uint32_t old = (cur >> (8 * k)) & 0xFFu;
         if (__hip_atomic_compare_exchange_strong(tw, &cur, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT)) {
             got = first + k;
+            was = old;
             return true;
         }
     }
@@ -596,7 +598,7 @@ __device__ __forceinline__ bool claim_in_word(CV_G uint32_t *tw, uint32_t cur, i
 
 template <class S>
 __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t *key, bool *created,
-                                              bool known_absent = false)
+                                              bool known_absent = false, uint32_t *was = nullptr)
 {
     uint32_t tag;
     const uint64_t h = home_hash<S>(key, tag);
@@ -638,8 +640,10 @@ __device__ __forceinline__ int64_t dev_upsert(const HashTable &t, const uint32_t
             cur = (uint64_t)tg.x | ((uint64_t)tg.y << 32);
         }
         int got = -1;
-        if (claim_in_word(bw, (uint32_t)cur, 0, S::SPB < 4 ? S::SPB : 4, tag, got) ||
-            (S::SPB > 4 && claim_in_word(bw + 1, (uint32_t)(cur >> 32), 4, S::SPB - 4, tag, got))) {
+        uint32_t old = TAG_DEAD;
+        if (claim_in_word(bw, (uint32_t)cur, 0, S::SPB < 4 ? S::SPB : 4, tag, got, old) ||
+            (S::SPB > 4 && claim_in_word(bw + 1, (uint32_t)(cur >> 32), 4, S::SPB - 4, tag, got, old))) {
+            if (was) *was = old;                                  // (the claimed slot's tag: empty or dead)
 #pragma unroll
             for (int j = 0; j < S::KW; ++j) bw[S::KEY0 + got * S::KS + j] = key[j];
             *created = true;

@@ -242,7 +242,6 @@ struct cv_ctx {
     DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
     DevBuf eam_buf, eam_keys, eam_snap;  // (many CT maps: per-slot intents + budgets, walk keys, the slot set)
     Snap eam_snap_host[2]{};
-    uint32_t snap_stamp = 0;
     uint64_t gcap = 0, gn = 0;
     bool g_egress = false;     // parent + egress scratch allocated
     uint32_t epoch = 0;
@@ -1925,7 +1924,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     Snap sn{};
     sn.log = c->eam_snap.as<uint4>();
     sn.cnt = reinterpret_cast<uint8_t *>(sn.log + scap * SNAP_U4);
-    sn.n = n;
+    sn.n = getenv("CV_SNAP_ABLATE") ? 0u : n;                      // (timing only: no slot saved, wrong undo)
     sn.err = a.cnt + 4;
     if ((r = launch_gather_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s))) return r;
     a.next = bud[0];
@@ -1934,8 +1933,6 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
     const bool stats = getenv("CV_ADMIT_STATS") != nullptr;
     int cur = 0, pass = 0;
     for (;; ++pass) {
-        if (++c->snap_stamp == 0) c->snap_stamp = 1;              // (a stamp per pass, never 0)
-        sn.stamp = c->snap_stamp;
         c->eam_snap_host[pass & 1] = sn;                          // (the async copy's source outlives the call)
         if (hipMemsetAsync(a.cnt, 0, 32, s) != hipSuccess || hipMemsetAsync(sn.cnt, 0, nb, s) != hipSuccess ||
             hipMemcpyAsync(a.cnt + 8, &c->eam_snap_host[pass & 1], sizeof(Snap), hipMemcpyHostToDevice, s) != hipSuccess)
@@ -1970,6 +1967,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
         }
         if ((r = launch_eam_walks(a, w[0], s))) return r;
         const uint32_t K = w[0];
+        if (sn.n && (r = launch_snap_clear(sn, s))) return r;    // (the slots' bits, before the next pass)
         e = hipMemcpyAsync(w, a.cnt, 32, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return -EIO;
@@ -1981,7 +1979,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
                     (unsigned long long)scap);
             return -EIO;
         }
-        if ((r = launch_snap_restore(sn, s)) ||                   // back to the state before the window
+        if ((sn.n && (r = launch_snap_restore(sn, s))) ||         // back to the state before the window
             (r = launch_scatter_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s)))
             return r;
         for (const Region &g : regs)

@@ -1054,28 +1054,29 @@ template <class S>
 __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh, uint32_t was,
                                           Acct &a)
 {
+    constexpr uint32_t SPARE = S::KEY0 + S::SPB * S::KS;          // (the bucket's first word past its slots)
+    static_assert(SPARE < S::BW, "a CT bucket has a spare word");
     const uint64_t b = (uint64_t)slot / S::SPB;
     const uint32_t s = (uint32_t)((uint64_t)slot % S::SPB);
-    const CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
-    CV_G uint32_t *cold = ct_cold<S>(t, slot);
-    const uint32_t prev = __hip_atomic_exchange(cold + SNAP_STAMP_WORD, sn.stamp, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == sn.stamp) return;                                 // (saved before in this pass)
+    CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
+    const uint32_t prev = __hip_atomic_fetch_or(bw + SPARE, 1u << s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev & (1u << s)) return;                                 // (saved before in this pass)
     if (a.scnt >= SNAP_PER || a.spkt >= sn.n) {
         atomicOr(sn.err, 1u);
         return;
     }
+    const CV_G uint32_t *cold = ct_cold<S>(t, slot);
     uint32_t *d = reinterpret_cast<uint32_t *>(sn.log + ((size_t)a.spkt * SNAP_PER + a.scnt++) * SNAP_U4);
     const uint32_t tag = fresh ? was : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
     const unsigned long long ba = (unsigned long long)(uintptr_t)bw, ca = (unsigned long long)(uintptr_t)cold;
     d[0] = (uint32_t)ba;
     d[1] = (uint32_t)(ba >> 32);
-    d[2] = s | tag << 8 | (uint32_t)S::KS << 16;
+    d[2] = s | tag << 8 | (uint32_t)S::KS << 16 | SPARE << 24;
     const CV_G uint32_t *kw = bw + S::KEY0 + s * S::KS;
 #pragma unroll 1
     for (int j = 0; j < S::KS; ++j) d[4 + j] = fresh ? 0u : kw[j];
 #pragma unroll 1
-    for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : j == (int)SNAP_STAMP_WORD ? prev : cold[j];
+    for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : cold[j];
     d[32] = (uint32_t)ca;
     d[33] = (uint32_t)(ca >> 32);
 }
@@ -1084,7 +1085,7 @@ template <class S>
 __device__ __forceinline__ void snap_before(Acct &a, const HashTable &t, int64_t slot, bool fresh = false,
                                             uint32_t was = TAG_DEAD)
 {
-    if (a.snap) snap_slot<S>(*a.snap, t, slot, fresh, was, a);
+    if (a.snap && a.snap->n) snap_slot<S>(*a.snap, t, slot, fresh, was, a);
 }
 
 // __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)

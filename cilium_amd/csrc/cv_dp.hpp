@@ -46,26 +46,23 @@ constexpr uint32_t EPH_CT_ID = 0x3FFFFFFFu, EPH_V4 = 0x80000000u;
 // Copy-on-first-write of conntrack slots (egress admission with many CT maps, cv_ctx.cpp
 // lxc_admitted_maps): before a pass's first write to a CT slot, the slot as it was -- its
 // tag byte, key and hot words, side slot -- goes to a log; a pass that was not the
-// sequential run is undone from the log (k_snap_*) instead of from a copy of every map.
-// "First" is the pass's stamp in word 6 of the slot's side slot (padding of the 56-B
-// ct_entry layout): one atomic exchange, no table of saved slots.  The log has SNAP_PER
-// entries per packet, written by the packet's own stages in order (no allocation
-// atomics).  A whole-entry store (ct_store) clears the stamp, so a slot created and then
-// hit by later packets of its group is logged again -- by a later packet, as a group runs
-// in packet order; a delete keeps it (dev_kill), so a slot deleted and claimed again by
-// another group is not.  The restore takes each slot's entry of least index: its state
-// before the pass.
+// sequential run is undone from the log (k_snap_restore) instead of from a copy of every
+// map.  "First" is the slot's bit in its bucket's spare word (the bucket line the write
+// touches anyway: CT4 buckets hold 30 of their 32 words, CT6 62 of 64), set with one
+// atomic OR and cleared from the log after every pass (k_snap_clear).  The log has
+// SNAP_PER entries per packet, written by the packet's own stages in order (no
+// allocation atomics).
 struct Snap {
-    uint4 *log;                // per entry SNAP_U4 x 16 B: {bucket address, s | tag << 8 | KS << 16, -,
-                               // the slot's KS bucket words from KEY0 at word 4, the side slot's 8 words
-                               // at word 24, the side slot's address at word 32}
+    uint4 *log;                // per entry SNAP_U4 x 16 B: {bucket address, s | tag << 8 | KS << 16 | spare
+                               // word << 24, the slot's KS bucket words from KEY0 at word 4, the side slot's
+                               // 8 words at word 24, the side slot's address at word 32}
     uint8_t *cnt;              // per packet the entries written
     uint32_t n;                // packets
-    uint32_t stamp;            // this pass's (never 0)
+    uint32_t pad;
     uint32_t *err;             // set when a packet has more entries than SNAP_PER (the pass cannot be undone:
                                // loud failure)
 };
-constexpr uint32_t SNAP_U4 = 9, SNAP_STAMP_WORD = 6, SNAP_PER = 8;
+constexpr uint32_t SNAP_U4 = 9, SNAP_PER = 8;
 
 struct DpParams {              // by value as the kernel argument
     uint32_t flags;
@@ -203,6 +200,7 @@ int launch_eam_first(const EAdmitM &a, hipStream_t s);     // first-pass budgets
 int launch_eam_keys(const EAdmitM &a, hipStream_t s);      // the elements -> keys, cnt[0] their number
 int launch_eam_walks(const EAdmitM &a, uint32_t K, hipStream_t s);   // sort + scan: cnt[1], next budgets
 int launch_snap_restore(const Snap &sn, hipStream_t s);
+int launch_snap_clear(const Snap &sn, hipStream_t s);   // every pass: the spare-word bits of the logged slots
 int launch_scatter_u64(unsigned long long *const *ptrs, const unsigned long long *in, uint32_t n, hipStream_t s);
 
 struct BatchDev {

@@ -672,11 +672,9 @@ __device__ __forceinline__ void dev_kill(const HashTable &t, int64_t slot)
     for (int j = 0; j < S::KS; ++j)                               // the key, and a CT slot's hot words
         __hip_atomic_exchange(G(t.buckets) + b * S::BW + S::KEY0 + s * S::KS + j, 0u, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
-    if (t.vals) {                                                 // (a CT side slot's last 8 B, padding, keep
+    if (t.vals) {
         CV_G unsigned long long *v = reinterpret_cast<CV_G unsigned long long *>(G(t.vals) + (size_t)slot * t.vstride);
-        const uint32_t nz = (S::KS > S::KW && t.vstride == 32) ? 3u : t.vstride / 8;   //  the egress admission's
-                                                                  //  stamp, cv_dp.hpp Snap)
-        for (uint32_t j = 0; j < nz; ++j)
+        for (uint32_t j = 0; j < t.vstride / 8; ++j)
             __hip_atomic_store(v + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

@@ -3497,27 +3497,16 @@ int launch_eam_walks(const EAdmitM &a, uint32_t K, hipStream_t s)
 
 // A pass undone (Snap, cv_dp.hpp): every logged slot back as it was -- its bucket words,
 // side slot and tag byte (a CAS on the tag word, which other slots of the bucket share).
-// A slot logged twice takes its entry of least index: the stamp word of its side slot is
-// set to ~0, then to the least entry index naming it, and only that entry writes.
-__device__ __forceinline__ uint32_t *snap_cold(const uint4 *d)
-{
-    const uint4 q = d[8];
-    return reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)q.y << 32 | q.x));
-}
-
+// Each slot is logged once per pass (its spare-word bit).
 __device__ __forceinline__ bool snap_used(const Snap &sn, uint32_t e)
 {
     return e % SNAP_PER < sn.cnt[e / SNAP_PER];
 }
 
-__global__ void __launch_bounds__(BLOCK) k_snap_mark(Snap sn, uint32_t phase)
+__device__ __forceinline__ uint32_t *snap_bucket(const uint4 *d)
 {
-    for (uint32_t e = blockIdx.x * BLOCK + threadIdx.x; e < sn.n * SNAP_PER; e += gridDim.x * BLOCK) {
-        if (!snap_used(sn, e)) continue;
-        uint32_t *w = snap_cold(sn.log + (size_t)e * SNAP_U4) + SNAP_STAMP_WORD;
-        if (phase == 0) *w = ~0u;
-        else atomicMin(w, e);
-    }
+    const uint4 h0 = d[0];
+    return reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)h0.y << 32 | h0.x));
 }
 
 __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
@@ -3525,15 +3514,14 @@ __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
     for (uint32_t e = blockIdx.x * BLOCK + threadIdx.x; e < sn.n * SNAP_PER; e += gridDim.x * BLOCK) {
         if (!snap_used(sn, e)) continue;
         const uint4 *d = sn.log + (size_t)e * SNAP_U4;
-        uint32_t *cold = snap_cold(d);
-        if (cold[SNAP_STAMP_WORD] != e) continue;                 // (a later entry of the slot)
-        const uint4 h0 = d[0];
-        uint32_t *bw = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)h0.y << 32 | h0.x));
-        const uint32_t s = h0.z & 0xFFu, tag = (h0.z >> 8) & 0xFFu, ks = (h0.z >> 16) & 0xFFu;
+        uint32_t *bw = snap_bucket(d);
+        const uint32_t meta = d[0].z, s = meta & 0xFFu, tag = (meta >> 8) & 0xFFu, ks = (meta >> 16) & 0xFFu;
         if (ks > 20) continue;                                    // (not a CT slot record)
         const uint32_t *w = reinterpret_cast<const uint32_t *>(d);
         uint32_t *kw = bw + 2 + s * ks;                           // (KEY0 = 2 for both CT specs)
         for (uint32_t j = 0; j < ks; ++j) kw[j] = w[4 + j];
+        const uint4 q = d[8];
+        uint32_t *cold = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)q.y << 32 | q.x));
         for (uint32_t j = 0; j < 8; ++j) cold[j] = w[24 + j];
         uint32_t *tw = bw + (s >> 2);
         const uint32_t sh = 8 * (s & 3);
@@ -3547,13 +3535,28 @@ __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
     }
 }
 
+// after every pass: the logged slots' bits in their buckets' spare words back to 0
+__global__ void __launch_bounds__(BLOCK) k_snap_clear(Snap sn)
+{
+    for (uint32_t e = blockIdx.x * BLOCK + threadIdx.x; e < sn.n * SNAP_PER; e += gridDim.x * BLOCK) {
+        if (!snap_used(sn, e)) continue;
+        const uint4 *d = sn.log + (size_t)e * SNAP_U4;
+        const uint32_t meta = d[0].z;
+        atomicAnd(snap_bucket(d) + (meta >> 24), ~(1u << (meta & 0xFFu)));
+    }
+}
+
 int launch_snap_restore(const Snap &sn, hipStream_t s)
 {
     const uint32_t g = (sn.n * SNAP_PER / BLOCK) + 1;
-    const dim3 grid(g < 4096 ? g : 4096), blk(BLOCK);
-    hipLaunchKernelGGL(k_snap_mark, grid, blk, 0, s, sn, 0u);
-    hipLaunchKernelGGL(k_snap_mark, grid, blk, 0, s, sn, 1u);
-    hipLaunchKernelGGL(k_snap_restore, grid, blk, 0, s, sn);
+    hipLaunchKernelGGL(k_snap_restore, dim3(g < 4096 ? g : 4096), dim3(BLOCK), 0, s, sn);
+    return launch_status(__func__);
+}
+
+int launch_snap_clear(const Snap &sn, hipStream_t s)
+{
+    const uint32_t g = (sn.n * SNAP_PER / BLOCK) + 1;
+    hipLaunchKernelGGL(k_snap_clear, dim3(g < 4096 ? g : 4096), dim3(BLOCK), 0, s, sn);
     return launch_status(__func__);
 }
 

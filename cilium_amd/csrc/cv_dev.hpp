@@ -1047,45 +1047,57 @@ __device__ __forceinline__ void ct_count(const HashTable &t, int64_t slot, CtE &
 }
 
 // The slot as it was before this pass's first write to it (Snap, cv_dp.hpp), into the
-// packet's next log entry: `fresh` = the slot was just claimed for a new key, `was` its tag
-// before the claim (empty or dead; restored exactly: a pass undone as tombstones would
-// lengthen every later miss's probe chain, and undone passes repeat).
+// packet's next log entry, part by part: SNAP_HOT its bucket words (tag byte, key, hot
+// run), SNAP_COLD its side slot -- a hit changes the hot run alone unless a counter
+// carries, so most entries never read the side slot's line.  SNAP_FRESH: the slot was
+// just claimed for a new key, `was` its tag before (empty or dead; restored exactly: a
+// pass undone as tombstones would lengthen every later miss's probe chain).
+enum : uint32_t { SNAP_HOT = 1, SNAP_COLD = 2, SNAP_FRESH = 4 };
 template <class S>
-__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, bool fresh, uint32_t was,
+__device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, int64_t slot, uint32_t parts, uint32_t was,
                                           Acct &a)
 {
     constexpr uint32_t SPARE = S::KEY0 + S::SPB * S::KS;          // (the bucket's first word past its slots)
-    static_assert(SPARE < S::BW, "a CT bucket has a spare word");
+    static_assert(SPARE < S::BW && S::SPB <= 8, "a CT bucket has a spare word");
     const uint64_t b = (uint64_t)slot / S::SPB;
     const uint32_t s = (uint32_t)((uint64_t)slot % S::SPB);
     CV_G uint32_t *bw = G(t.buckets) + b * S::BW;
-    const uint32_t prev = __hip_atomic_fetch_or(bw + SPARE, 1u << s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev & (1u << s)) return;                                 // (saved before in this pass)
+    const uint32_t want = ((parts & SNAP_HOT) ? 1u << s : 0u) | ((parts & SNAP_COLD) ? 1u << (8 + s) : 0u);
+    const uint32_t prev = __hip_atomic_fetch_or(bw + SPARE, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t hot = (want & ~prev) & (1u << s), cold_new = (want & ~prev) & (1u << (8 + s));
+    if (!hot && !cold_new) return;                                // (saved before in this pass)
     if (a.scnt >= SNAP_PER || a.spkt >= sn.n) {
         atomicOr(sn.err, 1u);
         return;
     }
+    const bool fresh = parts & SNAP_FRESH;
     const CV_G uint32_t *cold = ct_cold<S>(t, slot);
     uint32_t *d = reinterpret_cast<uint32_t *>(sn.log + ((size_t)a.spkt * SNAP_PER + a.scnt++) * SNAP_U4);
-    const uint32_t tag = fresh ? was : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
     const unsigned long long ba = (unsigned long long)(uintptr_t)bw, ca = (unsigned long long)(uintptr_t)cold;
     d[0] = (uint32_t)ba;
     d[1] = (uint32_t)(ba >> 32);
-    d[2] = s | tag << 8 | (uint32_t)S::KS << 16 | SPARE << 24;
-    const CV_G uint32_t *kw = bw + S::KEY0 + s * S::KS;
-#pragma unroll 1
-    for (int j = 0; j < S::KS; ++j) d[4 + j] = fresh ? 0u : kw[j];
-#pragma unroll 1
-    for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : cold[j];
     d[32] = (uint32_t)ca;
     d[33] = (uint32_t)(ca >> 32);
+    uint32_t tag = 0;
+    if (hot) {
+        tag = fresh ? was : (bw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+        const CV_G uint32_t *kw = bw + S::KEY0 + s * S::KS;
+#pragma unroll 1
+        for (int j = 0; j < S::KS; ++j) d[4 + j] = fresh ? 0u : kw[j];
+    }
+    if (cold_new) {
+#pragma unroll 1
+        for (int j = 0; j < 8; ++j) d[24 + j] = fresh ? 0u : cold[j];
+    }
+    d[2] = s | tag << 8 | (uint32_t)S::KS << 16 | SPARE << 24;
+    d[3] = (hot ? SNAP_HOT : 0u) | (cold_new ? SNAP_COLD : 0u);
 }
 
 template <class S>
-__device__ __forceinline__ void snap_before(Acct &a, const HashTable &t, int64_t slot, bool fresh = false,
+__device__ __forceinline__ void snap_before(Acct &a, const HashTable &t, int64_t slot, uint32_t parts,
                                             uint32_t was = TAG_DEAD)
 {
-    if (a.snap && a.snap->n) snap_slot<S>(*a.snap, t, slot, fresh, was, a);
+    if (a.snap && a.snap->n) snap_slot<S>(*a.snap, t, slot, parts, was, a);
 }
 
 // __ct_update_timeout (conntrack.h:103-161): true = report (the `monitor` result)
@@ -1201,9 +1213,13 @@ __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int ac
                                        uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a, bool *mon)
 {
     a.nu++;
-    snap_before<S>(a, ct, slot);
     CtE e;
     ct_load_hot<S>(ct, slot, e);
+    if (a.snap) {                                                 // (egress admission, many maps: the parts
+        const int k0 = dir == CT_INGRESS ? 0 : 4;                 //  the update writes; the side slot only
+        const bool carry = (flags & F_CT_ACCOUNTING) && (e.w[k0] + 1u < e.w[k0] || e.w[k0 + 2] + len < e.w[k0 + 2]);
+        snap_before<S>(a, ct, slot, SNAP_HOT | (carry ? SNAP_COLD : 0u));   //  when a counter carries)
+    }
     if (st) {
         st->rev_nat = e.w[9] >> 16;
         st->loopback = (e.bits() & CTB_LB_LOOPBACK) ? 1u : 0u;
@@ -1422,7 +1438,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
     uint32_t was = TAG_DEAD;
     const int64_t s = dev_upsert<typename T::Spec>(ct, k, &created, absent, &was);
     if (s < 0) return false;
-    snap_before<typename T::Spec>(a, ct, s, created, was);
+    snap_before<typename T::Spec>(a, ct, s, SNAP_HOT | SNAP_COLD | (created ? SNAP_FRESH : 0u), was);
     if (created) ct_live_add(ct, a, guard, 1);
     ct_store<typename T::Spec>(ct, s, e, created);
     return true;
@@ -1432,7 +1448,7 @@ __device__ __forceinline__ bool ct_put(const HashTable &ct, const T &t, const Ct
 template <class S>
 __device__ __forceinline__ void ct_kill(const HashTable &ct, int64_t slot, Acct &a, bool guard)
 {
-    snap_before<S>(a, ct, slot);
+    snap_before<S>(a, ct, slot, SNAP_HOT | SNAP_COLD);
     dev_kill<S>(ct, slot);
     ct_live_add(ct, a, guard, -1);
     a.nu++;

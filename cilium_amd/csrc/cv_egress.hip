@@ -515,7 +515,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         const int64_t s2 = dev_find<Ct4Spec, EGF>(ep.ct4, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
-            snap_before<Ct4Spec>(a, ep.ct4, s2);
+            snap_before<Ct4Spec>(a, ep.ct4, s2, SNAP_HOT);
             ct_load_hot<Ct4Spec>(ep.ct4, s2, e);                  // (w10: a hot word)
             const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
@@ -623,7 +623,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         const int64_t s2 = dev_find<Ct6Spec, EGF>(ep.ct6, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
-            snap_before<Ct6Spec>(a, ep.ct6, s2);
+            snap_before<Ct6Spec>(a, ep.ct6, s2, SNAP_HOT);
             ct_load_hot<Ct6Spec>(ep.ct6, s2, e);
             const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);

@@ -3515,14 +3515,18 @@ __global__ void __launch_bounds__(BLOCK) k_snap_restore(Snap sn)
         if (!snap_used(sn, e)) continue;
         const uint4 *d = sn.log + (size_t)e * SNAP_U4;
         uint32_t *bw = snap_bucket(d);
-        const uint32_t meta = d[0].z, s = meta & 0xFFu, tag = (meta >> 8) & 0xFFu, ks = (meta >> 16) & 0xFFu;
+        const uint32_t meta = d[0].z, parts = d[0].w, s = meta & 0xFFu, tag = (meta >> 8) & 0xFFu,
+                       ks = (meta >> 16) & 0xFFu;
         if (ks > 20) continue;                                    // (not a CT slot record)
         const uint32_t *w = reinterpret_cast<const uint32_t *>(d);
+        if (parts & 2u) {                                         // (SNAP_COLD: the side slot)
+            const uint4 q = d[8];
+            uint32_t *cold = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)q.y << 32 | q.x));
+            for (uint32_t j = 0; j < 8; ++j) cold[j] = w[24 + j];
+        }
+        if (!(parts & 1u)) continue;                              // (SNAP_HOT: bucket words and tag)
         uint32_t *kw = bw + 2 + s * ks;                           // (KEY0 = 2 for both CT specs)
         for (uint32_t j = 0; j < ks; ++j) kw[j] = w[4 + j];
-        const uint4 q = d[8];
-        uint32_t *cold = reinterpret_cast<uint32_t *>((uintptr_t)((unsigned long long)q.y << 32 | q.x));
-        for (uint32_t j = 0; j < 8; ++j) cold[j] = w[24 + j];
         uint32_t *tw = bw + (s >> 2);
         const uint32_t sh = 8 * (s & 3);
         uint32_t c = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3541,8 +3545,8 @@ __global__ void __launch_bounds__(BLOCK) k_snap_clear(Snap sn)
     for (uint32_t e = blockIdx.x * BLOCK + threadIdx.x; e < sn.n * SNAP_PER; e += gridDim.x * BLOCK) {
         if (!snap_used(sn, e)) continue;
         const uint4 *d = sn.log + (size_t)e * SNAP_U4;
-        const uint32_t meta = d[0].z;
-        atomicAnd(snap_bucket(d) + (meta >> 24), ~(1u << (meta & 0xFFu)));
+        const uint32_t meta = d[0].z, s = meta & 0xFFu, parts = d[0].w;
+        atomicAnd(snap_bucket(d) + (meta >> 24), ~(((parts & 1u) ? 1u << s : 0u) | ((parts & 2u) ? 1u << (8 + s) : 0u)));
     }
 }
 

@@ -1846,7 +1846,7 @@ int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_
 // and the event rings' counts were copied before the first pass.  Launches of at most
 // EAM_WINDOW packets; -EAGAIN (no fixed point, state restored) and -ENOMEM (no room for the
 // set, nothing ran) send the caller to planned launches.
-constexpr uint32_t EAM_WINDOW = 1u << 22;
+constexpr uint32_t EAM_WINDOW = 1u << 23;
 int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &oc, const std::vector<MapObj *> &cts,
                       hipStream_t s)

@@ -22,7 +22,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage<false>",
-            "config5": "k_egress_ct<true, false, false>"}
+            "config5": "k_egress_ct<true, false, false, false>"}
 # a kernel launched exactly once per step (counts the steps of a pass)
 STEP_KERNEL = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_netdev_front<false>",
                "config5": "k_egress_front<32, false>"}

@@ -127,10 +127,13 @@ int cv_map_dump(cv_ctx *ctx, int h, void *keys, void *vals, uint32_t max);
  * from-netdev, every packet's creates and deletes are resolved against its map's room
  * in packet order first; from-container (egress), the pipeline runs with per-packet
  * create budgets and a scan checks them against the sequential run, re-running the
- * launch from a saved state until they agree.  Layouts beyond what
- * admission tracks (more CT maps in one launch than ADMIT_MAPS from-netdev, more than
- * one CT4 / CT6 map from-container) fall back to launches of as many packets as surely
- * fit, and one-packet launches at the limit. */
+ * launch from a saved state until they agree.  Any number of CT maps
+ * (ConntrackLocal: every endpoint its own CT4 / CT6 map) is admitted the same way: each
+ * map's walk is a segment of one sorted scan; from-container, a packet's source program
+ * and its local delivery draw on budgets of their own (source map, destination map),
+ * and a pass is undone from a log of the CT slots it wrote.  An egress launch whose
+ * passes find no fixed point, or that has no device memory for its saved state, runs
+ * again in launches of as many packets as surely fit (one packet at the limit). */
 int cv_ct_gc(cv_ctx *ctx, int h, uint32_t time, uint32_t *deleted);
 /* Slot occupancy of a device CT map (diagnostics, no reference counterpart): out[0]
  * empty slots, out[1] tombstones (deleted entries not yet reclaimed by cv_ct_gc),

@@ -229,7 +229,8 @@ def test_config3_per_endpoint_ct_admission(dev, capfd):
     ctx.close()
 
 
-def test_config5_per_endpoint_ct_admission(dev, monkeypatch, capfd):
+@pytest.mark.parametrize("events", [False, True])
+def test_config5_per_endpoint_ct_admission(dev, monkeypatch, capfd, events):
     """ConntrackLocal on egress next to max_entries (verdict r04 item 3): every endpoint
     its own CT4 and CT6 map, sized so that about a third of them fill within the batch.
     A packet's source program creates in its source endpoint's map and its local delivery
@@ -238,11 +239,14 @@ def test_config5_per_endpoint_ct_admission(dev, monkeypatch, capfd):
     scan, a pass that was not the sequential run undone from the copy-on-first-write slot
     set), with no one-packet launches.  Every output, every endpoint's two maps, metrics
     and policy counters against the oracle, over two batches (the second after the agent
-    removed a third of the ingress L4 rules: denied established deliveries delete)."""
+    removed a third of the ingress L4 rules: denied established deliveries delete).  With
+    events, the instance with the optional outputs: drop and trace records and the
+    rewritten frames too (their rings' counts go back with an undone pass)."""
     import re
     from tests import ep_shard as E
     from tests.test_gpu_egress import run_egress
     from tests.test_gpu_ep_node import per_endpoint_ctx
+    from tests.test_gpu_parity import same_frames, same_notifications, same_traces
     kw = dict(n_svc=4000, n_ep=192, n_remote=768, seed=87)
     n = 1 << 17
     w = synth.config5(n, ct_max=1 << 20, **kw)                   # the creates per map with room for all
@@ -253,6 +257,11 @@ def test_config5_per_endpoint_ct_admission(dev, monkeypatch, capfd):
     w = synth.config5(n, ct_max=cap, **kw)
     dp, om = E.per_endpoint_dp(w)
     ctx, pm = per_endpoint_ctx(w)
+    if events:
+        ctx.notify_attach(w.n)
+        dp.notify_attach(w.n)
+        ctx.trace_attach(3 * w.n, 0)
+        dp.trace_attach(3 * w.n, 0)
     monkeypatch.setenv("CV_ADMIT_STATS", "1")
     capfd.readouterr()
     for rnd in (0, 1):
@@ -261,10 +270,14 @@ def test_config5_per_endpoint_ct_admission(dev, monkeypatch, capfd):
             for k in keys[(keys[:, 6] != 0) & (keys[:, 7] == 0)][::3]:           # ingress, L4
                 assert pm["policy"].delete(k.tobytes()) == 0 == om["policy"].delete(k.tobytes())
         now = w.now + 3 * rnd
-        o = run_egress(ctx, w, dev, 0, w.n, now, events=False)
-        ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=now)
+        o = run_egress(ctx, w, dev, 0, w.n, now, events=events)
+        ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=now, frames_out=events)
         _check_fields(o, ref, EGR, rnd)
         assert (ctx.metrics() == dp.metrics()).all(), rnd
+        if events:
+            assert same_notifications(ctx, dp) == int((o["reason"] != 0).sum())
+            same_traces(ctx, dp, ref.ret)
+            same_frames(o["frames_out"], ref.frames_out, w.frames)
     err = capfd.readouterr().err
     stats = re.findall(r"\[cv admit\] egress: (\d+) packets, (\d+) passes, (\d+) maps", err)
     assert stats and all(int(p) == w.n for p, _, _ in stats), err[-2000:]    # whole-batch launches

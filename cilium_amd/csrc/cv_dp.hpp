@@ -318,7 +318,10 @@ constexpr int BIG_WORD = 25;     // cursor[25]: big-bin records of the binned gr
 // a big bin (>= BIG_MIN entries): a record of BIGW words {bin, key, start, entries, the key's
 // members, the other entries, its job (~0: not taken out), the others' fill, per scatter
 // tile the key's members [GBLK] (then the tile's fill cursor [GBLK])}
-constexpr uint32_t BIG_MIN = 8192, BIG_PCNT = 8, BIG_FILL = 8 + 256, BIGW = 8 + 512;
+#ifndef CV_BIG_MIN
+#define CV_BIG_MIN 2048
+#endif
+constexpr uint32_t BIG_MIN = CV_BIG_MIN, BIG_PCNT = 8, BIG_FILL = 8 + 256, BIGW = 8 + 512;
 // a split-key job: {key, members c, order offset, listed, member base in gbig (u32 words), tile, pad[2],
 // head[NPOS <= 8], per tile its member count [GBLK] and offset [GBLK]}
 constexpr uint32_t SJOB_HEAD = 8, SJOB_PCNT = 16, SJOB_WORDS = 16 + 2 * 256;

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -1847,13 +1848,16 @@ int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_
 // EAM_WINDOW packets; -EAGAIN (no fixed point, state restored) and -ENOMEM (no room for the
 // set, nothing ran) send the caller to planned launches.
 constexpr uint32_t EAM_WINDOW = 1u << 23;
-int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_t *src_ep, uint32_t ep0,
-                      const uint32_t *flow_hash, uint32_t now, const OutDev &oc, const std::vector<MapObj *> &cts,
-                      hipStream_t s)
+// `launch` runs one pass of the n packets (the egress pipeline, or a delivery launch of n
+// records: cv_lxc_deliver).  `front`: the pass's first kernel resets every packet's
+// intents and loads its budgets (k_egress_front); otherwise (deliveries: slot 1 only)
+// the host does before each pass.
+int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *src_ep, uint32_t ep0,
+                      const std::vector<MapObj *> &cts, hipStream_t s,
+                      const std::function<int(const DpParams &)> &launch, bool front, const char *what)
 {
     const char *mp = getenv("CV_EADM_MAX_PASSES");
     const int MAX_PASSES = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
-    const uint32_t n = bc.n;
     if (n > EAM_WINDOW) return -EINVAL;
     int r = map_table(c, cts);
     if (r) return r;
@@ -1945,9 +1949,12 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
         pp.eg_intent2 = intent2;
         pp.eg_dst = dst;
         pp.snap = reinterpret_cast<const Snap *>(a.cnt + 8);
-        GroupScratch gs = next_groups(c, 3, s);
-        gs.gbits = gbin_bits(n);
-        if ((r = launch_lxc_egress(pp, bc, src_ep, ep0, flow_hash, now, oc, gs, s))) return r;
+        if (!front &&                                             // (slot 1 only: no source program ran)
+            (hipMemsetAsync(intent, 0, 2 * nb, s) != hipSuccess || hipMemsetAsync(left, 0, nb, s) != hipSuccess ||
+             hipMemsetAsync(dst, 0xFF, 2 * nb, s) != hipSuccess ||
+             hipMemcpyAsync(left2, bud[cur] + nb, nb, hipMemcpyDeviceToDevice, s) != hipSuccess))
+            return -EIO;
+        if ((r = launch(pp))) return r;
         a.used = bud[cur];
         a.used2 = bud[cur] + nb;
         a.next = bud[cur ^ 1];
@@ -1971,8 +1978,8 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
         e = hipMemcpyAsync(w, a.cnt, 32, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return -EIO;
-        if (stats) fprintf(stderr, "[cv admit] egress pass %d: %u elements, %u not sequential (first packet %d)\n",
-                           pass, K, w[1], w[1] ? (int)w[3] : -1);
+        if (stats) fprintf(stderr, "[cv admit] %s pass %d: %u elements, %u not sequential (first packet %d)\n",
+                           what, pass, K, w[1], w[1] ? (int)w[3] : -1);
         if (!w[1]) break;                                         // the sequential run
         if (w[4]) {                                               // (cannot be undone: never with <= 8 slots per packet)
             fprintf(stderr, "[cv] egress admission pass %d: slot set full (%llu entries)\n", pass,
@@ -1995,7 +2002,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, const BatchDev &bc, const ui
         m->live_upper = m->cap;                                   // (re-read when the next launch plans)
         m->gen++;
     }
-    if (stats) fprintf(stderr, "[cv admit] egress: %u packets, %d passes, %u maps\n", n, pass + 1, nm);
+    if (stats) fprintf(stderr, "[cv admit] %s: %u packets, %d passes, %u maps\n", what, n, pass + 1, nm);
     return 0;
 }
 
@@ -2523,9 +2530,18 @@ int lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep
         BatchDev bc = chunk(b, off, n);
         bc.hash = flow_hash ? flow_hash + off : nullptr;             // skb hash of the drop notifications
         if (!fits && !guarded) {
-            r = (one_map ? lxc_admitted : lxc_admitted_maps)(c, p, bc, src_ep ? src_ep + off : nullptr, ep0,
-                                                             flow_hash ? flow_hash + off : nullptr, now, oc(off), cts,
-                                                             (hipStream_t)stream);
+            const uint16_t *se = src_ep ? src_ep + off : nullptr;
+            const uint32_t *fh = flow_hash ? flow_hash + off : nullptr;
+            const OutDev od = oc(off);
+            if (one_map) {
+                r = lxc_admitted(c, p, bc, se, ep0, fh, now, od, cts, (hipStream_t)stream);
+            } else {
+                r = lxc_admitted_maps(c, p, n, se, ep0, cts, (hipStream_t)stream, [&](const DpParams &pp) {
+                    GroupScratch gs = next_groups(c, 3, (hipStream_t)stream);
+                    gs.gbits = gbin_bits(n);
+                    return launch_lxc_egress(pp, bc, se, ep0, fh, now, od, gs, (hipStream_t)stream);
+                }, true, "egress");
+            }
             // no fixed point (the state is back as before the chunk), or no room for the
             // state's copy (nothing ran): the chunk again in planned launches, one guarded
             // packet at a time next to the limit
@@ -2595,17 +2611,37 @@ int cv_lxc_deliver(cv_ctx *c, const uint8_t *records, uint32_t n, int v6, uint32
     }
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
+    const bool guarded = getenv("CV_EGRESS_GUARDED") != nullptr;
     for (uint32_t off = 0, m; off < n; off += m) {
         // a record creates at most the tuple and its ICMP twin in its destination's map: a
-        // launch that surely fits runs whole, else planned launches (one guarded record at
-        // a time next to the limit)
+        // launch that surely fits runs whole, else admitted (lxc_admitted_maps with the
+        // records' slot-1 budgets, windows of EAM_WINDOW), else planned launches (one
+        // guarded record at a time next to the limit)
         m = std::min(c->chunk, n - off);
-        if (!ct_fits(c, cts, m, 2)) m = ct_plan(c, cts, m, 2, (hipStream_t)stream, &p.ct_guard);
-        GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
-        gs.gbits = gbin_bits(m);
-        gs.del = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(records)) + (size_t)off * DEL_SLOTS;
-        const BatchDev bd{nullptr, v6 ? 128u : 64u, m, nullptr, nullptr, off, nullptr};
-        r = launch_lxc_deliver(p, bd, now, chunk(o, off), gs, v6, (hipStream_t)stream);
+        bool fits = ct_fits(c, cts, m, 2);
+        if (!fits && m > EAM_WINDOW) {
+            m = EAM_WINDOW;
+            fits = ct_fits(c, cts, m, 2);
+        }
+        auto one = [&](uint32_t o2, uint32_t k, const DpParams &pp) {
+            GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
+            gs.gbits = gbin_bits(k);
+            gs.del = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(records)) + (size_t)o2 * DEL_SLOTS;
+            const BatchDev bd{nullptr, v6 ? 128u : 64u, k, nullptr, nullptr, o2, nullptr};
+            return launch_lxc_deliver(pp, bd, now, chunk(o, o2), gs, v6, (hipStream_t)stream);
+        };
+        r = -EAGAIN;
+        if (!fits && !guarded)
+            r = lxc_admitted_maps(c, p, m, nullptr, 0, cts, (hipStream_t)stream,
+                                  [&](const DpParams &pp) { return one(off, m, pp); }, false, "deliver");
+        if (fits) r = one(off, m, p);
+        for (uint32_t o2 = off, k; (r == -EAGAIN || r == -ENOMEM) && o2 < off + m; o2 += k) {
+            k = ct_plan(c, cts, off + m - o2, 2, (hipStream_t)stream, &p.ct_guard);
+            int r2 = one(o2, k, p);
+            p.ct_guard = 0;
+            if (r2) return r2;
+            if (o2 + k == off + m) r = 0;
+        }
         p.ct_guard = 0;
         if (r) return r;
         for (const HashTable &t : pols)

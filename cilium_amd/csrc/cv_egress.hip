@@ -1633,12 +1633,12 @@ __global__ void __launch_bounds__(BLOCK) k_deliver_keys(DpParams p, BatchDev b, 
     }
 }
 
-template <bool V6>
+template <bool V6, bool SN = false>
 __global__ void __launch_bounds__(BLOCK) k_deliver_runs(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
-    using M = MetT<false>;
+    using M = MetT<false, SN>;                                    // (SN: admitted next to max_entries)
     M m;
     pol_cache_init(pc);
     met_init(m, lm);
@@ -1663,8 +1663,13 @@ int launch_lxc_deliver(const DpParams &p, const BatchDev &b, uint32_t now, const
     GroupScratch g6 = g;
     g6.single = g.single6;
     g6.work = g.work6;
-    if (v6) hipLaunchKernelGGL(k_deliver_runs<true>, grid, blk, 0, s, p, b, now, o, g6);
-    else hipLaunchKernelGGL(k_deliver_runs<false>, grid, blk, 0, s, p, b, now, o, g);
+    if (p.snap) {
+        if (v6) hipLaunchKernelGGL((k_deliver_runs<true, true>), grid, blk, 0, s, p, b, now, o, g6);
+        else hipLaunchKernelGGL((k_deliver_runs<false, true>), grid, blk, 0, s, p, b, now, o, g);
+    } else {
+        if (v6) hipLaunchKernelGGL((k_deliver_runs<true, false>), grid, blk, 0, s, p, b, now, o, g6);
+        else hipLaunchKernelGGL((k_deliver_runs<false, false>), grid, blk, 0, s, p, b, now, o, g);
+    }
     hipLaunchKernelGGL(k_out_unpack, grid, blk, 0, s, o, g, b.n);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -166,3 +166,32 @@ def test_endpoint_owned_two_ranks_gloo(dev, capsys):
     with capsys.disabled():
         print(f"\n  2 ranks: {w.n} packets in {results[0]['rounds']} rounds, "
               f"{sum(r['cross'] for r in results.values())} cross-rank deliveries")
+
+
+def test_endpoint_owned_at_capacity(dev, monkeypatch, capfd):
+    """The endpoint-owned node next to max_entries: maps sized so half of them fill within
+    the batch.  Split source launches and delivery launches both run admitted (budgets per
+    map, passes undone from the slot log), every output, table, counter and
+    metric against the sequential per-endpoint-map oracle."""
+    import re
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=0xE5, vip_frac=0.5)
+    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+    dp0, m0 = E.per_endpoint_dp(w)
+    dp0.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    cap = int(sizes[len(sizes) // 2])
+    w = synth.config5(1 << 12, ct_max=cap, **kw)
+    monkeypatch.setenv("CV_ADMIT_STATS", "1")
+    capfd.readouterr()
+    res = _rank_run(w, 0, 1, dev)
+    ref = _check(w, [res])
+    err = capfd.readouterr().err
+    assert re.search(r"\[cv admit\] deliver: \d+ packets", err), err[-2000:]
+    dp, om = E.per_endpoint_dp(w)
+    dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    full = sum(len(m) >= cap for fam in ("ct4", "ct6") for m in om[fam])
+    assert full >= 8, full
+    m = dp.metrics()
+    assert m[155, 2, 0] + m[155, 1, 0] > 0                        # DROP_CT_CREATE_FAILED
+    with capfd.disabled():
+        print(f"\n  at capacity: {w.n} packets, {res['rounds']} rounds, {full} maps full (max_entries {cap})")

@@ -1854,7 +1854,7 @@ constexpr uint32_t EAM_WINDOW = 1u << 23;
 // the host does before each pass.
 int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *src_ep, uint32_t ep0,
                       const std::vector<MapObj *> &cts, hipStream_t s,
-                      const std::function<int(const DpParams &)> &launch, bool front, const char *what)
+                      const std::function<int(const DpParams &)> &launch, bool front, const char *what, int v6 = 0)
 {
     const char *mp = getenv("CV_EADM_MAX_PASSES");
     const int MAX_PASSES = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
@@ -1949,8 +1949,9 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *
         pp.eg_intent2 = intent2;
         pp.eg_dst = dst;
         pp.snap = reinterpret_cast<const Snap *>(a.cnt + 8);
-        if (!front &&                                             // (slot 1 only: no source program ran)
-            (hipMemsetAsync(intent, 0, 2 * nb, s) != hipSuccess || hipMemsetAsync(left, 0, nb, s) != hipSuccess ||
+        if (!front &&                                             // (slot 1 only: no source program ran; the
+            (hipMemsetAsync(intent, v6 ? 16 : 0, nb, s) != hipSuccess ||   //  family bit of the intent byte)
+             hipMemsetAsync(intent2, 0, nb, s) != hipSuccess || hipMemsetAsync(left, 0, nb, s) != hipSuccess ||
              hipMemsetAsync(dst, 0xFF, 2 * nb, s) != hipSuccess ||
              hipMemcpyAsync(left2, bud[cur] + nb, nb, hipMemcpyDeviceToDevice, s) != hipSuccess))
             return -EIO;
@@ -2633,7 +2634,7 @@ int cv_lxc_deliver(cv_ctx *c, const uint8_t *records, uint32_t n, int v6, uint32
         r = -EAGAIN;
         if (!fits && !guarded)
             r = lxc_admitted_maps(c, p, m, nullptr, 0, cts, (hipStream_t)stream,
-                                  [&](const DpParams &pp) { return one(off, m, pp); }, false, "deliver");
+                                  [&](const DpParams &pp) { return one(off, m, pp); }, false, "deliver", v6);
         if (fits) r = one(off, m, p);
         for (uint32_t o2 = off, k; (r == -EAGAIN || r == -ENOMEM) && o2 < off + m; o2 += k) {
             k = ct_plan(c, cts, off + m - o2, 2, (hipStream_t)stream, &p.ct_guard);

@@ -241,9 +241,11 @@ int cv_lxc_egress(cv_ctx *ctx, const cv_batch *b, const uint16_t *src_ep, uint32
  * index as a u16), identity / ct as for cv_lxc_egress.
  * cv_lxc_deliver runs the destination programs of n such records (all IPv4, or all IPv6
  * with v6 = 1) in record order per (destination map, address pair): ret, reason, proxy,
- * nl, nu are the packet's final outputs, identity / ct the source program's.  The
- * caller exchanges the records between GPUs (RCCL all_to_all) and orders the calls so
- * every map sees its operations in packet order (cilium_amd/epnode.py). */
+ * nl, nu are the packet's final outputs, identity / ct the source program's.  Next to
+ * a map's max_entries both calls are admitted: creates succeed exactly as in packet
+ * (record) order within the call.  The caller exchanges the records between GPUs (RCCL
+ * all_to_all) and orders the calls so every map sees its operations in packet order
+ * (cilium_amd/epnode.py orders them per (map, peer), exact while maps have room). */
 #define CV_E_DEFER (-3)
 int cv_lxc_egress_split(cv_ctx *ctx, const cv_batch *b, const uint16_t *src_ep, uint32_t ep0,
                         const uint32_t *flow_hash, uint32_t now, cv_out *o, uint8_t *deliver, void *stream);

@@ -1307,8 +1307,12 @@ void group_stats(cv_ctx *c, const char *what, hipStream_t stream, bool flat)
         for (int q : {(int)Q_LB4, (int)Q_LB6, (int)Q_CT4, (int)Q_CT6}) {
             fprintf(stderr, "[cv groups] %s %s: largest %u; packets per member position:", what, qn[q],
                     cur[GMAX_WORD0 + q]);
-            for (uint32_t k = 0; k < NPOS; ++k) fprintf(stderr, " %u", cur[qcls(q, (int)k)]);
-            fprintf(stderr, " (the last: groups continued)\n");
+            uint32_t cont = 0;
+            for (uint32_t k = 0; k < 16; ++k) {
+                if (k + 1 < NPOS) fprintf(stderr, " %u", cur[qcls(q, (int)k)]);
+                else cont += cur[qcls(q, (int)k)];
+            }
+            fprintf(stderr, " %u (the last: groups continued)\n", cont);
         }
         return;
     }

@@ -2447,15 +2447,18 @@ __device__ __forceinline__ void for_each_run(const GroupScratch &g, int q, bool 
 }
 
 // fn(i) for member `pos` of every group of queue q (position lists, g.flat), in packet
-// order; the last list (pos = NPOS - 1) names runs: fn for their members from pos on.
+// order; the last lists (pos = NPOS - 1 .. 15, by size class) name runs: fn for their
+// members from pos on.
 // One call site of fn.
 template <class F>
 __device__ __forceinline__ void for_each_at(const GroupScratch &g, int q, uint32_t pos, F &&fn)
 {
     uint32_t base = 0;
     for (uint32_t l = 0; l < pos; ++l) base += g.cursor[qcls(q, l)];
-    const uint32_t total = g.cursor[qcls(q, pos)];
     const bool runs = pos + 1 == NPOS;
+    uint32_t total = g.cursor[qcls(q, pos)];
+    if (runs)                                                     // (the continuation: lists pos .. 15, one
+        for (uint32_t l = pos + 1; l < 16; ++l) total += g.cursor[qcls(q, l)];   //  per size class, in order)
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     for (uint32_t j = tid; j < total; j += stride) {
         const uint32_t e = g.work[base + j];

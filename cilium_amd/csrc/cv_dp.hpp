@@ -263,7 +263,8 @@ struct GroupScratch {          // address-pair grouping for conntrack (config 3)
     uint32_t *hcnt;            // per (list, tile) head counts -> positions (k_heads_count / place)
     uint32_t q4;               // the IPv4 queue the binned grouping fills (Q_NETDEV, or Q_LB4 / Q_CT4 on egress)
     uint32_t flat;             // 1: position lists (egress): list t < NPOS - 1 holds member t of every
-                               // group, list NPOS - 1 the runs of groups past NPOS - 1 members, in
+                               // group, lists NPOS - 1 .. 15 (by size class) the runs of groups past
+                               // NPOS - 1 members, in
                                // packet order (k_gbin_group -> k_heads_place)
     uint32_t pos;              // egress: the member position of the current launch pair
     uint4 *res;                // egress: per packet the packed final outputs of the scattered stages

@@ -1638,9 +1638,18 @@ __device__ __forceinline__ void gbin_mark(const GroupScratch &g, uint32_t key, u
     const uint32_t q6 = key & 1u;
     if (c > 8) atomicMax(&big[q6], c);
     if (g.flat) {
+        // member t < NPOS - 1 on list t; a group past NPOS - 1 members continues as a run
+        // on lists NPOS - 1 .. 15 by the size class of what is left of it, so a wave of the
+        // continuation launch takes runs of about one length (for_each_at)
         const uint32_t m = c < NPOS ? c : NPOS;
-        for (uint32_t t = 0; t < m; ++t)
-            g.hword[first[t]] = (1u + q6 * 16 + t) << 26 | (t + 1 == NPOS ? off : 0u);
+        for (uint32_t t = 0; t < m; ++t) {
+            uint32_t list = t;
+            if (t + 1 == NPOS) {
+                const uint32_t sc = (uint32_t)size_class(c - (NPOS - 1));
+                list = NPOS - 1 + (sc < 16 - NPOS ? sc : 16 - NPOS);
+            }
+            g.hword[first[t]] = (1u + q6 * 16 + list) << 26 | (t + 1 == NPOS ? off : 0u);
+        }
         return;
     }
     const uint32_t list = c > 1 ? 15 - (uint32_t)size_class(c) : 15u;   // 15: singletons (bit 25: a singleton)
@@ -2174,7 +2183,7 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
         const uint32_t hw = x < n ? g.hword[x] : 0u, h = hw >> 26;
         if (!h) continue;
         const uint32_t key = h - 1, q6 = key >> 4, at = atomicAdd(&pos[key], 1u);
-        if (g.flat) (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = (key & 15u) + 1 == NPOS ? (hw & ((1u << 25) - 1)) : x;
+        if (g.flat) (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = (key & 15u) + 1 >= NPOS ? (hw & ((1u << 25) - 1)) : x;
         else if ((key & 15u) == 15u) (q6 ? g.single6 : g.single)[at - start[q6 * 2 + 1]] = x;
         else (q6 ? g.work6 : g.work)[at - start[q6 * 2]] = hw & ((1u << 25) - 1);
     }

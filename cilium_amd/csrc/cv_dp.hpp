@@ -328,9 +328,11 @@ constexpr uint32_t BIG_MIN = CV_BIG_MIN, BIG_PCNT = 8, BIG_FILL = 8 + 256, BIGW 
 constexpr uint32_t SJOB_HEAD = 8, SJOB_PCNT = 16, SJOB_WORDS = 16 + 2 * 256;
 constexpr int EG_WORDS = 16;
 // position lists of the egress conntrack stage: one launch per member position, the last
-// one continuing the few groups past NPOS - 1 members (<= 16: the lists are k_heads' 16)
+// one continuing the groups past NPOS - 1 members (<= 16: the lists are k_heads' 16).  With
+// the continuation on lists by size class, 2 positions beat 3 and 4 (A/B on one box, per
+// step: 13.34 / 13.65 / 13.50 ms; round 4, one continuation list: 3 best)
 #ifndef CV_NPOS
-#define CV_NPOS 3
+#define CV_NPOS 2
 #endif
 constexpr uint32_t NPOS = CV_NPOS;
 constexpr uint32_t DEL_SLOTS = 4;                 // (64 B: one aligned half line per record)

@@ -203,8 +203,32 @@ struct Staging {                               // pinned host + device staging o
 
 }  // namespace
 
+// Test and measurement hooks, read once when the context opens (never per launch).
+// CV_SNAP_ABLATE is a timing-only ablation that makes undone egress passes wrong; it is
+// honoured only together with CV_TIMING_ONLY=1.
+struct Hooks {
+    bool coarse_groups = false;    // CV_COARSE_GROUPS: 8-bit group keys (merged runs, tests)
+    bool no_uni = false;           // CV_NO_UNI4: per-packet endpoint lines (tests)
+    bool eam_force = false;        // CV_EAM_FORCE: the many-map egress admission on one map (measurements)
+    bool egress_guarded = false;   // CV_EGRESS_GUARDED: planned launches instead of admission (tests)
+    bool snap_ablate = false;      // CV_SNAP_ABLATE + CV_TIMING_ONLY: no slot saved (timing only)
+    int eadm_max_passes = 8;       // CV_EADM_MAX_PASSES (tests of the fallback)
+    void read()
+    {
+        coarse_groups = getenv("CV_COARSE_GROUPS") != nullptr;
+        no_uni = getenv("CV_NO_UNI4") != nullptr;
+        eam_force = getenv("CV_EAM_FORCE") != nullptr;
+        egress_guarded = getenv("CV_EGRESS_GUARDED") != nullptr;
+        const char *t = getenv("CV_TIMING_ONLY");
+        snap_ablate = getenv("CV_SNAP_ABLATE") && t && !strcmp(t, "1");
+        const char *mp = getenv("CV_EADM_MAX_PASSES");
+        eadm_max_passes = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
+    }
+};
+
 struct cv_ctx {
     int device = 0;
+    Hooks hk;
     uint32_t flags = CV_F_DEFAULT;
     std::mutex mu;
     std::vector<std::unique_ptr<MapObj>> maps;
@@ -218,6 +242,7 @@ struct cv_ctx {
     cv_node_cfg node{};
     std::vector<Endpoint> eps;
     bool eps_dirty = true;
+    uint64_t eps_gen = 0;      // bumped by every endpoint change (map_table's cache key)
     DevBuf eps_dev, ephot_dev, ephot6_dev, ep_of_lxc;
     bool uni4_on = false;      // every endpoint on one policy + CT4 map, LXC_IPV4 set (DpParams::uni4)
     bool uni6_on = false;      // every endpoint on one policy + CT6 map (DpParams::uni6)
@@ -238,7 +263,7 @@ struct cv_ctx {
     uint32_t adm_stamp = 0;
     // the launch's CT maps as admission and the live-count reads see them (map_table)
     std::vector<MapObj *> mt_maps;
-    size_t mt_eps = ~(size_t)0;
+    uint64_t mt_eps = ~(uint64_t)0;   // (eps_gen the table was built at)
     DevBuf mt_live, mt_cap, mt_epmi4, mt_epmi6, mt_out;
     DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
     DevBuf eam_buf, eam_keys, eam_snap;  // (many CT maps: per-slot intents + budgets, walk keys, the slot set)
@@ -1112,7 +1137,7 @@ DpParams params(cv_ctx *c)
 {
     DpParams p{};
     p.flags = c->flags;
-    if (getenv("CV_COARSE_GROUPS")) p.flags |= F_TEST_COARSE_GROUPS;
+    if (c->hk.coarse_groups) p.flags |= F_TEST_COARSE_GROUPS;
     p.win_lo = 0;
     p.win_span = ~0u;
     p.n_eps = (uint32_t)c->eps.size();
@@ -1127,9 +1152,9 @@ DpParams params(cv_ctx *c)
     p.eps = c->eps_dev.as<EpDev>();
     p.ephot = c->ephot_dev.as<EpHot>();
     p.ephot6 = c->ephot6_dev.as<EpHot>();
-    p.uni4_on = c->uni4_on && !getenv("CV_NO_UNI4") ? 1u : 0u;
+    p.uni4_on = c->uni4_on && !c->hk.no_uni ? 1u : 0u;
     p.uni4 = c->uni4;
-    p.uni6_on = c->uni6_on && !getenv("CV_NO_UNI4") ? 1u : 0u;
+    p.uni6_on = c->uni6_on && !c->hk.no_uni ? 1u : 0u;
     p.uni6 = c->uni6;
     p.ep_of_lxc = c->ep_of_lxc.as<uint16_t>();
     p.metrics = c->metrics;
@@ -1497,7 +1522,7 @@ std::vector<MapObj *> batch_ct_maps(cv_ctx *c)
 // (per-endpoint maps: ConntrackLocal) and the batched live-count reads use.
 int map_table(cv_ctx *c, const std::vector<MapObj *> &maps)
 {
-    if (maps == c->mt_maps && c->mt_eps == c->eps.size()) return 0;
+    if (maps == c->mt_maps && c->mt_eps == c->eps_gen) return 0;
     if (maps.size() >= ADMIT_NO_MAP) return -E2BIG;
     std::unordered_map<const MapObj *, uint16_t> idx;
     std::vector<unsigned long long *> live(maps.size());
@@ -1520,7 +1545,7 @@ int map_table(cv_ctx *c, const std::vector<MapObj *> &maps)
         (r = c->mt_out.alloc(std::max<size_t>(1, maps.size()) * 8)))
         return r;
     c->mt_maps = maps;
-    c->mt_eps = c->eps.size();
+    c->mt_eps = c->eps_gen;
     return 0;
 }
 
@@ -1741,8 +1766,7 @@ int lxc_admitted(cv_ctx *c, const DpParams &p, const BatchDev &bc, const uint16_
                  const uint32_t *flow_hash, uint32_t now, const OutDev &oc, const std::vector<MapObj *> &cts,
                  hipStream_t s)
 {
-    const char *mp = getenv("CV_EADM_MAX_PASSES");             // (tests of the fallback)
-    const int MAX_PASSES = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
+    const int MAX_PASSES = c->hk.eadm_max_passes;              // (8; tests of the fallback lower it)
     const uint32_t n = bc.n;
     // the state a pass writes, and where its copy goes
     struct Region { void *src; size_t bytes, off; };
@@ -1860,8 +1884,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *
                       const std::vector<MapObj *> &cts, hipStream_t s,
                       const std::function<int(const DpParams &)> &launch, bool front, const char *what, int v6 = 0)
 {
-    const char *mp = getenv("CV_EADM_MAX_PASSES");
-    const int MAX_PASSES = mp && atoi(mp) >= 1 && atoi(mp) <= 64 ? atoi(mp) : 8;
+    const int MAX_PASSES = c->hk.eadm_max_passes;
     if (n > EAM_WINDOW) return -EINVAL;
     int r = map_table(c, cts);
     if (r) return r;
@@ -1932,7 +1955,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *
     Snap sn{};
     sn.log = c->eam_snap.as<uint4>();
     sn.cnt = reinterpret_cast<uint8_t *>(sn.log + scap * SNAP_U4);
-    sn.n = getenv("CV_SNAP_ABLATE") ? 0u : n;                      // (timing only: no slot saved, wrong undo)
+    sn.n = c->hk.snap_ablate ? 0u : n;                            // (timing only: no slot saved, wrong undo)
     sn.err = a.cnt + 4;
     if ((r = launch_gather_u64(c->mt_live.as<unsigned long long *const>(), live0, nm, s))) return r;
     a.next = bud[0];
@@ -1959,7 +1982,10 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *
              hipMemsetAsync(dst, 0xFF, 2 * nb, s) != hipSuccess ||
              hipMemcpyAsync(left2, bud[cur] + nb, nb, hipMemcpyDeviceToDevice, s) != hipSuccess))
             return -EIO;
-        if ((r = launch(pp))) return r;
+        if ((r = launch(pp))) {
+            if (sn.n) (void)launch_snap_clear(sn, s);
+            return r;
+        }
         a.used = bud[cur];
         a.used2 = bud[cur] + nb;
         a.next = bud[cur ^ 1];
@@ -1975,6 +2001,7 @@ int lxc_admitted_maps(cv_ctx *c, const DpParams &p, uint32_t n, const uint16_t *
         }
         if (w[2]) {
             fprintf(stderr, "[cv] egress admission pass %d: a create in a CT map outside the launch's\n", pass);
+            if (sn.n) (void)launch_snap_clear(sn, s);             // (no slot bit outlives the pass)
             return -EPROTO;
         }
         if ((r = launch_eam_walks(a, w[0], s))) return r;
@@ -2040,6 +2067,7 @@ int cv_open(int hip_device, cv_ctx **out)
     if (!out) return -EINVAL;
     cv_ctx *c = new cv_ctx();
     c->device = hip_device;
+    c->hk.read();
     for (int r = 0; r < CV_NUM_ROLES; ++r) { c->role[r] = -1; c->role_version[r] = 0; }
     if (hip_device == -1) {                 // host-only context: map store without a device
         *out = c;
@@ -2119,6 +2147,7 @@ int cv_map_close(cv_ctx *c, int h)
     if (c->device >= 0) (void)hipDeviceSynchronize();
     c->maps[h].reset(new MapObj());
     c->maps[h]->hm.reset(new HostMap(CV_MAP_HASH, 1, 1, 1, 0));
+    c->eps_gen++;                              // (a new map object may take the freed one's address)
     return 0;
 }
 
@@ -2351,6 +2380,7 @@ int cv_endpoint_add(cv_ctx *c, uint16_t lxc_id, uint32_t seclabel, int policy_ma
     }
     c->eps.push_back(Endpoint{lxc_id, seclabel, policy_map, ct4_map});
     c->eps_dirty = true;
+    c->eps_gen++;
     return (int)c->eps.size() - 1;
 }
 
@@ -2375,6 +2405,7 @@ int cv_endpoint_config(cv_ctx *c, int ep, const cv_endpoint_cfg *cfg)
     e.mac[0] = rd32(cfg->mac); e.mac[1] = rd16(cfg->mac + 4);
     e.node_mac[0] = rd32(cfg->node_mac); e.node_mac[1] = rd16(cfg->node_mac + 4);
     c->eps_dirty = true;
+    c->eps_gen++;
     return 0;
 }
 
@@ -2515,8 +2546,8 @@ int lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep
     }
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
-    const bool guarded = getenv("CV_EGRESS_GUARDED") != nullptr;   // (tests: the planned launches)
-    const bool one_map = egress_admissible(cts) && !getenv("CV_EAM_FORCE");   // (measurements: the many-map form)
+    const bool guarded = c->hk.egress_guarded;                    // (tests: the planned launches)
+    const bool one_map = egress_admissible(cts) && !c->hk.eam_force;   // (measurements: the many-map form)
     for (uint32_t off = 0, n; off < b->n; off += n) {     // sub-batches in packet order
         // a launch whose creates (at most 7 per packet) fit runs at full width; one that may
         // reach max_entries runs admitted: lxc_admitted with one CT map per family,
@@ -2607,7 +2638,7 @@ int cv_lxc_deliver(cv_ctx *c, const uint8_t *records, uint32_t n, int v6, uint32
     if ((r = set_device(c)) || (r = sync_locked(c, (hipStream_t)stream))) return r;
     StreamScope scope(c, (hipStream_t)stream);
     const uint32_t cmax = std::min(n, c->chunk);
-    if ((r = ensure_groups(c, std::max<uint32_t>(cmax, 1), false))) return r;
+    if ((r = ensure_groups(c, std::max<uint32_t>(cmax, 1), true))) return r;   // (gres / gdel_ev: egress scratch)
     std::set<const void *> seen;
     std::vector<HashTable> pols;
     for (auto &e : c->eps) {
@@ -2616,7 +2647,7 @@ int cv_lxc_deliver(cv_ctx *c, const uint8_t *records, uint32_t n, int v6, uint32
     }
     DpParams p = params(c);
     const std::vector<MapObj *> cts = batch_ct_maps(c);
-    const bool guarded = getenv("CV_EGRESS_GUARDED") != nullptr;
+    const bool guarded = c->hk.egress_guarded;
     for (uint32_t off = 0, m; off < n; off += m) {
         // a record creates at most the tuple and its ICMP twin in its destination's map: a
         // launch that surely fits runs whole, else admitted (lxc_admitted_maps with the

@@ -1066,7 +1066,9 @@ __device__ __forceinline__ void snap_slot(const Snap &sn, const HashTable &t, in
     const uint32_t prev = __hip_atomic_fetch_or(bw + SPARE, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t hot = (want & ~prev) & (1u << s), cold_new = (want & ~prev) & (1u << (8 + s));
     if (!hot && !cold_new) return;                                // (saved before in this pass)
-    if (a.scnt >= SNAP_PER || a.spkt >= sn.n) {
+    if (a.scnt >= SNAP_PER || a.spkt >= sn.n) {                  // (no log entry: the bits go back, so no
+        __hip_atomic_fetch_and(bw + SPARE, ~(want & ~prev), __ATOMIC_RELAXED,   //  later pass skips the slot)
+                               __HIP_MEMORY_SCOPE_AGENT);
         atomicOr(sn.err, 1u);
         return;
     }

@@ -85,7 +85,7 @@ class OMap:
         self.h = lib().or_map_create(type_, key_size, val_size, max_entries)
         if not self.h:
             raise ValueError("or_map_create failed")
-        self.ks, self.vs = key_size, val_size
+        self.ks, self.vs, self.max_entries = key_size, val_size, max_entries
 
     @classmethod
     def from_spec(cls, spec):

@@ -30,6 +30,10 @@ import numpy as np
 from cilium_amd import synth
 
 DEFER = -3                      # OR_E_DEFER
+# the most CT entries one operation creates in its map: a source program its service entry,
+# the tuple, its ICMP twin and the NAT tuple (lb4_local, ct_create4: lb.h:700-775,
+# conntrack.h:663-744) -- 7 bounds it as cv_lxc_egress does; a delivery the tuple and its twin
+MAX_CREATES = (7, 2)
 
 
 def per_endpoint_dp(w: synth.Workload):
@@ -104,6 +108,7 @@ class RankState:
         # (packet, source before delivery): the order the sequential run applies them in
         self.pending = {e: sorted(v, key=lambda o: (o[0], o[1])) for e, v in ops.items()}
         self.resolved = {}                       # (packet, endpoint) -> delivery record or None
+        self.v6 = (w.frames[:, 12] == 0x86) & (w.frames[:, 13] == 0xDD)   # (the op's map: CT6, else CT4)
         self.out = {k: np.zeros(w.n, np.int64) for k in self.FIELDS}
         self.mine = np.zeros(w.n, bool)          # outputs final on this rank
         self.cross = 0                           # deliveries whose source ran on another rank
@@ -142,21 +147,36 @@ class RankState:
         if int(self.w.extra["src_ep"][i]) % self.world != self.rank:
             self.cross += 1
 
+    def _tight(self, e):
+        """per family, whether endpoint e's CT map may reach max_entries with the creates its
+        pending operations may still make (MAX_CREATES per operation kind): then the creates
+        of different peers compete for the room, and the map's operations keep packet order
+        across all peers (conntrack.h:692-693: a create that finds the map full fails)"""
+        v6 = self.v6
+        need = [0, 0]
+        for i, kind, _ in self.pending[e]:
+            need[int(v6[i])] += MAX_CREATES[kind]
+        return [len(self.maps[f][e]) + need[k] > self.maps[f][e].max_entries for k, f in enumerate(("ct4", "ct6"))]
+
     def progress(self):
         """local operations until every owned map waits; returns {rank: records}.  A map's
         operation runs once every earlier operation of that map sharing a peer with it
-        has run (a delivery whose source program has not run yet blocks its peers)."""
+        has run (a delivery whose source program has not run yet blocks its peers); on a
+        map that may fill (`_tight`), once every earlier operation of the map has run."""
         outbox = {}
         moved = True
         while moved:
             moved = False
             for e in self.owned:
                 blocked, left = set(), []
+                tight, stop = self._tight(e), [False, False]
                 for op in self.pending[e]:
                     i, kind, pe = op
+                    fam = int(self.v6[i])
                     ready = kind == 0 or (i, e) in self.resolved
-                    if not ready or (pe & blocked):
+                    if not ready or (pe & blocked) or stop[fam]:
                         blocked |= pe
+                        stop[fam] |= tight[fam]
                         left.append(op)
                         continue
                     if kind == 0:

@@ -65,6 +65,24 @@ def test_endpoint_owned_ct_simulated(world):
     assert rounds < w.n // 32                                      # rounds follow reply chains, not packets
 
 
+def test_endpoint_owned_ct_at_capacity():
+    """Maps sized so half of them fill within the batch (DROP_CT_CREATE_FAILED): the
+    creates of different peers of one map compete for its room, so a map that may fill
+    keeps packet order over all its operations (ep_shard.RankState._tight) -- ordering
+    per (map, peer) alone differed from the sequential run in 48 of 4 096 packets."""
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=0xE5, vip_frac=0.5)
+    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+    _, _, m0 = _sequential(w)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    cap = int(sizes[len(sizes) // 2])
+    w = synth.config5(1 << 12, ct_max=cap, **kw)
+    results, rounds = E.simulate(w, 2, w.now)
+    _check(w, results, 2)
+    _, dp, maps = _sequential(w)
+    full = sum(len(m) >= cap for fam in ("ct4", "ct6") for m in maps[fam])
+    assert full >= 8 and dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0, full
+
+
 def test_candidates_cover_every_delivery():
     w = _workload(seed=0xE6)
     dp, _ = E.per_endpoint_dp(w)

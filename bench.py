@@ -342,6 +342,12 @@ def main():
     ap.add_argument("--ep-zipf", type=float, default=None,
                     help="configs 3/4: Zipf(a) popularity of the endpoints the preloaded flows belong to; config 5: "
                          "of the flows' client endpoints (with --ct-local: the busiest endpoints' maps are full)")
+    ap.add_argument("--ep-owned", action="store_true",
+                    help="config 5 as ONE node across the ranks with endpoint-owned conntrack (cilium_amd.epnode, "
+                         "include/cilium_epnode.h): every endpoint its own CT4 / CT6 map (--ct-local, default 64000), "
+                         "rank r runs the source programs of the endpoints e %% N == r and the deliveries into them, "
+                         "records exchanged per round (RCCL all_to_all); every rank holds the whole batch "
+                         "(--packets, default 2^20) and the node processes it once per step")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend at N > 1 (nccl = RCCL)")
     ap.add_argument("--dump", default=None,
                     help="test hook: every rank writes <dir>/rank<r>.npz (its packets' address-pair keys, its "
@@ -371,6 +377,8 @@ def main():
     cvbuild.build()
     from tests import harness as H
 
+    if args.ep_owned:
+        return ep_owned(args, rank, world, local, device, dist, out_fd)
     name = args.workload
     stateful = name in STATEFUL
     passes = args.warmup + args.steps + 1                          # + the accounting step after the timed ones
@@ -623,6 +631,123 @@ def main():
                     "gc_step_s": args.gc_step, "gc_deleted_in_timed_steps": gc_timed,
                     "how": "now advances gc_step seconds per step; ctmap.GC(GCFilterByTime, now) runs before "
                            "every step inside the timed region"}
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def ep_owned(args, rank, world, local, device, dist, out_fd):
+    """config 5 as one node across the ranks: a step = the node's rounds over
+    one fresh batch -- the scheduler's build (candidates, peers, operations: cv_epnode_open)
+    and every round's launches, exchanges and host waits, inside the timed region; the
+    batch's records already in HBM and its host copy (what the scheduler reads) built before."""
+    import torch
+    from cilium_amd import epnode, synth
+    from tests import harness as H
+    if args.workload != "config5":
+        raise SystemExit("--ep-owned: config 5")
+    n = args.packets if args.packets != 1 << 24 else 1 << 20
+    cap = args.ct_local or 64000
+    t0 = time.time()
+    w = synth.config5(n, ep_zipf=args.ep_zipf)
+    per4 = synth.per_endpoint_ct(w, cap)
+    per6 = synth.per_endpoint_ct(w, cap, "ct6")
+    ctx, maps = H.product_ctx(w, device=local, ct_per_ep=per4, ct6_per_ep=per6)
+    metrics_t = torch.zeros(2048, dtype=torch.int64, device=device)
+    ctx.metrics_attach(metrics_t)
+    log(f"[rank {rank}] ep-owned config 5: {n} packets, {len(w.endpoints)} endpoints, tables compiled "
+        f"({time.time() - t0:.1f}s)")
+    xdev = device if args.dist_backend == "nccl" else None         # (gloo: the exchange over host tensors)
+    exchange, all_sum = epnode.dist_exchange(world, rank, xdev) if dist else (None, None)
+    passes = args.warmup + args.steps + 1
+    v6, _ = epnode.families(w.frames)
+    batches = []
+    for v in range(1, passes + 1):                                 # (fresh client ports per step, built untimed)
+        f = H.apply_variant(w.frames, *synth.port_variant(w, v))
+        parts = []
+        for sel, stride in ((~v6, 64), (v6, 128)):
+            idx = np.nonzero(sel)[0]
+            parts.append({"frames": torch.from_numpy(np.ascontiguousarray(f[idx, :stride])).to(device),
+                          "length": to_device(w.length[idx].astype(np.uint32), device),
+                          "src_ep": to_device(w.extra["src_ep"][idx].astype(np.uint16), device),
+                          "flow_hash": to_device(w.extra["flow_hash"][idx].astype(np.uint32), device)})
+        batches.append((f, parts))
+    log(f"[rank {rank}] {passes} step batches built ({time.time() - t0:.1f}s)")
+
+    def step(v):
+        f, parts = batches[v - 1]
+        node = epnode.EpNode(ctx, rank, world, f, w.length, w.extra["src_ep"], w.extra["flow_hash"], device=device,
+                             exchange=exchange, all_sum=all_sum, parts=parts)
+        t = time.perf_counter()
+        node.run(w.now + v)
+        return node, time.perf_counter() - t
+
+    v = 1
+    for _ in range(args.warmup):
+        step(v)
+        v += 1
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    stats, t_run, t_start = [], 0.0, time.perf_counter()
+    for _ in range(args.steps):
+        node, tr = step(v)
+        t_run += tr
+        stats.append((node.rounds, node.launches, node.cross, node.sched.stats()))
+        v += 1
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    # accounting step (untimed): L(p), U(p) of the packets each rank finished
+    node, _ = step(v)
+    out, idx = node.results()
+    rec = np.where(v6[idx], 128, 64)
+    alg = int((rec + 9).sum()) + 64 * int(out["nl"].sum() + out["nu"].sum())
+    full = sum(len(m) >= cap for m in list(maps["ct4_ep"]) + list(maps["ct6_ep"]))
+    if dist:
+        t = torch.tensor([elapsed, t_run], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, t_run = float(t[0]), float(t[1])
+        a = torch.tensor([alg, sum(s[2] for s in stats), full], dtype=torch.int64, device=device)
+        dist.all_reduce(a)
+        alg, cross, full = (int(x) for x in a.cpu())
+        dist.all_reduce(metrics_t)
+    else:
+        cross = sum(s[2] for s in stats)
+    ms = elapsed * 1e3 / args.steps
+    achieved = alg / (ms * 1e-3) / 1e9
+    if rank == 0:
+        rounds = [s[0] for s in stats]
+        line = {
+            "metric": METRIC, "value": round(n * args.steps / elapsed / 1e6, 3), "unit": "Mpps", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (SplitMix64), tables + headers resident in HBM",
+            "config": {
+                "workload": "config5 as ONE node across the ranks: endpoint-owned conntrack (ConntrackLocal, every "
+                            "endpoint its own CT4 / CT6 map), source programs on the source's rank, deliveries on "
+                            "the destination's, records exchanged per round",
+                "packets_per_step_node": n, "endpoints": len(w.endpoints), "services": 50000,
+                "parallelism": f"{world} rank(s), endpoints e % {world} == rank, one batch per node per step",
+                "ct_local": {"maps": len(per4) + len(per6), "max_entries_per_map": cap, "ep_zipf": args.ep_zipf,
+                             "full_maps_after": full}},
+            "ep_owned": {
+                "rounds_per_step": [min(rounds), max(rounds)],
+                "launches_per_step_rank0": [min(s[1] for s in stats), max(s[1] for s in stats)],
+                "cross_rank_deliveries_per_step": cross // max(args.steps, 1),
+                "maps_ordered_whole_first_round_rank0": stats[-1][3]["maps_ordered_whole_at_open"],
+                "run_ms_per_step": round(t_run * 1e3 / args.steps, 3),
+                "schedule_build_ms_per_step": round(ms - t_run * 1e3 / args.steps, 3),
+                "how": "bench.ep_owned: step = cv_epnode_open (candidates, peers, operations) + EpNode.run "
+                       "(per round: split launches, exchange, delivery launches; one host wait)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "algorithmic_bytes_per_step": alg,
+                         "note": "whole node step (host-driven rounds), not one kernel"},
+            "cpu_baseline": None,
+        }
         os.write(out_fd, (json.dumps(line) + "\n").encode())
     if dist:
         dist.destroy_process_group()

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libcilium_hip.so")
-SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip", "cv_sort.hip", "cv_agent.cpp"]
+SOURCES = ["cv_ctx.cpp", "cv_kernels.hip", "cv_egress.hip", "cv_sort.hip", "cv_agent.cpp", "cv_epnode.cpp"]
 ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 
 
@@ -33,7 +33,7 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [os.path.join(SRC, f) for f in os.listdir(SRC)] + [os.path.join(HERE, "..", "include", "cilium_hip.h")]
+    deps = [os.path.join(SRC, f) for f in os.listdir(SRC)] + [os.path.join(HERE, "..", "include", h) for h in ("cilium_hip.h", "cilium_agent.h", "cilium_epnode.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

@@ -25,6 +25,7 @@
 #include "../../include/cilium_hip.h"
 #include "cv_dp.hpp"
 #include "cv_hostmap.hpp"
+#include "cv_node.hpp"
 
 using namespace cv;
 
@@ -2057,6 +2058,75 @@ void policy_counters(MapObj *mo, const uint8_t *key, uint8_t *val)
 
 }  // namespace
 
+// ================================================== the node view (cv_node.hpp)
+namespace cv {
+
+int node_view(cv_ctx *c, NodeView &v)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    v.eps.clear();
+    v.svc.clear();
+    for (const Endpoint &e : c->eps) {
+        NodeEndpoint ne{};
+        ne.ipv4 = e.ipv4;
+        memcpy(ne.ipv6, e.ipv6, 16);
+        ne.ct4 = e.ct4;
+        ne.ct6 = e.ct6;
+        v.eps.push_back(ne);
+    }
+    // the slave entries (slave != 0) of the service maps name the backends (lb.h:43-81)
+    for (int fam = 0; fam < 2; ++fam) {
+        MapObj *m = get(c, c->role[fam ? CV_ROLE_LB6_SERVICES : CV_ROLE_LB4_SERVICES]);
+        if (!m) continue;
+        const uint32_t alen = fam ? 16 : 4;
+        m->hm->for_each([&](const uint8_t *k, const uint8_t *val) {
+            if (!(k[alen + 2] | k[alen + 3])) return;
+            NodeService ns{};
+            ns.v6 = (uint8_t)fam;
+            memcpy(ns.vip, k, alen);
+            memcpy(ns.backend, val, alen);
+            v.svc.push_back(ns);
+        });
+    }
+    v.loopback = c->node.ipv4_loopback;
+    return 0;
+}
+
+int ct_counts(cv_ctx *c, const std::vector<int> &handles, std::vector<uint64_t> &live, std::vector<uint64_t> &cap)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    std::vector<MapObj *> ms;
+    for (int h : handles) {
+        MapObj *m = get(c, h);
+        if (!m) return -EBADF;
+        ms.push_back(m);
+    }
+    if (c->device < 0) {                                          // (host-only context: the host store)
+        live.resize(ms.size());
+        cap.resize(ms.size());
+        for (size_t k = 0; k < ms.size(); ++k) {
+            live[k] = ms[k]->hm->count();
+            cap[k] = ms[k]->hm->max_entries;
+        }
+        return 0;
+    }
+    if (set_device(c)) return -ENODEV;
+    for (MapObj *m : ms)
+        if (m->kind == MK_PLAIN) return -EINVAL;
+    refresh_live(c, ms);
+    live.resize(ms.size());
+    cap.resize(ms.size());
+    for (size_t k = 0; k < ms.size(); ++k) {
+        live[k] = ms[k]->live_upper;
+        cap[k] = ms[k]->cap;
+    }
+    return 0;
+}
+
+}  // namespace cv
+
 // ======================================================================= C-ABI
 extern "C" {
 
@@ -2372,9 +2442,9 @@ int cv_endpoint_add(cv_ctx *c, uint16_t lxc_id, uint32_t seclabel, int policy_ma
     if (p && (p->hm->ks != 8 || p->hm->vs != 24 || p->hm->is_lpm())) return -EINVAL;
     if (t && (t->hm->ks != 14 || t->hm->vs != 56 || t->hm->is_lpm())) return -EINVAL;
     for (auto &e : c->eps) if (e.lxc_id == lxc_id) return -EEXIST;
-    if (set_device(c)) return -ENODEV;
+    if (c->device >= 0 && set_device(c)) return -ENODEV;   // (host-only: the endpoint table alone)
     if (p && !p->is_policy) { p->is_policy = true; p->pol_version = 0; }
-    if (t && t->kind != MK_CT4) {
+    if (t && t->kind != MK_CT4 && c->device >= 0) {
         int r = compile_ct(c, t);
         if (r) return r;
     }
@@ -2392,7 +2462,7 @@ int cv_endpoint_config(cv_ctx *c, int ep, const cv_endpoint_cfg *cfg)
     MapObj *t6 = cfg->ct6_map >= 0 ? get(c, cfg->ct6_map) : nullptr;
     if (cfg->ct6_map >= 0 && !t6) return -EBADF;
     if (t6 && (t6->hm->ks != 40 || t6->hm->vs != 56 || t6->hm->is_lpm())) return -EINVAL;
-    if (t6 && t6->kind != MK_CT6) {
+    if (t6 && t6->kind != MK_CT6 && c->device >= 0) {
         if (t6->kind != MK_PLAIN) return -EINVAL;
         if (set_device(c)) return -ENODEV;
         int r = compile_ct6(c, t6);

@@ -2189,6 +2189,23 @@ __global__ void __launch_bounds__(1024) k_heads_place(GroupScratch g, uint32_t n
     }
 }
 
+// test hook (CV_JOB_INJECT): one split-key job more counted than the grouping wrote, its
+// run word past `order` -- the r05 fault's shape (an egress launch's two groupings once
+// shared the job count, so the second read the first's jobs); k_gbin_marks must skip it
+// and report it (-EPROTO at the context's next call), never index through it
+__global__ void k_job_inject(GroupScratch g)
+{
+    if (threadIdx.x) return;
+    const uint32_t j = g.cursor[SJOB_WORD];
+    if (j >= g.sjob_cap) return;
+    uint32_t *job = g.sjob + (size_t)j * SJOB_WORDS;
+    job[0] = 0u;
+    job[1] = 2u;
+    job[2] = 0xFFFFFFF0u;
+    job[3] = 1u;
+    g.cursor[SJOB_WORD] = j + 1u;
+}
+
 void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
 {
     const uint32_t nb = 1u << g.gbits, m = nb * GBLK;
@@ -2201,6 +2218,7 @@ void launch_gbin_groups(const GroupScratch &g, uint32_t n, hipStream_t s)
     hipLaunchKernelGGL(k_gbig_place, dim3(512), dim3(256), 0, s, g, n);
     hipLaunchKernelGGL(k_gbin_group, dim3(nb), dim3(256), 0, s, g, n);
     hipLaunchKernelGGL(k_gbin_tiles, dim3(1024), dim3(256), 0, s, g);   // (split keys: elephant pairs)
+    if (getenv("CV_JOB_INJECT")) hipLaunchKernelGGL(k_job_inject, dim3(1), dim3(64), 0, s, g);
     hipLaunchKernelGGL(k_gbin_marks, dim3(8), dim3(256), 0, s, g);
     const uint32_t tiles = (n + HTILE - 1) / HTILE;
     hipLaunchKernelGGL(k_heads_count, dim3(tiles), dim3(1024), 0, s, g, n, tiles);

@@ -1,0 +1,37 @@
+// cv_node.hpp — what the endpoint-owned node's scheduler (cv_epnode.cpp) reads from a
+// context: the endpoints' addresses and CT maps, the service table's VIP -> backend
+// pairs and the loopback address, as the agent wrote them (host images), and the live
+// counts of conntrack maps (device-authoritative).  Internal to the library.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+struct cv_ctx;
+
+namespace cv {
+
+struct NodeEndpoint {
+    uint32_t ipv4;             // LXC_IPV4, raw network-order word (0: none)
+    uint8_t ipv6[16];          // LXC_IP (all zero: none)
+    int ct4, ct6;              // CT_MAP4 / CT_MAP6 handles (-1: none)
+};
+
+// one slave entry of cilium_lb{4,6}_services (lb.h:43-81): the VIP and one backend
+struct NodeService {
+    uint8_t v6;
+    uint8_t vip[16];           // v4: first 4 bytes
+    uint8_t backend[16];
+};
+
+struct NodeView {
+    std::vector<NodeEndpoint> eps;
+    std::vector<NodeService> svc;
+    uint32_t loopback = 0;     // IPV4_LOOPBACK, raw network-order word
+};
+
+int node_view(cv_ctx *c, NodeView &v);
+// live entries and max_entries of CT maps (after every batch already submitted: a sync)
+int ct_counts(cv_ctx *c, const std::vector<int> &handles, std::vector<uint64_t> &live, std::vector<uint64_t> &cap);
+
+}  // namespace cv

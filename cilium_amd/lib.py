@@ -1,4 +1,5 @@
-"""ctypes binding of the product library (include/cilium_hip.h, include/cilium_agent.h).
+"""ctypes binding of the product library (include/cilium_hip.h, include/cilium_agent.h,
+include/cilium_epnode.h).
 
 The library is the HIP path; there is no CPU fallback.  ``load()`` raises when
 ``cilium_amd/_lib/libcilium_hip.so`` is missing (build it with
@@ -16,7 +17,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CV_LIB") or os.path.join(HERE, "_lib", "libcilium_hip.so")   # CV_LIB: A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "cilium_hip.h")
-HEADERS = [HEADER, os.path.join(os.path.dirname(HERE), "include", "cilium_agent.h")]
+HEADERS = [HEADER] + [os.path.join(os.path.dirname(HERE), "include", h) for h in ("cilium_agent.h", "cilium_epnode.h")]
 
 MAP_HASH, MAP_LRU_HASH, MAP_LPM_TRIE, MAP_PERCPU_HASH = 1, 9, 11, 5
 BPF_F_NO_PREALLOC = 1
@@ -128,6 +129,15 @@ def load():
         "cv_policy_sync_set_desired": (i32, [vp, vp, vp, u32]),
         "cv_policy_sync_run": (i32, [vp, vp, i32, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]),
         "cv_policy_sync_realized": (i32, [vp, vp, vp, u32]),
+        "cv_epnode_open": (i32, [vp, u32, u32, vp, u32, u32, vp, C.POINTER(vp)]),
+        "cv_epnode_close": (None, [vp]),
+        "cv_epnode_pending": (u64, [vp]),
+        "cv_epnode_set_counts": (i32, [vp, vp, vp]),
+        "cv_epnode_stats": (i32, [vp, vp]),
+        "cv_epnode_sources": (i32, [vp, vp, u32]),
+        "cv_epnode_sources_done": (i32, [vp, vp, vp, u32, vp, vp, vp, vp, vp, u32]),
+        "cv_epnode_receive": (i32, [vp, vp, vp, vp, u32, vp]),
+        "cv_epnode_deliveries": (i32, [vp, vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("CV_LIB") and not hasattr(L, name):
@@ -519,3 +529,96 @@ class PolicySync:
         if self.h:
             self.L.cv_policy_sync_free(self.h)
             self.h = None
+
+
+# ---------------------------------------------------------------- endpoint-owned node (include/cilium_epnode.h)
+class EpSched:
+    """The round scheduler of one rank of the endpoint-owned node (cv_epnode_*): host
+    arrays in, host arrays out; the batch, the records and the outputs stay on the
+    device (cilium_amd.epnode.EpNode drives the launches)."""
+
+    STATS = ("rounds", "source_ops", "delivery_ops", "maps_ordered_whole_at_open", "maps_ordered_whole_now",
+             "rows_sent")
+
+    def __init__(self, ctx, rank, world, frames, src_ep):
+        self.L, self.world = load(), world
+        frames = np.ascontiguousarray(frames, np.uint8)
+        src = np.ascontiguousarray(src_ep, np.uint16)
+        self.n = len(src)
+        h = C.c_void_p()
+        _check(self.L.cv_epnode_open(ctx.h, rank, world, frames.ctypes.data, frames.shape[1], self.n, src.ctypes.data,
+                                     C.byref(h)), "cv_epnode_open")
+        self.h = h
+        self._pk = np.zeros(max(self.n, 1), np.uint32)
+
+    COUNTS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint64),
+                            C.POINTER(C.c_uint64))
+
+    def set_counts(self, fn):
+        """fn(handles) -> (live, max_entries) lists: the CT maps' counts from the caller"""
+        def cb(_, hs, n, live, cap):
+            try:
+                lv, cp = fn([hs[i] for i in range(n)])
+                for i in range(n):
+                    live[i], cap[i] = int(lv[i]), int(cp[i])
+                return 0
+            except Exception:
+                return -5
+        self._cb = self.COUNTS_FN(cb)
+        _check(self.L.cv_epnode_set_counts(self.h, C.cast(self._cb, C.c_void_p), None), "cv_epnode_set_counts")
+
+    def pending(self):
+        return int(self.L.cv_epnode_pending(self.h))
+
+    def stats(self):
+        a = np.zeros(6, np.uint64)
+        _check(self.L.cv_epnode_stats(self.h, a.ctypes.data), "cv_epnode_stats")
+        return dict(zip(self.STATS, (int(x) for x in a)))
+
+    def sources(self):
+        k = _check(self.L.cv_epnode_sources(self.h, self._pk.ctypes.data, self.n), "cv_epnode_sources")
+        return self._pk[:k].copy()
+
+    def sources_done(self, pkts, dst):
+        """the exchange rows of the launched packets: (row_pkt, row_ep, row_has, row_pos,
+        rank_rows), sorted by owner rank"""
+        pkts = np.ascontiguousarray(pkts, np.uint32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        cap = 2 * len(pkts) + 64
+        while True:
+            rp, re_, rpos = (np.zeros(cap, np.uint32) for _ in range(3))
+            rh = np.zeros(cap, np.uint8)
+            rr = np.zeros(self.world, np.uint32)
+            k = self.L.cv_epnode_sources_done(self.h, pkts.ctypes.data, dst.ctypes.data, len(pkts), rp.ctypes.data,
+                                              re_.ctypes.data, rh.ctypes.data, rpos.ctypes.data, rr.ctypes.data, cap)
+            if k != -28:                                   # (-ENOSPC: more candidates than rows; nothing written)
+                break
+            cap *= 4
+        _check(k, "cv_epnode_sources_done")
+        return rp[:k], re_[:k], rh[:k], rpos[:k], rr
+
+    def receive(self, row_pkt, row_ep, row_has):
+        row_pkt = np.ascontiguousarray(row_pkt, np.uint32)
+        row_ep = np.ascontiguousarray(row_ep, np.uint32)
+        row_has = np.ascontiguousarray(row_has, np.uint8)
+        op = np.zeros(max(len(row_pkt), 1), np.int32)
+        _check(self.L.cv_epnode_receive(self.h, row_pkt.ctypes.data, row_ep.ctypes.data, row_has.ctypes.data,
+                                        len(row_pkt), op.ctypes.data), "cv_epnode_receive")
+        return op[:len(row_pkt)]
+
+    def deliveries(self, cap):
+        ops = np.zeros(max(cap, 1), np.uint32)
+        pk = np.zeros(max(cap, 1), np.uint32)
+        k = _check(self.L.cv_epnode_deliveries(self.h, ops.ctypes.data, pk.ctypes.data, cap), "cv_epnode_deliveries")
+        return ops[:k], pk[:k]
+
+    def close(self):
+        if self.h:
+            self.L.cv_epnode_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

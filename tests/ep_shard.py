@@ -25,6 +25,9 @@ cross-rank request / reply alternations within one address pair, not with the ba
 """
 from __future__ import annotations
 
+import struct
+from typing import Dict, List, Sequence
+
 import numpy as np
 
 from cilium_amd import synth
@@ -63,25 +66,94 @@ def per_endpoint_dp(w: synth.Workload):
     return dp, maps
 
 
+# the prototype's node tables, candidates and peers (the product's are cv_epnode.cpp's,
+# from the context's own tables; test_ep_sched_matches_prototype compares them)
+def node_tables(endpoints: Sequence[dict], services: Dict[str, tuple]):
+    """address -> local endpoints; VIP -> backend addresses; backend address -> VIPs.
+    services: {"lb4_services": (keys, vals), "lb6_services": (keys, vals)} as the agent
+    wrote them (lb4_key / lb4_service, lb.h): slave entries (slave != 0) name backends."""
+    where, backends, vips = {}, {}, {}
+    for idx, e in enumerate(endpoints):
+        if e.get("ip"):
+            where.setdefault(struct.pack(">I", e["ip"]), set()).add(idx)
+        if e.get("ip6") and any(e["ip6"]):
+            where.setdefault(bytes(e["ip6"]), set()).add(idx)
+    for name, alen in (("lb4_services", 4), ("lb6_services", 16)):
+        if name not in services:
+            continue
+        keys, vals = services[name]
+        slave = keys[:, alen + 2] | (keys[:, alen + 3].astype(np.int64) << 8)
+        for k, v in zip(keys[slave > 0], vals[slave > 0]):
+            vip, be = bytes(k[:alen]), bytes(v[:alen])
+            backends.setdefault(vip, set()).add(be)
+            vips.setdefault(be, set()).add(vip)
+    return where, backends, vips
+
+
+def _addrs(f):
+    """(saddr, daddr) bytes of a frame, or None"""
+    if f[12] == 0x08 and f[13] == 0x00:
+        return bytes(f[26:30]), bytes(f[30:34])
+    if f[12] == 0x86 and f[13] == 0xDD:
+        return bytes(f[22:38]), bytes(f[38:54])
+    return None
+
+
+def candidates_of(frames: np.ndarray, tables) -> List[frozenset]:
+    """per packet, the endpoints its source program may deliver it to (a superset): the
+    destination address's endpoint, or the local backends of the VIP it is"""
+    where, backends, _ = tables
+    out = []
+    for f in frames:
+        a = _addrs(f)
+        c = set()
+        if a is not None:
+            c |= where.get(a[1], set())
+            for be in backends.get(a[1], ()):
+                c |= where.get(be, set())
+        out.append(frozenset(c))
+    return out
+
+
+def peers_of(frames: np.ndarray, tables, loopback: int):
+    """per packet, the peer addresses of the CT entries its source program (on the
+    source's map) and its delivery (on the destination's map) may touch -- supersets.
+    The source program's peer is the destination address, or a VIP's backends (its
+    service entry, the translated connection, the NAT tuple) and, when the client backs
+    the VIP itself, the loopback address; the delivery's is the source address as the
+    source program left it: the original, a VIP (reverse NAT of a backend's reply) or the
+    loopback address."""
+    _, backends, vips = tables
+    lob = struct.pack(">I", loopback) if loopback else b""
+    src_p, dst_p = [], []
+    for f in frames:
+        a = _addrs(f)
+        if a is None:
+            src_p.append(frozenset())
+            dst_p.append(frozenset())
+            continue
+        loop = lob and a[0] in backends.get(a[1], ())                # a VIP the client itself backs
+        sp = {a[1]} | backends.get(a[1], set()) | ({lob} if loop else set())
+        dp = {a[0]} | vips.get(a[0], set()) | ({lob} if loop else set())
+        src_p.append(frozenset(sp))
+        dst_p.append(frozenset(dp))
+    return src_p, dst_p
+
+
 def _tables(w: synth.Workload):
-    from cilium_amd import epnode
-    return epnode.node_tables(w.endpoints, {k: (w.maps[k].keys, w.maps[k].vals) for k in ("lb4_services", "lb6_services")
-                                            if k in w.maps})
+    return node_tables(w.endpoints, {k: (w.maps[k].keys, w.maps[k].vals) for k in ("lb4_services", "lb6_services")
+                                     if k in w.maps})
 
 
 def candidates(w: synth.Workload):
-    """per packet, the endpoints its source program may deliver it to (a superset:
-    cilium_amd.epnode.candidates, shared with the HIP form)"""
-    from cilium_amd import epnode
-    return epnode.candidates(w.frames, _tables(w))
+    """per packet, the endpoints its source program may deliver it to (a superset)"""
+    return candidates_of(w.frames, _tables(w))
 
 
 def peers(w: synth.Workload):
-    """per packet, the peer addresses its source program and its delivery may touch
-    (supersets: cilium_amd.epnode.peers, shared with the HIP form)"""
-    from cilium_amd import epnode
+    """per packet, the peer addresses its source program and its delivery may touch (supersets)"""
     lo = w.extra.get("node", {}).get("loopback", 0) if w.extra else 0
-    return epnode.peers(w.frames, _tables(w), lo)
+    return peers_of(w.frames, _tables(w), lo)
 
 
 class RankState:

@@ -142,3 +142,151 @@ def test_endpoint_owned_ct_two_ranks_gloo():
         assert p.exitcode == 0
     w = _workload()
     _check(w, results, 2)
+
+
+# ---------------------------------------------------------------- the product scheduler (cv_epnode)
+def host_node_ctx(w):
+    """a host-only context (cv_open(-1)) holding w's service tables, endpoints with their
+    own CT4 / CT6 maps and node config: what cv_epnode_open reads"""
+    from cilium_amd import lib
+    ctx = lib.Ctx(-1)
+    for name in ("lb4_services", "lb6_services"):
+        if name in w.maps:
+            ctx.bind(name, ctx.map_from_spec(w.maps[name]))
+    c4, c6 = w.maps["ct4"], w.maps["ct6"]
+    handles = []
+    for e in w.endpoints:
+        m4 = ctx.map_create(c4.type, c4.key_size, c4.val_size, c4.max_entries)
+        m6 = ctx.map_create(c6.type, c6.key_size, c6.val_size, c6.max_entries)
+        i = ctx.endpoint_add(e["lxc_id"], e["seclabel"], None, m4)
+        ctx.endpoint_config(i, ct6=m6, **H._ep_cfg(e))
+        handles.append((m4.h, m6.h))
+    if w.extra and "node" in w.extra:
+        ctx.node_config(**w.extra["node"])
+    return ctx, handles
+
+
+def sched_simulate(w, world):
+    """the endpoint-owned node with the product's round scheduler (cv_epnode_*, one per
+    rank, lockstep rounds in-process) and the oracle as every rank's datapath; returns
+    (results as RankState.result() gives them, rounds, stats of rank 0)"""
+    from cilium_amd import lib
+    now, src, fh = w.now, w.extra["src_ep"], w.extra["flow_hash"]
+    ranks = []
+    for r in range(world):
+        ctx, handles = host_node_ctx(w)
+        dp, maps = E.per_endpoint_dp(w)
+        om = {}
+        for e, (h4, h6) in enumerate(handles):
+            om[h4], om[h6] = maps["ct4"][e], maps["ct6"][e]
+        s = lib.EpSched(ctx, r, world, w.frames, src)
+        s.set_counts(lambda hs, om=om: ([len(om[h]) for h in hs], [om[h].max_entries for h in hs]))
+        ranks.append({"ctx": ctx, "dp": dp, "maps": maps, "s": s, "rec": {}, "mine": np.zeros(w.n, bool),
+                      "out": {k: np.zeros(w.n, np.int64) for k in E.RankState.FIELDS}, "cross": 0})
+    rounds = 0
+    while sum(R["s"].pending() for R in ranks):
+        rounds += 1
+        assert rounds < w.n, "no progress"
+        before = sum(R["s"].pending() for R in ranks)
+        inbox = [[] for _ in range(world)]
+        for r, R in enumerate(ranks):
+            pk = R["s"].sources()
+            dst = np.full(len(pk), -1, np.int32)
+            recs = []
+            if len(pk):
+                o, dl, ifx, lab = R["dp"].lxc_egress_split(w.frames[pk], w.length[pk], src[pk], fh[pk], now=now)
+                for j, i in enumerate(pk):
+                    if o.ret[j] == E.DEFER:
+                        dst[j] = int(dl[j])
+                    else:
+                        for k in E.RankState.FIELDS:
+                            R["out"][k][i] = getattr(o, k)[j]
+                        R["mine"][i] = True
+                    recs.append({"frame": o.frames_out[j].copy(), "ifindex": int(ifx[j]), "label": int(lab[j]),
+                                 "identity": int(o.identity[j]), "ct": int(o.ct[j]), "nl": int(o.nl[j]),
+                                 "nu": int(o.nu[j])})
+            rp, re_, rh, rpos, rr = R["s"].sources_done(pk, dst)
+            at = 0
+            for q, cnt in enumerate(rr):
+                for j in range(at, at + int(cnt)):
+                    inbox[q].append((int(rp[j]), int(re_[j]), int(rh[j]), recs[rpos[j]] if rh[j] else None, r))
+                at += int(cnt)
+        for q, R in enumerate(ranks):
+            rows = inbox[q]
+            if not rows:
+                continue
+            ops = R["s"].receive([x[0] for x in rows], [x[1] for x in rows], [x[2] for x in rows])
+            for (i, d, has, rec, frm), op in zip(rows, ops):
+                if op >= 0:
+                    R["rec"][int(op)] = (i, d, rec)
+                    R["cross"] += frm != q
+        for R in ranks:
+            ops, pk = R["s"].deliveries(2 * w.n + 16)
+            if not len(ops):
+                continue
+            items = [R["rec"].pop(int(o)) for o in ops]
+            assert [x[0] for x in items] == list(pk)
+            o = R["dp"].lxc_deliver(np.stack([x[2]["frame"] for x in items]), w.length[pk], [x[1] for x in items],
+                                    [x[2]["ifindex"] for x in items], [x[2]["label"] for x in items],
+                                    [x[2]["nl"] for x in items], [x[2]["nu"] for x in items], now=now)
+            for j, (i, _, rec) in enumerate(items):
+                for k in ("ret", "proxy", "nl", "nu", "reason"):
+                    R["out"][k][i] = getattr(o, k)[j]
+                R["out"]["identity"][i] = rec["identity"]
+                R["out"]["ct"][i] = rec["ct"]
+                R["mine"][i] = True
+        assert sum(R["s"].pending() for R in ranks) < before, f"round {rounds}: no operation could run"
+    results = []
+    for r, R in enumerate(ranks):
+        owned = [e for e in range(len(w.endpoints)) if e % world == r]
+        results.append({"out": {k: v[R["mine"]] for k, v in R["out"].items()}, "idx": np.nonzero(R["mine"])[0],
+                        "ct": {e: (R["maps"]["ct4"][e].dump(), R["maps"]["ct6"][e].dump()) for e in owned},
+                        "metrics": R["dp"].metrics(), "policy": R["maps"]["policy"].dump(), "cross": R["cross"]})
+    st = ranks[0]["s"].stats()
+    for R in ranks:
+        R["s"].close()
+        R["ctx"].close()
+    return results, rounds, st
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_ep_sched_node(world):
+    """the product's round scheduler (cv_epnode, C++) with the oracle as datapath: the
+    ranks' merged result equals one sequential run"""
+    w = _workload()
+    results, rounds, st = sched_simulate(w, world)
+    print(f"world {world}: {w.n} packets in {rounds} rounds, {st}")
+    if world > 1:
+        _check(w, results, world)
+    else:
+        ref, dp, maps = _sequential(w)
+        out, ct, metrics, _ = E.merge(w, results)
+        for k in E.RankState.FIELDS:
+            assert (out[k] == getattr(ref, k).astype(np.int64)).all(), k
+        assert (metrics == dp.metrics()).all()
+    assert st["maps_ordered_whole_at_open"] == 0
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_ep_sched_node_at_capacity(world):
+    """maps sized so half of them fill: the scheduler orders a map that may fill over all
+    its peers, and the node stays exact (48 of 4 096 packets differed without it)"""
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=0xE5, vip_frac=0.5)
+    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+    _, _, m0 = _sequential(w)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    cap = int(sizes[len(sizes) // 2])
+    w = synth.config5(1 << 12, ct_max=cap, **kw)
+    results, rounds, st = sched_simulate(w, world)
+    print(f"world {world} at capacity: {rounds} rounds, {st}")
+    ref, dp, maps = _sequential(w)
+    out, ct, metrics, _ = E.merge(w, results)
+    for k in E.RankState.FIELDS:
+        bad = np.nonzero(out[k] != getattr(ref, k).astype(np.int64))[0]
+        assert len(bad) == 0, (k, len(bad), bad[:5])
+    for e in range(len(w.endpoints)):
+        for fam, (keys, vals) in zip(("ct4", "ct6"), ct[e]):
+            ok, ov = maps[fam][e].dump()
+            assert (H.sorted_rows(keys, vals) == H.sorted_rows(ok, ov)).all(), (e, fam)
+    assert (metrics == dp.metrics()).all()
+    assert st["maps_ordered_whole_at_open"] > 0 and dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0

@@ -62,15 +62,16 @@ def per_endpoint_ctx(w, device=0):
 def _rank_run(w, rank, world, device, exchange=None, all_sum=None):
     from cilium_amd import epnode
     ctx, maps = per_endpoint_ctx(w, int(device.split(":")[1]))
-    cand, (sp, dp) = E.candidates(w), E.peers(w)
-    node = epnode.EpNode(ctx, rank, world, w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], cand, sp, dp,
+    node = epnode.EpNode(ctx, rank, world, w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"],
                          device=device, exchange=exchange, all_sum=all_sum)
     rounds = node.run(w.now)
+    out, idx = node.results()
     owned = [e for e in range(len(w.endpoints)) if e % world == rank]
-    res = {"out": {k: v[node.mine] for k, v in node.out.items()}, "idx": np.nonzero(node.mine)[0],
+    res = {"out": out, "idx": idx,
            "ct": {e: (maps["ct4"][e].dump(), maps["ct6"][e].dump()) for e in owned},
            "metrics": ctx.metrics(), "policy": maps["policy"].dump(), "cross": node.cross, "rounds": rounds,
-           "launches": node.launches}
+           "launches": node.launches, "stats": node.sched.stats()}
+    node.sched.close()
     ctx.close()
     return res
 
@@ -140,7 +141,7 @@ def _rank_main(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        ex, s = epnode.dist_exchange(world, device=None)
+        ex, s = epnode.dist_exchange(world, rank, device=None)
         q.put((rank, _rank_run(_workload(), rank, world, "cuda:0", exchange=ex, all_sum=s)))
     finally:
         dist.destroy_process_group()
@@ -201,8 +202,13 @@ def test_split_then_deliver_at_capacity(dev, monkeypatch, capfd):
     ctx, maps = per_endpoint_ctx(w, int(dev.split(":")[1]))
     monkeypatch.setenv("CV_ADMIT_STATS", "1")
     capfd.readouterr()
-    node = epnode.EpNode(ctx, 0, 1, w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"],
-                         E.candidates(w), *E.peers(w), device=dev)
+    node = epnode.EpNode(ctx, 0, 1, w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], device=dev)
+
+    def host(o):
+        r = {k: v.cpu().numpy().astype(np.int64) for k, v in o.items()}
+        r["identity"] &= 0xFFFFFFFF
+        r["proxy"] &= 0xFFFF
+        return r
     got = {k: np.zeros(w.n, np.int64) for k in epnode.FIELDS}
     recs = {}
     for fam in (0, 1):
@@ -211,7 +217,7 @@ def test_split_then_deliver_at_capacity(dev, monkeypatch, capfd):
         out = node._dev_out(len(sel))
         buf = torch.zeros(len(sel) * epnode.REC, dtype=torch.uint8, device=dev)
         ctx.lxc_egress_split(f["frames"], f["length"], out, now, buf, src_ep=f["src_ep"], flow_hash=f["flow_hash"])
-        o = node._host_out(out)
+        o = host(out)
         r = buf.cpu().numpy().reshape(-1, epnode.REC)
         for k in epnode.FIELDS:
             got[k][sel] = o[k]
@@ -223,7 +229,7 @@ def test_split_then_deliver_at_capacity(dev, monkeypatch, capfd):
         out = node._dev_out(len(idx))
         rd = torch.from_numpy(np.ascontiguousarray(rr).reshape(-1)).to(dev)
         ctx.lxc_deliver(rd, len(idx), fam == 1, out, now)
-        o = node._host_out(out)
+        o = host(out)
         for k in ("ret", "reason", "proxy", "nl", "nu"):
             got[k][idx] = o[k]
     want["identity"] &= 0xFFFFFFFF
@@ -241,3 +247,112 @@ def test_split_then_deliver_at_capacity(dev, monkeypatch, capfd):
     full = sum(len(m) >= cap for fam in ("ct4", "ct6") for m in om[fam])
     assert full >= 4 and dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0, full
     ctx.close()
+
+
+def test_endpoint_owned_at_capacity(dev, monkeypatch, capfd):
+    """The endpoint-owned node next to max_entries (verdict r05 item 1): maps sized so half
+    of them fill within the batch.  The scheduler orders a map that may fill over all its
+    peers (include/cilium_epnode.h), the split source launches and the delivery launches
+    run admitted, and every output, table, counter and metric equals the sequential
+    per-endpoint-map oracle (59 of 4 096 verdicts differed with per-peer ordering alone)."""
+    import re
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=0xE5, vip_frac=0.5)
+    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+    dp0, m0 = E.per_endpoint_dp(w)
+    dp0.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    cap = int(sizes[len(sizes) // 2])
+    w = synth.config5(1 << 12, ct_max=cap, **kw)
+    monkeypatch.setenv("CV_ADMIT_STATS", "1")
+    capfd.readouterr()
+    res = _rank_run(w, 0, 1, dev)
+    _check(w, [res])
+    err = capfd.readouterr().err
+    assert re.search(r"\[cv admit\] deliver: \d+ packets", err), err[-2000:]
+    dp, om = E.per_endpoint_dp(w)
+    dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    full = sum(len(m) >= cap for fam in ("ct4", "ct6") for m in om[fam])
+    assert full >= 8 and res["stats"]["maps_ordered_whole_at_open"] > 0, (full, res["stats"])
+    m = dp.metrics()
+    assert m[155, 2, 0] + m[155, 1, 0] > 0                        # DROP_CT_CREATE_FAILED
+    with capfd.disabled():
+        print(f"\n  at capacity: {w.n} packets, {res['rounds']} rounds, {full} maps full (max_entries {cap}), "
+              f"{res['stats']}")
+
+
+def _cap_main(rank, world, port, q):
+    import torch.distributed as dist
+    from cilium_amd import epnode
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ex, s = epnode.dist_exchange(world, rank, device=None)
+        q.put((rank, _rank_run(_cap_workload(), rank, world, "cuda:0", exchange=ex, all_sum=s)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _cap_workload():
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=0xE5, vip_frac=0.5)
+    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+    dp0, m0 = E.per_endpoint_dp(w)
+    dp0.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    return synth.config5(1 << 12, ct_max=int(sizes[len(sizes) // 2]), **kw)
+
+
+def test_endpoint_owned_at_capacity_two_ranks_gloo(dev, capsys):
+    """the at-capacity node on two ranks (two processes on one GPU, gloo exchange)"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cap_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    _check(_cap_workload(), [results[0], results[1]])
+    with capsys.disabled():
+        print(f"\n  2 ranks at capacity: {results[0]['rounds']} rounds, "
+              f"{sum(r['cross'] for r in results.values())} cross-rank deliveries")
+
+
+def test_deliver_on_fresh_context(dev):
+    """cv_lxc_deliver on a context that never ran an egress launch (a rank whose endpoints
+    only receive): its records' outputs equal the oracle's (advisor r05: the egress scratch
+    the delivery launch writes was not allocated on such a context)."""
+    import torch
+    from cilium_amd import epnode
+    w = _workload()
+    dp, om = E.per_endpoint_dp(w)
+    o1, dl, ifx, lab = dp.lxc_egress_split(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    # the records from a first context's split launch (IPv4 part)
+    ctx1, _ = per_endpoint_ctx(w, int(dev.split(":")[1]))
+    v6, rows = epnode.families(w.frames)
+    idx = np.nonzero(~v6)[0]
+    f = torch.from_numpy(np.ascontiguousarray(w.frames[idx, :64])).to(dev)
+    ln = torch.from_numpy(w.length[idx].astype(np.uint32).view(np.int32)).to(dev)
+    se = torch.from_numpy(w.extra["src_ep"][idx].astype(np.uint16).view(np.int16)).to(dev)
+    fh = torch.from_numpy(w.extra["flow_hash"][idx].astype(np.uint32).view(np.int32)).to(dev)
+    out = H.dev_out(len(idx), dev)
+    buf = torch.zeros(len(idx) * epnode.REC, dtype=torch.uint8, device=dev)
+    ctx1.lxc_egress_split(f, ln, out, w.now, buf, src_ep=se, flow_hash=fh)
+    ret = out["ret"].cpu().numpy()
+    sel = np.nonzero(ret == epnode.DEFER)[0]
+    assert len(sel) > 0
+    recs = buf.view(-1, epnode.REC)[torch.from_numpy(sel).to(dev)].contiguous()
+    ctx1.close()
+    # a fresh context runs only the deliveries
+    ctx2, _ = per_endpoint_ctx(w, int(dev.split(":")[1]))
+    o = H.dev_out(len(sel), dev)
+    ctx2.lxc_deliver(recs.view(-1), len(sel), False, o, w.now)
+    got = H.host_out(o)
+    pk = idx[sel]
+    dp, _ = E.per_endpoint_dp(w)                                    # (the deliveries' own fresh maps, as ctx2's)
+    o2 = dp.lxc_deliver(o1.frames_out[pk], w.length[pk], dl[pk], ifx[pk], lab[pk], o1.nl[pk], o1.nu[pk], now=w.now)
+    for k in ("ret", "reason", "proxy", "nl", "nu"):
+        assert (got[k] == getattr(o2, k)).all(), k
+    ctx2.close()

@@ -557,6 +557,29 @@ def test_corrupt_group_list_fails_loudly(dev, monkeypatch):
     ctx.close()
 
 
+def test_overcounted_split_job_fails_loudly(dev, monkeypatch):
+    """The round-5 fault's shape (an egress launch's two binned groupings once shared the
+    split-key job count, and the second walked the first's jobs: an illegal address in
+    egress admission): CV_JOB_INJECT counts one job more than the grouping wrote, its run
+    word past `order`.  k_gbin_marks skips it (run_ok) -- no access through it, no fault --
+    and the context's next call fails with -EPROTO; a fresh context then runs the batch."""
+    from tests.test_gpu_egress import check_egress
+    w = synth.config5(1 << 14, n_svc=500, n_ep=64, n_remote=256, seed=93)
+    ctx, pm = H.product_ctx(w)
+    f, l, _ = H.to_dev(w, dev)
+    src, fh = H.egress_inputs(w, dev)
+    out = H.dev_out(w.n, dev)
+    monkeypatch.setenv("CV_JOB_INJECT", "1")
+    ctx.lxc_egress(f, l, out, w.now, src_ep=src, flow_hash=fh)    # (asynchronous: the error shows next)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("CV_JOB_INJECT")
+    with pytest.raises(OSError) as ei:
+        ctx.sync()
+    assert ei.value.errno == errno.EPROTO
+    ctx.close()
+    check_egress(w, dev, batches=1, events=False)
+
+
 def test_ct_churn_fill_gc_refill(dev):
     """Conntrack churn at about 50 % slot load: every round a fresh batch creates ~26k
     entries (lifetime now + 60), then ctmap.GC at the next `now` deletes the previous

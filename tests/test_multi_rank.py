@@ -322,6 +322,37 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert d[0]["elapsed"] == d[1]["elapsed"]                       # the MAX over ranks
 
 
+@pytest.mark.gpu
+def test_bench_ep_owned_two_ranks_gloo():
+    """bench.py --ep-owned at N = 2 (config 5 as one node: two spawned ranks on GPU 0, gloo
+    instead of RCCL): the rounds, the per-round exchange and the reductions run, one JSON
+    line (rank 0) with the node's packets, rounds and cross-rank deliveries."""
+    import json
+    import subprocess
+    import sys
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "config5", "--ep-owned",
+             "--packets", "16384", "--ct-local", "2048", "--steps", "2", "--warmup", "1", "--dist-backend", "gloo"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=280) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [l for l in outs[0][0].splitlines() if l.strip()]
+    assert len(lines) == 1 and not outs[1][0].strip()
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["packets_per_step_node"] == 16384
+    assert line["ep_owned"]["rounds_per_step"][0] >= 2 and line["ep_owned"]["cross_rank_deliveries_per_step"] > 0
+
+
 def test_family_oracle_equals_sequential():
     """test_config5_bench_regime's oracle: config 5's IPv4 and IPv6 packets as two batches
     on two datapaths (tests/harness.FamilyOracle, the split bench.py runs on the GPU) give

@@ -10,7 +10,7 @@ HBM traffic per launch follows MI355X_MICROARCH.md § HBM: FETCH_SIZE (KiB) doub
 (gfx950 tallies 128-B requests at 64 B) plus WRITE_SIZE (KiB).  Both derive from the
 L2's memory-side requests, so Infinity-Cache hits are included.
 
-  usage: python tools/pmc_summary.py <tag> <workload>
+  usage: python tools/pmc_summary.py <tag> <workload> [kernel]   (default: the largest total time)
 """
 import csv
 import hashlib
@@ -21,8 +21,21 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_ct_stage<false>",
-            "config5": "k_egress_ct<true, false, false, false>"}
+SETUP = ("k_ct_load", "k_ct_scan", "k_ct_op", "k_ct_gc", "k_ct_tags")   # table loads, map API, slot-load probe
+
+
+def dominant(stats_csv):
+    """the kernel with the largest total time in the kernel statistics (the step's
+    dominant kernel), as its name between `cv::` and the argument list"""
+    best, name = -1.0, None
+    for r in csv.DictReader(open(stats_csv)):
+        n = r["Name"]
+        if not n.startswith(("cv::", "void cv::")) or any(f"::{x}(" in n for x in SETUP):
+            continue
+        if float(r["TotalDurationNs"]) > best:
+            best, name = float(r["TotalDurationNs"]), n
+    short = name.split("cv::", 1)[1]
+    return short[:short.index("(")] if "(" in short else short
 # a kernel launched exactly once per step (counts the steps of a pass)
 STEP_KERNEL = {"config1": "k_xdp_prefilter", "config2": "k_policy_ingress", "config3": "k_netdev_front<false>",
                "config5": "k_egress_front<32, false>"}
@@ -42,8 +55,8 @@ def main():
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv"), os.path.join(dst, f"{w}_kernel_stats.csv"))
     shutil.copy(os.path.join(src, f"bench_{w}.json"), os.path.join(dst, f"bench_{w}.json"))
-    kname = DOMINANT[w]
-    setup = ("k_ct_load", "k_ct_scan", "k_ct_op", "k_ct_gc", "k_ct_tags")   # table loads, map API, slot-load probe
+    kname = sys.argv[3] if len(sys.argv) > 3 else dominant(os.path.join(src, f"stats_{w}", "run_kernel_stats.csv"))
+    setup = SETUP
     ctr, step = {}, defaultdict(float)
     nsteps = 0
     for i in (1, 2, 3):

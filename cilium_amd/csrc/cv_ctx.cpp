@@ -266,6 +266,8 @@ struct cv_ctx {
     std::vector<MapObj *> mt_maps;
     uint64_t mt_eps = ~(uint64_t)0;   // (eps_gen the table was built at)
     DevBuf mt_live, mt_cap, mt_epmi4, mt_epmi6, mt_out;
+    DevBuf bnd_buf;                    // the room check's per-map bounds, per-LB-slot counts, flags (CtBound)
+    uint64_t bound_checks = 0, bound_fits = 0;
     DevBuf eadm_save, eadm_buf;        // egress admission: the state a pass writes, intents + budgets
     DevBuf eam_buf, eam_keys, eam_snap;  // (many CT maps: per-slot intents + budgets, walk keys, the slot set)
     Snap eam_snap_host[2]{};
@@ -1570,6 +1572,54 @@ void refresh_live(cv_ctx *c, const std::vector<MapObj *> &maps)
     }
 }
 
+// Many CT maps (ConntrackLocal): whether a launch surely fits every map by a per-map
+// bound of its creates (CtBound, cv_dp.hpp) -- the global rule (every map's room >= W n)
+// sends every launch over 64 000-entry per-endpoint maps through the admission passes.
+// One sync (the flag).  A launch that fits leaves every map's count to be re-read when
+// the next launch plans.
+bool ct_bound_fits(cv_ctx *c, const DpParams &p, const BatchDev &b, const uint4 *records, uint32_t mode,
+                   const uint16_t *src_ep, uint32_t ep0, const std::vector<MapObj *> &cts, hipStream_t s)
+{
+    if (cts.size() < 2 || map_table(c, cts)) return false;
+    const uint32_t nm = (uint32_t)cts.size();
+    const uint64_t s4 = mode == 1 && p.lb4.buckets ? (p.lb4.mask + 1) * Lb4Spec::SPB : 0,
+                   s6 = mode == 1 && p.lb6.buckets ? (p.lb6.mask + 1) * Lb6Spec::SPB : 0;
+    const size_t bytes = (size_t)nm * 8 + (s4 + s6) * 4 + 64;
+    if (c->bnd_buf.n < bytes && c->bnd_buf.alloc(bytes)) return false;
+    if (hipMemsetAsync(c->bnd_buf.p, 0, bytes, s) != hipSuccess) return false;
+    CtBound bd{};
+    bd.bound = c->bnd_buf.as<unsigned long long>();
+    bd.svc4 = reinterpret_cast<uint32_t *>(bd.bound + nm);
+    bd.svc6 = bd.svc4 + s4;
+    bd.flag = bd.svc6 + s6;
+    bd.live = c->mt_live.as<unsigned long long *const>();
+    bd.cap = c->mt_cap.as<const unsigned long long>();
+    bd.epmi4 = c->mt_epmi4.as<const uint16_t>();
+    bd.epmi6 = c->mt_epmi6.as<const uint16_t>();
+    bd.src_ep = src_ep;
+    bd.ep0 = ep0;
+    bd.nmaps = nm;
+    bd.n_eps = (uint32_t)c->eps.size();
+    bd.w_src = 7;                              // (a source program's creates: cv_lxc_egress's W)
+    bd.w_dst = 2;                              // (a delivery: the tuple and its ICMP twin)
+    bd.mode = mode;
+    uint32_t flag[2] = {1u, 0u};
+    if (launch_ct_bound(p, b, records, bd, s) ||
+        hipMemcpyAsync(flag, bd.flag, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return false;
+    c->bound_checks++;
+    if (getenv("CV_ADMIT_STATS"))
+        fprintf(stderr, "[cv bound] mode %u: %u packets, %u maps, fits %d (unseen %u)\n", mode, b.n, nm, !flag[0],
+                flag[1]);
+    if (flag[0]) return false;
+    c->bound_fits++;
+    for (MapObj *m : cts) {
+        m->live_upper = m->cap;                // (re-read when the next launch plans)
+        m->gen++;
+    }
+    return true;
+}
+
 // Launch-chunk planning against max_entries (ct_live_add, cv_dev.hpp).  A packet
 // creates at most W entries in a map (ingress: the tuple and its ICMP-related twin;
 // egress: a service create, the connection with its NAT tuple, and the delivery's
@@ -2566,7 +2616,9 @@ int cv_netdev_ingress(cv_ctx *c, const cv_batch *b, uint32_t now, int with_prefi
         // 2 n for a 2^24-packet batch, though its real creates are a fraction of that
         uint32_t fit_n = ct_fit_count(c, cts, n, 2);
         if (fit_n < n && fit_n >= std::min<uint32_t>(n, SPLIT_MIN)) n = fit_n;
-        const bool fits = ct_fits(c, cts, n, 2);
+        bool fits = ct_fits(c, cts, n, 2);
+        if (!fits && cts.size() > 1)                      // (many maps: each map's own bound)
+            fits = ct_bound_fits(c, p, chunk(b, off, n), nullptr, 0, nullptr, 0, cts, (hipStream_t)stream);
         GroupScratch gs = next_groups(c, 1, (hipStream_t)stream);
         gs.gbits = gbin_bits(n);
         if (!fits) {
@@ -2628,6 +2680,9 @@ int lxc_egress(cv_ctx *c, const cv_batch *b, const uint16_t *src_ep, uint32_t ep
         const uint32_t fit_n = ct_fit_count(c, cts, n, 7);
         if (fit_n < n && fit_n >= std::min<uint32_t>(n, SPLIT_MIN)) n = fit_n;
         bool fits = ct_fits(c, cts, n, 7);
+        if (!fits && !one_map && !guarded)                // (many maps: each map's own bound)
+            fits = ct_bound_fits(c, p, chunk(b, off, n), nullptr, 1, src_ep ? src_ep + off : nullptr, ep0, cts,
+                                 (hipStream_t)stream);
         if (!fits && !one_map && n > EAM_WINDOW) {
             n = EAM_WINDOW;
             fits = ct_fits(c, cts, n, 7);
@@ -2725,6 +2780,11 @@ int cv_lxc_deliver(cv_ctx *c, const uint8_t *records, uint32_t n, int v6, uint32
         // guarded record at a time next to the limit)
         m = std::min(c->chunk, n - off);
         bool fits = ct_fits(c, cts, m, 2);
+        if (!fits && !guarded) {                          // (many maps: each destination map's own bound)
+            const BatchDev bd{nullptr, v6 ? 128u : 64u, m, nullptr, nullptr, off, nullptr};
+            fits = ct_bound_fits(c, p, bd, reinterpret_cast<const uint4 *>(records) + (size_t)off * DEL_SLOTS, 2,
+                                 nullptr, 0, cts, (hipStream_t)stream);
+        }
         if (!fits && m > EAM_WINDOW) {
             m = EAM_WINDOW;
             fits = ct_fits(c, cts, m, 2);

@@ -367,6 +367,28 @@ int launch_lxc_deliver(const DpParams &p, const BatchDev &b, uint32_t now, const
 // config 5: from-container of the packets' source endpoints (src_ep[i], or ep0)
 int launch_lxc_egress(const DpParams &p, const BatchDev &b, const uint16_t *src_ep, uint32_t ep0,
                       const uint32_t *flow_hash, uint32_t now, const OutDev &o, GroupScratch g, hipStream_t s);
+// Room check of a launch over many CT maps (ConntrackLocal: every endpoint its own CT4 /
+// CT6 map).  A map can only take creates from the packets whose source program or local
+// delivery is its endpoint's, so per map a bound of the launch's creates -- w_src per
+// packet from the endpoint (egress), w_dst per packet that may be delivered to it: the
+// endpoint owning the destination address, or backing a service the packet may be
+// served by -- against its room tells whether the launch surely fits every map (then
+// it runs at full width, no admission passes).  Packets whose destination the check
+// cannot see (an IPv6 extension header it does not walk) count against every map.
+struct CtBound {
+    unsigned long long *bound;         // per map: creates the launch may make in it
+    uint32_t *svc4, *svc6;             // per LB table slot: packets a service master may serve
+    uint32_t *flag;                    // [0] some map may fill, [1] packets of unseen destination
+    unsigned long long *const *live;   // per map: its live count (map_table)
+    const unsigned long long *cap;     // per map: max_entries
+    const uint16_t *epmi4, *epmi6;     // per endpoint: its CT4 / CT6 map's index
+    const uint16_t *src_ep;            // egress: per packet its source endpoint, or null (ep0)
+    uint32_t ep0, nmaps, n_eps;
+    uint32_t w_src, w_dst;             // creates per packet in its source's / destination's map
+    uint32_t mode;                     // 0 netdev, 1 egress (source + destination), 2 delivery records
+};
+int launch_ct_bound(const DpParams &p, const BatchDev &b, const uint4 *records, const CtBound &bd, hipStream_t s);
+
 // one run of words the agent's writes changed in a device table (cv_ctx.cpp PatchQueue)
 struct PatchRec {
     unsigned long long dst;    // device address of the first word

@@ -4,19 +4,22 @@
 // lists the operations of the rank's maps in packet order, and per round hands out the
 // operations no earlier pending operation blocks.
 //
-// Blocking is within one CT map: an operation's keys are (its map, a peer address), all
-// in its own map, so one in-order scan over a map's pending operations finds the ready
-// ones -- a blocked operation stamps its peers, and a later operation meeting a stamped
-// peer is blocked in turn; on a map that may fill (`tight`) the first blocked operation
-// blocks every later one (conntrack.h:692-693: creates of different peers compete for
-// the room).  Peers are 64-bit address hashes folded to PEER_SLOTS stamps: two peers
-// folding together only add an ordering constraint, never drop one.
+// An operation's keys are (its map, a peer address), all in its own map.  It waits for
+// the operation before it on each of its keys (a dependency DAG built once per batch,
+// predecessors counted per operation, Kahn-style): when an operation runs, its
+// successors' counts drop, and a successor of the same kind whose count reaches zero runs
+// in the same launch (the launch keeps packet order per address pair).  On a map that
+// may fill (`chain`) every operation also waits for the one before it in the map
+// (conntrack.h:692-693: creates of different peers compete for the room) until the
+// map's room is ample again.  Each key link is used once per batch, so a round costs the
+// operations it runs, not the ones still waiting.  Addresses are 64-bit hashes (two
+// colliding only add candidates or a dependency, never drop one).
 #include <errno.h>
 #include <string.h>
 
 #include <algorithm>
 #include <memory>
-#include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "../../include/cilium_epnode.h"
@@ -24,13 +27,12 @@
 
 namespace {
 
-constexpr uint32_t PEER_SLOTS = 1u << 22;
 // the most entries one operation creates in its map: a source program its service entry,
 // the connection's tuple, its ICMP-RELATED twin and the NAT tuple (lb{4,6}_local,
 // ct_create{4,6}: lb.h:700-775, conntrack.h:663-744) -- bounded by 7 as cv_lxc_egress
 // plans launches; a delivery the tuple and its twin (ipv4_policy / ipv6_policy)
 constexpr int64_t MAX_CREATES[2] = {7, 2};
-enum : uint8_t { OP_PENDING = 0, OP_RESOLVED = 1, OP_DONE = 2 };
+enum : uint8_t { OP_PENDING = 0, OP_RESOLVED = 1, OP_NOOP = 2, OP_DONE = 3 };
 
 struct Addr {
     uint64_t a, b;
@@ -45,9 +47,6 @@ inline uint64_t mix(uint64_t z)
     return z ^ (z >> 31);
 }
 
-struct AddrHash {
-    size_t operator()(const Addr &x) const { return (size_t)mix(mix(x.a ^ x.fam) + x.b); }
-};
 
 Addr addr4(const uint8_t *p)
 {
@@ -64,7 +63,46 @@ Addr addr6(const uint8_t *p)
     return r;
 }
 
-inline uint32_t peer_slot(const Addr &x) { return (uint32_t)(AddrHash()(x) & (PEER_SLOTS - 1)); }
+inline uint64_t ahash(const Addr &x) { return mix(mix(x.a ^ ((uint64_t)x.fam << 56)) + x.b) | 1u; }
+
+// key -> run of values, from (key, value) pairs: an open-addressing index over the
+// distinct keys and their values grouped (CSR)
+template <class V>
+struct Csr {
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> lo, hi;
+    std::vector<V> val;
+    uint64_t mask = 0;
+    explicit Csr(std::vector<std::pair<uint64_t, V>> kv)
+    {
+        std::sort(kv.begin(), kv.end());
+        kv.erase(std::unique(kv.begin(), kv.end()), kv.end());
+        uint64_t cap = 16;
+        while (cap < 2 * kv.size()) cap <<= 1;
+        mask = cap - 1;
+        keys.assign(cap, 0);
+        lo.assign(cap, 0);
+        hi.assign(cap, 0);
+        val.reserve(kv.size());
+        for (size_t k = 0; k < kv.size();) {
+            size_t e = k;
+            while (e < kv.size() && kv[e].first == kv[k].first) val.push_back(kv[e++].second);
+            uint64_t h = kv[k].first & mask;
+            while (keys[h]) h = (h + 1) & mask;
+            keys[h] = kv[k].first;
+            lo[h] = (uint32_t)(val.size() - (e - k));
+            hi[h] = (uint32_t)val.size();
+            k = e;
+        }
+    }
+    std::pair<uint32_t, uint32_t> find(uint64_t key) const
+    {
+        for (uint64_t h = key & mask;; h = (h + 1) & mask) {
+            if (keys[h] == key) return {lo[h], hi[h]};
+            if (!keys[h]) return {0u, 0u};
+        }
+    }
+};
 
 }  // namespace
 
@@ -73,51 +111,107 @@ struct cv_epnode {
     uint32_t rank = 0, world = 1, n = 0, n_eps = 0;
     std::vector<uint8_t> v6;
     std::vector<uint32_t> cand_off, cand;          // per packet its candidate destinations (CSR, ascending)
-    // operations of this rank in (packet, kind, endpoint) order
-    std::vector<uint32_t> op_pkt, op_map, op_poff, op_peer;
+    // operations of this rank in (packet, kind, endpoint) order; per key reference of an
+    // operation, the next operation on that key (or NONE)
+    std::vector<uint32_t> op_pkt, op_map, op_poff, op_mpos;
+    std::vector<uint32_t> ref_op, ref_next, ref_prev;   // per key reference: its operation, the neighbours on its key
     std::vector<uint8_t> op_kind, op_st;
-    std::vector<uint32_t> dl_first;                // per packet its first delivery operation here (or ~0)
+    std::vector<uint32_t> op_wait;                 // earlier pending operations it waits for
+    std::vector<uint32_t> dl_first;                // per packet its first delivery operation here (or NONE)
     std::vector<uint8_t> dl_cnt;
-    // per map (endpoint * 2 + family): its operations in order, the first not done
+    // per map (endpoint * 2 + family): its operations in order
     std::vector<uint32_t> map_off, map_ops, map_head;
     std::vector<int> map_handle;
     std::vector<int64_t> map_need;                 // creates its pending operations may still make
-    std::vector<uint64_t> map_live, map_cap;
-    std::vector<uint8_t> map_tight;
+    std::vector<uint8_t> map_chain;                // may fill: its operations wait for each other in order
     std::vector<uint32_t> active;                  // maps with operations
-    std::vector<uint32_t> stamp;
-    uint32_t cur = 0;
-    uint64_t pending = 0, rounds = 0, n_src = 0, n_dl = 0, tight0 = 0, sent = 0;
+    std::vector<uint32_t> zero[2];                 // per kind: operations waiting for nothing, not yet run
+    uint64_t pending = 0, rounds = 0, n_src = 0, n_dl = 0, chained0 = 0, sent = 0;
     cv_epnode_counts_fn counts = nullptr;          // (the caller's live counts, else the context's maps)
     void *counts_arg = nullptr;
 
-    uint32_t next_stamp()
+    static constexpr uint32_t NONE = ~0u;
+    bool owned(uint32_t ep) const { return ep % world == rank; }
+    uint32_t chain_next(uint32_t o) const
     {
-        if (++cur == 0) {                          // (wrapped: forget every stamp)
-            std::fill(stamp.begin(), stamp.end(), 0u);
-            cur = 1;
-        }
-        return cur;
+        const uint32_t m = op_map[o], k = op_mpos[o] + 1;
+        return k < map_off[m + 1] ? map_ops[k] : NONE;
     }
+    void release(uint32_t s)
+    {
+        if (--op_wait[s] == 0) zero[op_kind[s]].push_back(s);
+    }
+    // operation o has run (or will not run here): its successors wait for one less
     void finish(uint32_t o)
     {
         op_st[o] = OP_DONE;
         map_need[op_map[o]] -= MAX_CREATES[op_kind[o]];
         --pending;
+        for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q)
+            if (ref_next[q] != NONE) release(ref_op[ref_next[q]]);
+        if (map_chain[op_map[o]]) {
+            const uint32_t s = chain_next(o);
+            if (s != NONE) release(s);
+        }
     }
-    bool owned(uint32_t ep) const { return ep % world == rank; }
-    int refresh_tight(bool all);
-    template <class Ready>
-    void scan(Ready ready, std::vector<uint32_t> &out);
+    // a delivery that runs nowhere here leaves its keys' lists: each successor waits for
+    // the predecessor instead, or for nothing more when the predecessor has finished
+    void splice(uint32_t o)
+    {
+        for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q) {
+            const uint32_t pq = ref_prev[q], nq = ref_next[q];
+            const bool waits = pq != NONE && op_st[ref_op[pq]] != OP_DONE;   // (o still waited on pq)
+            if (pq != NONE) ref_next[pq] = waits ? nq : NONE;
+            if (nq != NONE) {
+                ref_prev[nq] = waits ? pq : NONE;
+                if (!waits) release(ref_op[nq]);
+            }
+            ref_prev[q] = ref_next[q] = NONE;
+        }
+        op_st[o] = OP_DONE;
+        map_need[op_map[o]] -= MAX_CREATES[op_kind[o]];
+        --pending;
+    }
+    int room(bool first);
+    // the operations of `kind` that can run now (deliveries: with their record), and
+    // those they free in turn, in packet order
+    void run_ready(int kind, std::vector<uint32_t> &out)
+    {
+        std::vector<uint32_t> keep, &z = zero[kind];
+        for (size_t k = 0; k < z.size(); ++k) {            // (z grows while successors free up)
+            const uint32_t o = z[k];
+            if (op_st[o] == OP_DONE) continue;
+            if (op_st[o] == OP_PENDING) {
+                keep.push_back(o);                             // (a delivery whose record has not arrived)
+                continue;
+            }
+            if (op_st[o] == OP_RESOLVED) out.push_back(o);     // (OP_NOOP: not delivered here, nothing to run)
+            finish(o);
+        }
+        z.swap(keep);
+        // in operation order, which is packet order (a flag pass when the round is large)
+        if (out.size() * 16 < op_pkt.size()) {
+            std::sort(out.begin(), out.end());
+        } else {
+            std::vector<uint8_t> f(op_pkt.size(), 0);
+            for (uint32_t o : out) f[o] = 1;
+            size_t j = 0;
+            for (uint32_t o = 0; o < (uint32_t)f.size(); ++o)
+                if (f[o]) out[j++] = o;
+        }
+    }
 };
 
-// live + the creates the pending operations may make > max_entries: the map may fill
-int cv_epnode::refresh_tight(bool all)
+// live + the creates the pending operations may make > max_entries: the map may fill.
+// First round: every map's room; chain the maps that may fill.  Later: the chained maps'
+// room again; a map with room for every create its operations may still make leaves
+// the chain (live + need never grows: an operation adds at most what it took from need).
+int cv_epnode::room(bool first)
 {
     std::vector<int> hs;
     std::vector<uint32_t> ms;
     for (uint32_t m : active)
-        if (map_handle[m] >= 0 && (all || map_tight[m])) {
+        if (map_handle[m] >= 0 && (first || map_chain[m])) {
             hs.push_back(map_handle[m]);
             ms.push_back(m);
         }
@@ -127,38 +221,21 @@ int cv_epnode::refresh_tight(bool all)
                          : cv::ct_counts(ctx, hs, live, cap);
     if (r) return r;
     for (size_t k = 0; k < ms.size(); ++k) {
-        map_live[ms[k]] = live[k];
-        map_cap[ms[k]] = cap[k];
-        map_tight[ms[k]] = (int64_t)live[k] + std::max<int64_t>(map_need[ms[k]], 0) > (int64_t)cap[k];
-    }
-    return 0;
-}
-
-// one in-order pass over every active map's pending operations; ready(o) says whether
-// operation o may run now if nothing earlier blocks it
-template <class Ready>
-void cv_epnode::scan(Ready ready, std::vector<uint32_t> &out)
-{
-    for (uint32_t m : active) {
+        const uint32_t m = ms[k];
+        const bool tight = (int64_t)live[k] + std::max<int64_t>(map_need[m], 0) > (int64_t)cap[k];
         uint32_t &h = map_head[m];
-        const uint32_t end = map_off[m + 1];
-        while (h < end && op_st[map_ops[h]] == OP_DONE) ++h;
-        if (h == end) continue;
-        const uint32_t st = next_stamp();
-        for (uint32_t k = h; k < end; ++k) {
-            const uint32_t o = map_ops[k];
-            if (op_st[o] == OP_DONE) continue;
-            bool free = ready(o);
-            for (uint32_t q = op_poff[o]; free && q < op_poff[o + 1]; ++q) free = stamp[op_peer[q]] != st;
-            if (free) {
-                out.push_back(o);
-                continue;
-            }
-            if (map_tight[m]) break;                       // (the map keeps packet order across peers)
-            for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q) stamp[op_peer[q]] = st;
+        while (h < map_off[m + 1] && op_st[map_ops[h]] == OP_DONE) ++h;
+        if (first && tight) {                                 // every operation after the first waits
+            map_chain[m] = 1;
+            chained0++;
+            for (uint32_t j = map_off[m] + 1; j < map_off[m + 1]; ++j) op_wait[map_ops[j]]++;
+        } else if (!first && !tight && map_chain[m]) {        // out of the chain: drop the links still counted
+            map_chain[m] = 0;
+            for (uint32_t j = std::max(h, map_off[m] + 1); j < map_off[m + 1]; ++j)
+                if (op_st[map_ops[j - 1]] != OP_DONE && op_st[map_ops[j]] != OP_DONE) release(map_ops[j]);
         }
     }
-    std::sort(out.begin(), out.end(), [&](uint32_t x, uint32_t y) { return op_pkt[x] < op_pkt[y]; });
+    return 0;
 }
 
 extern "C" {
@@ -180,22 +257,22 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
         std::sort(hs.begin(), hs.end());
         if (std::adjacent_find(hs.begin(), hs.end()) != hs.end()) return -EINVAL;
     }
-    // address -> endpoints; VIP -> backends; backend -> VIPs
-    std::unordered_map<Addr, std::vector<uint32_t>, AddrHash> where;
-    std::unordered_map<Addr, std::vector<Addr>, AddrHash> backends, vips;
+    // address -> endpoints; VIP -> backends; backend -> VIPs (by 64-bit address hash: a
+    // collision adds candidates or peers, supersets stay exact)
+    std::vector<std::pair<uint64_t, uint32_t>> ew;                // (address, endpoint)
+    std::vector<std::pair<uint64_t, uint64_t>> vb;                // (VIP, backend)
     for (uint32_t e = 0; e < ne; ++e) {
-        if (v.eps[e].ipv4) where[Addr{0, v.eps[e].ipv4, 4}].push_back(e);
         static const uint8_t zero[16] = {};
-        if (memcmp(v.eps[e].ipv6, zero, 16)) where[addr6(v.eps[e].ipv6)].push_back(e);
+        if (v.eps[e].ipv4) ew.push_back({ahash(Addr{0, v.eps[e].ipv4, 4}), e});
+        if (memcmp(v.eps[e].ipv6, zero, 16)) ew.push_back({ahash(addr6(v.eps[e].ipv6)), e});
     }
-    for (auto &s : v.svc) {
-        const Addr vip = s.v6 ? addr6(s.vip) : addr4(s.vip), be = s.v6 ? addr6(s.backend) : addr4(s.backend);
-        auto &b = backends[vip];
-        if (std::find(b.begin(), b.end(), be) == b.end()) b.push_back(be);
-        auto &q = vips[be];
-        if (std::find(q.begin(), q.end(), vip) == q.end()) q.push_back(vip);
-    }
-    const Addr lob{0, v.loopback, 4};
+    for (auto &q : v.svc)
+        vb.push_back({ahash(q.v6 ? addr6(q.vip) : addr4(q.vip)), ahash(q.v6 ? addr6(q.backend) : addr4(q.backend))});
+    std::vector<std::pair<uint64_t, uint64_t>> bv(vb.size());
+    for (size_t k = 0; k < vb.size(); ++k) bv[k] = {vb[k].second, vb[k].first};
+    const Csr<uint32_t> where(std::move(ew));
+    const Csr<uint64_t> backends(std::move(vb)), vips(std::move(bv));
+    const uint64_t lob = ahash(Addr{0, v.loopback, 4});
     std::unique_ptr<cv_epnode> nd(new cv_epnode());
     nd->ctx = ctx;
     nd->rank = rank;
@@ -207,66 +284,127 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
     nd->dl_first.assign(n, ~0u);
     nd->dl_cnt.assign(n, 0);
     nd->op_poff.push_back(0);
-    std::vector<uint32_t> c, sp, dp;
-    static const std::vector<Addr> none;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t *f = frames + (size_t)i * stride;
-        const uint32_t s = src_ep[i];
-        if (s >= ne) return -EINVAL;
-        c.clear();
-        sp.clear();
-        dp.clear();
-        const bool is4 = f[12] == 0x08 && f[13] == 0x00, is6 = f[12] == 0x86 && f[13] == 0xDD;
-        nd->v6[i] = is6;
-        if (is4 || is6) {
-            const Addr sa = is4 ? addr4(f + 26) : addr6(f + 22), da = is4 ? addr4(f + 30) : addr6(f + 38);
-            auto bi = backends.find(da);
-            const std::vector<Addr> &bes = bi == backends.end() ? none : bi->second;
-            auto add_where = [&](const Addr &a) {
-                auto w = where.find(a);
-                if (w != where.end()) c.insert(c.end(), w->second.begin(), w->second.end());
+    // per packet: candidates, peers and operations, over packet ranges on host threads
+    // (each range its own buffers, joined in packet order)
+    struct Part {
+        std::vector<uint32_t> cand, cand_n, op_pkt, op_map, op_np;
+        std::vector<uint8_t> op_kind;
+        std::vector<uint64_t> peer;
+        uint64_t n_src = 0, n_dl = 0;
+        int err = 0;
+    };
+    const uint32_t T = n < (1u << 14) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<Part> parts(T);
+    auto build = [&](uint32_t t, uint32_t i0, uint32_t i1) {
+        Part &P = parts[t];
+        std::vector<uint32_t> c;
+        std::vector<uint64_t> sp, dp;
+        for (uint32_t i = i0; i < i1; ++i) {
+            const uint8_t *f = frames + (size_t)i * stride;
+            const uint32_t s = src_ep[i];
+            if (s >= ne) { P.err = -EINVAL; return; }
+            c.clear();
+            sp.clear();
+            dp.clear();
+            const bool is4 = f[12] == 0x08 && f[13] == 0x00, is6 = f[12] == 0x86 && f[13] == 0xDD;
+            nd->v6[i] = is6;
+            if (is4 || is6) {
+                const uint64_t sa = ahash(is4 ? addr4(f + 26) : addr6(f + 22)), da = ahash(is4 ? addr4(f + 30) : addr6(f + 38));
+                const auto bes = backends.find(da);
+                auto add_where = [&](uint64_t a) {
+                    const auto w = where.find(a);
+                    c.insert(c.end(), where.val.begin() + w.first, where.val.begin() + w.second);
+                };
+                add_where(da);
+                bool loop = false;
+                for (uint32_t k = bes.first; k < bes.second; ++k) {
+                    add_where(backends.val[k]);
+                    loop |= backends.val[k] == sa;
+                }
+                std::sort(c.begin(), c.end());
+                c.erase(std::unique(c.begin(), c.end()), c.end());
+                // peers: the source program's -- the destination, a VIP's backends, and the
+                // loopback address when the client backs the VIP itself; the delivery's -- the
+                // source as the source program left it: itself, a VIP it backs (reverse NAT of
+                // a reply), or the loopback address
+                loop = loop && v.loopback;
+                sp.push_back(da);
+                sp.insert(sp.end(), backends.val.begin() + bes.first, backends.val.begin() + bes.second);
+                dp.push_back(sa);
+                const auto vi = vips.find(sa);
+                dp.insert(dp.end(), vips.val.begin() + vi.first, vips.val.begin() + vi.second);
+                if (loop) {
+                    sp.push_back(lob);
+                    dp.push_back(lob);
+                }
+            }
+            if (c.size() > 255) { P.err = -E2BIG; return; }          // (dl_cnt is a byte)
+            P.cand.insert(P.cand.end(), c.begin(), c.end());
+            P.cand_n.push_back((uint32_t)c.size());
+            const uint32_t fam = is6 ? 1 : 0;
+            auto add_op = [&](uint32_t kind, uint32_t ep, const std::vector<uint64_t> &ps) {
+                P.op_pkt.push_back(i);
+                P.op_kind.push_back((uint8_t)kind);
+                P.op_map.push_back(ep * 2 + fam);
+                P.peer.insert(P.peer.end(), ps.begin(), ps.end());
+                P.op_np.push_back((uint32_t)ps.size());
             };
-            add_where(da);
-            for (const Addr &b : bes) add_where(b);
-            std::sort(c.begin(), c.end());
-            c.erase(std::unique(c.begin(), c.end()), c.end());
-            // peers: the source program's -- the destination, a VIP's backends, and the
-            // loopback address when the client backs the VIP itself; the delivery's -- the
-            // source as the source program left it: itself, a VIP it backs (reverse NAT of
-            // a reply), or the loopback address
-            const bool loop = v.loopback && std::find(bes.begin(), bes.end(), sa) != bes.end();
-            sp.push_back(peer_slot(da));
-            for (const Addr &b : bes) sp.push_back(peer_slot(b));
-            dp.push_back(peer_slot(sa));
-            auto vi = vips.find(sa);
-            if (vi != vips.end())
-                for (const Addr &x : vi->second) dp.push_back(peer_slot(x));
-            if (loop) {
-                sp.push_back(peer_slot(lob));
-                dp.push_back(peer_slot(lob));
+            if (nd->owned(s)) {
+                add_op(0, s, sp);
+                P.n_src++;
             }
+            for (uint32_t d : c)
+                if (nd->owned(d)) {
+                    add_op(1, d, dp);
+                    P.n_dl++;
+                }
         }
-        nd->cand.insert(nd->cand.end(), c.begin(), c.end());
-        nd->cand_off[i + 1] = (uint32_t)nd->cand.size();
-        const uint32_t fam = is6 ? 1 : 0;
-        auto add_op = [&](uint32_t kind, uint32_t ep, const std::vector<uint32_t> &ps) {
-            nd->op_pkt.push_back(i);
-            nd->op_kind.push_back((uint8_t)kind);
-            nd->op_map.push_back(ep * 2 + fam);
-            nd->op_peer.insert(nd->op_peer.end(), ps.begin(), ps.end());
-            nd->op_poff.push_back((uint32_t)nd->op_peer.size());
-        };
-        if (nd->owned(s)) {
-            add_op(0, s, sp);
-            nd->n_src++;
+    };
+    {
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < T; ++t)
+            th.emplace_back(build, t, (uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T));
+        for (auto &x : th) x.join();
+    }
+    std::vector<uint64_t> peer64;                                 // (the operations' peers, as hashes)
+    {
+        size_t nc = 0, no = 0, np = 0;
+        for (auto &P : parts) {
+            if (P.err) return P.err;
+            nc += P.cand.size();
+            no += P.op_pkt.size();
+            np += P.peer.size();
         }
-        for (uint32_t d : c)
-            if (nd->owned(d)) {
-                if (nd->dl_first[i] == ~0u) nd->dl_first[i] = (uint32_t)nd->op_pkt.size();
-                nd->dl_cnt[i]++;
-                add_op(1, d, dp);
-                nd->n_dl++;
+        nd->cand.reserve(nc);
+        nd->op_pkt.reserve(no);
+        nd->op_kind.reserve(no);
+        nd->op_map.reserve(no);
+        nd->op_poff.reserve(no + 1);
+        peer64.reserve(np);
+        uint32_t i = 0;
+        for (auto &P : parts) {
+            for (uint32_t k : P.cand_n) {
+                nd->cand_off[i + 1] = nd->cand_off[i] + k;
+                ++i;
             }
+            nd->cand.insert(nd->cand.end(), P.cand.begin(), P.cand.end());
+            for (size_t k = 0; k < P.op_pkt.size(); ++k) {
+                const uint32_t o = (uint32_t)nd->op_pkt.size(), pk = P.op_pkt[k];
+                if (P.op_kind[k] == 1) {
+                    if (nd->dl_first[pk] == ~0u) nd->dl_first[pk] = o;
+                    nd->dl_cnt[pk]++;
+                }
+                nd->op_pkt.push_back(pk);
+                nd->op_kind.push_back(P.op_kind[k]);
+                nd->op_map.push_back(P.op_map[k]);
+                nd->op_poff.push_back(nd->op_poff.back() + P.op_np[k]);
+            }
+            peer64.insert(peer64.end(), P.peer.begin(), P.peer.end());
+            nd->n_src += P.n_src;
+            nd->n_dl += P.n_dl;
+            std::vector<uint32_t>().swap(P.cand);
+            std::vector<uint64_t>().swap(P.peer);
+        }
     }
     const uint32_t nops = (uint32_t)nd->op_pkt.size(), nm = ne * 2;
     nd->op_st.assign(nops, OP_PENDING);
@@ -283,18 +421,53 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
         for (uint32_t o = 0; o < nops; ++o) nd->map_ops[at[nd->op_map[o]]++] = o;
     }
     nd->map_head.assign(nd->map_off.begin(), nd->map_off.end() - 1);
+    nd->op_mpos.resize(nops);
+    for (uint32_t k = 0; k < nops; ++k) nd->op_mpos[nd->map_ops[k]] = k;
+    // the key links: per map, its (peer, operation) references sorted, consecutive ones on
+    // one peer linked (an operation naming a peer twice links once)
+    nd->ref_next.assign(peer64.size(), cv_epnode::NONE);
+    nd->ref_prev.assign(peer64.size(), cv_epnode::NONE);
+    nd->op_wait.assign(nops, 0);
+    {
+        std::vector<uint32_t> &ref_op = nd->ref_op;
+        ref_op.resize(peer64.size());
+        for (uint32_t o = 0; o < nops; ++o)
+            for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) ref_op[q] = o;
+        // maps are independent: their links are built on host threads, each with its
+        // maps' share of the wait counts (an operation is in one map)
+        auto link = [&](uint32_t m0, uint32_t m1) {
+            std::vector<std::pair<uint64_t, uint32_t>> u;         // (peer, reference)
+            for (uint32_t m = m0; m < m1; ++m) {
+                u.clear();
+                for (uint32_t k = nd->map_off[m]; k < nd->map_off[m + 1]; ++k) {
+                    const uint32_t o = nd->map_ops[k];
+                    for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) u.push_back({peer64[q], q});
+                }
+                std::sort(u.begin(), u.end());                // (references ascend with their operations)
+                for (size_t k = 1; k < u.size(); ++k) {
+                    if (u[k - 1].first != u[k].first) continue;
+                    const uint32_t a = ref_op[u[k - 1].second], b = ref_op[u[k].second];
+                    if (a == b) continue;                      // (a peer named twice by one operation)
+                    nd->ref_next[u[k - 1].second] = u[k].second;   // (b waits for a on this peer)
+                    nd->ref_prev[u[k].second] = u[k - 1].second;
+                    nd->op_wait[b]++;
+                }
+            }
+        };
+        const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < T; ++t) th.emplace_back(link, (uint32_t)((uint64_t)nm * t / T), (uint32_t)((uint64_t)nm * (t + 1) / T));
+        for (auto &x : th) x.join();
+    }
     nd->map_handle.assign(nm, -1);
     nd->map_need.assign(nm, 0);
-    nd->map_live.assign(nm, 0);
-    nd->map_cap.assign(nm, 0);
-    nd->map_tight.assign(nm, 0);
+    nd->map_chain.assign(nm, 0);
     for (uint32_t m = 0; m < nm; ++m) {
         if (nd->map_off[m + 1] == nd->map_off[m]) continue;
         nd->active.push_back(m);
         nd->map_handle[m] = (m & 1) ? v.eps[m >> 1].ct6 : v.eps[m >> 1].ct4;
     }
     for (uint32_t o = 0; o < nops; ++o) nd->map_need[nd->op_map[o]] += MAX_CREATES[nd->op_kind[o]];
-    nd->stamp.assign(PEER_SLOTS, 0u);
     *out = nd.release();
     return 0;
 }
@@ -315,11 +488,11 @@ int cv_epnode_stats(const cv_epnode *nd, uint64_t stats[6])
 {
     if (!nd || !stats) return -EINVAL;
     uint64_t t = 0;
-    for (uint32_t m : nd->active) t += nd->map_tight[m];
+    for (uint32_t m : nd->active) t += nd->map_chain[m];
     stats[0] = nd->rounds;
     stats[1] = nd->n_src;
     stats[2] = nd->n_dl;
-    stats[3] = nd->tight0;
+    stats[3] = nd->chained0;
     stats[4] = t;
     stats[5] = nd->sent;
     return 0;
@@ -329,21 +502,19 @@ int cv_epnode_sources(cv_epnode *nd, uint32_t *pkts, uint32_t cap)
 {
     if (!nd || (cap && !pkts)) return -EINVAL;
     int r;
-    if (!nd->rounds++) {                                   // every map's room, once
-        if ((r = nd->refresh_tight(true))) return r;
-        for (uint32_t m : nd->active) nd->tight0 += nd->map_tight[m];
+    if (!nd->rounds++) {                                   // every map's room, once; then who waits for nothing
+        if ((r = nd->room(true))) return r;
+        for (uint32_t o = 0; o < (uint32_t)nd->op_pkt.size(); ++o)
+            if (!nd->op_wait[o]) nd->zero[nd->op_kind[o]].push_back(o);
     } else {
         bool any = false;
-        for (uint32_t m : nd->active) any |= nd->map_tight[m] != 0;
-        if (any && (r = nd->refresh_tight(false))) return r;   // (room re-read for the maps that may fill)
+        for (uint32_t m : nd->active) any |= nd->map_chain[m] != 0;
+        if (any && (r = nd->room(false))) return r;        // (room re-read for the maps that may fill)
     }
     std::vector<uint32_t> out;
-    nd->scan([&](uint32_t o) { return nd->op_kind[o] == 0; }, out);
+    nd->run_ready(0, out);
     if (out.size() > cap) return -ENOSPC;
-    for (size_t j = 0; j < out.size(); ++j) {
-        pkts[j] = nd->op_pkt[out[j]];
-        nd->finish(out[j]);
-    }
+    for (size_t j = 0; j < out.size(); ++j) pkts[j] = nd->op_pkt[out[j]];
     return (int)out.size();
 }
 
@@ -386,17 +557,17 @@ int cv_epnode_receive(cv_epnode *nd, const uint32_t *row_pkt, const uint32_t *ro
     if (!nd || (n && (!row_pkt || !row_ep || !row_has || !op))) return -EINVAL;
     for (uint32_t j = 0; j < n; ++j) {
         const uint32_t i = row_pkt[j];
-        if (i >= nd->n || nd->dl_first[i] == ~0u) return -EPROTO;
+        if (i >= nd->n || nd->dl_first[i] == cv_epnode::NONE) return -EPROTO;
         uint32_t o = nd->dl_first[i], k = 0;
         while (k < nd->dl_cnt[i] && nd->op_map[o] >> 1 != row_ep[j]) ++k, ++o;
         if (k == nd->dl_cnt[i] || nd->op_st[o] != OP_PENDING) return -EPROTO;
-        if (row_has[j]) {
-            nd->op_st[o] = OP_RESOLVED;
-            op[j] = (int32_t)o;
-        } else {
-            nd->finish(o);                                 // (delivered elsewhere, or not at all)
-            op[j] = -1;
-        }
+        // a record: the delivery runs once nothing earlier on its keys waits; none: nothing
+        // runs here -- it leaves its keys' lists now (its successors wait for its pending
+        // predecessors instead), or, on a chained map, runs as a no-op in its turn
+        op[j] = row_has[j] ? (int32_t)o : -1;
+        if (row_has[j]) nd->op_st[o] = OP_RESOLVED;
+        else if (nd->map_chain[nd->op_map[o]]) nd->op_st[o] = OP_NOOP;
+        else nd->splice(o);
     }
     return 0;
 }
@@ -405,12 +576,11 @@ int cv_epnode_deliveries(cv_epnode *nd, uint32_t *ops, uint32_t *pkts, uint32_t 
 {
     if (!nd || (cap && (!ops || !pkts))) return -EINVAL;
     std::vector<uint32_t> out;
-    nd->scan([&](uint32_t o) { return nd->op_kind[o] == 1 && nd->op_st[o] == OP_RESOLVED; }, out);
+    nd->run_ready(1, out);
     if (out.size() > cap) return -ENOSPC;
     for (size_t j = 0; j < out.size(); ++j) {
         ops[j] = out[j];
         pkts[j] = nd->op_pkt[out[j]];
-        nd->finish(out[j]);
     }
     return (int)out.size();
 }

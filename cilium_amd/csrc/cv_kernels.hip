@@ -2512,6 +2512,136 @@ __global__ void __launch_bounds__(BLOCK) k_gather_u64(unsigned long long *const 
         out[k] = __hip_atomic_load(ptrs[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+int grid_for(uint32_t n);
+
+// ------------------------------------------------------------------ room check (CtBound, cv_dp.hpp)
+__device__ __forceinline__ void bound_add(const CtBound &bd, const uint16_t *epmi, uint32_t e, uint32_t w)
+{
+    if (e >= bd.n_eps) return;
+    const uint32_t m = epmi[e];
+    if (m < bd.nmaps) atomicAdd(bd.bound + m, (unsigned long long)w);
+}
+
+// the endpoint index (0-based) of a local endpoint address, or ~0 (host / none)
+__device__ __forceinline__ uint32_t bound_ep(const DpParams &p, const uint32_t *addr, bool v6)
+{
+    uint32_t iv = 0;
+    const int64_t sl = v6 ? dev_find<LxcV6Spec>(p.lxc6, addr, &iv) : dev_find<LxcV4Spec>(p.lxc4, addr, &iv);
+    if (sl < 0 || (iv & (1u << 16)) || !p.ep_of_lxc) return ~0u;
+    const uint32_t e = p.ep_of_lxc[iv & 0xFFFFu];
+    return e ? e - 1 : ~0u;
+}
+
+__device__ __forceinline__ uint32_t bound_ld32(const uint8_t *f) { return f[0] | f[1] << 8 | f[2] << 16 | (uint32_t)f[3] << 24; }
+
+// per packet (or delivery record): its source map's and destination map's creates; the
+// service masters that may serve it counted per LB slot
+__global__ void __launch_bounds__(BLOCK) k_bound_pkts(DpParams p, BatchDev b, const uint4 *records, CtBound bd)
+{
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
+        if (bd.mode == 2) {                                       // a delivery record: its destination
+            const uint32_t w = reinterpret_cast<const uint32_t *>(records + (size_t)i * DEL_SLOTS)[b.stride >= 128 ? 12 : 6];
+            bound_add(bd, b.stride >= 128 ? bd.epmi6 : bd.epmi4, w & 0xFFFFu, bd.w_dst);
+            continue;
+        }
+        const uint8_t *f = b.frames + (size_t)i * b.stride;
+        const uint32_t len = min(b.len[i], b.stride), eth = f[12] << 8 | f[13];
+        const bool v6 = eth == 0x86DDu;
+        if ((eth != 0x0800u && !v6) || len < (v6 ? 54u : 34u)) continue;   // (no conntrack)
+        const uint16_t *epmi = v6 ? bd.epmi6 : bd.epmi4;
+        if (bd.mode == 1) bound_add(bd, epmi, bd.src_ep ? bd.src_ep[i] : bd.ep0, bd.w_src);
+        uint32_t da[4];
+        for (int j = 0; j < (v6 ? 4 : 1); ++j) da[j] = bound_ld32(f + (v6 ? 38 : 30) + 4 * j);
+        bound_add(bd, epmi, bound_ep(p, da, v6), bd.w_dst);
+        if (bd.mode != 1) continue;
+        // the service masters (daddr, dport) and (daddr, 0) that may serve it (lb{4,6}_lookup_service)
+        uint32_t nh, off;
+        if (!v6) {
+            nh = f[23];
+            off = 14 + 4 * (f[14] & 0xFu);
+        } else {
+            nh = f[20];
+            off = 54;
+            if (nh != 6 && nh != 17 && nh != 58) {                // (an extension header, or no service: the
+                if (nh == 0 || nh == 43 || nh == 60 || nh == 51 || nh == 44 || nh == 50)   //  datapath's own
+                    atomicAdd(bd.flag + 1, 1u);                   //  ipv6_hdrlen walk decides: unseen)
+                continue;
+            }
+        }
+        uint32_t dport = 0;
+        if (nh == 6 || nh == 17) {
+            if (off + 4 > len) {                                  // (a port the check cannot read)
+                atomicAdd(bd.flag + 1, 1u);
+                continue;
+            }
+            dport = f[off + 2] | f[off + 3] << 8;
+        } else if (nh != 1 && nh != 58) {
+            continue;                                             // (skip_service_lookup)
+        }
+        for (int k = 0; k < 2; ++k) {
+            if (k == 0 && !dport) continue;
+            const uint32_t port = k == 0 ? dport : 0u;
+            if (!v6) {
+                const uint32_t key[2] = {da[0], port};
+                uint32_t v[3];
+                const int64_t sl = dev_find<Lb4Spec>(p.lb4, key, v);
+                if (sl >= 0 && (v[1] >> 16)) atomicAdd(bd.svc4 + sl, 1u);
+            } else {
+                const uint32_t key[5] = {da[0], da[1], da[2], da[3], port};
+                uint32_t v[6];
+                const int64_t sl = dev_find<Lb6Spec>(p.lb6, key, v);
+                if (sl >= 0 && (v[4] >> 16)) atomicAdd(bd.svc6 + sl, 1u);
+            }
+        }
+    }
+}
+
+// every backend (slave entry) of a master that may serve packets: its endpoint's map
+// takes up to w_dst creates per such packet
+template <class S, bool V6>
+__global__ void __launch_bounds__(BLOCK) k_bound_svc(DpParams p, CtBound bd)
+{
+    const HashTable &t = V6 ? p.lb6 : p.lb4;
+    const uint32_t *cnt = V6 ? bd.svc6 : bd.svc4;
+    const uint64_t slots = (t.mask + 1) * S::SPB;
+    for (uint64_t x = blockIdx.x * (uint64_t)BLOCK + threadIdx.x; x < slots; x += (uint64_t)gridDim.x * BLOCK) {
+        const uint64_t bk = x / S::SPB;
+        const uint32_t sl = (uint32_t)(x % S::SPB);
+        const uint32_t *bw = t.buckets + bk * S::BW;
+        const uint32_t tag = (bw[sl >> 2] >> (8 * (sl & 3))) & 0xFFu;
+        if (tag < 3) continue;
+        uint32_t key[S::KW];
+        for (int j = 0; j < S::KW; ++j) key[j] = bw[S::KEY0 + sl * S::KS + j];
+        if (!(key[S::KW - 1] >> 16)) continue;                   // (a master entry)
+        key[S::KW - 1] &= 0xFFFFu;
+        uint32_t v[S::IVW];
+        const int64_t ms = dev_find<S>(t, key, v);
+        if (ms < 0 || !cnt[ms]) continue;
+        uint32_t be[4];
+        for (int j = 0; j < (V6 ? 4 : 1); ++j) be[j] = bw[S::IVAL0 + sl * S::IVW + j];
+        bound_add(bd, V6 ? bd.epmi6 : bd.epmi4, bound_ep(p, be, V6), bd.w_dst * cnt[ms]);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_bound_check(CtBound bd)
+{
+    const unsigned long long unseen = (unsigned long long)bd.flag[1] * bd.w_dst;
+    for (uint32_t m = blockIdx.x * BLOCK + threadIdx.x; m < bd.nmaps; m += gridDim.x * BLOCK)
+        if (*bd.live[m] + bd.bound[m] + unseen > bd.cap[m]) bd.flag[0] = 1u;
+}
+
+int launch_ct_bound(const DpParams &p, const BatchDev &b, const uint4 *records, const CtBound &bd, hipStream_t s)
+{
+    if (b.n) hipLaunchKernelGGL(k_bound_pkts, dim3(grid_for(b.n)), dim3(BLOCK), 0, s, p, b, records, bd);
+    if (bd.mode == 1) {
+        if (p.lb4.buckets) hipLaunchKernelGGL((k_bound_svc<Lb4Spec, false>), dim3(1024), dim3(BLOCK), 0, s, p, bd);
+        if (p.lb6.buckets) hipLaunchKernelGGL((k_bound_svc<Lb6Spec, true>), dim3(1024), dim3(BLOCK), 0, s, p, bd);
+    }
+    hipLaunchKernelGGL(k_bound_check, dim3((bd.nmaps + BLOCK - 1) / BLOCK < 256 ? (bd.nmaps + BLOCK - 1) / BLOCK + 1 : 256),
+                       dim3(BLOCK), 0, s, bd);
+    return launch_status(__func__);
+}
+
 int launch_gather_u64(unsigned long long *const *ptrs, unsigned long long *out, uint32_t n, hipStream_t s)
 {
     if (!n) return 0;

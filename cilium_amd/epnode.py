@@ -61,7 +61,6 @@ class EpNode:
         self.v6, rows = families(frames)
         self.sched = lib.EpSched(ctx, rank, world, frames, src_ep)
         st = self.sched.stats()
-        self.v6_d = torch.from_numpy(self.v6).to(device)
         self.rows_d = torch.from_numpy(rows).to(device)
         # the batch on the device, per family (64-B IPv4 / 128-B IPv6 records); `parts`: already
         # resident (bench.py builds every step's batch before its timed region)
@@ -79,7 +78,7 @@ class EpNode:
         self.mine = torch.zeros(n, dtype=torch.bool, device=device)   # outputs final on this rank
         # records filed by delivery operation (the op ids cv_epnode_receive names index all of
         # this rank's operations, sources included)
-        self.store = torch.zeros((st["source_ops"] + st["delivery_ops"] + 1, REC), dtype=torch.uint8, device=device)
+        self.store = torch.empty((st["source_ops"] + st["delivery_ops"] + 1, REC), dtype=torch.uint8, device=device)
         self.rounds = 0
         self.launches = 0
         self.cross = 0                                             # deliveries whose source ran on another rank

@@ -499,21 +499,36 @@ def main():
     full_last = full_maps() if per_ep is not None else None
     gc_timed = gc_deleted[0]
 
-    # accounting step (untimed, after the timed region, in the same regime): L(p), U(p)
+    # accounting step (untimed, after the timed region, in the same regime): L(p), U(p); the
+    # stateful paths count with CV_F_ACCT_SPLIT, which splits out the conntrack lookups and
+    # writes (the HBM-resident lines of B(p)) -- pinned equal to the oracle's split in
+    # tests/test_gpu_egress.test_acct_split_counts and test_config5_bench_regime
+    from cilium_amd import lib
     acct = dict(out)
     acct["nl"] = torch.zeros(n, dtype=torch.uint8, device=device)
     acct["nu"] = torch.zeros(n, dtype=torch.uint8, device=device)
+    if stateful:
+        ctx.set_flags(lib.F_DEFAULT | lib.F_ACCT_SPLIT)
     step(acct, v)
     torch.cuda.synchronize()
+    if stateful:
+        ctx.set_flags(lib.F_DEFAULT)
     nl, nu = acct["nl"].cpu().numpy(), acct["nu"].cpu().numpy()
+    ct_lines = None
+    if stateful:
+        U = lib.ACCT_CT_UNIT
+        ct_lines = nl.astype(np.int64) // U + nu.astype(np.int64) // U
+        nl, nu = nl // U + nl % U, nu // U + nu % U
     created = int((acct["ct"].cpu().numpy() == 0).sum()) if stateful else 0
-    hbm_res = hbm_resident_bytes(acct["ct"].cpu().numpy(), acct["ret"].cpu().numpy()) \
+    hbm_model = hbm_resident_bytes(acct["ct"].cpu().numpy(), acct["ret"].cpu().numpy()) \
         if name in ("config3", "config4") else None
     if name == "config5":
         k4 = offs[1]
         alg_bytes = algorithmic_bytes(name, nl[:k4], nu[:k4], 64) + algorithmic_bytes(name, nl[k4:], nu[k4:], 128)
+        hbm_res = k4 * (64 + 9) + (n - k4) * (128 + 9) + 64 * int(ct_lines.sum())
     else:
         alg_bytes = algorithmic_bytes(name, nl, nu)
+        hbm_res = n * (64 + 9) + 64 * int(ct_lines.sum()) if stateful else None
     del acct
     log(f"[rank {rank}] accounting step done ({time.time() - t0:.1f}s)")
 
@@ -600,7 +615,9 @@ def main():
                     "achieved": round(hbm_res / (kern_ms * 1e-3) / 1e9, 1), "unit": "GB/s",
                     "frac_random_access": None if ra_peak is None else
                     round(hbm_res / (kern_ms * 1e-3) / 1e9 / ra_peak, 4),
-                    "how": "bench.hbm_resident_bytes: CT probes / writes per packet from its CT result"},
+                    "how": "the record stream, the outputs and 64 B per conntrack lookup / write the kernels "
+                           "counted (CV_F_ACCT_SPLIT accounting step)",
+                    "model_bytes_per_step": hbm_model},
             },
             "cpu_baseline": cpu,
         }
@@ -694,7 +711,7 @@ def ep_owned(args, rank, world, local, device, dist, out_fd):
     for _ in range(args.steps):
         node, tr = step(v)
         t_run += tr
-        stats.append((node.rounds, node.launches, node.cross, node.sched.stats()))
+        stats.append((node.rounds, node.launches, node.cross, node.sched.stats(), dict(node.times)))
         v += 1
     torch.cuda.synchronize()
     if dist:
@@ -739,6 +756,8 @@ def ep_owned(args, rank, world, local, device, dist, out_fd):
                 "cross_rank_deliveries_per_step": cross // max(args.steps, 1),
                 "maps_ordered_whole_first_round_rank0": stats[-1][3]["maps_ordered_whole_at_open"],
                 "run_ms_per_step": round(t_run * 1e3 / args.steps, 3),
+                "run_ms_split_rank0": {k: round(sum(x[4][k] for x in stats) * 1e3 / args.steps, 3)
+                                       for k in stats[0][4]},
                 "schedule_build_ms_per_step": round(ms - t_run * 1e3 / args.steps, 3),
                 "how": "bench.ep_owned: step = cv_epnode_open (candidates, peers, operations) + EpNode.run "
                        "(per round: split launches, exchange, delivery launches; one host wait)"},

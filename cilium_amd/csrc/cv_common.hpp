@@ -48,6 +48,9 @@ constexpr uint32_t F_FROM_HOST = 0x1, F_HAVE_L4_POLICY = 0x2, F_DROP_ALL = 0x4, 
 // group key, so groups of different address pairs and CT maps merge into long runs (a
 // coarser grouping is equally exact: DESIGN.md §4)
 constexpr uint32_t F_TEST_COARSE_GROUPS = 0x80000000u;
+// CV_F_ACCT_SPLIT (include/cilium_hip.h): nl / nu count conntrack lookups and writes
+// ACCT_CT_UNIT each (cv_dev.hpp), for the HBM-resident split of the algorithmic bytes
+constexpr uint32_t F_ACCT_SPLIT = 0x40;
 
 // conntrack.h:31-66
 constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,

@@ -449,7 +449,12 @@ struct Acct {
     uint32_t killed = 0;       // admission: entries deleted
     const Snap *snap = nullptr;  // egress admission with many CT maps: slots saved before their first write
     uint32_t spkt = 0, scnt = 0;   // (the packet and its log entries so far)
+    uint32_t ctu = 1;          // what a conntrack lookup / write adds to nl / nu (ACCT_CT_UNIT: the split)
 };
+// CV_F_ACCT_SPLIT: conntrack lookups and writes count ACCT_CT_UNIT in nl / nu, the other
+// lookups and writes 1 -- one accounting pass gives the HBM-resident share of B(p)
+constexpr uint32_t ACCT_CT_UNIT = 32;
+__device__ __forceinline__ uint32_t ct_unit(const DpParams &p) { return (p.flags & F_ACCT_SPLIT) ? ACCT_CT_UNIT : 1u; }
 
 // lookup_ip4_endpoint (eps.h:37-46): ival = lxc_id | HOST << 16 | (ifindex != 0) << 17
 __device__ __forceinline__ bool lxc4_find(const DpParams &p, uint32_t daddr_raw, uint32_t &ival, Acct &a)
@@ -1191,7 +1196,7 @@ __device__ __forceinline__ int ct_lookup_one(const HashTable &ct, const T &t, in
 {
     uint32_t k[T::KW];
     t.key(k);
-    a.nl++;
+    a.nl += a.ctu;
     slot = dev_find<typename T::Spec>(ct, k, nullptr);
     if (slot < 0) {
         if (mon) *mon = true;
@@ -1214,7 +1219,7 @@ template <class S>
 __device__ __forceinline__ void ct_hit(const HashTable &ct, int64_t slot, int action, int dir, bool tcp, uint32_t seen,
                                        uint32_t len, uint32_t now, uint32_t flags, CtState *st, Acct &a, bool *mon)
 {
-    a.nu++;
+    a.nu += a.ctu;
     CtE e;
     ct_load_hot<S>(ct, slot, e);
     if (a.snap) {                                                 // (egress admission, many maps: the parts
@@ -1328,7 +1333,7 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
             p2 = probe_begin<S, FRESH>(ct, k2);
         }
     }
-    a.nl++;
+    a.nl += a.ctu;
     slot = probe_end<S, FRESH>(p1, ct, k1, nullptr);
     if constexpr (ONE) {
         const bool first = slot >= 0;
@@ -1336,7 +1341,7 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
             if (mon) *mon = true;                                 // the first __ct_lookup missed
             if (dir == CT_SERVICE) return CT_NEW;
             t = t2;
-            a.nl++;
+            a.nl += a.ctu;
             slot = probe_end<S, FRESH>(p2, ct, k2, nullptr);
             if (slot < 0) return CT_NEW;
         }
@@ -1351,7 +1356,7 @@ __device__ __forceinline__ int ct_lookup(const HashTable &ct, T &t, const L4Hdr 
     if (mon) *mon = true;                                         // the first __ct_lookup missed
     if (dir == CT_SERVICE) return CT_NEW;
     t = t2;
-    a.nl++;
+    a.nl += a.ctu;
     slot = probe_end<S, FRESH>(p2, ct, k2, nullptr);
     if (slot < 0) return CT_NEW;
     ct_hit<S>(ct, slot, action, dir, tcp, seen, len, now, flags, st, a, mon);
@@ -1384,19 +1389,19 @@ __device__ __forceinline__ int ct_lookup_pre(const HashTable &ct, T &t, const L4
     t.key(k1);
     t2.key(k2);
     int ret;
-    a.nl++;
+    a.nl += a.ctu;
     slot = dev_find<S, false>(ct, k1, nullptr);
     if (slot >= 0) {
         ret = (t.flags & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
     } else {
         if (dir == CT_SERVICE) return CT_NEW;
         t = t2;
-        a.nl++;
+        a.nl += a.ctu;
         slot = dev_find<S, false>(ct, k2, nullptr);
         if (slot < 0) return CT_NEW;
         ret = CT_ESTABLISHED;
     }
-    a.nu++;
+    a.nu += a.ctu;
     const CV_G uint32_t *hw = ct_hot<S>(ct, slot);                 // hot words h1 = w9, h4 = w10
     const uint32_t w9 = hw[1], w10 = hw[4];
     if (st) {
@@ -1453,7 +1458,7 @@ __device__ __forceinline__ void ct_kill(const HashTable &ct, int64_t slot, Acct 
     snap_before<S>(a, ct, slot, SNAP_HOT | SNAP_COLD);
     dev_kill<S>(ct, slot);
     ct_live_add(ct, a, guard, -1);
-    a.nu++;
+    a.nu += a.ctu;
     a.killed++;
 }
 
@@ -1495,7 +1500,7 @@ __device__ __forceinline__ int ct_create(const HashTable &ct, const T &t, uint32
     const bool tcp = t.nexthdr == 6;
     ct_entry_new(e, tcp, len, dir, st, now);
     const bool nat = !V6 && st.addr;
-    a.nu += nat ? 3 : 2;
+    a.nu += (nat ? 3u : 2u) * a.ctu;
     if (!ct_put(ct, t, e, a, guard, absent)) return DROP_CT_CREATE_FAILED;
     if constexpr (!V6) {
         if (nat && !defer_nat) {
@@ -2080,7 +2085,7 @@ __device__ __forceinline__ int ipv4_policy(const DpParams &p, const EpDev &ep, S
             if (skip_proxy) verdict = 0;
             if (ret == CT_NEW) {
                 if (may_defer) {                                   // k_ct_commit writes it
-                    a.nu += 2;
+                    a.nu += 2 * a.ctu;
                     *defer = true;
                 } else {
                     CtState sn{0, 0, 0, 0, 0, src_label};
@@ -2183,7 +2188,7 @@ __device__ __forceinline__ int ipv6_policy(const DpParams &p, const EpDev &ep, S
             if (skip_proxy) verdict = 0;
             if (ret == CT_NEW) {
                 if (may_defer) {
-                    a.nu += 2;
+                    a.nu += 2 * a.ctu;
                     *defer = true;
                 } else {
                     const int c = ct_create<true>(ep.ct6, t, s.len, CT_INGRESS, sn, now, a, p.ct_guard, false, true);

@@ -382,6 +382,7 @@ __global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, 
 #pragma unroll
         for (int k = 0; k < 4; ++k) es[k] = make_uint4(0u, 0u, 0u, 0u);
         Acct a{0, 0};
+        a.ctu = ct_unit(p);
         EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
         uint32_t *eg = g.eg + (size_t)i * EG_WORDS;
         const uint32_t e = src_ep ? src_ep[i] : ep0;
@@ -469,6 +470,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    a.ctu = ct_unit(p);
     EgAdm adm(p, i, a, true, M::SN);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
@@ -511,7 +513,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
         st.slave = hsh % (v[1] >> 16) + 1;
         uint32_t tk[4];                                           // ct_update4_slave
         t.key(tk);
-        a.nl++;
+        a.nl += a.ctu;
         const int64_t s2 = dev_find<Ct4Spec, EGF>(ep.ct4, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
@@ -520,7 +522,7 @@ __device__ __forceinline__ void lb4_one(const DpParams &p, const BatchDev &b, co
             const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
             ct_store_hot_diff<Ct4Spec>(ep.ct4, s2, e, e0);
-            a.nu++;
+            a.nu += a.ctu;
         }
     }
     {
@@ -578,6 +580,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
     m.src_id = ep.lxc_id;
     m.src_label = ep.seclabel;
     Acct a{o.nl ? o.nl[i] : 0u, o.nu ? o.nu[i] : 0u, m.pc};
+    a.ctu = ct_unit(p);
     EgAdm adm(p, i, a, true, M::SN);
     EgOut res{TC_ACT_OK, 0, 0, CT_NONE, 0};
     const uint32_t hsh = hash ? hash[i] : 0u;
@@ -619,7 +622,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
         st.slave = hsh % (v[4] >> 16) + 1;
         uint32_t tk[10];                                          // ct_update6_slave
         t.key(tk);
-        a.nl++;
+        a.nl += a.ctu;
         const int64_t s2 = dev_find<Ct6Spec, EGF>(ep.ct6, tk, nullptr);
         if (s2 >= 0) {
             CtE e;
@@ -628,7 +631,7 @@ __device__ __forceinline__ void lb6_one(const DpParams &p, const BatchDev &b, co
             const CtE e0 = e;
             e.w[10] = (e.w[10] & 0xFFFF0000u) | (st.slave & 0xFFFFu);
             ct_store_hot_diff<Ct6Spec>(ep.ct6, s2, e, e0);
-            a.nu++;
+            a.nu += a.ctu;
         }
     }
     {
@@ -1059,6 +1062,7 @@ __device__ __forceinline__ void egress4_one(const DpParams &p, const BatchDev &b
     uint32_t epi = 0, fl = 0;
     EpDev ep{};
     Acct a{0, 0, m.pc};
+    a.ctu = ct_unit(p);
     if (live) {
         eg4_unpack(g.est + (size_t)i * 4, b.stride, x, epi, fl);
         // the source endpoint's tables and SECLABEL from its EpHot line (with one policy
@@ -1237,6 +1241,7 @@ __device__ __forceinline__ void egress6_one(const DpParams &p, const BatchDev &b
     uint32_t epi = 0;
     EpDev ep{};
     Acct a{0, 0, m.pc};
+    a.ctu = ct_unit(p);
     if (live) {
         eg6_unpack(g.est + (size_t)i * 4, b.stride, x, epi);
         ep = ep_uni6<M::EV>(p, epi);
@@ -1391,6 +1396,7 @@ __device__ __forceinline__ void deliver4_one(const DpParams &p, const BatchDev &
     }
     Skb4 s = skb4_unpack(d0, d1.x, d1.y & 0x3FFu, b.stride);
     Acct a{(d1.y >> 16) & 0xFFu, d1.y >> 24, m.pc};
+    a.ctu = ct_unit(p);
     EgAdm adm(p, i, a, live, M::SN, 1, d1.z & 0xFFFFu);
     EgOut res{TC_ACT_OK, 0, d2.y, (uint8_t)(d1.z >> 16), 0};
     if (live) {
@@ -1440,6 +1446,7 @@ __device__ __forceinline__ void deliver6_one(const DpParams &p, const BatchDev &
     s.h.c2a = unchk2((d2.w >> 6) & 3u);
     s.h.c2b = unchk2((d2.w >> 8) & 3u);
     Acct a{(d2.w >> 16) & 0xFFu, d2.w >> 24, m.pc};
+    a.ctu = ct_unit(p);
     EgAdm adm(p, i, a, live, M::SN, 1, d3.x & 0xFFFFu);
     EgOut res{TC_ACT_OK, 0, d3.w, (uint8_t)(d3.x >> 16), 0};
     if (live) {

@@ -58,6 +58,7 @@ __global__ void __launch_bounds__(BLOCK) k_xdp_prefilter(DpParams p, BatchDev b,
         Rec r;
         rec_load_wave(r, p, b, i0, i, live, st);
         Acct a{0, 0};
+        a.ctu = ct_unit(p);
         const uint8_t v = xdp_verdict_q(p, r, a, live, st);
         if (!live) continue;
         if (o.xdp) o.xdp[i] = v;                                 // (streaming byte stores: 1 % slower)
@@ -124,6 +125,7 @@ __global__ void __launch_bounds__(BLOCK) k_policy_ingress(DpParams p, int ep, Ba
         else if (!live) { r.len = 0; for (int j = 0; j < 16; ++j) r.w[j] = 0; }
         else rec_load(r, b, i, 3);
         Acct a{0, 0};
+        a.ctu = ct_unit(p);
         bool skip_proxy = false;
         uint32_t identity = 0;
         if (live && (p.flags & F_FROM_HOST)) identity = identity_from_mark(b.mark ? b.mark[i] : 0u, skip_proxy);
@@ -256,6 +258,7 @@ __global__ void __launch_bounds__(BLOCK) CV_NS_OCC k_netdev_front(DpParams p, Ba
         Rec r;
         rec_load_wave(r, p, b, i0, i, live, st);
         Acct a{0, 0};
+        a.ctu = ct_unit(p);
         uint8_t xv = XDP_PASS;
         int32_t ret = TC_ACT_OK, reason = 0;
         uint32_t ident = 0;
@@ -404,6 +407,7 @@ __device__ __forceinline__ void stage2_one(const DpParams &p, const BatchDev &b,
     const uint32_t meta = s1.z;
     const EpDev ep = ep_netdev4<M::EV>(p, meta & 0xFFFFu);
     Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
+    a.ctu = ct_unit(p);
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
     int32_t reason = 0;
@@ -872,6 +876,7 @@ __global__ void __launch_bounds__(HOTB) k_hpar_look(DpParams p, BatchDev b, Grou
         const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;
         HotMember h;
         Acct a{0, 0, nullptr};
+        a.ctu = ct_unit(p);
         hot_lookup(p, b, g, ct, off, cnt, k, h, a);
         if (threadIdx.x < 3) fl[threadIdx.x] = cnt;
         __syncthreads();
@@ -942,6 +947,7 @@ __global__ void __launch_bounds__(HOTB) k_hpar_fin(DpParams p, BatchDev b, OutDe
         const HashTable ct = ep_netdev4<false>(p, g.srec[2 * x0 + 1].z & 0xFFFFu).ct4;
         HotMember h;
         Acct a{0, 0, m.pc};
+        a.ctu = ct_unit(p);
         const uint32_t k = k0 + threadIdx.x;
         hot_lookup(p, b, g, ct, off, cnt, k, h, a);
         const bool fin = h.live && k < cut;
@@ -1098,6 +1104,7 @@ __global__ void __launch_bounds__(HOTB) k_ct_hot(DpParams p, BatchDev b, OutDev 
             // 1. the lookups against the chunk's starting table, read only
             HotMember h;
             Acct a{0, 0, m.pc};
+            a.ctu = ct_unit(p);
             hot_lookup(p, b, g, ct, off, cnt, k0 + threadIdx.x, h, a);
             if (threadIdx.x == 0) { L.c = HOTB; L.lead = HOTB; }
             __syncthreads();
@@ -1211,6 +1218,7 @@ __device__ __forceinline__ void stage2_one6(const DpParams &p, const BatchDev &b
     const uint32_t meta = s1.z;
     const EpDev ep = G(p.eps)[meta & 0xFFFFu];
     Acct a{(s1.y >> 16) & 0xFFu, s1.y >> 24, m.pc};
+    a.ctu = ct_unit(p);
     uint8_t ct = CT_NONE;
     uint16_t proxy = 0;
     int32_t reason = 0;
@@ -1340,6 +1348,7 @@ __global__ void __launch_bounds__(BLOCK) k_ct_commit(DpParams p, BatchDev b, Out
     __shared__ uint32_t list[COMMIT_SPAN], lcount;
     pol_cache_init(pc);
     Acct a{0, 0, &pc};
+    a.ctu = ct_unit(p);
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t base = blockIdx.x * COMMIT_SPAN; base < b.n; base += gridDim.x * COMMIT_SPAN) {
         if (threadIdx.x == 0) lcount = 0;
@@ -2515,11 +2524,45 @@ __global__ void __launch_bounds__(BLOCK) k_gather_u64(unsigned long long *const 
 int grid_for(uint32_t n);
 
 // ------------------------------------------------------------------ room check (CtBound, cv_dp.hpp)
-__device__ __forceinline__ void bound_add(const CtBound &bd, const uint16_t *epmi, uint32_t e, uint32_t w)
+// per-workgroup sums of the per-map bounds (a popular endpoint's map would take one
+// global atomic per packet: Zipf endpoints serialised the check on one word)
+constexpr uint32_t BND_SLOTS = 1024, BND_EMPTY = 0xFFFFFFFFu;
+struct BoundLds {
+    uint32_t key[BND_SLOTS];
+    uint32_t cnt[BND_SLOTS];
+};
+
+__device__ __forceinline__ void bound_lds_init(BoundLds &l)
+{
+    for (uint32_t k = threadIdx.x; k < BND_SLOTS; k += blockDim.x) {
+        l.key[k] = BND_EMPTY;
+        l.cnt[k] = 0;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void bound_lds_flush(BoundLds &l, const CtBound &bd)
+{
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < BND_SLOTS; k += blockDim.x)
+        if (l.key[k] != BND_EMPTY && l.cnt[k]) atomicAdd(bd.bound + l.key[k], (unsigned long long)l.cnt[k]);
+}
+
+__device__ __forceinline__ void bound_add(const CtBound &bd, BoundLds *l, const uint16_t *epmi, uint32_t e, uint32_t w)
 {
     if (e >= bd.n_eps) return;
     const uint32_t m = epmi[e];
-    if (m < bd.nmaps) atomicAdd(bd.bound + m, (unsigned long long)w);
+    if (m >= bd.nmaps) return;
+    if (l) {
+        for (uint32_t h = (m * 0x9E3779B1u) >> 22, k = 0; k < 16; ++k, h = (h + 1) & (BND_SLOTS - 1)) {
+            const uint32_t old = atomicCAS(&l->key[h], BND_EMPTY, m);
+            if (old == BND_EMPTY || old == m) {
+                atomicAdd(&l->cnt[h], w);
+                return;
+            }
+        }
+    }
+    atomicAdd(bd.bound + m, (unsigned long long)w);
 }
 
 // the endpoint index (0-based) of a local endpoint address, or ~0 (host / none)
@@ -2538,10 +2581,13 @@ __device__ __forceinline__ uint32_t bound_ld32(const uint8_t *f) { return f[0] |
 // service masters that may serve it counted per LB slot
 __global__ void __launch_bounds__(BLOCK) k_bound_pkts(DpParams p, BatchDev b, const uint4 *records, CtBound bd)
 {
+    __shared__ BoundLds lds;
+    BoundLds *L = &lds;
+    bound_lds_init(lds);
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < b.n; i += gridDim.x * BLOCK) {
         if (bd.mode == 2) {                                       // a delivery record: its destination
             const uint32_t w = reinterpret_cast<const uint32_t *>(records + (size_t)i * DEL_SLOTS)[b.stride >= 128 ? 12 : 6];
-            bound_add(bd, b.stride >= 128 ? bd.epmi6 : bd.epmi4, w & 0xFFFFu, bd.w_dst);
+            bound_add(bd, L, b.stride >= 128 ? bd.epmi6 : bd.epmi4, w & 0xFFFFu, bd.w_dst);
             continue;
         }
         const uint8_t *f = b.frames + (size_t)i * b.stride;
@@ -2549,10 +2595,10 @@ __global__ void __launch_bounds__(BLOCK) k_bound_pkts(DpParams p, BatchDev b, co
         const bool v6 = eth == 0x86DDu;
         if ((eth != 0x0800u && !v6) || len < (v6 ? 54u : 34u)) continue;   // (no conntrack)
         const uint16_t *epmi = v6 ? bd.epmi6 : bd.epmi4;
-        if (bd.mode == 1) bound_add(bd, epmi, bd.src_ep ? bd.src_ep[i] : bd.ep0, bd.w_src);
+        if (bd.mode == 1) bound_add(bd, L, epmi, bd.src_ep ? bd.src_ep[i] : bd.ep0, bd.w_src);
         uint32_t da[4];
         for (int j = 0; j < (v6 ? 4 : 1); ++j) da[j] = bound_ld32(f + (v6 ? 38 : 30) + 4 * j);
-        bound_add(bd, epmi, bound_ep(p, da, v6), bd.w_dst);
+        bound_add(bd, L, epmi, bound_ep(p, da, v6), bd.w_dst);
         if (bd.mode != 1) continue;
         // the service masters (daddr, dport) and (daddr, 0) that may serve it (lb{4,6}_lookup_service)
         uint32_t nh, off;
@@ -2594,6 +2640,7 @@ __global__ void __launch_bounds__(BLOCK) k_bound_pkts(DpParams p, BatchDev b, co
             }
         }
     }
+    bound_lds_flush(lds, bd);
 }
 
 // every backend (slave entry) of a master that may serve packets: its endpoint's map
@@ -2619,7 +2666,7 @@ __global__ void __launch_bounds__(BLOCK) k_bound_svc(DpParams p, CtBound bd)
         if (ms < 0 || !cnt[ms]) continue;
         uint32_t be[4];
         for (int j = 0; j < (V6 ? 4 : 1); ++j) be[j] = bw[S::IVAL0 + sl * S::IVW + j];
-        bound_add(bd, V6 ? bd.epmi6 : bd.epmi4, bound_ep(p, be, V6), bd.w_dst * cnt[ms]);
+        bound_add(bd, nullptr, V6 ? bd.epmi6 : bd.epmi4, bound_ep(p, be, V6), bd.w_dst * cnt[ms]);
     }
 }
 

@@ -141,19 +141,32 @@ class EpNode:
             self._put(torch.from_numpy(pk[sel].astype(np.int64)).to(self.dev), out)
 
     def run(self, now: int):
-        """every operation of this rank; returns the rounds"""
+        """every operation of this rank; returns the rounds.  self.times: host seconds in
+        the scheduler, in the source launches up to their destinations' read (the round's
+        wait), in the exchange and record filing, and in issuing the delivery launches."""
+        import time
         import torch
         S = self.sched
+        clk = time.perf_counter
+        self.times = dict.fromkeys(("schedule", "sources", "exchange", "deliveries"), 0.0)
+        T = self.times
         while True:
             if not self.all_sum(S.pending()):
                 return self.rounds
             self.rounds += 1
             before = S.pending()
             # 1. the unblocked source programs
+            t0 = clk()
             pk = S.sources()
+            t1 = clk()
             recs, dst = self._sources(pk, now) if len(pk) else (None, np.zeros(0, np.int32))
+            t2 = clk()
+            T["schedule"] += t1 - t0
+            T["sources"] += t2 - t1
             # 2. every candidate's owner learns the record or "not for you"
             rp, re_, rh, rpos, rr = S.sources_done(pk, dst)
+            t3 = clk()
+            T["schedule"] += t3 - t2
             meta = np.stack([rp, re_, rh.astype(np.uint32)], 1).astype(np.int32) if len(rp) else \
                 np.zeros((0, 3), np.int32)
             rrec = recs.index_select(0, torch.from_numpy(rpos.astype(np.int64)).to(self.dev)) if len(rp) else \
@@ -161,16 +174,24 @@ class EpNode:
             if self.exchange is not None:
                 meta, rrec, from_rank = self.exchange(meta, rrec, rr)
                 self.cross += int(((from_rank != self.rank) & (meta[:, 2] != 0)).sum())
+            t4 = clk()
             ops = S.receive(meta[:, 0], meta[:, 1], meta[:, 2])
+            t5 = clk()
             has = np.nonzero(ops >= 0)[0]
             if len(has):
                 h = torch.from_numpy(has).to(self.dev)
                 self.store.index_copy_(0, torch.from_numpy(ops[has].astype(np.int64)).to(self.dev),
                                        rrec.index_select(0, h))
             # 3. the unblocked deliveries
+            t6 = clk()
             dops, dpk = S.deliveries(S.n * 2 + 16)
+            t7 = clk()
             if len(dops):
                 self._deliveries(dops, dpk, now)
+            t8 = clk()
+            T["exchange"] += (t4 - t3) + (t6 - t5)
+            T["schedule"] += (t5 - t4) + (t7 - t6)
+            T["deliveries"] += t8 - t7
             if not self.all_sum(before - S.pending()):
                 raise RuntimeError(f"rank {self.rank}: no operation could run in round {self.rounds}")
 

@@ -28,6 +28,8 @@ ROLES = {"v4_fix": 0, "v4_dyn": 1, "v6_fix": 2, "v6_dyn": 3, "lxc": 4, "ipcache"
          "lb4_services": 6, "lb6_services": 7, "lb4_revnat": 8, "lb6_revnat": 9}
 F_FROM_HOST, F_HAVE_L4_POLICY, F_DROP_ALL, F_CT_ACCOUNTING = 0x1, 0x2, 0x4, 0x8
 F_POLICY_INGRESS, F_POLICY_EGRESS, F_DEFAULT = 0x10, 0x20, 0x3B
+F_ACCT_SPLIT = 0x40              # nl / nu: conntrack lookups / writes count ACCT_CT_UNIT, the rest 1
+ACCT_CT_UNIT = 32
 
 _lib = None
 
@@ -250,6 +252,9 @@ class Ctx:
         self.device = device
         if flags != F_DEFAULT:
             _check(L.cv_set_flags(self.h, flags), "cv_set_flags")
+
+    def set_flags(self, flags):
+        _check(load().cv_set_flags(self.h, flags), "cv_set_flags")
 
     def close(self):
         if self.h:

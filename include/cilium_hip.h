@@ -71,6 +71,9 @@ typedef struct cv_ctx cv_ctx;
 #define CV_F_POLICY_INGRESS  0x10  /* POLICY_INGRESS                                */
 #define CV_F_POLICY_EGRESS   0x20  /* POLICY_EGRESS                                 */
 #define CV_F_DEFAULT         0x3b
+/* measurement: cv_out.nl / nu count every conntrack lookup / write 32 and every other
+ * map lookup / write 1 (the HBM-resident share of the algorithmic bytes) */
+#define CV_F_ACCT_SPLIT      0x40
 
 /* ---- per-packet codes (bpf/include/linux/bpf.h:623-628, bpf/include/bpf/api.h:18-25) */
 #define CV_XDP_DROP 1

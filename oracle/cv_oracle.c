@@ -711,15 +711,21 @@ static inline int ct_alive(const or_ct_entry *e)   /* conntrack.h:194-197 */
     return !(e->bits & B_RX_CLOSING) || !(e->bits & B_TX_CLOSING);
 }
 
+/* The accounting split (include/cilium_hip.h CV_F_ACCT_SPLIT): conntrack lookups and
+ * writes count OR_ACCT_CT_UNIT in nl / nu, every other map lookup / write 1, so one run
+ * gives the HBM-resident share of B(p).  Test infrastructure's knob, as the device's. */
+static uint8_t or_ctu = 1;
+void or_set_acct_split(int on) { or_ctu = on ? 32 : 1; }
+
 /* __ct_lookup (conntrack.h:199-263) */
 static int ct_lookup_one(or_map *map, const void *t, int action, int dir, or_ct_state *st,
                          int tcp, uint8_t seen, uint32_t skb_len, uint32_t now, uint32_t flags,
                          uint8_t *nl, uint8_t *nu, int *mon)
 {
-    (*nl)++;
+    *nl += or_ctu;
     or_ct_entry *e = or_map_lookup_ptr(map, t);
     if (!e) { *mon = 1; return OR_CT_NEW; }
-    (*nu)++;
+    *nu += or_ctu;
     if (ct_alive(e)) *mon = ct_update_timeout(e, tcp, dir, seen, now);
     if (st) {
         st->rev_nat_index = e->rev_nat_index;
@@ -1116,7 +1122,7 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
                                             &ps->nl, &ps->nu);
     if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
         if (ret == OR_CT_ESTABLISHED) {               /* ct_delete4 */
-            if (or_map_delete(ep->ct4, &t) == 0) ps->nu++;
+            if (or_map_delete(ep->ct4, &t) == 0) ps->nu += or_ctu;
         }
         ret = OR_DROP_POLICY;
         goto drop;
@@ -1126,7 +1132,7 @@ static int ipv4_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
         st_new.orig_dport = t.dport;
         st_new.src_sec_id = src_label;
         int r = or_ct_create4(ep->ct4, &t, len, OR_CT_INGRESS, &st_new, now);
-        ps->nu += 2;
+        ps->nu += 2 * or_ctu;
         if (IS_ERR(r)) { ret = r; goto drop; }
     }
     if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
@@ -1430,11 +1436,11 @@ static or_lb6_service *lb6_lookup_slave(or_map *m, or_lb6_key *key, uint16_t sla
 /* ct_update4_slave / ct_update6_slave (conntrack.h:572-586, 649-661) */
 static void ct_update_slave(or_map *map, const void *t, const or_ct_state *st, uint8_t *nl, uint8_t *nu)
 {
-    (*nl)++;
+    *nl += or_ctu;
     or_ct_entry *e = or_map_lookup_ptr(map, t);
     if (!e) return;
     e->slave = st->slave;
-    (*nu)++;
+    *nu += or_ctu;
 }
 
 /* extract_l4_port (lb.h:192-216): TCP/UDP dport; ICMP/ICMPv6 none; else DROP_UNKNOWN_L4 */
@@ -1464,7 +1470,7 @@ static int lb4_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb4_key 
     case OR_CT_NEW:
         st->slave = lb_select_slave(hash, svc->count);
         ret = or_ct_create4(ct, t, skb->len, OR_CT_SERVICE, st, now);
-        ps->nu += 2;
+        ps->nu += 2 * or_ctu;
         if (IS_ERR(ret)) { t->flags = flags; return OR_DROP_NO_SERVICE; }
         break;
     case OR_CT_ESTABLISHED: case OR_CT_RELATED: case OR_CT_REPLY:
@@ -1575,7 +1581,7 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     verdict = policy_can_egress(ep->policy, dp->flags, len, dst, t.dport, t.nexthdr, &ps->nl, &ps->nu);
     if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
         if (ret == OR_CT_ESTABLISHED) {                             /* ct_delete4 */
-            if (or_map_delete(ep->ct4, &t) == 0) ps->nu++;
+            if (or_map_delete(ep->ct4, &t) == 0) ps->nu += or_ctu;
         }
         return verdict;
     }
@@ -1584,7 +1590,7 @@ static int handle_ipv4_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
         st_new.src_sec_id = ep->seclabel;
         int nat = st_new.addr != 0;
         int r = or_ct_create4(ep->ct4, &t, len, OR_CT_EGRESS, &st_new, now);
-        ps->nu += nat ? 3 : 2;
+        ps->nu += (nat ? 3 : 2) * or_ctu;
         if (IS_ERR(r)) return r;
         break;
     }
@@ -1810,7 +1816,7 @@ static int lb6_local(or_dp *dp, or_map *ct, or_skb *skb, int l4_off, or_lb6_key 
     case OR_CT_NEW:
         st->slave = lb_select_slave(hash, svc->count);
         ret = ct_create6(ct, t, skb->len, OR_CT_SERVICE, st, now);
-        ps->nu += 2;
+        ps->nu += 2 * or_ctu;
         if (IS_ERR(ret)) { t->flags = flags; return OR_DROP_NO_SERVICE; }
         break;
     case OR_CT_ESTABLISHED: case OR_CT_RELATED: case OR_CT_REPLY:
@@ -1906,7 +1912,7 @@ static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
     verdict = policy_can_access_ingress(ep->policy, dp->flags, len, src_label, t.dport, t.nexthdr, &ps->nl, &ps->nu);
     if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
         if (ret == OR_CT_ESTABLISHED) {
-            if (or_map_delete(ep->ct6, &t) == 0) ps->nu++;
+            if (or_map_delete(ep->ct6, &t) == 0) ps->nu += or_ctu;
         }
         ret = OR_DROP_POLICY;
         goto drop;
@@ -1916,7 +1922,7 @@ static int ipv6_policy(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, uint32_t if
         st_new.orig_dport = t.dport;
         st_new.src_sec_id = src_label;
         int r = ct_create6(ep->ct6, &t, len, OR_CT_INGRESS, &st_new, now);
-        ps->nu += 2;
+        ps->nu += 2 * or_ctu;
         if (IS_ERR(r)) { ret = r; goto drop; }
     }
     if (verdict > 0 && (ret == OR_CT_NEW || ret == OR_CT_ESTABLISHED)) {
@@ -2047,7 +2053,7 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     verdict = policy_can_egress(ep->policy, dp->flags, len, dst, t.dport, t.nexthdr, &ps->nl, &ps->nu);
     if (ret != OR_CT_REPLY && ret != OR_CT_RELATED && verdict < 0) {
         if (ret == OR_CT_ESTABLISHED) {
-            if (or_map_delete(ep->ct6, &t) == 0) ps->nu++;
+            if (or_map_delete(ep->ct6, &t) == 0) ps->nu += or_ctu;
         }
         return verdict;
     }
@@ -2055,7 +2061,7 @@ static int handle_ipv6_from_lxc(or_dp *dp, or_endpoint_prog *ep, or_skb *skb, ui
     case OR_CT_NEW: {
         st_new.src_sec_id = ep->seclabel;
         int r = ct_create6(ep->ct6, &t, len, OR_CT_EGRESS, &st_new, now);
-        ps->nu += 2;
+        ps->nu += 2 * or_ctu;
         if (IS_ERR(r)) return r;
         break;
     }

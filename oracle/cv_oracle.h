@@ -129,6 +129,8 @@ uint32_t or_map_count(const or_map *m);
 /* all entries, sorted by key bytes; returns the count written (<= max) */
 uint32_t or_map_dump(const or_map *m, void *keys, void *vals, uint32_t max);
 void or_map_digest(const or_map *m, uint64_t out[3]);   /* test infrastructure */
+/* nl / nu: conntrack lookups and writes count 32 (CV_F_ACCT_SPLIT's split), or 1 */
+void or_set_acct_split(int on);
 /* the kernel checksum helper restatement (known-answer tests) */
 int or_csum_apply(uint8_t *frame, uint32_t len, uint32_t op, uint32_t off, uint32_t from, uint32_t to,
                   uint32_t flags, uint64_t *diff);

@@ -46,6 +46,8 @@ def lib():
         L.or_map_dump.argtypes = [vp, vp, vp, u32]
         L.or_map_digest.restype = None
         L.or_map_digest.argtypes = [vp, vp]
+        L.or_set_acct_split.restype = None
+        L.or_set_acct_split.argtypes = [i32]
         L.or_ct_gc.restype = u32
         L.or_ct_gc.argtypes = [vp, u32]
         L.or_get_prefix.restype = u32
@@ -347,3 +349,8 @@ def ref_probe():
     L.ref_layout.restype = C.c_long
     L.ref_layout.argtypes = [C.c_int]
     return L
+
+
+def set_acct_split(on):
+    """nl / nu count conntrack lookups / writes 32 each (include/cilium_hip.h CV_F_ACCT_SPLIT)"""
+    lib().or_set_acct_split(1 if on else 0)

@@ -346,3 +346,34 @@ def test_ct_capacity_egress_admission_fallback(dev, monkeypatch):
     w = synth.config5(1 << 12, n_svc=2000, n_ep=256, n_remote=512, ct_max=1500, seed=83)
     dp = check_egress(w, dev, batches=2, rounds=1)
     assert dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0       # DROP_CT_CREATE_FAILED happened
+
+
+def test_acct_split_counts(dev):
+    """CV_F_ACCT_SPLIT (bench.py's HBM-resident split): nl / nu count every conntrack lookup
+    / write ACCT_CT_UNIT and every other lookup / write 1, equal to the oracle's under the
+    same split -- config 5 (service, egress and delivery conntrack) and config 3 (netdev)."""
+    from cilium_amd import lib
+    from oracle import oracle as O
+    from tests.test_gpu_parity import run_ingress
+    try:
+        O.set_acct_split(True)
+        w = synth.config5(1 << 15, n_svc=1000, n_ep=128, n_remote=512, seed=95)
+        dp, om = H.oracle_dp(w)
+        ctx, pm = H.product_ctx(w, flags=lib.F_DEFAULT | lib.F_ACCT_SPLIT)
+        o = run_egress(ctx, w, dev, 0, w.n, w.now, events=False)
+        ref = dp.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+        for k in ("ret", "nl", "nu"):
+            assert (o[k] == getattr(ref, k)).all(), k
+        assert (o["nl"] >= lib.ACCT_CT_UNIT).sum() > w.n // 2 and (o["nl"] % lib.ACCT_CT_UNIT).sum() > 0
+        ctx.close()
+        w = synth.config3(1 << 15, 1 << 13, n_ep=64, n_cidrs=1024, n_ids=100, seed=96)
+        dp, om = H.oracle_dp(w)
+        ctx, pm = H.product_ctx(w, flags=lib.F_DEFAULT | lib.F_ACCT_SPLIT)
+        o = run_ingress(ctx, w, dev, 0, w.n, events=False)
+        ref = dp.netdev_ingress(w.frames, w.length, w.mark, now=w.now)
+        for k in ("ret", "nl", "nu"):
+            assert (o[k] == getattr(ref, k)).all(), k
+        assert (o["nl"] >= lib.ACCT_CT_UNIT).sum() > w.n // 4
+        ctx.close()
+    finally:
+        O.set_acct_split(False)

@@ -198,7 +198,12 @@ def test_config5_bench_regime(dev, say):
     dev_parts = [{k: bench.to_device(v, dev) for k, v in p.items()} for p in parts]
     base = [p["frames"] for p in dev_parts]
     say("device tables compiled")
+    from cilium_amd import lib
+    from oracle import oracle as O
     for v in (1, 2):
+        split = v == 2                                 # (step 2: nl / nu with the conntrack share split out)
+        ctx.set_flags(lib.F_DEFAULT | (lib.F_ACCT_SPLIT if split else 0))
+        O.set_acct_split(split)
         fv = bench.step_batch("config5", w, v, base, where, dev)
         got = []
         for k, p in enumerate(dev_parts):
@@ -227,5 +232,9 @@ def test_config5_bench_regime(dev, say):
             del ck, cv
         news = sum(int((g["ct"] == 0).sum()) for g in got)
         say(f"step {v}: outputs, metrics, policy counters, CT4 {fo.digest('ct4')[0]} / CT6 {fo.digest('ct6')[0]} "
-            f"entries bit-exact ({news} CT_NEW)")
+            f"entries bit-exact ({news} CT_NEW)" + (", nl / nu split (conntrack share) equal" if split else ""))
+        if split:
+            ctl = sum(int((g["nl"].astype(np.int64) // lib.ACCT_CT_UNIT).sum()) for g in got)
+            assert ctl > w.n                           # (every IP packet probes its conntrack map at least once)
+    O.set_acct_split(False)
     ctx.close()

@@ -2136,6 +2136,8 @@ int node_view(cv_ctx *c, NodeView &v)
             ns.v6 = (uint8_t)fam;
             memcpy(ns.vip, k, alen);
             memcpy(ns.backend, val, alen);
+            memcpy(&ns.vport, k + alen, 2);
+            memcpy(&ns.bport, val + alen, 2);
             v.svc.push_back(ns);
         });
     }

@@ -65,6 +65,16 @@ Addr addr6(const uint8_t *p)
 
 inline uint64_t ahash(const Addr &x) { return mix(mix(x.a ^ ((uint64_t)x.fam << 56)) + x.b) | 1u; }
 
+struct VipPort {
+    uint64_t vip;
+    uint16_t vport, bport;
+    bool operator<(const VipPort &o) const
+    {
+        return vip != o.vip ? vip < o.vip : vport != o.vport ? vport < o.vport : bport < o.bport;
+    }
+    bool operator==(const VipPort &o) const { return vip == o.vip && vport == o.vport && bport == o.bport; }
+};
+
 // key -> run of values, from (key, value) pairs: an open-addressing index over the
 // distinct keys and their values grouped (CSR)
 template <class V>
@@ -268,10 +278,13 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
     }
     for (auto &q : v.svc)
         vb.push_back({ahash(q.v6 ? addr6(q.vip) : addr4(q.vip)), ahash(q.v6 ? addr6(q.backend) : addr4(q.backend))});
-    std::vector<std::pair<uint64_t, uint64_t>> bv(vb.size());
-    for (size_t k = 0; k < vb.size(); ++k) bv[k] = {vb[k].second, vb[k].first};
+    // backend -> (VIP, the key's dport, the backend's port): the VIPs a reply may be
+    // reverse-NATed to (see `rev_vip`)
+    std::vector<std::pair<uint64_t, VipPort>> bv(vb.size());
+    for (size_t k = 0; k < vb.size(); ++k) bv[k] = {vb[k].second, VipPort{vb[k].first, v.svc[k].vport, v.svc[k].bport}};
     const Csr<uint32_t> where(std::move(ew));
-    const Csr<uint64_t> backends(std::move(vb)), vips(std::move(bv));
+    const Csr<uint64_t> backends(std::move(vb));
+    const Csr<VipPort> vips(std::move(bv));
     const uint64_t lob = ahash(Addr{0, v.loopback, 4});
     std::unique_ptr<cv_epnode> nd(new cv_epnode());
     nd->ctx = ctx;
@@ -283,7 +296,6 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
     nd->cand_off.assign(n + 1, 0);
     nd->dl_first.assign(n, ~0u);
     nd->dl_cnt.assign(n, 0);
-    nd->op_poff.push_back(0);
     // per packet: candidates, peers and operations, over packet ranges on host threads
     // (each range its own buffers, joined in packet order)
     struct Part {
@@ -292,6 +304,7 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
         std::vector<uint64_t> peer;
         uint64_t n_src = 0, n_dl = 0;
         int err = 0;
+        void swap_out(Part &o) { std::swap(cand, o.cand); std::swap(peer, o.peer); }   // (frees o's big arrays)
     };
     const uint32_t T = n < (1u << 14) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<Part> parts(T);
@@ -331,8 +344,25 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
                 sp.push_back(da);
                 sp.insert(sp.end(), backends.val.begin() + bes.first, backends.val.begin() + bes.second);
                 dp.push_back(sa);
+                // a TCP / UDP reply is reverse-NATed only by a connection whose translated
+                // dport is its sport (lb4_xlate / lb6_xlate: the backend's port, else the
+                // original dport -- the VIP's for an L4 service); ICMP (RELATED) or an
+                // unparsed header: any VIP the source backs
+                uint32_t sport = 0;
+                bool ports = false;
+                if (is4) {
+                    const uint32_t pr = f[23], off = 14 + 4 * (f[14] & 0xFu);
+                    ports = (pr == 6 || pr == 17) && off + 2 <= stride;
+                    if (ports) sport = f[off] | f[off + 1] << 8;
+                } else {
+                    ports = (f[20] == 6 || f[20] == 17) && 56 <= stride;
+                    if (ports) sport = f[54] | f[55] << 8;
+                }
                 const auto vi = vips.find(sa);
-                dp.insert(dp.end(), vips.val.begin() + vi.first, vips.val.begin() + vi.second);
+                for (uint32_t k = vi.first; k < vi.second; ++k) {
+                    const VipPort &x = vips.val[k];
+                    if (!ports || (x.bport ? x.bport == sport : (!x.vport || x.vport == sport))) dp.push_back(x.vip);
+                }
                 if (loop) {
                     sp.push_back(lob);
                     dp.push_back(lob);
@@ -368,43 +398,55 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
     }
     std::vector<uint64_t> peer64;                                 // (the operations' peers, as hashes)
     {
-        size_t nc = 0, no = 0, np = 0;
-        for (auto &P : parts) {
+        // the parts joined in packet order: offsets first, then every part copies itself
+        std::vector<size_t> co(T + 1, 0), oo(T + 1, 0), po(T + 1, 0);
+        std::vector<uint32_t> io(T + 1, 0);
+        for (uint32_t t = 0; t < T; ++t) {
+            const Part &P = parts[t];
             if (P.err) return P.err;
-            nc += P.cand.size();
-            no += P.op_pkt.size();
-            np += P.peer.size();
+            co[t + 1] = co[t] + P.cand.size();
+            oo[t + 1] = oo[t] + P.op_pkt.size();
+            po[t + 1] = po[t] + P.peer.size();
+            io[t + 1] = io[t] + (uint32_t)P.cand_n.size();
+            nd->n_src += P.n_src;
+            nd->n_dl += P.n_dl;
         }
-        nd->cand.reserve(nc);
-        nd->op_pkt.reserve(no);
-        nd->op_kind.reserve(no);
-        nd->op_map.reserve(no);
-        nd->op_poff.reserve(no + 1);
-        peer64.reserve(np);
-        uint32_t i = 0;
-        for (auto &P : parts) {
-            for (uint32_t k : P.cand_n) {
-                nd->cand_off[i + 1] = nd->cand_off[i] + k;
-                ++i;
+        if (po[T] >= 0xFFFFFFFFull || co[T] >= 0xFFFFFFFFull) return -E2BIG;
+        nd->cand.resize(co[T]);
+        nd->op_pkt.resize(oo[T]);
+        nd->op_kind.resize(oo[T]);
+        nd->op_map.resize(oo[T]);
+        nd->op_poff.resize(oo[T] + 1);
+        peer64.resize(po[T]);
+        auto join = [&](uint32_t t) {
+            Part &P = parts[t];
+            std::copy(P.cand.begin(), P.cand.end(), nd->cand.begin() + co[t]);
+            uint32_t c = (uint32_t)co[t];
+            for (size_t k = 0; k < P.cand_n.size(); ++k) {
+                nd->cand_off[io[t] + k] = c;
+                c += P.cand_n[k];
             }
-            nd->cand.insert(nd->cand.end(), P.cand.begin(), P.cand.end());
+            uint32_t q = (uint32_t)po[t];
             for (size_t k = 0; k < P.op_pkt.size(); ++k) {
-                const uint32_t o = (uint32_t)nd->op_pkt.size(), pk = P.op_pkt[k];
+                const uint32_t o = (uint32_t)(oo[t] + k), pk = P.op_pkt[k];
                 if (P.op_kind[k] == 1) {
                     if (nd->dl_first[pk] == ~0u) nd->dl_first[pk] = o;
                     nd->dl_cnt[pk]++;
                 }
-                nd->op_pkt.push_back(pk);
-                nd->op_kind.push_back(P.op_kind[k]);
-                nd->op_map.push_back(P.op_map[k]);
-                nd->op_poff.push_back(nd->op_poff.back() + P.op_np[k]);
+                nd->op_pkt[o] = pk;
+                nd->op_kind[o] = P.op_kind[k];
+                nd->op_map[o] = P.op_map[k];
+                nd->op_poff[o] = q;
+                q += P.op_np[k];
             }
-            peer64.insert(peer64.end(), P.peer.begin(), P.peer.end());
-            nd->n_src += P.n_src;
-            nd->n_dl += P.n_dl;
-            std::vector<uint32_t>().swap(P.cand);
-            std::vector<uint64_t>().swap(P.peer);
-        }
+            std::copy(P.peer.begin(), P.peer.end(), peer64.begin() + po[t]);
+            Part().swap_out(P);
+        };
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < T; ++t) th.emplace_back(join, t);
+        for (auto &x : th) x.join();
+        nd->cand_off[n] = (uint32_t)co[T];
+        nd->op_poff[oo[T]] = (uint32_t)po[T];
     }
     const uint32_t nops = (uint32_t)nd->op_pkt.size(), nm = ne * 2;
     nd->op_st.assign(nops, OP_PENDING);

@@ -22,6 +22,7 @@ struct NodeService {
     uint8_t v6;
     uint8_t vip[16];           // v4: first 4 bytes
     uint8_t backend[16];
+    uint16_t vport, bport;     // the key's dport and the backend's port (lb{4,6}_service.port), raw network order
 };
 
 struct NodeView {

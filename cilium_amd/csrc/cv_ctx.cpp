@@ -1580,7 +1580,10 @@ void refresh_live(cv_ctx *c, const std::vector<MapObj *> &maps)
 bool ct_bound_fits(cv_ctx *c, const DpParams &p, const BatchDev &b, const uint4 *records, uint32_t mode,
                    const uint16_t *src_ep, uint32_t ep0, const std::vector<MapObj *> &cts, hipStream_t s)
 {
-    if (cts.size() < 2 || map_table(c, cts)) return false;
+    if (cts.size() < 2) return false;
+    for (MapObj *m : cts)                      // (a full map: the launch is admitted anyway -- ct_fits
+        if (m->live_upper >= m->cap) return false;   //  just read the exact counts -- skip the check)
+    if (map_table(c, cts)) return false;
     const uint32_t nm = (uint32_t)cts.size();
     const uint64_t s4 = mode == 1 && p.lb4.buckets ? (p.lb4.mask + 1) * Lb4Spec::SPB : 0,
                    s6 = mode == 1 && p.lb6.buckets ? (p.lb6.mask + 1) * Lb6Spec::SPB : 0;

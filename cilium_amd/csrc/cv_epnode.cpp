@@ -185,18 +185,69 @@ struct cv_epnode {
     int room(bool first);
     // the operations of `kind` that can run now (deliveries: with their record), and
     // those they free in turn, in packet order
+    // finish() for one of many host threads: the counts it changes are shared
+    void finish_mt(uint32_t o, std::vector<uint32_t> *rel, uint64_t &done)
+    {
+        op_st[o] = OP_DONE;
+        __atomic_fetch_sub(&map_need[op_map[o]], MAX_CREATES[op_kind[o]], __ATOMIC_RELAXED);
+        ++done;
+        auto rel1 = [&](uint32_t x) {
+            if (__atomic_sub_fetch(&op_wait[x], 1u, __ATOMIC_ACQ_REL) == 0) rel[op_kind[x]].push_back(x);
+        };
+        for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q)
+            if (ref_next[q] != NONE) rel1(ref_op[ref_next[q]]);
+        if (map_chain[op_map[o]]) {
+            const uint32_t x = chain_next(o);
+            if (x != NONE) rel1(x);
+        }
+    }
+    // the operations of `kind` that can run now (deliveries: with their record), and
+    // those they free in turn, in packet order.  Level by level: a large level is
+    // finished on host threads (atomic wait counts), a small one in place.
     void run_ready(int kind, std::vector<uint32_t> &out)
     {
-        std::vector<uint32_t> keep, &z = zero[kind];
-        for (size_t k = 0; k < z.size(); ++k) {            // (z grows while successors free up)
-            const uint32_t o = z[k];
-            if (op_st[o] == OP_DONE) continue;
-            if (op_st[o] == OP_PENDING) {
-                keep.push_back(o);                             // (a delivery whose record has not arrived)
+        std::vector<uint32_t> keep, cur, &z = zero[kind];
+        auto sift = [&](std::vector<uint32_t> &from) {       // runnable ones to cur, the rest kept
+            for (uint32_t o : from) {
+                if (op_st[o] == OP_DONE) continue;
+                if (op_st[o] == OP_PENDING) keep.push_back(o);  // (a delivery whose record has not arrived)
+                else cur.push_back(o);
+            }
+            from.clear();
+        };
+        sift(z);
+        const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        while (!cur.empty()) {
+            std::vector<uint32_t> lvl;
+            lvl.swap(cur);
+            if (lvl.size() < 8192 || T == 1) {
+                for (uint32_t o : lvl) {
+                    if (op_st[o] == OP_RESOLVED) out.push_back(o);   // (OP_NOOP: not delivered here, nothing to run)
+                    finish(o);
+                }
+                sift(z);
                 continue;
             }
-            if (op_st[o] == OP_RESOLVED) out.push_back(o);     // (OP_NOOP: not delivered here, nothing to run)
-            finish(o);
+            std::vector<std::vector<uint32_t>> rel(2 * T), outs(T);
+            std::vector<uint64_t> done(T, 0);
+            std::vector<std::thread> th;
+            for (uint32_t t = 0; t < T; ++t)
+                th.emplace_back([&, t] {
+                    const size_t a = lvl.size() * t / T, b = lvl.size() * (t + 1) / T;
+                    for (size_t k = a; k < b; ++k) {
+                        const uint32_t o = lvl[k];
+                        if (op_st[o] == OP_RESOLVED) outs[t].push_back(o);
+                        finish_mt(o, &rel[2 * t], done[t]);
+                    }
+                });
+            for (auto &x : th) x.join();
+            for (uint32_t t = 0; t < T; ++t) {
+                out.insert(out.end(), outs[t].begin(), outs[t].end());
+                pending -= done[t];
+                zero[1 - kind].insert(zero[1 - kind].end(), rel[2 * t + 1 - kind].begin(), rel[2 * t + 1 - kind].end());
+                z.insert(z.end(), rel[2 * t + kind].begin(), rel[2 * t + kind].end());
+            }
+            sift(z);
         }
         z.swap(keep);
         // in operation order, which is packet order (a flag pass when the round is large)

@@ -584,21 +584,28 @@ class EpSched:
         k = _check(self.L.cv_epnode_sources(self.h, self._pk.ctypes.data, self.n), "cv_epnode_sources")
         return self._pk[:k].copy()
 
+    def _rows(self, cap):
+        """the exchange-row buffers, reused across rounds (grown when a round needs more)"""
+        if getattr(self, "_rb", None) is None or len(self._rb[0]) < cap:
+            self._rb = (np.empty(cap, np.uint32), np.empty(cap, np.uint32), np.empty(cap, np.uint8),
+                        np.empty(cap, np.uint32))
+        return self._rb
+
     def sources_done(self, pkts, dst):
         """the exchange rows of the launched packets: (row_pkt, row_ep, row_has, row_pos,
-        rank_rows), sorted by owner rank"""
+        rank_rows), sorted by owner rank (views of buffers the next round reuses)"""
         pkts = np.ascontiguousarray(pkts, np.uint32)
         dst = np.ascontiguousarray(dst, np.int32)
-        cap = 2 * len(pkts) + 64
+        cap = max(2 * self.n + 64, len(self._rb[0]) if getattr(self, "_rb", None) is not None else 0)
         while True:
-            rp, re_, rpos = (np.zeros(cap, np.uint32) for _ in range(3))
-            rh = np.zeros(cap, np.uint8)
+            rp, re_, rh, rpos = self._rows(cap)
             rr = np.zeros(self.world, np.uint32)
             k = self.L.cv_epnode_sources_done(self.h, pkts.ctypes.data, dst.ctypes.data, len(pkts), rp.ctypes.data,
-                                              re_.ctypes.data, rh.ctypes.data, rpos.ctypes.data, rr.ctypes.data, cap)
+                                              re_.ctypes.data, rh.ctypes.data, rpos.ctypes.data, rr.ctypes.data,
+                                              len(rp))
             if k != -28:                                   # (-ENOSPC: more candidates than rows; nothing written)
                 break
-            cap *= 4
+            cap = 4 * len(rp)
         _check(k, "cv_epnode_sources_done")
         return rp[:k], re_[:k], rh[:k], rpos[:k], rr
 
@@ -606,16 +613,17 @@ class EpSched:
         row_pkt = np.ascontiguousarray(row_pkt, np.uint32)
         row_ep = np.ascontiguousarray(row_ep, np.uint32)
         row_has = np.ascontiguousarray(row_has, np.uint8)
-        op = np.zeros(max(len(row_pkt), 1), np.int32)
+        op = np.empty(max(len(row_pkt), 1), np.int32)
         _check(self.L.cv_epnode_receive(self.h, row_pkt.ctypes.data, row_ep.ctypes.data, row_has.ctypes.data,
                                         len(row_pkt), op.ctypes.data), "cv_epnode_receive")
         return op[:len(row_pkt)]
 
     def deliveries(self, cap):
-        ops = np.zeros(max(cap, 1), np.uint32)
-        pk = np.zeros(max(cap, 1), np.uint32)
+        if getattr(self, "_db", None) is None or len(self._db[0]) < cap:
+            self._db = (np.empty(max(cap, 1), np.uint32), np.empty(max(cap, 1), np.uint32))
+        ops, pk = self._db
         k = _check(self.L.cv_epnode_deliveries(self.h, ops.ctypes.data, pk.ctypes.data, cap), "cv_epnode_deliveries")
-        return ops[:k], pk[:k]
+        return ops[:k].copy(), pk[:k].copy()
 
     def close(self):
         if self.h:

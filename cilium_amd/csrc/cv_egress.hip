@@ -1519,9 +1519,34 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_deliver(DpParams p, 
 }
 
 
+// the continuation list's instance may take a budget of its own (its lanes walk several
+// members of a group and deliver inline: more live state per lane)
+#ifndef CV_EG_CONT_WAVES
+#define CV_EG_CONT_WAVES CV_EG_WAVES
+#endif
+#define CV_EG_CONT_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_CONT_WAVES, 8)))
+
+template <bool V6, bool EV, bool INL, bool SN>
+__device__ __forceinline__ void egress_ct_body(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                               const GroupScratch &g, uint32_t pos);
+
 template <bool V6, bool EV, bool INL, bool SN = false>
 __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_ct(DpParams p, BatchDev b, uint32_t now, OutDev o, GroupScratch g,
                                                                 uint32_t pos)
+{
+    egress_ct_body<V6, EV, INL, SN>(p, b, now, o, g, pos);
+}
+
+template <bool V6, bool EV, bool SN = false>
+__global__ void __launch_bounds__(BLOCK) CV_EG_CONT_OCC k_egress_cont(DpParams p, BatchDev b, uint32_t now, OutDev o,
+                                                                       GroupScratch g, uint32_t pos)
+{
+    egress_ct_body<V6, EV, true, SN>(p, b, now, o, g, pos);
+}
+
+template <bool V6, bool EV, bool INL, bool SN>
+__device__ __forceinline__ void egress_ct_body(const DpParams &p, const BatchDev &b, uint32_t now, const OutDev &o,
+                                               const GroupScratch &g, uint32_t pos)
 {
     __shared__ LdsMetrics lm;
     __shared__ LdsPolicy pc;
@@ -1728,8 +1753,8 @@ void eg_stages(const DpParams &p, const BatchDev &b, const uint32_t *flow_hash, 
         for (int v6 = 0; v6 < (b.stride >= 128 ? 2 : 1); ++v6) {
             const GroupScratch &gv = v6 ? g6 : gp;
             if (last) {
-                if (v6) hipLaunchKernelGGL((k_egress_ct<true, EV, true, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
-                else hipLaunchKernelGGL((k_egress_ct<false, EV, true, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
+                if (v6) hipLaunchKernelGGL((k_egress_cont<true, EV, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
+                else hipLaunchKernelGGL((k_egress_cont<false, EV, SN>), gk, blk, 0, s, p, b, now, o, gv, k);
                 continue;
             }
             if (v6) {

@@ -2594,6 +2594,7 @@ __global__ void __launch_bounds__(BLOCK) k_bound_pkts(DpParams p, BatchDev b, co
         const uint32_t len = min(b.len[i], b.stride), eth = f[12] << 8 | f[13];
         const bool v6 = eth == 0x86DDu;
         if ((eth != 0x0800u && !v6) || len < (v6 ? 54u : 34u)) continue;   // (no conntrack)
+        if (v6 && b.stride < 128) continue;                       // (E_TRUNC: IPv6 needs 128-B records)
         const uint16_t *epmi = v6 ? bd.epmi6 : bd.epmi4;
         if (bd.mode == 1) bound_add(bd, L, epmi, bd.src_ep ? bd.src_ep[i] : bd.ep0, bd.w_src);
         uint32_t da[4];
@@ -2608,14 +2609,22 @@ __global__ void __launch_bounds__(BLOCK) k_bound_pkts(DpParams p, BatchDev b, co
         } else {
             nh = f[20];
             off = 54;
-            if (nh != 6 && nh != 17 && nh != 58) {                // (an extension header, or no service: the
-                if (nh == 0 || nh == 43 || nh == 60 || nh == 51 || nh == 44 || nh == 50)   //  datapath's own
-                    atomicAdd(bd.flag + 1, 1u);                   //  ipv6_hdrlen walk decides: unseen)
-                continue;
-            }
         }
         uint32_t dport = 0;
-        if (nh == 6 || nh == 17) {
+        if (v6 && nh != 6 && nh != 17 && nh != 58) {              // extension headers: the datapath's own
+            Rec6 r;                                               // walk (ipv6_hdrlen, as the front runs it)
+            rec_load(r, b, i, 8);
+            const int hl = ipv6_hdrlen(r, nh);
+            if (hl < 0) continue;                                 // (dropped before any conntrack)
+            off = 14 + hl;
+            if (nh == 6 || nh == 17) {
+                const L4Hdr h = l4_read<54>(r, (int)off);
+                if (h.c2b) continue;                              // (dropped: E_FAULT / E_TRUNC)
+                dport = h.p2;
+            } else if (nh != 58 && nh != 1) {
+                continue;                                         // (skip_service_lookup)
+            }
+        } else if (nh == 6 || nh == 17) {
             if (off + 4 > len) {                                  // (a port the check cannot read)
                 atomicAdd(bd.flag + 1, 1u);
                 continue;

@@ -1519,10 +1519,12 @@ __global__ void __launch_bounds__(BLOCK) CV_EG_OCC k_egress_deliver(DpParams p, 
 }
 
 
-// the continuation list's instance may take a budget of its own (its lanes walk several
-// members of a group and deliver inline: more live state per lane)
+// the continuation list's instance takes a budget of its own (its lanes walk several
+// members of a group and deliver inline: more live state per lane; at 4 waves / SIMD it
+// spilled 48-64 B per lane).  A/B on one box, two runs each (`profiles/r06g`): 4 waves
+// 3.51 ms per step, 3 waves 3.36, 2 waves 3.38 -- config 5 1 273 -> 1 291 Mpps
 #ifndef CV_EG_CONT_WAVES
-#define CV_EG_CONT_WAVES CV_EG_WAVES
+#define CV_EG_CONT_WAVES 3
 #endif
 #define CV_EG_CONT_OCC __attribute__((amdgpu_waves_per_eu(CV_EG_CONT_WAVES, 8)))
 

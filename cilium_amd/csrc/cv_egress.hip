@@ -31,6 +31,18 @@ __device__ __forceinline__ void eg_changed() { l1_inv(); }
 
 int grid_for(uint32_t n);
 
+// occupancy knobs of the egress stages (measurements: 0 leaves the choice to the compiler)
+#ifndef CV_LB_WAVES
+#define CV_LB_WAVES 0
+#endif
+#ifndef CV_PAIRS_WAVES
+#define CV_PAIRS_WAVES 0
+#endif
+#ifndef CV_EFRONT_WAVES
+#define CV_EFRONT_WAVES 0
+#endif
+#define CV_WAVES_ATTR(w) __attribute__((amdgpu_waves_per_eu((w) ? (w) : 1, (w) ? 8 : 10)))
+
 
 // egress scratch words (GroupScratch::eg, EG_WORDS per packet)
 enum : uint32_t {
@@ -361,7 +373,7 @@ __device__ __forceinline__ uint32_t front_one(const DpParams &p, const EpDev &ep
 }
 
 template <int NW, bool EV>
-__global__ void __launch_bounds__(BLOCK) k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
+__global__ void __launch_bounds__(BLOCK) CV_WAVES_ATTR(CV_EFRONT_WAVES) k_egress_front(DpParams p, BatchDev b, const uint16_t *src_ep, uint32_t ep0,
                                                         OutDev o, GroupScratch g)
 {
     __shared__ LdsMetrics lm;
@@ -664,7 +676,7 @@ fin:
 // the service groups by member position, as the conntrack stage (position lists of the
 // binned grouping; one launch per position)
 template <bool V6, bool EV, bool SN = false>
-__global__ void __launch_bounds__(BLOCK) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
+__global__ void __launch_bounds__(BLOCK) CV_WAVES_ATTR(CV_LB_WAVES) k_lb_stage(DpParams p, BatchDev b, const uint32_t *hash, uint32_t now,
                                                     OutDev o, GroupScratch g, uint32_t pos)
 {
     __shared__ LdsMetrics lm;
@@ -938,7 +950,7 @@ __device__ __forceinline__ void pairs_one(const DpParams &p, const BatchDev &b, 
 // The records come in through LDS (a wave's 64 consecutive records in coalesced 1-KiB
 // loads) and the packed input states leave the same way, one 64-B line per packet.
 template <int NW>
-__global__ void __launch_bounds__(BLOCK) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
+__global__ void __launch_bounds__(BLOCK) CV_WAVES_ATTR(CV_PAIRS_WAVES) k_egress_pairs(DpParams p, BatchDev b, GroupScratch g)
 {
     __shared__ uint4 stage[BLOCK / 64][16 * NW];
     uint4 *st = stage[threadIdx.x >> 6];

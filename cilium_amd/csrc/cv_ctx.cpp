@@ -15,6 +15,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <set>
 #include <string>
@@ -244,6 +245,7 @@ struct cv_ctx {
     std::vector<Endpoint> eps;
     bool eps_dirty = true;
     uint64_t eps_gen = 0;      // bumped by every endpoint change (map_table's cache key)
+    uint64_t uid = 0;          // unique per cv_open in the process (caches keyed by context)
     DevBuf eps_dev, ephot_dev, ephot6_dev, ep_of_lxc;
     bool uni4_on = false;      // every endpoint on one policy + CT4 map, LXC_IPV4 set (DpParams::uni4)
     bool uni6_on = false;      // every endpoint on one policy + CT6 map (DpParams::uni6)
@@ -2148,6 +2150,23 @@ int node_view(cv_ctx *c, NodeView &v)
     return 0;
 }
 
+int node_key(cv_ctx *c, NodeKey &k)
+{
+    if (!c) return -EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    k = NodeKey{};
+    k.uid = c->uid;
+    k.eps = c->eps_gen;
+    for (int fam = 0; fam < 2; ++fam) {
+        const int h = c->role[fam ? CV_ROLE_LB6_SERVICES : CV_ROLE_LB4_SERVICES];
+        MapObj *m = get(c, h);
+        k.lb[2 * fam] = (uint64_t)(int64_t)h;
+        k.lb[2 * fam + 1] = m ? m->hm->version : 0;
+    }
+    k.loopback = c->node.ipv4_loopback;
+    return 0;
+}
+
 int ct_counts(cv_ctx *c, const std::vector<int> &handles, std::vector<uint64_t> &live, std::vector<uint64_t> &cap)
 {
     if (!c) return -EINVAL;
@@ -2190,7 +2209,9 @@ const char *cv_version(void) { return "cilium_hip 0.1.0 gfx950"; }
 int cv_open(int hip_device, cv_ctx **out)
 {
     if (!out) return -EINVAL;
+    static std::atomic<uint64_t> uids{0};
     cv_ctx *c = new cv_ctx();
+    c->uid = ++uids;
     c->device = hip_device;
     c->hk.read();
     for (int r = 0; r < CV_NUM_ROLES; ++r) { c->role[r] = -1; c->role_version[r] = 0; }

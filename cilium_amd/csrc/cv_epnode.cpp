@@ -18,7 +18,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <stdio.h>
+#include <stdlib.h>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -114,6 +118,75 @@ struct Csr {
     }
 };
 
+// the node's indexes: address -> endpoints, VIP -> backends, backend -> (VIP, ports), by
+// 64-bit address hash (a collision adds candidates or peers, supersets stay exact); built
+// once per node view and reused by every batch while the view's key holds
+struct NodeIdx {
+    cv::NodeKey key;
+    cv::NodeView v;
+    Csr<uint32_t> where;
+    Csr<uint64_t> backends;
+    Csr<VipPort> vips;
+    uint64_t lob = 0;
+    NodeIdx(const cv::NodeKey &k, cv::NodeView &&view, std::vector<std::pair<uint64_t, uint32_t>> ew,
+            std::vector<std::pair<uint64_t, uint64_t>> vb, std::vector<std::pair<uint64_t, VipPort>> bv)
+        : key(k), v(std::move(view)), where(std::move(ew)), backends(std::move(vb)), vips(std::move(bv)),
+          lob(ahash(Addr{0, v.loopback, 4}))
+    {
+    }
+};
+
+std::shared_ptr<const NodeIdx> build_index(cv_ctx *ctx, const cv::NodeKey &key, int &err)
+{
+    cv::NodeView v;
+    if ((err = cv::node_view(ctx, v))) return nullptr;
+    const uint32_t ne = (uint32_t)v.eps.size();
+    if (ne > 0xFFFF) { err = -E2BIG; return nullptr; }
+    {                                                      // every endpoint's CT maps its own
+        std::vector<int> hs;
+        for (auto &e : v.eps)
+            for (int h : {e.ct4, e.ct6})
+                if (h >= 0) hs.push_back(h);
+        std::sort(hs.begin(), hs.end());
+        if (std::adjacent_find(hs.begin(), hs.end()) != hs.end()) { err = -EINVAL; return nullptr; }
+    }
+    std::vector<std::pair<uint64_t, uint32_t>> ew;                // (address, endpoint)
+    std::vector<std::pair<uint64_t, uint64_t>> vb;                // (VIP, backend)
+    for (uint32_t e = 0; e < ne; ++e) {
+        static const uint8_t zero[16] = {};
+        if (v.eps[e].ipv4) ew.push_back({ahash(Addr{0, v.eps[e].ipv4, 4}), e});
+        if (memcmp(v.eps[e].ipv6, zero, 16)) ew.push_back({ahash(addr6(v.eps[e].ipv6)), e});
+    }
+    for (auto &q : v.svc)
+        vb.push_back({ahash(q.v6 ? addr6(q.vip) : addr4(q.vip)), ahash(q.v6 ? addr6(q.backend) : addr4(q.backend))});
+    // backend -> (VIP, the key's dport, the backend's port): the VIPs a reply may be
+    // reverse-NATed to (see the delivery's peers)
+    std::vector<std::pair<uint64_t, VipPort>> bv(vb.size());
+    for (size_t k = 0; k < vb.size(); ++k) bv[k] = {vb[k].second, VipPort{vb[k].first, v.svc[k].vport, v.svc[k].bport}};
+    return std::make_shared<const NodeIdx>(key, std::move(v), std::move(ew), std::move(vb), std::move(bv));
+}
+
+// the most recent node's indexes (one context's node per process at a time; another
+// context or a changed view rebuilds them)
+std::mutex idx_mu;
+std::shared_ptr<const NodeIdx> idx_last;
+
+std::shared_ptr<const NodeIdx> node_index(cv_ctx *ctx, int &err)
+{
+    cv::NodeKey key;
+    if ((err = cv::node_key(ctx, key))) return nullptr;
+    {
+        std::lock_guard<std::mutex> g(idx_mu);
+        if (idx_last && idx_last->key == key) return idx_last;
+    }
+    std::shared_ptr<const NodeIdx> ix = build_index(ctx, key, err);
+    if (ix) {
+        std::lock_guard<std::mutex> g(idx_mu);
+        idx_last = ix;
+    }
+    return ix;
+}
+
 }  // namespace
 
 struct cv_epnode {
@@ -165,8 +238,10 @@ struct cv_epnode {
         }
     }
     // a delivery that runs nowhere here leaves its keys' lists: each successor waits for
-    // the predecessor instead, or for nothing more when the predecessor has finished
-    void splice(uint32_t o)
+    // the predecessor instead, or for nothing more when the predecessor has finished.
+    // Everything it touches is in its own map (rel: what becomes free)
+    template <class R>
+    void splice_core(uint32_t o, R &&rel)
     {
         for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q) {
             const uint32_t pq = ref_prev[q], nq = ref_next[q];
@@ -174,13 +249,39 @@ struct cv_epnode {
             if (pq != NONE) ref_next[pq] = waits ? nq : NONE;
             if (nq != NONE) {
                 ref_prev[nq] = waits ? pq : NONE;
-                if (!waits) release(ref_op[nq]);
+                if (!waits) rel(ref_op[nq]);
             }
             ref_prev[q] = ref_next[q] = NONE;
         }
         op_st[o] = OP_DONE;
         map_need[op_map[o]] -= MAX_CREATES[op_kind[o]];
+    }
+    void splice(uint32_t o)
+    {
+        splice_core(o, [&](uint32_t x) { release(x); });
         --pending;
+    }
+    // one row of cv_epnode_receive (rel / done: as splice_core, the pending count's share)
+    template <class R>
+    int receive_row(uint32_t i, uint32_t ep, uint8_t has, int32_t &op, R &&rel, uint64_t &done)
+    {
+        if (i >= n || dl_first[i] == NONE) return -EPROTO;
+        uint32_t o = dl_first[i], k = 0;
+        while (k < dl_cnt[i] && op_map[o] >> 1 != ep) ++k, ++o;
+        if (k == dl_cnt[i] || op_st[o] != OP_PENDING) return -EPROTO;
+        // a record: the delivery runs once nothing earlier on its keys waits; none: nothing
+        // runs here -- it leaves its keys' lists now (its successors wait for its pending
+        // predecessors instead), or, on a chained map, runs as a no-op in its turn
+        op = has ? (int32_t)o : -1;
+        if (has) {
+            op_st[o] = OP_RESOLVED;
+        } else if (map_chain[op_map[o]]) {
+            op_st[o] = OP_NOOP;
+        } else {
+            splice_core(o, rel);
+            ++done;
+        }
+        return 0;
     }
     int room(bool first);
     // the operations of `kind` that can run now (deliveries: with their record), and
@@ -305,38 +406,24 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
                    const uint16_t *src_ep, cv_epnode **out)
 {
     if (!ctx || !out || !world || rank >= world || (n && (!frames || !src_ep)) || stride < 54) return -EINVAL;
-    cv::NodeView v;
-    int r = cv::node_view(ctx, v);
-    if (r) return r;
+    const bool tm = getenv("CV_EPNODE_TIMES") != nullptr;
+    auto t_0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!tm) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[epnode open] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_0).count());
+        t_0 = t;
+    };
+    int r = 0;
+    const std::shared_ptr<const NodeIdx> ix = node_index(ctx, r);
+    if (!ix) return r;
+    const cv::NodeView &v = ix->v;
     const uint32_t ne = (uint32_t)v.eps.size();
-    if (ne > 0xFFFF) return -E2BIG;
-    {                                                      // every endpoint's CT maps its own
-        std::vector<int> hs;
-        for (auto &e : v.eps)
-            for (int h : {e.ct4, e.ct6})
-                if (h >= 0) hs.push_back(h);
-        std::sort(hs.begin(), hs.end());
-        if (std::adjacent_find(hs.begin(), hs.end()) != hs.end()) return -EINVAL;
-    }
-    // address -> endpoints; VIP -> backends; backend -> VIPs (by 64-bit address hash: a
-    // collision adds candidates or peers, supersets stay exact)
-    std::vector<std::pair<uint64_t, uint32_t>> ew;                // (address, endpoint)
-    std::vector<std::pair<uint64_t, uint64_t>> vb;                // (VIP, backend)
-    for (uint32_t e = 0; e < ne; ++e) {
-        static const uint8_t zero[16] = {};
-        if (v.eps[e].ipv4) ew.push_back({ahash(Addr{0, v.eps[e].ipv4, 4}), e});
-        if (memcmp(v.eps[e].ipv6, zero, 16)) ew.push_back({ahash(addr6(v.eps[e].ipv6)), e});
-    }
-    for (auto &q : v.svc)
-        vb.push_back({ahash(q.v6 ? addr6(q.vip) : addr4(q.vip)), ahash(q.v6 ? addr6(q.backend) : addr4(q.backend))});
-    // backend -> (VIP, the key's dport, the backend's port): the VIPs a reply may be
-    // reverse-NATed to (see `rev_vip`)
-    std::vector<std::pair<uint64_t, VipPort>> bv(vb.size());
-    for (size_t k = 0; k < vb.size(); ++k) bv[k] = {vb[k].second, VipPort{vb[k].first, v.svc[k].vport, v.svc[k].bport}};
-    const Csr<uint32_t> where(std::move(ew));
-    const Csr<uint64_t> backends(std::move(vb));
-    const Csr<VipPort> vips(std::move(bv));
-    const uint64_t lob = ahash(Addr{0, v.loopback, 4});
+    const Csr<uint32_t> &where = ix->where;
+    const Csr<uint64_t> &backends = ix->backends;
+    const Csr<VipPort> &vips = ix->vips;
+    const uint64_t lob = ix->lob;
+    lap("node view and indexes");
     std::unique_ptr<cv_epnode> nd(new cv_epnode());
     nd->ctx = ctx;
     nd->rank = rank;
@@ -447,6 +534,7 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
             th.emplace_back(build, t, (uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T));
         for (auto &x : th) x.join();
     }
+    lap("per-packet build");
     std::vector<uint64_t> peer64;                                 // (the operations' peers, as hashes)
     {
         // the parts joined in packet order: offsets first, then every part copies itself
@@ -499,6 +587,7 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
         nd->cand_off[n] = (uint32_t)co[T];
         nd->op_poff[oo[T]] = (uint32_t)po[T];
     }
+    lap("join");
     const uint32_t nops = (uint32_t)nd->op_pkt.size(), nm = ne * 2;
     nd->op_st.assign(nops, OP_PENDING);
     for (uint32_t o = 0; o < nops; ++o)
@@ -518,6 +607,7 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
     for (uint32_t k = 0; k < nops; ++k) nd->op_mpos[nd->map_ops[k]] = k;
     // the key links: per map, its (peer, operation) references sorted, consecutive ones on
     // one peer linked (an operation naming a peer twice links once)
+    lap("map order");
     nd->ref_next.assign(peer64.size(), cv_epnode::NONE);
     nd->ref_prev.assign(peer64.size(), cv_epnode::NONE);
     nd->op_wait.assign(nops, 0);
@@ -528,23 +618,50 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
             for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) ref_op[q] = o;
         // maps are independent: their links are built on host threads, each with its
         // maps' share of the wait counts (an operation is in one map)
+        // per map one pass over its references in operation order (= packet order) with a
+        // small open-addressing table peer -> the last reference on it: each reference
+        // links to that one (the same links as sorting the (peer, reference) pairs)
         auto link = [&](uint32_t m0, uint32_t m1) {
-            std::vector<std::pair<uint64_t, uint32_t>> u;         // (peer, reference)
+            std::vector<uint64_t> tk;                             // (peer, or 0: empty)
+            std::vector<uint32_t> tv;                             // (its last reference)
+            std::vector<uint32_t> used;
             for (uint32_t m = m0; m < m1; ++m) {
-                u.clear();
+                size_t refs = 0;
                 for (uint32_t k = nd->map_off[m]; k < nd->map_off[m + 1]; ++k) {
                     const uint32_t o = nd->map_ops[k];
-                    for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) u.push_back({peer64[q], q});
+                    refs += nd->op_poff[o + 1] - nd->op_poff[o];
                 }
-                std::sort(u.begin(), u.end());                // (references ascend with their operations)
-                for (size_t k = 1; k < u.size(); ++k) {
-                    if (u[k - 1].first != u[k].first) continue;
-                    const uint32_t a = ref_op[u[k - 1].second], b = ref_op[u[k].second];
-                    if (a == b) continue;                      // (a peer named twice by one operation)
-                    nd->ref_next[u[k - 1].second] = u[k].second;   // (b waits for a on this peer)
-                    nd->ref_prev[u[k].second] = u[k - 1].second;
-                    nd->op_wait[b]++;
+                if (!refs) continue;
+                size_t cap = 64;
+                while (cap < 2 * refs) cap <<= 1;
+                if (tk.size() < cap) {
+                    tk.assign(cap, 0);
+                    tv.assign(cap, 0);
+                    used.clear();
                 }
+                const uint64_t mask = cap - 1;
+                for (uint32_t k = nd->map_off[m]; k < nd->map_off[m + 1]; ++k) {
+                    const uint32_t o = nd->map_ops[k];
+                    for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) {
+                        const uint64_t pe = peer64[q];            // (ahash: never 0)
+                        uint64_t h = (pe ^ (pe >> 29)) & mask;
+                        while (tk[h] && tk[h] != pe) h = (h + 1) & mask;
+                        if (!tk[h]) {
+                            tk[h] = pe;
+                            used.push_back((uint32_t)h);
+                        } else {
+                            const uint32_t pq = tv[h], a = ref_op[pq];
+                            if (a != o) {                         // (a peer named twice by one operation links once)
+                                nd->ref_next[pq] = q;             // (o waits for a on this peer)
+                                nd->ref_prev[q] = pq;
+                                nd->op_wait[o]++;
+                            }
+                        }
+                        tv[h] = q;
+                    }
+                }
+                for (uint32_t h : used) tk[h] = 0;                // (only the slots this map took)
+                used.clear();
             }
         };
         const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -552,6 +669,7 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
         for (uint32_t t = 0; t < T; ++t) th.emplace_back(link, (uint32_t)((uint64_t)nm * t / T), (uint32_t)((uint64_t)nm * (t + 1) / T));
         for (auto &x : th) x.join();
     }
+    lap("links");
     nd->map_handle.assign(nm, -1);
     nd->map_need.assign(nm, 0);
     nd->map_chain.assign(nm, 0);
@@ -561,6 +679,7 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
         nd->map_handle[m] = (m & 1) ? v.eps[m >> 1].ct6 : v.eps[m >> 1].ct4;
     }
     for (uint32_t o = 0; o < nops; ++o) nd->map_need[nd->op_map[o]] += MAX_CREATES[nd->op_kind[o]];
+    lap("maps");
     *out = nd.release();
     return 0;
 }
@@ -648,20 +767,41 @@ int cv_epnode_receive(cv_epnode *nd, const uint32_t *row_pkt, const uint32_t *ro
                       uint32_t n, int32_t *op)
 {
     if (!nd || (n && (!row_pkt || !row_ep || !row_has || !op))) return -EINVAL;
-    for (uint32_t j = 0; j < n; ++j) {
-        const uint32_t i = row_pkt[j];
-        if (i >= nd->n || nd->dl_first[i] == cv_epnode::NONE) return -EPROTO;
-        uint32_t o = nd->dl_first[i], k = 0;
-        while (k < nd->dl_cnt[i] && nd->op_map[o] >> 1 != row_ep[j]) ++k, ++o;
-        if (k == nd->dl_cnt[i] || nd->op_st[o] != OP_PENDING) return -EPROTO;
-        // a record: the delivery runs once nothing earlier on its keys waits; none: nothing
-        // runs here -- it leaves its keys' lists now (its successors wait for its pending
-        // predecessors instead), or, on a chained map, runs as a no-op in its turn
-        op[j] = row_has[j] ? (int32_t)o : -1;
-        if (row_has[j]) nd->op_st[o] = OP_RESOLVED;
-        else if (nd->map_chain[nd->op_map[o]]) nd->op_st[o] = OP_NOOP;
-        else nd->splice(o);
+    const uint32_t T = n < (1u << 16) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (T == 1) {
+        uint64_t done = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+            const int r = nd->receive_row(row_pkt[j], row_ep[j], row_has[j], op[j],
+                                          [&](uint32_t x) { nd->release(x); }, done);
+            nd->pending -= done;
+            done = 0;
+            if (r) return r;
+        }
+        return 0;
     }
+    // a row changes only its destination's maps: the rows split by endpoint over host
+    // threads, each with its own lists of what becomes free
+    std::vector<std::vector<uint32_t>> rel(2 * T);
+    std::vector<uint64_t> done(T, 0);
+    std::vector<int> err(T, 0);
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            auto push = [&](uint32_t x) {
+                if (--nd->op_wait[x] == 0) rel[2 * t + nd->op_kind[x]].push_back(x);
+            };
+            for (uint32_t j = 0; j < n; ++j) {
+                if (row_ep[j] % T != t) continue;
+                if ((err[t] = nd->receive_row(row_pkt[j], row_ep[j], row_has[j], op[j], push, done[t]))) return;
+            }
+        });
+    for (auto &x : th) x.join();
+    for (uint32_t t = 0; t < T; ++t) {
+        nd->pending -= done[t];
+        for (int k = 0; k < 2; ++k) nd->zero[k].insert(nd->zero[k].end(), rel[2 * t + k].begin(), rel[2 * t + k].end());
+    }
+    for (uint32_t t = 0; t < T; ++t)
+        if (err[t]) return err[t];
     return 0;
 }
 

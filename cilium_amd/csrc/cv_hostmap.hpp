@@ -120,6 +120,7 @@ class HostMap {
         if (is_lpm()) return;
         tab_.reset(new ByteTable(ks, vs));
         log_clear();
+        version++;
     }
     uint32_t data_bits() const { return dbits_; }
 

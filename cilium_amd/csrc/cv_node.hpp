@@ -32,6 +32,17 @@ struct NodeView {
 };
 
 int node_view(cv_ctx *c, NodeView &v);
+// what a node view depends on: the context (unique per cv_open), its endpoint generation,
+// the service maps bound and their versions, the loopback address -- equal keys, equal views
+struct NodeKey {
+    uint64_t uid = 0, eps = 0, lb[4] = {0, 0, 0, 0}, loopback = 0;
+    bool operator==(const NodeKey &o) const
+    {
+        return uid == o.uid && eps == o.eps && lb[0] == o.lb[0] && lb[1] == o.lb[1] && lb[2] == o.lb[2] &&
+               lb[3] == o.lb[3] && loopback == o.loopback;
+    }
+};
+int node_key(cv_ctx *c, NodeKey &k);
 // live entries and max_entries of CT maps (after every batch already submitted: a sync)
 int ct_counts(cv_ctx *c, const std::vector<int> &handles, std::vector<uint64_t> &live, std::vector<uint64_t> &cap);
 

@@ -318,7 +318,12 @@ struct cv_epnode {
         };
         sift(z);
         const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        static const bool tm = getenv("CV_EPNODE_TIMES") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t levels = 0, big = 0;
+        const size_t first = cur.size();
         while (!cur.empty()) {
+            ++levels;
             std::vector<uint32_t> lvl;
             lvl.swap(cur);
             if (lvl.size() < 8192 || T == 1) {
@@ -329,6 +334,7 @@ struct cv_epnode {
                 sift(z);
                 continue;
             }
+            ++big;
             std::vector<std::vector<uint32_t>> rel(2 * T), outs(T);
             std::vector<uint64_t> done(T, 0);
             std::vector<std::thread> th;
@@ -351,6 +357,10 @@ struct cv_epnode {
             sift(z);
         }
         z.swap(keep);
+        if (tm)
+            fprintf(stderr, "[epnode run] kind %d: %zu first, %zu out, %u levels (%u threaded), %.1f ms\n", kind, first,
+                    out.size(), levels, big,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         // in operation order, which is packet order (a flag pass when the round is large)
         if (out.size() * 16 < op_pkt.size()) {
             std::sort(out.begin(), out.end());

@@ -356,3 +356,56 @@ def test_per_endpoint_ct_room_bound(dev, monkeypatch, capfd):
         bk, bv = b.dump()
         assert len(ak) == len(bk) and (H.sorted_rows(ak, av) == H.sorted_rows(bk, bv)).all()
     ctx.close()
+
+
+def test_config5_ep_zipf_per_endpoint_ct(dev, monkeypatch, capfd):
+    """ConntrackLocal with a Zipf-popular client endpoint (`bench.py --workload config5
+    --ct-local --ep-zipf 0.6` at 2^18 packets, verdict r05 item 4): the busiest endpoints'
+    maps fill in the first step and stay full while the others keep room, as in the bench's
+    steady state.  Three steps built the way bench.py builds them (synth.port_variant: a
+    fifth of the flows take fresh client ports each step, so full maps see new creates fail
+    next to closing connections freeing room); each launch over a full map runs admitted.
+    Every output, every endpoint's CT4 / CT6 map, metrics and policy counters against the
+    oracle after every step."""
+    import copy
+    import re
+    from tests import ep_shard as E
+    from tests.test_gpu_egress import run_egress
+    from tests.test_gpu_ep_node import per_endpoint_ctx
+    kw = dict(n_svc=8000, n_ep=512, n_remote=2048, seed=91, ep_zipf=0.6)
+    n = 1 << 18
+    w = synth.config5(n, ct_max=1 << 20, **kw)                   # the creates per map with room for all
+    dp0, m0 = E.per_endpoint_dp(w)
+    dp0.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+    sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+    cap = int(sizes[-8])                                          # (the 8 busiest maps fill in step 1)
+    w = synth.config5(n, ct_max=cap, **kw)
+    dp, om = E.per_endpoint_dp(w)
+    ctx, pm = per_endpoint_ctx(w)
+    monkeypatch.setenv("CV_ADMIT_STATS", "1")
+    capfd.readouterr()
+    for v in (1, 2, 3):
+        wv = copy.copy(w)
+        wv.frames = H.apply_variant(w.frames, *synth.port_variant(w, v))
+        now = w.now + v
+        o = run_egress(ctx, wv, dev, 0, w.n, now, events=False)
+        ref = dp.lxc_egress(wv.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=now)
+        _check_fields(o, ref, EGR, v)
+        assert (ctx.metrics() == dp.metrics()).all(), v
+        full = 0
+        for fam in ("ct4", "ct6"):
+            for e, (a, b) in enumerate(zip(pm[fam], om[fam])):
+                ak, av = a.dump()
+                bk, bv = b.dump()
+                assert len(ak) == len(bk), (v, fam, e, len(ak), len(bk))
+                assert (H.sorted_rows(ak, av) == H.sorted_rows(bk, bv)).all(), (v, fam, e)
+                full += len(bk) == cap
+        assert full >= 4, (v, full)
+    err = capfd.readouterr().err
+    assert re.search(r"\[cv admit\] egress: \d+ packets, [2-9] passes", err), err[-2000:]   # (a pass undone)
+    ok, ov = om["policy"].dump()
+    pk, pv = pm["policy"].dump()
+    assert (H.sorted_rows(pk, pv) == H.sorted_rows(ok, ov)).all()
+    m = dp.metrics()
+    assert m[155, 2, 0] + m[155, 1, 0] > 0                        # DROP_CT_CREATE_FAILED in the full maps
+    ctx.close()

@@ -290,3 +290,66 @@ def test_ep_sched_node_at_capacity(world):
             assert (H.sorted_rows(keys, vals) == H.sorted_rows(ok, ov)).all(), (e, fam)
     assert (metrics == dp.metrics()).all()
     assert st["maps_ordered_whole_at_open"] > 0 and dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0
+
+
+def test_ep_sched_node_index_follows_changes():
+    """cv_epnode_open caches the node's address / service indexes per node view
+    (cv::node_key: the context, its endpoint generation, the service maps bound and their
+    versions, the loopback address).  A service whose backend moves to a local endpoint,
+    and a new endpoint at an address packets already target, must show in the next
+    batch's candidate destinations (the rows cv_epnode_sources_done lists per candidate)."""
+    from cilium_amd import lib
+    w = synth.config5(1 << 12, n_svc=200, n_ep=32, n_remote=128, seed=5, family=4)
+    ctx = lib.Ctx(-1)
+    lb = ctx.map_from_spec(w.maps["lb4_services"])
+    ctx.bind("lb4_services", lb)
+    c4, c6 = w.maps["ct4"], w.maps["ct6"]
+
+    def add_ep(lxc_id, seclabel, cfg):
+        m4 = ctx.map_create(c4.type, c4.key_size, c4.val_size, c4.max_entries)
+        m6 = ctx.map_create(c6.type, c6.key_size, c6.val_size, c6.max_entries)
+        i = ctx.endpoint_add(lxc_id, seclabel, None, m4)
+        ctx.endpoint_config(i, ct6=m6, **cfg)
+        return i
+
+    for e in w.endpoints:
+        add_ep(e["lxc_id"], e["seclabel"], H._ep_cfg(e))
+    if w.extra and "node" in w.extra:
+        ctx.node_config(**w.extra["node"])
+    n, src = w.n, w.extra["src_ep"]
+    dst = w.frames[:, 30:34].copy().view(">u4").reshape(-1)
+
+    def cands():
+        s = lib.EpSched(ctx, 0, 1, w.frames, src)
+        rp, re_, _, _, _ = s.sources_done(np.arange(n, dtype=np.uint32), np.full(n, -1, np.int32))
+        s.close()
+        out = {}
+        for p, e in zip(rp.tolist(), re_.tolist()):
+            out.setdefault(p, set()).add(e)
+        return out
+
+    before = cands()
+    assert before == cands()                                      # (the cached indexes: same answer)
+    # a service's first backend moved to local endpoint 0 (10.0.1.0)
+    keys = w.maps["lb4_services"].keys
+    slave1 = np.nonzero((keys[:, 6] | keys[:, 7]) == 1)[0]
+    vip_hit = [int(k) for k in slave1 if (dst == int.from_bytes(keys[k, 0:4].tobytes(), "big")).any()]
+    k = keys[vip_hit[0]]
+    vip = int.from_bytes(k[0:4].tobytes(), "big")
+    rc, val = lb.lookup(k.tobytes())
+    assert rc == 0
+    val = bytearray(val)
+    val[0:4] = (0x0A000100).to_bytes(4, "big")
+    assert lb.update(k.tobytes(), bytes(val)) == 0
+    after = cands()
+    to_vip = np.nonzero(dst == vip)[0]
+    assert len(to_vip) and all(0 in after.get(int(p), set()) for p in to_vip)
+    # a new endpoint at a remote pod's address that packets target directly
+    remote = np.nonzero((dst & 0xFFFF0000) == 0x0A100000)[0]
+    addr = int(dst[remote[0]])
+    ne = add_ep(9999, 0x2FFF, dict(ipv4=addr, ipv6=bytes(16), mac=H.DEFAULT_MAC, node_mac=H.NODE_MAC))
+    again = cands()
+    hit = np.nonzero(dst == addr)[0]
+    assert all(ne in again.get(int(p), set()) for p in hit)
+    assert all(ne not in after.get(int(p), set()) for p in hit)
+    ctx.close()

@@ -599,33 +599,61 @@ int cv_epnode_open(cv_ctx *ctx, uint32_t rank, uint32_t world, const uint8_t *fr
     }
     lap("join");
     const uint32_t nops = (uint32_t)nd->op_pkt.size(), nm = ne * 2;
-    nd->op_st.assign(nops, OP_PENDING);
-    for (uint32_t o = 0; o < nops; ++o)
-        if (nd->op_kind[o] == 0) nd->op_st[o] = OP_RESOLVED;    // (a source program needs no record)
     nd->pending = nops;
-    // per map, its operations in order (a stable counting sort by map)
-    nd->map_off.assign(nm + 1, 0);
-    for (uint32_t o = 0; o < nops; ++o) nd->map_off[nd->op_map[o] + 1]++;
-    for (uint32_t m = 0; m < nm; ++m) nd->map_off[m + 1] += nd->map_off[m];
+    // per map, its operations in order: a stable counting sort by map over operation ranges
+    // on host threads (each range counts, the counts are scanned map by map and range by
+    // range, each range places its operations); with it each operation's state and its key
+    // references' owner
+    nd->op_st.resize(nops);
     nd->map_ops.resize(nops);
-    {
-        std::vector<uint32_t> at(nd->map_off.begin(), nd->map_off.end() - 1);
-        for (uint32_t o = 0; o < nops; ++o) nd->map_ops[at[nd->op_map[o]]++] = o;
-    }
-    nd->map_head.assign(nd->map_off.begin(), nd->map_off.end() - 1);
     nd->op_mpos.resize(nops);
-    for (uint32_t k = 0; k < nops; ++k) nd->op_mpos[nd->map_ops[k]] = k;
-    // the key links: per map, its (peer, operation) references sorted, consecutive ones on
-    // one peer linked (an operation naming a peer twice links once)
-    lap("map order");
+    nd->ref_op.resize(peer64.size());
     nd->ref_next.assign(peer64.size(), cv_epnode::NONE);
     nd->ref_prev.assign(peer64.size(), cv_epnode::NONE);
+    {
+        const uint32_t T = nops < (1u << 16) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::vector<uint32_t>> at(T, std::vector<uint32_t>(nm, 0));
+        auto range = [&](uint32_t t) {
+            return std::make_pair((uint32_t)((uint64_t)nops * t / T), (uint32_t)((uint64_t)nops * (t + 1) / T));
+        };
+        auto par = [&](auto &&f) {
+            std::vector<std::thread> th;
+            for (uint32_t t = 0; t < T; ++t) th.emplace_back(f, t);
+            for (auto &x : th) x.join();
+        };
+        par([&](uint32_t t) {
+            const auto r = range(t);
+            for (uint32_t o = r.first; o < r.second; ++o) {
+                nd->op_st[o] = nd->op_kind[o] == 0 ? OP_RESOLVED : OP_PENDING;   // (a source program needs no record)
+                at[t][nd->op_map[o]]++;
+                for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) nd->ref_op[q] = o;
+            }
+        });
+        nd->map_off.assign(nm + 1, 0);
+        uint32_t run = 0;
+        for (uint32_t m = 0; m < nm; ++m) {
+            nd->map_off[m] = run;
+            for (uint32_t t = 0; t < T; ++t) {
+                const uint32_t c = at[t][m];
+                at[t][m] = run;
+                run += c;
+            }
+        }
+        nd->map_off[nm] = run;
+        par([&](uint32_t t) {
+            const auto r = range(t);
+            for (uint32_t o = r.first; o < r.second; ++o) {
+                const uint32_t k = at[t][nd->op_map[o]]++;
+                nd->map_ops[k] = o;
+                nd->op_mpos[o] = k;
+            }
+        });
+    }
+    nd->map_head.assign(nd->map_off.begin(), nd->map_off.end() - 1);
+    lap("map order");
     nd->op_wait.assign(nops, 0);
     {
-        std::vector<uint32_t> &ref_op = nd->ref_op;
-        ref_op.resize(peer64.size());
-        for (uint32_t o = 0; o < nops; ++o)
-            for (uint32_t q = nd->op_poff[o]; q < nd->op_poff[o + 1]; ++q) ref_op[q] = o;
+        const std::vector<uint32_t> &ref_op = nd->ref_op;
         // maps are independent: their links are built on host threads, each with its
         // maps' share of the wait counts (an operation is in one map)
         // per map one pass over its references in operation order (= packet order) with a

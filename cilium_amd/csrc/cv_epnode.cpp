@@ -224,18 +224,24 @@ struct cv_epnode {
     {
         if (--op_wait[s] == 0) zero[op_kind[s]].push_back(s);
     }
-    // operation o has run (or will not run here): its successors wait for one less
-    void finish(uint32_t o)
+    // operation o has run (or will not run here): its successors wait for one less.  Its
+    // successors are in its own map (rel: what becomes free)
+    template <class R>
+    void finish_core(uint32_t o, R &&rel)
     {
         op_st[o] = OP_DONE;
         map_need[op_map[o]] -= MAX_CREATES[op_kind[o]];
-        --pending;
         for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q)
-            if (ref_next[q] != NONE) release(ref_op[ref_next[q]]);
+            if (ref_next[q] != NONE) rel(ref_op[ref_next[q]]);
         if (map_chain[op_map[o]]) {
             const uint32_t s = chain_next(o);
-            if (s != NONE) release(s);
+            if (s != NONE) rel(s);
         }
+    }
+    void finish(uint32_t o)
+    {
+        finish_core(o, [&](uint32_t x) { release(x); });
+        --pending;
     }
     // a delivery that runs nowhere here leaves its keys' lists: each successor waits for
     // the predecessor instead, or for nothing more when the predecessor has finished.
@@ -286,25 +292,10 @@ struct cv_epnode {
     int room(bool first);
     // the operations of `kind` that can run now (deliveries: with their record), and
     // those they free in turn, in packet order
-    // finish() for one of many host threads: the counts it changes are shared
-    void finish_mt(uint32_t o, std::vector<uint32_t> *rel, uint64_t &done)
-    {
-        op_st[o] = OP_DONE;
-        __atomic_fetch_sub(&map_need[op_map[o]], MAX_CREATES[op_kind[o]], __ATOMIC_RELAXED);
-        ++done;
-        auto rel1 = [&](uint32_t x) {
-            if (__atomic_sub_fetch(&op_wait[x], 1u, __ATOMIC_ACQ_REL) == 0) rel[op_kind[x]].push_back(x);
-        };
-        for (uint32_t q = op_poff[o]; q < op_poff[o + 1]; ++q)
-            if (ref_next[q] != NONE) rel1(ref_op[ref_next[q]]);
-        if (map_chain[op_map[o]]) {
-            const uint32_t x = chain_next(o);
-            if (x != NONE) rel1(x);
-        }
-    }
     // the operations of `kind` that can run now (deliveries: with their record), and
     // those they free in turn, in packet order.  Level by level: a large level is
-    // finished on host threads (atomic wait counts), a small one in place.
+    // finished on host threads, each taking the operations of its maps (an operation's
+    // successors are in its map: no shared count), a small one in place.
     void run_ready(int kind, std::vector<uint32_t> &out)
     {
         std::vector<uint32_t> keep, cur, &z = zero[kind];
@@ -339,12 +330,15 @@ struct cv_epnode {
             std::vector<uint64_t> done(T, 0);
             std::vector<std::thread> th;
             for (uint32_t t = 0; t < T; ++t)
-                th.emplace_back([&, t] {
-                    const size_t a = lvl.size() * t / T, b = lvl.size() * (t + 1) / T;
-                    for (size_t k = a; k < b; ++k) {
-                        const uint32_t o = lvl[k];
+                th.emplace_back([&, t] {                      // (thread t: the level's operations of its maps)
+                    auto push = [&](uint32_t x) {
+                        if (--op_wait[x] == 0) rel[2 * t + op_kind[x]].push_back(x);
+                    };
+                    for (const uint32_t o : lvl) {
+                        if (op_map[o] % T != t) continue;
                         if (op_st[o] == OP_RESOLVED) outs[t].push_back(o);
-                        finish_mt(o, &rel[2 * t], done[t]);
+                        finish_core(o, push);
+                        ++done[t];
                     }
                 });
             for (auto &x : th) x.join();

@@ -291,8 +291,6 @@ struct cv_epnode {
     }
     int room(bool first);
     // the operations of `kind` that can run now (deliveries: with their record), and
-    // those they free in turn, in packet order
-    // the operations of `kind` that can run now (deliveries: with their record), and
     // those they free in turn, in packet order.  Level by level: a large level is
     // finished on host threads, each taking the operations of its maps (an operation's
     // successors are in its map: no shared count), a small one in place.

@@ -267,18 +267,17 @@ def test_ep_sched_node(world):
     assert st["maps_ordered_whole_at_open"] == 0
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_ep_sched_node_at_capacity(world):
-    """maps sized so half of them fill: the scheduler orders a map that may fill over all
-    its peers, and the node stays exact (48 of 4 096 packets differed without it)"""
-    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=0xE5, vip_frac=0.5)
-    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+def _sched_at_capacity(world, seed=0xE5, frac=0.5, n=1 << 12):
+    """maps sized so that `frac` of them fill: the node run by the product's scheduler on
+    `world` ranks against one sequential run -- every output, every map, metrics"""
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=seed, vip_frac=0.5)
+    w = synth.config5(n, ct_max=1 << 16, **kw)
     _, _, m0 = _sequential(w)
     sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
-    cap = int(sizes[len(sizes) // 2])
-    w = synth.config5(1 << 12, ct_max=cap, **kw)
+    cap = int(sizes[int(len(sizes) * (1 - frac))])
+    w = synth.config5(n, ct_max=cap, **kw)
     results, rounds, st = sched_simulate(w, world)
-    print(f"world {world} at capacity: {rounds} rounds, {st}")
+    print(f"world {world} at capacity (seed {seed:#x}, {frac} full): {rounds} rounds, {st}")
     ref, dp, maps = _sequential(w)
     out, ct, metrics, _ = E.merge(w, results)
     for k in E.RankState.FIELDS:
@@ -289,7 +288,22 @@ def test_ep_sched_node_at_capacity(world):
             ok, ov = maps[fam][e].dump()
             assert (H.sorted_rows(keys, vals) == H.sorted_rows(ok, ov)).all(), (e, fam)
     assert (metrics == dp.metrics()).all()
+    return st, dp
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_ep_sched_node_at_capacity(world):
+    """maps sized so half of them fill: the scheduler orders a map that may fill over all
+    its peers, and the node stays exact (48 of 4 096 packets differed without it)"""
+    st, dp = _sched_at_capacity(world)
     assert st["maps_ordered_whole_at_open"] > 0 and dp.metrics()[155, 2, 0] + dp.metrics()[155, 1, 0] > 0
+
+
+@pytest.mark.parametrize("seed,world,frac", [(0xE6, 3, 0.5), (0xE7, 2, 0.25), (0xE8, 4, 0.75), (0xE9, 3, 0.1)])
+def test_ep_sched_node_at_capacity_sweep(seed, world, frac):
+    """other seeds, odd and even rank counts (endpoint e on rank e % world) and other
+    shares of full maps: exact every time"""
+    _sched_at_capacity(world, seed, frac)
 
 
 def test_ep_sched_node_index_follows_changes():

@@ -21,15 +21,22 @@ def dev():
     return "cuda:0"
 
 
-@pytest.mark.parametrize("seed,vip,reply", [(101, 0.7, 0.2), (102, 0.4, 0.5), (103, 0.9, 0.05), (104, 0.2, 0.8)])
-def test_config5_seed_sweep(dev, seed, vip, reply):
-    w = synth.config5(1 << 15, seed=seed, n_svc=1500, n_ep=192, n_remote=640, vip_frac=vip, reply_frac=reply,
-                      odd_frac=10.0)
+@pytest.mark.parametrize("seed,vip,reply,kw", [
+    (101, 0.7, 0.2, {}), (102, 0.4, 0.5, {}), (103, 0.9, 0.05, {}), (104, 0.2, 0.8, {}),
+    (105, 0.7, 0.3, {"family": 4}), (106, 0.7, 0.3, {"family": 6}), (107, 0.6, 0.4, {"ep_zipf": 0.9}),
+    (108, 0.8, 0.3, {"n": 1 << 17, "n_flows": 1 << 12})])
+def test_config5_seed_sweep(dev, seed, vip, reply, kw):
+    kw = dict(kw)
+    n = kw.pop("n", 1 << 15)
+    w = synth.config5(n, seed=seed, n_svc=1500, n_ep=192, n_remote=640, vip_frac=vip, reply_frac=reply,
+                      odd_frac=10.0, **kw)
     check_egress(w, dev, batches=3)
 
 
-@pytest.mark.parametrize("seed,v6,zipf", [(201, 0.3, None), (202, 0.0, 0.9), (203, 0.5, 1.1), (204, 0.2, None)])
-def test_config3_seed_sweep(dev, seed, v6, zipf):
-    w = synth.config3(1 << 15, 1 << 12, seed=seed, n_ep=128, n_cidrs=2048, n_ids=300, v6_frac=v6, zipf=zipf,
-                      ttl_low=0.01)
+@pytest.mark.parametrize("seed,v6,zipf,flows,n", [
+    (201, 0.3, None, 1 << 12, 1 << 15), (202, 0.0, 0.9, 1 << 12, 1 << 15), (203, 0.5, 1.1, 1 << 12, 1 << 15),
+    (204, 0.2, None, 1 << 12, 1 << 15), (205, 0.0, None, 256, 1 << 15), (206, 0.4, 0.6, 1 << 14, 1 << 17),
+    (207, 1.0, None, 1 << 12, 1 << 15), (208, 0.1, 1.3, 1 << 10, 1 << 16)])
+def test_config3_seed_sweep(dev, seed, v6, zipf, flows, n):
+    w = synth.config3(n, flows, seed=seed, n_ep=128, n_cidrs=2048, n_ids=300, v6_frac=v6, zipf=zipf, ttl_low=0.01)
     check_ingress(w, dev, batches=3)

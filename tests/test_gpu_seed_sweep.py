@@ -108,3 +108,21 @@ def test_config3_ct_local_seed_sweep(dev, seed, zipf, full):
         assert len(ak) == len(bk) and (H.sorted_rows(ak, av) == H.sorted_rows(bk, bv)).all()
     assert dp.metrics()[155, 1, 0] > 0                           # DROP_CT_CREATE_FAILED in the full maps
     ctx.close()
+
+
+@pytest.mark.parametrize("seed,frac", [(0xF1, 0.0), (0xF2, 0.25), (0xF3, 0.5), (0xF4, 0.75)])
+def test_endpoint_owned_seed_sweep(dev, seed, frac):
+    """The endpoint-owned node (the native scheduler driving the HIP split / deliver
+    launches) over several seeds, with none, a quarter, half or three quarters of the
+    per-endpoint maps filling within the batch: the sequential per-endpoint oracle's
+    every output, table, counter and metric."""
+    from tests import ep_shard as E
+    from tests.test_gpu_ep_node import _check, _rank_run
+    kw = dict(n_svc=120, n_ep=24, n_remote=32, seed=seed, vip_frac=0.5)
+    w = synth.config5(1 << 12, ct_max=1 << 16, **kw)
+    if frac:
+        dp0, m0 = E.per_endpoint_dp(w)
+        dp0.lxc_egress(w.frames, w.length, w.extra["src_ep"], w.extra["flow_hash"], now=w.now)
+        sizes = np.array(sorted(max(len(a), len(b)) for a, b in zip(m0["ct4"], m0["ct6"])))
+        w = synth.config5(1 << 12, ct_max=int(sizes[int(len(sizes) * (1 - frac))]), **kw)
+    _check(w, [_rank_run(w, 0, 1, dev)])
